@@ -1,0 +1,158 @@
+/*
+ * fdengine.h — C-ABI of the MI355X-native fraud-scoring engine (libfdengine.so).
+ *
+ * The engine is the drop-in for ONE hot path of AjayAlluri/realtime-fraud-detection:
+ *   windowed per-card features -> XGBoost primary classifier + Isolation Forest anomaly score
+ *   -> ensemble blend / decision.
+ *
+ * Every entry point below replaces a named reference interface (paths relative to the
+ * reference repo root; "ml/" = services/ml-models/src/, "fl/" = services/flink-jobs/src/main/
+ * java/com/frauddetection/).  The Python host shim (realtime-fraud-detection_amd/fdengine/)
+ * binds these with ctypes; INTEGRATION.md shows the binding a maintainer adds.
+ *
+ * Conventions (mirroring ml/models/model_manager.py:279-307):
+ *   - every function returns int status, FD_OK == 0; nothing throws across the ABI;
+ *   - fd_last_error() returns a thread-local message for the last failure on this thread;
+ *   - caller-owned buffers; "_device" functions take device pointers (HBM-resident inputs),
+ *     "_host" functions take host pointers and are synchronous;
+ *   - one engine per GPU; calls on one engine must be serialised by the caller
+ *     (the reference serialises on one asyncio loop, ml/main.py:337-344).
+ * No PyTorch / HIP types appear in these signatures; streams are passed as void*.
+ */
+#ifndef FDENGINE_H
+#define FDENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FD_ABI_VERSION 1
+
+enum fd_status {
+  FD_OK = 0,
+  FD_ERR_INVALID_ARG = 1,
+  FD_ERR_HIP = 2,
+  FD_ERR_NOT_LOADED = 3, /* ValueError("Model ... not loaded"), ml/models/model_manager.py:281-282 */
+  FD_ERR_UNSUPPORTED = 4,
+  FD_ERR_OOM = 5,
+};
+
+/* Forest kinds: the two tree model types on the path. */
+enum fd_forest_kind {
+  /* xgboost 2.0.3 gbtree, objective binary:logistic
+     (ml/models/model_manager.py:157-161 load, :309-311 predict_proba[:,1]) */
+  FD_FOREST_XGB_BINARY_LOGISTIC = 1,
+  /* scikit-learn IsolationForest, decision_function then 1/(1+e^s)
+     (ml/models/model_manager.py:197-200 load, :338-346 predict) */
+  FD_FOREST_SKLEARN_IFOREST = 2,
+};
+
+typedef struct fd_engine fd_engine;
+
+/* Original (un-repacked) tree arrays of one forest, concatenated over trees.
+   Node ids are per tree, 0-based, exactly as the source library numbers them
+   (XGBoost JSON `left_children`/... arrays; sklearn `tree_.children_left`/...). */
+typedef struct {
+  int32_t n_trees;
+  const int64_t* tree_offsets; /* n_trees+1 offsets into the node arrays */
+  const int32_t* left;         /* left child, -1 marks a leaf */
+  const int32_t* right;        /* right child */
+  const int32_t* feature;      /* split column in the caller's feature matrix */
+  const double* threshold;     /* split value as the library stores it (XGB: f32 value; sklearn: f64) */
+  const uint8_t* default_left; /* missing-value (NaN) direction; NULL = right */
+  const double* leaf_value;    /* per node, read at leaves (XGB: leaf weight; IF: depth+c(n)-1) */
+} fd_tree_arrays;
+
+typedef struct {
+  int32_t kind;        /* enum fd_forest_kind */
+  int32_t num_feature; /* model columns (XGB learner_model_param.num_feature / sklearn n_features_in_) */
+  double base_score;   /* XGB: learner_model_param.base_score (probability space) */
+  double if_offset;    /* IF: offset_ */
+  double if_denominator; /* IF: n_estimators * _average_path_length([max_samples]) */
+} fd_forest_params;
+
+/* Ensemble blend parameters (ml/models/ensemble_predictor.py:62-73, 252-369). Models are listed
+   in the reference's enabled-model order (ml/utils/config.py:128-199). */
+#define FD_MAX_MODELS 8
+enum fd_blend_strategy { FD_BLEND_WEIGHTED_AVERAGE = 0, FD_BLEND_VOTING = 1, FD_BLEND_STACKING = 2 };
+enum fd_decision { FD_APPROVE = 0, FD_REVIEW = 1, FD_DECLINE = 2, FD_APPROVE_WITH_MONITORING = 3 };
+enum fd_risk { FD_VERY_LOW = 0, FD_LOW = 1, FD_MEDIUM = 2, FD_HIGH = 3, FD_CRITICAL = 4 };
+typedef struct {
+  int32_t n_models;
+  int32_t strategy;                  /* enum fd_blend_strategy */
+  double weight[FD_MAX_MODELS];      /* normalised weights, _get_model_weights :62-73 */
+  double conf_mult[FD_MAX_MODELS];   /* _calculate_model_confidence multipliers :331-337 */
+  double fraud_threshold;            /* EnsembleConfig.fraud_threshold (0.5) */
+  double confidence_threshold;       /* EnsembleConfig.confidence_threshold (0.7) */
+} fd_blend_params;
+
+/* ---------------------------------------------------------------- engine lifecycle */
+const char* fd_last_error(void);
+int fd_abi_version(void);
+int fd_device_count(int* out);
+/* ModelManager.__init__ (ml/models/model_manager.py:33-45): one engine per GPU. */
+int fd_engine_create(int device, fd_engine** out);
+int fd_engine_destroy(fd_engine* eng);
+/* Use a caller stream (hipStream_t as void*); NULL restores the engine's own stream. */
+int fd_engine_set_stream(fd_engine* eng, void* hip_stream);
+int fd_engine_sync(fd_engine* eng);
+
+/* ---------------------------------------------------------------- forests (a8, a9) */
+/* Replaces _load_xgboost_model (ml/models/model_manager.py:157-161) and _load_sklearn_model
+   (:197-200): repacks the original trees into the engine's depth-major layout and uploads them. */
+int fd_load_forest(fd_engine* eng, int slot, const fd_forest_params* params, const fd_tree_arrays* trees);
+int fd_unload_forest(fd_engine* eng, int slot);
+int fd_forest_info(fd_engine* eng, int slot, int32_t* n_trees, int32_t* depth, int32_t* num_feature);
+
+/* Replaces _predict_xgboost (:309-311) / _predict_sklearn (:338-346) for a batch.
+   d_X: n x ld row-major f32 (what XGBoost's DMatrix / sklearn's validate_data cast the f64 vector to).
+   d_prob: P(fraud) per row (XGB: f32 sigmoid widened; IF: 1/(1+exp(decision_function))).
+   d_raw (optional): XGB margin / IF summed path length.
+   d_leaf (optional): n x n_trees original leaf node ids (xgboost pred_leaf / sklearn apply). */
+int fd_forest_predict_device(fd_engine* eng, int slot, const float* d_X, int64_t n, int32_t ld,
+                             double* d_prob, double* d_raw, int32_t* d_leaf);
+int fd_forest_predict_host(fd_engine* eng, int slot, const float* X, int64_t n, int32_t ld,
+                           double* prob, double* raw, int32_t* leaf);
+
+/* Host-only repack (no device needed): the depth-major layout fd_load_forest uploads, for layout
+   inspection and CPU tests. Call with NULL buffers to query sizes in *info. */
+typedef struct {
+  int32_t n_trees;
+  int32_t n_chunks;
+  int32_t chunk;        /* trees per LDS staging chunk */
+  int32_t depth;        /* D: every tree is padded to a perfect depth-D tree */
+  int64_t tree_bytes;   /* (2^D-1)*8 node bytes + 2^D leaf values (f32 XGB / f64 IF) */
+  int64_t chunk_stride; /* bytes per chunk, 1 KiB multiple */
+  int64_t blob_bytes;
+  int64_t n_leaf_ids;
+  float base_margin;    /* XGB: f32 margin seeded by base_score */
+} fd_pack_info;
+int fd_pack_forest_host(const fd_forest_params* params, const fd_tree_arrays* trees, void* blob,
+                        int64_t blob_cap, int32_t* leaf_ids, int64_t ids_cap, fd_pack_info* info);
+
+/* ---------------------------------------------------------------- blend (a11-a13) */
+/* Replaces _calculate_model_confidence + _combine_predictions + _make_decision +
+   _calculate_risk_level (ml/models/ensemble_predictor.py:252-369) for a batch.
+   d_probs[m] (host array of device pointers) is model m's probability column; present[m] == 0
+   drops model m as a failed prediction is dropped (:175-181). */
+int fd_blend_device(fd_engine* eng, const fd_blend_params* params, int64_t n,
+                    const double* const* d_probs, const uint8_t* present,
+                    double* d_fraud_prob, double* d_confidence, uint8_t* d_decision, uint8_t* d_risk);
+int fd_blend_host(fd_engine* eng, const fd_blend_params* params, int64_t n,
+                  const double* const* probs, const uint8_t* present,
+                  double* fraud_prob, double* confidence, uint8_t* decision, uint8_t* risk);
+
+/* ---------------------------------------------------------------- diagnostics */
+/* Per-launch device timing of the engine's hot kernels, measured with HIP events recorded on the
+   launch stream around each kernel. fd_timing_read synchronises, returns the summed kernel time (ms)
+   and the number of timed launches since the last read, and resets the counters. */
+int fd_engine_set_timing(fd_engine* eng, int enable);
+int fd_timing_read(fd_engine* eng, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FDENGINE_H */

@@ -1,0 +1,299 @@
+// engine.hip — C-ABI surface of libfdengine.so (declared in include/fdengine.h).
+// Every entry point catches everything: status codes + a thread-local message cross the ABI,
+// exceptions never do (mirrors the reference's log-and-raise contract, ml/models/model_manager.py:302-307,
+// with the raise done by the Python shim).
+#include <cstring>
+#include <string>
+
+#include "fd_internal.h"
+
+namespace fd {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+std::pair<hipEvent_t, hipEvent_t>* Engine::next_event_pair() {
+  if (events_used == events.size()) {
+    hipEvent_t a, b;
+    FD_HIP(hipEventCreate(&a));
+    FD_HIP(hipEventCreate(&b));
+    events.push_back({a, b});
+  }
+  return &events[events_used++];
+}
+
+}  // namespace fd
+
+using fd::Engine;
+
+#define FD_API_BEGIN try {
+#define FD_API_END                    \
+  return FD_OK;                       \
+  }                                   \
+  catch (const fd::Error& e) {        \
+    fd::set_error(e.what());          \
+    return e.code;                    \
+  }                                   \
+  catch (const std::bad_alloc&) {     \
+    fd::set_error("out of memory");   \
+    return FD_ERR_OOM;                \
+  }                                   \
+  catch (const std::exception& e) {   \
+    fd::set_error(e.what());          \
+    return FD_ERR_INVALID_ARG;        \
+  }
+
+struct fd_engine {
+  Engine e;
+};
+
+static Engine& E(fd_engine* p) {
+  FD_REQUIRE(p != nullptr, FD_ERR_INVALID_ARG, "null engine");
+  p->e.activate();
+  return p->e;
+}
+
+static fd::PackedForest& slot_of(Engine& e, int slot) {
+  FD_REQUIRE(slot >= 0 && slot < fd::kMaxSlots, FD_ERR_INVALID_ARG, "slot out of range");
+  return e.forests[slot];
+}
+
+extern "C" {
+
+const char* fd_last_error(void) { return fd::g_last_error.c_str(); }
+
+int fd_abi_version(void) { return FD_ABI_VERSION; }
+
+int fd_device_count(int* out) {
+  FD_API_BEGIN
+  FD_REQUIRE(out, FD_ERR_INVALID_ARG, "null out");
+  int c = 0;
+  FD_HIP(hipGetDeviceCount(&c));
+  *out = c;
+  FD_API_END
+}
+
+int fd_engine_create(int device, fd_engine** out) {
+  FD_API_BEGIN
+  FD_REQUIRE(out, FD_ERR_INVALID_ARG, "null out");
+  *out = nullptr;
+  int c = 0;
+  FD_HIP(hipGetDeviceCount(&c));
+  FD_REQUIRE(device >= 0 && device < c, FD_ERR_INVALID_ARG,
+             "device " + std::to_string(device) + " not present (" + std::to_string(c) + " visible)");
+  auto* p = new fd_engine();
+  p->e.device = device;
+  try {
+    FD_HIP(hipSetDevice(device));
+    FD_HIP(hipStreamCreateWithFlags(&p->e.own_stream, hipStreamNonBlocking));
+    p->e.stream = p->e.own_stream;
+  } catch (...) {
+    delete p;
+    throw;
+  }
+  *out = p;
+  FD_API_END
+}
+
+int fd_engine_destroy(fd_engine* eng) {
+  FD_API_BEGIN
+  if (!eng) return FD_OK;
+  Engine& e = E(eng);
+  (void)hipStreamSynchronize(e.stream);
+  for (auto& f : e.forests) {
+    f.blob.release();
+    f.leaf_ids.release();
+  }
+  e.stage_in.release();
+  e.stage_out0.release();
+  e.stage_out1.release();
+  e.stage_out2.release();
+  e.stage_out3.release();
+  for (auto& ev : e.events) {
+    (void)hipEventDestroy(ev.first);
+    (void)hipEventDestroy(ev.second);
+  }
+  if (e.own_stream) (void)hipStreamDestroy(e.own_stream);
+  delete eng;
+  FD_API_END
+}
+
+int fd_engine_set_stream(fd_engine* eng, void* hip_stream) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  e.stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : e.own_stream;
+  FD_API_END
+}
+
+int fd_engine_sync(fd_engine* eng) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_HIP(hipStreamSynchronize(e.stream));
+  FD_API_END
+}
+
+int fd_engine_set_timing(fd_engine* eng, int enable) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  e.timing = enable != 0;
+  FD_API_END
+}
+
+int fd_timing_read(fd_engine* eng, double* total_ms, int64_t* launches) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  double tot = 0.0;
+  for (size_t i = 0; i < e.events_used; ++i) {
+    FD_HIP(hipEventSynchronize(e.events[i].second));
+    float ms = 0.f;
+    FD_HIP(hipEventElapsedTime(&ms, e.events[i].first, e.events[i].second));
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = (int64_t)e.events_used;
+  e.events_used = 0;
+  FD_API_END
+}
+
+int fd_load_forest(fd_engine* eng, int slot, const fd_forest_params* params, const fd_tree_arrays* trees) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params && trees, FD_ERR_INVALID_ARG, "null params/trees");
+  fd::PackedForest& pf = slot_of(e, slot);
+  FD_HIP(hipStreamSynchronize(e.stream));  // a reload must not race an in-flight predict
+  pf.loaded = false;
+  fd::repack_forest(pf, *params, *trees);
+  FD_API_END
+}
+
+int fd_pack_forest_host(const fd_forest_params* params, const fd_tree_arrays* trees, void* blob,
+                        int64_t blob_cap, int32_t* leaf_ids, int64_t ids_cap, fd_pack_info* info) {
+  FD_API_BEGIN
+  FD_REQUIRE(params && trees && info, FD_ERR_INVALID_ARG, "null params/trees/info");
+  const fd::HostPack hp = fd::pack_forest_host(*params, *trees);
+  info->n_trees = hp.n_trees;
+  info->n_chunks = hp.n_chunks;
+  info->chunk = hp.chunk;
+  info->depth = hp.depth;
+  info->tree_bytes = (int64_t)hp.tree_bytes;
+  info->chunk_stride = (int64_t)hp.chunk_stride;
+  info->blob_bytes = (int64_t)hp.blob.size();
+  info->n_leaf_ids = (int64_t)hp.leaf_ids.size();
+  info->base_margin = hp.base_margin;
+  if (blob) {
+    FD_REQUIRE(blob_cap >= (int64_t)hp.blob.size(), FD_ERR_INVALID_ARG, "blob buffer too small");
+    std::memcpy(blob, hp.blob.data(), hp.blob.size());
+  }
+  if (leaf_ids) {
+    FD_REQUIRE(ids_cap >= (int64_t)hp.leaf_ids.size(), FD_ERR_INVALID_ARG, "leaf id buffer too small");
+    std::memcpy(leaf_ids, hp.leaf_ids.data(), hp.leaf_ids.size() * sizeof(int32_t));
+  }
+  FD_API_END
+}
+
+int fd_unload_forest(fd_engine* eng, int slot) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::PackedForest& pf = slot_of(e, slot);
+  FD_HIP(hipStreamSynchronize(e.stream));
+  pf.blob.release();
+  pf.leaf_ids.release();
+  pf.loaded = false;
+  FD_API_END
+}
+
+int fd_forest_info(fd_engine* eng, int slot, int32_t* n_trees, int32_t* depth, int32_t* num_feature) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::PackedForest& pf = slot_of(e, slot);
+  FD_REQUIRE(pf.loaded, FD_ERR_NOT_LOADED, "Model in slot " + std::to_string(slot) + " not loaded");
+  if (n_trees) *n_trees = pf.n_trees;
+  if (depth) *depth = pf.depth;
+  if (num_feature) *num_feature = pf.num_feature;
+  FD_API_END
+}
+
+int fd_forest_predict_device(fd_engine* eng, int slot, const float* d_X, int64_t n, int32_t ld,
+                             double* d_prob, double* d_raw, int32_t* d_leaf) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::PackedForest& pf = slot_of(e, slot);
+  FD_REQUIRE(pf.loaded, FD_ERR_NOT_LOADED, "Model in slot " + std::to_string(slot) + " not loaded");
+  FD_REQUIRE(n >= 0, FD_ERR_INVALID_ARG, "negative n");
+  fd::launch_forest(e, pf, d_X, n, ld, d_prob, d_raw, d_leaf);
+  FD_API_END
+}
+
+int fd_forest_predict_host(fd_engine* eng, int slot, const float* X, int64_t n, int32_t ld, double* prob,
+                           double* raw, int32_t* leaf) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::PackedForest& pf = slot_of(e, slot);
+  FD_REQUIRE(pf.loaded, FD_ERR_NOT_LOADED, "Model in slot " + std::to_string(slot) + " not loaded");
+  FD_REQUIRE(n >= 0 && ld > 0 && X && prob, FD_ERR_INVALID_ARG, "bad arguments");
+  if (n == 0) return FD_OK;
+  const size_t xb = (size_t)n * ld * sizeof(float);
+  e.stage_in.ensure(xb);
+  e.stage_out0.ensure((size_t)n * sizeof(double));
+  if (raw) e.stage_out1.ensure((size_t)n * sizeof(double));
+  if (leaf) e.stage_out2.ensure((size_t)n * pf.n_trees * sizeof(int32_t));
+  FD_HIP(hipMemcpyAsync(e.stage_in.ptr, X, xb, hipMemcpyHostToDevice, e.stream));
+  fd::launch_forest(e, pf, e.stage_in.as<float>(), n, ld, e.stage_out0.as<double>(),
+                    raw ? e.stage_out1.as<double>() : nullptr, leaf ? e.stage_out2.as<int32_t>() : nullptr);
+  FD_HIP(hipMemcpyAsync(prob, e.stage_out0.ptr, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, e.stream));
+  if (raw)
+    FD_HIP(hipMemcpyAsync(raw, e.stage_out1.ptr, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, e.stream));
+  if (leaf)
+    FD_HIP(hipMemcpyAsync(leaf, e.stage_out2.ptr, (size_t)n * pf.n_trees * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, e.stream));
+  FD_HIP(hipStreamSynchronize(e.stream));
+  FD_API_END
+}
+
+int fd_blend_device(fd_engine* eng, const fd_blend_params* params, int64_t n, const double* const* d_probs,
+                    const uint8_t* present, double* d_fraud_prob, double* d_confidence, uint8_t* d_decision,
+                    uint8_t* d_risk) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
+  fd::launch_blend(e, *params, n, d_probs, present, d_fraud_prob, d_confidence, d_decision, d_risk);
+  FD_API_END
+}
+
+int fd_blend_host(fd_engine* eng, const fd_blend_params* params, int64_t n, const double* const* probs,
+                  const uint8_t* present, double* fraud_prob, double* confidence, uint8_t* decision,
+                  uint8_t* risk) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params && probs && fraud_prob, FD_ERR_INVALID_ARG, "bad arguments");
+  FD_REQUIRE(params->n_models >= 0 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG,
+             "n_models out of range");
+  if (n == 0) return FD_OK;
+  const int M = params->n_models;
+  // stage_in holds the M probability columns; outputs in stage_out0..3
+  e.stage_in.ensure((size_t)n * sizeof(double) * (M > 0 ? M : 1));
+  e.stage_out0.ensure((size_t)n * sizeof(double));
+  e.stage_out1.ensure((size_t)n * sizeof(double));
+  e.stage_out2.ensure((size_t)n);
+  e.stage_out3.ensure((size_t)n);
+  const double* dcols[FD_MAX_MODELS] = {};
+  for (int m = 0; m < M; ++m) {
+    double* col = e.stage_in.as<double>() + (size_t)m * n;
+    dcols[m] = col;
+    if (present && !present[m]) continue;
+    FD_REQUIRE(probs[m], FD_ERR_INVALID_ARG, "null probability column");
+    FD_HIP(hipMemcpyAsync(col, probs[m], (size_t)n * sizeof(double), hipMemcpyHostToDevice, e.stream));
+  }
+  fd::launch_blend(e, *params, n, dcols, present, e.stage_out0.as<double>(), e.stage_out1.as<double>(),
+                   e.stage_out2.as<uint8_t>(), e.stage_out3.as<uint8_t>());
+  FD_HIP(hipMemcpyAsync(fraud_prob, e.stage_out0.ptr, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, e.stream));
+  if (confidence)
+    FD_HIP(hipMemcpyAsync(confidence, e.stage_out1.ptr, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, e.stream));
+  if (decision) FD_HIP(hipMemcpyAsync(decision, e.stage_out2.ptr, (size_t)n, hipMemcpyDeviceToHost, e.stream));
+  if (risk) FD_HIP(hipMemcpyAsync(risk, e.stage_out3.ptr, (size_t)n, hipMemcpyDeviceToHost, e.stream));
+  FD_HIP(hipStreamSynchronize(e.stream));
+  FD_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,113 @@
+// fd_internal.h — engine internals shared by the HIP translation units of libfdengine.so.
+// Not part of the ABI (see include/fdengine.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fdengine.h"
+
+namespace fd {
+
+constexpr int kMaxSlots = 8;      // forest slots per engine
+constexpr int kTile = 256;        // transactions per workgroup in the forest kernel (one per thread)
+constexpr int kMaxFeatures = 64;  // model columns held in LDS ([feature][kTile] f32 = 64 KiB max)
+constexpr int kMaxDepth = 10;     // deepest tree the repacker accepts
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_error(const std::string& msg);
+
+#define FD_HIP(call)                                                                       \
+  do {                                                                                     \
+    hipError_t _e = (call);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      throw ::fd::Error(FD_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e));    \
+  } while (0)
+
+#define FD_REQUIRE(cond, code, msg)              \
+  do {                                           \
+    if (!(cond)) throw ::fd::Error((code), (msg)); \
+  } while (0)
+
+// Device allocation owned by the engine; grows, never shrinks.
+struct DeviceBuffer {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t need) {
+    if (need <= bytes) return;
+    release();
+    FD_HIP(hipMalloc(&ptr, need));
+    bytes = need;
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(ptr); }
+};
+
+// A forest repacked into perfect depth-D trees (see DESIGN.md "Forest layout"):
+//   per tree, 2^D-1 internal node records {f32 thr, u32 meta} in breadth-first order
+//   (children of slot s are 2s+1 / 2s+2), followed by 2^D leaf values (f32 for XGBoost,
+//   f64 for Isolation Forest). Trees are grouped in chunks of `chunk` trees; each chunk
+//   occupies `chunk_stride` bytes (rounded to 1 KiB for the LDS-DMA staging).
+//   meta = feature * kTile * 4 (byte offset of the feature row in the LDS tile) | default_left << 31.
+struct PackedForest {
+  bool loaded = false;
+  int kind = 0;
+  int n_trees = 0;
+  int n_chunks = 0;
+  int chunk = 0;
+  int depth = 0;
+  int num_feature = 0;
+  size_t tree_bytes = 0;
+  size_t chunk_stride = 0;
+  float base_margin = 0.f;  // XGB: -logf(1/base_score - 1)
+  double if_offset = 0.0;
+  double if_denominator = 0.0;
+  DeviceBuffer blob;      // n_chunks * chunk_stride
+  DeviceBuffer leaf_ids;  // n_trees_padded * 2^D original node ids (parity output)
+};
+
+struct Engine {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  PackedForest forests[kMaxSlots];
+  // host-API staging
+  DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
+  // optional per-launch kernel timing (HIP events on the launch stream)
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pool
+  size_t events_used = 0;
+  void activate() const { FD_HIP(hipSetDevice(device)); }
+  std::pair<hipEvent_t, hipEvent_t>* next_event_pair();
+};
+
+// forest.hip
+struct HostPack {
+  std::vector<char> blob;
+  std::vector<int32_t> leaf_ids;
+  int kind = 0, n_trees = 0, n_chunks = 0, chunk = 0, depth = 0, num_feature = 0;
+  size_t tree_bytes = 0, chunk_stride = 0;
+  float base_margin = 0.f;
+};
+HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t);
+void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);
+void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
+                   double* d_prob, double* d_raw, int32_t* d_leaf);
+// blend.hip
+void launch_blend(Engine& e, const fd_blend_params& p, int64_t n, const double* const* d_probs,
+                  const uint8_t* present, double* d_fp, double* d_conf, uint8_t* d_dec, uint8_t* d_risk);
+
+}  // namespace fd

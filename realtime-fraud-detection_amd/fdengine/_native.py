@@ -1,0 +1,144 @@
+"""ctypes binding of libfdengine.so (the C-ABI declared in include/fdengine.h).
+
+The product path has exactly one implementation: the HIP library. If it is missing this module
+raises at import time — there is no CPU fallback (the CPU restatement under oracle/ is test
+infrastructure only and is never imported from here).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # realtime-fraud-detection_amd/
+REPO_ROOT = PKG_ROOT.parent
+LIB_PATH = Path(os.environ.get("FDENGINE_LIB", PKG_ROOT / "lib" / "libfdengine.so"))
+
+FD_OK = 0
+FD_ERR_INVALID_ARG = 1
+FD_ERR_HIP = 2
+FD_ERR_NOT_LOADED = 3
+FD_ERR_UNSUPPORTED = 4
+FD_ERR_OOM = 5
+
+FD_FOREST_XGB_BINARY_LOGISTIC = 1
+FD_FOREST_SKLEARN_IFOREST = 2
+
+FD_MAX_MODELS = 8
+FD_BLEND_WEIGHTED_AVERAGE = 0
+FD_BLEND_VOTING = 1
+FD_BLEND_STACKING = 2
+
+DECISIONS = ("APPROVE", "REVIEW", "DECLINE", "APPROVE_WITH_MONITORING")
+RISK_LEVELS = ("VERY_LOW", "LOW", "MEDIUM", "HIGH", "CRITICAL")
+
+
+class fd_tree_arrays(C.Structure):
+    _fields_ = [
+        ("n_trees", C.c_int32),
+        ("tree_offsets", C.POINTER(C.c_int64)),
+        ("left", C.POINTER(C.c_int32)),
+        ("right", C.POINTER(C.c_int32)),
+        ("feature", C.POINTER(C.c_int32)),
+        ("threshold", C.POINTER(C.c_double)),
+        ("default_left", C.POINTER(C.c_uint8)),
+        ("leaf_value", C.POINTER(C.c_double)),
+    ]
+
+
+class fd_forest_params(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("num_feature", C.c_int32),
+        ("base_score", C.c_double),
+        ("if_offset", C.c_double),
+        ("if_denominator", C.c_double),
+    ]
+
+
+class fd_blend_params(C.Structure):
+    _fields_ = [
+        ("n_models", C.c_int32),
+        ("strategy", C.c_int32),
+        ("weight", C.c_double * FD_MAX_MODELS),
+        ("conf_mult", C.c_double * FD_MAX_MODELS),
+        ("fraud_threshold", C.c_double),
+        ("confidence_threshold", C.c_double),
+    ]
+
+
+class fd_pack_info(C.Structure):
+    _fields_ = [
+        ("n_trees", C.c_int32),
+        ("n_chunks", C.c_int32),
+        ("chunk", C.c_int32),
+        ("depth", C.c_int32),
+        ("tree_bytes", C.c_int64),
+        ("chunk_stride", C.c_int64),
+        ("blob_bytes", C.c_int64),
+        ("n_leaf_ids", C.c_int64),
+        ("base_margin", C.c_float),
+    ]
+
+
+_vp = C.c_void_p
+_i32 = C.c_int32
+_i64 = C.c_int64
+_dp = C.POINTER(C.c_double)
+
+# (name, restype, argtypes) for every function the header declares.
+SIGNATURES = {
+    "fd_last_error": (C.c_char_p, []),
+    "fd_abi_version": (C.c_int, []),
+    "fd_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "fd_engine_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+    "fd_engine_destroy": (C.c_int, [_vp]),
+    "fd_engine_set_stream": (C.c_int, [_vp, _vp]),
+    "fd_engine_sync": (C.c_int, [_vp]),
+    "fd_load_forest": (C.c_int, [_vp, C.c_int, C.POINTER(fd_forest_params), C.POINTER(fd_tree_arrays)]),
+    "fd_unload_forest": (C.c_int, [_vp, C.c_int]),
+    "fd_forest_info": (C.c_int, [_vp, C.c_int, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
+    "fd_forest_predict_device": (C.c_int, [_vp, C.c_int, _vp, _i64, _i32, _vp, _vp, _vp]),
+    "fd_forest_predict_host": (C.c_int, [_vp, C.c_int, _vp, _i64, _i32, _vp, _vp, _vp]),
+    "fd_blend_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _i64, C.POINTER(_vp), _vp, _vp, _vp, _vp, _vp]),
+    "fd_blend_host": (C.c_int, [_vp, C.POINTER(fd_blend_params), _i64, C.POINTER(_vp), _vp, _vp, _vp, _vp, _vp]),
+    "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
+    "fd_timing_read": (C.c_int, [_vp, _dp, C.POINTER(_i64)]),
+    "fd_pack_forest_host": (C.c_int, [C.POINTER(fd_forest_params), C.POINTER(fd_tree_arrays), _vp, _i64, _vp, _i64,
+                                      C.POINTER(fd_pack_info)]),
+}
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code: int, fn: str, msg: str):
+        super().__init__(f"{fn} failed ({code}): {msg}")
+        self.code = code
+
+
+def _load() -> C.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"libfdengine.so not found at {LIB_PATH}. Build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950). "
+            "There is no CPU fallback for the scoring path.")
+    lib = C.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(code: int, fn: str) -> None:
+    if code != FD_OK:
+        msg = lib.fd_last_error().decode("utf-8", "replace")
+        if code == FD_ERR_NOT_LOADED:
+            raise ValueError(msg)
+        raise NativeError(code, fn, msg)
+
+
+def call(fn: str, *args) -> None:
+    check(getattr(lib, fn)(*args), fn)

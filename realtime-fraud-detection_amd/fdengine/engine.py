@@ -1,0 +1,170 @@
+"""Thin object wrapper over the C-ABI (one FraudEngine per GPU).
+
+Host-array calls (`predict`, `blend`) copy through engine-owned staging buffers; `*_device` calls
+take device pointers (ints) so HBM-resident inputs (e.g. torch tensors' data_ptr()) are scored in
+place. The engine never falls back to the CPU: every call goes through libfdengine.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .forest import ForestArrays
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class FraudEngine:
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        N.call("fd_engine_create", int(device), C.byref(h))
+        self._h = h
+        self.device = int(device)
+        self.forests: Dict[int, dict] = {}
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            N.call("fd_engine_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream_ptr: Optional[int]) -> None:
+        N.call("fd_engine_set_stream", self._h, C.c_void_p(stream_ptr) if stream_ptr else None)
+
+    def sync(self) -> None:
+        N.call("fd_engine_sync", self._h)
+
+    def set_timing(self, enable: bool) -> None:
+        N.call("fd_engine_set_timing", self._h, 1 if enable else 0)
+
+    def read_timing(self):
+        """-> (total kernel ms, timed launches) since the last read."""
+        ms = C.c_double()
+        cnt = C.c_int64()
+        N.call("fd_timing_read", self._h, C.byref(ms), C.byref(cnt))
+        return ms.value, cnt.value
+
+    # ------------------------------------------------------------------ forests
+    def load_forest(self, slot: int, fa: ForestArrays) -> None:
+        p, t, keep = fa.c_structs()
+        N.call("fd_load_forest", self._h, int(slot), C.byref(p), C.byref(t))
+        del keep
+        nt, d, nf = C.c_int32(), C.c_int32(), C.c_int32()
+        N.call("fd_forest_info", self._h, int(slot), C.byref(nt), C.byref(d), C.byref(nf))
+        self.forests[slot] = {"kind": fa.kind, "n_trees": nt.value, "depth": d.value, "num_feature": nf.value}
+
+    def unload_forest(self, slot: int) -> None:
+        N.call("fd_unload_forest", self._h, int(slot))
+        self.forests.pop(slot, None)
+
+    def forest_info(self, slot: int) -> dict:
+        if slot not in self.forests:
+            raise ValueError(f"Model in slot {slot} not loaded")
+        return dict(self.forests[slot])
+
+    def predict(self, slot: int, X: np.ndarray, want_raw: bool = False, want_leaf: bool = False):
+        """X: [n, ld] (cast to f32 as XGBoost's DMatrix / sklearn's validate_data do).
+        -> prob f64 [n] (+ raw f64 [n], leaf int32 [n, T])."""
+        X = np.ascontiguousarray(np.asarray(X, dtype=np.float32))
+        if X.ndim == 1:
+            X = X.reshape(1, -1)
+        n, ld = X.shape
+        prob = np.empty(n, np.float64)
+        raw = np.empty(n, np.float64) if want_raw else None
+        T = self.forests.get(slot, {}).get("n_trees", 0)
+        leaf = np.empty((n, T), np.int32) if want_leaf else None
+        N.call("fd_forest_predict_host", self._h, int(slot), _ptr(X), n, ld, _ptr(prob), _ptr(raw), _ptr(leaf))
+        out = [prob]
+        if want_raw:
+            out.append(raw)
+        if want_leaf:
+            out.append(leaf)
+        return out[0] if len(out) == 1 else tuple(out)
+
+    def predict_device(self, slot: int, X_ptr: int, n: int, ld: int, prob_ptr: int, raw_ptr: int = 0,
+                       leaf_ptr: int = 0) -> None:
+        N.call("fd_forest_predict_device", self._h, int(slot), C.c_void_p(X_ptr), int(n), int(ld),
+               C.c_void_p(prob_ptr), C.c_void_p(raw_ptr) if raw_ptr else None,
+               C.c_void_p(leaf_ptr) if leaf_ptr else None)
+
+    # ------------------------------------------------------------------ blend
+    @staticmethod
+    def blend_params(weights: Sequence[float], conf_mult: Sequence[float], strategy: int = 0,
+                     fraud_threshold: float = 0.5, confidence_threshold: float = 0.7) -> N.fd_blend_params:
+        p = N.fd_blend_params()
+        p.n_models = len(weights)
+        p.strategy = int(strategy)
+        for i, (w, m) in enumerate(zip(weights, conf_mult)):
+            p.weight[i] = float(w)
+            p.conf_mult[i] = float(m)
+        p.fraud_threshold = float(fraud_threshold)
+        p.confidence_threshold = float(confidence_threshold)
+        return p
+
+    def blend(self, params: N.fd_blend_params, probs: Sequence[Optional[np.ndarray]]):
+        """probs[m]: f64 [n] or None (model failed -> dropped). -> (fraud_prob, confidence, decision u8, risk u8)."""
+        M = params.n_models
+        assert len(probs) == M
+        n = next((len(p) for p in probs if p is not None), 0)
+        cols = [None if p is None else np.ascontiguousarray(p, dtype=np.float64) for p in probs]
+        present = np.array([0 if c is None else 1 for c in cols], np.uint8)
+        arr = (C.c_void_p * N.FD_MAX_MODELS)()
+        for i, c in enumerate(cols):
+            arr[i] = None if c is None else c.ctypes.data
+        fp = np.empty(n, np.float64)
+        conf = np.empty(n, np.float64)
+        dec = np.empty(n, np.uint8)
+        risk = np.empty(n, np.uint8)
+        N.call("fd_blend_host", self._h, C.byref(params), n, arr, _ptr(present), _ptr(fp), _ptr(conf),
+               _ptr(dec), _ptr(risk))
+        return fp, conf, dec, risk
+
+    def blend_device(self, params: N.fd_blend_params, n: int, prob_ptrs: Sequence[Optional[int]],
+                     fp_ptr: int, conf_ptr: int = 0, dec_ptr: int = 0, risk_ptr: int = 0) -> None:
+        present = np.array([0 if p is None else 1 for p in prob_ptrs], np.uint8)
+        arr = (C.c_void_p * N.FD_MAX_MODELS)()
+        for i, p in enumerate(prob_ptrs):
+            arr[i] = p if p else None
+        N.call("fd_blend_device", self._h, C.byref(params), int(n), arr, _ptr(present), C.c_void_p(fp_ptr),
+               C.c_void_p(conf_ptr) if conf_ptr else None, C.c_void_p(dec_ptr) if dec_ptr else None,
+               C.c_void_p(risk_ptr) if risk_ptr else None)
+
+
+def pack_forest_host(fa: ForestArrays):
+    """Host-only repack (no GPU): -> (blob bytes, leaf_ids int32, fd_pack_info)."""
+    p, t, keep = fa.c_structs()
+    info = N.fd_pack_info()
+    N.call("fd_pack_forest_host", C.byref(p), C.byref(t), None, 0, None, 0, C.byref(info))
+    blob = np.empty(info.blob_bytes, np.uint8)
+    ids = np.empty(info.n_leaf_ids, np.int32)
+    N.call("fd_pack_forest_host", C.byref(p), C.byref(t), C.c_void_p(blob.ctypes.data), info.blob_bytes,
+           C.c_void_p(ids.ctypes.data), info.n_leaf_ids, C.byref(info))
+    del keep
+    return blob.tobytes(), ids, info
+
+
+def device_count() -> int:
+    c = C.c_int()
+    rc = N.lib.fd_device_count(C.byref(c))
+    return c.value if rc == N.FD_OK else 0

@@ -1,0 +1,113 @@
+"""GPU parity: the HIP forest kernel (through the C-ABI) against the CPU oracle on the same seeded
+inputs. Bars (BASELINE.json north_star): leaf indices bit-exact; probabilities within 1e-5 absolute.
+This suite also holds the engine to more than that bar: XGBoost margins are the same f32 sum sequence
+(bit-exact) and IsolationForest path-length sums the same f64 sequence (bit-exact)."""
+import numpy as np
+import pytest
+
+import oracle
+from fdengine import FraudEngine, iforest_from_sklearn, synth, xgboost_from_json_doc
+
+pytestmark = pytest.mark.gpu
+
+PROB_TOL = 1e-5  # north_star: fraud probabilities within 1e-5 absolute
+
+
+def _xgb_case(engine, slot, n, n_trees, depth, nf, seed, p_leaf=0.0, nan_frac=0.0, ld=None, base_score=0.5):
+    X = synth.feature_matrix(n, nf, seed=seed, nan_frac=nan_frac)
+    doc = synth.xgboost_doc(n_trees, depth, nf, synth.feature_matrix(512, nf, seed=seed + 1), seed=seed + 2,
+                            p_leaf=p_leaf, base_score=base_score)
+    fa = xgboost_from_json_doc(doc)
+    if ld is not None and ld < nf:
+        X = np.ascontiguousarray(X[:, :ld])
+    engine.load_forest(slot, fa)
+    prob, raw, leaf = engine.predict(slot, X, want_raw=True, want_leaf=True)
+    rp, rm, rl = oracle.xgb_predict(fa, X, want_leaf=True)
+    return prob, raw, leaf, rp, rm, rl
+
+
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 4099])
+def test_xgb_parity_sizes(engine, n):
+    prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 0, n, 64, 8, 50, seed=11)
+    np.testing.assert_array_equal(leaf, rl)
+    np.testing.assert_array_equal(raw.astype(np.float32), rm)  # same f32 sequence
+    assert np.abs(prob - rp.astype(np.float64)).max() <= PROB_TOL
+
+
+@pytest.mark.parametrize("depth", [1, 2, 5, 8, 9, 10])
+def test_xgb_parity_depths(engine, depth):
+    prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 1, 1000, 37, depth, 20, seed=20 + depth, p_leaf=0.2)
+    np.testing.assert_array_equal(leaf, rl)
+    np.testing.assert_array_equal(raw.astype(np.float32), rm)
+    assert np.abs(prob - rp).max() <= PROB_TOL
+
+
+def test_xgb_missing_values_and_short_rows(engine):
+    # NaN -> default_left; columns beyond the caller's ld are missing (DMatrix semantics)
+    prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 2, 3000, 100, 8, 50, seed=31, p_leaf=0.1, nan_frac=0.1)
+    np.testing.assert_array_equal(leaf, rl)
+    np.testing.assert_array_equal(raw.astype(np.float32), rm)
+    prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 2, 700, 50, 7, 50, seed=32, ld=33)
+    np.testing.assert_array_equal(leaf, rl)
+    np.testing.assert_array_equal(raw.astype(np.float32), rm)
+    assert np.abs(prob - rp).max() <= PROB_TOL
+
+
+def test_xgb_base_score(engine):
+    prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 3, 500, 20, 6, 16, seed=41, base_score=0.137)
+    np.testing.assert_array_equal(raw.astype(np.float32), rm)
+    assert np.abs(prob - rp).max() <= PROB_TOL
+
+
+def test_xgb_config2_full_batch(engine):
+    """BASELINE config 2 at full size: 500 trees x depth 8, 50 features, 64k micro-batch."""
+    prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 4, 65536, 500, 8, 50, seed=51)
+    np.testing.assert_array_equal(leaf, rl)
+    np.testing.assert_array_equal(raw.astype(np.float32), rm)
+    assert np.abs(prob - rp).max() <= PROB_TOL
+
+
+def test_iforest_parity_vs_sklearn(engine):
+    Xtr = synth.feature_matrix(4000, 64, seed=61).astype(np.float64)
+    m = synth.isolation_forest(Xtr)
+    fa = iforest_from_sklearn(m)
+    X = synth.feature_matrix(5000, 64, seed=62)
+    X[::97, 3] = np.nan  # missing_go_to_left path
+    engine.load_forest(5, fa)
+    prob, raw, leaf = engine.predict(5, X, want_raw=True, want_leaf=True)
+    rp, rd, rl = oracle.iforest_predict(fa, X, want_leaf=True)
+    np.testing.assert_array_equal(leaf, rl)
+    np.testing.assert_array_equal(raw, rd)  # same f64 sequence
+    assert np.abs(prob - rp).max() <= PROB_TOL
+    # and against sklearn + the reference's transform itself (finite rows)
+    Xf = synth.feature_matrix(2000, 64, seed=63)
+    p2 = engine.predict(5, Xf)
+    ref = 1.0 / (1.0 + np.exp(m.decision_function(Xf)))
+    assert np.abs(p2 - ref).max() <= 1e-12
+    np.testing.assert_array_equal(engine.predict(5, Xf, want_leaf=True)[1],
+                                  np.stack([e.apply(Xf) for e in m.estimators_], 1))
+
+
+def test_empty_batch_and_unloaded_slot(engine):
+    engine.load_forest(6, xgboost_from_json_doc(synth.xgboost_doc(3, 3, 4, synth.feature_matrix(64, 4))))
+    out = engine.predict(6, np.zeros((0, 4), np.float32))
+    assert out.shape == (0,)
+    with pytest.raises(ValueError):
+        engine.predict(7, np.zeros((3, 4), np.float32))
+
+
+def test_device_pointer_path_matches_host_path(engine):
+    import torch
+    X = synth.feature_matrix(3000, 50, seed=71)
+    fa = xgboost_from_json_doc(synth.xgboost_doc(80, 8, 50, X, seed=72))
+    engine.load_forest(0, fa)
+    host = engine.predict(0, X)
+    dX = torch.from_numpy(X).cuda()
+    dp = torch.empty(3000, dtype=torch.float64, device="cuda")
+    engine.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        engine.predict_device(0, dX.data_ptr(), 3000, 50, dp.data_ptr())
+        torch.cuda.synchronize()
+    finally:
+        engine.set_stream(None)
+    np.testing.assert_array_equal(dp.cpu().numpy(), host)
