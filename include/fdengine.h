@@ -96,8 +96,11 @@ int fd_device_count(int* out);
 /* ModelManager.__init__ (ml/models/model_manager.py:33-45): one engine per GPU. */
 int fd_engine_create(int device, fd_engine** out);
 int fd_engine_destroy(fd_engine* eng);
-/* Use a caller stream (hipStream_t as void*); NULL restores the engine's own stream. */
+/* Launch on a caller stream (hipStream_t as void*). NULL is the device's null (default) stream,
+   e.g. PyTorch's default stream, whose handle is 0. fd_engine_reset_stream restores the engine's
+   own non-blocking stream. */
 int fd_engine_set_stream(fd_engine* eng, void* hip_stream);
+int fd_engine_reset_stream(fd_engine* eng);
 int fd_engine_sync(fd_engine* eng);
 
 /* ---------------------------------------------------------------- forests (a8, a9) */
@@ -150,6 +153,9 @@ int fd_blend_host(fd_engine* eng, const fd_blend_params* params, int64_t n,
    launch stream around each kernel. fd_timing_read synchronises, returns the summed kernel time (ms)
    and the number of timed launches since the last read, and resets the counters. */
 int fd_engine_set_timing(fd_engine* eng, int enable);
+/* Engine tuning knobs (for A/B measurement; defaults are the tuned choices):
+     "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel */
+int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
 int fd_timing_read(fd_engine* eng, double* total_ms, int64_t* launches);
 
 #ifdef __cplusplus

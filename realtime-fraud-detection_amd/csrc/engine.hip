@@ -122,7 +122,14 @@ int fd_engine_destroy(fd_engine* eng) {
 int fd_engine_set_stream(fd_engine* eng, void* hip_stream) {
   FD_API_BEGIN
   Engine& e = E(eng);
-  e.stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : e.own_stream;
+  e.stream = static_cast<hipStream_t>(hip_stream);
+  FD_API_END
+}
+
+int fd_engine_reset_stream(fd_engine* eng) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  e.stream = e.own_stream;
   FD_API_END
 }
 
@@ -137,6 +144,20 @@ int fd_engine_set_timing(fd_engine* eng, int enable) {
   FD_API_BEGIN
   Engine& e = E(eng);
   e.timing = enable != 0;
+  FD_API_END
+}
+
+int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(key, FD_ERR_INVALID_ARG, "null key");
+  const std::string k(key);
+  if (k == "forest_kernel") {
+    FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "forest_kernel must be 0, 1 or 2");
+    e.forest_variant = (int)value;
+  } else {
+    throw fd::Error(FD_ERR_INVALID_ARG, "unknown option: " + k);
+  }
   FD_API_END
 }
 

@@ -87,6 +87,7 @@ struct Engine {
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   // optional per-launch kernel timing (HIP events on the launch stream)
+  int forest_variant = 0;  // "forest_kernel" option
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pool
   size_t events_used = 0;

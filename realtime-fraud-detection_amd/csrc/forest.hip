@@ -322,6 +322,180 @@ forest_kernel(const float* __restrict__ X, int64_t n, int ld, int nf, const char
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// v2 (depth <= 8, the configurations on the path): 1024-thread workgroups on the same 256-txn tile.
+// The 64k-txn micro-batch gives exactly 256 tiles = one workgroup per CU, so v1 (256 threads) ran
+// ONE wave per SIMD and was issue/latency bound. v2 runs 16 waves: wave w walks, for the 64
+// transactions of txn group (w & 3), the trees of tree group (w >> 2) of each staged chunk (2 of the
+// chunk's 8 trees) and stores the leaf values in LDS; one rotating "owner" tree group per chunk then
+// adds the chunk's 8 values per transaction in tree order into the LDS accumulator, so the sum is
+// still the reference's sequential order (bit-exact) while the walking is spread over 16 waves.
+//
+// LDS layout (absolute byte addresses, dynamic LDS starts at 0):
+//   [0, nf*1024)            Xs[f][256] f32     -> x address = (meta & 0x7fffffff) | txn*4 (one v_and_or)
+//   buf0, buf1              2 x chunk_stride   staged trees (LDS-DMA)
+//   lv0, lv1                2 x [8][256] LeafT leaf values of the chunk being summed / being walked
+//   accL                    [256] LeafT        running sum per transaction
+// A node address a walks as a' = 2a - tb + 8 + 8*right (tb = tree base), i.e. breadth-first slots.
+
+typedef __attribute__((address_space(3))) char lds_char;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+template <typename T>
+__device__ __forceinline__ T lds_load(uint32_t addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) T*>((size_t)addr);
+}
+template <typename T>
+__device__ __forceinline__ void lds_store(uint32_t addr, T v) {
+  *reinterpret_cast<__attribute__((address_space(3))) T*>((size_t)addr) = v;
+}
+
+constexpr int kWG2 = 1024;
+constexpr int kTreeGroups2 = kWG2 / kTile;  // 4
+constexpr int kCH2 = 8;                     // trees per staged chunk
+constexpr int kTPG2 = kCH2 / kTreeGroups2;  // trees per wave per chunk
+
+template <int D, typename LeafT, bool NAN_AWARE>
+__device__ __forceinline__ void walk2(uint32_t buf, int gg, uint32_t lane4, uint32_t (&a)[kTPG2]) {
+  using G = Geo<D, LeafT>;
+  uint32_t tb[kTPG2], k0[kTPG2], k1[kTPG2];
+#pragma unroll
+  for (int j = 0; j < kTPG2; ++j) {
+    tb[j] = buf + (uint32_t)((gg * kTPG2 + j) * G::TREE_BYTES);
+    k0[j] = 8u - tb[j];
+    k1[j] = 16u - tb[j];
+    a[j] = tb[j];
+  }
+#pragma unroll
+  for (int l = 0; l < D; ++l) {
+#pragma unroll
+    for (int j = 0; j < kTPG2; ++j) {
+      const u32x2 nd = lds_load<u32x2>(a[j]);
+      const float x = lds_load<float>((nd.y & 0x7fffffffu) | lane4);
+      bool right = !(x < __uint_as_float(nd.x));
+      if (NAN_AWARE) {
+        if (x != x) right = (nd.y >> 31) == 0u;
+      }
+      a[j] = 2u * a[j] + (right ? k1[j] : k0[j]);
+    }
+  }
+}
+
+template <int D, typename LeafT, int KIND>
+__global__ void __launch_bounds__(kWG2)
+forest_kernel_v2(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
+                 int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
+                 float base_margin, double if_offset, double if_denom, double* __restrict__ out_prob,
+                 double* __restrict__ out_raw, int32_t* __restrict__ out_leaf) {
+  using G = Geo<D, LeafT>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t s0 = (uint32_t)(size_t)((lds_char*)smem);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int gg = wave >> 2;                // tree group
+  const int txn = ((wave & 3) << 6) + lane;  // 0..255 within the tile
+  const uint32_t lane4 = s0 + (uint32_t)txn * 4u;
+  const uint32_t xbytes = (uint32_t)nf * 1024u;
+  const uint32_t bufA = s0 + xbytes, bufB = bufA + (uint32_t)chunk_stride;
+  const uint32_t lvA = bufB + (uint32_t)chunk_stride;
+  const uint32_t lvB = lvA + kCH2 * kTile * sizeof(LeafT);
+  const uint32_t accL = lvB + kCH2 * kTile * sizeof(LeafT);
+  const int64_t row = (int64_t)blockIdx.x * kTile + txn;
+  const bool valid = row < n;
+
+  // chunk 0 lands while the feature tile loads (16 waves issue its 1 KiB pieces)
+  {
+    const int pieces = chunk_stride >> 10;
+    for (int p = wave; p < pieces; p += kWG2 / 64)
+      __builtin_amdgcn_global_load_lds((const void*)(blob + (p << 10) + lane * 16),
+                                       (lds_ptr)(smem + xbytes + (p << 10)), 16, 0, 0);
+  }
+  // feature tile: 4 threads per transaction, each a strided subset of the columns
+  int anynan = 0;
+  const int ncopy = ld < nf ? ld : nf;
+  {
+    const int q = tid >> 8;  // 0..3 (the four threads sharing `txn` have q = tree group)
+    float* Xs = reinterpret_cast<float*>(smem);
+    if (valid) {
+      const float* xr = X + row * (int64_t)ld;
+      for (int f = q; f < ncopy; f += 4) {
+        const float v = xr[f];
+        Xs[f * kTile + txn] = v;
+        anynan |= (v != v);
+      }
+      for (int f = ncopy + q; f < nf; f += 4) Xs[f * kTile + txn] = __builtin_nanf("");
+      anynan |= (ncopy < nf);
+    } else {
+      for (int f = q; f < nf; f += 4) Xs[f * kTile + txn] = 0.f;
+    }
+    if (gg == 0)
+      lds_store<LeafT>(accL + txn * sizeof(LeafT),
+                       (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0);
+  }
+  const bool tile_nan = __syncthreads_or(anynan) != 0;
+
+  for (int k = 0; k < n_chunks; ++k) {
+    const uint32_t cur = (k & 1) ? bufB : bufA;
+    if (k + 1 < n_chunks) {
+      const char* src = blob + (size_t)(k + 1) * chunk_stride;
+      char* dst = smem + xbytes + ((k + 1) & 1) * chunk_stride;
+      const int pieces = chunk_stride >> 10;
+      for (int p = wave; p < pieces; p += kWG2 / 64)
+        __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16), (lds_ptr)(dst + (p << 10)),
+                                         16, 0, 0);
+    }
+    // owner of chunk k-1 adds its leaf values in tree order
+    if (k > 0 && gg == ((k - 1) & 3)) {
+      const uint32_t lv = ((k - 1) & 1) ? lvB : lvA;
+      LeafT acc = lds_load<LeafT>(accL + txn * sizeof(LeafT));
+#pragma unroll
+      for (int c = 0; c < kCH2; ++c) acc += lds_load<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT));
+      lds_store<LeafT>(accL + txn * sizeof(LeafT), acc);
+    }
+    uint32_t a[kTPG2];
+    if (tile_nan)
+      walk2<D, LeafT, true>(cur, gg, lane4, a);
+    else
+      walk2<D, LeafT, false>(cur, gg, lane4, a);
+    const uint32_t lv = (k & 1) ? lvB : lvA;
+#pragma unroll
+    for (int j = 0; j < kTPG2; ++j) {
+      const int c = gg * kTPG2 + j;
+      const uint32_t tb = cur + (uint32_t)(c * G::TREE_BYTES);
+      const uint32_t la = (sizeof(LeafT) == 8) ? a[j] : (tb + G::NI * 4u + ((a[j] - tb) >> 1));
+      lds_store<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT), lds_load<LeafT>(la));
+      if (out_leaf != nullptr && valid) {
+        const int tg = k * kCH2 + c;
+        if (tg < n_trees)
+          out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * G::NL + ((a[j] - tb) >> 3) - G::NI];
+      }
+    }
+    __syncthreads();  // chunk k+1 landed; lv[k&1] complete; owner of k-1 done with lv[(k-1)&1]
+  }
+  const int last = n_chunks - 1;
+  if (gg != (last & 3)) return;
+  LeafT acc = lds_load<LeafT>(accL + txn * sizeof(LeafT));
+  {
+    const uint32_t lv = (last & 1) ? lvB : lvA;
+#pragma unroll
+    for (int c = 0; c < kCH2; ++c) acc += lds_load<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT));
+  }
+  if (!valid) return;
+  if (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) {
+    const float m = (float)acc;
+    const float xm = fminf(-m, 88.7f);
+    const float denom = expf(xm) + 1.0f + 1e-16f;
+    out_prob[row] = (double)(1.0f / denom);
+    if (out_raw) out_raw[row] = (double)m;
+  } else {
+    const double d = (double)acc;
+    const double q = (if_denom != 0.0) ? d / if_denom : 1.0;
+    const double score = pow(2.0, -q);
+    const double decision = -score - if_offset;
+    out_prob[row] = 1.0 / (1.0 + exp(decision));
+    if (out_raw) out_raw[row] = d;
+  }
+}
+
 using KernelFn = void (*)(const float*, int64_t, int, int, const char*, int, int, const int32_t*, int,
                           float, double, double, double*, double*, int32_t*);
 
@@ -348,6 +522,21 @@ KernelFn pick(int D) {
   }
 }
 
+template <typename LeafT, int KIND>
+KernelFn pick_v2(int D) {
+  switch (D) {
+    case 1: return forest_kernel_v2<1, LeafT, KIND>;
+    case 2: return forest_kernel_v2<2, LeafT, KIND>;
+    case 3: return forest_kernel_v2<3, LeafT, KIND>;
+    case 4: return forest_kernel_v2<4, LeafT, KIND>;
+    case 5: return forest_kernel_v2<5, LeafT, KIND>;
+    case 6: return forest_kernel_v2<6, LeafT, KIND>;
+    case 7: return forest_kernel_v2<7, LeafT, KIND>;
+    case 8: return forest_kernel_v2<8, LeafT, KIND>;
+    default: return nullptr;
+  }
+}
+
 }  // namespace
 
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
@@ -355,16 +544,32 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   FD_REQUIRE(d_X && d_prob && ld > 0, FD_ERR_INVALID_ARG, "null buffer or bad ld");
   if (n == 0) return;
   const bool xgb = pf.kind == FD_FOREST_XGB_BINARY_LOGISTIC;
-  KernelFn fn = xgb ? pick<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth)
-                    : pick<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth);
-  const size_t lds = (size_t)pf.num_feature * kTile * 4 + 2 * pf.chunk_stride;
+  const size_t leaf_sz = xgb ? sizeof(float) : sizeof(double);
+  const size_t xbytes = (size_t)pf.num_feature * kTile * 4;
+  KernelFn fn = nullptr;
+  int threads = kTile;
+  size_t lds = 0;
+  // v2: 1024-thread tree-split kernel where it fits the 160 KiB LDS budget
+  const size_t lds2 = xbytes + 2 * pf.chunk_stride + 2 * (size_t)kCH2 * kTile * leaf_sz + kTile * leaf_sz;
+  if (e.forest_variant != 1 && pf.depth <= 8 && pf.chunk == kCH2 && lds2 <= 160 * 1024) {
+    fn = xgb ? pick_v2<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth)
+             : pick_v2<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth);
+    threads = kWG2;
+    lds = lds2;
+  }
+  if (!fn) {
+    FD_REQUIRE(e.forest_variant != 2, FD_ERR_UNSUPPORTED, "forest kernel v2 does not fit this forest");
+    fn = xgb ? pick<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth)
+             : pick<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth);
+    lds = xbytes + 2 * pf.chunk_stride;
+  }
   FD_REQUIRE(lds <= 160 * 1024, FD_ERR_UNSUPPORTED, "LDS budget exceeded");
   FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int64_t blocks = (n + kTile - 1) / kTile;
   FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
   std::pair<hipEvent_t, hipEvent_t>* ev = e.timing ? e.next_event_pair() : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->first, e.stream));
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kTile), lds, e.stream, d_X, n, (int)ld,
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(threads), lds, e.stream, d_X, n, (int)ld,
                      pf.num_feature, pf.blob.as<const char>(), pf.n_chunks, (int)pf.chunk_stride,
                      pf.leaf_ids.as<const int32_t>(), pf.n_trees, pf.base_margin, pf.if_offset,
                      pf.if_denominator, d_prob, d_raw, d_leaf);

@@ -94,6 +94,7 @@ SIGNATURES = {
     "fd_engine_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
     "fd_engine_destroy": (C.c_int, [_vp]),
     "fd_engine_set_stream": (C.c_int, [_vp, _vp]),
+    "fd_engine_reset_stream": (C.c_int, [_vp]),
     "fd_engine_sync": (C.c_int, [_vp]),
     "fd_load_forest": (C.c_int, [_vp, C.c_int, C.POINTER(fd_forest_params), C.POINTER(fd_tree_arrays)]),
     "fd_unload_forest": (C.c_int, [_vp, C.c_int]),
@@ -103,6 +104,7 @@ SIGNATURES = {
     "fd_blend_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _i64, C.POINTER(_vp), _vp, _vp, _vp, _vp, _vp]),
     "fd_blend_host": (C.c_int, [_vp, C.POINTER(fd_blend_params), _i64, C.POINTER(_vp), _vp, _vp, _vp, _vp, _vp]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
+    "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
     "fd_timing_read": (C.c_int, [_vp, _dp, C.POINTER(_i64)]),
     "fd_pack_forest_host": (C.c_int, [C.POINTER(fd_forest_params), C.POINTER(fd_tree_arrays), _vp, _i64, _vp, _i64,
                                       C.POINTER(fd_pack_info)]),

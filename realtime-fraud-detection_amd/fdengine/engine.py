@@ -50,13 +50,21 @@ class FraudEngine:
         return self._h
 
     def set_stream(self, stream_ptr: Optional[int]) -> None:
-        N.call("fd_engine_set_stream", self._h, C.c_void_p(stream_ptr) if stream_ptr else None)
+        """stream_ptr: a hipStream_t handle (torch.cuda.Stream.cuda_stream; 0 = the null/default
+        stream). None restores the engine's own stream."""
+        if stream_ptr is None:
+            N.call("fd_engine_reset_stream", self._h)
+        else:
+            N.call("fd_engine_set_stream", self._h, C.c_void_p(int(stream_ptr)) if stream_ptr else None)
 
     def sync(self) -> None:
         N.call("fd_engine_sync", self._h)
 
     def set_timing(self, enable: bool) -> None:
         N.call("fd_engine_set_timing", self._h, 1 if enable else 0)
+
+    def set_option(self, key: str, value: int) -> None:
+        N.call("fd_engine_set_option", self._h, key.encode(), int(value))
 
     def read_timing(self):
         """-> (total kernel ms, timed launches) since the last read."""

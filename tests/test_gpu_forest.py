@@ -111,3 +111,24 @@ def test_device_pointer_path_matches_host_path(engine):
     finally:
         engine.set_stream(None)
     np.testing.assert_array_equal(dp.cpu().numpy(), host)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_kernel_variants_agree(engine, variant):
+    """Both forest kernels (256-thread, 1024-thread tree-split) give the oracle's bits."""
+    engine.set_option("forest_kernel", variant)
+    try:
+        prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 0, 3001, 203, 8, 50, seed=81, p_leaf=0.05, nan_frac=0.01)
+        np.testing.assert_array_equal(leaf, rl)
+        np.testing.assert_array_equal(raw.astype(np.float32), rm)
+        assert np.abs(prob - rp).max() <= PROB_TOL
+        Xtr = synth.feature_matrix(2000, 40, seed=82).astype(np.float64)
+        fa = iforest_from_sklearn(synth.isolation_forest(Xtr, n_estimators=37))
+        X = synth.feature_matrix(1500, 40, seed=83)
+        engine.load_forest(1, fa)
+        p, d, lf = engine.predict(1, X, want_raw=True, want_leaf=True)
+        rp2, rd2, rl2 = oracle.iforest_predict(fa, X, want_leaf=True)
+        np.testing.assert_array_equal(lf, rl2)
+        np.testing.assert_array_equal(d, rd2)
+    finally:
+        engine.set_option("forest_kernel", 0)
