@@ -198,6 +198,18 @@ __device__ __forceinline__ void stage_chunk(const char* __restrict__ src, char* 
   }
 }
 
+// Tile-wide OR that is also the prologue barrier. Hand-rolled (per-wave ballot -> one LDS word per
+// wave) because __syncthreads_or pulls 256 B of STATIC LDS into the kernel, which shifts the
+// dynamic-LDS base and breaks the 1 KiB-aligned feature-tile addressing of forest_kernel_v2.
+__device__ __forceinline__ bool tile_any(int pred, uint32_t* flags, int nwaves) {
+  const unsigned long long b = __ballot(pred);
+  if ((threadIdx.x & 63) == 0) flags[threadIdx.x >> 6] = (b != 0ull) ? 1u : 0u;
+  __syncthreads();
+  uint32_t r = 0;
+  for (int i = 0; i < nwaves; ++i) r |= flags[i];
+  return r != 0u;
+}
+
 // Walk CH perfect trees of one LDS chunk for this lane; returns leaf slots in idx[].
 template <int D, int CH, typename LeafT, bool NAN_AWARE>
 __device__ __forceinline__ void walk_chunk(const char* cb, const char* xlane, uint32_t (&idx)[CH]) {
@@ -270,7 +282,8 @@ forest_kernel(const float* __restrict__ X, int64_t n, int ld, int nf, const char
   } else {
     for (int f = 0; f < nf; ++f) Xs[f * kTile + t] = 0.f;
   }
-  const bool tile_nan = __syncthreads_or(anynan) != 0;  // barrier: tile + chunk 0 visible
+  // barrier: feature tile + chunk 0 visible (the barrier's vmcnt(0) drains the LDS-DMA)
+  const bool tile_nan = tile_any(anynan, reinterpret_cast<uint32_t*>(bufs + 2 * chunk_stride), kTile / 64);
 
   const char* xlane = reinterpret_cast<const char*>(Xs + t);
   LeafT acc = (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0;
@@ -389,7 +402,11 @@ forest_kernel_v2(const float* __restrict__ X, int64_t n, int ld, int nf, const c
                  double* __restrict__ out_raw, int32_t* __restrict__ out_leaf) {
   using G = Geo<D, LeafT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const uint32_t s0 = (uint32_t)(size_t)((lds_char*)smem);
+  // Feature-tile addressing needs a 1 KiB-aligned base: (meta & 0x7fffffff) | txn*4. The kernel uses
+  // no static LDS, so the dynamic base is 0; the host reserves 1 KiB of slack in case it is not.
+  const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
+  const uint32_t s0 = (sdyn + 1023u) & ~1023u;
+  char* const lbase = smem + (s0 - sdyn);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int gg = wave >> 2;                // tree group
   const int txn = ((wave & 3) << 6) + lane;  // 0..255 within the tile
@@ -407,14 +424,14 @@ forest_kernel_v2(const float* __restrict__ X, int64_t n, int ld, int nf, const c
     const int pieces = chunk_stride >> 10;
     for (int p = wave; p < pieces; p += kWG2 / 64)
       __builtin_amdgcn_global_load_lds((const void*)(blob + (p << 10) + lane * 16),
-                                       (lds_ptr)(smem + xbytes + (p << 10)), 16, 0, 0);
+                                       (lds_ptr)(lbase + xbytes + (p << 10)), 16, 0, 0);
   }
   // feature tile: 4 threads per transaction, each a strided subset of the columns
   int anynan = 0;
   const int ncopy = ld < nf ? ld : nf;
   {
     const int q = tid >> 8;  // 0..3 (the four threads sharing `txn` have q = tree group)
-    float* Xs = reinterpret_cast<float*>(smem);
+    float* Xs = reinterpret_cast<float*>(lbase);
     if (valid) {
       const float* xr = X + row * (int64_t)ld;
       for (int f = q; f < ncopy; f += 4) {
@@ -431,13 +448,14 @@ forest_kernel_v2(const float* __restrict__ X, int64_t n, int ld, int nf, const c
       lds_store<LeafT>(accL + txn * sizeof(LeafT),
                        (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0);
   }
-  const bool tile_nan = __syncthreads_or(anynan) != 0;
+  const bool tile_nan =
+      tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (accL - s0) + kTile * sizeof(LeafT)), kWG2 / 64);
 
   for (int k = 0; k < n_chunks; ++k) {
     const uint32_t cur = (k & 1) ? bufB : bufA;
     if (k + 1 < n_chunks) {
       const char* src = blob + (size_t)(k + 1) * chunk_stride;
-      char* dst = smem + xbytes + ((k + 1) & 1) * chunk_stride;
+      char* dst = lbase + xbytes + ((k + 1) & 1) * chunk_stride;
       const int pieces = chunk_stride >> 10;
       for (int p = wave; p < pieces; p += kWG2 / 64)
         __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16), (lds_ptr)(dst + (p << 10)),
@@ -550,7 +568,8 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   int threads = kTile;
   size_t lds = 0;
   // v2: 1024-thread tree-split kernel where it fits the 160 KiB LDS budget
-  const size_t lds2 = xbytes + 2 * pf.chunk_stride + 2 * (size_t)kCH2 * kTile * leaf_sz + kTile * leaf_sz;
+  // + 16 wave flags (tile_any) + 1 KiB alignment slack for the feature tile
+  const size_t lds2 = xbytes + 2 * pf.chunk_stride + 2 * (size_t)kCH2 * kTile * leaf_sz + kTile * leaf_sz + 64 + 1024;
   if (e.forest_variant != 1 && pf.depth <= 8 && pf.chunk == kCH2 && lds2 <= 160 * 1024) {
     fn = xgb ? pick_v2<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth)
              : pick_v2<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth);
@@ -561,7 +580,7 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
     FD_REQUIRE(e.forest_variant != 2, FD_ERR_UNSUPPORTED, "forest kernel v2 does not fit this forest");
     fn = xgb ? pick<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth)
              : pick<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth);
-    lds = xbytes + 2 * pf.chunk_stride;
+    lds = xbytes + 2 * pf.chunk_stride + 64;  // + tile_any flags
   }
   FD_REQUIRE(lds <= 160 * 1024, FD_ERR_UNSUPPORTED, "LDS budget exceeded");
   FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

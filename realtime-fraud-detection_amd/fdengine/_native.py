@@ -117,7 +117,27 @@ class NativeError(RuntimeError):
         self.code = code
 
 
+def _preload_hip_runtime() -> None:
+    """One process, one HIP runtime. PyTorch-ROCm wheels bundle their own libamdhip64.so and NEED it
+    by the unversioned name, so if libfdengine.so (NEEDED libamdhip64.so.7) pulled /opt/rocm's copy in
+    first, a later `import torch` would map a SECOND runtime that finds no GPU. Load the copy torch
+    will use first (by path, so the loader identifies it as the same file when torch asks for it)."""
+    if os.environ.get("FDENGINE_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.origin:
+        return
+    cand = Path(spec.origin).parent / "lib" / "libamdhip64.so"
+    if cand.exists():
+        C.CDLL(str(cand), mode=C.RTLD_GLOBAL)
+
+
 def _load() -> C.CDLL:
+    _preload_hip_runtime()
     if not LIB_PATH.exists():
         raise ImportError(
             f"libfdengine.so not found at {LIB_PATH}. Build it with "
