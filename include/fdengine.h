@@ -148,6 +148,22 @@ int fd_blend_host(fd_engine* eng, const fd_blend_params* params, int64_t n,
                   const double* const* probs, const uint8_t* present,
                   double* fraud_prob, double* confidence, uint8_t* decision, uint8_t* risk);
 
+/* ---------------------------------------------------------------- batched scoring */
+/* Replaces the per-transaction loop of /batch-predict (ml/main.py:235-249) for prepared scoring
+   vectors: every forest model scores the same X, then the blend runs, all on the device.
+   Model m (blend order) is either a loaded forest (slots[m] >= 0) or an externally computed
+   probability column ext_probs[m] (slots[m] < 0; host pointer for _host, device for _device);
+   present[m] == 0 drops model m. d_model_probs (optional) receives the n x n_models column-major
+   per-model probabilities (model m at offset m*n). */
+int fd_score_matrix_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                           const double* const* ext_probs, const uint8_t* present, const float* d_X,
+                           int64_t n, int32_t ld, double* d_model_probs, double* d_fraud_prob,
+                           double* d_confidence, uint8_t* d_decision, uint8_t* d_risk);
+int fd_score_matrix_host(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                         const double* const* ext_probs, const uint8_t* present, const float* X, int64_t n,
+                         int32_t ld, double* model_probs, double* fraud_prob, double* confidence,
+                         uint8_t* decision, uint8_t* risk);
+
 /* ---------------------------------------------------------------- diagnostics */
 /* Per-launch device timing of the engine's hot kernels, measured with HIP events recorded on the
    launch stream around each kernel. fd_timing_read synchronises, returns the summed kernel time (ms)

@@ -59,6 +59,37 @@ static fd::PackedForest& slot_of(Engine& e, int slot) {
   return e.forests[slot];
 }
 
+// Score the same feature matrix with every forest model, then blend (all on e.stream).
+static void score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slots, const double* const* ext,
+                         const uint8_t* present, const float* dX, int64_t n, int32_t ld, double* dMP,
+                         double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk) {
+  FD_REQUIRE(p.n_models > 0 && p.n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "n_models out of range");
+  FD_REQUIRE(slots != nullptr && dfp != nullptr, FD_ERR_INVALID_ARG, "null slots/output");
+  if (n == 0) return;
+  const int M = p.n_models;
+  if (!dMP) {
+    e.scratch_probs.ensure((size_t)n * M * sizeof(double));
+    dMP = e.scratch_probs.as<double>();
+  }
+  const double* cols[FD_MAX_MODELS] = {};
+  for (int m = 0; m < M; ++m) {
+    if (present && !present[m]) continue;
+    double* col = dMP + (size_t)m * n;
+    if (slots[m] >= 0) {
+      const fd::PackedForest& pf = slot_of(e, slots[m]);
+      FD_REQUIRE(pf.loaded, FD_ERR_NOT_LOADED, "Model in slot " + std::to_string(slots[m]) + " not loaded");
+      fd::launch_forest(e, pf, dX, n, ld, col, nullptr, nullptr);
+      cols[m] = col;
+    } else {
+      FD_REQUIRE(ext && ext[m], FD_ERR_INVALID_ARG, "model without slot needs an external probability column");
+      if (ext[m] != col)
+        FD_HIP(hipMemcpyAsync(col, ext[m], (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, e.stream));
+      cols[m] = col;
+    }
+  }
+  fd::launch_blend(e, p, n, cols, present, dfp, dconf, ddec, drisk);
+}
+
 extern "C" {
 
 const char* fd_last_error(void) { return fd::g_last_error.c_str(); }
@@ -110,6 +141,8 @@ int fd_engine_destroy(fd_engine* eng) {
   e.stage_out1.release();
   e.stage_out2.release();
   e.stage_out3.release();
+  e.scratch_probs.release();
+  e.stage_ext.release();
   for (auto& ev : e.events) {
     (void)hipEventDestroy(ev.first);
     (void)hipEventDestroy(ev.second);
@@ -268,6 +301,58 @@ int fd_forest_predict_host(fd_engine* eng, int slot, const float* X, int64_t n, 
   if (leaf)
     FD_HIP(hipMemcpyAsync(leaf, e.stage_out2.ptr, (size_t)n * pf.n_trees * sizeof(int32_t),
                           hipMemcpyDeviceToHost, e.stream));
+  FD_HIP(hipStreamSynchronize(e.stream));
+  FD_API_END
+}
+
+int fd_score_matrix_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                           const double* const* ext_probs, const uint8_t* present, const float* d_X,
+                           int64_t n, int32_t ld, double* d_model_probs, double* d_fraud_prob,
+                           double* d_confidence, uint8_t* d_decision, uint8_t* d_risk) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params && d_X && ld > 0 && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  score_matrix(e, *params, slots, ext_probs, present, d_X, n, ld, d_model_probs, d_fraud_prob, d_confidence,
+               d_decision, d_risk);
+  FD_API_END
+}
+
+int fd_score_matrix_host(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                         const double* const* ext_probs, const uint8_t* present, const float* X, int64_t n,
+                         int32_t ld, double* model_probs, double* fraud_prob, double* confidence,
+                         uint8_t* decision, uint8_t* risk) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params && slots && X && fraud_prob && ld > 0 && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  FD_REQUIRE(params->n_models > 0 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "n_models out of range");
+  if (n == 0) return FD_OK;
+  const int M = params->n_models;
+  const size_t xb = (size_t)n * ld * sizeof(float);
+  e.stage_in.ensure(xb);
+  e.scratch_probs.ensure((size_t)n * M * sizeof(double));
+  e.stage_out0.ensure((size_t)n * sizeof(double));
+  e.stage_out1.ensure((size_t)n * sizeof(double));
+  e.stage_out2.ensure((size_t)n);
+  e.stage_out3.ensure((size_t)n);
+  FD_HIP(hipMemcpyAsync(e.stage_in.ptr, X, xb, hipMemcpyHostToDevice, e.stream));
+  double* dMP = e.scratch_probs.as<double>();
+  const double* dext[FD_MAX_MODELS] = {};
+  for (int m = 0; m < M; ++m) {
+    if (slots[m] >= 0 || (present && !present[m])) continue;
+    FD_REQUIRE(ext_probs && ext_probs[m], FD_ERR_INVALID_ARG, "model without slot needs an external probability column");
+    FD_HIP(hipMemcpyAsync(dMP + (size_t)m * n, ext_probs[m], (size_t)n * sizeof(double), hipMemcpyHostToDevice,
+                          e.stream));
+    dext[m] = dMP + (size_t)m * n;
+  }
+  score_matrix(e, *params, slots, dext, present, e.stage_in.as<float>(), n, ld, dMP, e.stage_out0.as<double>(),
+               e.stage_out1.as<double>(), e.stage_out2.as<uint8_t>(), e.stage_out3.as<uint8_t>());
+  if (model_probs)
+    FD_HIP(hipMemcpyAsync(model_probs, dMP, (size_t)n * M * sizeof(double), hipMemcpyDeviceToHost, e.stream));
+  FD_HIP(hipMemcpyAsync(fraud_prob, e.stage_out0.ptr, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, e.stream));
+  if (confidence)
+    FD_HIP(hipMemcpyAsync(confidence, e.stage_out1.ptr, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, e.stream));
+  if (decision) FD_HIP(hipMemcpyAsync(decision, e.stage_out2.ptr, (size_t)n, hipMemcpyDeviceToHost, e.stream));
+  if (risk) FD_HIP(hipMemcpyAsync(risk, e.stage_out3.ptr, (size_t)n, hipMemcpyDeviceToHost, e.stream));
   FD_HIP(hipStreamSynchronize(e.stream));
   FD_API_END
 }

@@ -86,6 +86,7 @@ struct Engine {
   PackedForest forests[kMaxSlots];
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
+  DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
   // optional per-launch kernel timing (HIP events on the launch stream)
   int forest_variant = 0;  // "forest_kernel" option
   bool timing = false;

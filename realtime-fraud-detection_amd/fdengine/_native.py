@@ -103,6 +103,10 @@ SIGNATURES = {
     "fd_forest_predict_host": (C.c_int, [_vp, C.c_int, _vp, _i64, _i32, _vp, _vp, _vp]),
     "fd_blend_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _i64, C.POINTER(_vp), _vp, _vp, _vp, _vp, _vp]),
     "fd_blend_host": (C.c_int, [_vp, C.POINTER(fd_blend_params), _i64, C.POINTER(_vp), _vp, _vp, _vp, _vp, _vp]),
+    "fd_score_matrix_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, C.POINTER(_vp), _vp, _vp, _i64, _i32,
+                                         _vp, _vp, _vp, _vp, _vp]),
+    "fd_score_matrix_host": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, C.POINTER(_vp), _vp, _vp, _i64, _i32,
+                                       _vp, _vp, _vp, _vp, _vp]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
     "fd_timing_read": (C.c_int, [_vp, _dp, C.POINTER(_i64)]),

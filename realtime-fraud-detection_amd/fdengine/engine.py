@@ -148,6 +148,32 @@ class FraudEngine:
                _ptr(dec), _ptr(risk))
         return fp, conf, dec, risk
 
+    def score_matrix(self, params: N.fd_blend_params, slots: Sequence[int], X: np.ndarray,
+                     ext_probs: Optional[Sequence[Optional[np.ndarray]]] = None,
+                     present: Optional[Sequence[int]] = None):
+        """Every forest model (slots[m] >= 0) scores X, external columns fill the rest, then blend.
+        -> (model_probs [M, n] f64, fraud_prob, confidence, decision u8, risk u8)."""
+        X = np.ascontiguousarray(np.asarray(X, dtype=np.float32))
+        n, ld = X.shape
+        M = params.n_models
+        sl = np.array(list(slots) + [-1] * (N.FD_MAX_MODELS - len(slots)), np.int32)
+        pres = np.array([1] * M if present is None else list(present), np.uint8)
+        ext = (C.c_void_p * N.FD_MAX_MODELS)()
+        keep = []
+        for m in range(M):
+            if sl[m] < 0 and pres[m]:
+                col = np.ascontiguousarray(ext_probs[m], dtype=np.float64)
+                keep.append(col)
+                ext[m] = col.ctypes.data
+        mp = np.empty((M, n), np.float64)
+        fp = np.empty(n, np.float64)
+        conf = np.empty(n, np.float64)
+        dec = np.empty(n, np.uint8)
+        risk = np.empty(n, np.uint8)
+        N.call("fd_score_matrix_host", self._h, C.byref(params), _ptr(sl), ext, _ptr(pres), _ptr(X), n, ld,
+               _ptr(mp), _ptr(fp), _ptr(conf), _ptr(dec), _ptr(risk))
+        return mp, fp, conf, dec, risk
+
     def blend_device(self, params: N.fd_blend_params, n: int, prob_ptrs: Sequence[Optional[int]],
                      fp_ptr: int, conf_ptr: int = 0, dec_ptr: int = 0, risk_ptr: int = 0) -> None:
         present = np.array([0 if p is None else 1 for p in prob_ptrs], np.uint8)
