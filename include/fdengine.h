@@ -148,6 +148,58 @@ int fd_blend_host(fd_engine* eng, const fd_blend_params* params, int64_t n,
                   const double* const* probs, const uint8_t* present,
                   double* fraud_prob, double* confidence, uint8_t* decision, uint8_t* risk);
 
+/* ---------------------------------------------------------------- card state + features (a2-a7) */
+/* HBM-resident keyed state replacing the Redis round trips of the feature half:
+   velocity hashes velocity:{user}:{5min|1hour|24hour} (fl/services/RedisService.java:178-207,
+   fl/sinks/RedisTransactionSink.java:116-135) and the user-profile lookups (RedisService.java:83-100).
+   Cards are keyed by a u64 (hash of the reference's user_id); open addressing, insert on first use. */
+enum fd_window_mode {
+  FD_WINDOW_REDIS_COMPAT = 0, /* session counter, TTL 3600 s refreshed per write: the reference's behaviour */
+  FD_WINDOW_SLIDING = 1       /* true (t-W, t] windows over the card's last ring_k events */
+};
+#define FD_RAW_FEATURES 16  /* bridged Flink features per txn (column order: DESIGN.md "Features") */
+#define FD_VECTOR_WIDTH 64  /* EnsemblePredictor._prepare_features width (ml/models/ensemble_predictor.py:241) */
+typedef struct {
+  int64_t capacity;    /* card slots (rounded up to a power of two; keep >= 2x the cards expected) */
+  int32_t window_mode; /* enum fd_window_mode */
+  int32_t ring_k;      /* events kept per card in sliding mode (1..64) */
+} fd_state_params;
+int fd_state_init(fd_engine* eng, const fd_state_params* params);
+int fd_state_clear(fd_engine* eng);
+int fd_state_info(fd_engine* eng, int64_t* capacity, int64_t* cards);
+/* user profiles (simulator.py:40-58 UserProfile; FeatureExtractor.java:216-252, 301-313) */
+typedef struct {
+  int64_t n;
+  const uint64_t* key;
+  const double* avg_amount;        /* NaN = null (-> 0.0, FeatureExtractor.java:239-240) */
+  const int32_t* account_age_days;
+  const uint64_t* device_fp;       /* n x 3 fingerprint hashes, 0 = none */
+} fd_users;
+int fd_state_load_users_host(fd_engine* eng, const fd_users* users);
+/* merchant table, replicated (simulator.py:60-75; FeatureExtractor.java:257-296) */
+typedef struct {
+  int64_t n;
+  const double* fraud_rate;      /* NaN = null (-> 0.05) */
+  const double* risk_multiplier; /* MerchantProfile.getRiskMultiplier() (class absent in the reference) */
+} fd_merchants;
+int fd_load_merchants_host(fd_engine* eng, const fd_merchants* merchants);
+/* one micro-batch of transactions in arrival order (SoA; device pointers for _device, host for _host) */
+typedef struct {
+  const uint64_t* card_key;
+  const int64_t* ts_ms;
+  const int64_t* amount_cents;
+  const int32_t* merchant;   /* index into the merchant table, -1 = unknown */
+  const uint64_t* device_fp; /* 0 = null */
+  const uint8_t* ip_class;   /* 0 = null, 1 = private, 2 = public (FeatureExtractor.java:434-445) */
+  const uint8_t* hour;       /* Transaction.hourOfDay, 255 = null (-> UTC hour of ts) */
+  const uint8_t* weekend;    /* Transaction.isWeekend, 255 = null (-> ISO day >= 6) */
+} fd_txn_batch;
+/* Replaces FeatureExtractor.extractAllFeatures + the velocity read/write + FeatureProcessor +
+   _prepare_features for a batch: per card in arrival order, read-before-write. Outputs the scoring
+   vectors (n x 64 f32) and optionally the bridged raw features (n x FD_RAW_FEATURES f64). */
+int fd_features_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* d_vectors, double* d_raw);
+int fd_features_host(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* vectors, double* raw);
+
 /* ---------------------------------------------------------------- batched scoring */
 /* Replaces the per-transaction loop of /batch-predict (ml/main.py:235-249) for prepared scoring
    vectors: every forest model scores the same X, then the blend runs, all on the device.

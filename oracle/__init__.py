@@ -53,9 +53,8 @@ def lib() -> C.CDLL:
 
 
 def _register_features(L) -> None:
-    if hasattr(L, "orc_features_batch"):
-        from . import features_c
-        features_c.register(L)
+    from . import features_c
+    features_c.register(L)
 
 
 def _ptr(a):

@@ -143,6 +143,11 @@ int fd_engine_destroy(fd_engine* eng) {
   e.stage_out3.release();
   e.scratch_probs.release();
   e.stage_ext.release();
+  e.feat_vec.release();
+  e.feat_in.release();
+  for (auto* b : {&e.state.headers, &e.state.fps, &e.state.ring, &e.state.merchants, &e.state.slot,
+                  &e.state.next, &e.state.err})
+    b->release();
   for (auto& ev : e.events) {
     (void)hipEventDestroy(ev.first);
     (void)hipEventDestroy(ev.second);
@@ -302,6 +307,93 @@ int fd_forest_predict_host(fd_engine* eng, int slot, const float* X, int64_t n, 
     FD_HIP(hipMemcpyAsync(leaf, e.stage_out2.ptr, (size_t)n * pf.n_trees * sizeof(int32_t),
                           hipMemcpyDeviceToHost, e.stream));
   FD_HIP(hipStreamSynchronize(e.stream));
+  FD_API_END
+}
+
+int fd_state_init(fd_engine* eng, const fd_state_params* params) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
+  FD_HIP(hipStreamSynchronize(e.stream));
+  fd::state_init(e, *params);
+  FD_API_END
+}
+
+int fd_state_clear(fd_engine* eng) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::state_clear(e);
+  FD_API_END
+}
+
+int fd_state_info(fd_engine* eng, int64_t* capacity, int64_t* cards) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::features_check(e);
+  if (capacity) *capacity = e.state.cap;
+  if (cards) *cards = fd::state_count(e);
+  FD_API_END
+}
+
+int fd_state_load_users_host(fd_engine* eng, const fd_users* users) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(users, FD_ERR_INVALID_ARG, "null users");
+  fd::load_users(e, *users);
+  FD_API_END
+}
+
+int fd_load_merchants_host(fd_engine* eng, const fd_merchants* merchants) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(merchants, FD_ERR_INVALID_ARG, "null merchants");
+  FD_HIP(hipStreamSynchronize(e.stream));
+  fd::load_merchants(e, *merchants);
+  FD_API_END
+}
+
+int fd_features_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* d_vectors, double* d_raw) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
+  fd::launch_features(e, *txns, n, d_vectors, d_raw);
+  FD_API_END
+}
+
+int fd_features_host(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* vectors, double* raw) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(txns && vectors && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  if (n == 0) return FD_OK;
+  // stage the SoA columns in one device buffer (8-byte aligned segments)
+  const size_t seg8 = (size_t)n * 8, seg4 = ((size_t)n * 4 + 7) / 8 * 8, seg1 = ((size_t)n + 7) / 8 * 8;
+  const size_t total = 4 * seg8 + seg4 + 3 * seg1;
+  e.feat_in.ensure(total);
+  char* b = e.feat_in.as<char>();
+  fd_txn_batch d{};
+  size_t off = 0;
+  auto put = [&](const void* src, size_t bytes, size_t seg) -> void* {
+    FD_REQUIRE(src, FD_ERR_INVALID_ARG, "incomplete transaction batch");
+    void* dst = b + off;
+    FD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e.stream));
+    off += seg;
+    return dst;
+  };
+  d.card_key = (const uint64_t*)put(txns->card_key, n * 8, seg8);
+  d.ts_ms = (const int64_t*)put(txns->ts_ms, n * 8, seg8);
+  d.amount_cents = (const int64_t*)put(txns->amount_cents, n * 8, seg8);
+  d.device_fp = (const uint64_t*)put(txns->device_fp, n * 8, seg8);
+  d.merchant = (const int32_t*)put(txns->merchant, n * 4, seg4);
+  d.ip_class = (const uint8_t*)put(txns->ip_class, n, seg1);
+  d.hour = (const uint8_t*)put(txns->hour, n, seg1);
+  d.weekend = (const uint8_t*)put(txns->weekend, n, seg1);
+  e.feat_vec.ensure((size_t)n * FD_VECTOR_WIDTH * 4 + (raw ? (size_t)n * FD_RAW_FEATURES * 8 : 0));
+  float* dv = e.feat_vec.as<float>();
+  double* dr = raw ? reinterpret_cast<double*>(e.feat_vec.as<char>() + (size_t)n * FD_VECTOR_WIDTH * 4) : nullptr;
+  fd::launch_features(e, d, n, dv, dr);
+  FD_HIP(hipMemcpyAsync(vectors, dv, (size_t)n * FD_VECTOR_WIDTH * 4, hipMemcpyDeviceToHost, e.stream));
+  if (raw) FD_HIP(hipMemcpyAsync(raw, dr, (size_t)n * FD_RAW_FEATURES * 8, hipMemcpyDeviceToHost, e.stream));
+  fd::features_check(e);  // synchronises
   FD_API_END
 }
 

@@ -79,11 +79,24 @@ struct PackedForest {
   DeviceBuffer leaf_ids;  // n_trees_padded * 2^D original node ids (parity output)
 };
 
+// HBM-resident keyed card state (features.hip)
+struct CardStore {
+  bool ready = false;
+  int64_t cap = 0;   // slots (power of two)
+  int mode = 0;      // fd_window_mode
+  int K = 1;         // ring events per card (sliding)
+  unsigned epoch = 0;
+  int64_t n_merchants = 0;
+  DeviceBuffer headers, fps, ring, merchants, slot, next, err;
+};
+
 struct Engine {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   PackedForest forests[kMaxSlots];
+  CardStore state;
+  DeviceBuffer feat_vec, feat_in;  // host-API / fused-pipeline staging for features
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
@@ -108,6 +121,14 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t);
 void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
                    double* d_prob, double* d_raw, int32_t* d_leaf);
+// features.hip
+void state_init(Engine& e, const fd_state_params& p);
+void state_clear(Engine& e);
+int64_t state_count(Engine& e);
+void load_users(Engine& e, const fd_users& u);
+void load_merchants(Engine& e, const fd_merchants& m);
+void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw);
+void features_check(Engine& e);
 // blend.hip
 void launch_blend(Engine& e, const fd_blend_params& p, int64_t n, const double* const* d_probs,
                   const uint8_t* present, double* d_fp, double* d_conf, uint8_t* d_dec, uint8_t* d_risk);

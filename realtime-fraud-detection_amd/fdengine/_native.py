@@ -81,6 +81,31 @@ class fd_pack_info(C.Structure):
     ]
 
 
+class fd_state_params(C.Structure):
+    _fields_ = [("capacity", C.c_int64), ("window_mode", C.c_int32), ("ring_k", C.c_int32)]
+
+
+class fd_users(C.Structure):
+    _fields_ = [("n", C.c_int64), ("key", C.c_void_p), ("avg_amount", C.c_void_p),
+                ("account_age_days", C.c_void_p), ("device_fp", C.c_void_p)]
+
+
+class fd_merchants(C.Structure):
+    _fields_ = [("n", C.c_int64), ("fraud_rate", C.c_void_p), ("risk_multiplier", C.c_void_p)]
+
+
+class fd_txn_batch(C.Structure):
+    _fields_ = [("card_key", C.c_void_p), ("ts_ms", C.c_void_p), ("amount_cents", C.c_void_p),
+                ("merchant", C.c_void_p), ("device_fp", C.c_void_p), ("ip_class", C.c_void_p),
+                ("hour", C.c_void_p), ("weekend", C.c_void_p)]
+
+
+FD_WINDOW_REDIS_COMPAT = 0
+FD_WINDOW_SLIDING = 1
+FD_RAW_FEATURES = 16
+FD_VECTOR_WIDTH = 64
+TXN_FIELDS = ("card_key", "ts_ms", "amount_cents", "merchant", "device_fp", "ip_class", "hour", "weekend")
+
 _vp = C.c_void_p
 _i32 = C.c_int32
 _i64 = C.c_int64
@@ -107,6 +132,13 @@ SIGNATURES = {
                                          _vp, _vp, _vp, _vp, _vp]),
     "fd_score_matrix_host": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, C.POINTER(_vp), _vp, _vp, _i64, _i32,
                                        _vp, _vp, _vp, _vp, _vp]),
+    "fd_state_init": (C.c_int, [_vp, C.POINTER(fd_state_params)]),
+    "fd_state_clear": (C.c_int, [_vp]),
+    "fd_state_info": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_i64)]),
+    "fd_state_load_users_host": (C.c_int, [_vp, C.POINTER(fd_users)]),
+    "fd_load_merchants_host": (C.c_int, [_vp, C.POINTER(fd_merchants)]),
+    "fd_features_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _vp, _vp]),
+    "fd_features_host": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _vp, _vp]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
     "fd_timing_read": (C.c_int, [_vp, _dp, C.POINTER(_i64)]),

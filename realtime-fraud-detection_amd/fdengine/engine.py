@@ -116,6 +116,50 @@ class FraudEngine:
                C.c_void_p(prob_ptr), C.c_void_p(raw_ptr) if raw_ptr else None,
                C.c_void_p(leaf_ptr) if leaf_ptr else None)
 
+    # ------------------------------------------------------------------ card state + features
+    _TXN_DTYPES = {"card_key": np.uint64, "ts_ms": np.int64, "amount_cents": np.int64, "merchant": np.int32,
+                   "device_fp": np.uint64, "ip_class": np.uint8, "hour": np.uint8, "weekend": np.uint8}
+
+    def state_init(self, capacity: int, window_mode: int = N.FD_WINDOW_REDIS_COMPAT, ring_k: int = 16) -> None:
+        p = N.fd_state_params(int(capacity), int(window_mode), int(ring_k))
+        N.call("fd_state_init", self._h, C.byref(p))
+
+    def state_clear(self) -> None:
+        N.call("fd_state_clear", self._h)
+
+    def state_info(self):
+        cap, cards = C.c_int64(), C.c_int64()
+        N.call("fd_state_info", self._h, C.byref(cap), C.byref(cards))
+        return {"capacity": cap.value, "cards": cards.value}
+
+    def load_users(self, key, avg_amount, account_age_days, device_fp) -> None:
+        arr = [np.ascontiguousarray(key, np.uint64), np.ascontiguousarray(avg_amount, np.float64),
+               np.ascontiguousarray(account_age_days, np.int32),
+               np.ascontiguousarray(np.asarray(device_fp).reshape(-1, 3), np.uint64)]
+        u = N.fd_users(len(arr[0]), *[a.ctypes.data for a in arr])
+        N.call("fd_state_load_users_host", self._h, C.byref(u))
+
+    def load_merchants(self, fraud_rate, risk_multiplier) -> None:
+        arr = [np.ascontiguousarray(fraud_rate, np.float64), np.ascontiguousarray(risk_multiplier, np.float64)]
+        m = N.fd_merchants(len(arr[0]), *[a.ctypes.data for a in arr])
+        N.call("fd_load_merchants_host", self._h, C.byref(m))
+
+    def features(self, txns: dict, want_raw: bool = False):
+        """Host SoA batch (dict of arrays, arrival order) -> vectors f32 [n, 64] (+ raw f64 [n, 16])."""
+        cols = [np.ascontiguousarray(txns[f], self._TXN_DTYPES[f]) for f in N.TXN_FIELDS]
+        n = len(cols[0])
+        vec = np.empty((n, N.FD_VECTOR_WIDTH), np.float32)
+        raw = np.empty((n, N.FD_RAW_FEATURES), np.float64) if want_raw else None
+        b = N.fd_txn_batch(*[c.ctypes.data for c in cols])
+        N.call("fd_features_host", self._h, C.byref(b), n, _ptr(vec), _ptr(raw))
+        return (vec, raw) if want_raw else vec
+
+    def features_device(self, ptrs: dict, n: int, vec_ptr: int, raw_ptr: int = 0) -> None:
+        """ptrs: field -> device pointer (see fdengine._native.TXN_FIELDS)."""
+        b = N.fd_txn_batch(*[int(ptrs[f]) for f in N.TXN_FIELDS])
+        N.call("fd_features_device", self._h, C.byref(b), int(n), C.c_void_p(vec_ptr),
+               C.c_void_p(raw_ptr) if raw_ptr else None)
+
     # ------------------------------------------------------------------ blend
     @staticmethod
     def blend_params(weights: Sequence[float], conf_mult: Sequence[float], strategy: int = 0,

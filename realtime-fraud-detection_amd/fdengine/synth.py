@@ -108,6 +108,85 @@ def write_xgboost_json(path: str, doc: dict) -> None:
         json.dump(doc, f)
 
 
+# (category, risk level, avg amount, fraud rate): services/data-simulator/src/main/python/simulator.py:255-266
+MERCHANT_CATEGORIES = (("retail", "low", 50.0, 0.01), ("grocery", "low", 25.0, 0.005),
+                       ("gas_station", "medium", 40.0, 0.02), ("restaurant", "low", 35.0, 0.008),
+                       ("online_retail", "medium", 75.0, 0.025), ("gambling", "high", 200.0, 0.15),
+                       ("adult_entertainment", "high", 100.0, 0.12), ("pharmacy", "medium", 30.0, 0.01),
+                       ("jewelry", "high", 500.0, 0.08), ("electronics", "medium", 300.0, 0.03))
+# MerchantProfile.getRiskMultiplier() is referenced by FeatureExtractor.java:281 but the class is
+# missing from the reference source; the engine takes the multiplier per merchant from the host and
+# this is the build's declared table (clamped to [0,1] by FeatureProcessor as merchant_risk_score).
+RISK_MULTIPLIER = {"low": 0.25, "medium": 0.5, "high": 0.9}
+
+
+def _nonzero_u64(rng, n):
+    k = rng.integers(1, np.iinfo(np.int64).max, size=n, dtype=np.int64).astype(np.uint64)
+    return k | np.uint64(1) << np.uint64(63)
+
+
+def population(n_users: int, n_merchants: int = 5000, seed: int = 42) -> dict:
+    """Users (= cards) and merchants with the simulator's distributions (simulator.py:206-296).
+    Card keys are random 64-bit values standing in for hash64(user_id)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n_fp = rng.integers(1, 4, n_users)
+    fps = _nonzero_u64(rng, n_users * 3).reshape(n_users, 3)
+    fps[np.arange(3)[None, :] >= n_fp[:, None]] = 0
+    cat = rng.integers(0, len(MERCHANT_CATEGORIES), n_merchants)
+    return {
+        "users": {
+            "key": _nonzero_u64(rng, n_users),
+            "avg_amount": rng.lognormal(4.0, 1.0, n_users),
+            "account_age_days": rng.integers(0, 730, n_users).astype(np.int32),
+            "device_fp": fps,
+            "txn_frequency": (np.floor(rng.gamma(2.0, 2.0, n_users)) + 1).astype(np.int32),
+        },
+        "merchants": {
+            "category": cat.astype(np.int32),
+            "avg_amount": np.array([MERCHANT_CATEGORIES[c][2] for c in cat]) * rng.uniform(0.5, 2.0, n_merchants),
+            "fraud_rate": np.array([MERCHANT_CATEGORIES[c][3] for c in cat]),
+            "risk_multiplier": np.array([RISK_MULTIPLIER[MERCHANT_CATEGORIES[c][1]] for c in cat]),
+        },
+    }
+
+
+def txn_stream(pop: dict, n: int, seed: int = 7, t0_ms: int = 1_757_030_400_000, rate_per_s: float = None,
+               unknown_user_frac: float = 0.01, unknown_merchant_frac: float = 0.005) -> dict:
+    """Transactions in arrival order (simulator.py:298-374): user/merchant uniform, amount =
+    max(1, round(avg * N(1,.3) * N(1,.2), 2)) in integer cents, fraud patterns card_testing
+    (U(1,5)) / account_takeover (new device) / synthetic (U(1000,5000)) with the simulator's
+    probabilities (:107-127). Event time: Poisson arrivals at the population's aggregate rate
+    (sum of txn_frequency / 86400 s unless rate_per_s is given) from t0_ms."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    U, M = pop["users"], pop["merchants"]
+    nu, nm = len(U["key"]), len(M["category"])
+    lam = rate_per_s if rate_per_s else max(float(U["txn_frequency"].sum()) / 86400.0, 1e-3)
+    ts = t0_ms + np.floor(np.cumsum(rng.exponential(1000.0 / lam, n))).astype(np.int64)
+    u = rng.integers(0, nu, n)
+    key = U["key"][u].copy()
+    unknown = rng.random(n) < unknown_user_frac
+    key[unknown] = _nonzero_u64(rng, int(unknown.sum()))
+    merchant = rng.integers(0, nm, n).astype(np.int32)
+    merchant[rng.random(n) < unknown_merchant_frac] = -1
+    base = U["avg_amount"][u] * rng.normal(1.0, 0.3, n) * rng.normal(1.0, 0.2, n)
+    cents = np.maximum(100, np.rint(base * 100.0)).astype(np.int64)
+    roll = rng.random(n)
+    card_testing = roll < 0.02
+    takeover = (roll >= 0.02) & (roll < 0.03)
+    synthetic = (roll >= 0.03) & (roll < 0.035)
+    cents[card_testing] = np.rint(rng.uniform(1.0, 5.0, int(card_testing.sum())) * 100).astype(np.int64)
+    cents[synthetic] = np.rint(rng.uniform(1000.0, 5000.0, int(synthetic.sum())) * 100).astype(np.int64)
+    fp_pick = rng.integers(0, 3, n)
+    dfp = U["device_fp"][u, fp_pick]
+    first = U["device_fp"][u, 0]
+    dfp = np.where(dfp == 0, first, dfp)
+    dfp[takeover] = _nonzero_u64(rng, int(takeover.sum()))
+    ip_class = np.where(rng.random(n) < 0.05, 1, 2).astype(np.uint8)
+    return {"card_key": key, "ts_ms": ts, "amount_cents": cents, "merchant": merchant, "device_fp": dfp,
+            "ip_class": ip_class, "hour": np.full(n, 255, np.uint8), "weekend": np.full(n, 255, np.uint8),
+            "is_fraud": roll < 0.055}
+
+
 def isolation_forest(X_train: np.ndarray, n_estimators: int = 100, contamination: float = 0.05,
                      random_state: int = 42):
     from sklearn.ensemble import IsolationForest
