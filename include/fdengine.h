@@ -216,6 +216,15 @@ int fd_score_matrix_host(fd_engine* eng, const fd_blend_params* params, const in
                          int32_t ld, double* model_probs, double* fraud_prob, double* confidence,
                          uint8_t* decision, uint8_t* risk);
 
+/* The whole hot path for one micro-batch of transactions: fd_features_* (card state read/update,
+   scoring vectors) then fd_score_matrix_* on those vectors (ld = FD_VECTOR_WIDTH). d_vectors may be
+   NULL (engine scratch). Equivalent to the reference's per-transaction chain
+   FeatureExtractor -> RedisTransactionSink -> FeatureProcessor -> EnsemblePredictor.predict. */
+int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                          const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
+                          int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
+                          double* d_confidence, uint8_t* d_decision, uint8_t* d_risk);
+
 /* ---------------------------------------------------------------- diagnostics */
 /* Per-launch device timing of the engine's hot kernels, measured with HIP events recorded on the
    launch stream around each kernel. fd_timing_read synchronises, returns the summed kernel time (ms)

@@ -449,6 +449,25 @@ int fd_score_matrix_host(fd_engine* eng, const fd_blend_params* params, const in
   FD_API_END
 }
 
+int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                          const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
+                          int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
+                          double* d_confidence, uint8_t* d_decision, uint8_t* d_risk) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params && txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  if (n == 0) return FD_OK;
+  float* vec = d_vectors;
+  if (!vec) {
+    e.feat_vec.ensure((size_t)n * FD_VECTOR_WIDTH * 4);
+    vec = e.feat_vec.as<float>();
+  }
+  fd::launch_features(e, *txns, n, vec, nullptr);
+  score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
+               d_confidence, d_decision, d_risk);
+  FD_API_END
+}
+
 int fd_blend_device(fd_engine* eng, const fd_blend_params* params, int64_t n, const double* const* d_probs,
                     const uint8_t* present, double* d_fraud_prob, double* d_confidence, uint8_t* d_decision,
                     uint8_t* d_risk) {

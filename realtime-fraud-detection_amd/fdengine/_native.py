@@ -139,6 +139,8 @@ SIGNATURES = {
     "fd_load_merchants_host": (C.c_int, [_vp, C.POINTER(fd_merchants)]),
     "fd_features_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _vp, _vp]),
     "fd_features_host": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _vp, _vp]),
+    "fd_score_batch_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, C.POINTER(_vp), _vp,
+                                        C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
     "fd_timing_read": (C.c_int, [_vp, _dp, C.POINTER(_i64)]),

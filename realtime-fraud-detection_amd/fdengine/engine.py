@@ -160,6 +160,25 @@ class FraudEngine:
         N.call("fd_features_device", self._h, C.byref(b), int(n), C.c_void_p(vec_ptr),
                C.c_void_p(raw_ptr) if raw_ptr else None)
 
+    def score_batch_device(self, params: N.fd_blend_params, slots: Sequence[int], txn_ptrs: dict, n: int,
+                           fp_ptr: int, conf_ptr: int = 0, dec_ptr: int = 0, risk_ptr: int = 0,
+                           vec_ptr: int = 0, model_probs_ptr: int = 0,
+                           ext_ptrs: Optional[Sequence[Optional[int]]] = None,
+                           present: Optional[Sequence[int]] = None) -> None:
+        """Whole hot path for one device-resident micro-batch: features (card state updated) ->
+        every forest model -> blend. All pointers are device pointers."""
+        M = params.n_models
+        sl = np.array(list(slots) + [-1] * (N.FD_MAX_MODELS - len(slots)), np.int32)
+        pres = np.array([1] * M if present is None else list(present), np.uint8)
+        ext = (C.c_void_p * N.FD_MAX_MODELS)()
+        if ext_ptrs:
+            for i, p in enumerate(ext_ptrs):
+                ext[i] = p if p else None
+        b = N.fd_txn_batch(*[int(txn_ptrs[f]) for f in N.TXN_FIELDS])
+        opt = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        N.call("fd_score_batch_device", self._h, C.byref(params), _ptr(sl), ext, _ptr(pres), C.byref(b), int(n),
+               opt(vec_ptr), opt(model_probs_ptr), C.c_void_p(fp_ptr), opt(conf_ptr), opt(dec_ptr), opt(risk_ptr))
+
     # ------------------------------------------------------------------ blend
     @staticmethod
     def blend_params(weights: Sequence[float], conf_mult: Sequence[float], strategy: int = 0,

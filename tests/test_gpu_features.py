@@ -30,6 +30,13 @@ def _slice(tx, a, b):
     return {k: v[a:b] for k, v in tx.items()}
 
 
+def _check_raw(raw, rraw):
+    """Exact except column 1 (Java Math.log(amount + 1)): device log vs libm, <= 1 f64 ulp."""
+    cols = [c for c in range(raw.shape[1]) if c != 1]
+    np.testing.assert_array_equal(raw[:, cols], rraw[:, cols])
+    np.testing.assert_array_max_ulp(raw[:, 1], rraw[:, 1], maxulp=1)
+
+
 def _check_vectors(vec, rvec):
     same = vec == rvec
     if not same.all():
@@ -48,7 +55,7 @@ def test_features_match_oracle_across_batches(engine, mode, n_users, rate):
         part = _slice(tx, a, b)
         vec, raw = engine.features(part, want_raw=True)
         rraw, rvec = orc.run(part)
-        np.testing.assert_array_equal(raw, rraw)
+        _check_raw(raw, rraw)
         _check_vectors(vec, rvec)
     info = engine.state_info()
     assert info["cards"] >= n_users
@@ -67,7 +74,7 @@ def test_small_stream_against_python_chain(engine):
     tx = synth.txn_stream(pop, 600, seed=10, rate_per_s=0.2)
     vec, raw = engine.features(tx, want_raw=True)
     rraw = py.run(tx)
-    np.testing.assert_array_equal(raw, rraw)
+    _check_raw(raw, rraw)
     _check_vectors(vec, VR.vectors(rraw).astype(np.float32))
 
 
@@ -78,3 +85,57 @@ def test_table_full_is_reported(engine):
     with pytest.raises(Exception) as ei:
         engine.features(tx)
     assert "card table full" in str(ei.value)
+
+
+def test_fused_pipeline_matches_oracle_chain(engine):
+    """fd_score_batch_device (features -> XGBoost + IsolationForest -> blend) == oracle chain."""
+    import torch
+    import oracle
+    from oracle import scoring_ref as S
+    from fdengine import iforest_from_sklearn, xgboost_from_json_doc
+    from fdengine._native import DECISIONS, RISK_LEVELS, TXN_FIELDS
+    pop, orc = _pair(engine, 0, 5000)
+    tx = synth.txn_stream(pop, 20000, seed=4, rate_per_s=5.0)
+    # models on realistic vectors (a warm-up slice through the oracle state)
+    orc_ref = OracleFeatureState(1 << 15, 0, 1)
+    orc_ref.load_users(pop["users"]["key"], pop["users"]["avg_amount"], pop["users"]["account_age_days"],
+                       pop["users"]["device_fp"])
+    orc_ref.load_merchants(pop["merchants"]["fraud_rate"], pop["merchants"]["risk_multiplier"])
+    _, Xref = orc_ref.run(tx)
+    xgb = xgboost_from_json_doc(synth.xgboost_doc(150, 8, 64, Xref[:4096], seed=6, p_leaf=0.1))
+    ifm = iforest_from_sklearn(synth.isolation_forest(Xref[:4096].astype(np.float64)))
+    engine.load_forest(0, xgb)
+    engine.load_forest(1, ifm)
+    names = ["xgboost_primary", "isolation_forest"]
+    w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
+    params = FraudEngine.blend_params([w[n] for n in names], [S.CONF_MULT[n] for n in names])
+    engine.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        for a, b in [(0, 7000), (7000, 20000)]:
+            part = _slice(tx, a, b)
+            n = b - a
+            dev = {f: torch.from_numpy(np.ascontiguousarray(part[f])).cuda() for f in TXN_FIELDS}
+            vec = torch.empty((n, 64), dtype=torch.float32, device="cuda")
+            mp = torch.empty((2, n), dtype=torch.float64, device="cuda")
+            fp = torch.empty(n, dtype=torch.float64, device="cuda")
+            conf = torch.empty(n, dtype=torch.float64, device="cuda")
+            dec = torch.empty(n, dtype=torch.uint8, device="cuda")
+            risk = torch.empty(n, dtype=torch.uint8, device="cuda")
+            engine.score_batch_device(params, [0, 1], {f: t.data_ptr() for f, t in dev.items()}, n, fp.data_ptr(),
+                                      conf.data_ptr(), dec.data_ptr(), risk.data_ptr(), vec_ptr=vec.data_ptr(),
+                                      model_probs_ptr=mp.data_ptr())
+            torch.cuda.synchronize()
+            _, rvec = orc.run(part)
+            V = vec.cpu().numpy()
+            _check_vectors(V, rvec)
+            px, _, _ = oracle.xgb_predict(xgb, V)
+            pi, _, _ = oracle.iforest_predict(ifm, V)
+            M = mp.cpu().numpy()
+            assert np.abs(M[0] - px).max() <= 1e-5 and np.abs(M[1] - pi).max() <= 1e-5
+            FP, CF, DC, RK = fp.cpu().numpy(), conf.cpu().numpy(), dec.cpu().numpy(), risk.cpu().numpy()
+            for i in range(0, n, 7):
+                rfp, rcf, rdc, rrk = S.blend_row(names, [float(M[0, i]), float(M[1, i])], w)
+                assert FP[i] == rfp and CF[i] == rcf
+                assert DECISIONS[DC[i]] == rdc and RISK_LEVELS[RK[i]] == rrk
+    finally:
+        engine.set_stream(None)
