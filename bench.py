@@ -1,19 +1,24 @@
 #!/usr/bin/env python3
 """bench.py — scored transactions/sec on the hot path (BASELINE.json metric).
 
-Workload at N=1 (BASELINE.json configs[1], "config 2"): XGBoost binary:logistic, 500 trees x
-depth 8, 50 features, 64k-transaction micro-batches on one MI355X. One *step* = one pass of the
-hot path (fd_forest_predict_device) over one micro-batch whose features are already resident in
-HBM; output = P(fraud) per transaction in HBM.
+Default workload (N=1 headline, BASELINE.json configs[1], "config 2"): XGBoost binary:logistic,
+500 trees x depth 8, 50 features, 64k-transaction micro-batches on one MI355X. One *step* = one
+pass of the hot path (fd_forest_predict_device) over one micro-batch whose features are already
+resident in HBM; output = P(fraud) per transaction in HBM.
+
+`--workload config3` (BASELINE configs[2]): the full pipeline per step on one GPU — card-state
+features (10M cards resident in HBM, sliding windows) -> XGBoost 500x8 + IsolationForest 100 ->
+ensemble blend/decision (fd_score_batch_device), 64k transactions per micro-batch, the stream's
+transactions resident in HBM.
 
 Multi-GPU (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`): one process per
-GPU, each scoring its own micro-batches with a replica of the model — config 2 has no keyed state,
-so there is no data-path collective ("scaling": "weak"); RCCL is used only for the barrier and the
-max-over-ranks timing reduction.
+GPU, each scoring its own micro-batches — config 2 has no keyed state, so there is no data-path
+collective ("scaling": "weak"); RCCL carries only the barrier and the max-over-ranks time.
 
-Also reported: p50/p99 micro-batch latency (host submit -> scores on host), the dominant kernel's
-roofline (algorithmic bytes / HIP-event-timed kernel duration vs 8 TB/s HBM), node-steps/s, and the
-CPU oracle (C restatement, OpenMP) timed on this host on a bounded sample (rank 0, N=1 only).
+Also reported: p50/p99 micro-batch latency (host submit -> scores in host memory), the dominant
+kernel's roofline (algorithmic bytes / HIP-event-timed kernel duration vs 8 TB/s HBM), per-kernel
+times, and the CPU oracle (C restatement, OpenMP) timed on this host on a bounded sample (rank 0,
+N=1 only).
 """
 import argparse
 import json
@@ -34,16 +39,301 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_threads():
+    t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    return max(1, min(t, os.cpu_count() or 1))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def forest_blob_bytes(forest) -> int:
+    from fdengine import pack_forest_host
+    _, _, info = pack_forest_host(forest)
+    return int(info.blob_bytes)
+
+
+def pmc_traffic(workload, B):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    p = REPO / "profiles" / f"pmc_{workload}.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get("hbm_bytes_per_launch") if int(d.get("batch", -1)) == B else None
+    except Exception:
+        return None
+
+
+# --------------------------------------------------------------------------------------- config 2
+class Config2:
+    name = "config2"
+    dtype = "f32"
+
+    def __init__(self, args, rank, dev, eng):
+        import numpy as np
+        import torch
+        import fdengine
+        from fdengine import synth
+        self.np, self.torch = np, torch
+        self.B, self.F, self.T, self.D = args.batch, args.features, args.trees, args.depth
+        X_ref = synth.feature_matrix(2048, self.F, seed=7)
+        doc = synth.xgboost_doc(self.T, self.D, self.F, X_ref, seed=8)
+        with tempfile.TemporaryDirectory() as td:  # exercise the unchanged-file load path
+            path = os.path.join(td, "fraud_classifier.json")
+            synth.write_xgboost_json(path, doc)
+            self.forest = fdengine.load_xgboost_json(path)
+        self.eng = eng
+        eng.load_forest(0, self.forest)
+        self.info = eng.forest_info(0)
+        self.pool = max(1, args.pool)
+        self.Xpool = synth.feature_matrix(self.pool * self.B, self.F, seed=1000 + rank)
+        self.X_dev = torch.from_numpy(self.Xpool).to(dev)
+        self.prob = torch.empty(self.pool * self.B, dtype=torch.float64, device=dev)
+        self.host_out = torch.empty(self.B, dtype=torch.float64, pin_memory=True)
+
+    def step(self, i):
+        s = i % self.pool
+        self.eng.predict_device(0, self.X_dev.data_ptr() + s * self.B * self.F * 4, self.B, self.F,
+                                self.prob.data_ptr() + s * self.B * 8)
+
+    def fetch(self, i):
+        s = i % self.pool
+        self.host_out.copy_(self.prob[s * self.B:(s + 1) * self.B], non_blocking=True)
+
+    def parity(self):
+        import oracle
+        self.step(0)
+        self.torch.cuda.synchronize()
+        rp, _, _ = oracle.xgb_predict(self.forest, self.Xpool[:512], nthreads=cpu_threads())
+        return float(self.np.abs(self.prob[:512].cpu().numpy() - rp).max())
+
+    def roofline(self, timing):
+        from fdengine import _native as N
+        ms, launches = timing[N.FD_TIMING_XGB]
+        avg = (ms / 1e3) / max(1, launches)
+        model_bytes = forest_blob_bytes(self.forest)
+        per_launch = self.B * (self.F * 4 + 8) + model_bytes
+        achieved = per_launch / avg / 1e9
+        return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(self.name, self.B),
+                "kernel": f"forest_kernel_v2<D={self.info['depth']},f32,XGB>", "kernel_avg_us": round(avg * 1e6, 3),
+                "algorithmic_bytes_per_launch": per_launch, "bytes_per_txn": self.F * 4 + 8,
+                "model_bytes_per_launch": model_bytes,
+                "node_steps_per_s": round(self.B * self.T * self.info["depth"] / avg, 1)}
+
+    def kernels(self, timing):
+        return {}
+
+    def config(self, world):
+        return {"workload": "config2: XGBoost binary:logistic 500 trees depth 8, 50 features, "
+                            "64k-txn micro-batches, features resident in HBM",
+                "trees": self.T, "depth": self.D, "features": self.F, "batch": self.B,
+                "parallelism": f"replicas x{world} (one process per GPU, no data-path collective)"}
+
+    def cpu_baseline(self, seconds):
+        import oracle
+        th = cpu_threads()
+        n0 = min(len(self.Xpool), 256 * th)
+        a = time.perf_counter()
+        oracle.xgb_predict(self.forest, self.Xpool[:n0], nthreads=th)
+        dt = time.perf_counter() - a
+        reps = max(1, int(seconds / max(dt, 1e-6) * n0 / len(self.Xpool)))
+        n = min(len(self.Xpool), max(n0, int(n0 * seconds / max(dt, 1e-6))))
+        a = time.perf_counter()
+        done = 0
+        while True:
+            oracle.xgb_predict(self.forest, self.Xpool[:n], nthreads=th)
+            done += n
+            if time.perf_counter() - a >= seconds or done >= reps * len(self.Xpool):
+                break
+        dt = time.perf_counter() - a
+        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
+                "sample": f"{done} txns of the config-2 workload (500 trees x depth 8, 50 features) through "
+                          f"oracle/oracle_forest.c orc_xgb_predict, {th} OpenMP threads, {dt:.2f} s, "
+                          f"CPU: {cpu_model()}"}
+
+
+# --------------------------------------------------------------------------------------- config 3
+class Config3:
+    name = "config3"
+    dtype = "f32 (features f64, forests f32/f64, blend f64)"
+
+    def __init__(self, args, rank, dev, eng):
+        import numpy as np
+        import torch
+        import fdengine
+        from fdengine import _native as N
+        from fdengine import synth
+        from oracle.features_c import OracleFeatureState
+        from oracle import scoring_ref as S
+        self.np, self.torch, self.N, self.S = np, torch, N, S
+        self.B, self.T, self.D = args.batch, args.trees, args.depth
+        self.cards, self.mode, self.K = args.cards, (1 if args.window == "sliding" else 0), args.ring_k
+        self.eng = eng
+        t = time.time()
+        # models on realistic scoring vectors: a small population through the CPU feature oracle
+        spop = synth.population(20000, 500, seed=11)
+        stx = synth.txn_stream(spop, 40000, seed=12, rate_per_s=20.0)
+        so = OracleFeatureState(1 << 16, self.mode, self.K)
+        so.load_users(spop["users"]["key"], spop["users"]["avg_amount"], spop["users"]["account_age_days"],
+                      spop["users"]["device_fp"])
+        so.load_merchants(spop["merchants"]["fraud_rate"], spop["merchants"]["risk_multiplier"])
+        _, Xref = so.run(stx, want_raw=False)
+        self.xgb = fdengine.xgboost_from_json_doc(synth.xgboost_doc(self.T, self.D, 64, Xref[-8192:], seed=13))
+        self.ifm = fdengine.iforest_from_sklearn(synth.isolation_forest(Xref[-8192:].astype(np.float64)))
+        eng.load_forest(0, self.xgb)
+        eng.load_forest(1, self.ifm)
+        self.names = ["xgboost_primary", "isolation_forest"]
+        w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
+        self.weights = [w[n] for n in self.names]
+        self.mults = [S.CONF_MULT[n] for n in self.names]
+        self.params = fdengine.FraudEngine.blend_params(self.weights, self.mults)
+        # population: cards resident in HBM
+        self.pop = synth.population(self.cards, 5000, seed=100 + rank)
+        cap = 1
+        while cap < int(self.cards * 1.6):
+            cap *= 2
+        self.cap = cap
+        eng.state_init(cap, self.mode, self.K)
+        U, M = self.pop["users"], self.pop["merchants"]
+        eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        self.n_batches = args.warmup + args.steps + args.latency_iters + 1
+        self.tx = synth.txn_stream(self.pop, self.n_batches * self.B, seed=200 + rank)
+        self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
+        self.elem = {f: self.tx[f].dtype.itemsize for f in N.TXN_FIELDS}
+        B = self.B
+        self.fp = torch.empty(B, dtype=torch.float64, device=dev)
+        self.conf = torch.empty(B, dtype=torch.float64, device=dev)
+        self.dec = torch.empty(B, dtype=torch.uint8, device=dev)
+        self.risk = torch.empty(B, dtype=torch.uint8, device=dev)
+        self.mp = torch.empty((2, B), dtype=torch.float64, device=dev)
+        self.vec = torch.empty((B, 64), dtype=torch.float32, device=dev)
+        self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
+        self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
+        self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
+        self.next_batch = 0
+        log(f"[rank {rank}] config3 setup {time.time() - t:.1f}s: {self.cards} cards, capacity {cap}, "
+            f"{self.n_batches} batches resident, window={'sliding' if self.mode else 'redis_compat'}")
+
+    def _ptrs(self, b):
+        return {f: t.data_ptr() + b * self.B * self.elem[f] for f, t in self.dev.items()}
+
+    def step(self, i):
+        b = self.next_batch
+        self.next_batch += 1
+        if self.next_batch >= self.n_batches:
+            raise RuntimeError("stream exhausted: raise n_batches")
+        self.eng.score_batch_device(self.params, [0, 1], self._ptrs(b), self.B, self.fp.data_ptr(),
+                                    self.conf.data_ptr(), self.dec.data_ptr(), self.risk.data_ptr(),
+                                    vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
+
+    def fetch(self, i):
+        self.h_fp.copy_(self.fp, non_blocking=True)
+        self.h_dec.copy_(self.dec, non_blocking=True)
+        self.h_risk.copy_(self.risk, non_blocking=True)
+
+    def parity(self):
+        """Batch 0 through the oracle chain (fresh oracle state == fresh engine state)."""
+        import oracle
+        from oracle.features_c import OracleFeatureState
+        np = self.np
+        U, M = self.pop["users"], self.pop["merchants"]
+        o = OracleFeatureState(self.cap, self.mode, self.K)
+        o.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        o.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        part = {f: self.tx[f][:self.B] for f in self.N.TXN_FIELDS}
+        self.step(0)
+        self.torch.cuda.synchronize()
+        _, rvec = o.run(part, want_raw=False)
+        del o
+        V = self.vec.cpu().numpy()
+        px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
+        pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
+        fp, _, dec, _ = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults)
+        vec_diff = int((V != rvec).sum())
+        return {"vector_mismatched_elements": vec_diff,
+                "max_abs_prob_diff": float(np.abs(self.fp.cpu().numpy() - fp).max()),
+                "decision_mismatches": int((self.dec.cpu().numpy() != dec).sum())}
+
+    def roofline(self, timing):
+        N = self.N
+        ms, launches = timing[N.FD_TIMING_XGB]
+        avg = (ms / 1e3) / max(1, launches)
+        model_bytes = forest_blob_bytes(self.xgb)
+        per_launch = self.B * (64 * 4 + 8) + model_bytes
+        achieved = per_launch / avg / 1e9
+        return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(self.name, self.B),
+                "kernel": "forest_kernel_v2<D=8,f32,XGB> (dominant)", "kernel_avg_us": round(avg * 1e6, 3),
+                "algorithmic_bytes_per_launch": per_launch, "bytes_per_txn": 64 * 4 + 8,
+                "model_bytes_per_launch": model_bytes}
+
+    def kernels(self, timing):
+        N = self.N
+        names = {N.FD_TIMING_XGB: "xgboost_forest", N.FD_TIMING_IFOREST: "iforest_forest",
+                 N.FD_TIMING_FEATURES: "features (assign+process)", N.FD_TIMING_BLEND: "blend"}
+        return {names[k]: round(ms / max(1, c) * 1e3, 3) for k, (ms, c) in timing.items() if c}
+
+    def config(self, world):
+        return {"workload": "config3: card-state features (sliding 5m/1h/24h windows, HBM-resident) -> "
+                            "XGBoost 500x8 + IsolationForest 100 -> blend/decision, 64k-txn micro-batches",
+                "cards": self.cards, "window_mode": "sliding" if self.mode else "redis_compat", "ring_k": self.K,
+                "trees": self.T, "depth": self.D, "features": 64, "batch": self.B,
+                "parallelism": f"replicas x{world}"}
+
+    def cpu_baseline(self, seconds):
+        """Oracle chain on the first transactions of the same stream: features (sequential by
+        definition), both forests and the blend (OpenMP)."""
+        import oracle
+        from oracle.features_c import OracleFeatureState
+        np = self.np
+        th = cpu_threads()
+        U, M = self.pop["users"], self.pop["merchants"]
+        o = OracleFeatureState(self.cap, self.mode, self.K)
+        o.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        o.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        chunk = 16384
+        done, a = 0, time.perf_counter()
+        while time.perf_counter() - a < seconds and done + chunk <= len(self.tx["ts_ms"]):
+            part = {f: self.tx[f][done:done + chunk] for f in self.N.TXN_FIELDS}
+            _, V = o.run(part, want_raw=False)
+            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=th)
+            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=th)
+            oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults, nthreads=th)
+            done += chunk
+        dt = time.perf_counter() - a
+        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
+                "sample": f"first {done} txns of the config-3 stream through the oracle chain (features C "
+                          f"single-threaded + XGBoost + IsolationForest + blend, {th} OpenMP threads), "
+                          f"{dt:.2f} s, CPU: {cpu_model()}"}
+
+
+WORKLOADS = {"config2": Config2, "config3": Config3}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--trees", type=int, default=500)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--features", type=int, default=50)
-    ap.add_argument("--pool", type=int, default=8, help="distinct HBM-resident micro-batches cycled through")
+    ap.add_argument("--pool", type=int, default=8, help="config2: distinct HBM-resident micro-batches cycled")
+    ap.add_argument("--cards", type=int, default=10_000_000, help="config3: cards resident in HBM")
+    ap.add_argument("--window", choices=["sliding", "redis"], default="sliding")
+    ap.add_argument("--ring-k", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=200)
@@ -57,7 +347,6 @@ def main():
     import torch
 
     import fdengine
-    from fdengine import synth
 
     dist = None
     if world > 1:
@@ -67,45 +356,21 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-
-    B, F, T, D = args.batch, args.features, args.trees, args.depth
-    t_setup = time.time()
-    X_ref = synth.feature_matrix(2048, F, seed=7)
-    doc = synth.xgboost_doc(T, D, F, X_ref, seed=8)
-    with tempfile.TemporaryDirectory() as td:  # exercise the unchanged-file load path
-        path = os.path.join(td, "fraud_classifier.json")
-        synth.write_xgboost_json(path, doc)
-        forest = fdengine.load_xgboost_json(path)
     eng = fdengine.FraudEngine(dev.index)
-    eng.load_forest(0, forest)
-    info = eng.forest_info(0)
-    pool = max(1, args.pool)
-    Xpool = synth.feature_matrix(pool * B, F, seed=1000 + rank)
-    X_dev = torch.from_numpy(Xpool).to(dev)
-    prob_dev = torch.empty(pool * B, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
-    log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s; forest depth={info['depth']} trees={info['n_trees']}")
+    wl = WORKLOADS[args.workload](args, rank, dev, eng)
 
-    xp, pp = X_dev.data_ptr(), prob_dev.data_ptr()
-
-    def step(i):
-        s = i % pool
-        eng.predict_device(0, xp + s * B * F * 4, B, F, pp + s * B * 8)
-
-    # parity spot-check of this run's outputs against the CPU oracle (first 512 rows of slot 0)
-    step(0)
-    torch.cuda.synchronize()
     parity = None
     try:
-        import oracle
-        rp, _, _ = oracle.xgb_predict(forest, Xpool[:512], nthreads=0)
-        parity = float(np.abs(prob_dev[:512].cpu().numpy() - rp).max())
+        parity = wl.parity()
     except Exception as e:  # the oracle is only a checker; report, never fall back
         log(f"[rank {rank}] parity spot-check unavailable: {e}")
+    if args.workload == "config3":  # parity consumed batch 0 of the stream with fresh state
+        pass
 
     for i in range(args.warmup):
-        step(i)
+        wl.step(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -116,46 +381,32 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        wl.step(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
     eng.set_timing(False)
-    kern_ms, launches = eng.read_timing()
+    timing = eng.read_timing()
     elapsed = t1 - t0
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # latency: host submit -> P(fraud) for the whole micro-batch back in host memory
-    host_out = torch.empty(B, dtype=torch.float64, pin_memory=True)
     lat = []
     for i in range(args.latency_iters):
-        s = i % pool
         a = time.perf_counter()
-        step(i)
-        host_out.copy_(prob_dev[s * B:(s + 1) * B], non_blocking=True)
+        wl.step(i)
+        wl.fetch(i)
         stream.synchronize()
         lat.append(time.perf_counter() - a)
-    lat_ms = np.array(lat) * 1e3
+    lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
 
-    value = world * args.steps * B / elapsed
-    avg_kernel_s = (kern_ms / 1e3) / max(1, launches)
-    model_bytes = forest_bytes(eng, forest)
-    bytes_per_launch = B * (F * 4 + 8) + model_bytes
-    achieved = bytes_per_launch / avg_kernel_s / 1e9
-    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(B),
-                "kernel": "forest_kernel<D=8,CH=8,f32,XGB>", "kernel_avg_us": round(avg_kernel_s * 1e6, 3),
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "bytes_per_txn": F * 4 + 8, "model_bytes_per_launch": model_bytes,
-                "node_steps_per_s": round(B * T * info["depth"] / avg_kernel_s, 1)}
-
+    value = world * args.steps * args.batch / elapsed
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(forest, Xpool, args.cpu_seconds)
+        cpu = wl.cpu_baseline(args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -169,70 +420,21 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (seeded scoring-vector-shaped features; random-init XGBoost 2.0.3-schema model)",
-            "config": {"workload": "config2: XGBoost binary:logistic 500 trees depth 8, 50 features, "
-                                   "64k-txn micro-batches, features resident in HBM",
-                       "trees": T, "depth": D, "features": F, "batch": B,
-                       "parallelism": f"replicas x{world} (one process per GPU, no data-path collective)"},
+            "dtype": wl.dtype,
+            "data": "synthetic (seeded simulator-distribution stream / scoring vectors; random-init models in the "
+                    "reference's file formats)",
+            "config": wl.config(world),
             "p50_batch_latency_ms": round(float(np.percentile(lat_ms, 50)), 4),
             "p99_batch_latency_ms": round(float(np.percentile(lat_ms, 99)), 4),
-            "roofline": roofline,
+            "roofline": wl.roofline(timing),
+            "kernel_avg_us": wl.kernels(timing),
             "cpu_baseline": cpu,
-            "parity_max_abs_prob_diff_vs_oracle": parity,
+            "parity_vs_oracle": parity,
         }
         print(json.dumps(line), flush=True)
     eng.close()
     if dist:
         dist.destroy_process_group()
-
-
-def forest_bytes(eng, forest) -> int:
-    from fdengine import pack_forest_host
-    _, _, info = pack_forest_host(forest)
-    return int(info.blob_bytes)
-
-
-def pmc_traffic(B):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
-    p = REPO / "profiles" / "pmc_config2.json"
-    if not p.exists():
-        return None
-    try:
-        d = json.loads(p.read_text())
-        if int(d.get("batch", -1)) != B:
-            return None
-        return d.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-
-
-def cpu_baseline(forest, Xpool, seconds):
-    import numpy as np
-    import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    # calibrate, then run a sample sized to ~`seconds` of CPU work
-    n0 = min(len(Xpool), 256 * threads)
-    a = time.perf_counter()
-    oracle.xgb_predict(forest, Xpool[:n0], nthreads=threads)
-    dt = time.perf_counter() - a
-    n = int(min(len(Xpool), max(n0, n0 * seconds / max(dt, 1e-6))))
-    a = time.perf_counter()
-    oracle.xgb_predict(forest, Xpool[:n], nthreads=threads)
-    dt = time.perf_counter() - a
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": round(n / dt, 1), "unit": "txn/s", "cores": threads, "kind": "port",
-            "sample": f"{n} txns of the config-2 workload (500 trees x depth 8, 50 features) through "
-                      f"oracle/oracle_forest.c orc_xgb_predict, {threads} OpenMP threads, {dt:.2f} s, "
-                      f"CPU: {cpu_model}"}
 
 
 if __name__ == "__main__":

@@ -227,13 +227,16 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
 
 /* ---------------------------------------------------------------- diagnostics */
 /* Per-launch device timing of the engine's hot kernels, measured with HIP events recorded on the
-   launch stream around each kernel. fd_timing_read synchronises, returns the summed kernel time (ms)
-   and the number of timed launches since the last read, and resets the counters. */
+   launch stream around each kernel. fd_timing_read synchronises and returns the summed time (ms) and
+   count of the timed launches of `kind` (FD_TIMING_ALL: every kind) since the last fd_timing_reset. */
+enum fd_timing_kind { FD_TIMING_ALL = -1, FD_TIMING_XGB = 0, FD_TIMING_IFOREST = 1, FD_TIMING_FEATURES = 2,
+                      FD_TIMING_BLEND = 3 };
 int fd_engine_set_timing(fd_engine* eng, int enable);
 /* Engine tuning knobs (for A/B measurement; defaults are the tuned choices):
      "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel */
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
-int fd_timing_read(fd_engine* eng, double* total_ms, int64_t* launches);
+int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches);
+int fd_timing_reset(fd_engine* eng);
 
 #ifdef __cplusplus
 }

@@ -45,6 +45,8 @@ def lib() -> C.CDLL:
         L.orc_xgb_predict.argtypes = [i64, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, d, i32, vp, vp, vp]
         L.orc_iforest_predict.restype = C.c_int
         L.orc_iforest_predict.argtypes = [i64, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, d, d, i32, vp, vp, vp]
+        L.orc_blend_weighted.restype = C.c_int
+        L.orc_blend_weighted.argtypes = [i64, i32, vp, vp, vp, d, i32, vp, vp, vp, vp]
         L.orc_xgb_base_margin.restype = C.c_float
         L.orc_xgb_base_margin.argtypes = [d]
         _register_features(L)
@@ -97,3 +99,16 @@ def iforest_predict(fa, X: np.ndarray, nthreads: int = 0, want_leaf: bool = Fals
                               _ptr(a["feat"]), _ptr(a["thr"]), _ptr(a["dl"]), _ptr(a["lv"]), float(fa.if_offset),
                               float(fa.if_denominator), nthreads, _ptr(depth), _ptr(prob), _ptr(leaf))
     return prob, depth, leaf
+
+
+def blend_weighted(probs: np.ndarray, weights, mults, confidence_threshold=0.7, nthreads: int = 0):
+    """CPU-baseline blend (weighted average), probs [M, n] -> (fp, conf, decision, risk)."""
+    P = np.ascontiguousarray(probs, np.float64)
+    M, n = P.shape
+    w = np.ascontiguousarray(weights, np.float64)
+    m = np.ascontiguousarray(mults, np.float64)
+    fp, conf = np.empty(n), np.empty(n)
+    dec, risk = np.empty(n, np.uint8), np.empty(n, np.uint8)
+    lib().orc_blend_weighted(n, M, _ptr(P), _ptr(w), _ptr(m), float(confidence_threshold), nthreads, _ptr(fp),
+                             _ptr(conf), _ptr(dec), _ptr(risk))
+    return fp, conf, dec, risk

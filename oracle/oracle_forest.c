@@ -113,3 +113,35 @@ int orc_iforest_predict(int64_t n, int32_t ld, const float* X, int32_t n_trees, 
   }
   return 0;
 }
+
+/* Ensemble blend, weighted-average strategy (ensemble_predictor.py:263-284 with the clamp :203 and
+   confidence :325-342), f64 in the reference's order. Used only by bench.py's full-pipeline CPU
+   baseline; the exact restatement tested against the reference is scoring_ref.py. */
+int orc_blend_weighted(int64_t n, int32_t n_models, const double* probs /* n_models x n */,
+                       const double* weight, const double* mult, double confidence_threshold,
+                       int32_t nthreads, double* fp_out, double* conf_out, uint8_t* dec_out,
+                       uint8_t* risk_out) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static) if (nthreads != 1)
+#endif
+  for (int64_t i = 0; i < n; ++i) {
+    double tw = 0.0, ws = 0.0, cs = 0.0;
+    for (int m = 0; m < n_models; ++m) {
+      double p = probs[(int64_t)m * n + i];
+      p = (p < 1.0) ? p : 1.0;
+      p = (p > 0.0) ? p : 0.0;
+      double c = fabs(p - 0.5) * 2.0 * mult[m];
+      c = (c < 1.0) ? c : 1.0;
+      ws += p * weight[m];
+      cs += c * weight[m];
+      tw += weight[m];
+    }
+    const double fp = tw == 0.0 ? 0.5 : ws / tw, conf = tw == 0.0 ? 0.0 : cs / tw;
+    fp_out[i] = fp;
+    conf_out[i] = conf;
+    dec_out[i] = conf < confidence_threshold ? 1 : (fp >= 0.95 ? 2 : (fp >= 0.8 ? 1 : (fp >= 0.6 ? 3 : 0)));
+    risk_out[i] = fp >= 0.95 ? 4 : (fp >= 0.8 ? 3 : (fp >= 0.6 ? 2 : (fp >= 0.3 ? 1 : 0)));
+  }
+  return 0;
+}

@@ -127,9 +127,12 @@ void launch_blend(Engine& e, const fd_blend_params& p, int64_t n, const double* 
   a.fraud_threshold = p.fraud_threshold;
   a.confidence_threshold = p.confidence_threshold;
   const int64_t blocks = (n + 255) / 256;
+  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_BLEND) : nullptr;
+  if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
   hipLaunchKernelGGL(blend_kernel, dim3((unsigned)blocks), dim3(256), 0, e.stream, a, n, d_fp, d_conf,
                      d_dec, d_risk);
   FD_HIP(hipGetLastError());
+  if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
 }
 
 }  // namespace fd

@@ -13,14 +13,16 @@ static thread_local std::string g_last_error;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 
-std::pair<hipEvent_t, hipEvent_t>* Engine::next_event_pair() {
+Engine::Timed* Engine::next_event_pair(int kind) {
   if (events_used == events.size()) {
     hipEvent_t a, b;
     FD_HIP(hipEventCreate(&a));
     FD_HIP(hipEventCreate(&b));
-    events.push_back({a, b});
+    events.push_back({a, b, 0});
   }
-  return &events[events_used++];
+  Timed* t = &events[events_used++];
+  t->kind = kind;
+  return t;
 }
 
 }  // namespace fd
@@ -149,8 +151,8 @@ int fd_engine_destroy(fd_engine* eng) {
                   &e.state.next, &e.state.err})
     b->release();
   for (auto& ev : e.events) {
-    (void)hipEventDestroy(ev.first);
-    (void)hipEventDestroy(ev.second);
+    (void)hipEventDestroy(ev.a);
+    (void)hipEventDestroy(ev.b);
   }
   if (e.own_stream) (void)hipStreamDestroy(e.own_stream);
   delete eng;
@@ -199,18 +201,28 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   FD_API_END
 }
 
-int fd_timing_read(fd_engine* eng, double* total_ms, int64_t* launches) {
+int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches) {
   FD_API_BEGIN
   Engine& e = E(eng);
   double tot = 0.0;
+  int64_t cnt = 0;
   for (size_t i = 0; i < e.events_used; ++i) {
-    FD_HIP(hipEventSynchronize(e.events[i].second));
+    if (kind >= 0 && e.events[i].kind != kind) continue;
+    FD_HIP(hipEventSynchronize(e.events[i].b));
     float ms = 0.f;
-    FD_HIP(hipEventElapsedTime(&ms, e.events[i].first, e.events[i].second));
+    FD_HIP(hipEventElapsedTime(&ms, e.events[i].a, e.events[i].b));
     tot += ms;
+    ++cnt;
   }
   if (total_ms) *total_ms = tot;
-  if (launches) *launches = (int64_t)e.events_used;
+  if (launches) *launches = cnt;
+  FD_API_END
+}
+
+int fd_timing_reset(fd_engine* eng) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  if (e.events_used) FD_HIP(hipEventSynchronize(e.events[e.events_used - 1].b));
   e.events_used = 0;
   FD_API_END
 }

@@ -103,10 +103,14 @@ struct Engine {
   // optional per-launch kernel timing (HIP events on the launch stream)
   int forest_variant = 0;  // "forest_kernel" option
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pool
+  struct Timed {
+    hipEvent_t a, b;
+    int kind;
+  };
+  std::vector<Timed> events;  // pool
   size_t events_used = 0;
   void activate() const { FD_HIP(hipSetDevice(device)); }
-  std::pair<hipEvent_t, hipEvent_t>* next_event_pair();
+  Timed* next_event_pair(int kind);
 };
 
 // forest.hip

@@ -427,8 +427,8 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
   st.next.ensure((size_t)n * 4);
   if (st.merchants.ptr == nullptr) st.merchants.ensure(16);
   st.epoch = (st.epoch == 0xffffffffu) ? 1u : st.epoch + 1u;
-  std::pair<hipEvent_t, hipEvent_t>* ev = e.timing ? e.next_event_pair() : nullptr;
-  if (ev) FD_HIP(hipEventRecord(ev->first, e.stream));
+  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
+  if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
   hipLaunchKernelGGL(feat_assign_kernel, dim3(grid_for(n)), dim3(256), 0, e.stream, st.headers.as<CardHeader>(),
                      (long long)(st.cap - 1), n, reinterpret_cast<const unsigned long long*>(t.card_key), st.epoch,
                      st.slot.as<unsigned>(), st.next.as<int>(), st.err.as<unsigned>());
@@ -441,7 +441,7 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
                      (int)st.n_merchants, st.mode, st.K, n, a, st.slot.as<const unsigned>(), st.next.as<const int>(),
                      d_vec, d_raw);
   FD_HIP(hipGetLastError());
-  if (ev) FD_HIP(hipEventRecord(ev->second, e.stream));
+  if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
 }
 
 void features_check(Engine& e) { check_err(e); }

@@ -586,14 +586,14 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int64_t blocks = (n + kTile - 1) / kTile;
   FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
-  std::pair<hipEvent_t, hipEvent_t>* ev = e.timing ? e.next_event_pair() : nullptr;
-  if (ev) FD_HIP(hipEventRecord(ev->first, e.stream));
+  Engine::Timed* ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
+  if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(threads), lds, e.stream, d_X, n, (int)ld,
                      pf.num_feature, pf.blob.as<const char>(), pf.n_chunks, (int)pf.chunk_stride,
                      pf.leaf_ids.as<const int32_t>(), pf.n_trees, pf.base_margin, pf.if_offset,
                      pf.if_denominator, d_prob, d_raw, d_leaf);
   FD_HIP(hipGetLastError());
-  if (ev) FD_HIP(hipEventRecord(ev->second, e.stream));
+  if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
 }
 
 }  // namespace fd

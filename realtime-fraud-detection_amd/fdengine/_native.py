@@ -100,6 +100,7 @@ class fd_txn_batch(C.Structure):
                 ("hour", C.c_void_p), ("weekend", C.c_void_p)]
 
 
+FD_TIMING_ALL, FD_TIMING_XGB, FD_TIMING_IFOREST, FD_TIMING_FEATURES, FD_TIMING_BLEND = -1, 0, 1, 2, 3
 FD_WINDOW_REDIS_COMPAT = 0
 FD_WINDOW_SLIDING = 1
 FD_RAW_FEATURES = 16
@@ -143,7 +144,8 @@ SIGNATURES = {
                                         C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
-    "fd_timing_read": (C.c_int, [_vp, _dp, C.POINTER(_i64)]),
+    "fd_timing_read": (C.c_int, [_vp, C.c_int, _dp, C.POINTER(_i64)]),
+    "fd_timing_reset": (C.c_int, [_vp]),
     "fd_pack_forest_host": (C.c_int, [C.POINTER(fd_forest_params), C.POINTER(fd_tree_arrays), _vp, _i64, _vp, _i64,
                                       C.POINTER(fd_pack_info)]),
 }

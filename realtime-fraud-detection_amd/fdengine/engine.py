@@ -66,12 +66,20 @@ class FraudEngine:
     def set_option(self, key: str, value: int) -> None:
         N.call("fd_engine_set_option", self._h, key.encode(), int(value))
 
-    def read_timing(self):
-        """-> (total kernel ms, timed launches) since the last read."""
-        ms = C.c_double()
-        cnt = C.c_int64()
-        N.call("fd_timing_read", self._h, C.byref(ms), C.byref(cnt))
-        return ms.value, cnt.value
+    def read_timing(self, kinds=(N.FD_TIMING_XGB, N.FD_TIMING_IFOREST, N.FD_TIMING_FEATURES, N.FD_TIMING_BLEND),
+                    reset: bool = True):
+        """-> {kind: (total kernel ms, timed launches)} since the last reset (then resets).
+        With a single int `kinds`, returns just that (ms, launches) pair."""
+        single = isinstance(kinds, int)
+        out = {}
+        for k in ([kinds] if single else kinds):
+            ms = C.c_double()
+            cnt = C.c_int64()
+            N.call("fd_timing_read", self._h, int(k), C.byref(ms), C.byref(cnt))
+            out[k] = (ms.value, cnt.value)
+        if reset:
+            N.call("fd_timing_reset", self._h)
+        return out[kinds] if single else out
 
     # ------------------------------------------------------------------ forests
     def load_forest(self, slot: int, fa: ForestArrays) -> None:

@@ -37,7 +37,7 @@ for r in range(rounds):
             eng.predict_device(0, dX.data_ptr() + (i % 4) * B * F * 4, B, F, dp.data_ptr() + (i % 4) * B * 8)
         torch.cuda.synchronize()
         eng.set_timing(False)
-        ms, n = eng.read_timing()
+        ms, n = eng.read_timing(0)
         res[v].append(ms / n * 1e3)
         out = dp[:B].cpu().numpy()
         if ref is None:
