@@ -229,9 +229,9 @@ class Config3:
 
     def step(self, i):
         b = self.next_batch
-        self.next_batch += 1
-        if self.next_batch >= self.n_batches:
+        if b >= self.n_batches:
             raise RuntimeError("stream exhausted: raise n_batches")
+        self.next_batch += 1
         self.eng.score_batch_device(self.params, [0, 1], self._ptrs(b), self.B, self.fp.data_ptr(),
                                     self.conf.data_ptr(), self.dec.data_ptr(), self.risk.data_ptr(),
                                     vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
