@@ -71,13 +71,12 @@ def packed_walk(blob: bytes, leaf_ids: np.ndarray, info, kind_xgb: bool, x_row):
     """Walk the engine's packed layout exactly as forest_kernel does (x < thr, meta = f*TILE*4|dl<<31).
     -> (sum of leaf values in tree order (f32 for XGB / f64 for IF) from 0 or base margin, [leaf ids])"""
     D = info.depth
-    NI, NL = (1 << D) - 1, 1 << D
-    leaf_sz = 4 if kind_xgb else 8
+    NL = 1 << D  # 1-based heap: node records at slots 1..NL-1, children 2i / 2i+1, leaves after NL records
     acc = np.float32(info.base_margin) if kind_xgb else 0.0
     leaves = []
     for t in range(info.n_trees):
         base = (t // info.chunk) * info.chunk_stride + (t % info.chunk) * info.tree_bytes
-        idx = 0
+        idx = 1
         for _ in range(D):
             thr_bits, meta = struct.unpack_from("<II", blob, base + idx * 8)
             thr = np.frombuffer(struct.pack("<I", thr_bits), np.float32)[0]
@@ -87,13 +86,13 @@ def packed_walk(blob: bytes, leaf_ids: np.ndarray, info, kind_xgb: bool, x_row):
                 right = 1 - (meta >> 31)
             else:
                 right = 0 if x < thr else 1
-            idx = 2 * idx + 1 + right
-        s = idx - NI
+            idx = 2 * idx + right
+        s = idx - NL
         if kind_xgb:
-            v = struct.unpack_from("<f", blob, base + NI * 8 + s * 4)[0]
+            v = struct.unpack_from("<f", blob, base + NL * 8 + s * 4)[0]
             acc = np.float32(acc + np.float32(v))
         else:
-            v = struct.unpack_from("<d", blob, base + NI * 8 + s * 8)[0]
+            v = struct.unpack_from("<d", blob, base + NL * 8 + s * 8)[0]
             acc = acc + v
         leaves.append(int(leaf_ids[t * NL + s]))
     return float(acc), leaves

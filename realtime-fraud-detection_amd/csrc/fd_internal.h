@@ -17,6 +17,7 @@ constexpr int kMaxSlots = 8;      // forest slots per engine
 constexpr int kTile = 256;        // transactions per workgroup in the forest kernel (one per thread)
 constexpr int kMaxFeatures = 64;  // model columns held in LDS ([feature][kTile] f32 = 64 KiB max)
 constexpr int kMaxDepth = 10;     // deepest tree the repacker accepts
+constexpr size_t kLdsBudget = 160 * 1024;  // LDS per CU (one workgroup per CU at 64k batches)
 
 struct Error : std::runtime_error {
   int code;
@@ -56,11 +57,10 @@ struct DeviceBuffer {
   T* as() const { return static_cast<T*>(ptr); }
 };
 
-// A forest repacked into perfect depth-D trees (see DESIGN.md "Forest layout"):
-//   per tree, 2^D-1 internal node records {f32 thr, u32 meta} in breadth-first order
-//   (children of slot s are 2s+1 / 2s+2), followed by 2^D leaf values (f32 for XGBoost,
-//   f64 for Isolation Forest). Trees are grouped in chunks of `chunk` trees; each chunk
-//   occupies `chunk_stride` bytes (rounded to 1 KiB for the LDS-DMA staging).
+// A forest repacked into perfect depth-D trees stored as 1-based heaps (see forest.hip header and
+// DESIGN.md "Forest layout"): per tree 2^D node records {f32 thr, u32 meta} (slot 0 unused; children
+// of slot s are 2s / 2s+1) then 2^D leaf values (f32 XGBoost, f64 Isolation Forest); chunks of
+// `chunk` trees, each `chunk_stride` bytes (1 KiB multiple, LDS-DMA staging).
 //   meta = feature * kTile * 4 (byte offset of the feature row in the LDS tile) | default_left << 31.
 struct PackedForest {
   bool loaded = false;

@@ -60,7 +60,7 @@ def test_xgb_c_oracle_matches_python_walker_and_packed_layout():
     fa = xgboost_from_json_doc(synth.xgboost_doc(25, 8, 30, X, seed=4, p_leaf=0.2, base_score=0.3))
     _, margin, leaf = oracle.xgb_predict(fa, X, want_leaf=True)
     blob, ids, info = pack_forest_host(fa)
-    assert info.depth == 8 and info.chunk == 8
+    assert info.depth == 8 and info.chunk in (4, 8, 12, 16)
     for r in range(0, 300, 7):
         m, lv = forest_ref.xgb_walk(fa, X[r])
         pm, pl = forest_ref.packed_walk(blob, ids, info, True, X[r])
