@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 1
+#define FD_ABI_VERSION 2
 
 enum fd_status {
   FD_OK = 0,
@@ -120,21 +120,35 @@ int fd_forest_predict_device(fd_engine* eng, int slot, const float* d_X, int64_t
 int fd_forest_predict_host(fd_engine* eng, int slot, const float* X, int64_t n, int32_t ld,
                            double* prob, double* raw, int32_t* leaf);
 
-/* Host-only repack (no device needed): the depth-major layout fd_load_forest uploads, for layout
-   inspection and CPU tests. Call with NULL buffers to query sizes in *info. */
+/* Host-only repack (no device needed): the layouts fd_load_forest uploads, for layout inspection
+   and CPU tests. Call with NULL buffers to query sizes in *info.
+   fd_pack_forest_host: threshold layout — per tree a 1-based heap of 2^D {f32 thr, u32 meta}
+   records (slot 0 unused, children of slot s at 2s / 2s+1) then 2^D leaf values.
+   fd_pack_forest_binned_host: binned layout — every split threshold replaced by its index j in the
+   feature's sorted table of distinct thresholds (x < t_j  <=>  bin(x) <= j, bin(x) = #{t <= x}), so a
+   node is one u32 (j << 16 | feature * 1024 | default_left); 2^D node words then 2^D leaf values.
+   Returns FD_ERR_UNSUPPORTED when a feature has more than 65534 distinct thresholds. */
 typedef struct {
   int32_t n_trees;
   int32_t n_chunks;
   int32_t chunk;        /* trees per LDS staging chunk */
   int32_t depth;        /* D: every tree is padded to a perfect depth-D tree */
-  int64_t tree_bytes;   /* (2^D-1)*8 node bytes + 2^D leaf values (f32 XGB / f64 IF) */
+  int64_t tree_bytes;   /* 2^D node records (8 B threshold layout / 4 B binned) + 2^D leaf values
+                           (f32 XGB / f64 IF) */
   int64_t chunk_stride; /* bytes per chunk, 1 KiB multiple */
   int64_t blob_bytes;
   int64_t n_leaf_ids;
   float base_margin;    /* XGB: f32 margin seeded by base_score */
+  int32_t layout;       /* 0 threshold layout, 1 binned layout */
+  int64_t n_thresholds; /* binned: total distinct thresholds over all features */
+  int32_t bin_steps;    /* binned: largest power of two <= the longest feature table (0 if none) */
 } fd_pack_info;
 int fd_pack_forest_host(const fd_forest_params* params, const fd_tree_arrays* trees, void* blob,
                         int64_t blob_cap, int32_t* leaf_ids, int64_t ids_cap, fd_pack_info* info);
+/* thresholds: n_thresholds f32 (feature-major, ascending per feature); offsets: num_feature + 1. */
+int fd_pack_forest_binned_host(const fd_forest_params* params, const fd_tree_arrays* trees, void* blob,
+                               int64_t blob_cap, float* thresholds, int64_t thr_cap, int32_t* offsets,
+                               fd_pack_info* info);
 
 /* ---------------------------------------------------------------- blend (a11-a13) */
 /* Replaces _calculate_model_confidence + _combine_predictions + _make_decision +
@@ -233,7 +247,8 @@ enum fd_timing_kind { FD_TIMING_ALL = -1, FD_TIMING_XGB = 0, FD_TIMING_IFOREST =
                       FD_TIMING_BLEND = 3 };
 int fd_engine_set_timing(fd_engine* eng, int enable);
 /* Engine tuning knobs (for A/B measurement; defaults are the tuned choices):
-     "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel */
+     "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel
+     on the threshold layout, 3 force the 1024-thread kernel on the binned layout */
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
 int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches);
 int fd_timing_reset(fd_engine* eng);

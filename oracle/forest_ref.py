@@ -96,3 +96,40 @@ def packed_walk(blob: bytes, leaf_ids: np.ndarray, info, kind_xgb: bool, x_row):
             acc = acc + v
         leaves.append(int(leaf_ids[t * NL + s]))
     return float(acc), leaves
+
+
+def bin_of(thr_f32: np.ndarray, v) -> int:
+    """Binned layout: bin(x) = #{t in the feature's sorted distinct thresholds : t <= x}."""
+    return int(np.searchsorted(thr_f32, np.float32(v), side="right"))
+
+
+def packed_walk_binned(blob: bytes, leaf_ids: np.ndarray, thr: np.ndarray, off: np.ndarray, info, kind_xgb: bool,
+                       x_row):
+    """Walk the engine's BINNED layout as forest_kernel4 does: node word = j << 16 | f * 1024 | dl,
+    go right iff bin(x_f) << 16 > node (i.e. bin > j); missing -> default direction."""
+    D = info.depth
+    NL = 1 << D  # 1-based heap: node words at slots 1..NL-1 (4 B), children 2i / 2i+1, then NL leaves
+    acc = np.float32(info.base_margin) if kind_xgb else 0.0
+    leaves = []
+    for t in range(info.n_trees):
+        base = (t // info.chunk) * info.chunk_stride + (t % info.chunk) * info.tree_bytes
+        idx = 1
+        for _ in range(D):
+            (node,) = struct.unpack_from("<I", blob, base + idx * 4)
+            f = (node & 0xFC00) // (TILE * 4)
+            x = np.float32(x_row[f]) if f < len(x_row) else np.float32("nan")
+            if np.isnan(x):
+                right = 1 - (node & 1)
+            else:
+                b = bin_of(thr[off[f]:off[f + 1]], x)
+                right = 1 if (b << 16) > node else 0
+            idx = 2 * idx + right
+        s = idx - NL
+        if kind_xgb:
+            v = struct.unpack_from("<f", blob, base + NL * 4 + s * 4)[0]
+            acc = np.float32(acc + np.float32(v))
+        else:
+            v = struct.unpack_from("<d", blob, base + NL * 4 + s * 8)[0]
+            acc = acc + v
+        leaves.append(int(leaf_ids[t * NL + s]))
+    return float(acc), leaves

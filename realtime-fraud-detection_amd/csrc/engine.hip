@@ -137,6 +137,9 @@ int fd_engine_destroy(fd_engine* eng) {
   for (auto& f : e.forests) {
     f.blob.release();
     f.leaf_ids.release();
+    f.b_blob.release();
+    f.b_thr.release();
+    f.b_thr_off.release();
   }
   e.stage_in.release();
   e.stage_out0.release();
@@ -193,7 +196,7 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   FD_REQUIRE(key, FD_ERR_INVALID_ARG, "null key");
   const std::string k(key);
   if (k == "forest_kernel") {
-    FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "forest_kernel must be 0, 1 or 2");
+    FD_REQUIRE(value >= 0 && value <= 3, FD_ERR_INVALID_ARG, "forest_kernel must be 0, 1, 2 or 3");
     e.forest_variant = (int)value;
   } else {
     throw fd::Error(FD_ERR_INVALID_ARG, "unknown option: " + k);
@@ -252,6 +255,9 @@ int fd_pack_forest_host(const fd_forest_params* params, const fd_tree_arrays* tr
   info->blob_bytes = (int64_t)hp.blob.size();
   info->n_leaf_ids = (int64_t)hp.leaf_ids.size();
   info->base_margin = hp.base_margin;
+  info->layout = 0;
+  info->n_thresholds = (int64_t)hp.b_thr.size();
+  info->bin_steps = hp.bin_steps;
   if (blob) {
     FD_REQUIRE(blob_cap >= (int64_t)hp.blob.size(), FD_ERR_INVALID_ARG, "blob buffer too small");
     std::memcpy(blob, hp.blob.data(), hp.blob.size());
@@ -263,6 +269,38 @@ int fd_pack_forest_host(const fd_forest_params* params, const fd_tree_arrays* tr
   FD_API_END
 }
 
+int fd_pack_forest_binned_host(const fd_forest_params* params, const fd_tree_arrays* trees, void* blob,
+                               int64_t blob_cap, float* thresholds, int64_t thr_cap, int32_t* offsets,
+                               fd_pack_info* info) {
+  FD_API_BEGIN
+  FD_REQUIRE(params && trees && info, FD_ERR_INVALID_ARG, "null params/trees/info");
+  const fd::HostPack hp = fd::pack_forest_host(*params, *trees);
+  FD_REQUIRE(hp.binned, FD_ERR_UNSUPPORTED,
+             "forest has no binned layout (depth > 8 or > 65534 distinct thresholds in a feature)");
+  info->n_trees = hp.n_trees;
+  info->n_chunks = hp.b_n_chunks;
+  info->chunk = hp.b_chunk;
+  info->depth = hp.depth;
+  info->tree_bytes = (int64_t)hp.b_tree_bytes;
+  info->chunk_stride = (int64_t)hp.b_chunk_stride;
+  info->blob_bytes = (int64_t)hp.b_blob.size();
+  info->n_leaf_ids = (int64_t)hp.leaf_ids.size();
+  info->base_margin = hp.base_margin;
+  info->layout = 1;
+  info->n_thresholds = (int64_t)hp.b_thr.size();
+  info->bin_steps = hp.bin_steps;
+  if (blob) {
+    FD_REQUIRE(blob_cap >= (int64_t)hp.b_blob.size(), FD_ERR_INVALID_ARG, "blob buffer too small");
+    std::memcpy(blob, hp.b_blob.data(), hp.b_blob.size());
+  }
+  if (thresholds) {
+    FD_REQUIRE(thr_cap >= (int64_t)hp.b_thr.size(), FD_ERR_INVALID_ARG, "threshold buffer too small");
+    std::memcpy(thresholds, hp.b_thr.data(), hp.b_thr.size() * sizeof(float));
+  }
+  if (offsets) std::memcpy(offsets, hp.b_thr_off.data(), hp.b_thr_off.size() * sizeof(int32_t));
+  FD_API_END
+}
+
 int fd_unload_forest(fd_engine* eng, int slot) {
   FD_API_BEGIN
   Engine& e = E(eng);
@@ -270,6 +308,10 @@ int fd_unload_forest(fd_engine* eng, int slot) {
   FD_HIP(hipStreamSynchronize(e.stream));
   pf.blob.release();
   pf.leaf_ids.release();
+  pf.b_blob.release();
+  pf.b_thr.release();
+  pf.b_thr_off.release();
+  pf.binned = false;
   pf.loaded = false;
   FD_API_END
 }

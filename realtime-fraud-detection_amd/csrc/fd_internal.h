@@ -18,6 +18,7 @@ constexpr int kTile = 256;        // transactions per workgroup in the forest ke
 constexpr int kMaxFeatures = 64;  // model columns held in LDS ([feature][kTile] f32 = 64 KiB max)
 constexpr int kMaxDepth = 10;     // deepest tree the repacker accepts
 constexpr size_t kLdsBudget = 160 * 1024;  // LDS per CU (one workgroup per CU at 64k batches)
+constexpr int kMaxBins = 65534;   // distinct thresholds per feature in the binned layout
 
 struct Error : std::runtime_error {
   int code;
@@ -77,6 +78,13 @@ struct PackedForest {
   double if_denominator = 0.0;
   DeviceBuffer blob;      // n_chunks * chunk_stride
   DeviceBuffer leaf_ids;  // n_trees_padded * 2^D original node ids (parity output)
+  // binned layout (forest_kernel4), present when every feature has <= 65534 distinct thresholds
+  bool binned = false;
+  int b_chunk = 0, b_n_chunks = 0, bin_steps = 0;
+  size_t b_tree_bytes = 0, b_chunk_stride = 0;
+  DeviceBuffer b_blob;     // b_n_chunks * b_chunk_stride
+  DeviceBuffer b_thr;      // distinct thresholds, feature-major ascending (f32)
+  DeviceBuffer b_thr_off;  // num_feature + 1 offsets (int32)
 };
 
 // HBM-resident keyed card state (features.hip)
@@ -120,6 +128,13 @@ struct HostPack {
   int kind = 0, n_trees = 0, n_chunks = 0, chunk = 0, depth = 0, num_feature = 0;
   size_t tree_bytes = 0, chunk_stride = 0;
   float base_margin = 0.f;
+  // binned layout
+  bool binned = false;
+  std::vector<char> b_blob;
+  std::vector<float> b_thr;
+  std::vector<int32_t> b_thr_off;
+  int b_chunk = 0, b_n_chunks = 0, bin_steps = 0;
+  size_t b_tree_bytes = 0, b_chunk_stride = 0;
 };
 HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t);
 void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);

@@ -74,18 +74,26 @@ size_t lds_bytes_kernel3(int nf, size_t chunk_stride, int ch, size_t leaf_sz) {
 
 size_t lds_bytes_kernel1(int nf, size_t chunk_stride) { return (size_t)nf * kTile * 4 + 2 * chunk_stride + 64; }
 
+// forest_kernel4 has kernel 3's LDS map (bins are u32 words, nodes 4 B)
+size_t lds_bytes_kernel4(int nf, size_t chunk_stride, int ch, size_t leaf_sz) {
+  return lds_bytes_kernel3(nf, chunk_stride, ch, leaf_sz);
+}
+
+namespace {
+
 // Trees per staged chunk: for depth <= 8 the largest multiple of 4 (one tree per wave of each of the
-// four tree groups, x TPG) whose LDS image fits forest_kernel3's 160 KiB; deeper trees: kernel 1.
-static int choose_chunk(int D, int nf, size_t leaf_sz) {
-  const size_t tb = ((size_t)8 + leaf_sz) << D;
+// four tree groups, x TPG) whose LDS image fits forest_kernel3/4's 160 KiB; deeper trees: kernel 1.
+int choose_chunk(int D, int nf, size_t tree_bytes, size_t leaf_sz) {
   if (D <= 8) {
     for (int ch = 16; ch >= 4; ch -= 4)
-      if (lds_bytes_kernel3(nf, round1k(ch * tb), ch, leaf_sz) <= kLdsBudget) return ch;
+      if (lds_bytes_kernel3(nf, round1k(ch * tree_bytes), ch, leaf_sz) <= kLdsBudget) return ch;
   }
   for (int ch = 8; ch >= 1; ch /= 2)
-    if (lds_bytes_kernel1(nf, round1k(ch * tb)) <= kLdsBudget) return ch;
-  throw Error(FD_ERR_UNSUPPORTED, "forest does not fit the LDS budget");
+    if (lds_bytes_kernel1(nf, round1k(ch * tree_bytes)) <= kLdsBudget) return ch;
+  return 0;
 }
+
+}  // namespace
 
 HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
   FD_REQUIRE(p.kind == FD_FOREST_XGB_BINARY_LOGISTIC || p.kind == FD_FOREST_SKLEARN_IFOREST,
@@ -96,53 +104,106 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
   FD_REQUIRE(p.num_feature > 0 && p.num_feature <= kMaxFeatures, FD_ERR_UNSUPPORTED,
              "num_feature must be in [1, 64]");
   const bool xgb = p.kind == FD_FOREST_XGB_BINARY_LOGISTIC;
-  const int T = t.n_trees;
+  const int T = t.n_trees, nf = p.num_feature;
   int D = 1;
   for (int i = 0; i < T; ++i) {
     const int64_t a = t.tree_offsets[i], b = t.tree_offsets[i + 1];
     FD_REQUIRE(b > a, FD_ERR_INVALID_ARG, "empty tree");
     D = std::max(D, tree_depth(t.left + a, t.right + a, b - a));
   }
+  // engine threshold of an internal node: the f32 t with "go left <=> x < t"
+  auto engine_thr = [&](int64_t g) { return xgb ? (float)t.threshold[g] : sklearn_threshold_to_lt(t.threshold[g]); };
+
+  // distinct thresholds per feature (binned layout)
+  HostPack hp;
+  std::vector<std::vector<float>> tf(nf);
+  bool binnable = true;
+  for (int64_t g = 0; g < t.tree_offsets[T]; ++g) {
+    if (t.left[g] < 0) continue;
+    FD_REQUIRE(t.feature[g] >= 0 && t.feature[g] < nf, FD_ERR_INVALID_ARG, "split feature outside [0, num_feature)");
+    const float v = engine_thr(g);
+    if (v != v) binnable = false;
+    tf[t.feature[g]].push_back(v);
+  }
+  size_t max_cnt = 0;
+  for (auto& v : tf) {
+    if (!binnable) break;
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());  // == merges -0.0 / 0.0: same comparisons
+    max_cnt = std::max(max_cnt, v.size());
+  }
+  binnable = binnable && max_cnt <= (size_t)kMaxBins;
+
   const int NL = 1 << D;  // heap slots 1..NL-1 internal, NL..2NL-1 leaves
   const size_t leaf_sz = xgb ? sizeof(float) : sizeof(double);
   const size_t tree_bytes = (size_t)NL * 8 + (size_t)NL * leaf_sz;
-  const int CH = choose_chunk(D, p.num_feature, leaf_sz);
+  const int CH = choose_chunk(D, nf, tree_bytes, leaf_sz);
+  FD_REQUIRE(CH > 0, FD_ERR_UNSUPPORTED, "forest does not fit the LDS budget");
   const size_t chunk_stride = round1k(CH * tree_bytes);
   const int n_chunks = (T + CH - 1) / CH;
-  HostPack hp;
   hp.blob.assign(n_chunks * chunk_stride, 0);  // padding trees: all-zero nodes/leaves
   hp.leaf_ids.assign((size_t)n_chunks * CH * NL, -1);
-  std::vector<int32_t> cur(2 * NL);
 
+  const size_t b_tree_bytes = (size_t)NL * 4 + (size_t)NL * leaf_sz;
+  int BCH = 0;
+  if (binnable && D <= 8)
+    for (int ch = 16; ch >= 4 && !BCH; ch -= 4)
+      if (lds_bytes_kernel4(nf, round1k(ch * b_tree_bytes), ch, leaf_sz) <= kLdsBudget) BCH = ch;
+  binnable = binnable && BCH > 0;
+  if (binnable) {
+    hp.binned = true;
+    hp.b_chunk = BCH;
+    hp.b_tree_bytes = b_tree_bytes;
+    hp.b_chunk_stride = round1k(BCH * b_tree_bytes);
+    hp.b_n_chunks = (T + BCH - 1) / BCH;
+    hp.b_blob.assign(hp.b_n_chunks * hp.b_chunk_stride, 0);
+    hp.b_thr_off.assign(nf + 1, 0);
+    for (int f = 0; f < nf; ++f) {
+      hp.b_thr_off[f + 1] = hp.b_thr_off[f] + (int32_t)tf[f].size();
+      hp.b_thr.insert(hp.b_thr.end(), tf[f].begin(), tf[f].end());
+    }
+    int st = 1;
+    while ((size_t)st * 2 <= max_cnt) st *= 2;
+    hp.bin_steps = max_cnt ? st : 0;  // largest power of two <= max_cnt
+  }
+
+  std::vector<int32_t> cur(2 * NL);
   for (int i = 0; i < T; ++i) {
     const int64_t a = t.tree_offsets[i], m = t.tree_offsets[i + 1] - a;
     const int32_t* L = t.left + a;
     const int32_t* R = t.right + a;
     const int32_t* F = t.feature + a;
-    const double* TH = t.threshold + a;
     const uint8_t* DL = t.default_left ? t.default_left + a : nullptr;
     const double* LV = t.leaf_value + a;
     char* tb = hp.blob.data() + (size_t)(i / CH) * chunk_stride + (size_t)(i % CH) * tree_bytes;
     uint32_t* nodes = reinterpret_cast<uint32_t*>(tb);
     char* leaves = tb + (size_t)NL * 8;
+    char* btb = binnable ? hp.b_blob.data() + (size_t)(i / BCH) * hp.b_chunk_stride + (size_t)(i % BCH) * b_tree_bytes
+                         : nullptr;
+    uint32_t* bnodes = reinterpret_cast<uint32_t*>(btb);
+    char* bleaves = binnable ? btb + (size_t)NL * 4 : nullptr;
     cur[1] = 0;
     for (int s = 1; s < NL; ++s) {
       const int32_t o = cur[s];
       if (L[o] < 0) {  // leaf above depth D: pad node, both subtrees resolve to the same leaf
         nodes[2 * s] = 0;
         nodes[2 * s + 1] = 0;
+        if (binnable) bnodes[s] = 0;
         cur[2 * s] = o;
         cur[2 * s + 1] = o;
       } else {
         FD_REQUIRE(R[o] >= 0 && R[o] < m && L[o] < m, FD_ERR_INVALID_ARG, "bad child index");
-        FD_REQUIRE(F[o] >= 0 && F[o] < p.num_feature, FD_ERR_INVALID_ARG,
-                   "split feature outside [0, num_feature)");
-        const float thr = xgb ? (float)TH[o] : sklearn_threshold_to_lt(TH[o]);
+        const float thr = engine_thr(a + o);
         uint32_t tb32;
         std::memcpy(&tb32, &thr, 4);
         const uint32_t dl = (DL && DL[o]) ? 1u : 0u;
         nodes[2 * s] = tb32;
         nodes[2 * s + 1] = (uint32_t)F[o] * (uint32_t)(kTile * 4) | (dl << 31);
+        if (binnable) {
+          const auto& v = tf[F[o]];
+          const uint32_t j = (uint32_t)(std::lower_bound(v.begin(), v.end(), thr) - v.begin());
+          bnodes[s] = j << 16 | (uint32_t)F[o] * (uint32_t)(kTile * 4) | dl;
+        }
         cur[2 * s] = L[o];
         cur[2 * s + 1] = R[o];
       }
@@ -153,9 +214,11 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
       if (xgb) {
         const float v = (float)LV[o];
         std::memcpy(leaves + s * 4, &v, 4);
+        if (binnable) std::memcpy(bleaves + s * 4, &v, 4);
       } else {
         const double v = LV[o];
         std::memcpy(leaves + s * 8, &v, 8);
+        if (binnable) std::memcpy(bleaves + s * 8, &v, 8);
       }
       hp.leaf_ids[(size_t)i * NL + s] = o;
     }
@@ -165,7 +228,7 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
   hp.n_chunks = n_chunks;
   hp.chunk = CH;
   hp.depth = D;
-  hp.num_feature = p.num_feature;
+  hp.num_feature = nf;
   hp.tree_bytes = tree_bytes;
   hp.chunk_stride = chunk_stride;
   if (xgb) {
@@ -177,13 +240,18 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
   return hp;
 }
 
+namespace {
+template <typename T>
+void upload(DeviceBuffer& d, const std::vector<T>& h) {
+  d.ensure(std::max<size_t>(h.size() * sizeof(T), 4));
+  if (!h.empty()) FD_HIP(hipMemcpy(d.ptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+}  // namespace
+
 void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t) {
   const HostPack hp = pack_forest_host(p, t);
-  pf.blob.ensure(hp.blob.size());
-  FD_HIP(hipMemcpy(pf.blob.ptr, hp.blob.data(), hp.blob.size(), hipMemcpyHostToDevice));
-  pf.leaf_ids.ensure(hp.leaf_ids.size() * sizeof(int32_t));
-  FD_HIP(hipMemcpy(pf.leaf_ids.ptr, hp.leaf_ids.data(), hp.leaf_ids.size() * sizeof(int32_t),
-                   hipMemcpyHostToDevice));
+  upload(pf.blob, hp.blob);
+  upload(pf.leaf_ids, hp.leaf_ids);
   pf.kind = hp.kind;
   pf.n_trees = hp.n_trees;
   pf.n_chunks = hp.n_chunks;
@@ -195,6 +263,17 @@ void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_ar
   pf.base_margin = hp.base_margin;
   pf.if_offset = p.if_offset;
   pf.if_denominator = p.if_denominator;
+  pf.binned = hp.binned;
+  if (hp.binned) {
+    upload(pf.b_blob, hp.b_blob);
+    upload(pf.b_thr, hp.b_thr);
+    upload(pf.b_thr_off, hp.b_thr_off);
+    pf.b_chunk = hp.b_chunk;
+    pf.b_n_chunks = hp.b_n_chunks;
+    pf.b_tree_bytes = hp.b_tree_bytes;
+    pf.b_chunk_stride = hp.b_chunk_stride;
+    pf.bin_steps = hp.bin_steps;
+  }
   pf.loaded = true;
 }
 
@@ -238,6 +317,27 @@ __device__ __forceinline__ void stage_chunk(const char* __restrict__ src, char* 
     __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16), (lds_ptr)(dst + (p << 10)), 16,
                                      0, 0);
 }
+
+// Same staging, issued through inline asm. While an LDS-DMA issued by the builtin is outstanding,
+// LLVM's waitcnt insertion cannot count LDS reads and emits lgkmcnt(0) before every use, which
+// serialises the walk's independent chains. Hidden from the compiler, the DMA must be completed by
+// the caller: dma_wait() (vmcnt(0)) before the barrier that publishes the chunk.
+__device__ __forceinline__ void stage_chunk_asm(const char* __restrict__ src, uint32_t dst, int stride, int nwaves) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pieces = stride >> 10;
+  for (int p = wave; p < pieces; p += nwaves) {
+    const char* g = src + (p << 10) + lane * 16;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(dst + ((uint32_t)p << 10));
+    asm volatile(
+        "s_mov_b32 m0, %0\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off"
+        :
+        : "s"(m0), "v"(g)
+        : "memory", "m0");
+  }
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // XGBoost common::Sigmoid (src/common/math.h) in f32 / sklearn score -> decision -> the
 // reference's 1/(1+exp(s)) in f64.
@@ -354,50 +454,76 @@ forest_kernel1(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 
 constexpr int kWG3 = 1024;
 
+#ifdef FD_FOREST_PROFILE
+// Phase-cycle instrumentation (s_memtime), built only into the profiling variant of the library:
+// per wave of the first 256 workgroups {prologue, walk, leaf store, owner sum, barrier, total}.
+__device__ unsigned long long g_prof[256 * 16 * 8];
+#define FD_PROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define FD_PROF_ADD(acc, a, b) acc += (b) - (a)
+#else
+#define FD_PROF_T(v)
+#define FD_PROF_ADD(acc, a, b)
+#endif
+
+// Opaque copy: stops LLVM from folding `c ? v.z : v.x` over one loaded vector into a variable-index
+// element extract (a 4-way compare/select chain per component).
+__device__ __forceinline__ void opaque4(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+
+// Walks TPG trees of the staged chunk at `buf` for this lane's transaction. A[j] is the LDS address
+// of the children pair of the current node (heap slot i: tb + 16 i); per level one feature read and
+// one 16 B read of the chosen child's own children are in flight together. Returns leaf slots.
 template <int D, int TPG, typename LeafT, bool NAN_AWARE>
-__device__ __forceinline__ void walk3(uint32_t buf, int gg, uint32_t lane4, uint32_t (&idx)[TPG]) {
+__device__ __forceinline__ void walk3(uint32_t buf, int gg, uint32_t lane4, uint32_t (&slot)[TPG]) {
   constexpr uint32_t TB = (8u + (uint32_t)sizeof(LeafT)) << D;
-  uint32_t tb[TPG];
-  u32x2 nd[TPG];
-  u32x4 kids[TPG];
+  constexpr uint32_t NL = 1u << D;
+  uint32_t tb[TPG], A[TPG], thr[TPG], meta[TPG], k0[TPG], k1[TPG], k2[TPG], k3[TPG];
   float x[TPG];
 #pragma unroll
   for (int j = 0; j < TPG; ++j) {
     tb[j] = buf + (uint32_t)(gg * TPG + j) * TB;
-    idx[j] = 1u;
-    nd[j] = lds_load<u32x2>(tb[j] + 8u);  // root = heap slot 1
+    const u32x2 root = lds_load<u32x2>(tb[j] + 8u);  // heap slot 1
+    thr[j] = root.x;
+    meta[j] = root.y;
+    A[j] = tb[j] + 16u;
   }
 #pragma unroll
   for (int j = 0; j < TPG; ++j) {
-    x[j] = lds_load<float>((nd[j].y & 0x7fffffffu) | lane4);
-    if (D > 1) kids[j] = lds_load<u32x4>(tb[j] + 16u);  // slots 2, 3
+    x[j] = lds_load<float>((meta[j] & 0x7fffffffu) | lane4);
+    if (D > 1) {
+      const u32x4 k = lds_load<u32x4>(A[j]);  // slots 2, 3
+      k0[j] = k.x; k1[j] = k.y; k2[j] = k.z; k3[j] = k.w;
+    }
   }
 #pragma unroll
-  for (int l = 0; l + 1 < D; ++l) {
+  for (int l = 0; l < D; ++l) {
 #pragma unroll
     for (int j = 0; j < TPG; ++j) {
-      bool right = !(x[j] < __uint_as_float(nd[j].x));
+      bool right = !(x[j] < __uint_as_float(thr[j]));
       if (NAN_AWARE) {
-        if (x[j] != x[j]) right = (nd[j].y >> 31) == 0u;
+        if (x[j] != x[j]) right = (int32_t)meta[j] >= 0;  // missing: default direction
       }
-      idx[j] = 2u * idx[j] + (right ? 1u : 0u);
-      nd[j].x = right ? kids[j].z : kids[j].x;
-      nd[j].y = right ? kids[j].w : kids[j].y;
+      A[j] = 2u * A[j] - tb[j] + (right ? 16u : 0u);  // children pair of the chosen child
+      if (l + 1 < D) {
+        opaque4(k0[j], k1[j], k2[j], k3[j]);
+        thr[j] = right ? k2[j] : k0[j];
+        meta[j] = right ? k3[j] : k1[j];
+      }
     }
+    if (l + 1 < D) {
 #pragma unroll
-    for (int j = 0; j < TPG; ++j) {
-      x[j] = lds_load<float>((nd[j].y & 0x7fffffffu) | lane4);
-      if (l + 2 < D) kids[j] = lds_load<u32x4>(tb[j] + 16u * idx[j]);  // children of the new node
+      for (int j = 0; j < TPG; ++j) {
+        x[j] = lds_load<float>((meta[j] & 0x7fffffffu) | lane4);
+        if (l + 2 < D) {
+          const u32x4 k = lds_load<u32x4>(A[j]);
+          k0[j] = k.x; k1[j] = k.y; k2[j] = k.z; k3[j] = k.w;
+        }
+      }
     }
   }
 #pragma unroll
-  for (int j = 0; j < TPG; ++j) {
-    bool right = !(x[j] < __uint_as_float(nd[j].x));
-    if (NAN_AWARE) {
-      if (x[j] != x[j]) right = (nd[j].y >> 31) == 0u;
-    }
-    idx[j] = 2u * idx[j] + (right ? 1u : 0u);  // leaf heap slot in [2^D, 2^(D+1))
-  }
+  for (int j = 0; j < TPG; ++j) slot[j] = ((A[j] - tb[j]) >> 4) - NL;  // leaf heap slot - 2^D
 }
 
 template <int D, int CH, typename LeafT, int KIND>
@@ -425,8 +551,12 @@ forest_kernel3(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
   const uint32_t accL = lvB + CH * kTile * sizeof(LeafT);
   const int64_t row = (int64_t)blockIdx.x * kTile + txn;
   const bool valid = row < n;
+#ifdef FD_FOREST_PROFILE
+  unsigned long long p_walk = 0, p_leaf = 0, p_own = 0, p_sync = 0;
+#endif
+  FD_PROF_T(p_t0);
 
-  stage_chunk(blob, lbase + xbytes, chunk_stride, kWG3 / 64);  // chunk 0 lands while the tile loads
+  stage_chunk_asm(blob, bufA, chunk_stride, kWG3 / 64);  // chunk 0 lands while the tile loads
   int anynan = 0;
   const int ncopy = ld < nf ? ld : nf;
   {
@@ -448,14 +578,16 @@ forest_kernel3(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
       lds_store<LeafT>(accL + txn * sizeof(LeafT),
                        (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0);
   }
+  dma_wait();  // chunk 0 (published by tile_any's barrier)
   const bool tile_nan =
       tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (accL - s0) + kTile * sizeof(LeafT)), kWG3 / 64);
+  FD_PROF_T(p_t1);
 
   for (int k = 0; k < n_chunks; ++k) {
+    FD_PROF_T(q0);
     const uint32_t cur = (k & 1) ? bufB : bufA;
     if (k + 1 < n_chunks)
-      stage_chunk(blob + (size_t)(k + 1) * chunk_stride, lbase + xbytes + ((k + 1) & 1) * chunk_stride,
-                  chunk_stride, kWG3 / 64);
+      stage_chunk_asm(blob + (size_t)(k + 1) * chunk_stride, (k & 1) ? bufA : bufB, chunk_stride, kWG3 / 64);
     // owner of chunk k-1 adds its leaf values in tree order
     if (k > 0 && gg == ((k - 1) & 3)) {
       const uint32_t lv = ((k - 1) & 1) ? lvB : lvA;
@@ -464,25 +596,254 @@ forest_kernel3(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
       for (int c = 0; c < CH; ++c) acc += lds_load<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT));
       lds_store<LeafT>(accL + txn * sizeof(LeafT), acc);
     }
-    uint32_t idx[TPG];
+    FD_PROF_T(q1);
+    uint32_t slots[TPG];
     if (tile_nan)
-      walk3<D, TPG, LeafT, true>(cur, gg, lane4, idx);
+      walk3<D, TPG, LeafT, true>(cur, gg, lane4, slots);
     else
-      walk3<D, TPG, LeafT, false>(cur, gg, lane4, idx);
+      walk3<D, TPG, LeafT, false>(cur, gg, lane4, slots);
+#ifdef FD_FOREST_PROFILE
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    FD_PROF_T(q2);
     const uint32_t lv = (k & 1) ? lvB : lvA;
 #pragma unroll
     for (int j = 0; j < TPG; ++j) {
       const int c = gg * TPG + j;
       const uint32_t tb = cur + (uint32_t)c * TB;
-      const uint32_t slot = idx[j] - NL;
+      const uint32_t slot = slots[j];
       lds_store<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT), lds_load<LeafT>(tb + NL * 8u + slot * sizeof(LeafT)));
       if (out_leaf != nullptr && valid) {
         const int tg = k * CH + c;
         if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slot];
       }
     }
+    FD_PROF_T(q3);
+    dma_wait();
     __syncthreads();  // chunk k+1 landed; lv[k&1] complete; owner of k-1 done with lv[(k-1)&1]
+    FD_PROF_T(q4);
+    FD_PROF_ADD(p_own, q0, q1);
+    FD_PROF_ADD(p_walk, q1, q2);
+    FD_PROF_ADD(p_leaf, q2, q3);
+    FD_PROF_ADD(p_sync, q3, q4);
   }
+#ifdef FD_FOREST_PROFILE
+  if (lane == 0 && blockIdx.x < 256) {
+    FD_PROF_T(p_t2);
+    unsigned long long* o = g_prof + ((size_t)blockIdx.x * 16 + wave) * 8;
+    o[0] = p_t1 - p_t0; o[1] = p_walk; o[2] = p_leaf; o[3] = p_own; o[4] = p_sync; o[5] = p_t2 - p_t0;
+    o[6] = p_t0; o[7] = 0;
+  }
+#endif
+  const int last = n_chunks - 1;
+  if (gg != (last & 3)) return;
+  LeafT acc = lds_load<LeafT>(accL + txn * sizeof(LeafT));
+  {
+    const uint32_t lv = (last & 1) ? lvB : lvA;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) acc += lds_load<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT));
+  }
+  if (valid) write_outputs<KIND, LeafT>(acc, row, if_offset, if_denom, out_prob, out_raw);
+}
+
+// ------------------------------------------------------------------------------------------------
+// forest_kernel4 (depth <= 8, binned layout): kernel 3's structure with 4-byte nodes.
+//
+// The prologue replaces every feature value by its bin: the count of the feature's distinct split
+// thresholds that are <= x (branchless binary lifting over the sorted table, staged in LDS when it
+// fits), stored as the u32 word bin << 16 (missing/NaN: 0xFFFF << 16). A node word is
+// j << 16 | feature * 1024 | default_left, so "x < t_j" is "bin <= j" is ONE unsigned compare
+// word(x) <= node, the feature-row address is (node & 0xFC00) | lane, and a node's two children are
+// one 8-byte pair read: per level one ds_read_b32 (feature) and one ds_read_b64 (children).
+
+template <int D, int TPG, typename LeafT, bool NAN_AWARE>
+__device__ __forceinline__ void walk4(uint32_t buf, int gg, uint32_t lane4, uint32_t (&slot)[TPG]) {
+  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
+  constexpr uint32_t NL = 1u << D;
+  // P = LDS address of the children pair of the current node (heap slot i: tb + 8 i). Chosen child
+  // c = 2i + r has its pair at tb + 8c = 2P - tb + 8r = (P << 1) + (r ? 8 - tb : -tb).
+  uint32_t tb[TPG], c0[TPG], c8[TPG], P[TPG], node[TPG], kl[TPG], kr[TPG], xw[TPG];
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) {
+    tb[j] = buf + (uint32_t)(gg * TPG + j) * TB;
+    c0[j] = 0u - tb[j];
+    c8[j] = 8u - tb[j];
+    asm volatile("" : "+v"(c0[j]), "+v"(c8[j]));  // keep the two-term form (one cndmask + one lshl_add)
+    node[j] = lds_load<uint32_t>(tb[j] + 4u);     // heap slot 1
+    P[j] = tb[j] + 8u;                            // slots 2, 3
+  }
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) {
+    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+    if (D > 1) {
+      const u32x2 k = lds_load<u32x2>(P[j]);
+      kl[j] = k.x;
+      kr[j] = k.y;
+    }
+  }
+  // software-pipelined over the TPG chains: chain j's next reads are issued right after its step, so
+  // the wave keeps ~2 (TPG - 1) LDS reads in flight while it steps the other chains
+#pragma unroll
+  for (int l = 0; l < D; ++l) {
+#pragma unroll
+    for (int j = 0; j < TPG; ++j) {
+      bool right = xw[j] > node[j];  // bin > j  <=>  !(x < t_j)
+      if (NAN_AWARE) {
+        if (xw[j] == 0xFFFF0000u) right = (node[j] & 1u) == 0u;  // missing: default direction
+      }
+      P[j] = (P[j] << 1) + (right ? c8[j] : c0[j]);
+      if (l + 1 < D) {
+        uint32_t a = kl[j], b = kr[j];
+        asm volatile("" : "+v"(a), "+v"(b));
+        node[j] = right ? b : a;
+        xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+        if (l + 2 < D) {
+          const u32x2 k = lds_load<u32x2>(P[j]);
+          kl[j] = k.x;
+          kr[j] = k.y;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) slot[j] = ((P[j] - tb[j]) >> 3) - NL;  // leaf heap slot - 2^D
+}
+
+// bin(v) = #{t in tbl[0, cnt) : t <= v}, tbl ascending; steps = largest power of two <= max count.
+template <bool IN_LDS>
+__device__ __forceinline__ uint32_t bin_of(float v, const float* __restrict__ gt, uint32_t lt, int cnt, int steps) {
+  int pos = 0;
+  for (int st = steps; st > 0; st >>= 1) {
+    const int np = pos + st;
+    if (np <= cnt) {
+      const float t = IN_LDS ? lds_load<float>(lt + (uint32_t)(np - 1) * 4u) : gt[np - 1];
+      if (t <= v) pos = np;
+    }
+  }
+  return (uint32_t)pos;
+}
+
+template <int D, int CH, typename LeafT, int KIND>
+__global__ void __launch_bounds__(kWG3)
+forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
+               int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
+               const float* __restrict__ thr, const int32_t* __restrict__ thr_off, int bin_steps,
+               float base_margin, double if_offset, double if_denom, double* __restrict__ out_prob,
+               double* __restrict__ out_raw, int32_t* __restrict__ out_leaf) {
+  constexpr int TPG = CH / 4;
+  constexpr int NL = 1 << D;
+  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
+  const uint32_t s0 = (sdyn + 1023u) & ~1023u;
+  char* const lbase = smem + (s0 - sdyn);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int gg = wave >> 2;
+  const int txn = ((wave & 3) << 6) + lane;
+  const uint32_t lane4 = s0 + (uint32_t)txn * 4u;
+  const uint32_t xbytes = (uint32_t)nf * 1024u;
+  const uint32_t bufA = s0 + xbytes, bufB = bufA + (uint32_t)chunk_stride;
+  const uint32_t lvA = bufB + (uint32_t)chunk_stride;
+  const uint32_t lvB = lvA + CH * kTile * sizeof(LeafT);
+  const uint32_t accL = lvB + CH * kTile * sizeof(LeafT);
+  const int64_t row = (int64_t)blockIdx.x * kTile + txn;
+  const bool valid = row < n;
+#ifdef FD_FOREST_PROFILE
+  unsigned long long p_walk = 0, p_leaf = 0, p_own = 0, p_sync = 0;
+#endif
+  FD_PROF_T(p_t0);
+
+  stage_chunk_asm(blob, bufA, chunk_stride, kWG3 / 64);  // chunk 0 lands while the tile is binned
+  // threshold tables: into LDS over bufB + lv (dead until chunk 1 / the first leaf store) if they fit
+  const int n_thr = thr_off[nf];
+  const bool tbl_lds = (uint32_t)n_thr * 4u <= accL - bufB;
+  if (tbl_lds) {
+    float* tl = reinterpret_cast<float*>(lbase + (bufB - s0));
+    for (int i = tid; i < n_thr; i += kWG3) tl[i] = thr[i];
+    __syncthreads();
+  }
+  int anynan = 0;
+  const int ncopy = ld < nf ? ld : nf;
+  {
+    const int q = tid >> 8;  // the four threads sharing `txn` bin every 4th column
+    uint32_t* Xs = reinterpret_cast<uint32_t*>(lbase);
+    const float* xr = X + row * (int64_t)ld;
+    for (int f = q; f < nf; f += 4) {
+      uint32_t w = 0;
+      if (valid) {
+        const float v = f < ncopy ? xr[f] : __builtin_nanf("");  // DMatrix: missing column = NaN
+        if (v != v) {
+          w = 0xFFFF0000u;
+          anynan = 1;
+        } else {
+          const int o = thr_off[f], cnt = thr_off[f + 1] - o;
+          const uint32_t b = tbl_lds ? bin_of<true>(v, nullptr, bufB + (uint32_t)o * 4u, cnt, bin_steps)
+                                     : bin_of<false>(v, thr + o, 0u, cnt, bin_steps);
+          w = b << 16;
+        }
+      }
+      Xs[f * kTile + txn] = w;
+    }
+    if (gg == 0)
+      lds_store<LeafT>(accL + txn * sizeof(LeafT),
+                       (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0);
+  }
+  dma_wait();  // chunk 0 (published by tile_any's barrier)
+  const bool tile_nan =
+      tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (accL - s0) + kTile * sizeof(LeafT)), kWG3 / 64);
+  FD_PROF_T(p_t1);
+
+  for (int k = 0; k < n_chunks; ++k) {
+    FD_PROF_T(q0);
+    const uint32_t cur = (k & 1) ? bufB : bufA;
+    if (k + 1 < n_chunks)
+      stage_chunk_asm(blob + (size_t)(k + 1) * chunk_stride, (k & 1) ? bufA : bufB, chunk_stride, kWG3 / 64);
+    if (k > 0 && gg == ((k - 1) & 3)) {  // owner of chunk k-1 adds its leaf values in tree order
+      const uint32_t lv = ((k - 1) & 1) ? lvB : lvA;
+      LeafT acc = lds_load<LeafT>(accL + txn * sizeof(LeafT));
+#pragma unroll
+      for (int c = 0; c < CH; ++c) acc += lds_load<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT));
+      lds_store<LeafT>(accL + txn * sizeof(LeafT), acc);
+    }
+    FD_PROF_T(q1);
+    uint32_t slots[TPG];
+    if (tile_nan)
+      walk4<D, TPG, LeafT, true>(cur, gg, lane4, slots);
+    else
+      walk4<D, TPG, LeafT, false>(cur, gg, lane4, slots);
+#ifdef FD_FOREST_PROFILE
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    FD_PROF_T(q2);
+    const uint32_t lv = (k & 1) ? lvB : lvA;
+#pragma unroll
+    for (int j = 0; j < TPG; ++j) {
+      const int c = gg * TPG + j;
+      const uint32_t tb = cur + (uint32_t)c * TB;
+      lds_store<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT),
+                       lds_load<LeafT>(tb + NL * 4u + slots[j] * sizeof(LeafT)));
+      if (out_leaf != nullptr && valid) {
+        const int tg = k * CH + c;
+        if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slots[j]];
+      }
+    }
+    FD_PROF_T(q3);
+    dma_wait();
+    __syncthreads();  // chunk k+1 landed; lv[k&1] complete; owner of k-1 done with lv[(k-1)&1]
+    FD_PROF_T(q4);
+    FD_PROF_ADD(p_own, q0, q1);
+    FD_PROF_ADD(p_walk, q1, q2);
+    FD_PROF_ADD(p_leaf, q2, q3);
+    FD_PROF_ADD(p_sync, q3, q4);
+  }
+#ifdef FD_FOREST_PROFILE
+  if (lane == 0 && blockIdx.x < 256) {
+    FD_PROF_T(p_t2);
+    unsigned long long* o = g_prof + ((size_t)blockIdx.x * 16 + wave) * 8;
+    o[0] = p_t1 - p_t0; o[1] = p_walk; o[2] = p_leaf; o[3] = p_own; o[4] = p_sync; o[5] = p_t2 - p_t0;
+    o[6] = p_t0; o[7] = 0;
+  }
+#endif
   const int last = n_chunks - 1;
   if (gg != (last & 3)) return;
   LeafT acc = lds_load<LeafT>(accL + txn * sizeof(LeafT));
@@ -556,26 +917,91 @@ KernelFn pick3(int D, int CH) {
   }
 }
 
+using KernelFn4 = void (*)(const float*, int64_t, int, int, const char*, int, int, const int32_t*, int,
+                           const float*, const int32_t*, int, float, double, double, double*, double*, int32_t*);
+
+template <typename LeafT, int KIND, int CH>
+KernelFn4 pick4_ch(int D) {
+  switch (D) {
+    case 1: return forest_kernel4<1, CH, LeafT, KIND>;
+    case 2: return forest_kernel4<2, CH, LeafT, KIND>;
+    case 3: return forest_kernel4<3, CH, LeafT, KIND>;
+    case 4: return forest_kernel4<4, CH, LeafT, KIND>;
+    case 5: return forest_kernel4<5, CH, LeafT, KIND>;
+    case 6: return forest_kernel4<6, CH, LeafT, KIND>;
+    case 7: return forest_kernel4<7, CH, LeafT, KIND>;
+    case 8: return forest_kernel4<8, CH, LeafT, KIND>;
+    default: return nullptr;
+  }
+}
+
+template <typename LeafT, int KIND>
+KernelFn4 pick4(int D, int CH) {
+  switch (CH) {
+    case 4: return pick4_ch<LeafT, KIND, 4>(D);
+    case 8: return pick4_ch<LeafT, KIND, 8>(D);
+    case 12: return pick4_ch<LeafT, KIND, 12>(D);
+    case 16: return pick4_ch<LeafT, KIND, 16>(D);
+    default: return nullptr;
+  }
+}
+
 }  // namespace
 
+#ifdef FD_FOREST_PROFILE
+extern "C" __attribute__((visibility("default"))) int fd_debug_forest_profile(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * (size_t)n);
+}
+#endif
+
+// Kernel choice (option "forest_kernel"): 0 auto = kernel 4 when the binned layout exists (depth <= 8,
+// <= 65534 distinct thresholds per feature), else kernel 3 (depth <= 8), else kernel 1; 1/2/3 force
+// kernel 1/3/4 (FD_ERR_UNSUPPORTED when the forest cannot use it).
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
                    double* d_prob, double* d_raw, int32_t* d_leaf) {
   FD_REQUIRE(d_X && d_prob && ld > 0, FD_ERR_INVALID_ARG, "null buffer or bad ld");
   if (n == 0) return;
   const bool xgb = pf.kind == FD_FOREST_XGB_BINARY_LOGISTIC;
   const size_t leaf_sz = xgb ? sizeof(float) : sizeof(double);
+  const int64_t blocks = (n + kTile - 1) / kTile;
+  FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
+  const int v = e.forest_variant;
+  FD_REQUIRE(v >= 0 && v <= 3, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..3");
+  Engine::Timed* ev = nullptr;
+
+  const size_t lds4 = pf.binned ? lds_bytes_kernel4(pf.num_feature, pf.b_chunk_stride, pf.b_chunk, leaf_sz) : 0;
+  const bool ok4 = pf.binned && pf.depth <= 8 && pf.b_chunk % 4 == 0 && lds4 <= kLdsBudget;
+  if (v == 3) FD_REQUIRE(ok4, FD_ERR_UNSUPPORTED, "forest kernel 4 needs the binned layout (depth <= 8)");
+  if ((v == 0 || v == 3) && ok4) {
+    KernelFn4 fn = xgb ? pick4<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.b_chunk)
+                       : pick4<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.b_chunk);
+    FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel 4 for this depth/chunk");
+    FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4));
+    ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
+    if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
+    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kWG3), lds4, e.stream, d_X, n, (int)ld, pf.num_feature,
+                       pf.b_blob.as<const char>(), pf.b_n_chunks, (int)pf.b_chunk_stride,
+                       pf.leaf_ids.as<const int32_t>(), pf.n_trees, pf.b_thr.as<const float>(),
+                       pf.b_thr_off.as<const int32_t>(), pf.bin_steps, pf.base_margin, pf.if_offset,
+                       pf.if_denominator, d_prob, d_raw, d_leaf);
+    FD_HIP(hipGetLastError());
+    if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
+    return;
+  }
+
   KernelFn fn = nullptr;
   int threads = kTile;
   size_t lds = 0;
   const size_t lds3 = lds_bytes_kernel3(pf.num_feature, pf.chunk_stride, pf.chunk, leaf_sz);
-  if (e.forest_variant != 1 && pf.depth <= 8 && pf.chunk % 4 == 0 && lds3 <= kLdsBudget) {
+  const bool ok3 = pf.depth <= 8 && pf.chunk % 4 == 0 && lds3 <= kLdsBudget;
+  if (v == 2) FD_REQUIRE(ok3, FD_ERR_UNSUPPORTED, "forest kernel 3 does not fit this forest");
+  if (v != 1 && ok3) {
     fn = xgb ? pick3<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.chunk)
              : pick3<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.chunk);
     threads = kWG3;
     lds = lds3;
   }
   if (!fn) {
-    FD_REQUIRE(e.forest_variant != 2, FD_ERR_UNSUPPORTED, "forest kernel 3 does not fit this forest");
     fn = xgb ? pick1<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.chunk)
              : pick1<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.chunk);
     lds = lds_bytes_kernel1(pf.num_feature, pf.chunk_stride);
@@ -583,9 +1009,7 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel for this depth/chunk");
   FD_REQUIRE(lds <= kLdsBudget, FD_ERR_UNSUPPORTED, "LDS budget exceeded");
   FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const int64_t blocks = (n + kTile - 1) / kTile;
-  FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
-  Engine::Timed* ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
+  ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(threads), lds, e.stream, d_X, n, (int)ld, pf.num_feature,
                      pf.blob.as<const char>(), pf.n_chunks, (int)pf.chunk_stride, pf.leaf_ids.as<const int32_t>(),

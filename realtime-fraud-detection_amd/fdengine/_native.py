@@ -78,6 +78,9 @@ class fd_pack_info(C.Structure):
         ("blob_bytes", C.c_int64),
         ("n_leaf_ids", C.c_int64),
         ("base_margin", C.c_float),
+        ("layout", C.c_int32),
+        ("n_thresholds", C.c_int64),
+        ("bin_steps", C.c_int32),
     ]
 
 
@@ -148,6 +151,8 @@ SIGNATURES = {
     "fd_timing_reset": (C.c_int, [_vp]),
     "fd_pack_forest_host": (C.c_int, [C.POINTER(fd_forest_params), C.POINTER(fd_tree_arrays), _vp, _i64, _vp, _i64,
                                       C.POINTER(fd_pack_info)]),
+    "fd_pack_forest_binned_host": (C.c_int, [C.POINTER(fd_forest_params), C.POINTER(fd_tree_arrays), _vp, _i64,
+                                             _vp, _i64, _vp, C.POINTER(fd_pack_info)]),
 }
 
 

@@ -37,15 +37,18 @@ def _stale(out: Path, inputs) -> bool:
     return any(Path(p).stat().st_mtime > t for p in inputs)
 
 
-def build_engine(force: bool = False, verbose: bool = True) -> Path:
+def build_engine(force: bool = False, verbose: bool = True, profile: bool = False) -> Path:
+    """profile=True builds lib/libfdengine_prof.so with the forest kernel's phase-cycle
+    instrumentation (-DFD_FOREST_PROFILE; tools/forest_phases.py loads it via FDENGINE_LIB)."""
     LIB_DIR.mkdir(exist_ok=True)
-    out = LIB_DIR / "libfdengine.so"
+    out = LIB_DIR / ("libfdengine_prof.so" if profile else "libfdengine.so")
     srcs = [CSRC / s for s in HIP_SOURCES if (CSRC / s).exists()]
     deps = srcs + list(CSRC.glob("*.h")) + [REPO_ROOT / "include" / "fdengine.h"]
     if not force and not _stale(out, deps):
         return out
     tmp = out.with_suffix(".so.tmp")
-    cmd = [_hipcc(), *HIPCC_FLAGS, f"-I{REPO_ROOT / 'include'}", f"-I{CSRC}", *map(str, srcs), "-o", str(tmp)]
+    cmd = [_hipcc(), *HIPCC_FLAGS, *(["-DFD_FOREST_PROFILE"] if profile else []), f"-I{REPO_ROOT / 'include'}",
+           f"-I{CSRC}", *map(str, srcs), "-o", str(tmp)]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -79,3 +82,5 @@ def build_all(force: bool = False, verbose: bool = True) -> None:
 if __name__ == "__main__":
     import sys
     build_all(force="--force" in sys.argv)
+    if "--profile" in sys.argv:
+        build_engine(force="--force" in sys.argv, profile=True)

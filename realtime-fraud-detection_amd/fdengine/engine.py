@@ -269,6 +269,21 @@ def pack_forest_host(fa: ForestArrays):
     return blob.tobytes(), ids, info
 
 
+def pack_forest_binned_host(fa: ForestArrays):
+    """Host-only binned repack (no GPU): -> (blob bytes, thresholds f32, offsets int32, fd_pack_info).
+    Raises NativeError(FD_ERR_UNSUPPORTED) when a feature has more than 65534 distinct thresholds."""
+    p, t, keep = fa.c_structs()
+    info = N.fd_pack_info()
+    N.call("fd_pack_forest_binned_host", C.byref(p), C.byref(t), None, 0, None, 0, None, C.byref(info))
+    blob = np.empty(info.blob_bytes, np.uint8)
+    thr = np.empty(info.n_thresholds, np.float32)
+    off = np.empty(fa.num_feature + 1, np.int32)
+    N.call("fd_pack_forest_binned_host", C.byref(p), C.byref(t), C.c_void_p(blob.ctypes.data), info.blob_bytes,
+           C.c_void_p(thr.ctypes.data), info.n_thresholds, C.c_void_p(off.ctypes.data), C.byref(info))
+    del keep
+    return blob.tobytes(), thr, off, info
+
+
 def device_count() -> int:
     c = C.c_int()
     rc = N.lib.fd_device_count(C.byref(c))

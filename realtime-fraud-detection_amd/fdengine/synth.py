@@ -40,11 +40,21 @@ def feature_matrix(n: int, n_features: int, seed: int = 42, nan_frac: float = 0.
 
 
 def xgboost_doc(n_trees: int, depth: int, n_features: int, X_ref: np.ndarray, seed: int = 7,
-                p_leaf: float = 0.0, base_score: float = 0.5, num_feature: Optional[int] = None) -> dict:
+                p_leaf: float = 0.0, base_score: float = 0.5, num_feature: Optional[int] = None,
+                max_bin: Optional[int] = 256) -> dict:
     """Random gbtree trees in the XGBoost 2.0.3 JSON schema. p_leaf: chance a node at depth >= 2
-    stops early (ragged trees exercise the perfect-tree padding)."""
+    stops early (ragged trees exercise the perfect-tree padding). max_bin: split conditions are drawn
+    from per-feature quantile cuts of X_ref, as XGBoost 2.0's default tree_method="hist" (max_bin=256)
+    produces them (<= max_bin - 1 distinct thresholds per feature); None draws raw X_ref values."""
     rng = np.random.Generator(np.random.PCG64(seed))
     X_ref = np.asarray(X_ref, dtype=np.float32)
+    cuts = {}
+    if max_bin is not None:
+        q = np.linspace(0.0, 1.0, max_bin + 1)[1:-1]
+        for f in range(n_features):
+            col = X_ref[:, f]
+            col = col[~np.isnan(col)]
+            cuts[f] = np.unique(np.quantile(col, q).astype(np.float32)) if len(col) else np.zeros(1, np.float32)
     trees = []
     for tid in range(n_trees):
         left, right, parent, feat, cond, dleft, depthv = [], [], [], [], [], [], []
@@ -60,9 +70,12 @@ def xgboost_doc(n_trees: int, depth: int, n_features: int, X_ref: np.ndarray, se
             d = depthv[q]
             if d < depth and not (d >= 2 and rng.random() < p_leaf):
                 f = int(rng.integers(0, n_features))
-                col = X_ref[:, f]
-                col = col[~np.isnan(col)]
-                thr = float(col[rng.integers(0, len(col))]) if len(col) else 0.0
+                if max_bin is not None:
+                    thr = float(cuts[f][rng.integers(0, len(cuts[f]))])
+                else:
+                    col = X_ref[:, f]
+                    col = col[~np.isnan(col)]
+                    thr = float(col[rng.integers(0, len(col))]) if len(col) else 0.0
                 feat[q] = f
                 cond[q] = float(np.float32(thr))
                 dleft[q] = int(rng.integers(0, 2))

@@ -7,16 +7,18 @@ import pytest
 
 import oracle
 from fdengine import FraudEngine, iforest_from_sklearn, synth, xgboost_from_json_doc
+from fdengine import _native as N
 
 pytestmark = pytest.mark.gpu
 
 PROB_TOL = 1e-5  # north_star: fraud probabilities within 1e-5 absolute
 
 
-def _xgb_case(engine, slot, n, n_trees, depth, nf, seed, p_leaf=0.0, nan_frac=0.0, ld=None, base_score=0.5):
+def _xgb_case(engine, slot, n, n_trees, depth, nf, seed, p_leaf=0.0, nan_frac=0.0, ld=None, base_score=0.5,
+              max_bin=256):
     X = synth.feature_matrix(n, nf, seed=seed, nan_frac=nan_frac)
     doc = synth.xgboost_doc(n_trees, depth, nf, synth.feature_matrix(512, nf, seed=seed + 1), seed=seed + 2,
-                            p_leaf=p_leaf, base_score=base_score)
+                            p_leaf=p_leaf, base_score=base_score, max_bin=max_bin)
     fa = xgboost_from_json_doc(doc)
     if ld is not None and ld < nf:
         X = np.ascontiguousarray(X[:, :ld])
@@ -113,12 +115,15 @@ def test_device_pointer_path_matches_host_path(engine):
     np.testing.assert_array_equal(dp.cpu().numpy(), host)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-def test_kernel_variants_agree(engine, variant):
-    """Both forest kernels (256-thread, 1024-thread tree-split) give the oracle's bits."""
+@pytest.mark.parametrize("max_bin", [256, None])
+@pytest.mark.parametrize("variant", [1, 2, 3])
+def test_kernel_variants_agree(engine, variant, max_bin):
+    """Every forest kernel (256-thread; 1024-thread tree-split on the threshold layout; 1024-thread on
+    the binned layout) gives the oracle's bits, for hist-style and raw-valued split thresholds."""
     engine.set_option("forest_kernel", variant)
     try:
-        prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 0, 3001, 203, 8, 50, seed=81, p_leaf=0.05, nan_frac=0.01)
+        prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 0, 3001, 203, 8, 50, seed=81, p_leaf=0.05, nan_frac=0.01,
+                                                max_bin=max_bin)
         np.testing.assert_array_equal(leaf, rl)
         np.testing.assert_array_equal(raw.astype(np.float32), rm)
         assert np.abs(prob - rp).max() <= PROB_TOL
@@ -130,5 +135,24 @@ def test_kernel_variants_agree(engine, variant):
         rp2, rd2, rl2 = oracle.iforest_predict(fa, X, want_leaf=True)
         np.testing.assert_array_equal(lf, rl2)
         np.testing.assert_array_equal(d, rd2)
+    finally:
+        engine.set_option("forest_kernel", 0)
+
+
+def test_unbinnable_forest_falls_back(engine):
+    """> 65534 distinct thresholds in a feature: auto picks the threshold-layout kernel (still exact);
+    forcing the binned kernel is refused."""
+    Xr = np.random.default_rng(2).normal(size=(200000, 1)).astype(np.float32)
+    fa = xgboost_from_json_doc(synth.xgboost_doc(400, 8, 1, Xr, seed=5, max_bin=None))
+    engine.load_forest(0, fa)
+    X = synth.feature_matrix(1000, 1, seed=6, nan_frac=0.05)
+    prob, raw, leaf = engine.predict(0, X, want_raw=True, want_leaf=True)
+    rp, rm, rl = oracle.xgb_predict(fa, X, want_leaf=True)
+    np.testing.assert_array_equal(leaf, rl)
+    np.testing.assert_array_equal(raw.astype(np.float32), rm)
+    engine.set_option("forest_kernel", 3)
+    try:
+        with pytest.raises(N.NativeError):
+            engine.predict(0, X)
     finally:
         engine.set_option("forest_kernel", 0)

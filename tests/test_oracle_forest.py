@@ -101,3 +101,70 @@ def test_sklearn_threshold_rewrite_is_exact_at_the_boundary():
             d, _ = forest_ref.iforest_walk(fa, [x])
             pd_, _ = forest_ref.packed_walk(blob, ids, info, False, [x])
             assert d == pd_, (thr, x)
+
+
+# ---------------------------------------------------------------- binned layout (forest_kernel4)
+
+from fdengine.engine import pack_forest_binned_host  # noqa: E402
+
+
+@pytest.mark.parametrize("max_bin", [256, None])
+def test_binned_layout_matches_oracle_xgb(max_bin):
+    X = synth.feature_matrix(300, 30, seed=3, nan_frac=0.05)
+    fa = xgboost_from_json_doc(synth.xgboost_doc(25, 8, 30, X, seed=4, p_leaf=0.2, base_score=0.3, max_bin=max_bin))
+    _, margin, leaf = oracle.xgb_predict(fa, X, want_leaf=True)
+    blob, ids, info = pack_forest_host(fa)
+    bblob, thr, off, binfo = pack_forest_binned_host(fa)
+    assert binfo.layout == 1 and binfo.depth == 8 and binfo.tree_bytes == 256 * 4 + 256 * 4
+    assert len(off) == 31 and off[0] == 0 and off[-1] == len(thr) == binfo.n_thresholds
+    for f in range(30):
+        t = thr[off[f]:off[f + 1]]
+        assert np.all(np.diff(t) > 0)  # ascending, distinct
+    if max_bin:
+        assert np.diff(off).max() <= 255
+    assert binfo.bin_steps == (1 << int(np.floor(np.log2(np.diff(off).max()))))
+    for r in range(0, 300, 7):
+        pm, pl = forest_ref.packed_walk_binned(bblob, ids, thr, off, binfo, True, X[r])
+        assert np.float32(pm) == margin[r]
+        assert pl == list(leaf[r])
+
+
+def test_binned_layout_matches_sklearn_iforest():
+    Xtr = synth.feature_matrix(1500, 16, seed=8).astype(np.float64)
+    m = synth.isolation_forest(Xtr, n_estimators=30)
+    fa = iforest_from_sklearn(m)
+    X = synth.feature_matrix(200, 16, seed=9, nan_frac=0.02)
+    prob, depth, leaf = oracle.iforest_predict(fa, X, want_leaf=True)
+    bblob, thr, off, binfo = pack_forest_binned_host(fa)
+    _, ids, _ = pack_forest_host(fa)
+    for r in range(0, 200, 9):
+        d, lv = forest_ref.packed_walk_binned(bblob, ids, thr, off, binfo, False, X[r])
+        assert d == depth[r]
+        assert lv == list(leaf[r])
+
+
+def test_binned_sklearn_threshold_boundary():
+    rng = np.random.default_rng(1)
+    left = np.array([1, -1, -1]); right = np.array([2, -1, -1])
+    for _ in range(100):
+        thr = float(rng.normal() * 10.0 ** int(rng.integers(-3, 4)))
+        fa = ForestArrays(kind=N.FD_FOREST_SKLEARN_IFOREST, num_feature=1, offsets=np.array([0, 3]), left=left,
+                          right=right, feature=np.zeros(3, int), threshold=np.array([thr, 0, 0]),
+                          default_left=np.zeros(3, int), leaf_value=np.array([0, 1.0, 2.0]), if_denominator=1.0)
+        bblob, thr_t, off, binfo = pack_forest_binned_host(fa)
+        _, ids, _ = pack_forest_host(fa)
+        f = np.float32(thr)
+        for x in (np.nextafter(f, np.float32(-np.inf)), f, np.nextafter(f, np.float32(np.inf))):
+            d, _ = forest_ref.iforest_walk(fa, [x])
+            bd, _ = forest_ref.packed_walk_binned(bblob, ids, thr_t, off, binfo, False, [x])
+            assert d == bd, (thr, x)
+
+
+def test_binned_layout_refused_beyond_65534_thresholds():
+    X = np.random.default_rng(2).normal(size=(200000, 1)).astype(np.float32)
+    fa = xgboost_from_json_doc(synth.xgboost_doc(400, 8, 1, X, seed=5, max_bin=None))
+    with pytest.raises(N.NativeError) as ei:
+        pack_forest_binned_host(fa)
+    assert ei.value.code == N.FD_ERR_UNSUPPORTED
+    blob, ids, info = pack_forest_host(fa)  # the threshold layout still packs
+    assert info.layout == 0 and info.n_thresholds == 0

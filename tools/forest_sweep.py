@@ -21,7 +21,7 @@ X = synth.feature_matrix(4 * B, F, seed=1000)
 forest = fdengine.xgboost_from_json_doc(synth.xgboost_doc(T, D, F, synth.feature_matrix(2048, F, seed=7), seed=8))
 eng = fdengine.FraudEngine(0)
 eng.load_forest(0, forest)
-info = eng.forest_info(0); print(f"depth {info.depth} chunk {info.chunk} chunk_stride {info.chunk_stride}")
+print("forest", eng.forest_info(0))
 dX = torch.from_numpy(X).cuda()
 dp = torch.empty(4 * B, dtype=torch.float64, device="cuda")
 eng.set_stream(torch.cuda.current_stream().cuda_stream)
