@@ -124,7 +124,7 @@ class Config2:
         achieved = per_launch / avg / 1e9
         return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(self.name, self.B),
-                "kernel": f"forest_kernel_v2<D={self.info['depth']},f32,XGB>", "kernel_avg_us": round(avg * 1e6, 3),
+                "kernel": f"forest_kernel4<D={self.info['depth']},f32,XGB> (binned layout)", "kernel_avg_us": round(avg * 1e6, 3),
                 "algorithmic_bytes_per_launch": per_launch, "bytes_per_txn": self.F * 4 + 8,
                 "model_bytes_per_launch": model_bytes,
                 "node_steps_per_s": round(self.B * self.T * self.info["depth"] / avg, 1)}
@@ -273,7 +273,7 @@ class Config3:
         achieved = per_launch / avg / 1e9
         return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(self.name, self.B),
-                "kernel": "forest_kernel_v2<D=8,f32,XGB> (dominant)", "kernel_avg_us": round(avg * 1e6, 3),
+                "kernel": "forest_kernel4<D=8,f32,XGB> (binned layout; dominant)", "kernel_avg_us": round(avg * 1e6, 3),
                 "algorithmic_bytes_per_launch": per_launch, "bytes_per_txn": 64 * 4 + 8,
                 "model_bytes_per_launch": model_bytes}
 
