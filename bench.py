@@ -280,7 +280,8 @@ class Config3:
     def kernels(self, timing):
         N = self.N
         names = {N.FD_TIMING_XGB: "xgboost_forest", N.FD_TIMING_IFOREST: "iforest_forest",
-                 N.FD_TIMING_FEATURES: "features (assign+process)", N.FD_TIMING_BLEND: "blend"}
+                 N.FD_TIMING_FEATURES: "features (assign+process)", N.FD_TIMING_BLEND: "blend",
+                 N.FD_TIMING_ROUTE: "route_partition (count+scan+scatter)"}
         return {names[k]: round(ms / max(1, c) * 1e3, 3) for k, (ms, c) in timing.items() if c}
 
     def config(self, world):
@@ -317,7 +318,161 @@ class Config3:
                           f"{dt:.2f} s, CPU: {cpu_model()}"}
 
 
-WORKLOADS = {"config2": Config2, "config3": Config3}
+# --------------------------------------------------------------------------------------- config 4
+class Config4(Config3):
+    """BASELINE configs[3]: card-hash-sharded keyed state + scoring, RCCL all-to-all routing.
+    Each rank ingests its own 64k-txn micro-batch per step (drawn over ALL cards), routes every
+    transaction to the GPU owning its card (fdengine.sharding.ShardedScorer: partition kernel ->
+    all-to-all of 48-B records -> owner scores features + XGBoost + IsolationForest + blend ->
+    all-to-all of 24-B results back -> scatter to arrival order). Cards: 100M over the node (each GPU
+    holds only the cards it owns). At N=1 the same kernels run with no collective."""
+    name = "config4"
+
+    def __init__(self, args, rank, dev, eng):
+        import numpy as np
+        import torch
+        import fdengine
+        from fdengine import _native as N
+        from fdengine import synth
+        from fdengine.sharding import EngineShardBackend, ShardedScorer
+        from oracle import scoring_ref as S
+        self.np, self.torch, self.N, self.S = np, torch, N, S
+        self.B, self.T, self.D = args.batch, args.trees, args.depth
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = rank
+        self.cards = args.cards
+        self.mode, self.K = (1 if args.window == "sliding" else 0), args.ring_k
+        self.eng = eng
+        t = time.time()
+        self.merchants = synth.merchants_table(5000, seed=100)
+        # models fitted on realistic scoring vectors (same recipe as config 3)
+        from oracle.features_c import OracleFeatureState
+        spop = synth.population(20000, 500, seed=11)
+        stx = synth.txn_stream(spop, 40000, seed=12, rate_per_s=20.0)
+        so = OracleFeatureState(1 << 16, self.mode, self.K)
+        so.load_users(spop["users"]["key"], spop["users"]["avg_amount"], spop["users"]["account_age_days"],
+                      spop["users"]["device_fp"])
+        so.load_merchants(spop["merchants"]["fraud_rate"], spop["merchants"]["risk_multiplier"])
+        _, Xref = so.run(stx, want_raw=False)
+        del so
+        self.xgb = fdengine.xgboost_from_json_doc(synth.xgboost_doc(self.T, self.D, 64, Xref[-8192:], seed=13))
+        self.ifm = fdengine.iforest_from_sklearn(synth.isolation_forest(Xref[-8192:].astype(np.float64)))
+        eng.load_forest(0, self.xgb)
+        eng.load_forest(1, self.ifm)
+        self.names = ["xgboost_primary", "isolation_forest"]
+        w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
+        self.weights = [w[n] for n in self.names]
+        self.mults = [S.CONF_MULT[n] for n in self.names]
+        self.params = fdengine.FraudEngine.blend_params(self.weights, self.mults)
+        # this GPU's cards
+        own = synth.owned_cards(self.cards, rank, self.world, seed=42)
+        self.n_owned = len(own["key"])
+        cap = 1
+        while cap < int(self.n_owned * 1.6) + 65536:
+            cap *= 2
+        self.cap = cap
+        eng.state_init(cap, self.mode, self.K)
+        eng.load_users(own["key"], own["avg_amount"], own["account_age_days"], own["device_fp"])
+        del own
+        eng.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
+        # this rank's ingest stream (over all cards), resident in HBM
+        self.n_batches = args.warmup + args.steps + args.latency_iters + 1
+        self.tx = synth.txn_stream_cards(self.cards, self.merchants, self.n_batches * self.B, seed=200 + rank,
+                                         card_seed=42, rate_per_s=2000.0)
+        self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
+        self.scorer = ShardedScorer(EngineShardBackend(eng, self.params, [0, 1]), rank, self.world)
+        self.out = None
+        B = self.B
+        self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
+        self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
+        self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
+        self.next_batch = 0
+        log(f"[rank {rank}] config4 setup {time.time() - t:.1f}s: {self.cards} cards over {self.world} GPU(s), "
+            f"{self.n_owned} owned here, capacity {cap}, {self.n_batches} batches resident")
+
+    def step(self, i):
+        b = self.next_batch
+        if b >= self.n_batches:
+            raise RuntimeError("stream exhausted: raise n_batches")
+        self.next_batch += 1
+        B = self.B
+        part = {f: t[b * B:(b + 1) * B] for f, t in self.dev.items()}
+        self.out = self.scorer.step(part, B)
+
+    def fetch(self, i):
+        fp, conf, dec, risk = self.out
+        self.h_fp.copy_(fp, non_blocking=True)
+        self.h_dec.copy_(dec, non_blocking=True)
+        self.h_risk.copy_(risk, non_blocking=True)
+
+    def parity(self):
+        """N=1 only: batch 0 (fresh state) through the oracle chain. The oracle state holds just the
+        profiles of the cards batch 0 touches (identical results, bounded host memory at 100M cards).
+        The N>1 exchange is checked by tests/test_sharding.py (gloo) and tests/test_gpu_sharding.py."""
+        if self.world > 1:
+            self.step(0)
+            return None
+        import oracle
+        from fdengine import synth
+        from oracle.features_c import OracleFeatureState
+        np = self.np
+        part = {f: self.tx[f][:self.B] for f in self.N.TXN_FIELDS}
+        self.step(0)
+        self.torch.cuda.synchronize()
+        o = OracleFeatureState(1 << 18, self.mode, self.K)
+        ids_keys = np.unique(part["card_key"])
+        at = synth.card_attrs(self.tx["card_id"][:self.B], 42)  # the profiles of the cards batch 0 touches
+        _, first = np.unique(at["key"], return_index=True)
+        o.load_users(at["key"][first], at["avg_amount"][first], at["account_age_days"][first], at["device_fp"][first])
+        o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
+        _, V = o.run(part, want_raw=False)
+        del o
+        px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
+        pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
+        fp, _, dec, _ = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults)
+        got_fp, got_dec = self.out[0].cpu().numpy(), self.out[2].cpu().numpy()
+        return {"max_abs_prob_diff": float(np.abs(got_fp - fp).max()),
+                "decision_mismatches": int((got_dec != dec).sum()), "cards_touched": int(len(ids_keys))}
+
+    def config(self, world):
+        return {"workload": "config4: card-hash-sharded keyed state (fmix64 owner) + RCCL all-to-all routing "
+                            "(48-B txn records out, 24-B results back) -> features + XGBoost 500x8 + "
+                            "IsolationForest 100 + blend on the owner, 64k-txn micro-batch per GPU per step",
+                "cards": self.cards, "cards_per_gpu": self.n_owned, "window_mode": "sliding" if self.mode else
+                "redis_compat", "ring_k": self.K, "trees": self.T, "depth": self.D, "features": 64,
+                "batch_per_gpu": self.B, "parallelism": f"card-hash shards x{world}, RCCL all-to-all"}
+
+    def cpu_baseline(self, seconds):
+        """Oracle chain on the first transactions of this rank's stream (N=1)."""
+        import oracle
+        from fdengine import synth
+        from oracle.features_c import OracleFeatureState
+        np = self.np
+        th = cpu_threads()
+        o = OracleFeatureState(1 << 22, self.mode, self.K)
+        chunk = 16384
+        done, a = 0, time.perf_counter()
+        u = self.tx["card_id"][:1 << 21]
+        at = synth.card_attrs(u, 42)
+        _, first = np.unique(at["key"], return_index=True)
+        o.load_users(at["key"][first], at["avg_amount"][first], at["account_age_days"][first], at["device_fp"][first])
+        o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
+        a = time.perf_counter()
+        while time.perf_counter() - a < seconds and done + chunk <= len(u):
+            part = {f: self.tx[f][done:done + chunk] for f in self.N.TXN_FIELDS}
+            _, V = o.run(part, want_raw=False)
+            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=th)
+            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=th)
+            oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults, nthreads=th)
+            done += chunk
+        dt = time.perf_counter() - a
+        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
+                "sample": f"first {done} txns of the config-4 stream through the oracle chain (features C "
+                          f"single-threaded + XGBoost + IsolationForest + blend, {th} OpenMP threads), "
+                          f"{dt:.2f} s, CPU: {cpu_model()}"}
+
+
+WORKLOADS = {"config2": Config2, "config3": Config3, "config4": Config4}
 
 
 def main():
@@ -331,13 +486,16 @@ def main():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--features", type=int, default=50)
     ap.add_argument("--pool", type=int, default=8, help="config2: distinct HBM-resident micro-batches cycled")
-    ap.add_argument("--cards", type=int, default=10_000_000, help="config3: cards resident in HBM")
+    ap.add_argument("--cards", type=int, default=None,
+                    help="cards resident in HBM (config3 default 10M; config4 default 100M over the node)")
     ap.add_argument("--window", choices=["sliding", "redis"], default="sliding")
     ap.add_argument("--ring-k", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=200)
     args = ap.parse_args()
+    if args.cards is None:
+        args.cards = 100_000_000 if args.workload == "config4" else 10_000_000
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 2
+#define FD_ABI_VERSION 3
 
 enum fd_status {
   FD_OK = 0,
@@ -239,12 +239,41 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
                           int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
                           double* d_confidence, uint8_t* d_decision, uint8_t* d_risk);
 
+/* ---------------------------------------------------------------- card-hash sharding */
+/* The reference partitions per-card work by key (Kafka key / Flink keyBy(userId),
+   fl/FraudDetectionJob.java; velocity state in one Redis, fl/services/RedisService.java:178-207).
+   Here GPU r of G owns the cards with fd_shard_of(card_key, G) == r and keeps their state in its HBM.
+   One micro-batch step on G GPUs (the host shim drives the two RCCL all-to-alls):
+     ingest GPU : fd_route_partition_device   -> records grouped by owner (stable) + per-owner counts
+     (all-to-all of counts, then of FD_ROUTE_RECORD_BYTES records)
+     owner GPU  : fd_score_records_device      -> features + forests + blend, FD_RESULT_RECORD_BYTES records
+     (all-to-all of result records back, reversed splits)
+     ingest GPU : fd_route_scatter_results_device -> results in the micro-batch's original order.
+   Records from one source keep their arrival order, so every card sees its transactions in
+   (step, ingest rank, ingest index) order. */
+#define FD_MAX_SHARDS 64
+#define FD_ROUTE_RECORD_BYTES 48
+#define FD_RESULT_RECORD_BYTES 24
+/* owner shard of each key (host-only; what the shim uses to load each GPU's user profiles) */
+int fd_shard_of_host(const uint64_t* keys, int64_t n, int32_t n_shards, int32_t* out);
+/* d_records: n x FD_ROUTE_RECORD_BYTES, owner-major, stable; d_counts: n_shards int64 (device) */
+int fd_route_partition_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, int32_t n_shards,
+                              void* d_records, int64_t* d_counts);
+/* the whole hot path (fd_score_batch_device) over received records; d_results: n x FD_RESULT_RECORD_BYTES
+   {f64 fraud_prob, f64 confidence, u32 seq, u8 decision, u8 risk, u16 pad} in the records' order */
+int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                            const uint8_t* present, const void* d_records, int64_t n, void* d_results);
+/* out[seq] = result for each of the n returned records; conf/decision/risk may be NULL.
+   fd_engine_sync reports a record whose seq is outside [0, n). */
+int fd_route_scatter_results_device(fd_engine* eng, const void* d_results, int64_t n, double* d_fraud_prob,
+                                    double* d_confidence, uint8_t* d_decision, uint8_t* d_risk);
+
 /* ---------------------------------------------------------------- diagnostics */
 /* Per-launch device timing of the engine's hot kernels, measured with HIP events recorded on the
    launch stream around each kernel. fd_timing_read synchronises and returns the summed time (ms) and
    count of the timed launches of `kind` (FD_TIMING_ALL: every kind) since the last fd_timing_reset. */
 enum fd_timing_kind { FD_TIMING_ALL = -1, FD_TIMING_XGB = 0, FD_TIMING_IFOREST = 1, FD_TIMING_FEATURES = 2,
-                      FD_TIMING_BLEND = 3 };
+                      FD_TIMING_BLEND = 3, FD_TIMING_ROUTE = 4 };
 int fd_engine_set_timing(fd_engine* eng, int enable);
 /* Engine tuning knobs (for A/B measurement; defaults are the tuned choices):
      "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel

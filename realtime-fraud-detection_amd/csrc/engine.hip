@@ -150,6 +150,7 @@ int fd_engine_destroy(fd_engine* eng) {
   e.stage_ext.release();
   e.feat_vec.release();
   e.feat_in.release();
+  for (auto* b : {&e.route_blk, &e.route_soa, &e.route_out, &e.route_err}) b->release();
   for (auto* b : {&e.state.headers, &e.state.fps, &e.state.ring, &e.state.merchants, &e.state.slot,
                   &e.state.next, &e.state.err})
     b->release();
@@ -180,6 +181,7 @@ int fd_engine_sync(fd_engine* eng) {
   FD_API_BEGIN
   Engine& e = E(eng);
   FD_HIP(hipStreamSynchronize(e.stream));
+  fd::route_check(e);
   FD_API_END
 }
 
@@ -519,6 +521,55 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
   fd::launch_features(e, *txns, n, vec, nullptr);
   score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
                d_confidence, d_decision, d_risk);
+  FD_API_END
+}
+
+int fd_shard_of_host(const uint64_t* keys, int64_t n, int32_t n_shards, int32_t* out) {
+  FD_API_BEGIN
+  FD_REQUIRE(n >= 0 && (n == 0 || (keys && out)), FD_ERR_INVALID_ARG, "bad arguments");
+  FD_REQUIRE(n_shards >= 1 && n_shards <= FD_MAX_SHARDS, FD_ERR_INVALID_ARG, "n_shards must be in [1, 64]");
+  for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)fd::shard_of_host(keys[i], (unsigned)n_shards);
+  FD_API_END
+}
+
+int fd_route_partition_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, int32_t n_shards,
+                              void* d_records, int64_t* d_counts) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
+  fd::launch_route_partition(e, *txns, n, n_shards, d_records, d_counts);
+  FD_API_END
+}
+
+int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                            const uint8_t* present, const void* d_records, int64_t n, void* d_results) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params && slots && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  for (int m = 0; m < params->n_models && m < FD_MAX_MODELS; ++m)
+    FD_REQUIRE(slots[m] >= 0 || (present && !present[m]), FD_ERR_INVALID_ARG,
+               "routed scoring needs every present model in a forest slot");
+  if (n == 0) return FD_OK;
+  unsigned* seq = nullptr;
+  const fd_txn_batch t = fd::launch_route_unpack(e, d_records, n, &seq);
+  e.feat_vec.ensure((size_t)n * FD_VECTOR_WIDTH * 4);
+  e.route_out.ensure((size_t)n * (2 * sizeof(double) + 2));
+  double* fp = e.route_out.as<double>();
+  double* conf = fp + n;
+  uint8_t* dec = reinterpret_cast<uint8_t*>(conf + n);
+  uint8_t* risk = dec + n;
+  fd::launch_features(e, t, n, e.feat_vec.as<float>(), nullptr);
+  score_matrix(e, *params, slots, nullptr, present, e.feat_vec.as<float>(), n, FD_VECTOR_WIDTH, nullptr, fp, conf,
+               dec, risk);
+  fd::launch_result_pack(e, fp, conf, dec, risk, seq, n, d_results);
+  FD_API_END
+}
+
+int fd_route_scatter_results_device(fd_engine* eng, const void* d_results, int64_t n, double* d_fraud_prob,
+                                    double* d_confidence, uint8_t* d_decision, uint8_t* d_risk) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::launch_result_scatter(e, d_results, n, d_fraud_prob, d_confidence, d_decision, d_risk);
   FD_API_END
 }
 

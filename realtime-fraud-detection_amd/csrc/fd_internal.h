@@ -87,6 +87,25 @@ struct PackedForest {
   DeviceBuffer b_thr_off;  // num_feature + 1 offsets (int32)
 };
 
+// card-hash routing records (route.hip): one transaction (48 B) / one result (24 B)
+struct __attribute__((aligned(16))) RouteRecord {
+  unsigned long long key;
+  long long ts;
+  long long cents;
+  unsigned long long dfp;
+  int merchant;
+  unsigned seq;  // index in the ingest rank's micro-batch
+  unsigned char ipc, hour, wk, pad0;
+  unsigned pad1;
+};
+struct __attribute__((aligned(8))) ResultRecord {
+  double fraud_prob;
+  double confidence;
+  unsigned seq;
+  unsigned char decision, risk;
+  unsigned short pad;
+};
+
 // HBM-resident keyed card state (features.hip)
 struct CardStore {
   bool ready = false;
@@ -108,6 +127,8 @@ struct Engine {
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
+  DeviceBuffer route_blk, route_soa, route_out, route_err;  // card-hash routing scratch (route.hip)
+  bool route_err_live = false;
   // optional per-launch kernel timing (HIP events on the launch stream)
   int forest_variant = 0;  // "forest_kernel" option
   bool timing = false;
@@ -148,6 +169,15 @@ void load_users(Engine& e, const fd_users& u);
 void load_merchants(Engine& e, const fd_merchants& m);
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw);
 void features_check(Engine& e);
+// route.hip
+unsigned shard_of_host(unsigned long long key, unsigned G);
+void launch_route_partition(Engine& e, const fd_txn_batch& t, int64_t n, int G, void* d_records, int64_t* d_counts);
+fd_txn_batch launch_route_unpack(Engine& e, const void* d_records, int64_t n, unsigned** d_seq);
+void launch_result_pack(Engine& e, const double* fp, const double* conf, const uint8_t* dec, const uint8_t* risk,
+                        const unsigned* seq, int64_t n, void* d_results);
+void launch_result_scatter(Engine& e, const void* d_results, int64_t n, double* fp, double* conf, uint8_t* dec,
+                           uint8_t* risk);
+void route_check(Engine& e);
 // blend.hip
 void launch_blend(Engine& e, const fd_blend_params& p, int64_t n, const double* const* d_probs,
                   const uint8_t* present, double* d_fp, double* d_conf, uint8_t* d_dec, uint8_t* d_risk);

@@ -104,6 +104,10 @@ class fd_txn_batch(C.Structure):
 
 
 FD_TIMING_ALL, FD_TIMING_XGB, FD_TIMING_IFOREST, FD_TIMING_FEATURES, FD_TIMING_BLEND = -1, 0, 1, 2, 3
+FD_TIMING_ROUTE = 4
+FD_MAX_SHARDS = 64
+FD_ROUTE_RECORD_BYTES = 48
+FD_RESULT_RECORD_BYTES = 24
 FD_WINDOW_REDIS_COMPAT = 0
 FD_WINDOW_SLIDING = 1
 FD_RAW_FEATURES = 16
@@ -145,6 +149,10 @@ SIGNATURES = {
     "fd_features_host": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _vp, _vp]),
     "fd_score_batch_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, C.POINTER(_vp), _vp,
                                         C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fd_shard_of_host": (C.c_int, [_vp, _i64, _i32, _vp]),
+    "fd_route_partition_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _i32, _vp, _vp]),
+    "fd_score_records_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, _vp, _vp, _i64, _vp]),
+    "fd_route_scatter_results_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
     "fd_timing_read": (C.c_int, [_vp, C.c_int, _dp, C.POINTER(_i64)]),

@@ -66,7 +66,8 @@ class FraudEngine:
     def set_option(self, key: str, value: int) -> None:
         N.call("fd_engine_set_option", self._h, key.encode(), int(value))
 
-    def read_timing(self, kinds=(N.FD_TIMING_XGB, N.FD_TIMING_IFOREST, N.FD_TIMING_FEATURES, N.FD_TIMING_BLEND),
+    def read_timing(self, kinds=(N.FD_TIMING_XGB, N.FD_TIMING_IFOREST, N.FD_TIMING_FEATURES, N.FD_TIMING_BLEND,
+                                 N.FD_TIMING_ROUTE),
                     reset: bool = True):
         """-> {kind: (total kernel ms, timed launches)} since the last reset (then resets).
         With a single int `kinds`, returns just that (ms, launches) pair."""
@@ -187,6 +188,32 @@ class FraudEngine:
         N.call("fd_score_batch_device", self._h, C.byref(params), _ptr(sl), ext, _ptr(pres), C.byref(b), int(n),
                opt(vec_ptr), opt(model_probs_ptr), C.c_void_p(fp_ptr), opt(conf_ptr), opt(dec_ptr), opt(risk_ptr))
 
+    # ------------------------------------------------------------------ card-hash sharding (fdengine/sharding.py)
+    def route_partition_device(self, txn_ptrs: dict, n: int, n_shards: int, records_ptr: int, counts_ptr: int) -> None:
+        """Group one device-resident micro-batch by owner GPU: n records of FD_ROUTE_RECORD_BYTES at
+        records_ptr (owner-major, arrival order kept), n_shards int64 counts at counts_ptr."""
+        b = N.fd_txn_batch(*[int(txn_ptrs[f]) for f in N.TXN_FIELDS])
+        N.call("fd_route_partition_device", self._h, C.byref(b), int(n), int(n_shards),
+               C.c_void_p(records_ptr) if records_ptr else None, C.c_void_p(counts_ptr))
+
+    def score_records_device(self, params: N.fd_blend_params, slots: Sequence[int], records_ptr: int, n: int,
+                             results_ptr: int, present: Optional[Sequence[int]] = None) -> None:
+        """Owner side: features (this GPU's card state) -> forests -> blend over n received records;
+        n result records of FD_RESULT_RECORD_BYTES at results_ptr."""
+        M = params.n_models
+        sl = np.array(list(slots) + [-1] * (N.FD_MAX_MODELS - len(slots)), np.int32)
+        pres = np.array([1] * M if present is None else list(present), np.uint8)
+        N.call("fd_score_records_device", self._h, C.byref(params), _ptr(sl), _ptr(pres),
+               C.c_void_p(records_ptr) if records_ptr else None, int(n),
+               C.c_void_p(results_ptr) if results_ptr else None)
+
+    def route_scatter_results_device(self, results_ptr: int, n: int, fp_ptr: int, conf_ptr: int = 0,
+                                     dec_ptr: int = 0, risk_ptr: int = 0) -> None:
+        """Ingest side: put the n returned result records back in micro-batch order."""
+        opt = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        N.call("fd_route_scatter_results_device", self._h, opt(results_ptr), int(n), opt(fp_ptr), opt(conf_ptr),
+               opt(dec_ptr), opt(risk_ptr))
+
     # ------------------------------------------------------------------ blend
     @staticmethod
     def blend_params(weights: Sequence[float], conf_mult: Sequence[float], strategy: int = 0,
@@ -282,6 +309,14 @@ def pack_forest_binned_host(fa: ForestArrays):
            C.c_void_p(thr.ctypes.data), info.n_thresholds, C.c_void_p(off.ctypes.data), C.byref(info))
     del keep
     return blob.tobytes(), thr, off, info
+
+
+def shard_of(keys, n_shards: int) -> np.ndarray:
+    """Owner shard of each card key (host-only, no GPU): the partition fd_route_partition_device uses."""
+    k = np.ascontiguousarray(keys, np.uint64)
+    out = np.empty(len(k), np.int32)
+    N.call("fd_shard_of_host", _ptr(k), len(k), int(n_shards), _ptr(out))
+    return out
 
 
 def device_count() -> int:

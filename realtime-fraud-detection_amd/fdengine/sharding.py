@@ -1,0 +1,111 @@
+"""Card-hash sharded scoring across the GPUs of one node (BASELINE config 4).
+
+The reference keys all per-card work by user id — Kafka partition key and Flink keyBy
+(services/flink-jobs/.../FraudDetectionJob.java, WindowProcessor.java:45-64) — with the velocity state
+in one Redis (RedisService.java:178-207). Here GPU r of G owns the cards with
+shard_of(card_key, G) == r (fdengine.shard_of / fd_shard_of_host) and keeps their state resident in its
+HBM. Models (≈2 MB) and the merchant table are replicated.
+
+One micro-batch step, per rank (one process per GPU, torch.distributed: RCCL over xGMI on the GPU,
+gloo in the CPU tests):
+  1. fd_route_partition_device: group the ingested batch by owner (stable), 48-B records + counts;
+  2. all_to_all of the per-owner counts (G int64), then both count vectors to the host (one sync:
+     RCCL all-to-all needs host split sizes);
+  3. all_to_all of the records (uneven splits);
+  4. fd_score_records_device: features (this GPU's card state) -> XGBoost + IsolationForest -> blend;
+  5. all_to_all of the 24-B result records back (splits reversed);
+  6. fd_route_scatter_results_device: results in the ingest batch's original order.
+Records from one source keep their arrival order and all_to_all concatenates sources in rank order,
+so every card sees its transactions in (step, ingest rank, ingest index) order.
+
+The exchange logic is backend-agnostic: `EngineShardBackend` drives libfdengine.so (the product path);
+the CPU tests plug an oracle-backed backend into the same `ShardedScorer` to check the protocol.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .engine import FraudEngine, shard_of  # noqa: F401  (shard_of re-exported for callers)
+
+REC = N.FD_ROUTE_RECORD_BYTES
+RES = N.FD_RESULT_RECORD_BYTES
+
+
+class EngineShardBackend:
+    """Steps 1, 4 and 6 on one GPU through the C-ABI (device tensors in, device tensors out)."""
+
+    def __init__(self, eng: FraudEngine, params: N.fd_blend_params, slots: Sequence[int],
+                 present: Optional[Sequence[int]] = None):
+        import torch
+        self.torch = torch
+        self.eng, self.params, self.slots, self.present = eng, params, list(slots), present
+        self.device = torch.device("cuda", eng.device)
+
+    def partition(self, txns: dict, n: int, G: int):
+        t = self.torch
+        rec = t.empty((n, REC), dtype=t.uint8, device=self.device)
+        counts = t.empty(G, dtype=t.int64, device=self.device)
+        self.eng.route_partition_device({f: txns[f].data_ptr() for f in N.TXN_FIELDS}, n, G,
+                                        rec.data_ptr() if n else 0, counts.data_ptr())
+        return rec, counts
+
+    def score_records(self, rec, m: int):
+        t = self.torch
+        res = t.empty((m, RES), dtype=t.uint8, device=self.device)
+        if m:
+            self.eng.score_records_device(self.params, self.slots, rec.data_ptr(), m, res.data_ptr(), self.present)
+        return res
+
+    def scatter_results(self, res, n: int):
+        t = self.torch
+        fp = t.empty(n, dtype=t.float64, device=self.device)
+        conf = t.empty(n, dtype=t.float64, device=self.device)
+        dec = t.empty(n, dtype=t.uint8, device=self.device)
+        risk = t.empty(n, dtype=t.uint8, device=self.device)
+        if n:
+            self.eng.route_scatter_results_device(res.data_ptr(), n, fp.data_ptr(), conf.data_ptr(),
+                                                  dec.data_ptr(), risk.data_ptr())
+        return fp, conf, dec, risk
+
+
+class ShardedScorer:
+    """One rank's side of the sharded hot path. `world == 1` runs the same kernels with no collective."""
+
+    def __init__(self, backend, rank: int, world: int, group=None):
+        self.be, self.rank, self.world, self.group = backend, int(rank), int(world), group
+        self.last_counts = None  # (send, recv) split sizes of the last step, for diagnostics
+
+    def _a2a(self, out, inp, out_splits=None, in_splits=None):
+        import torch.distributed as dist
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+    def step(self, txns: dict, n: int):
+        """txns: field -> tensor (n rows) on the backend's device, in arrival order.
+        -> (fraud_prob f64, confidence f64, decision u8, risk u8) tensors in the same order."""
+        import torch
+        G = self.world
+        rec, counts = self.be.partition(txns, n, G)
+        if G == 1:
+            res = self.be.score_records(rec, n)
+            self.last_counts = ([n], [n])
+            return self.be.scatter_results(res, n)
+        recv_counts = torch.empty_like(counts)
+        self._a2a(recv_counts, counts)
+        both = torch.cat([counts, recv_counts]).cpu().tolist()
+        send, recv = [int(c) for c in both[:G]], [int(c) for c in both[G:]]
+        self.last_counts = (send, recv)
+        m = sum(recv)
+        inbox = torch.empty((m, REC), dtype=torch.uint8, device=rec.device)
+        self._a2a(inbox, rec, recv, send)
+        res = self.be.score_records(inbox, m)
+        back = torch.empty((n, RES), dtype=torch.uint8, device=rec.device)
+        self._a2a(back, res, send, recv)
+        return self.be.scatter_results(back, n)
+
+
+def owned_mask(keys, rank: int, world: int) -> np.ndarray:
+    """Which cards (e.g. user profiles to load) this rank owns."""
+    return shard_of(keys, world) == rank

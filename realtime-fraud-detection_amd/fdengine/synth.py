@@ -206,3 +206,110 @@ def isolation_forest(X_train: np.ndarray, n_estimators: int = 100, contamination
     m = IsolationForest(contamination=contamination, n_estimators=n_estimators, random_state=random_state)
     m.fit(X_train)
     return m
+
+
+# ------------------------------------------------------------------ hash-derived card populations
+# For the sharded configurations (BASELINE config 4: 100M cards over 8 GPUs) every rank needs the
+# attributes of the cards it owns and of the cards its own stream touches, without materialising the
+# whole population: card i's attributes are a pure function of (i, seed).
+_HM1 = np.uint64(0xff51afd7ed558ccd)
+_HM2 = np.uint64(0xc4ceb9fe1a85ec53)
+
+
+def _fmix64(k: np.ndarray) -> np.ndarray:
+    k = np.asarray(k, np.uint64).copy()
+    with np.errstate(over="ignore"):
+        k ^= k >> np.uint64(33)
+        k *= _HM1
+        k ^= k >> np.uint64(33)
+        k *= _HM2
+        k ^= k >> np.uint64(33)
+    return k
+
+
+def _u01(ids: np.ndarray, seed: int, lane: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        h = _fmix64(np.asarray(ids, np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+                    + np.uint64((seed * 131 + lane) * 0x632BE59BD9B4E019 % (1 << 64)))
+    return ((h >> np.uint64(11)).astype(np.float64) + 0.5) * (1.0 / (1 << 53))
+
+
+def card_keys(ids, seed: int = 42) -> np.ndarray:
+    """64-bit card key of card ids (stands in for hash64(user_id)); never 0."""
+    ids = np.asarray(ids, np.int64).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        return _fmix64(ids ^ np.uint64((seed * 0x2545F4914F6CDD1D) % (1 << 64))) | (np.uint64(1) << np.uint64(63))
+
+
+def card_attrs(ids, seed: int = 42) -> dict:
+    """Attributes of cards `ids` (int64 in [0, n_cards)) with the simulator's distributions
+    (simulator.py:212-238: avg amount LogNormal(4,1), 1-3 device fingerprints, account age)."""
+    from scipy.special import ndtri
+    ids = np.asarray(ids, np.int64).astype(np.uint64)
+    key = card_keys(ids, seed)
+    n_fp = 1 + np.floor(_u01(ids, seed, 1) * 3).astype(np.int64)
+    fps = np.stack([_fmix64(ids * np.uint64(4) + np.uint64(j + 1) + np.uint64(seed)) | (np.uint64(1) << np.uint64(63))
+                    for j in range(3)], axis=1)
+    fps[np.arange(3)[None, :] >= n_fp[:, None]] = 0
+    return {"key": key, "avg_amount": np.exp(4.0 + ndtri(_u01(ids, seed, 2))),
+            "account_age_days": np.floor(_u01(ids, seed, 3) * 730).astype(np.int32), "device_fp": fps}
+
+
+def merchants_table(n_merchants: int = 5000, seed: int = 42) -> dict:
+    return population(1, n_merchants, seed)["merchants"]
+
+
+def owned_cards(n_cards: int, rank: int, world: int, seed: int = 42, chunk: int = 1 << 23) -> dict:
+    """The cards GPU `rank` of `world` owns (fdengine.shard_of(key, world) == rank), with attributes."""
+    from .engine import shard_of
+    parts = []
+    for a in range(0, n_cards, chunk):
+        ids = np.arange(a, min(n_cards, a + chunk), dtype=np.int64)
+        if world > 1:
+            ids = ids[shard_of(card_keys(ids, seed), world) == rank]
+        parts.append(card_attrs(ids, seed))
+    return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+
+
+def txn_stream_cards(n_cards: int, merchants: dict, n: int, seed: int = 7, card_seed: int = 42,
+                     t0_ms: int = 1_757_030_400_000, rate_per_s: float = 1000.0,
+                     unknown_user_frac: float = 0.01, unknown_merchant_frac: float = 0.005) -> dict:
+    """txn_stream over a hash-derived population of n_cards (same per-transaction distributions)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    u = rng.integers(0, n_cards, n)
+    at = card_attrs(u, card_seed)
+    pop = {"users": {"key": at["key"], "avg_amount": at["avg_amount"], "device_fp": at["device_fp"],
+                     "txn_frequency": np.ones(n, np.int32)},
+           "merchants": merchants}
+    # draw the per-transaction fields with the user index being the identity over `at`
+    tx = _txn_stream_indexed(pop, np.arange(n), rng, t0_ms, rate_per_s, unknown_user_frac, unknown_merchant_frac)
+    tx["card_id"] = u  # population index of each transaction's card (unknown-user rows keep theirs)
+    return tx
+
+
+def _txn_stream_indexed(pop, u, rng, t0_ms, rate_per_s, unknown_user_frac, unknown_merchant_frac):
+    U, M = pop["users"], pop["merchants"]
+    n, nm = len(u), len(M["category"])
+    ts = t0_ms + np.floor(np.cumsum(rng.exponential(1000.0 / rate_per_s, n))).astype(np.int64)
+    key = U["key"][u].copy()
+    unknown = rng.random(n) < unknown_user_frac
+    key[unknown] = _nonzero_u64(rng, int(unknown.sum()))
+    merchant = rng.integers(0, nm, n).astype(np.int32)
+    merchant[rng.random(n) < unknown_merchant_frac] = -1
+    base = U["avg_amount"][u] * rng.normal(1.0, 0.3, n) * rng.normal(1.0, 0.2, n)
+    cents = np.maximum(100, np.rint(base * 100.0)).astype(np.int64)
+    roll = rng.random(n)
+    card_testing = roll < 0.02
+    takeover = (roll >= 0.02) & (roll < 0.03)
+    synthetic = (roll >= 0.03) & (roll < 0.035)
+    cents[card_testing] = np.rint(rng.uniform(1.0, 5.0, int(card_testing.sum())) * 100).astype(np.int64)
+    cents[synthetic] = np.rint(rng.uniform(1000.0, 5000.0, int(synthetic.sum())) * 100).astype(np.int64)
+    fp_pick = rng.integers(0, 3, n)
+    dfp = U["device_fp"][u, fp_pick]
+    first = U["device_fp"][u, 0]
+    dfp = np.where(dfp == 0, first, dfp)
+    dfp[takeover] = _nonzero_u64(rng, int(takeover.sum()))
+    ip_class = np.where(rng.random(n) < 0.05, 1, 2).astype(np.uint8)
+    return {"card_key": key, "ts_ms": ts, "amount_cents": cents, "merchant": merchant, "device_fp": dfp,
+            "ip_class": ip_class, "hour": np.full(n, 255, np.uint8), "weekend": np.full(n, 255, np.uint8),
+            "is_fraud": roll < 0.055}
