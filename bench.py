@@ -33,6 +33,7 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "realtime-fraud-detection_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+F32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA peak (MI355X_MICROARCH.md "Peak FP32 (matrix)")
 
 
 def log(*a):
@@ -165,6 +166,8 @@ class Config2:
 class Config3:
     name = "config3"
     dtype = "f32 (features f64, forests f32/f64, blend f64)"
+    with_lstm = False
+    seq_len = 10  # lstm_sequential sequence_length (ml/utils/config.py:152)
 
     def __init__(self, args, rank, dev, eng):
         import numpy as np
@@ -192,7 +195,16 @@ class Config3:
         eng.load_forest(0, self.xgb)
         eng.load_forest(1, self.ifm)
         self.names = ["xgboost_primary", "isolation_forest"]
-        w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
+        self.slots = [0, 1]
+        reg = {"xgboost_primary": 0.4, "isolation_forest": 0.05}
+        if self.with_lstm:
+            from fdengine import lstm as L
+            self.lw = L.random_weights(16, 128, 1, seed=14)
+            eng.load_lstm(self.lw)
+            self.names.append("lstm_sequential")
+            self.slots.append(N.FD_SLOT_LSTM)
+            reg["lstm_sequential"] = 0.25
+        w = S.normalized_weights(reg)
         self.weights = [w[n] for n in self.names]
         self.mults = [S.CONF_MULT[n] for n in self.names]
         self.params = fdengine.FraudEngine.blend_params(self.weights, self.mults)
@@ -202,7 +214,7 @@ class Config3:
         while cap < int(self.cards * 1.6):
             cap *= 2
         self.cap = cap
-        eng.state_init(cap, self.mode, self.K)
+        eng.state_init(cap, self.mode, self.K, seq_len=self.seq_len if self.with_lstm else 0)
         U, M = self.pop["users"], self.pop["merchants"]
         eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
         eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
@@ -215,7 +227,7 @@ class Config3:
         self.conf = torch.empty(B, dtype=torch.float64, device=dev)
         self.dec = torch.empty(B, dtype=torch.uint8, device=dev)
         self.risk = torch.empty(B, dtype=torch.uint8, device=dev)
-        self.mp = torch.empty((2, B), dtype=torch.float64, device=dev)
+        self.mp = torch.empty((len(self.names), B), dtype=torch.float64, device=dev)
         self.vec = torch.empty((B, 64), dtype=torch.float32, device=dev)
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
@@ -232,7 +244,7 @@ class Config3:
         if b >= self.n_batches:
             raise RuntimeError("stream exhausted: raise n_batches")
         self.next_batch += 1
-        self.eng.score_batch_device(self.params, [0, 1], self._ptrs(b), self.B, self.fp.data_ptr(),
+        self.eng.score_batch_device(self.params, self.slots, self._ptrs(b), self.B, self.fp.data_ptr(),
                                     self.conf.data_ptr(), self.dec.data_ptr(), self.risk.data_ptr(),
                                     vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
 
@@ -253,16 +265,24 @@ class Config3:
         part = {f: self.tx[f][:self.B] for f in self.N.TXN_FIELDS}
         self.step(0)
         self.torch.cuda.synchronize()
-        _, rvec = o.run(part, want_raw=False)
+        rraw, rvec = o.run(part, want_raw=self.with_lstm)
         del o
         V = self.vec.cpu().numpy()
         px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
         pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
-        fp, _, dec, _ = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults)
+        cols = [px.astype(np.float64), pi]
+        out = {}
+        if self.with_lstm:
+            from oracle import lstm_ref
+            pl = lstm_ref.lstm_forward(self.lw, lstm_ref.SequenceState(self.seq_len).run(part["card_key"], rraw))
+            cols.append(pl)
+            out["lstm_max_abs_prob_diff"] = float(np.abs(self.mp[2].cpu().numpy() - pl).max())
+        fp, _, dec, _ = oracle.blend_weighted(np.stack(cols), self.weights, self.mults)
         vec_diff = int((V != rvec).sum())
-        return {"vector_mismatched_elements": vec_diff,
-                "max_abs_prob_diff": float(np.abs(self.fp.cpu().numpy() - fp).max()),
-                "decision_mismatches": int((self.dec.cpu().numpy() != dec).sum())}
+        out.update({"vector_mismatched_elements": vec_diff,
+                    "max_abs_prob_diff": float(np.abs(self.fp.cpu().numpy() - fp).max()),
+                    "decision_mismatches": int((self.dec.cpu().numpy() != dec).sum())})
+        return out
 
     def roofline(self, timing):
         N = self.N
@@ -281,7 +301,7 @@ class Config3:
         N = self.N
         names = {N.FD_TIMING_XGB: "xgboost_forest", N.FD_TIMING_IFOREST: "iforest_forest",
                  N.FD_TIMING_FEATURES: "features (assign+process)", N.FD_TIMING_BLEND: "blend",
-                 N.FD_TIMING_ROUTE: "route_partition (count+scan+scatter)"}
+                 N.FD_TIMING_ROUTE: "route_partition (count+scan+scatter)", N.FD_TIMING_LSTM: "lstm_head"}
         return {names[k]: round(ms / max(1, c) * 1e3, 3) for k, (ms, c) in timing.items() if c}
 
     def config(self, world):
@@ -316,6 +336,69 @@ class Config3:
                 "sample": f"first {done} txns of the config-3 stream through the oracle chain (features C "
                           f"single-threaded + XGBoost + IsolationForest + blend, {th} OpenMP threads), "
                           f"{dt:.2f} s, CPU: {cpu_model()}"}
+
+
+# --------------------------------------------------------------------------------------- config 5
+class Config5(Config3):
+    """BASELINE configs[4]: the ensemble with the LSTM sequence head on the matrix cores, latency-bound
+    1k-transaction micro-batches: card-state features (+ each card's last 10 events) -> XGBoost 500x8
+    + IsolationForest 100 (main stream) || LSTM(128) over the card histories (f32 MFMA, second stream)
+    -> blend/decision. p99 micro-batch latency is the headline here."""
+    name = "config5"
+    with_lstm = True
+
+    def roofline(self, timing):
+        N = self.N
+        ms, launches = timing[N.FD_TIMING_LSTM]
+        avg = (ms / 1e3) / max(1, launches)
+        H, I, T = 128, 16, self.seq_len
+        flops = self.B * T * 2 * 4 * H * (I + H) + self.B * 2 * H  # gates GEMMs + dense head
+        achieved = flops / avg / 1e12
+        return {"bound": "mfma", "achieved": round(achieved, 4), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 6), "traffic": pmc_traffic(self.name, self.B),
+                "kernel": "lstm_kernel (v_mfma_f32_16x16x4_f32, 16 txn x 512 gates per workgroup)",
+                "kernel_avg_us": round(avg * 1e6, 3), "flops_per_launch": flops, "flops_per_txn": flops // self.B,
+                "workgroups": (self.B + 15) // 16,
+                "note": "latency-bound: a 1k batch fills (B/16) of 256 CUs; f32 MFMA = reference fp32 precision"}
+
+    def config(self, world):
+        c = super().config(world)
+        c["workload"] = ("config5: card-state features (sliding windows + last-10-event history) -> XGBoost 500x8 "
+                         "+ IsolationForest 100 || LSTM(128) head on f32 MFMA -> blend/decision, latency-bound "
+                         "1k-txn micro-batches")
+        c["lstm"] = {"hidden": 128, "seq_len": self.seq_len, "input": 16, "head": "dense(1)+sigmoid"}
+        return c
+
+    def cpu_baseline(self, seconds):
+        """Oracle chain incl. the LSTM head (PyTorch fp32 CPU forward) on the first txns of the stream."""
+        import torch
+
+        import oracle
+        from oracle import lstm_ref
+        from oracle.features_c import OracleFeatureState
+        np = self.np
+        th = cpu_threads()
+        torch.set_num_threads(th)
+        U, M = self.pop["users"], self.pop["merchants"]
+        o = OracleFeatureState(self.cap, self.mode, self.K)
+        o.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        o.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        hist = lstm_ref.SequenceState(self.seq_len)
+        chunk = 4096
+        done, a = 0, time.perf_counter()
+        while time.perf_counter() - a < seconds and done + chunk <= len(self.tx["ts_ms"]):
+            part = {f: self.tx[f][done:done + chunk] for f in self.N.TXN_FIELDS}
+            raw, V = o.run(part, want_raw=True)
+            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=th)
+            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=th)
+            pl = lstm_ref.lstm_forward(self.lw, hist.run(part["card_key"], raw))
+            oracle.blend_weighted(np.stack([px.astype(np.float64), pi, pl]), self.weights, self.mults, nthreads=th)
+            done += chunk
+        dt = time.perf_counter() - a
+        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
+                "sample": f"first {done} txns of the config-5 stream through the oracle chain (features C + card "
+                          f"history single-threaded, XGBoost + IsolationForest + blend {th} OpenMP threads, LSTM "
+                          f"torch fp32 CPU {th} threads), {dt:.2f} s, CPU: {cpu_model()}"}
 
 
 # --------------------------------------------------------------------------------------- config 4
@@ -472,7 +555,7 @@ class Config4(Config3):
                           f"{dt:.2f} s, CPU: {cpu_model()}"}
 
 
-WORKLOADS = {"config2": Config2, "config3": Config3, "config4": Config4}
+WORKLOADS = {"config2": Config2, "config3": Config3, "config4": Config4, "config5": Config5}
 
 
 def main():
@@ -481,7 +564,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
-    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--batch", type=int, default=None, help="micro-batch (default 64k; config5: 1k)")
     ap.add_argument("--trees", type=int, default=500)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--features", type=int, default=50)
@@ -494,6 +577,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=200)
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 1024 if args.workload == "config5" else 65536
     if args.cards is None:
         args.cards = 100_000_000 if args.workload == "config4" else 10_000_000
 

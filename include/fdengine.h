@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 3
+#define FD_ABI_VERSION 4
 
 enum fd_status {
   FD_OK = 0,
@@ -173,10 +173,13 @@ enum fd_window_mode {
 };
 #define FD_RAW_FEATURES 16  /* bridged Flink features per txn (column order: DESIGN.md "Features") */
 #define FD_VECTOR_WIDTH 64  /* EnsemblePredictor._prepare_features width (ml/models/ensemble_predictor.py:241) */
+#define FD_MAX_SEQ_LEN 16
 typedef struct {
   int64_t capacity;    /* card slots (rounded up to a power of two; keep >= 2x the cards expected) */
   int32_t window_mode; /* enum fd_window_mode */
   int32_t ring_k;      /* events kept per card in sliding mode (1..64) */
+  int32_t seq_len;     /* events of per-card history kept for the LSTM head (0 = off, <= 16;
+                          lstm_sequential sequence_length = 10, ml/utils/config.py:152) */
 } fd_state_params;
 int fd_state_init(fd_engine* eng, const fd_state_params* params);
 int fd_state_clear(fd_engine* eng);
@@ -213,6 +216,38 @@ typedef struct {
    vectors (n x 64 f32) and optionally the bridged raw features (n x FD_RAW_FEATURES f64). */
 int fd_features_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* d_vectors, double* d_raw);
 int fd_features_host(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* vectors, double* raw);
+
+/* ---------------------------------------------------------------- LSTM sequence head (a10) */
+/* Replaces _load_tensorflow_model / _predict_tensorflow (ml/models/model_manager.py:162-165, 313-319)
+   for lstm_sequential (ml/utils/config.py:145-157). Model: 1-layer LSTM(hidden = 128) over a sequence
+   of per-event inputs (input_size <= 16), gates in Keras / PyTorch order i, f, g, o, then a dense head:
+   n_out = 1 -> sigmoid(z), n_out = 2 -> softmax(z)[1] (_predict_tensorflow takes [:, 1] when the output
+   has 2 columns, else flattens). Weights in PyTorch layout, f32 (the host converts Keras kernels):
+   w_ih [4H x input_size], w_hh [4H x H], b_ih / b_hh [4H] (either may be NULL), w_out [n_out x H],
+   b_out [n_out]. Computed in f32 on the matrix cores. */
+typedef struct {
+  int32_t input_size;
+  int32_t hidden;
+  int32_t n_out;
+  const float* w_ih;
+  const float* w_hh;
+  const float* b_ih;
+  const float* b_hh;
+  const float* w_out;
+  const float* b_out;
+} fd_lstm_params;
+int fd_load_lstm(fd_engine* eng, const fd_lstm_params* params);
+int fd_unload_lstm(fd_engine* eng);
+/* d_seq: n x T x 16 f32 (events oldest -> newest, inputs beyond input_size ignored); d_prob: n f64 */
+int fd_lstm_predict_device(fd_engine* eng, const float* d_seq, int64_t n, int32_t T, double* d_prob);
+int fd_lstm_predict_host(fd_engine* eng, const float* seq, int64_t n, int32_t T, double* prob);
+/* In fd_score_batch_device / fd_score_records_device, a model whose slot is FD_SLOT_LSTM is the LSTM head
+   over each transaction's card history (the last seq_len events including itself, fd_state_params.seq_len
+   > 0); it runs on a second stream concurrently with the forests. fd_features_seq_device also returns
+   those sequences (n x seq_len x 16 f32). */
+#define FD_SLOT_LSTM 64
+int fd_features_seq_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* d_vectors, double* d_raw,
+                           float* d_seq);
 
 /* ---------------------------------------------------------------- batched scoring */
 /* Replaces the per-transaction loop of /batch-predict (ml/main.py:235-249) for prepared scoring
@@ -273,7 +308,7 @@ int fd_route_scatter_results_device(fd_engine* eng, const void* d_results, int64
    launch stream around each kernel. fd_timing_read synchronises and returns the summed time (ms) and
    count of the timed launches of `kind` (FD_TIMING_ALL: every kind) since the last fd_timing_reset. */
 enum fd_timing_kind { FD_TIMING_ALL = -1, FD_TIMING_XGB = 0, FD_TIMING_IFOREST = 1, FD_TIMING_FEATURES = 2,
-                      FD_TIMING_BLEND = 3, FD_TIMING_ROUTE = 4 };
+                      FD_TIMING_BLEND = 3, FD_TIMING_ROUTE = 4, FD_TIMING_LSTM = 5 };
 int fd_engine_set_timing(fd_engine* eng, int enable);
 /* Engine tuning knobs (for A/B measurement; defaults are the tuned choices):
      "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel

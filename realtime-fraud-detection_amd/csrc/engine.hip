@@ -61,10 +61,13 @@ static fd::PackedForest& slot_of(Engine& e, int slot) {
   return e.forests[slot];
 }
 
-// Score the same feature matrix with every forest model, then blend (all on e.stream).
+// Score the same feature matrix with every forest model, then blend (all on e.stream). A model in slot
+// FD_SLOT_LSTM runs the LSTM head over d_seq (n x T x 16) on the auxiliary stream, forked after
+// everything already queued on e.stream (the feature kernel that wrote d_seq) and joined before the blend.
 static void score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slots, const double* const* ext,
                          const uint8_t* present, const float* dX, int64_t n, int32_t ld, double* dMP,
-                         double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk) {
+                         double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk, const float* d_seq = nullptr,
+                         int T = 0) {
   FD_REQUIRE(p.n_models > 0 && p.n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "n_models out of range");
   FD_REQUIRE(slots != nullptr && dfp != nullptr, FD_ERR_INVALID_ARG, "null slots/output");
   if (n == 0) return;
@@ -74,8 +77,26 @@ static void score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     dMP = e.scratch_probs.as<double>();
   }
   const double* cols[FD_MAX_MODELS] = {};
+  bool joined = true;
+  for (int m = 0; m < M; ++m) {  // the LSTM first, so it overlaps the forests
+    if ((present && !present[m]) || slots[m] != FD_SLOT_LSTM) continue;
+    FD_REQUIRE(d_seq != nullptr, FD_ERR_INVALID_ARG,
+               "the LSTM head needs card-history sequences (fd_score_batch_device with seq_len > 0)");
+    if (!e.aux_stream) {
+      FD_HIP(hipStreamCreateWithFlags(&e.aux_stream, hipStreamNonBlocking));
+      FD_HIP(hipEventCreateWithFlags(&e.fork_ev, hipEventDisableTiming));
+      FD_HIP(hipEventCreateWithFlags(&e.join_ev, hipEventDisableTiming));
+    }
+    FD_HIP(hipEventRecord(e.fork_ev, e.stream));
+    FD_HIP(hipStreamWaitEvent(e.aux_stream, e.fork_ev, 0));
+    double* col = dMP + (size_t)m * n;
+    fd::launch_lstm(e, e.aux_stream, d_seq, n, T, col);
+    FD_HIP(hipEventRecord(e.join_ev, e.aux_stream));
+    joined = false;
+    cols[m] = col;
+  }
   for (int m = 0; m < M; ++m) {
-    if (present && !present[m]) continue;
+    if ((present && !present[m]) || slots[m] == FD_SLOT_LSTM) continue;
     double* col = dMP + (size_t)m * n;
     if (slots[m] >= 0) {
       const fd::PackedForest& pf = slot_of(e, slots[m]);
@@ -89,7 +110,21 @@ static void score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
       cols[m] = col;
     }
   }
+  if (!joined) FD_HIP(hipStreamWaitEvent(e.stream, e.join_ev, 0));
   fd::launch_blend(e, p, n, cols, present, dfp, dconf, ddec, drisk);
+}
+
+// engine scratch for the fused path's LSTM input sequences, when a present model is the LSTM head
+static float* lstm_seq_buffer(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
+                              int64_t n) {
+  bool want = false;
+  for (int m = 0; m < p.n_models && m < FD_MAX_MODELS; ++m)
+    want = want || (slots && slots[m] == FD_SLOT_LSTM && !(present && !present[m]));
+  if (!want) return nullptr;
+  FD_REQUIRE(e.state.ready && e.state.S > 0, FD_ERR_INVALID_ARG,
+             "the LSTM head needs card history: fd_state_params.seq_len > 0");
+  e.seq_buf.ensure((size_t)n * e.state.S * fd::kSeqInput * sizeof(float));
+  return e.seq_buf.as<float>();
 }
 
 extern "C" {
@@ -150,7 +185,15 @@ int fd_engine_destroy(fd_engine* eng) {
   e.stage_ext.release();
   e.feat_vec.release();
   e.feat_in.release();
-  for (auto* b : {&e.route_blk, &e.route_soa, &e.route_out, &e.route_err}) b->release();
+  for (auto* b : {&e.route_blk, &e.route_soa, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.bias,
+                  &e.lstm.wout, &e.lstm.bout, &e.state.seq})
+    b->release();
+  if (e.aux_stream) {
+    (void)hipStreamSynchronize(e.aux_stream);
+    (void)hipStreamDestroy(e.aux_stream);
+    (void)hipEventDestroy(e.fork_ev);
+    (void)hipEventDestroy(e.join_ev);
+  }
   for (auto* b : {&e.state.headers, &e.state.fps, &e.state.ring, &e.state.merchants, &e.state.slot,
                   &e.state.next, &e.state.err})
     b->release();
@@ -181,6 +224,7 @@ int fd_engine_sync(fd_engine* eng) {
   FD_API_BEGIN
   Engine& e = E(eng);
   FD_HIP(hipStreamSynchronize(e.stream));
+  if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
   fd::route_check(e);
   FD_API_END
 }
@@ -518,9 +562,62 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
     e.feat_vec.ensure((size_t)n * FD_VECTOR_WIDTH * 4);
     vec = e.feat_vec.as<float>();
   }
-  fd::launch_features(e, *txns, n, vec, nullptr);
+  float* seq = lstm_seq_buffer(e, *params, slots, present, n);
+  fd::launch_features(e, *txns, n, vec, nullptr, seq);
   score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
-               d_confidence, d_decision, d_risk);
+               d_confidence, d_decision, d_risk, seq, e.state.S);
+  FD_API_END
+}
+
+int fd_load_lstm(fd_engine* eng, const fd_lstm_params* params) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
+  FD_HIP(hipStreamSynchronize(e.stream));
+  if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
+  fd::load_lstm(e, *params);
+  FD_API_END
+}
+
+int fd_unload_lstm(fd_engine* eng) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_HIP(hipStreamSynchronize(e.stream));
+  if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
+  for (auto* b : {&e.lstm.wpk, &e.lstm.bias, &e.lstm.wout, &e.lstm.bout}) b->release();
+  e.lstm.loaded = false;
+  FD_API_END
+}
+
+int fd_lstm_predict_device(fd_engine* eng, const float* d_seq, int64_t n, int32_t T, double* d_prob) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::launch_lstm(e, e.stream, d_seq, n, T, d_prob);
+  FD_API_END
+}
+
+int fd_lstm_predict_host(fd_engine* eng, const float* seq, int64_t n, int32_t T, double* prob) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(n >= 0 && T >= 1 && T <= FD_MAX_SEQ_LEN, FD_ERR_INVALID_ARG, "bad arguments");
+  if (n == 0) return FD_OK;
+  FD_REQUIRE(seq && prob, FD_ERR_INVALID_ARG, "null sequence / output");
+  const size_t sb = (size_t)n * T * fd::kSeqInput * sizeof(float);
+  e.stage_in.ensure(sb);
+  e.stage_out0.ensure((size_t)n * sizeof(double));
+  FD_HIP(hipMemcpyAsync(e.stage_in.ptr, seq, sb, hipMemcpyHostToDevice, e.stream));
+  fd::launch_lstm(e, e.stream, e.stage_in.as<float>(), n, T, e.stage_out0.as<double>());
+  FD_HIP(hipMemcpyAsync(prob, e.stage_out0.ptr, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, e.stream));
+  FD_HIP(hipStreamSynchronize(e.stream));
+  FD_API_END
+}
+
+int fd_features_seq_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* d_vectors, double* d_raw,
+                           float* d_seq) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
+  fd::launch_features(e, *txns, n, d_vectors, d_raw, d_seq);
   FD_API_END
 }
 
@@ -548,7 +645,7 @@ int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const
   FD_REQUIRE(params && slots && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   for (int m = 0; m < params->n_models && m < FD_MAX_MODELS; ++m)
     FD_REQUIRE(slots[m] >= 0 || (present && !present[m]), FD_ERR_INVALID_ARG,
-               "routed scoring needs every present model in a forest slot");
+               "routed scoring needs every present model in a forest slot or FD_SLOT_LSTM");
   if (n == 0) return FD_OK;
   unsigned* seq = nullptr;
   const fd_txn_batch t = fd::launch_route_unpack(e, d_records, n, &seq);
@@ -558,9 +655,10 @@ int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const
   double* conf = fp + n;
   uint8_t* dec = reinterpret_cast<uint8_t*>(conf + n);
   uint8_t* risk = dec + n;
-  fd::launch_features(e, t, n, e.feat_vec.as<float>(), nullptr);
+  float* sq = lstm_seq_buffer(e, *params, slots, present, n);
+  fd::launch_features(e, t, n, e.feat_vec.as<float>(), nullptr, sq);
   score_matrix(e, *params, slots, nullptr, present, e.feat_vec.as<float>(), n, FD_VECTOR_WIDTH, nullptr, fp, conf,
-               dec, risk);
+               dec, risk, sq, e.state.S);
   fd::launch_result_pack(e, fp, conf, dec, risk, seq, n, d_results);
   FD_API_END
 }

@@ -19,6 +19,8 @@ constexpr int kMaxFeatures = 64;  // model columns held in LDS ([feature][kTile]
 constexpr int kMaxDepth = 10;     // deepest tree the repacker accepts
 constexpr size_t kLdsBudget = 160 * 1024;  // LDS per CU (one workgroup per CU at 64k batches)
 constexpr int kMaxBins = 65534;   // distinct thresholds per feature in the binned layout
+constexpr int kSeqInput = 16;     // LSTM per-event input width (the bridged raw features)
+constexpr int kLstmHidden = 128;  // lstm_sequential hidden_units (ml/utils/config.py:152-156)
 
 struct Error : std::runtime_error {
   int code;
@@ -106,15 +108,23 @@ struct __attribute__((aligned(8))) ResultRecord {
   unsigned short pad;
 };
 
+// LSTM head (lstm.hip): B operands packed per wave/gate/k-step/lane, summed biases, dense head
+struct LstmModel {
+  bool loaded = false;
+  int input_size = 0, n_out = 0;
+  DeviceBuffer wpk, bias, wout, bout;
+};
+
 // HBM-resident keyed card state (features.hip)
 struct CardStore {
   bool ready = false;
   int64_t cap = 0;   // slots (power of two)
   int mode = 0;      // fd_window_mode
   int K = 1;         // ring events per card (sliding)
+  int S = 0;         // LSTM history events per card (0 = off)
   unsigned epoch = 0;
   int64_t n_merchants = 0;
-  DeviceBuffer headers, fps, ring, merchants, slot, next, err;
+  DeviceBuffer headers, fps, ring, merchants, slot, next, err, seq;
 };
 
 struct Engine {
@@ -123,6 +133,10 @@ struct Engine {
   hipStream_t stream = nullptr;
   PackedForest forests[kMaxSlots];
   CardStore state;
+  LstmModel lstm;
+  hipStream_t aux_stream = nullptr;            // LSTM head runs here, concurrent with the forests
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  DeviceBuffer seq_buf;                        // per-txn LSTM input sequences of the fused path
   DeviceBuffer feat_vec, feat_in;  // host-API / fused-pipeline staging for features
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
@@ -167,7 +181,8 @@ void state_clear(Engine& e);
 int64_t state_count(Engine& e);
 void load_users(Engine& e, const fd_users& u);
 void load_merchants(Engine& e, const fd_merchants& m);
-void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw);
+void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw,
+                     float* d_seq = nullptr);
 void features_check(Engine& e);
 // route.hip
 unsigned shard_of_host(unsigned long long key, unsigned G);
@@ -178,6 +193,9 @@ void launch_result_pack(Engine& e, const double* fp, const double* conf, const u
 void launch_result_scatter(Engine& e, const void* d_results, int64_t n, double* fp, double* conf, uint8_t* dec,
                            uint8_t* risk);
 void route_check(Engine& e);
+// lstm.hip
+void load_lstm(Engine& e, const fd_lstm_params& p);
+void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, int T, double* d_prob);
 // blend.hip
 void launch_blend(Engine& e, const fd_blend_params& p, int64_t n, const double* const* d_probs,
                   const uint8_t* present, double* d_fp, double* d_conf, uint8_t* d_dec, uint8_t* d_risk);

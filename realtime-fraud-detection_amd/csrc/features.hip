@@ -38,7 +38,7 @@ struct __attribute__((aligned(16))) CardHeader {  // 64 B: one card's header, Ao
   int ring_head;            // sliding: next write position
   double avg;               // profile: avg_transaction_amount (NaN = null)
   int age;                  // profile: account_age_days
-  unsigned flags;           // bit 0: has a user profile
+  unsigned flags;           // bit 0: has a user profile; bits 8-15 seq events held; bits 16-23 seq write pos
 };
 static_assert(sizeof(CardHeader) == 64, "CardHeader must be 64 B");
 
@@ -188,6 +188,14 @@ __device__ void write_vector(const double* r, float* __restrict__ out) {
   for (; k < FD_VECTOR_WIDTH; ++k) out[k] = 0.f;
 }
 
+// per-event LSTM input: the bridged raw feature, NaN (null) -> 0, then sign(x) * log1p(|x|) in f64,
+// stored f32 (DESIGN.md "LSTM head"). Mirrors oracle/lstm_ref.py event_inputs.
+__device__ __forceinline__ float seq_input(double x) {
+  if (isnan(x)) return 0.f;
+  const double a = log1p(fabs(x));
+  return (float)(x < 0 ? -a : a);
+}
+
 struct TxnArgs {
   const unsigned long long* key;
   const long long* ts;
@@ -204,7 +212,8 @@ __global__ void __launch_bounds__(256) feat_process_kernel(CardHeader* H, const 
                                                            int mode, int K, int64_t n, TxnArgs t,
                                                            const unsigned* slot, const int* next,
                                                            float* __restrict__ vec_out,
-                                                           double* __restrict__ raw_out) {
+                                                           double* __restrict__ raw_out, float* seq_ring,
+                                                           int S, float* __restrict__ seq_out) {
 #pragma clang fp contract(off)
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -215,7 +224,10 @@ __global__ void __launch_bounds__(256) feat_process_kernel(CardHeader* H, const 
   // card state in registers for the whole list
   int cnt = h->cnt, has_ts = h->has_ts, ring_n = h->ring_n, ring_head = h->ring_head;
   long long last_ts = h->last_ts, sum_cents = h->sum_cents;
-  const bool has_user = (h->flags & 1u) != 0u;
+  unsigned flags = h->flags;
+  const bool has_user = (flags & 1u) != 0u;
+  int seq_n = (int)((flags >> 8) & 0xffu), seq_head = (int)((flags >> 16) & 0xffu);
+  float* sr = S ? seq_ring + (size_t)s * S * kSeqInput : nullptr;
   const double uavg_raw = h->avg;
   const int uage = h->age;
   const unsigned long long fp0 = fps[(size_t)s * 4], fp1 = fps[(size_t)s * 4 + 1], fp2 = fps[(size_t)s * 4 + 2];
@@ -305,7 +317,30 @@ __global__ void __launch_bounds__(256) feat_process_kernel(CardHeader* H, const 
       for (int c = 0; c < FD_RAW_FEATURES; ++c) ro[c] = r[c];
     }
     write_vector(r, vec_out + (size_t)best * FD_VECTOR_WIDTH);
+    if (S) {  // LSTM head input: this event appended to the card's history, last S events emitted
+      float* slot_ev = sr + (size_t)seq_head * kSeqInput;
+#pragma unroll
+      for (int c = 0; c < kSeqInput; ++c) slot_ev[c] = seq_input(r[c]);
+      seq_head = (seq_head + 1 == S) ? 0 : seq_head + 1;
+      if (seq_n < S) ++seq_n;
+      if (seq_out) {  // oldest -> newest, left-padded with zero events (Keras pad_sequences 'pre')
+        float* so = seq_out + (size_t)best * S * kSeqInput;
+        const int pad = S - seq_n;
+        for (int q = 0; q < S; ++q) {
+          float4* dst = reinterpret_cast<float4*>(so + (size_t)q * kSeqInput);
+          if (q < pad) {
+            for (int c = 0; c < kSeqInput / 4; ++c) dst[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+          } else {
+            int src = seq_head - seq_n + (q - pad);
+            if (src < 0) src += S;
+            const float4* sp = reinterpret_cast<const float4*>(sr + (size_t)src * kSeqInput);
+            for (int c = 0; c < kSeqInput / 4; ++c) dst[c] = sp[c];
+          }
+        }
+      }
+    }
   }
+  h->flags = (flags & 0xffu) | ((unsigned)seq_n << 8) | ((unsigned)seq_head << 16);
   h->cnt = cnt;
   h->has_ts = has_ts;
   h->ring_n = ring_n;
@@ -331,6 +366,7 @@ void state_init(Engine& e, const fd_state_params& p) {
   FD_REQUIRE(p.window_mode == FD_WINDOW_REDIS_COMPAT || p.window_mode == FD_WINDOW_SLIDING, FD_ERR_INVALID_ARG,
              "unknown window_mode");
   FD_REQUIRE(p.ring_k >= 1 && p.ring_k <= 64, FD_ERR_INVALID_ARG, "ring_k must be in [1, 64]");
+  FD_REQUIRE(p.seq_len >= 0 && p.seq_len <= FD_MAX_SEQ_LEN, FD_ERR_INVALID_ARG, "seq_len must be in [0, 16]");
   int64_t cap = 1;
   while (cap < p.capacity) cap <<= 1;
   CardStore& st = e.state;
@@ -340,6 +376,8 @@ void state_init(Engine& e, const fd_state_params& p) {
   st.headers.ensure((size_t)cap * sizeof(CardHeader));
   st.fps.ensure((size_t)cap * 4 * sizeof(unsigned long long));
   st.ring.ensure((size_t)cap * st.K * sizeof(RingEvent));
+  st.S = p.seq_len;
+  if (st.S) st.seq.ensure((size_t)cap * st.S * kSeqInput * sizeof(float));
   st.err.ensure(16);
   st.ready = true;
   state_clear(e);
@@ -414,10 +452,11 @@ void load_merchants(Engine& e, const fd_merchants& m) {
   st.n_merchants = m.n;
 }
 
-void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw) {
+void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw, float* d_seq) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
   FD_REQUIRE(d_vec != nullptr, FD_ERR_INVALID_ARG, "null vector output");
+  FD_REQUIRE(d_seq == nullptr || st.S > 0, FD_ERR_INVALID_ARG, "sequence output needs fd_state_params.seq_len > 0");
   FD_REQUIRE(n >= 0 && n < (1ll << 31), FD_ERR_INVALID_ARG, "batch size out of range");
   if (n == 0) return;
   FD_REQUIRE(t.card_key && t.ts_ms && t.amount_cents && t.merchant && t.device_fp && t.ip_class && t.hour &&
@@ -439,7 +478,7 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
   hipLaunchKernelGGL(feat_process_kernel, dim3(grid_for(n)), dim3(256), 0, e.stream, st.headers.as<CardHeader>(),
                      st.fps.as<const unsigned long long>(), st.ring.as<RingEvent>(), st.merchants.as<const Merchant>(),
                      (int)st.n_merchants, st.mode, st.K, n, a, st.slot.as<const unsigned>(), st.next.as<const int>(),
-                     d_vec, d_raw);
+                     d_vec, d_raw, st.S ? st.seq.as<float>() : nullptr, st.S, d_seq);
   FD_HIP(hipGetLastError());
   if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
 }

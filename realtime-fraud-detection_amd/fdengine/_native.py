@@ -85,7 +85,13 @@ class fd_pack_info(C.Structure):
 
 
 class fd_state_params(C.Structure):
-    _fields_ = [("capacity", C.c_int64), ("window_mode", C.c_int32), ("ring_k", C.c_int32)]
+    _fields_ = [("capacity", C.c_int64), ("window_mode", C.c_int32), ("ring_k", C.c_int32), ("seq_len", C.c_int32)]
+
+
+class fd_lstm_params(C.Structure):
+    _fields_ = [("input_size", C.c_int32), ("hidden", C.c_int32), ("n_out", C.c_int32), ("w_ih", C.c_void_p),
+                ("w_hh", C.c_void_p), ("b_ih", C.c_void_p), ("b_hh", C.c_void_p), ("w_out", C.c_void_p),
+                ("b_out", C.c_void_p)]
 
 
 class fd_users(C.Structure):
@@ -105,6 +111,10 @@ class fd_txn_batch(C.Structure):
 
 FD_TIMING_ALL, FD_TIMING_XGB, FD_TIMING_IFOREST, FD_TIMING_FEATURES, FD_TIMING_BLEND = -1, 0, 1, 2, 3
 FD_TIMING_ROUTE = 4
+FD_TIMING_LSTM = 5
+FD_MAX_SEQ_LEN = 16
+FD_SLOT_LSTM = 64
+FD_SEQ_INPUT = 16
 FD_MAX_SHARDS = 64
 FD_ROUTE_RECORD_BYTES = 48
 FD_RESULT_RECORD_BYTES = 24
@@ -149,6 +159,11 @@ SIGNATURES = {
     "fd_features_host": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _vp, _vp]),
     "fd_score_batch_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, C.POINTER(_vp), _vp,
                                         C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fd_load_lstm": (C.c_int, [_vp, C.POINTER(fd_lstm_params)]),
+    "fd_unload_lstm": (C.c_int, [_vp]),
+    "fd_lstm_predict_device": (C.c_int, [_vp, _vp, _i64, _i32, _vp]),
+    "fd_lstm_predict_host": (C.c_int, [_vp, _vp, _i64, _i32, _vp]),
+    "fd_features_seq_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp]),
     "fd_shard_of_host": (C.c_int, [_vp, _i64, _i32, _vp]),
     "fd_route_partition_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _i32, _vp, _vp]),
     "fd_score_records_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, _vp, _vp, _i64, _vp]),

@@ -67,7 +67,7 @@ class FraudEngine:
         N.call("fd_engine_set_option", self._h, key.encode(), int(value))
 
     def read_timing(self, kinds=(N.FD_TIMING_XGB, N.FD_TIMING_IFOREST, N.FD_TIMING_FEATURES, N.FD_TIMING_BLEND,
-                                 N.FD_TIMING_ROUTE),
+                                 N.FD_TIMING_ROUTE, N.FD_TIMING_LSTM),
                     reset: bool = True):
         """-> {kind: (total kernel ms, timed launches)} since the last reset (then resets).
         With a single int `kinds`, returns just that (ms, launches) pair."""
@@ -129,8 +129,11 @@ class FraudEngine:
     _TXN_DTYPES = {"card_key": np.uint64, "ts_ms": np.int64, "amount_cents": np.int64, "merchant": np.int32,
                    "device_fp": np.uint64, "ip_class": np.uint8, "hour": np.uint8, "weekend": np.uint8}
 
-    def state_init(self, capacity: int, window_mode: int = N.FD_WINDOW_REDIS_COMPAT, ring_k: int = 16) -> None:
-        p = N.fd_state_params(int(capacity), int(window_mode), int(ring_k))
+    def state_init(self, capacity: int, window_mode: int = N.FD_WINDOW_REDIS_COMPAT, ring_k: int = 16,
+                   seq_len: int = 0) -> None:
+        """seq_len > 0 keeps each card's last seq_len events for the LSTM head (lstm_sequential)."""
+        p = N.fd_state_params(int(capacity), int(window_mode), int(ring_k), int(seq_len))
+        self.seq_len = int(seq_len)
         N.call("fd_state_init", self._h, C.byref(p))
 
     def state_clear(self) -> None:
@@ -187,6 +190,42 @@ class FraudEngine:
         opt = lambda p: C.c_void_p(p) if p else None  # noqa: E731
         N.call("fd_score_batch_device", self._h, C.byref(params), _ptr(sl), ext, _ptr(pres), C.byref(b), int(n),
                opt(vec_ptr), opt(model_probs_ptr), C.c_void_p(fp_ptr), opt(conf_ptr), opt(dec_ptr), opt(risk_ptr))
+
+    def features_seq_device(self, ptrs: dict, n: int, vec_ptr: int, seq_ptr: int, raw_ptr: int = 0) -> None:
+        """features_device plus each transaction's LSTM input sequence (n x seq_len x 16 f32)."""
+        b = N.fd_txn_batch(*[int(ptrs[f]) for f in N.TXN_FIELDS])
+        N.call("fd_features_seq_device", self._h, C.byref(b), int(n), C.c_void_p(vec_ptr),
+               C.c_void_p(raw_ptr) if raw_ptr else None, C.c_void_p(seq_ptr) if seq_ptr else None)
+
+    # ------------------------------------------------------------------ LSTM head
+    def load_lstm(self, model) -> None:
+        """model: fdengine.lstm.LstmWeights (PyTorch layout, f32)."""
+        keep = [np.ascontiguousarray(a, np.float32) if a is not None else None
+                for a in (model.w_ih, model.w_hh, model.b_ih, model.b_hh, model.w_out, model.b_out)]
+        ptr = [a.ctypes.data if a is not None else None for a in keep]
+        p = N.fd_lstm_params(int(model.input_size), int(model.hidden), int(model.n_out), *ptr)
+        N.call("fd_load_lstm", self._h, C.byref(p))
+        self.lstm_info = {"input_size": model.input_size, "hidden": model.hidden, "n_out": model.n_out}
+
+    def unload_lstm(self) -> None:
+        N.call("fd_unload_lstm", self._h)
+        self.lstm_info = None
+
+    def lstm_predict(self, seq: np.ndarray) -> np.ndarray:
+        """seq: [n, T, 16] (or [n, T, input_size], zero-padded here) -> P(fraud) f64 [n]."""
+        seq = np.asarray(seq, np.float32)
+        if seq.ndim != 3:
+            raise ValueError(f"LSTM input must be [n, T, features], got shape {seq.shape}")
+        n, T, I = seq.shape
+        if I < N.FD_SEQ_INPUT:
+            seq = np.concatenate([seq, np.zeros((n, T, N.FD_SEQ_INPUT - I), np.float32)], axis=2)
+        seq = np.ascontiguousarray(seq)
+        prob = np.empty(n, np.float64)
+        N.call("fd_lstm_predict_host", self._h, _ptr(seq), n, T, _ptr(prob))
+        return prob
+
+    def lstm_predict_device(self, seq_ptr: int, n: int, T: int, prob_ptr: int) -> None:
+        N.call("fd_lstm_predict_device", self._h, C.c_void_p(seq_ptr), int(n), int(T), C.c_void_p(prob_ptr))
 
     # ------------------------------------------------------------------ card-hash sharding (fdengine/sharding.py)
     def route_partition_device(self, txn_ptrs: dict, n: int, n_shards: int, records_ptr: int, counts_ptr: int) -> None:

@@ -246,6 +246,8 @@ class EnsemblePredictor:
                         raise ValueError("stand-in returned the wrong number of rows")
                 except Exception:
                     ok, col = 0, None
+            elif slot == N.FD_SLOT_LSTM:
+                ok, slot = 0, -1  # flat vectors carry no sequence: dropped, as the reference's LSTM is
             elif mm.models[name].kind == "xgboost" and X.shape[1] > mm.models[name].num_feature:
                 ok = 0  # XGBoost rejects wider matrices; the reference drops the model
             slots.append(slot)

@@ -10,6 +10,11 @@ Same public surface — `load_all_models`, `predict(model_name, features) -> np.
   model_type "sklearn"  unchanged joblib IsolationForest (`_load_sklearn_model` :197-200) -> engine
                         slot; predict returns 1/(1+exp(decision_function)) (`_predict_sklearn` :338-346)
 
+  model_type "tensorflow" lstm_sequential weights (`_load_tensorflow_model` :162-165) -> the engine's LSTM
+                        head (fdengine/lstm.py formats; the .h5 path's .safetensors/.npz sibling);
+                        predict takes [n, T, I] sequences (`_predict_tensorflow` :313-319); a flat
+                        scoring vector raises as a Keras LSTM given a 2-D input does
+
 Everything else keeps the reference's observable behaviour, so the ensemble above sees the same
 model set: a missing model file yields the reference's random DummyModel (:115-118, 244-277);
 its tensorflow / pytorch predict branches fail for a DummyModel exactly as the reference's do
@@ -56,6 +61,22 @@ class DummyModel:
         return p / p.sum(axis=1, keepdims=True)
 
 
+class EngineLstm:
+    """The LSTM head resident in the engine (one per engine)."""
+
+    def __init__(self, input_size: int, hidden: int, n_out: int, path: str):
+        self.kind, self.input_size, self.hidden, self.n_out, self.path = "lstm", input_size, hidden, n_out, path
+
+
+def _lstm_weight_file(path: str) -> Optional[str]:
+    """The .h5 the registry names cannot be read without TensorFlow; its exported siblings can."""
+    stem, ext = os.path.splitext(path)
+    for cand in ([path] if ext in (".npz", ".safetensors") else []) + [stem + ".safetensors", stem + ".npz"]:
+        if os.path.exists(cand):
+            return cand
+    return None
+
+
 class EngineForest:
     """A forest resident in the engine (one slot)."""
 
@@ -97,7 +118,10 @@ class ModelManager:
             self.logger.info(f"Loaded {ok}/{len(enabled)} models successfully")
 
     async def _load_single_model(self, name: str, cfg) -> None:
-        if not os.path.exists(cfg.model_path):
+        lstm_file = _lstm_weight_file(cfg.model_path) if cfg.model_type == "tensorflow" else None
+        if lstm_file is not None:
+            model = self._load_lstm(lstm_file)
+        elif not os.path.exists(cfg.model_path):
             self.logger.warning(f"Model file not found: {cfg.model_path}. Creating dummy model.")
             model = DummyModel(cfg.model_type, name)
         else:
@@ -109,7 +133,7 @@ class ModelManager:
             "loaded_at": self.model_load_times[name].isoformat(),
             "hyperparameters": getattr(cfg, "hyperparameters", {}),
             "preprocessing_steps": getattr(cfg, "preprocessing_steps", []),
-            "engine": (vars(model) if isinstance(model, EngineForest) else None),
+            "engine": (vars(model) if isinstance(model, (EngineForest, EngineLstm)) else None),
         }
 
     def _load_by_type(self, name: str, cfg):
@@ -124,6 +148,12 @@ class ModelManager:
                 raise UnsupportedModel(f"sklearn model {type(model).__name__} is not on the engine path")
             return self._upload(slot, iforest_from_sklearn(model), "isolation_forest")
         raise UnsupportedModel(f"model_type {cfg.model_type!r} files are not served by the engine")
+
+    def _load_lstm(self, path: str) -> EngineLstm:
+        from .lstm import load_lstm_file
+        w = load_lstm_file(path)
+        self.engine.load_lstm(w)
+        return EngineLstm(w.input_size, w.hidden, w.n_out, path)
 
     def _upload(self, slot: int, fa, kind: str) -> EngineForest:
         self.engine.load_forest(slot, fa)
@@ -144,6 +174,11 @@ class ModelManager:
             raise
 
     def predict_sync(self, name: str, model, model_type: str, features: np.ndarray) -> np.ndarray:
+        if isinstance(model, EngineLstm):
+            X = np.asarray(features)
+            if X.ndim != 3:  # Keras: an LSTM layer needs [batch, timesteps, features]
+                raise ValueError(f"Input 0 of layer lstm is incompatible: expected ndim=3, found ndim={X.ndim}")
+            return self.engine.lstm_predict(X).astype(np.float32)
         if isinstance(model, EngineForest):
             X = np.asarray(features)
             if X.ndim == 1:
@@ -179,15 +214,12 @@ class ModelManager:
                 m = self.models.pop(model_name)
                 self.model_metadata.pop(model_name, None)
                 self.model_load_times.pop(model_name, None)
-                if isinstance(m, EngineForest):
-                    self.engine.unload_forest(m.slot)
+                self._unload(m)
             await self._load_single_model(model_name, cfg)
 
     async def reload_all_models(self) -> None:
         for name in list(self.models):
-            m = self.models[name]
-            if isinstance(m, EngineForest):
-                self.engine.unload_forest(m.slot)
+            self._unload(self.models[name])
         self.models.clear()
         self.model_metadata.clear()
         self.model_load_times.clear()
@@ -204,16 +236,24 @@ class ModelManager:
     def is_model_loaded(self, model_name: str) -> bool:
         return model_name in self.models
 
+    def _unload(self, m) -> None:
+        if isinstance(m, EngineForest):
+            self.engine.unload_forest(m.slot)
+        elif isinstance(m, EngineLstm):
+            self.engine.unload_lstm()
+
     def engine_slot(self, model_name: str) -> int:
-        """Engine slot of a device-resident forest, -1 otherwise (host stand-in)."""
+        """Engine slot of a device-resident model (FD_SLOT_LSTM for the LSTM head), -1 otherwise."""
         m = self.models.get(model_name)
+        if isinstance(m, EngineLstm):
+            from ._native import FD_SLOT_LSTM
+            return FD_SLOT_LSTM
         return m.slot if isinstance(m, EngineForest) else -1
 
     async def cleanup(self) -> None:
         async with self.model_lock:
             for name, m in list(self.models.items()):
-                if isinstance(m, EngineForest):
-                    self.engine.unload_forest(m.slot)
+                self._unload(m)
             self.models.clear()
             self.model_metadata.clear()
             self.model_load_times.clear()
