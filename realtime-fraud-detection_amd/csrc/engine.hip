@@ -242,7 +242,7 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   FD_REQUIRE(key, FD_ERR_INVALID_ARG, "null key");
   const std::string k(key);
   if (k == "forest_kernel") {
-    FD_REQUIRE(value >= 0 && value <= 3, FD_ERR_INVALID_ARG, "forest_kernel must be 0, 1, 2 or 3");
+    FD_REQUIRE(value >= 0 && value <= 5, FD_ERR_INVALID_ARG, "forest_kernel must be in 0..5");
     e.forest_variant = (int)value;
   } else {
     throw fd::Error(FD_ERR_INVALID_ARG, "unknown option: " + k);

@@ -87,6 +87,7 @@ struct PackedForest {
   DeviceBuffer b_blob;     // b_n_chunks * b_chunk_stride
   DeviceBuffer b_thr;      // distinct thresholds, feature-major ascending (f32)
   DeviceBuffer b_thr_off;  // num_feature + 1 offsets (int32)
+  int b_n_thr = 0;         // distinct thresholds in b_thr
 };
 
 // card-hash routing records (route.hip): one transaction (48 B) / one result (24 B)

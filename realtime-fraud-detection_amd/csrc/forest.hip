@@ -273,6 +273,7 @@ void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_ar
     pf.b_tree_bytes = hp.b_tree_bytes;
     pf.b_chunk_stride = hp.b_chunk_stride;
     pf.bin_steps = hp.bin_steps;
+    pf.b_n_thr = (int)hp.b_thr.size();
   }
   pf.loaded = true;
 }
@@ -856,6 +857,213 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 }
 
 // ------------------------------------------------------------------------------------------------
+// forest_kernel5 (depth <= 8, kernel 4's binned blob): pair lanes, sums in registers.
+//
+// 512 threads (8 waves, two per SIMD) on a 256-transaction tile. Wave w holds transactions
+// 32w..32w+31 TWICE: lanes 0-31 walk the even tree of every pair (2j, 2j+1) of the staged chunk,
+// lanes 32-63 the odd tree. After a pair, v_permlane32_swap hands every lane both leaf values
+// (even in one register, odd in the other), so each half adds them in tree order to its own copy of
+// the transaction's running sum: the reference's sequential f32 / f64 sum, with no leaf values in
+// LDS, no owner pass and identical work in every wave (kernel 4 spent ~37 % of its time there).
+// Per level and chain: SPEC = false reads the chosen node after the compare (2 x ds_read_b32, 4 VALU:
+// compare, select, shift-add, and-or); SPEC = true reads both children with the feature (kernel 4's
+// ds_read_b32 + ds_read_b64, one more select). All CH / 2 pairs of a chunk are walked interleaved.
+// ds_read_b32 banks per 32-lane group, so the two halves never conflict with each other; within a
+// half the 32 transactions' feature columns are 32 consecutive words (conflict-free).
+//
+// LDS: [0, nf KiB) Xs[f][256] u32 bins | 1 KiB flags | bufA | bufB; the threshold table is staged
+// over bufB (dead until chunk 1) when it fits, else binning reads it from global memory.
+constexpr int kWG5 = 512;
+
+__host__ __device__ constexpr uint32_t lds5_base(int nf, uint32_t cs) { return (uint32_t)nf * 1024u + 2048u + 2u * cs; }
+__host__ __device__ constexpr uint32_t lds5_table(int nf, uint32_t cs, int n_thr) {
+  return (uint32_t)nf * 1024u + 2048u + cs + ((uint32_t)n_thr * 4u + 1023u) / 1024u * 1024u;
+}
+__host__ __device__ constexpr bool lds5_table_fits(int nf, uint32_t cs, int n_thr) {
+  return lds5_table(nf, cs, n_thr) <= (uint32_t)kLdsBudget;
+}
+__host__ __device__ constexpr uint32_t lds_bytes_kernel5(int nf, uint32_t cs, int n_thr) {
+  return (lds5_table_fits(nf, cs, n_thr) && lds5_table(nf, cs, n_thr) > lds5_base(nf, cs)) ? lds5_table(nf, cs, n_thr)
+                                                                                         : lds5_base(nf, cs);
+}
+
+template <int D, int NP, typename LeafT, bool NAN_AWARE, bool SPEC>
+__device__ __forceinline__ void walk5(uint32_t buf, uint32_t half, uint32_t lane4, uint32_t (&A)[NP]) {
+  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
+  uint32_t c0[NP], c4[NP], node[NP], kl[NP], kr[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const uint32_t tb = buf + (uint32_t)(2 * j) * TB + half * TB;
+    c0[j] = 0u - tb;
+    c4[j] = (SPEC ? 8u : 4u) - tb;
+    A[j] = tb + (SPEC ? 8u : 4u);  // SPEC: children pair of slot s at tb + 8 s; else slot s at tb + 4 s
+    asm volatile("" : "+v"(c0[j]), "+v"(c4[j]));
+    node[j] = lds_load<uint32_t>(tb + 4u);
+  }
+  if (SPEC) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const u32x2 k = lds_load<u32x2>(A[j]);
+      kl[j] = k.x;
+      kr[j] = k.y;
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < D; ++l) {
+    uint32_t xw[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      bool right = xw[j] > node[j];  // bin > j  <=>  !(x < t_j)
+      if (NAN_AWARE) {
+        if (xw[j] == 0xFFFF0000u) right = (node[j] & 1u) == 0u;  // missing: default direction
+      }
+      A[j] = (A[j] << 1) + (right ? c4[j] : c0[j]);
+      if (l + 1 < D) {
+        if (SPEC) {
+          uint32_t a = kl[j], b = kr[j];
+          asm volatile("" : "+v"(a), "+v"(b));
+          node[j] = right ? b : a;
+          if (l + 2 < D) {
+            const u32x2 k = lds_load<u32x2>(A[j]);
+            kl[j] = k.x;
+            kr[j] = k.y;
+          }
+        } else {
+          node[j] = lds_load<uint32_t>(A[j]);
+        }
+      }
+    }
+  }
+}
+
+// v_permlane32_swap(v, v) is a half exchange: the first result holds v's lanes 0-31 (even-tree leaf)
+// in every lane, the second v's lanes 32-63 (odd-tree leaf)
+__device__ __forceinline__ float lane_swap_even(float v, float& odd) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  odd = __uint_as_float(r[1]);
+  return __uint_as_float(r[0]);
+}
+
+__device__ __forceinline__ double lane_swap_even(double v, double& odd) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+  odd = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+  return __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+}
+
+template <int D, int CH, typename LeafT, int KIND, bool SPEC>
+__global__ void __launch_bounds__(kWG5)
+forest_kernel5(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
+               int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
+               const float* __restrict__ thr, const int32_t* __restrict__ thr_off, int bin_steps,
+               float base_margin, double if_offset, double if_denom, double* __restrict__ out_prob,
+               double* __restrict__ out_raw, int32_t* __restrict__ out_leaf) {
+  constexpr int NP = CH / 2;
+  constexpr int NL = 1 << D;
+  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
+  const uint32_t s0 = (sdyn + 1023u) & ~1023u;
+  char* const lbase = smem + (s0 - sdyn);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t half = (uint32_t)(lane >> 5);
+  const int txn = (wave << 5) + (lane & 31);
+  const uint32_t lane4 = s0 + (uint32_t)txn * 4u;
+  const uint32_t flags = s0 + (uint32_t)nf * 1024u;
+  const uint32_t bufA = flags + 1024u, bufB = bufA + (uint32_t)chunk_stride;
+  const int64_t row = (int64_t)blockIdx.x * kTile + txn;
+  const bool valid = row < n;
+
+  stage_chunk_asm(blob, bufA, chunk_stride, kWG5 / 64);  // chunk 0 lands while the tile is binned
+  const int n_thr = thr_off[nf];
+  const bool tbl_lds = lds5_table_fits(nf, (uint32_t)chunk_stride, n_thr);
+  if (tbl_lds) {
+    float* tl = reinterpret_cast<float*>(lbase + (bufB - s0));
+    for (int i = tid; i < n_thr; i += kWG5) tl[i] = thr[i];
+    __syncthreads();
+  }
+  // prologue: 2 threads per transaction, each bins every other feature, 4 binary searches interleaved
+  int anynan = 0;
+  {
+    const int t = tid & 255, q = tid >> 8;
+    const int64_t r = (int64_t)blockIdx.x * kTile + t;
+    const bool ok = r < n;
+    const int ncopy = ld < nf ? ld : nf;
+    uint32_t* Xs = reinterpret_cast<uint32_t*>(lbase);
+    const float* xr = X + r * (int64_t)ld;
+    for (int f0 = q; f0 < nf; f0 += 8) {
+      float v[4];
+      int o[4], cnt[4], pos[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int f = f0 + 2 * u;
+        v[u] = (ok && f < nf) ? (f < ncopy ? xr[f] : __builtin_nanf("")) : 0.f;  // DMatrix: missing = NaN
+        o[u] = f < nf ? thr_off[f] : 0;
+        cnt[u] = f < nf ? thr_off[f + 1] - o[u] : 0;
+        pos[u] = 0;
+      }
+      for (int st = bin_steps; st > 0; st >>= 1) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int np = pos[u] + st;
+          if (np <= cnt[u]) {
+            const float tv = tbl_lds ? lds_load<float>(bufB + (uint32_t)(o[u] + np - 1) * 4u) : thr[o[u] + np - 1];
+            if (tv <= v[u]) pos[u] = np;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int f = f0 + 2 * u;
+        if (f < nf) {
+          uint32_t w = (uint32_t)pos[u] << 16;
+          if (v[u] != v[u]) {
+            w = 0xFFFF0000u;
+            anynan |= ok ? 1 : 0;
+          }
+          Xs[f * kTile + t] = ok ? w : 0u;
+        }
+      }
+    }
+  }
+  dma_wait();  // chunk 0 (published by tile_any's barrier)
+  const bool tile_nan = tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (flags - s0)), kWG5 / 64);
+
+  LeafT acc = (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0;
+  for (int k = 0; k < n_chunks; ++k) {
+    const uint32_t cur = (k & 1) ? bufB : bufA;
+    if (k + 1 < n_chunks)
+      stage_chunk_asm(blob + (size_t)(k + 1) * chunk_stride, (k & 1) ? bufA : bufB, chunk_stride, kWG5 / 64);
+    uint32_t A[NP];
+    if (tile_nan)
+      walk5<D, NP, LeafT, true, SPEC>(cur, half, lane4, A);
+    else
+      walk5<D, NP, LeafT, false, SPEC>(cur, half, lane4, A);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const uint32_t tb = cur + (uint32_t)(2 * j) * TB + half * TB;
+      // leaf heap slot P in [NL, 2NL): SPEC's A is tb + 8 P, the plain walk's tb + 4 P
+      const uint32_t slot = (SPEC ? (A[j] - tb) >> 3 : (A[j] - tb) >> 2) - NL;
+      const LeafT lv = lds_load<LeafT>(tb + NL * 4u + slot * (uint32_t)sizeof(LeafT));
+      LeafT odd;
+      const LeafT even = lane_swap_even(lv, odd);
+      acc += even;
+      acc += odd;
+      if (out_leaf != nullptr && valid) {
+        const int tg = k * CH + 2 * j + (int)half;
+        if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slot];
+      }
+    }
+    dma_wait();
+    __syncthreads();  // chunk k+1 landed; every wave is done with chunk k's buffer
+  }
+  if (half == 0 && valid) write_outputs<KIND, LeafT>(acc, row, if_offset, if_denom, out_prob, out_raw);
+}
+
+// ------------------------------------------------------------------------------------------------
 // dispatch
 
 using KernelFn = void (*)(const float*, int64_t, int, int, const char*, int, int, const int32_t*, int,
@@ -946,6 +1154,43 @@ KernelFn4 pick4(int D, int CH) {
   }
 }
 
+template <typename LeafT, int KIND, int CH>
+KernelFn4 pick5_ch(int D) {
+  switch (D) {
+    case 1: return forest_kernel5<1, CH, LeafT, KIND, false>;
+    case 2: return forest_kernel5<2, CH, LeafT, KIND, false>;
+    case 3: return forest_kernel5<3, CH, LeafT, KIND, false>;
+    case 4: return forest_kernel5<4, CH, LeafT, KIND, false>;
+    case 5: return forest_kernel5<5, CH, LeafT, KIND, false>;
+    case 6: return forest_kernel5<6, CH, LeafT, KIND, false>;
+    case 7: return forest_kernel5<7, CH, LeafT, KIND, false>;
+    case 8: return forest_kernel5<8, CH, LeafT, KIND, false>;
+    default: return nullptr;
+  }
+}
+
+// spec = true (speculative children reads) is instantiated for depth 8 only (the A/B configuration)
+template <typename LeafT, int KIND>
+KernelFn4 pick5(int D, int CH, bool spec) {
+  if (spec) {
+    if (D != 8) return nullptr;
+    switch (CH) {
+      case 4: return forest_kernel5<8, 4, LeafT, KIND, true>;
+      case 8: return forest_kernel5<8, 8, LeafT, KIND, true>;
+      case 12: return forest_kernel5<8, 12, LeafT, KIND, true>;
+      case 16: return forest_kernel5<8, 16, LeafT, KIND, true>;
+      default: return nullptr;
+    }
+  }
+  switch (CH) {
+    case 4: return pick5_ch<LeafT, KIND, 4>(D);
+    case 8: return pick5_ch<LeafT, KIND, 8>(D);
+    case 12: return pick5_ch<LeafT, KIND, 12>(D);
+    case 16: return pick5_ch<LeafT, KIND, 16>(D);
+    default: return nullptr;
+  }
+}
+
 }  // namespace
 
 #ifdef FD_FOREST_PROFILE
@@ -956,7 +1201,8 @@ extern "C" __attribute__((visibility("default"))) int fd_debug_forest_profile(un
 
 // Kernel choice (option "forest_kernel"): 0 auto = kernel 4 when the binned layout exists (depth <= 8,
 // <= 65534 distinct thresholds per feature), else kernel 3 (depth <= 8), else kernel 1; 1/2/3 force
-// kernel 1/3/4 (FD_ERR_UNSUPPORTED when the forest cannot use it).
+// kernel 1/3/4, 4/5 force kernel 5 (plain / speculative-children walk) (FD_ERR_UNSUPPORTED when the
+// forest cannot use it).
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
                    double* d_prob, double* d_raw, int32_t* d_leaf) {
   FD_REQUIRE(d_X && d_prob && ld > 0, FD_ERR_INVALID_ARG, "null buffer or bad ld");
@@ -966,8 +1212,29 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   const int64_t blocks = (n + kTile - 1) / kTile;
   FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
   const int v = e.forest_variant;
-  FD_REQUIRE(v >= 0 && v <= 3, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..3");
+  FD_REQUIRE(v >= 0 && v <= 5, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..5");
   Engine::Timed* ev = nullptr;
+
+  if (v == 4 || v == 5) {  // forest_kernel5 on kernel 4's binned blob
+    const uint32_t lds5 =
+        pf.binned ? lds_bytes_kernel5(pf.num_feature, (uint32_t)pf.b_chunk_stride, pf.b_n_thr) : 0u;
+    FD_REQUIRE(pf.binned && pf.depth <= 8 && pf.b_chunk % 2 == 0 && lds5 <= kLdsBudget, FD_ERR_UNSUPPORTED,
+               "forest kernel 5 needs the binned layout (depth <= 8)");
+    KernelFn4 fn = xgb ? pick5<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.b_chunk, v == 5)
+                       : pick5<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.b_chunk, v == 5);
+    FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel 5 for this depth/chunk");
+    FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds5));
+    ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
+    if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
+    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kWG5), lds5, e.stream, d_X, n, (int)ld, pf.num_feature,
+                       pf.b_blob.as<const char>(), pf.b_n_chunks, (int)pf.b_chunk_stride,
+                       pf.leaf_ids.as<const int32_t>(), pf.n_trees, pf.b_thr.as<const float>(),
+                       pf.b_thr_off.as<const int32_t>(), pf.bin_steps, pf.base_margin, pf.if_offset,
+                       pf.if_denominator, d_prob, d_raw, d_leaf);
+    FD_HIP(hipGetLastError());
+    if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
+    return;
+  }
 
   const size_t lds4 = pf.binned ? lds_bytes_kernel4(pf.num_feature, pf.b_chunk_stride, pf.b_chunk, leaf_sz) : 0;
   const bool ok4 = pf.binned && pf.depth <= 8 && pf.b_chunk % 4 == 0 && lds4 <= kLdsBudget;

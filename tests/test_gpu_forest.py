@@ -115,8 +115,22 @@ def test_device_pointer_path_matches_host_path(engine):
     np.testing.assert_array_equal(dp.cpu().numpy(), host)
 
 
+@pytest.mark.parametrize("depth", [1, 3, 6, 8])
+def test_kernel5_depths(engine, depth):
+    """The pair-lane kernel (option 4) across depths, ragged trees, NaNs, odd tree counts."""
+    engine.set_option("forest_kernel", 4)
+    try:
+        prob, raw, leaf, rp, rm, rl = _xgb_case(engine, 1, 777, 45, depth, 20, seed=90 + depth, p_leaf=0.2,
+                                                nan_frac=0.02)
+        np.testing.assert_array_equal(leaf, rl)
+        np.testing.assert_array_equal(raw.astype(np.float32), rm)
+        assert np.abs(prob - rp).max() <= PROB_TOL
+    finally:
+        engine.set_option("forest_kernel", 0)
+
+
 @pytest.mark.parametrize("max_bin", [256, None])
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
 def test_kernel_variants_agree(engine, variant, max_bin):
     """Every forest kernel (256-thread; 1024-thread tree-split on the threshold layout; 1024-thread on
     the binned layout) gives the oracle's bits, for hist-style and raw-valued split thresholds."""
