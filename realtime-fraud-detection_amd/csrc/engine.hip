@@ -95,13 +95,30 @@ static void score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     joined = false;
     cols[m] = col;
   }
+  // small (latency) batches: every forest after the first runs on a second stream, concurrently,
+  // forked after everything queued so far (the feature kernel)
+  int n_forests = 0;
+  for (int m = 0; m < M; ++m) n_forests += (!(present && !present[m]) && slots[m] >= 0 && slots[m] != FD_SLOT_LSTM);
+  const bool small = (n + fd::kTile - 1) / fd::kTile < fd::kSplitTiles && n_forests > 1;
+  if (small) {
+    if (!e.aux2_stream) {
+      FD_HIP(hipStreamCreateWithFlags(&e.aux2_stream, hipStreamNonBlocking));
+      FD_HIP(hipEventCreateWithFlags(&e.join2_ev, hipEventDisableTiming));
+      if (!e.fork_ev) FD_HIP(hipEventCreateWithFlags(&e.fork_ev, hipEventDisableTiming));
+    }
+    FD_HIP(hipEventRecord(e.fork_ev, e.stream));
+    FD_HIP(hipStreamWaitEvent(e.aux2_stream, e.fork_ev, 0));
+  }
+  int forests_seen = 0;
+  bool joined2 = !small;
   for (int m = 0; m < M; ++m) {
     if ((present && !present[m]) || slots[m] == FD_SLOT_LSTM) continue;
     double* col = dMP + (size_t)m * n;
     if (slots[m] >= 0) {
       const fd::PackedForest& pf = slot_of(e, slots[m]);
       FD_REQUIRE(pf.loaded, FD_ERR_NOT_LOADED, "Model in slot " + std::to_string(slots[m]) + " not loaded");
-      fd::launch_forest(e, pf, dX, n, ld, col, nullptr, nullptr);
+      const hipStream_t st = (small && forests_seen++ > 0) ? e.aux2_stream : nullptr;
+      fd::launch_forest(e, pf, dX, n, ld, col, nullptr, nullptr, st);
       cols[m] = col;
     } else {
       FD_REQUIRE(ext && ext[m], FD_ERR_INVALID_ARG, "model without slot needs an external probability column");
@@ -111,6 +128,10 @@ static void score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     }
   }
   if (!joined) FD_HIP(hipStreamWaitEvent(e.stream, e.join_ev, 0));
+  if (!joined2) {
+    FD_HIP(hipEventRecord(e.join2_ev, e.aux2_stream));
+    FD_HIP(hipStreamWaitEvent(e.stream, e.join2_ev, 0));
+  }
   fd::launch_blend(e, p, n, cols, present, dfp, dconf, ddec, drisk);
 }
 
@@ -170,6 +191,7 @@ int fd_engine_destroy(fd_engine* eng) {
   Engine& e = E(eng);
   (void)hipStreamSynchronize(e.stream);
   for (auto& f : e.forests) {
+    for (auto* b : {&f.split.bins, &f.split.nan, &f.split.leaves}) b->release();
     f.blob.release();
     f.leaf_ids.release();
     f.b_blob.release();
@@ -193,6 +215,11 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipStreamDestroy(e.aux_stream);
     (void)hipEventDestroy(e.fork_ev);
     (void)hipEventDestroy(e.join_ev);
+  }
+  if (e.aux2_stream) {
+    (void)hipStreamSynchronize(e.aux2_stream);
+    (void)hipStreamDestroy(e.aux2_stream);
+    (void)hipEventDestroy(e.join2_ev);
   }
   for (auto* b : {&e.state.headers, &e.state.fps, &e.state.ring, &e.state.merchants, &e.state.slot,
                   &e.state.next, &e.state.err})
@@ -225,6 +252,7 @@ int fd_engine_sync(fd_engine* eng) {
   Engine& e = E(eng);
   FD_HIP(hipStreamSynchronize(e.stream));
   if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
+  if (e.aux2_stream) FD_HIP(hipStreamSynchronize(e.aux2_stream));
   fd::route_check(e);
   FD_API_END
 }
@@ -242,7 +270,7 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   FD_REQUIRE(key, FD_ERR_INVALID_ARG, "null key");
   const std::string k(key);
   if (k == "forest_kernel") {
-    FD_REQUIRE(value >= 0 && value <= 5, FD_ERR_INVALID_ARG, "forest_kernel must be in 0..5");
+    FD_REQUIRE(value >= 0 && value <= 6, FD_ERR_INVALID_ARG, "forest_kernel must be in 0..6");
     e.forest_variant = (int)value;
   } else {
     throw fd::Error(FD_ERR_INVALID_ARG, "unknown option: " + k);
@@ -357,6 +385,8 @@ int fd_unload_forest(fd_engine* eng, int slot) {
   pf.b_blob.release();
   pf.b_thr.release();
   pf.b_thr_off.release();
+  for (auto* b : {&pf.split.bins, &pf.split.nan, &pf.split.leaves}) b->release();
+  pf.split.epoch = 0;
   pf.binned = false;
   pf.loaded = false;
   FD_API_END

@@ -19,6 +19,7 @@ constexpr int kMaxFeatures = 64;  // model columns held in LDS ([feature][kTile]
 constexpr int kMaxDepth = 10;     // deepest tree the repacker accepts
 constexpr size_t kLdsBudget = 160 * 1024;  // LDS per CU (one workgroup per CU at 64k batches)
 constexpr int kMaxBins = 65534;   // distinct thresholds per feature in the binned layout
+constexpr int kSplitTiles = 128;  // below this many 256-txn tiles the forest runs the tree-split path
 constexpr int kSeqInput = 16;     // LSTM per-event input width (the bridged raw features)
 constexpr int kLstmHidden = 128;  // lstm_sequential hidden_units (ml/utils/config.py:152-156)
 
@@ -60,6 +61,12 @@ struct DeviceBuffer {
   T* as() const { return static_cast<T*>(ptr); }
 };
 
+// small-batch tree-split scratch of one forest (forest.hip launch_split)
+struct SplitScratch {
+  DeviceBuffer bins, nan, leaves;
+  uint32_t epoch = 0;
+};
+
 // A forest repacked into perfect depth-D trees stored as 1-based heaps (see forest.hip header and
 // DESIGN.md "Forest layout"): per tree 2^D node records {f32 thr, u32 meta} (slot 0 unused; children
 // of slot s are 2s / 2s+1) then 2^D leaf values (f32 XGBoost, f64 Isolation Forest); chunks of
@@ -88,6 +95,7 @@ struct PackedForest {
   DeviceBuffer b_thr;      // distinct thresholds, feature-major ascending (f32)
   DeviceBuffer b_thr_off;  // num_feature + 1 offsets (int32)
   int b_n_thr = 0;         // distinct thresholds in b_thr
+  mutable SplitScratch split;
 };
 
 // card-hash routing records (route.hip): one transaction (48 B) / one result (24 B)
@@ -137,6 +145,8 @@ struct Engine {
   LstmModel lstm;
   hipStream_t aux_stream = nullptr;            // LSTM head runs here, concurrent with the forests
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  hipStream_t aux2_stream = nullptr;           // small batches: the second forest, concurrent with the first
+  hipEvent_t join2_ev = nullptr;
   DeviceBuffer seq_buf;                        // per-txn LSTM input sequences of the fused path
   DeviceBuffer feat_vec, feat_in;  // host-API / fused-pipeline staging for features
   // host-API staging
@@ -175,7 +185,7 @@ struct HostPack {
 HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t);
 void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
-                   double* d_prob, double* d_raw, int32_t* d_leaf);
+                   double* d_prob, double* d_raw, int32_t* d_leaf, hipStream_t stream = nullptr);
 // features.hip
 void state_init(Engine& e, const fd_state_params& p);
 void state_clear(Engine& e);

@@ -42,7 +42,7 @@ struct __attribute__((aligned(16))) CardHeader {  // 64 B: one card's header, Ao
 };
 static_assert(sizeof(CardHeader) == 64, "CardHeader must be 64 B");
 
-struct RingEvent {
+struct __attribute__((aligned(16))) RingEvent {
   long long ts;
   long long cents;
 };
@@ -139,53 +139,50 @@ __device__ void write_vector(const double* r, float* __restrict__ out) {
   if (isnan(mrisk)) mrisk = 0.5;
   const double age = pmax(r[15], 0.0);
   if (amount > 0) alog = log1p(amount);
-  // the 41 definitions in declaration order (feature_processor.py:66-147)
-  out[0] = clip10(amount);
-  out[1] = clip10(alog);
-  out[2] = 0.f;
-  out[3] = 0.f;
-  out[4] = 0.f;
-  out[5] = clip10(hour);
-  out[6] = clip10(dow);
-  out[7] = r[4] > 0.5 ? 1.f : 0.f;
-  out[8] = 0.f;
-  out[9] = 0.f;
-  out[10] = 0.f;
-  out[11] = 0.f;
-  out[12] = 0.5f;
-  out[13] = 0.f;
-  out[14] = clip10(c1);
-  out[15] = clip10(c24);
-  out[16] = clip10(s24);
-  out[17] = clip10(uavg);
-  out[18] = 0.f;
-  out[19] = clip10(age);
-  out[20] = 0.f;
-  out[21] = clip10(mfr);
-  out[22] = 0.f;
-  out[23] = clip10(mrisk);
-  out[24] = 0.5f;
-  out[25] = 0.5f;
-  out[26] = r[6] > 0.5 ? 1.f : 0.f;
-  out[27] = clip10(ip);
-  out[28] = 0.f;
-  out[29] = 0.f;
-  out[30] = 0.f;
-  out[31] = clip10(s1);
-  out[32] = clip10(c5);
-  out[33] = 0.5f;
-  out[34] = 0.5f;
-  for (int k = 35; k < 41; ++k) out[k] = 0.f;
-  // derived, appended in order when present (feature_processor.py:330-363)
-  int k = 41;
-  if (amount > 0) out[k++] = clip10(sqrt(amount));
-  if (uavg > 0) out[k++] = clip10(amount / uavg);
-  // merchant_avg_amount is 0 on this path: no amount_to_merchant_avg_ratio
-  if (c24 > 0) out[k++] = clip10(c1 / (c24 / 24));
-  out[k++] = clip10((0.5 + ip) / 2);
-  out[k++] = (9 <= hour && hour <= 17) ? 1.f : 0.f;
-  out[k++] = (hour < 6 || hour > 22) ? 1.f : 0.f;
-  for (; k < FD_VECTOR_WIDTH; ++k) out[k] = 0.f;
+  // the 41 definitions in declaration order (feature_processor.py:66-147); built in registers
+  // (compile-time indices only) and stored as 16 x 16 B
+  float o[FD_VECTOR_WIDTH];
+#pragma unroll
+  for (int k = 0; k < FD_VECTOR_WIDTH; ++k) o[k] = 0.f;
+  o[0] = clip10(amount);
+  o[1] = clip10(alog);
+  o[5] = clip10(hour);
+  o[6] = clip10(dow);
+  o[7] = r[4] > 0.5 ? 1.f : 0.f;
+  o[12] = 0.5f;
+  o[14] = clip10(c1);
+  o[15] = clip10(c24);
+  o[16] = clip10(s24);
+  o[17] = clip10(uavg);
+  o[19] = clip10(age);
+  o[21] = clip10(mfr);
+  o[23] = clip10(mrisk);
+  o[24] = 0.5f;
+  o[25] = 0.5f;
+  o[26] = r[6] > 0.5 ? 1.f : 0.f;
+  o[27] = clip10(ip);
+  o[31] = clip10(s1);
+  o[32] = clip10(c5);
+  o[33] = 0.5f;
+  o[34] = 0.5f;
+  // derived, appended in order when present (feature_processor.py:330-363); merchant_avg_amount is 0 on
+  // this path, so there is no amount_to_merchant_avg_ratio
+  const bool pres[6] = {amount > 0, uavg > 0, c24 > 0, true, true, true};
+  const float dv[6] = {clip10(sqrt(amount)), clip10(amount / uavg), clip10(c1 / (c24 / 24)), clip10((0.5 + ip) / 2),
+                       (9 <= hour && hour <= 17) ? 1.f : 0.f, (hour < 6 || hour > 22) ? 1.f : 0.f};
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    if (pres[i]) {
+#pragma unroll
+      for (int m = 0; m < 6; ++m)
+        if (m == k) o[41 + m] = dv[i];
+      ++k;
+    }
+  }
+  float4* o4 = reinterpret_cast<float4*>(out);
+#pragma unroll
+  for (int q = 0; q < FD_VECTOR_WIDTH / 4; ++q) o4[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
 }
 
 // per-event LSTM input: the bridged raw feature, NaN (null) -> 0, then sign(x) * log1p(|x|) in f64,
@@ -286,17 +283,24 @@ __global__ void __launch_bounds__(256) feat_process_kernel(CardHeader* H, const 
       last_ts = ts;
       has_ts = 1;
     } else {
-      for (int e = 0; e < ring_n; ++e) {
-        const RingEvent ev = rg[e];
-        if (ev.ts <= ts) {
-          if (ts - 300000LL < ev.ts) c0 += 1;
-          if (ts - 3600000LL < ev.ts) {
-            c1 += 1;
-            s1 += ev.cents;
-          }
-          if (ts - 86400000LL < ev.ts) {
-            c2 += 1;
-            s2 += ev.cents;
+      // 8 events per round trip: the loads of a group are independent (slots past ring_n are read
+      // from the allocated ring and ignored)
+      for (int e0 = 0; e0 < ring_n; e0 += 8) {
+        RingEvent ev[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ev[u] = rg[min(e0 + u, K - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (e0 + u < ring_n && ev[u].ts <= ts) {
+            if (ts - 300000LL < ev[u].ts) c0 += 1;
+            if (ts - 3600000LL < ev[u].ts) {
+              c1 += 1;
+              s1 += ev[u].cents;
+            }
+            if (ts - 86400000LL < ev[u].ts) {
+              c2 += 1;
+              s2 += ev[u].cents;
+            }
           }
         }
       }
@@ -312,9 +316,9 @@ __global__ void __launch_bounds__(256) feat_process_kernel(CardHeader* H, const 
     r[14] = mult;
     r[15] = has_user ? (double)uage : 0.0;
     if (raw_out) {
-      double* ro = raw_out + (size_t)best * FD_RAW_FEATURES;
+      double2* ro = reinterpret_cast<double2*>(raw_out + (size_t)best * FD_RAW_FEATURES);
 #pragma unroll
-      for (int c = 0; c < FD_RAW_FEATURES; ++c) ro[c] = r[c];
+      for (int c = 0; c < FD_RAW_FEATURES / 2; ++c) ro[c] = make_double2(r[2 * c], r[2 * c + 1]);
     }
     write_vector(r, vec_out + (size_t)best * FD_VECTOR_WIDTH);
     if (S) {  // LSTM head input: this event appended to the card's history, last S events emitted

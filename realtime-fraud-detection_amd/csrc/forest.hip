@@ -1064,6 +1064,156 @@ forest_kernel5(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 }
 
 // ------------------------------------------------------------------------------------------------
+// Small-batch (latency) path: tree-split over workgroups. A 1k micro-batch is 4 tiles, so the
+// tile-per-workgroup kernels keep 4 CUs busy for the whole forest (~90 us for 500 x depth 8). Here
+//   split_bin_kernel   : every feature value -> its bin word once, feature-major [nf][n_pad] in HBM,
+//                        plus a per-tile "has NaN" flag;
+//   split_walk_kernel  : grid (tiles, chunk groups): kernel 4's walk over the group's chunks; the bin
+//                        rows of the tile arrive by LDS-DMA (1 KiB per feature row), every leaf value
+//                        goes to a [tree][n] scratch in HBM (and the leaf id when asked);
+//   split_sum_kernel   : per transaction, base margin + the leaf values in tree order (the
+//                        reference's sequential f32 / f64 sum, bit for bit), then the outputs.
+constexpr int kSplitBin = 256;
+
+// one thread per (feature, transaction): the binary search's dependent loads are the only latency
+__global__ void __launch_bounds__(kSplitBin)
+split_bin_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, int nf, const float* __restrict__ thr,
+                 const int32_t* __restrict__ thr_off, int bin_steps, uint32_t* __restrict__ bins,
+                 uint32_t* __restrict__ tile_nan, uint32_t epoch) {
+  const int64_t r = (int64_t)blockIdx.x * kSplitBin + threadIdx.x;  // row within [0, n_pad)
+  const int f = blockIdx.y;
+  const bool ok = r < n;
+  float v = 0.f;
+  if (ok) v = f < ld ? X[r * (int64_t)ld + f] : __builtin_nanf("");  // DMatrix: missing column = NaN
+  const int o = thr_off[f], cnt = thr_off[f + 1] - o;
+  int pos = 0;
+  for (int st = bin_steps; st > 0; st >>= 1) {
+    const int np = pos + st;
+    if (np <= cnt && thr[o + np - 1] <= v) pos = np;
+  }
+  const bool isnan_v = ok && v != v;
+  bins[(size_t)f * n_pad + r] = !ok ? 0u : (isnan_v ? 0xFFFF0000u : (uint32_t)pos << 16);
+  // tile flag = this call's epoch when the tile holds a NaN (no per-call clearing of the flags)
+  if (__ballot(isnan_v) != 0ull && (threadIdx.x & 63) == 0) atomicMax(&tile_nan[r / kTile], epoch);
+}
+
+// Stage `rows` rows of 1 KiB (row r at src + r * row_stride) into LDS at dst + r * 1024 by LDS-DMA.
+__device__ __forceinline__ void stage_rows_asm(const char* __restrict__ src, size_t row_stride, uint32_t dst, int rows,
+                                               int nwaves) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int p = wave; p < rows; p += nwaves) {
+    const char* g = src + (size_t)p * row_stride + lane * 16;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(dst + ((uint32_t)p << 10));
+    asm volatile(
+        "s_mov_b32 m0, %0\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off"
+        :
+        : "s"(m0), "v"(g)
+        : "memory", "m0");
+  }
+}
+
+template <int D, int CH, typename LeafT>
+__global__ void __launch_bounds__(kWG3)
+split_walk_kernel(const uint32_t* __restrict__ bins, int64_t n, int64_t n_pad, int nf,
+                  const uint32_t* __restrict__ tile_nan, uint32_t epoch, const char* __restrict__ blob, int n_chunks,
+                  int chunk_stride, int chunks_per_group, const int32_t* __restrict__ leaf_ids, int n_trees,
+                  LeafT* __restrict__ leaves, int32_t* __restrict__ out_leaf) {
+  constexpr int TPG = CH / 4;
+  constexpr int NL = 1 << D;
+  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
+  const uint32_t s0 = (sdyn + 1023u) & ~1023u;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int gg = wave >> 2;
+  const int txn = ((wave & 3) << 6) + lane;
+  const uint32_t lane4 = s0 + (uint32_t)txn * 4u;
+  const uint32_t bufA = s0 + (uint32_t)nf * 1024u, bufB = bufA + (uint32_t)chunk_stride;
+  const int tile = blockIdx.x;
+  const int64_t row = (int64_t)tile * kTile + txn;
+  const int k0 = blockIdx.y * chunks_per_group;
+  const int k1 = min(n_chunks, k0 + chunks_per_group);
+  if (k0 >= k1) return;  // uniform per workgroup
+  stage_rows_asm(reinterpret_cast<const char*>(bins + (size_t)tile * kTile), (size_t)n_pad * 4u, s0, nf, kWG3 / 64);
+  stage_chunk_asm(blob + (size_t)k0 * chunk_stride, bufA, chunk_stride, kWG3 / 64);
+  const bool tile_has_nan = tile_nan[tile] == epoch;
+  dma_wait();
+  __syncthreads();
+  for (int k = k0; k < k1; ++k) {
+    const uint32_t cur = ((k - k0) & 1) ? bufB : bufA;
+    if (k + 1 < k1)
+      stage_chunk_asm(blob + (size_t)(k + 1) * chunk_stride, ((k - k0) & 1) ? bufA : bufB, chunk_stride, kWG3 / 64);
+    uint32_t slots[TPG];
+    if (tile_has_nan)
+      walk4<D, TPG, LeafT, true>(cur, gg, lane4, slots);
+    else
+      walk4<D, TPG, LeafT, false>(cur, gg, lane4, slots);
+#pragma unroll
+    for (int j = 0; j < TPG; ++j) {
+      const int c = gg * TPG + j;
+      const int tg = k * CH + c;
+      const uint32_t tb = cur + (uint32_t)c * TB;
+      if (row < n && tg < n_trees) {
+        leaves[(size_t)tg * n + row] = lds_load<LeafT>(tb + NL * 4u + slots[j] * sizeof(LeafT));
+        if (out_leaf != nullptr) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slots[j]];
+      }
+    }
+    dma_wait();
+    __syncthreads();
+  }
+}
+
+// 32 transactions per workgroup: all 256 threads stream a [trees][32] block of leaf values into LDS
+// (independent coalesced loads), then 32 threads add them in tree order (the sequential sum)
+constexpr int kSumRows = 32;
+
+template <int KIND, typename LeafT>
+__global__ void __launch_bounds__(256)
+split_sum_kernel(const LeafT* __restrict__ leaves, int64_t n, int n_trees, float base_margin, double if_offset,
+                 double if_denom, double* __restrict__ out_prob, double* __restrict__ out_raw) {
+  constexpr int kTc = 65536 / (kSumRows * (int)sizeof(LeafT));  // trees per LDS block (64 KiB)
+  __shared__ LeafT blk[kTc * kSumRows];
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * kSumRows;
+  const int rows = (int)min<int64_t>(kSumRows, n - r0);
+  LeafT acc = (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0;
+  for (int t0 = 0; t0 < n_trees; t0 += kTc) {
+    const int tc = min(kTc, n_trees - t0);
+    const int total = tc * kSumRows;
+    for (int base = 0; base < total; base += 256 * 16) {  // 16 independent loads in flight per thread
+      LeafT v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = base + u * 256 + tid;
+        const int t = i / kSumRows, r = i - t * kSumRows;
+        v[u] = (i < total && r < rows) ? leaves[(size_t)(t0 + t) * n + r0 + r] : (LeafT)0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = base + u * 256 + tid;
+        if (i < total) blk[i] = v[u];
+      }
+    }
+    __syncthreads();
+    if (tid < rows) {
+      int t = 0;
+      for (; t + 16 <= tc; t += 16) {
+        LeafT v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = blk[(t + u) * kSumRows + tid];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += v[u];
+      }
+      for (; t < tc; ++t) acc += blk[t * kSumRows + tid];
+    }
+    __syncthreads();
+  }
+  if (tid < rows) write_outputs<KIND, LeafT>(acc, r0 + tid, if_offset, if_denom, out_prob, out_raw);
+}
+
+// ------------------------------------------------------------------------------------------------
 // dispatch
 
 using KernelFn = void (*)(const float*, int64_t, int, int, const char*, int, int, const int32_t*, int,
@@ -1191,6 +1341,74 @@ KernelFn4 pick5(int D, int CH, bool spec) {
   }
 }
 
+template <int D, typename LeafT>
+void* pick_split_ch(int CH) {
+  switch (CH) {
+    case 4: return (void*)split_walk_kernel<D, 4, LeafT>;
+    case 8: return (void*)split_walk_kernel<D, 8, LeafT>;
+    case 12: return (void*)split_walk_kernel<D, 12, LeafT>;
+    case 16: return (void*)split_walk_kernel<D, 16, LeafT>;
+    default: return nullptr;
+  }
+}
+
+template <typename LeafT>
+void* pick_split(int D, int CH) {
+  switch (D) {
+    case 1: return pick_split_ch<1, LeafT>(CH);
+    case 2: return pick_split_ch<2, LeafT>(CH);
+    case 3: return pick_split_ch<3, LeafT>(CH);
+    case 4: return pick_split_ch<4, LeafT>(CH);
+    case 5: return pick_split_ch<5, LeafT>(CH);
+    case 6: return pick_split_ch<6, LeafT>(CH);
+    case 7: return pick_split_ch<7, LeafT>(CH);
+    case 8: return pick_split_ch<8, LeafT>(CH);
+    default: return nullptr;
+  }
+}
+
+// small-batch launch: bin once, walk (tiles x chunk groups), sequential sum
+template <typename LeafT, int KIND>
+void launch_split(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld, double* d_prob,
+                  double* d_raw, int32_t* d_leaf, int64_t tiles, hipStream_t stream) {
+  const int64_t n_pad = tiles * kTile;
+  SplitScratch& sc = pf.split;  // per forest: two forests may run concurrently on different streams
+  sc.bins.ensure((size_t)pf.num_feature * n_pad * 4);
+  if (sc.nan.bytes < (size_t)tiles * 4) {
+    sc.nan.ensure((size_t)tiles * 4);
+    FD_HIP(hipMemsetAsync(sc.nan.ptr, 0, sc.nan.bytes, stream));
+    sc.epoch = 0;
+  }
+  sc.epoch = (sc.epoch == 0xffffffffu) ? 1u : sc.epoch + 1u;
+  if (sc.epoch == 1u) FD_HIP(hipMemsetAsync(sc.nan.ptr, 0, sc.nan.bytes, stream));
+  sc.leaves.ensure((size_t)pf.n_trees * n * sizeof(LeafT));
+  hipLaunchKernelGGL(split_bin_kernel, dim3((unsigned)(n_pad / kSplitBin), (unsigned)pf.num_feature), dim3(kSplitBin), 0,
+                     stream, d_X, n, n_pad, (int)ld, pf.num_feature, pf.b_thr.as<const float>(),
+                     pf.b_thr_off.as<const int32_t>(), pf.bin_steps, sc.bins.as<uint32_t>(), sc.nan.as<uint32_t>(),
+                     sc.epoch);
+  FD_HIP(hipGetLastError());
+  // chunk groups: enough workgroups to cover the CUs (tiles x groups >= 256)
+  const int want = (int)std::max<int64_t>(1, (256 + tiles - 1) / tiles);
+  const int cpg = std::max(1, (pf.b_n_chunks + want - 1) / want);
+  const int groups = (pf.b_n_chunks + cpg - 1) / cpg;
+  void* fn = pick_split<LeafT>(pf.depth, pf.b_chunk);
+  FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no split forest kernel for this depth/chunk");
+  const size_t lds = (size_t)pf.num_feature * 1024 + 2 * pf.b_chunk_stride + 1024;
+  FD_REQUIRE(lds <= kLdsBudget, FD_ERR_UNSUPPORTED, "split forest kernel exceeds the LDS budget");
+  FD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  using WalkFn = void (*)(const uint32_t*, int64_t, int64_t, int, const uint32_t*, uint32_t, const char*, int, int, int,
+                          const int32_t*, int, LeafT*, int32_t*);
+  hipLaunchKernelGGL((WalkFn)fn, dim3((unsigned)tiles, (unsigned)groups), dim3(kWG3), lds, stream,
+                     sc.bins.as<const uint32_t>(), n, n_pad, pf.num_feature, sc.nan.as<const uint32_t>(), sc.epoch,
+                     pf.b_blob.as<const char>(), pf.b_n_chunks, (int)pf.b_chunk_stride, cpg,
+                     pf.leaf_ids.as<const int32_t>(), pf.n_trees, sc.leaves.as<LeafT>(), d_leaf);
+  FD_HIP(hipGetLastError());
+  hipLaunchKernelGGL((split_sum_kernel<KIND, LeafT>), dim3((unsigned)((n + kSumRows - 1) / kSumRows)), dim3(256), 0,
+                     stream, sc.leaves.as<const LeafT>(), n, pf.n_trees, pf.base_margin, pf.if_offset,
+                     pf.if_denominator, d_prob, d_raw);
+  FD_HIP(hipGetLastError());
+}
+
 }  // namespace
 
 #ifdef FD_FOREST_PROFILE
@@ -1201,10 +1419,11 @@ extern "C" __attribute__((visibility("default"))) int fd_debug_forest_profile(un
 
 // Kernel choice (option "forest_kernel"): 0 auto = kernel 4 when the binned layout exists (depth <= 8,
 // <= 65534 distinct thresholds per feature), else kernel 3 (depth <= 8), else kernel 1; 1/2/3 force
-// kernel 1/3/4, 4/5 force kernel 5 (plain / speculative-children walk) (FD_ERR_UNSUPPORTED when the
-// forest cannot use it).
+// kernel 1/3/4, 4/5 force kernel 5 (plain / speculative-children walk), 6 forces the tree-split
+// small-batch path, which auto also takes below kSplitTiles tiles (FD_ERR_UNSUPPORTED when the forest
+// cannot use it).
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
-                   double* d_prob, double* d_raw, int32_t* d_leaf) {
+                   double* d_prob, double* d_raw, int32_t* d_leaf, hipStream_t stream) {
   FD_REQUIRE(d_X && d_prob && ld > 0, FD_ERR_INVALID_ARG, "null buffer or bad ld");
   if (n == 0) return;
   const bool xgb = pf.kind == FD_FOREST_XGB_BINARY_LOGISTIC;
@@ -1212,8 +1431,23 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   const int64_t blocks = (n + kTile - 1) / kTile;
   FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
   const int v = e.forest_variant;
-  FD_REQUIRE(v >= 0 && v <= 5, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..5");
+  FD_REQUIRE(v >= 0 && v <= 6, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..6");
   Engine::Timed* ev = nullptr;
+
+  // small batches: tree-split latency path (option 6 forces it; auto below 128 tiles)
+  const bool ok_split = pf.binned && pf.depth <= 8 && pf.b_chunk % 4 == 0;
+  if (v == 6) FD_REQUIRE(ok_split, FD_ERR_UNSUPPORTED, "the split forest path needs the binned layout (depth <= 8)");
+  if ((v == 6 || (v == 0 && blocks < kSplitTiles)) && ok_split) {
+    const hipStream_t st = stream ? stream : e.stream;
+    ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
+    if (ev) FD_HIP(hipEventRecord(ev->a, st));
+    if (xgb)
+      launch_split<float, FD_FOREST_XGB_BINARY_LOGISTIC>(e, pf, d_X, n, ld, d_prob, d_raw, d_leaf, blocks, st);
+    else
+      launch_split<double, FD_FOREST_SKLEARN_IFOREST>(e, pf, d_X, n, ld, d_prob, d_raw, d_leaf, blocks, st);
+    if (ev) FD_HIP(hipEventRecord(ev->b, st));
+    return;
+  }
 
   if (v == 4 || v == 5) {  // forest_kernel5 on kernel 4's binned blob
     const uint32_t lds5 =

@@ -130,7 +130,7 @@ def test_kernel5_depths(engine, depth):
 
 
 @pytest.mark.parametrize("max_bin", [256, None])
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
 def test_kernel_variants_agree(engine, variant, max_bin):
     """Every forest kernel (256-thread; 1024-thread tree-split on the threshold layout; 1024-thread on
     the binned layout) gives the oracle's bits, for hist-style and raw-valued split thresholds."""
