@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 4
+#define FD_ABI_VERSION 5
 
 enum fd_status {
   FD_OK = 0,
@@ -216,6 +216,74 @@ typedef struct {
    vectors (n x 64 f32) and optionally the bridged raw features (n x FD_RAW_FEATURES f64). */
 int fd_features_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* d_vectors, double* d_raw);
 int fd_features_host(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* vectors, double* raw);
+
+/* ---------------------------------------------------------------- full feature map + rule scores (a3, (f)) */
+/* FeatureExtractor.extractAllFeatures as a whole (fl/features/FeatureExtractor.java:50-493): the 64
+   features of FeatureStore.getRegisteredFeatures (fl/features/FeatureStore.java:325-365, that order),
+   f64, NaN where the Java map would have no key; string features as the host's vocabulary codes
+   (FD_CODE_UNKNOWN for the literal "unknown"). Plus the Flink rule scores that consume them:
+   FeatureEnrichmentProcessor (calculateFeatureBasedFraudScore, combine with the incoming score,
+   updateRiskLevel; fl/processors/FeatureEnrichmentProcessor.java:80-93,122-367) and TransactionProcessor
+   (calculateBasicFeatures, applyFraudDetectionRules, makeFinalDecision with minimal profiles for
+   unknown users / merchants; fl/processors/TransactionProcessor.java:143-508). */
+#define FD_FEATURE_MAP_WIDTH 64
+#define FD_CODE_UNKNOWN 254
+/* per-transaction context beyond fd_txn_batch; any pointer may be NULL (= all null) */
+typedef struct {
+  const double* geo_lat;          /* Transaction.geolocation lat / lon, NaN = absent */
+  const double* geo_lon;
+  const double* merchant_lat;     /* Transaction.merchantLocation lat / lon, NaN = absent */
+  const double* merchant_lon;
+  const uint8_t* payment_method;  /* vocabulary code, 255 = null */
+  const uint8_t* transaction_type;
+  const uint8_t* card_type;
+  const uint8_t* user_agent_flag; /* analyzeSuspiciousUserAgent (host-side string test), 255 = null UA */
+  const double* fraud_score;      /* incoming Transaction.fraudScore, NaN = null */
+} fd_txn_context;
+typedef struct {
+  double tp_score;      /* TransactionProcessor fraud score */
+  double fe_score;      /* FeatureEnrichmentProcessor fraud score */
+  uint8_t tp_decision;  /* enum fd_decision */
+  uint8_t tp_risk;      /* enum fd_risk */
+  uint8_t fe_decision;
+  uint8_t fe_risk;
+  uint8_t pad[4];
+} fd_rule_scores;
+/* UserProfile fields beyond fd_users (simulator.py:40-58); keyed like fd_users; NULL arrays = null */
+typedef struct {
+  int64_t n;
+  const uint64_t* key;
+  const double* risk_score;        /* NaN = null */
+  const uint8_t* kyc_status;       /* vocabulary code, 255 = null */
+  const uint8_t* verified;         /* UserProfile.isVerified() */
+  const int8_t* pref_start;        /* preferred hours, -1 = null */
+  const int8_t* pref_end;
+  const double* weekend_activity;  /* behavioral pattern values, NaN = absent */
+  const double* online_preference;
+  const double* intl_preference;   /* international_transactions, NaN = null */
+  const int32_t* txn_frequency;    /* -1 = null */
+  const uint8_t* has_patterns;     /* getBehavioralPatterns() != null */
+} fd_users_ext;
+/* MerchantProfile fields beyond fd_merchants (simulator.py:60-75), indexed like fd_merchants */
+typedef struct {
+  int64_t n;
+  const double* avg_amount;           /* NaN = null */
+  const uint8_t* risk_level;          /* 0 low, 1 medium, 2 high (vocabulary), 255 = null */
+  const uint8_t* blacklisted;         /* 255 = null */
+  const uint8_t* category;            /* vocabulary code, 255 = null */
+  const uint8_t* high_risk_category;  /* MerchantProfile.isHighRiskCategory() */
+  const uint8_t* open_hour;           /* operating hours [open, close), 255 = null */
+  const uint8_t* close_hour;
+  const uint8_t* suspicious_name;     /* analyzeMerchantName (host regexes), 255 = null name */
+} fd_merchants_ext;
+int fd_state_load_users_ext_host(fd_engine* eng, const fd_users_ext* users);
+int fd_load_merchants_ext_host(fd_engine* eng, const fd_merchants_ext* merchants);
+/* 256 flags each: payment-method code -> isHighRiskPaymentMethod, transaction-type code -> "refund" */
+int fd_load_vocab_host(fd_engine* eng, const uint8_t* payment_high_risk, const uint8_t* type_is_refund);
+/* fd_features_* plus the feature map (n x FD_FEATURE_MAP_WIDTH f64) and rule scores; d_fmap / d_rules /
+   d_raw may be NULL. Advances the card state exactly like fd_features_device. */
+int fd_features_full_device(fd_engine* eng, const fd_txn_batch* txns, const fd_txn_context* ctx, int64_t n,
+                            float* d_vectors, double* d_raw, double* d_fmap, fd_rule_scores* d_rules);
 
 /* ---------------------------------------------------------------- LSTM sequence head (a10) */
 /* Replaces _load_tensorflow_model / _predict_tensorflow (ml/models/model_manager.py:162-165, 313-319)

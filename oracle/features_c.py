@@ -21,6 +21,8 @@ def register(L) -> None:
     L.orc_state_load_merchants.argtypes = [vp, i64, vp, vp]
     L.orc_features_run.restype = C.c_int
     L.orc_features_run.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.orc_features_run_ex.restype = C.c_int
+    L.orc_features_run_ex.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.orc_vector_from_raw.restype = None
     L.orc_vector_from_raw.argtypes = [vp, vp]
 
@@ -54,6 +56,20 @@ class OracleFeatureState:
     def load_merchants(self, fraud_rate, risk_mult):
         fr, m = _c(fraud_rate, np.float64), _c(risk_mult, np.float64)
         assert self.L.orc_state_load_merchants(self.h, len(fr), fr.ctypes.data, m.ctypes.data) == 0
+
+    def run_ex(self, txns: dict):
+        """-> (raw [n,16], vectors [n,64], velocity_5min_amount [n])."""
+        cols = [_c(txns["card_key"], np.uint64), _c(txns["ts_ms"], np.int64), _c(txns["amount_cents"], np.int64),
+                _c(txns["merchant"], np.int32), _c(txns["device_fp"], np.uint64), _c(txns["ip_class"], np.uint8),
+                _c(txns["hour"], np.uint8), _c(txns["weekend"], np.uint8)]
+        n = len(cols[0])
+        raw = np.empty((n, RAW), np.float64)
+        vec = np.empty((n, VEC), np.float32)
+        vel5 = np.empty(n, np.float64)
+        rc = self.L.orc_features_run_ex(self.h, n, *[c.ctypes.data for c in cols], raw.ctypes.data, vec.ctypes.data,
+                                        vel5.ctypes.data)
+        assert rc == 0
+        return raw, vec, vel5
 
     def run(self, txns: dict, want_raw: bool = True):
         cols = [_c(txns["card_key"], np.uint64), _c(txns["ts_ms"], np.int64), _c(txns["amount_cents"], np.int64),

@@ -207,9 +207,10 @@ void orc_vector_from_raw(const double* r, float* out) {
   }
 }
 
-int orc_features_run(void* p, int64_t n, const uint64_t* key, const int64_t* ts, const int64_t* cents,
-                     const int32_t* merchant, const uint64_t* dfp, const uint8_t* ipc, const uint8_t* hour_in,
-                     const uint8_t* wk_in, double* raw_out, float* vec_out) {
+/* also returns velocity_5min_amount (5-minute window sum / 100) per transaction when vel5_out != NULL */
+int orc_features_run_ex(void* p, int64_t n, const uint64_t* key, const int64_t* ts, const int64_t* cents,
+                        const int32_t* merchant, const uint64_t* dfp, const uint8_t* ipc, const uint8_t* hour_in,
+                        const uint8_t* wk_in, double* raw_out, float* vec_out, double* vel5_out) {
   orc_state* s = p;
   const int64_t W[3] = {300000, 3600000, 86400000};
   for (int64_t i = 0; i < n; ++i) {
@@ -282,6 +283,13 @@ int orc_features_run(void* p, int64_t n, const uint64_t* key, const int64_t* ts,
     r[15] = s->has_user[j] ? s->age[j] : 0;
     if (raw_out) memcpy(raw_out + i * ORC_RAW, r, sizeof(r));
     if (vec_out) orc_vector_from_raw(r, vec_out + i * ORC_VEC);
+    if (vel5_out) vel5_out[i] = (double)sm[0] / 100.0;
   }
   return 0;
+}
+
+int orc_features_run(void* p, int64_t n, const uint64_t* key, const int64_t* ts, const int64_t* cents,
+                     const int32_t* merchant, const uint64_t* dfp, const uint8_t* ipc, const uint8_t* hour_in,
+                     const uint8_t* wk_in, double* raw_out, float* vec_out) {
+  return orc_features_run_ex(p, n, key, ts, cents, merchant, dfp, ipc, hour_in, wk_in, raw_out, vec_out, NULL);
 }

@@ -221,6 +221,7 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipStreamDestroy(e.aux2_stream);
     (void)hipEventDestroy(e.join2_ev);
   }
+  for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
   for (auto* b : {&e.state.headers, &e.state.fps, &e.state.ring, &e.state.merchants, &e.state.slot,
                   &e.state.next, &e.state.err})
     b->release();
@@ -272,6 +273,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   if (k == "forest_kernel") {
     FD_REQUIRE(value >= 0 && value <= 6, FD_ERR_INVALID_ARG, "forest_kernel must be in 0..6");
     e.forest_variant = (int)value;
+  } else if (k == "rule_fraud_threshold_permille") {  // JobConfig.fraudThreshold x 1000
+    FD_REQUIRE(value >= 0 && value <= 1000, FD_ERR_INVALID_ARG, "rule_fraud_threshold_permille must be in 0..1000");
+    e.state.tp_threshold = (double)value / 1000.0;
   } else {
     throw fd::Error(FD_ERR_INVALID_ARG, "unknown option: " + k);
   }
@@ -596,6 +600,41 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
   fd::launch_features(e, *txns, n, vec, nullptr, seq);
   score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
                d_confidence, d_decision, d_risk, seq, e.state.S);
+  FD_API_END
+}
+
+int fd_state_load_users_ext_host(fd_engine* eng, const fd_users_ext* users) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(users, FD_ERR_INVALID_ARG, "null users");
+  fd::load_users_ext(e, *users);
+  FD_API_END
+}
+
+int fd_load_merchants_ext_host(fd_engine* eng, const fd_merchants_ext* merchants) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(merchants, FD_ERR_INVALID_ARG, "null merchants");
+  FD_HIP(hipStreamSynchronize(e.stream));
+  fd::load_merchants_ext(e, *merchants);
+  FD_API_END
+}
+
+int fd_load_vocab_host(fd_engine* eng, const uint8_t* payment_high_risk, const uint8_t* type_is_refund) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_HIP(hipStreamSynchronize(e.stream));
+  fd::load_vocab(e, payment_high_risk, type_is_refund);
+  FD_API_END
+}
+
+int fd_features_full_device(fd_engine* eng, const fd_txn_batch* txns, const fd_txn_context* ctx, int64_t n,
+                            float* d_vectors, double* d_raw, double* d_fmap, fd_rule_scores* d_rules) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
+  const fd_txn_context none{};
+  fd::launch_features_full(e, *txns, ctx ? *ctx : none, n, d_vectors, d_raw, d_fmap, d_rules);
   FD_API_END
 }
 

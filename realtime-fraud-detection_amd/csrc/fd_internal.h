@@ -134,6 +134,10 @@ struct CardStore {
   unsigned epoch = 0;
   int64_t n_merchants = 0;
   DeviceBuffer headers, fps, ring, merchants, slot, next, err, seq;
+  DeviceBuffer uext, mext, vocab;  // extended profiles + vocabulary flags (feature map, rule scores)
+  int64_t n_mext = 0;
+  bool vocab_loaded = false;
+  double tp_threshold = 0.7;  // JobConfig.fraudThreshold (fl/config/JobConfig.java:47)
 };
 
 struct Engine {
@@ -148,7 +152,7 @@ struct Engine {
   hipStream_t aux2_stream = nullptr;           // small batches: the second forest, concurrent with the first
   hipEvent_t join2_ev = nullptr;
   DeviceBuffer seq_buf;                        // per-txn LSTM input sequences of the fused path
-  DeviceBuffer feat_vec, feat_in;  // host-API / fused-pipeline staging for features
+  DeviceBuffer feat_vec, feat_in, feat_ext;  // host-API / fused-pipeline staging for features
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
@@ -193,7 +197,12 @@ int64_t state_count(Engine& e);
 void load_users(Engine& e, const fd_users& u);
 void load_merchants(Engine& e, const fd_merchants& m);
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw,
-                     float* d_seq = nullptr);
+                     float* d_seq = nullptr, double* d_vel5 = nullptr);
+void load_users_ext(Engine& e, const fd_users_ext& u);
+void load_merchants_ext(Engine& e, const fd_merchants_ext& m);
+void load_vocab(Engine& e, const uint8_t* pay_high_risk, const uint8_t* type_refund);
+void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context& c, int64_t n, float* d_vec,
+                          double* d_raw, double* d_fmap, fd_rule_scores* d_rules);
 void features_check(Engine& e);
 // route.hip
 unsigned shard_of_host(unsigned long long key, unsigned G);

@@ -88,6 +88,37 @@ class fd_state_params(C.Structure):
     _fields_ = [("capacity", C.c_int64), ("window_mode", C.c_int32), ("ring_k", C.c_int32), ("seq_len", C.c_int32)]
 
 
+class fd_txn_context(C.Structure):
+    _fields_ = [("geo_lat", C.c_void_p), ("geo_lon", C.c_void_p), ("merchant_lat", C.c_void_p),
+                ("merchant_lon", C.c_void_p), ("payment_method", C.c_void_p), ("transaction_type", C.c_void_p),
+                ("card_type", C.c_void_p), ("user_agent_flag", C.c_void_p), ("fraud_score", C.c_void_p)]
+
+
+class fd_users_ext(C.Structure):
+    _fields_ = [("n", C.c_int64), ("key", C.c_void_p), ("risk_score", C.c_void_p), ("kyc_status", C.c_void_p),
+                ("verified", C.c_void_p), ("pref_start", C.c_void_p), ("pref_end", C.c_void_p),
+                ("weekend_activity", C.c_void_p), ("online_preference", C.c_void_p), ("intl_preference", C.c_void_p),
+                ("txn_frequency", C.c_void_p), ("has_patterns", C.c_void_p)]
+
+
+class fd_merchants_ext(C.Structure):
+    _fields_ = [("n", C.c_int64), ("avg_amount", C.c_void_p), ("risk_level", C.c_void_p), ("blacklisted", C.c_void_p),
+                ("category", C.c_void_p), ("high_risk_category", C.c_void_p), ("open_hour", C.c_void_p),
+                ("close_hour", C.c_void_p), ("suspicious_name", C.c_void_p)]
+
+
+CTX_FIELDS = ("geo_lat", "geo_lon", "merchant_lat", "merchant_lon", "payment_method", "transaction_type",
+              "card_type", "user_agent_flag", "fraud_score")
+USER_EXT_FIELDS = ("risk_score", "kyc_status", "verified", "pref_start", "pref_end", "weekend_activity",
+                   "online_preference", "intl_preference", "txn_frequency", "has_patterns")
+MERCHANT_EXT_FIELDS = ("avg_amount", "risk_level", "blacklisted", "category", "high_risk_category", "open_hour",
+                       "close_hour", "suspicious_name")
+FD_FEATURE_MAP_WIDTH = 64
+FD_CODE_UNKNOWN = 254
+RULE_DTYPE = [("tp_score", "<f8"), ("fe_score", "<f8"), ("tp_decision", "u1"), ("tp_risk", "u1"),
+              ("fe_decision", "u1"), ("fe_risk", "u1"), ("pad", "u1", 4)]
+
+
 class fd_lstm_params(C.Structure):
     _fields_ = [("input_size", C.c_int32), ("hidden", C.c_int32), ("n_out", C.c_int32), ("w_ih", C.c_void_p),
                 ("w_hh", C.c_void_p), ("b_ih", C.c_void_p), ("b_hh", C.c_void_p), ("w_out", C.c_void_p),
@@ -159,6 +190,11 @@ SIGNATURES = {
     "fd_features_host": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _vp, _vp]),
     "fd_score_batch_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, C.POINTER(_vp), _vp,
                                         C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fd_state_load_users_ext_host": (C.c_int, [_vp, C.POINTER(fd_users_ext)]),
+    "fd_load_merchants_ext_host": (C.c_int, [_vp, C.POINTER(fd_merchants_ext)]),
+    "fd_load_vocab_host": (C.c_int, [_vp, _vp, _vp]),
+    "fd_features_full_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_txn_context), _i64, _vp, _vp,
+                                          _vp, _vp]),
     "fd_load_lstm": (C.c_int, [_vp, C.POINTER(fd_lstm_params)]),
     "fd_unload_lstm": (C.c_int, [_vp]),
     "fd_lstm_predict_device": (C.c_int, [_vp, _vp, _i64, _i32, _vp]),

@@ -197,6 +197,46 @@ class FraudEngine:
         N.call("fd_features_seq_device", self._h, C.byref(b), int(n), C.c_void_p(vec_ptr),
                C.c_void_p(raw_ptr) if raw_ptr else None, C.c_void_p(seq_ptr) if seq_ptr else None)
 
+    # ------------------------------------------------------------------ full feature map + rule scores
+    _USER_EXT_DT = {"risk_score": np.float64, "kyc_status": np.uint8, "verified": np.uint8, "pref_start": np.int8,
+                    "pref_end": np.int8, "weekend_activity": np.float64, "online_preference": np.float64,
+                    "intl_preference": np.float64, "txn_frequency": np.int32, "has_patterns": np.uint8}
+    _MERCH_EXT_DT = {"avg_amount": np.float64, "risk_level": np.uint8, "blacklisted": np.uint8, "category": np.uint8,
+                     "high_risk_category": np.uint8, "open_hour": np.uint8, "close_hour": np.uint8,
+                     "suspicious_name": np.uint8}
+
+    def load_users_ext(self, key, **fields) -> None:
+        """Extended UserProfile fields (fd_users_ext); omitted fields are null."""
+        keep = {"key": np.ascontiguousarray(key, np.uint64)}
+        for f, dt in self._USER_EXT_DT.items():
+            if fields.get(f) is not None:
+                keep[f] = np.ascontiguousarray(fields[f], dt)
+        u = N.fd_users_ext(len(keep["key"]), keep["key"].ctypes.data,
+                           *[keep[f].ctypes.data if f in keep else None for f in N.USER_EXT_FIELDS])
+        N.call("fd_state_load_users_ext_host", self._h, C.byref(u))
+
+    def load_merchants_ext(self, n: int, **fields) -> None:
+        keep = {f: np.ascontiguousarray(fields[f], dt) for f, dt in self._MERCH_EXT_DT.items()
+                if fields.get(f) is not None}
+        m = N.fd_merchants_ext(int(n), *[keep[f].ctypes.data if f in keep else None for f in N.MERCHANT_EXT_FIELDS])
+        N.call("fd_load_merchants_ext_host", self._h, C.byref(m))
+
+    def load_vocab(self, payment_high_risk, type_is_refund) -> None:
+        a = np.ascontiguousarray(payment_high_risk, np.uint8)
+        b = np.ascontiguousarray(type_is_refund, np.uint8)
+        assert len(a) == 256 and len(b) == 256
+        N.call("fd_load_vocab_host", self._h, _ptr(a), _ptr(b))
+
+    def features_full_device(self, txn_ptrs: dict, ctx_ptrs: Optional[dict], n: int, vec_ptr: int, fmap_ptr: int = 0,
+                             rules_ptr: int = 0, raw_ptr: int = 0) -> None:
+        """features_device plus the 64-wide FeatureExtractor map (f64) and the rule scores
+        (N.RULE_DTYPE records); ctx_ptrs: field -> device pointer (N.CTX_FIELDS), missing = null."""
+        b = N.fd_txn_batch(*[int(txn_ptrs[f]) for f in N.TXN_FIELDS])
+        cx = N.fd_txn_context(*[int(ctx_ptrs[f]) if ctx_ptrs and ctx_ptrs.get(f) else None for f in N.CTX_FIELDS])
+        opt = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        N.call("fd_features_full_device", self._h, C.byref(b), C.byref(cx), int(n), C.c_void_p(vec_ptr), opt(raw_ptr),
+               opt(fmap_ptr), opt(rules_ptr))
+
     # ------------------------------------------------------------------ LSTM head
     def load_lstm(self, model) -> None:
         """model: fdengine.lstm.LstmWeights (PyTorch layout, f32)."""

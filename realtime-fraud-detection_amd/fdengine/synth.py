@@ -313,3 +313,86 @@ def _txn_stream_indexed(pop, u, rng, t0_ms, rate_per_s, unknown_user_frac, unkno
     return {"card_key": key, "ts_ms": ts, "amount_cents": cents, "merchant": merchant, "device_fp": dfp,
             "ip_class": ip_class, "hour": np.full(n, 255, np.uint8), "weekend": np.full(n, 255, np.uint8),
             "is_fraud": roll < 0.055}
+
+
+# ------------------------------------------------------------------ extended profiles + context (feature map)
+# vocabularies (simulator.py:330-332 payment/type/card lists; kyc statuses :221-223; risk levels :255-266)
+PAYMENT_METHODS = ("credit_card", "debit_card", "digital_wallet", "bank_transfer", "crypto", "prepaid_card",
+                   "gift_card", "wire_transfer")
+TXN_TYPES = ("purchase", "withdrawal", "transfer", "refund")
+CARD_TYPES = ("visa", "mastercard", "amex", "discover")
+KYC_STATUSES = ("verified", "pending", "rejected")
+RISK_LEVELS = ("low", "medium", "high")
+
+
+def vocab_flags():
+    """-> (payment code -> isHighRiskPaymentMethod, type code -> is "refund"), 256 flags each."""
+    pay = np.zeros(256, np.uint8)
+    for i, p in enumerate(PAYMENT_METHODS):
+        pay[i] = any(s in p.lower() for s in ("prepaid", "gift", "crypto", "wire"))
+    ref = np.zeros(256, np.uint8)
+    ref[TXN_TYPES.index("refund")] = 1
+    return pay, ref
+
+
+def users_ext(pop: dict, seed: int = 5, null_frac: float = 0.05) -> dict:
+    """Extended UserProfile fields with the simulator's distributions (simulator.py:212-238) and some nulls."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = len(pop["users"]["key"])
+    kyc = rng.choice(3, n, p=[0.85, 0.12, 0.03]).astype(np.uint8)
+    d = {"key": pop["users"]["key"], "risk_score": rng.beta(2, 8, n), "kyc_status": kyc,
+         "verified": (kyc == 0).astype(np.uint8), "pref_start": rng.integers(6, 11, n).astype(np.int8),
+         "pref_end": rng.integers(18, 24, n).astype(np.int8), "weekend_activity": rng.uniform(0.3, 1.0, n),
+         "online_preference": rng.uniform(0.5, 0.95, n), "intl_preference": rng.uniform(0.0, 0.1, n),
+         "txn_frequency": pop["users"]["txn_frequency"].astype(np.int32),
+         "has_patterns": (rng.random(n) < 0.9).astype(np.uint8)}
+    for f in ("risk_score", "weekend_activity", "intl_preference"):
+        d[f] = d[f].copy()
+        d[f][rng.random(n) < null_frac] = np.nan
+    d["weekend_activity"][rng.random(n) < 0.1] = 0.2  # exercise the < 0.3 rule
+    d["pref_start"][rng.random(n) < null_frac] = -1
+    d["kyc_status"][rng.random(n) < null_frac] = 255
+    d["txn_frequency"][rng.random(n) < null_frac] = -1
+    return d
+
+
+def merchants_ext(pop: dict, seed: int = 6) -> dict:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    M = pop["merchants"]
+    n = len(M["category"])
+    rl = np.array([RISK_LEVELS.index(MERCHANT_CATEGORIES[c][1]) for c in M["category"]], np.uint8)
+    d = {"avg_amount": M["avg_amount"].copy(), "risk_level": rl, "blacklisted": (rng.random(n) < 0.02).astype(np.uint8),
+         "category": M["category"].astype(np.uint8), "high_risk_category": (rl == 2).astype(np.uint8),
+         "open_hour": rng.integers(6, 11, n).astype(np.uint8), "close_hour": rng.integers(20, 25, n).astype(np.uint8),
+         "suspicious_name": (rng.random(n) < 0.05).astype(np.uint8)}
+    d["avg_amount"][rng.random(n) < 0.05] = np.nan
+    d["risk_level"][rng.random(n) < 0.03] = 255
+    d["open_hour"][rng.random(n) < 0.03] = 255
+    d["suspicious_name"][rng.random(n) < 0.03] = 255
+    return d
+
+
+def txn_context(tx: dict, seed: int = 8) -> dict:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = len(tx["ts_ms"])
+    lat = rng.uniform(-70, 70, n)
+    lon = rng.uniform(-180, 180, n)
+    lat[rng.random(n) < 0.05] = np.nan
+    lon[rng.random(n) < 0.05] = np.nan
+    near = rng.random(n) < 0.1  # the (|lat| < 10 and |lon| < 10) high-risk box
+    lat[near], lon[near] = rng.uniform(-9, 9, int(near.sum())), rng.uniform(-9, 9, int(near.sum()))
+    mlat = lat + rng.normal(0, 2, n)
+    mlon = lon + rng.normal(0, 2, n)
+    mlat[rng.random(n) < 0.1] = np.nan
+    fs = rng.beta(2, 5, n)
+    fs[rng.random(n) < 0.3] = np.nan
+    pay = rng.integers(0, len(PAYMENT_METHODS), n).astype(np.uint8)
+    pay[rng.random(n) < 0.02] = 255
+    tt = rng.integers(0, len(TXN_TYPES), n).astype(np.uint8)
+    tt[rng.random(n) < 0.02] = 255
+    ct = rng.integers(0, len(CARD_TYPES), n).astype(np.uint8)
+    ct[rng.random(n) < 0.02] = 255
+    ua = (rng.random(n) < 0.05).astype(np.uint8)
+    ua[rng.random(n) < 0.05] = 255
+    return {"geo_lat": lat, "geo_lon": lon, "merchant_lat": mlat, "merchant_lon": mlon, "payment_method": pay,
+            "transaction_type": tt, "card_type": ct, "user_agent_flag": ua, "fraud_score": fs}
