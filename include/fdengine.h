@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 5
+#define FD_ABI_VERSION 6
 
 enum fd_status {
   FD_OK = 0,
@@ -371,12 +371,64 @@ int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const
 int fd_route_scatter_results_device(fd_engine* eng, const void* d_results, int64_t n, double* d_fraud_prob,
                                     double* d_confidence, uint8_t* d_decision, uint8_t* d_risk);
 
+/* ---------------------------------------------------------------- Flink window aggregates (a5) */
+/* WindowProcessor.processUserVelocity / processMerchantPatterns (fl/windows/WindowProcessor.java:36-66)
+   with UserVelocityAggregateFunction (:248-352) and MerchantAggregateFunction (:357-484), evaluated per
+   micro-batch on the device: keyBy(card key) sliding 5 min / slide 1 min, keyBy(merchant) tumbling 1 h,
+   event time with BoundedOutOfOrderness watermarks. Micro-batch semantics (DESIGN.md "Windows"): after a
+   batch's events are added, the watermark becomes max(previous, max event time - lag - 1) and every window
+   whose last millisecond it passed fires once with the events of its range that arrived so far (later
+   arrivals are late for it and dropped, allowed lateness 0). Transactions with an unknown merchant (-1)
+   are not aggregated by merchant (keyBy on a null id). Amount sums are exact integer cents. */
+typedef struct {
+  int64_t log_capacity;            /* events kept per log (user / merchant), 40 B each, device-resident */
+  int64_t max_out_of_orderness_ms; /* watermark lag: forBoundedOutOfOrderness(10 s) = 10000 */
+} fd_window_params;
+/* per-transaction window inputs beyond fd_txn_batch; any pointer may be NULL */
+typedef struct {
+  const uint8_t* payment_method; /* vocabulary code, 255 = null (NULL: all null) */
+  const uint8_t* is_fraud;       /* Transaction.isFraud, nonzero = TRUE (NULL: all false) */
+  const double* fraud_score;     /* Transaction.fraudScore, NaN = null (NULL: all null) */
+} fd_window_inputs;
+/* UserVelocityAggregate (getResult :292-311) + the Flink window bounds; 96 B */
+typedef struct {
+  uint64_t user_key;
+  int64_t window_start, window_end; /* Flink TimeWindow [start, end) */
+  int64_t first_ts, last_ts;        /* accumulator windowStart / windowEnd: min / max event time (ms) */
+  int32_t count, fraud_count, high_risk_count, unique_merchants, unique_payment_methods, pad;
+  double total_amount, avg_amount, fraud_rate, velocity_score;
+} fd_user_window;
+/* MerchantAggregate (getResult :403-424) + the Flink window bounds; 104 B */
+typedef struct {
+  int32_t merchant, count;
+  int64_t window_start, window_end, first_ts, last_ts;
+  int32_t fraud_count, high_risk_count, unique_users, unique_payment_methods;
+  double total_amount, fraud_amount, avg_amount, fraud_rate, amount_stddev, risk_score;
+} fd_merchant_window;
+/* allocate the event logs and reset the watermark (needs fd_state_init: cards are keyed by its table;
+   fd_state_init / fd_state_clear empty the logs and reset the watermark too). After a failed step
+   (FD_ERR_OOM) the window state is unspecified until the next fd_windows_init. */
+int fd_windows_init(fd_engine* eng, const fd_window_params* params);
+/* add one micro-batch (device pointers) and return the windows that fired, into host arrays of the given
+   capacities (FD_ERR_OOM if more fired); with flush != 0 the watermark then moves past every held event
+   (end of input: Flink's final MAX_WATERMARK) and all remaining windows fire. Synchronous. */
+int fd_windows_step_device(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n,
+                           int flush, fd_user_window* user_out, int64_t user_cap, int64_t* n_user,
+                           fd_merchant_window* merchant_out, int64_t merchant_cap, int64_t* n_merchant);
+/* same, host input pointers (staged to the device) */
+int fd_windows_step_host(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n,
+                         int flush, fd_user_window* user_out, int64_t user_cap, int64_t* n_user,
+                         fd_merchant_window* merchant_out, int64_t merchant_cap, int64_t* n_merchant);
+/* current watermark (INT64_MIN before the first) and events held in the user / merchant logs */
+int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, int64_t* merchant_events);
+
 /* ---------------------------------------------------------------- diagnostics */
 /* Per-launch device timing of the engine's hot kernels, measured with HIP events recorded on the
    launch stream around each kernel. fd_timing_read synchronises and returns the summed time (ms) and
    count of the timed launches of `kind` (FD_TIMING_ALL: every kind) since the last fd_timing_reset. */
 enum fd_timing_kind { FD_TIMING_ALL = -1, FD_TIMING_XGB = 0, FD_TIMING_IFOREST = 1, FD_TIMING_FEATURES = 2,
-                      FD_TIMING_BLEND = 3, FD_TIMING_ROUTE = 4, FD_TIMING_LSTM = 5 };
+                      FD_TIMING_BLEND = 3, FD_TIMING_ROUTE = 4, FD_TIMING_LSTM = 5,
+                      FD_TIMING_WINDOWS = 6 };
 int fd_engine_set_timing(fd_engine* eng, int enable);
 /* Engine tuning knobs (for A/B measurement; defaults are the tuned choices):
      "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel

@@ -207,6 +207,7 @@ int fd_engine_destroy(fd_engine* eng) {
   e.stage_ext.release();
   e.feat_vec.release();
   e.feat_in.release();
+  fd::windows_release(e);
   for (auto* b : {&e.route_blk, &e.route_soa, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.bias,
                   &e.lstm.wout, &e.lstm.bout, &e.state.seq})
     b->release();
@@ -635,6 +636,85 @@ int fd_features_full_device(fd_engine* eng, const fd_txn_batch* txns, const fd_t
   FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
   const fd_txn_context none{};
   fd::launch_features_full(e, *txns, ctx ? *ctx : none, n, d_vectors, d_raw, d_fmap, d_rules);
+  FD_API_END
+}
+
+int fd_windows_init(fd_engine* eng, const fd_window_params* params) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
+  FD_HIP(hipStreamSynchronize(e.stream));
+  fd::windows_init(e, *params);
+  FD_API_END
+}
+
+int fd_windows_step_device(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n,
+                           int flush, fd_user_window* user_out, int64_t user_cap, int64_t* n_user,
+                           fd_merchant_window* merchant_out, int64_t merchant_cap, int64_t* n_merchant) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(n_user && n_merchant, FD_ERR_INVALID_ARG, "null result counts");
+  const fd_txn_batch none_t{};
+  const fd_window_inputs none_in{};
+  FD_REQUIRE(txns || n == 0, FD_ERR_INVALID_ARG, "null txns");
+  Engine::Timed* tm = e.timing ? e.next_event_pair(FD_TIMING_WINDOWS) : nullptr;
+  if (tm) FD_HIP(hipEventRecord(tm->a, e.stream));
+  fd::windows_step(e, txns ? *txns : none_t, in ? *in : none_in, n, flush != 0, user_out, user_cap, n_user,
+                   merchant_out, merchant_cap, n_merchant);
+  if (tm) FD_HIP(hipEventRecord(tm->b, e.stream));
+  FD_API_END
+}
+
+int fd_windows_step_host(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n, int flush,
+                         fd_user_window* user_out, int64_t user_cap, int64_t* n_user,
+                         fd_merchant_window* merchant_out, int64_t merchant_cap, int64_t* n_merchant) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(n_user && n_merchant, FD_ERR_INVALID_ARG, "null result counts");
+  FD_REQUIRE(n >= 0 && (txns || n == 0), FD_ERR_INVALID_ARG, "bad batch");
+  fd_txn_batch dt{};
+  fd_window_inputs di{};
+  if (n > 0) {
+    FD_REQUIRE(txns->card_key && txns->ts_ms && txns->amount_cents && txns->merchant, FD_ERR_INVALID_ARG,
+               "batch needs card_key, ts_ms, amount_cents and merchant");
+    const fd_window_inputs none_in{};
+    const fd_window_inputs& hi = in ? *in : none_in;
+    // staging layout: key | ts | cents | fraud_score (8 B each) | merchant (4 B) | pm | fraud (1 B each)
+    const size_t n8 = (size_t)n * 8, n4 = (size_t)n * 4;
+    e.windows.stage.ensure(4 * n8 + n4 + 2 * (size_t)n + 64);
+    char* d = e.windows.stage.as<char>();
+    FD_HIP(hipMemcpyAsync(d, txns->card_key, n8, hipMemcpyHostToDevice, e.stream));
+    FD_HIP(hipMemcpyAsync(d + n8, txns->ts_ms, n8, hipMemcpyHostToDevice, e.stream));
+    FD_HIP(hipMemcpyAsync(d + 2 * n8, txns->amount_cents, n8, hipMemcpyHostToDevice, e.stream));
+    FD_HIP(hipMemcpyAsync(d + 4 * n8, txns->merchant, n4, hipMemcpyHostToDevice, e.stream));
+    dt.card_key = reinterpret_cast<const uint64_t*>(d);
+    dt.ts_ms = reinterpret_cast<const int64_t*>(d + n8);
+    dt.amount_cents = reinterpret_cast<const int64_t*>(d + 2 * n8);
+    dt.merchant = reinterpret_cast<const int32_t*>(d + 4 * n8);
+    if (hi.fraud_score) {
+      FD_HIP(hipMemcpyAsync(d + 3 * n8, hi.fraud_score, n8, hipMemcpyHostToDevice, e.stream));
+      di.fraud_score = reinterpret_cast<const double*>(d + 3 * n8);
+    }
+    if (hi.payment_method) {
+      FD_HIP(hipMemcpyAsync(d + 4 * n8 + n4, hi.payment_method, (size_t)n, hipMemcpyHostToDevice, e.stream));
+      di.payment_method = reinterpret_cast<const uint8_t*>(d + 4 * n8 + n4);
+    }
+    if (hi.is_fraud) {
+      FD_HIP(hipMemcpyAsync(d + 4 * n8 + n4 + n, hi.is_fraud, (size_t)n, hipMemcpyHostToDevice, e.stream));
+      di.is_fraud = reinterpret_cast<const uint8_t*>(d + 4 * n8 + n4 + n);
+    }
+  }
+  fd::windows_step(e, dt, di, n, flush != 0, user_out, user_cap, n_user, merchant_out, merchant_cap, n_merchant);
+  FD_API_END
+}
+
+int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, int64_t* merchant_events) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(e.windows.ready, FD_ERR_NOT_LOADED, "windows not initialised (fd_windows_init)");
+  if (watermark) *watermark = e.windows.wm;
+  if (user_events) *user_events = e.windows.ucount;
+  if (merchant_events) *merchant_events = e.windows.mcount;
   FD_API_END
 }
 

@@ -140,6 +140,26 @@ struct CardStore {
   double tp_threshold = 0.7;  // JobConfig.fraudThreshold (fl/config/JobConfig.java:47)
 };
 
+// Flink window aggregates (windows.hip): device event logs (double-buffered for compaction), sort scratch
+struct WindowState {
+  bool ready = false;
+  int64_t cap = 0, cand_cap = 0;
+  int64_t ooo = 10000;                    // watermark lag (ms)
+  int64_t wm = INT64_MIN;                 // current watermark
+  int64_t min_seen = INT64_MAX;           // smallest event time added (bases the first firing's keys)
+  int64_t max_seen = INT64_MIN;           // largest event time added (flush)
+  DeviceBuffer ulog[2], mlog[2];
+  int ucur = 0, mcur = 0;
+  int64_t ucount = 0, mcount = 0;
+  DeviceBuffer keys, vals, sort_tmp, uout, mout, scalars, stage;
+};
+
+inline int64_t floor_div_host(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+
 struct Engine {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -147,6 +167,7 @@ struct Engine {
   PackedForest forests[kMaxSlots];
   CardStore state;
   LstmModel lstm;
+  WindowState windows;
   hipStream_t aux_stream = nullptr;            // LSTM head runs here, concurrent with the forests
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   hipStream_t aux2_stream = nullptr;           // small batches: the second forest, concurrent with the first
@@ -190,6 +211,12 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t);
 void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
                    double* d_prob, double* d_raw, int32_t* d_leaf, hipStream_t stream = nullptr);
+// windows.hip
+void windows_init(Engine& e, const fd_window_params& p);
+void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, int64_t n, bool flush,
+                  fd_user_window* u_out, int64_t u_cap, int64_t* n_user, fd_merchant_window* m_out, int64_t m_cap,
+                  int64_t* n_merch);
+void windows_release(Engine& e);
 // features.hip
 void state_init(Engine& e, const fd_state_params& p);
 void state_clear(Engine& e);

@@ -742,6 +742,9 @@ void state_init(Engine& e, const fd_state_params& p) {
   st.ring.ensure((size_t)cap * st.K * sizeof(RingEvent));
   st.S = p.seq_len;
   if (st.S) st.seq.ensure((size_t)cap * st.S * kSeqInput * sizeof(float));
+  // extended user profiles are per slot: a re-initialised table starts without them (fd_state_load_users_ext
+  // allocates for the new capacity)
+  st.uext.release();
   st.err.ensure(16);
   st.ready = true;
   state_clear(e);
@@ -756,6 +759,12 @@ void state_clear(Engine& e) {
   FD_HIP(hipMemsetAsync(st.err.ptr, 0, 16, e.stream));
   FD_HIP(hipStreamSynchronize(e.stream));
   st.epoch = 0;
+  // the window event logs hold card-table slots: clearing the table empties them too
+  WindowState& w = e.windows;
+  w.ucount = w.mcount = 0;
+  w.wm = INT64_MIN;
+  w.min_seen = INT64_MAX;
+  w.max_seen = INT64_MIN;
 }
 
 int64_t state_count(Engine& e) {

@@ -143,6 +143,28 @@ class fd_txn_batch(C.Structure):
 FD_TIMING_ALL, FD_TIMING_XGB, FD_TIMING_IFOREST, FD_TIMING_FEATURES, FD_TIMING_BLEND = -1, 0, 1, 2, 3
 FD_TIMING_ROUTE = 4
 FD_TIMING_LSTM = 5
+FD_TIMING_WINDOWS = 6
+
+
+class fd_window_params(C.Structure):
+    _fields_ = [("log_capacity", C.c_int64), ("max_out_of_orderness_ms", C.c_int64)]
+
+
+class fd_window_inputs(C.Structure):
+    _fields_ = [("payment_method", C.c_void_p), ("is_fraud", C.c_void_p), ("fraud_score", C.c_void_p)]
+
+
+# fd_user_window / fd_merchant_window as numpy record dtypes (the host result arrays)
+USER_WINDOW_DTYPE = [("user_key", "<u8"), ("window_start", "<i8"), ("window_end", "<i8"), ("first_ts", "<i8"),
+                     ("last_ts", "<i8"), ("count", "<i4"), ("fraud_count", "<i4"), ("high_risk_count", "<i4"),
+                     ("unique_merchants", "<i4"), ("unique_payment_methods", "<i4"), ("pad", "<i4"),
+                     ("total_amount", "<f8"), ("avg_amount", "<f8"), ("fraud_rate", "<f8"),
+                     ("velocity_score", "<f8")]
+MERCHANT_WINDOW_DTYPE = [("merchant", "<i4"), ("count", "<i4"), ("window_start", "<i8"), ("window_end", "<i8"),
+                         ("first_ts", "<i8"), ("last_ts", "<i8"), ("fraud_count", "<i4"),
+                         ("high_risk_count", "<i4"), ("unique_users", "<i4"), ("unique_payment_methods", "<i4"),
+                         ("total_amount", "<f8"), ("fraud_amount", "<f8"), ("avg_amount", "<f8"),
+                         ("fraud_rate", "<f8"), ("amount_stddev", "<f8"), ("risk_score", "<f8")]
 FD_MAX_SEQ_LEN = 16
 FD_SLOT_LSTM = 64
 FD_SEQ_INPUT = 16
@@ -204,6 +226,12 @@ SIGNATURES = {
     "fd_route_partition_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _i32, _vp, _vp]),
     "fd_score_records_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, _vp, _vp, _i64, _vp]),
     "fd_route_scatter_results_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "fd_windows_init": (C.c_int, [_vp, C.POINTER(fd_window_params)]),
+    "fd_windows_step_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_window_inputs), _i64, C.c_int,
+                                         _vp, _i64, C.POINTER(_i64), _vp, _i64, C.POINTER(_i64)]),
+    "fd_windows_step_host": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_window_inputs), _i64, C.c_int,
+                                       _vp, _i64, C.POINTER(_i64), _vp, _i64, C.POINTER(_i64)]),
+    "fd_windows_stats": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64)]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
     "fd_timing_read": (C.c_int, [_vp, C.c_int, _dp, C.POINTER(_i64)]),

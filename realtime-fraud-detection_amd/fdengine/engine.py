@@ -237,6 +237,59 @@ class FraudEngine:
         N.call("fd_features_full_device", self._h, C.byref(b), C.byref(cx), int(n), C.c_void_p(vec_ptr), opt(raw_ptr),
                opt(fmap_ptr), opt(rules_ptr))
 
+    # ------------------------------------------------------------------ Flink window aggregates (a5)
+    def windows_init(self, log_capacity: int, max_out_of_orderness_ms: int = 10000) -> None:
+        """WindowProcessor's user-velocity (sliding 5 min / 1 min) and merchant (tumbling 1 h) windows
+        (fl/windows/WindowProcessor.java:36-66); needs state_init (cards are keyed by its table)."""
+        p = N.fd_window_params(int(log_capacity), int(max_out_of_orderness_ms))
+        N.call("fd_windows_init", self._h, C.byref(p))
+
+    def _windows_out(self, user_cap: int, merchant_cap: int):
+        uo = np.zeros(max(int(user_cap), 1), N.USER_WINDOW_DTYPE)
+        mo = np.zeros(max(int(merchant_cap), 1), N.MERCHANT_WINDOW_DTYPE)
+        return uo, mo
+
+    def windows_step_host(self, key, ts_ms, amount_cents, merchant, payment_method=None, is_fraud=None,
+                          fraud_score=None, flush: bool = False, user_cap: int = 0, merchant_cap: int = 0):
+        """Add one micro-batch (host arrays) and return (user windows, merchant windows) fired by it
+        as numpy record arrays (N.USER_WINDOW_DTYPE / N.MERCHANT_WINDOW_DTYPE)."""
+        n = len(key)
+        keep = [np.ascontiguousarray(key, np.uint64), np.ascontiguousarray(ts_ms, np.int64),
+                np.ascontiguousarray(amount_cents, np.int64), np.ascontiguousarray(merchant, np.int32)]
+        b = N.fd_txn_batch(*[a.ctypes.data for a in keep], None, None, None, None)
+        ins = [None if a is None else np.ascontiguousarray(a, dt)
+               for a, dt in ((payment_method, np.uint8), (is_fraud, np.uint8), (fraud_score, np.float64))]
+        wi = N.fd_window_inputs(*[None if a is None else a.ctypes.data for a in ins])
+        held = self.windows_stats()
+        ucap = user_cap or 5 * (n + held["user_events"]) + 16   # each event is in at most 5 user windows
+        mcap = merchant_cap or n + held["merchant_events"] + 16
+        uo, mo = self._windows_out(ucap, mcap)
+        nu, nm = C.c_int64(), C.c_int64()
+        N.call("fd_windows_step_host", self._h, C.byref(b), C.byref(wi), int(n), int(bool(flush)),
+               uo.ctypes.data, int(ucap), C.byref(nu), mo.ctypes.data, int(mcap), C.byref(nm))
+        return uo[:nu.value].copy(), mo[:nm.value].copy()
+
+    def windows_step_device(self, txn_ptrs: dict, n: int, in_ptrs: Optional[dict] = None, flush: bool = False,
+                            user_cap: int = 0, merchant_cap: int = 0):
+        """Device-resident variant: txn_ptrs as features_device; in_ptrs: payment_method / is_fraud /
+        fraud_score device pointers (missing = null)."""
+        b = N.fd_txn_batch(*[int(txn_ptrs.get(f) or 0) or None for f in N.TXN_FIELDS])
+        wi = N.fd_window_inputs(*[int(in_ptrs[f]) if in_ptrs and in_ptrs.get(f) else None
+                                  for f in ("payment_method", "is_fraud", "fraud_score")])
+        held = self.windows_stats()
+        ucap = user_cap or 5 * (n + held["user_events"]) + 16   # each event is in at most 5 user windows
+        mcap = merchant_cap or n + held["merchant_events"] + 16
+        uo, mo = self._windows_out(ucap, mcap)
+        nu, nm = C.c_int64(), C.c_int64()
+        N.call("fd_windows_step_device", self._h, C.byref(b), C.byref(wi), int(n), int(bool(flush)),
+               uo.ctypes.data, int(ucap), C.byref(nu), mo.ctypes.data, int(mcap), C.byref(nm))
+        return uo[:nu.value].copy(), mo[:nm.value].copy()
+
+    def windows_stats(self) -> dict:
+        wm, ue, me = C.c_int64(), C.c_int64(), C.c_int64()
+        N.call("fd_windows_stats", self._h, C.byref(wm), C.byref(ue), C.byref(me))
+        return {"watermark": wm.value, "user_events": ue.value, "merchant_events": me.value}
+
     # ------------------------------------------------------------------ LSTM head
     def load_lstm(self, model) -> None:
         """model: fdengine.lstm.LstmWeights (PyTorch layout, f32)."""

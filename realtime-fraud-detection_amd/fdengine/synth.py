@@ -396,3 +396,35 @@ def txn_context(tx: dict, seed: int = 8) -> dict:
     ua[rng.random(n) < 0.05] = 255
     return {"geo_lat": lat, "geo_lon": lon, "merchant_lat": mlat, "merchant_lon": mlon, "payment_method": pay,
             "transaction_type": tt, "card_type": ct, "user_agent_flag": ua, "fraud_score": fs}
+
+
+def window_stream(n_batches: int, batch: int, n_cards: int, n_merchants: int, seed: int = 0,
+                  t0_ms: int = 1_756_684_800_000, batch_span_ms: int = 20_000, jitter_ms: int = 15_000,
+                  late_frac: float = 0.01, late_ms: int = 900_000, unknown_merchant_frac: float = 0.05,
+                  hot_merchant_frac: float = 0.1):
+    """Micro-batches for the Flink window aggregates (a5): card keys drawn with a skew (some cards
+    repeat within 5 minutes), event times advancing ~batch_span_ms per batch with out-of-order jitter
+    (within the 10 s watermark lag and beyond it) plus a few very late events; payment-method codes with
+    nulls, isFraud flags, incoming fraud scores with nulls; one hot merchant (large tumbling segments)."""
+    rng = np.random.default_rng(seed)
+    keys = card_keys(np.arange(n_cards, dtype=np.int64), seed=seed + 11)
+    out = []
+    for b in range(n_batches):
+        base = t0_ms + b * batch_span_ms
+        idx = np.minimum((rng.pareto(1.2, batch) * n_cards / 20).astype(np.int64), n_cards - 1)
+        ts = base + rng.integers(0, batch_span_ms, batch) - rng.integers(0, jitter_ms, batch)
+        late = rng.random(batch) < late_frac
+        ts = np.where(late, ts - rng.integers(late_ms // 2, late_ms, batch), ts)
+        merchant = rng.integers(0, n_merchants, batch).astype(np.int32)
+        merchant = np.where(rng.random(batch) < hot_merchant_frac, 0, merchant).astype(np.int32)
+        merchant = np.where(rng.random(batch) < unknown_merchant_frac, -1, merchant).astype(np.int32)
+        cents = np.where(rng.random(batch) < 0.05, rng.integers(100_000, 2_000_000, batch),
+                         rng.integers(1, 50_000, batch)).astype(np.int64)
+        pm = rng.integers(0, 6, batch).astype(np.uint8)
+        pm = np.where(rng.random(batch) < 0.1, 255, pm).astype(np.uint8)
+        fraud = (rng.random(batch) < 0.05).astype(np.uint8)
+        score = rng.random(batch)
+        score = np.where(rng.random(batch) < 0.2, np.nan, score)
+        out.append(dict(key=keys[idx], ts_ms=ts.astype(np.int64), amount_cents=cents, merchant=merchant,
+                        payment_method=pm, is_fraud=fraud, fraud_score=score))
+    return out
