@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 6
+#define FD_ABI_VERSION 7
 
 enum fd_status {
   FD_OK = 0,
@@ -38,6 +38,7 @@ enum fd_status {
   FD_ERR_NOT_LOADED = 3, /* ValueError("Model ... not loaded"), ml/models/model_manager.py:281-282 */
   FD_ERR_UNSUPPORTED = 4,
   FD_ERR_OOM = 5,
+  FD_ERR_IO = 6, /* snapshot file missing / truncated / corrupt (checksum) */
 };
 
 /* Forest kinds: the two tree model types on the path. */
@@ -421,6 +422,24 @@ int fd_windows_step_host(fd_engine* eng, const fd_txn_batch* txns, const fd_wind
                          fd_merchant_window* merchant_out, int64_t merchant_cap, int64_t* n_merchant);
 /* current watermark (INT64_MIN before the first) and events held in the user / merchant logs */
 int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, int64_t* merchant_events);
+
+/* ---------------------------------------------------------------- state snapshot / restore */
+/* Durable image of the HBM keyed state: the counterpart of Flink's keyed-state checkpoints
+   (fl/FraudDetectionJob.java:112-136) and the Redis RDB of the velocity / profile hashes
+   (config/redis/redis-master.conf:6-13). Key-addressed (one record per card: header, fingerprints, ring,
+   LSTM history, extended profile), then the replicated merchant / vocabulary tables and the window event
+   logs; per-section FNV-1a-64 checksums. Synchronous; written to `path`.tmp then renamed.
+   (shard, n_shards) are recorded in the image for bookkeeping (0, 1 for an unsharded engine). */
+int fd_state_snapshot(fd_engine* eng, const char* path, int32_t shard, int32_t n_shards, int64_t* bytes_written);
+/* Re-insert an image's cards by key into the current table (any capacity; window_mode / ring_k / seq_len
+   must match fd_state_init's) keeping only the cards with shard_of(key, n_shards) == shard — restoring
+   every old shard's image on every new shard re-shards the state onto a different GPU count. Replicated
+   tables are replaced. Window logs are appended (fd_windows_init first) unless FD_RESTORE_SKIP_WINDOWS;
+   images merged onto one engine must share the window watermark. On FD_ERR_IO / FD_ERR_OOM the state is
+   unspecified until fd_state_clear. */
+#define FD_RESTORE_SKIP_WINDOWS 1
+int fd_state_restore(fd_engine* eng, const char* path, int32_t shard, int32_t n_shards, int32_t flags,
+                     int64_t* cards_restored);
 
 /* ---------------------------------------------------------------- diagnostics */
 /* Per-launch device timing of the engine's hot kernels, measured with HIP events recorded on the

@@ -718,6 +718,23 @@ int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, i
   FD_API_END
 }
 
+int fd_state_snapshot(fd_engine* eng, const char* path, int32_t shard, int32_t n_shards, int64_t* bytes_written) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::features_check(e);
+  fd::state_snapshot(e, path, shard, n_shards, bytes_written);
+  FD_API_END
+}
+
+int fd_state_restore(fd_engine* eng, const char* path, int32_t shard, int32_t n_shards, int32_t flags,
+                     int64_t* cards_restored) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::features_check(e);
+  fd::state_restore(e, path, shard, n_shards, flags, cards_restored);
+  FD_API_END
+}
+
 int fd_load_lstm(fd_engine* eng, const fd_lstm_params* params) {
   FD_API_BEGIN
   Engine& e = E(eng);

@@ -217,6 +217,9 @@ void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, 
                   fd_user_window* u_out, int64_t u_cap, int64_t* n_user, fd_merchant_window* m_out, int64_t m_cap,
                   int64_t* n_merch);
 void windows_release(Engine& e);
+// snapshot.hip
+void state_snapshot(Engine& e, const char* path, int shard, int n_shards, int64_t* bytes_written);
+void state_restore(Engine& e, const char* path, int shard, int n_shards, int flags, int64_t* cards_restored);
 // features.hip
 void state_init(Engine& e, const fd_state_params& p);
 void state_clear(Engine& e);

@@ -20,6 +20,8 @@ FD_ERR_HIP = 2
 FD_ERR_NOT_LOADED = 3
 FD_ERR_UNSUPPORTED = 4
 FD_ERR_OOM = 5
+FD_ERR_IO = 6
+FD_RESTORE_SKIP_WINDOWS = 1
 
 FD_FOREST_XGB_BINARY_LOGISTIC = 1
 FD_FOREST_SKLEARN_IFOREST = 2
@@ -232,6 +234,8 @@ SIGNATURES = {
     "fd_windows_step_host": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_window_inputs), _i64, C.c_int,
                                        _vp, _i64, C.POINTER(_i64), _vp, _i64, C.POINTER(_i64)]),
     "fd_windows_stats": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64)]),
+    "fd_state_snapshot": (C.c_int, [_vp, C.c_char_p, _i32, _i32, C.POINTER(_i64)]),
+    "fd_state_restore": (C.c_int, [_vp, C.c_char_p, _i32, _i32, _i32, C.POINTER(_i64)]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
     "fd_timing_read": (C.c_int, [_vp, C.c_int, _dp, C.POINTER(_i64)]),

@@ -19,7 +19,7 @@ LIB_DIR = PKG_ROOT / "lib"
 ORACLE_DIR = REPO_ROOT / "oracle"
 
 HIP_SOURCES = ["engine.hip", "forest.hip", "blend.hip", "features.hip", "route.hip", "lstm.hip",
-               "windows.hip"]
+               "windows.hip", "snapshot.hip"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-result"]
 
@@ -39,17 +39,42 @@ def _stale(out: Path, inputs) -> bool:
 
 
 def build_engine(force: bool = False, verbose: bool = True, profile: bool = False) -> Path:
-    """profile=True builds lib/libfdengine_prof.so with the forest kernel's phase-cycle
+    """One object per translation unit (compiled in parallel, rebuilt only when stale), then one link.
+    profile=True builds lib/libfdengine_prof.so with the forest kernel's phase-cycle
     instrumentation (-DFD_FOREST_PROFILE; tools/forest_phases.py loads it via FDENGINE_LIB)."""
+    from concurrent.futures import ThreadPoolExecutor
     LIB_DIR.mkdir(exist_ok=True)
+    obj_dir = LIB_DIR / ("obj_prof" if profile else "obj")
+    obj_dir.mkdir(exist_ok=True)
     out = LIB_DIR / ("libfdengine_prof.so" if profile else "libfdengine.so")
     srcs = [CSRC / s for s in HIP_SOURCES if (CSRC / s).exists()]
-    deps = srcs + list(CSRC.glob("*.h")) + [REPO_ROOT / "include" / "fdengine.h"]
-    if not force and not _stale(out, deps):
+    headers = list(CSRC.glob("*.h")) + [REPO_ROOT / "include" / "fdengine.h"]
+    extra = ["-DFD_FOREST_PROFILE"] if profile else []
+    compile_flags = [f for f in HIPCC_FLAGS if f != "-shared"]
+    if not force and not _stale(out, [*srcs, *headers]):
+        return out  # (the GPU box gets the library without the objects)
+
+    def obj(src: Path) -> Path:
+        o = obj_dir / (src.stem + ".o")
+        if force or _stale(o, [src, *headers]):
+            tmp = o.with_suffix(".o.tmp")
+            cmd = [_hipcc(), *compile_flags, *extra, f"-I{REPO_ROOT / 'include'}", f"-I{CSRC}", "-c", str(src),
+                   "-o", str(tmp)]
+            if verbose:
+                print("[build]", " ".join(cmd), flush=True)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed on {src.name}:\n{r.stderr[-6000:]}")
+            tmp.replace(o)
+        return o
+
+    jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(obj, srcs))
+    if not force and not _stale(out, objs):
         return out
     tmp = out.with_suffix(".so.tmp")
-    cmd = [_hipcc(), *HIPCC_FLAGS, *(["-DFD_FOREST_PROFILE"] if profile else []), f"-I{REPO_ROOT / 'include'}",
-           f"-I{CSRC}", *map(str, srcs), "-o", str(tmp)]
+    cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -7,6 +7,7 @@ place. The engine never falls back to the CPU: every call goes through libfdengi
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -289,6 +290,22 @@ class FraudEngine:
         wm, ue, me = C.c_int64(), C.c_int64(), C.c_int64()
         N.call("fd_windows_stats", self._h, C.byref(wm), C.byref(ue), C.byref(me))
         return {"watermark": wm.value, "user_events": ue.value, "merchant_events": me.value}
+
+    # ------------------------------------------------------------------ state snapshot / restore
+    def state_snapshot(self, path, shard: int = 0, n_shards: int = 1) -> int:
+        """Durable key-addressed image of the HBM keyed state (+ replicated tables, window logs);
+        Flink keyed-state checkpoint / Redis RDB counterpart. Returns the bytes written."""
+        nb = C.c_int64()
+        N.call("fd_state_snapshot", self._h, os.fsencode(str(path)), int(shard), int(n_shards), C.byref(nb))
+        return nb.value
+
+    def state_restore(self, path, shard: int = 0, n_shards: int = 1, skip_windows: bool = False) -> int:
+        """Re-insert an image's cards owned by `shard` of `n_shards` (any table capacity); returns the
+        number of cards restored. Restore every old shard's image on each new shard to re-shard."""
+        nc = C.c_int64()
+        N.call("fd_state_restore", self._h, os.fsencode(str(path)), int(shard), int(n_shards),
+               N.FD_RESTORE_SKIP_WINDOWS if skip_windows else 0, C.byref(nc))
+        return nc.value
 
     # ------------------------------------------------------------------ LSTM head
     def load_lstm(self, model) -> None:

@@ -59,6 +59,12 @@ class EngineShardBackend:
             self.eng.score_records_device(self.params, self.slots, rec.data_ptr(), m, res.data_ptr(), self.present)
         return res
 
+    def snapshot(self, path: str, rank: int, world: int) -> int:
+        return self.eng.state_snapshot(path, rank, world)
+
+    def restore(self, path: str, rank: int, world: int) -> int:
+        return self.eng.state_restore(path, rank, world, skip_windows=True)
+
     def scatter_results(self, res, n: int):
         t = self.torch
         fp = t.empty(n, dtype=t.float64, device=self.device)
@@ -104,6 +110,58 @@ class ShardedScorer:
         back = torch.empty((n, RES), dtype=torch.uint8, device=rec.device)
         self._a2a(back, res, send, recv)
         return self.be.scatter_results(back, n)
+
+    # ------------------------------------------------------------------ checkpoint / rescale
+    # Counterpart of Flink's externalized keyed-state checkpoints (fl/FraudDetectionJob.java:112-136):
+    # every rank writes its key-addressed image, rank 0 writes the manifest after a barrier (the image set
+    # is complete when the manifest exists). Restoring on any world size re-shards: each new rank reads every
+    # old image and keeps the cards it owns.
+    def checkpoint(self, directory: str, step: int) -> str:
+        import json
+        import os
+        import torch.distributed as dist
+        os.makedirs(directory, exist_ok=True)
+        name = image_name(step, self.rank, self.world)
+        nbytes = self.be.snapshot(os.path.join(directory, name), self.rank, self.world)
+        sizes = [None] * self.world
+        if self.world > 1:
+            dist.all_gather_object(sizes, nbytes, group=self.group)
+        else:
+            sizes = [nbytes]
+        man = os.path.join(directory, f"checkpoint-{step:08d}.json")
+        if self.rank == 0:
+            doc = {"format": "fdsnap/1", "step": int(step), "world": self.world,
+                   "images": [image_name(step, r, self.world) for r in range(self.world)], "bytes": sizes}
+            tmp = man + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump(doc, f)
+            os.replace(tmp, man)
+        if self.world > 1:
+            dist.barrier(group=self.group)
+        return man
+
+    def restore(self, manifest: str) -> int:
+        """Load a checkpoint written at any world size; returns the cards this rank now owns."""
+        import json
+        import os
+        with open(manifest) as f:
+            doc = json.load(f)
+        if doc.get("format") != "fdsnap/1":
+            raise ValueError(f"{manifest}: not an fdengine checkpoint manifest")
+        base = os.path.dirname(manifest)
+        return sum(self.be.restore(os.path.join(base, img), self.rank, self.world) for img in doc["images"])
+
+
+def image_name(step: int, rank: int, world: int) -> str:
+    return f"state-{step:08d}-{rank:03d}-of-{world:03d}.fdsnap"
+
+
+def latest_checkpoint(directory: str) -> Optional[str]:
+    """Manifest of the newest complete checkpoint in `directory` (None if there is none)."""
+    import glob
+    import os
+    found = sorted(glob.glob(os.path.join(directory, "checkpoint-*.json")))
+    return found[-1] if found else None
 
 
 def owned_mask(keys, rank: int, world: int) -> np.ndarray:

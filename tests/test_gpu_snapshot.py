@@ -1,0 +1,250 @@
+"""GPU: snapshot / restore of the HBM keyed state (SURVEY §8(f) rank 4 — the counterpart of Flink keyed-state
+checkpoints, fl/FraudDetectionJob.java:112-136, and the Redis RDB, config/redis/redis-master.conf:6-13).
+
+Property bar (size-independent, bit-exact): a stream cut by snapshot -> restore (into a fresh engine with a
+different table capacity) produces exactly the outputs of the uninterrupted stream — scoring vectors, the
+64-column feature map, rule scores, LSTM history sequences and the Flink window results; re-sharding 2 -> 3
+GPUs by restoring every old image on every new shard reproduces the unsharded engine per transaction.
+Images are byte-identical for the same table; corrupt / truncated / mismatched images fail loudly."""
+import numpy as np
+import pytest
+
+from fdengine import FraudEngine, synth
+from fdengine.engine import shard_of
+from fdengine._native import CTX_FIELDS, FD_ERR_IO, TXN_FIELDS, NativeError
+
+pytestmark = pytest.mark.gpu
+
+UF = ("user_key", "window_start", "window_end", "first_ts", "last_ts", "count", "total_amount", "velocity_score")
+
+
+def _setup(eng, pop, cap, mode, seq_len=0, windows=True, owner=None):
+    """owner = (rank, world): load only the users this shard owns (each card lives on one shard)."""
+    U, M = pop["users"], pop["merchants"]
+    keep = np.ones(len(U["key"]), bool) if owner is None else shard_of(U["key"], owner[1]) == owner[0]
+    eng.state_init(cap, mode, 8, seq_len)
+    eng.load_users(U["key"][keep], U["avg_amount"][keep], U["account_age_days"][keep],
+                   np.asarray(U["device_fp"]).reshape(-1, 3)[keep])
+    eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+    ue = synth.users_ext(pop)
+    eng.load_users_ext(ue["key"][keep], **{k: v[keep] for k, v in ue.items() if k != "key"})
+    me = synth.merchants_ext(pop)
+    eng.load_merchants_ext(len(me["avg_amount"]), **me)
+    pay, ref = synth.vocab_flags()
+    eng.load_vocab(pay, ref)
+    if windows:
+        eng.windows_init(1 << 16)
+
+
+def _stream(n_users=1200, n=16000, seed=3):
+    pop = synth.population(n_users, 120, seed=seed)
+    tx = synth.txn_stream(pop, n, seed=seed + 1, rate_per_s=3.0, unknown_user_frac=0.05,
+                          unknown_merchant_frac=0.03)
+    ctx = synth.txn_context(tx)
+    return pop, tx, ctx
+
+
+def _full(eng, part, cpart):
+    import torch
+    n = len(part["card_key"])
+    dev = {f: torch.from_numpy(np.ascontiguousarray(part[f])).cuda() for f in TXN_FIELDS}
+    dctx = {f: torch.from_numpy(np.ascontiguousarray(cpart[f])).cuda() for f in CTX_FIELDS}
+    vec = torch.empty((n, 64), dtype=torch.float32, device="cuda")
+    fmap = torch.empty((n, 64), dtype=torch.float64, device="cuda")
+    rules = torch.empty((n, 24), dtype=torch.uint8, device="cuda")
+    eng.features_full_device({f: t.data_ptr() for f, t in dev.items()}, {f: t.data_ptr() for f, t in dctx.items()},
+                             n, vec.data_ptr(), fmap.data_ptr(), rules.data_ptr())
+    torch.cuda.synchronize()
+    return vec.cpu().numpy(), fmap.cpu().numpy(), rules.cpu().numpy()
+
+
+def _windows(eng, part, flush=False):
+    gu, gm = eng.windows_step_host(part["card_key"], part["ts_ms"], part["amount_cents"], part["merchant"],
+                                   flush=flush)
+    u = sorted(tuple(r[f].item() for f in UF) for r in gu)
+    m = sorted((int(r["merchant"]), int(r["window_start"]), int(r["count"]), float(r["total_amount"]),
+                float(r["amount_stddev"])) for r in gm)
+    return u, m
+
+
+def _cuts(n, k):
+    e = np.linspace(0, n, k + 1).astype(int)
+    return list(zip(e[:-1], e[1:]))
+
+
+def _run(eng, tx, ctx, cuts, windows=True, flush=True):
+    out = []
+    for a, b in cuts:
+        part = {k: v[a:b] for k, v in tx.items()}
+        cpart = {k: v[a:b] for k, v in ctx.items()}
+        res = _full(eng, part, cpart)
+        if windows:
+            res = res + _windows(eng, part)
+        out.append(res)
+    if windows and flush:
+        empty = {k: v[:0] for k, v in tx.items()}
+        out.append(_windows(eng, empty, flush=True))
+    return out
+
+
+def _same(a, b):
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        for p, q in zip(x, y):
+            if isinstance(p, np.ndarray):
+                np.testing.assert_array_equal(p.view(np.uint8), q.view(np.uint8))
+            else:
+                assert p == q
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_resume_equals_uninterrupted(engine, tmp_path, mode):
+    pop, tx, ctx = _stream(seed=3 + mode)
+    cuts = _cuts(len(tx["card_key"]), 8)
+    _setup(engine, pop, 8192, mode)
+    _run(engine, tx, ctx, cuts[:4], flush=False)
+    path = tmp_path / "state.fdsnap"
+    nbytes = engine.state_snapshot(path)
+    assert nbytes == path.stat().st_size > 256
+    cards = engine.state_info()["cards"]
+    ref = _run(engine, tx, ctx, cuts[4:])
+    fresh = FraudEngine(0)
+    try:
+        fresh.state_init(1 << 15, mode, 8)  # different capacity: records land in other slots
+        fresh.windows_init(1 << 16)
+        assert fresh.state_restore(path) == cards
+        got = _run(fresh, tx, ctx, cuts[4:])
+    finally:
+        fresh.close()
+    _same(got, ref)
+    assert sum(len(r[3]) for r in ref[:-1]) > 100  # user windows did fire after the cut
+
+
+def test_resume_lstm_history(engine, tmp_path):
+    import torch
+    pop, tx, _ = _stream(n_users=800, n=9000, seed=11)
+    cuts = _cuts(len(tx["card_key"]), 6)
+
+    def run(eng, cs):
+        out = []
+        for a, b in cs:
+            part = {k: v[a:b] for k, v in tx.items()}
+            n = b - a
+            dev = {f: torch.from_numpy(np.ascontiguousarray(part[f])).cuda() for f in TXN_FIELDS}
+            vec = torch.empty((n, 64), dtype=torch.float32, device="cuda")
+            seq = torch.empty((n, 10, 16), dtype=torch.float32, device="cuda")
+            eng.features_seq_device({f: t.data_ptr() for f, t in dev.items()}, n, vec.data_ptr(), seq.data_ptr())
+            torch.cuda.synchronize()
+            out.append((vec.cpu().numpy(), seq.cpu().numpy()))
+        return out
+
+    _setup(engine, pop, 4096, 1, seq_len=10, windows=False)
+    run(engine, cuts[:3])
+    path = tmp_path / "lstm.fdsnap"
+    engine.state_snapshot(path)
+    ref = run(engine, cuts[3:])
+    fresh = FraudEngine(0)
+    try:
+        fresh.state_init(3000, 1, 8, 10)
+        fresh.state_restore(path)
+        got = run(fresh, cuts[3:])
+    finally:
+        fresh.close()
+    _same(got, ref)
+
+
+def test_reshard_two_to_three(engine, tmp_path):
+    """Emulated shards: old shard r of 2 sees only its cards' transactions; after the cut every new shard of 3
+    restores both old images (keeping its own cards) and must match the unsharded engine per transaction."""
+    pop, tx, ctx = _stream(n_users=1500, n=12000, seed=21)
+    n = len(tx["card_key"])
+    cuts = _cuts(n, 6)
+    _setup(engine, pop, 1 << 14, 1, windows=False)
+    ref = _run(engine, tx, ctx, cuts, windows=False)
+    ref_vec = np.concatenate([r[0] for r in ref])
+    ref_fmap = np.concatenate([r[1] for r in ref])
+    ref_rules = np.concatenate([r[2] for r in ref])
+
+    def sub(d, m):
+        return {k: v[m] for k, v in d.items()}
+
+    old = [FraudEngine(0) for _ in range(2)]
+    new = [FraudEngine(0) for _ in range(3)]
+    try:
+        o2 = shard_of(tx["card_key"], 2)
+        paths = []
+        for r, e in enumerate(old):
+            _setup(e, pop, 1 << 13, 1, windows=False, owner=(r, 2))
+            for a, b in cuts[:3]:
+                m = np.zeros(n, bool)
+                m[a:b] = o2[a:b] == r
+                _full(e, sub(tx, m), sub(ctx, m))
+            p = tmp_path / f"state-{r}-of-2.fdsnap"
+            e.state_snapshot(p, r, 2)
+            paths.append(p)
+        o3 = shard_of(tx["card_key"], 3)
+        restored = 0
+        vec = np.zeros_like(ref_vec)
+        fmap = np.zeros_like(ref_fmap)
+        rules = np.zeros_like(ref_rules)
+        for r, e in enumerate(new):
+            e.state_init(1 << 13, 1, 8)
+            for p in paths:
+                restored += e.state_restore(p, r, 3)
+            for a, b in cuts[3:]:
+                m = np.zeros(n, bool)
+                m[a:b] = o3[a:b] == r
+                v, f, ru = _full(e, sub(tx, m), sub(ctx, m))
+                vec[m], fmap[m], rules[m] = v, f, ru
+        tail = slice(cuts[3][0], n)
+        np.testing.assert_array_equal(vec[tail].view(np.uint32), ref_vec[tail].view(np.uint32))
+        np.testing.assert_array_equal(fmap[tail].view(np.uint64), ref_fmap[tail].view(np.uint64))
+        np.testing.assert_array_equal(rules[tail], ref_rules[tail])
+        assert restored == sum(e.state_info()["cards"] for e in old)
+    finally:
+        for e in old + new:
+            e.close()
+
+
+def test_image_deterministic_and_corruption_detected(engine, tmp_path):
+    pop, tx, ctx = _stream(n_users=500, n=4000, seed=31)
+    _setup(engine, pop, 2048, 0)
+    _run(engine, tx, ctx, _cuts(4000, 2), flush=False)
+    a, b = tmp_path / "a.fdsnap", tmp_path / "b.fdsnap"
+    engine.state_snapshot(a)
+    engine.state_snapshot(b)
+    blob = a.read_bytes()
+    assert blob == b.read_bytes()
+    fresh = FraudEngine(0)
+    try:
+        fresh.state_init(2048, 0, 8)
+        fresh.windows_init(1 << 16)
+        bad = bytearray(blob)
+        bad[256 + 1000] ^= 0x40  # a byte inside the card records
+        (tmp_path / "bad.fdsnap").write_bytes(bytes(bad))
+        with pytest.raises(NativeError, match="checksum") as ei:
+            fresh.state_restore(tmp_path / "bad.fdsnap")
+        assert ei.value.code == FD_ERR_IO
+        (tmp_path / "short.fdsnap").write_bytes(blob[: len(blob) // 2])
+        fresh.state_clear()
+        with pytest.raises(NativeError, match="truncated"):
+            fresh.state_restore(tmp_path / "short.fdsnap")
+        with pytest.raises(NativeError, match="cannot open"):
+            fresh.state_restore(tmp_path / "missing.fdsnap")
+        fresh.state_init(2048, 0, 8, 4)  # seq_len differs
+        with pytest.raises(NativeError, match="seq_len"):
+            fresh.state_restore(a)
+        fresh.state_init(64, 0, 8)  # too small for the image's cards
+        fresh.windows_init(1 << 16)
+        with pytest.raises(NativeError, match="card table full"):
+            fresh.state_restore(a)
+    finally:
+        fresh.close()
+    fresh = FraudEngine(0)
+    try:
+        fresh.state_init(2048, 0, 8)  # the image holds window state; windows not initialised here
+        with pytest.raises(ValueError, match="fd_windows_init"):
+            fresh.state_restore(a)
+        assert fresh.state_restore(a, skip_windows=True) == engine.state_info()["cards"]
+    finally:
+        fresh.close()
