@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 7
+#define FD_ABI_VERSION 8
 
 enum fd_status {
   FD_OK = 0,
@@ -441,13 +441,75 @@ int fd_state_snapshot(fd_engine* eng, const char* path, int32_t shard, int32_t n
 int fd_state_restore(fd_engine* eng, const char* path, int32_t shard, int32_t n_shards, int32_t flags,
                      int64_t* cards_restored);
 
+/* ---------------------------------------------------------------- Kafka JSON ingest codec */
+/* TransactionDeserializationSchema.deserialize (fl/serialization/TransactionDeserializationSchema.java:28-49)
+   of the simulator's messages (json.dumps(asdict(Transaction), default=str),
+   services/data-simulator/src/main/python/simulator.py:77-101,186,376-385) on the device: one micro-batch of
+   raw messages (concatenated bytes + n+1 offsets) -> the SoA columns below. Identities: card_key =
+   fd_hash64(user_id), device_fp = fd_hash64(device_fingerprint), txn_hash = fd_hash64(transaction_id);
+   merchant = index of merchant_id in fd_ingest_set_merchants (-1 unknown / null); payment_method /
+   transaction_type / card_type = index in fd_ingest_set_vocab (255 null, FD_VOCAB_OTHER unknown);
+   ip_class 0 null / 1 private / 2 public and user_agent_flag 0 / 1 / 255 null (FeatureExtractor.java:434-451);
+   ts_ms = ISO-8601 timestamp as epoch ms (UTC without offset); amount_cents exact. Declared semantics and
+   limits: DESIGN.md "Ingest". Rows with status & FD_INGEST_INVALID are the reference's ERROR placeholder
+   (all other columns default). Any output pointer may be NULL. */
+#define FD_VOCAB_OTHER 254
+enum fd_vocab_kind { FD_VOCAB_PAYMENT_METHOD = 0, FD_VOCAB_TRANSACTION_TYPE = 1, FD_VOCAB_CARD_TYPE = 2 };
+enum fd_ingest_status {
+  FD_INGEST_MALFORMED = 1,     /* not one JSON object / bad member syntax / value of the wrong type */
+  FD_INGEST_TOO_LONG = 2,      /* message longer than 4096 bytes */
+  FD_INGEST_UNKNOWN_VOCAB = 4, /* a payment / type / card string outside its vocabulary (code FD_VOCAB_OTHER) */
+  FD_INGEST_INEXACT = 8,       /* sub-cent amount (rounded half-even) or a > 19-digit number at a rounding tie */
+  FD_INGEST_MISSING = 16,      /* user_id, amount or timestamp missing / null */
+};
+#define FD_INGEST_INVALID (FD_INGEST_MALFORMED | FD_INGEST_TOO_LONG | FD_INGEST_MISSING)
+typedef struct {
+  uint64_t* card_key;
+  int64_t* ts_ms;
+  int64_t* amount_cents;
+  int32_t* merchant;
+  uint64_t* device_fp;
+  uint8_t* ip_class;
+  uint8_t* hour;
+  uint8_t* weekend;
+  double* geo_lat;
+  double* geo_lon;
+  double* merchant_lat;
+  double* merchant_lon;
+  uint8_t* payment_method;
+  uint8_t* transaction_type;
+  uint8_t* card_type;
+  uint8_t* user_agent_flag;
+  double* fraud_score;
+  uint8_t* is_fraud;
+  uint64_t* txn_hash;
+  uint8_t* status;
+} fd_ingest_out;
+/* the identity hash of the codec: fmix64(FNV-1a-64(bytes)) (host; profiles / merchants are keyed with it) */
+int fd_hash64(const uint8_t* bytes, int64_t n, uint64_t* out);
+/* vocabulary `which` (enum fd_vocab_kind): string i (bytes[offsets[i]..offsets[i+1])) gets code i (n <= 254) */
+int fd_ingest_set_vocab(fd_engine* eng, int32_t which, const uint8_t* bytes, const int64_t* offsets, int64_t n);
+/* merchant_id strings in merchant-table order (index = the engine's merchant index) */
+int fd_ingest_set_merchants(fd_engine* eng, const uint8_t* bytes, const int64_t* offsets, int64_t n);
+/* device pointers (HBM-resident messages, outputs); asynchronous on the engine stream; n <= 2^30 */
+int fd_ingest_json_device(fd_engine* eng, const uint8_t* d_bytes, const int64_t* d_offsets, int64_t n,
+                          const fd_ingest_out* d_out);
+/* host pointers (staged through the device); synchronous */
+int fd_ingest_json_host(fd_engine* eng, const uint8_t* bytes, const int64_t* offsets, int64_t n,
+                        const fd_ingest_out* out);
+/* the codec's scalar conversions on the host (diagnostics / tests): kind 0 = JSON number text -> f64
+   (correctly rounded), 1 = amount text -> cents, 2 = ISO-8601 text -> epoch ms. flags: bit 0 grammar error,
+   bit 1 inexact. */
+int fd_ingest_scalar_host(int32_t kind, const uint8_t* text, int32_t n, double* f64_out, int64_t* i64_out,
+                          int32_t* flags_out);
+
 /* ---------------------------------------------------------------- diagnostics */
 /* Per-launch device timing of the engine's hot kernels, measured with HIP events recorded on the
    launch stream around each kernel. fd_timing_read synchronises and returns the summed time (ms) and
    count of the timed launches of `kind` (FD_TIMING_ALL: every kind) since the last fd_timing_reset. */
 enum fd_timing_kind { FD_TIMING_ALL = -1, FD_TIMING_XGB = 0, FD_TIMING_IFOREST = 1, FD_TIMING_FEATURES = 2,
                       FD_TIMING_BLEND = 3, FD_TIMING_ROUTE = 4, FD_TIMING_LSTM = 5,
-                      FD_TIMING_WINDOWS = 6 };
+                      FD_TIMING_WINDOWS = 6, FD_TIMING_INGEST = 7 };
 int fd_engine_set_timing(fd_engine* eng, int enable);
 /* Engine tuning knobs (for A/B measurement; defaults are the tuned choices):
      "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel

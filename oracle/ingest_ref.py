@@ -1,0 +1,293 @@
+"""TEST INFRASTRUCTURE ONLY (oracle) — never imported by the product path (fdengine/).
+
+CPU restatement of the JSON ingest codec's declared semantics (DESIGN.md "Ingest"; kernel:
+realtime-fraud-detection_amd/csrc/ingest.hip), built on Python's own json module:
+
+  wire format   services/data-simulator/src/main/python/simulator.py:77-101 (Transaction fields),
+                :186 (json.dumps(v, default=str)), :376-385 (send)
+  deserializer  services/flink-jobs/.../serialization/TransactionDeserializationSchema.java:28-49
+                (Jackson; any exception -> an ERROR placeholder transaction)
+  derived codes services/flink-jobs/.../features/FeatureExtractor.java:300-325, 366-381, 434-451
+                (isPrivateIP startsWith 192.168. / 10. / 172.16.; analyzeSuspiciousUserAgent contains
+                "bot" / "crawler" or length() < 20 in UTF-16 units)
+
+Numbers are exact: Python's float() of the decimal text is correctly rounded (pins the device's
+decimal -> binary64 conversion); amounts go through decimal.Decimal to exact cents.
+Parity vs Jackson itself is unpinned (no JDK in the build container); the Python side of the
+reference (json / datetime) pins the number and time conversions.
+"""
+from __future__ import annotations
+
+import json
+import re
+from decimal import ROUND_HALF_EVEN, Decimal
+from typing import Dict, List, Optional
+
+import numpy as np
+
+MALFORMED, TOO_LONG, UNKNOWN_VOCAB, INEXACT, MISSING = 1, 2, 4, 8, 16
+INVALID = MALFORMED | TOO_LONG | MISSING
+VOCAB_OTHER = 254
+MAX_MSG, MAX_MEMBERS = 4096, 64
+
+FIELDS = {
+    "transaction_id": "txn", "transactionId": "txn", "user_id": "user", "userId": "user",
+    "merchant_id": "merchant", "merchantId": "merchant", "amount": "amount", "timestamp": "ts",
+    "ip_address": "ip", "ipAddress": "ip", "device_fingerprint": "dfp", "deviceFingerprint": "dfp",
+    "user_agent": "ua", "userAgent": "ua", "geolocation": "geo", "merchant_location": "mloc",
+    "merchantLocation": "mloc", "is_weekend": "weekend", "isWeekend": "weekend", "hour_of_day": "hour",
+    "hourOfDay": "hour", "is_fraud": "fraud", "isFraud": "fraud", "fraud_score": "score",
+    "fraudScore": "score", "payment_method": "pay", "paymentMethod": "pay",
+    "transaction_type": "ttype", "transactionType": "ttype", "card_type": "ctype", "cardType": "ctype",
+}
+NUMBER_RE = re.compile(r"-?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?\Z")
+ISO_RE = re.compile(r"(\d{4})-(\d{2})-(\d{2})T(\d{2}):(\d{2}):(\d{2})(\.(\d{1,9}))?(Z|z|[+-]\d{2}:\d{2})?\Z")
+M64 = (1 << 64) - 1
+
+
+def h64(b: bytes) -> int:
+    """fmix64(FNV-1a-64(bytes)) — the codec's identity hash (fd_hash64)."""
+    h = 0xcbf29ce484222325
+    for c in b:
+        h = ((h ^ c) * 0x100000001b3) & M64
+    h ^= h >> 33
+    h = (h * 0xff51afd7ed558ccd) & M64
+    h ^= h >> 33
+    h = (h * 0xc4ceb9fe1a85ec53) & M64
+    h ^= h >> 33
+    return h
+
+
+class Num:
+    """A JSON number literal, kept as text (exactness, int vs float)."""
+    __slots__ = ("text",)
+
+    def __init__(self, text):
+        self.text = text
+
+    @property
+    def is_int(self):
+        return not any(c in self.text for c in ".eE")
+
+
+class Malformed(Exception):
+    pass
+
+
+def _reject_constant(name):
+    raise Malformed(name)  # NaN / Infinity are not JSON
+
+
+class Obj(list):
+    """A JSON object as its member list (duplicates kept, in order)."""
+
+
+def _load(raw: bytes):
+    return json.loads(raw.decode("utf-8", "surrogatepass"), object_pairs_hook=Obj, parse_int=Num, parse_float=Num,
+                      parse_constant=_reject_constant)
+
+
+def _utf8(s: str) -> bytes:
+    return s.encode("utf-8", "surrogatepass")
+
+
+def _text_of_scalar(v) -> Optional[bytes]:
+    """String-typed field: string, or a scalar coerced to its literal text; None = null."""
+    if v is None:
+        return None
+    if isinstance(v, str):
+        return _utf8(v)
+    if isinstance(v, bool):
+        return b"true" if v else b"false"
+    if isinstance(v, Num):
+        return v.text.encode()
+    raise Malformed("container for a string field")  # Obj / list
+
+
+def _decimal_of(v) -> Optional[Decimal]:
+    """Number-typed field: number or a string holding exactly a JSON number; None = null."""
+    if v is None:
+        return None
+    if isinstance(v, Num):
+        return Decimal(v.text)
+    if isinstance(v, str) and NUMBER_RE.match(v):
+        return Decimal(v)
+    raise Malformed("not a number")
+
+
+def _f64(d: Optional[Decimal]) -> float:
+    return float("nan") if d is None else float(d)
+
+
+def days_from_civil(y, m, d):
+    y -= m <= 2
+    era = (y if y >= 0 else y - 399) // 400
+    yoe = y - era * 400
+    doy = (153 * (m + (-3 if m > 2 else 9)) + 2) // 5 + d - 1
+    doe = yoe * 365 + yoe // 4 - yoe // 100 + doy
+    return era * 146097 + doe - 719468
+
+
+def iso_to_ms(s: str) -> Optional[int]:
+    """ISO-8601 'YYYY-MM-DDTHH:MM:SS[.f{1,9}][Z|±HH:MM]' -> epoch ms (UTC if no offset, fraction truncated
+    to ms as java.time.Instant.toEpochMilli); None if it does not parse."""
+    m = ISO_RE.match(s)
+    if not m:
+        return None
+    Y, Mo, D, h, mi, se = (int(m.group(i)) for i in range(1, 7))
+    leap = (Y % 4 == 0 and Y % 100 != 0) or Y % 400 == 0
+    mdays = [31, 29 if leap else 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31]
+    if not (1 <= Mo <= 12) or D < 1 or D > mdays[Mo - 1] or h > 23 or mi > 59 or se > 59:
+        return None
+    frac = m.group(8) or ""
+    frac_ms = int((frac + "000")[:3]) if frac else 0
+    off = 0
+    z = m.group(9)
+    if z and z not in "Zz":
+        oh, om = int(z[1:3]), int(z[4:6])
+        if oh > 18 or om > 59:
+            return None
+        off = (-1 if z[0] == "-" else 1) * (oh * 60 + om)
+    secs = days_from_civil(Y, Mo, D) * 86400 + h * 3600 + mi * 60 + se - off * 60
+    return secs * 1000 + frac_ms
+
+
+def cents_of(d: Decimal):
+    """exact cents (half-even below a cent) -> (cents, inexact)"""
+    c = (d * 100).quantize(Decimal(1), rounding=ROUND_HALF_EVEN)
+    inexact = c != d * 100
+    if abs(c) > (1 << 63) - 1:
+        raise Malformed("amount overflow")
+    return int(c), inexact
+
+
+def _sig_digits(text: str) -> int:
+    mant = re.split(r"[eE]", text)[0].lstrip("-").replace(".", "").lstrip("0")
+    return len(mant.rstrip("0")) if mant else 0
+
+
+DEFAULT = dict(card_key=0, ts_ms=0, amount_cents=0, merchant=-1, device_fp=0, ip_class=0, hour=255, weekend=255,
+               geo_lat=float("nan"), geo_lon=float("nan"), merchant_lat=float("nan"), merchant_lon=float("nan"),
+               payment_method=255, transaction_type=255, card_type=255, user_agent_flag=255,
+               fraud_score=float("nan"), is_fraud=0, txn_hash=0, status=0)
+
+
+def parse_message(raw: bytes, merchants: Dict[str, int], vocabs: List[Dict[str, int]]) -> dict:
+    """One message -> the codec's output row (dict of DEFAULT's keys)."""
+    row = dict(DEFAULT)
+    if len(raw) > MAX_MSG:
+        row["status"] = TOO_LONG
+        return row
+    status = 0
+    try:
+        doc = _load(raw)
+        if not isinstance(doc, Obj):
+            raise Malformed("not an object")
+        if len(doc) > MAX_MEMBERS:
+            raise Malformed("too many members")
+        vals = {}
+        for k, v in doc:  # the last member mapping to a field wins (duplicates and snake / camel aliases)
+            f = FIELDS.get(k)
+            if f is not None:
+                vals[f] = v
+        out = {}
+        for f, v in vals.items():
+            if f in ("txn", "user", "merchant", "ip", "dfp", "ua", "pay", "ttype", "ctype"):
+                b = _text_of_scalar(v)
+                if b is None:
+                    continue
+                if f == "txn":
+                    out["txn_hash"] = h64(b)
+                elif f == "user":
+                    out["card_key"] = h64(b)
+                elif f == "dfp":
+                    out["device_fp"] = h64(b)
+                elif f == "merchant":
+                    out["merchant"] = merchants.get(b.decode("utf-8", "surrogatepass"), -1)
+                elif f == "ip":
+                    out["ip_class"] = 1 if b.startswith((b"192.168.", b"10.", b"172.16.")) else 2
+                elif f == "ua":
+                    units = len(b.decode("utf-8", "surrogatepass").encode("utf-16-le", "surrogatepass")) // 2
+                    out["user_agent_flag"] = 1 if (b"bot" in b or b"crawler" in b or units < 20) else 0
+                else:
+                    key = {"pay": ("payment_method", 0), "ttype": ("transaction_type", 1),
+                           "ctype": ("card_type", 2)}[f]
+                    code = vocabs[key[1]].get(b.decode("utf-8", "surrogatepass"), VOCAB_OTHER)
+                    if code == VOCAB_OTHER:
+                        status |= UNKNOWN_VOCAB
+                    out[key[0]] = code
+            elif f == "amount":
+                d = _decimal_of(v)
+                if d is None:
+                    continue
+                c, inexact = cents_of(d)
+                text = v.text if isinstance(v, Num) else v
+                if inexact or _sig_digits(text) > 19:
+                    status |= INEXACT
+                out["amount_cents"] = c
+            elif f == "score":
+                d = _decimal_of(v)
+                if d is None:
+                    continue
+                out["fraud_score"] = float(d)
+            elif f == "ts":
+                if v is None:
+                    continue
+                if not isinstance(v, str) or "\\" in v:
+                    raise Malformed("timestamp")
+                ms = iso_to_ms(v)
+                if ms is None:
+                    raise Malformed("timestamp")
+                out["ts_ms"] = ms
+            elif f in ("geo", "mloc"):
+                if v is None:
+                    continue
+                if not isinstance(v, Obj):
+                    raise Malformed("location")
+                lat = lon = float("nan")
+                for k2, x in v:
+                    if k2 == "lat":
+                        lat = _f64(_decimal_of(x))
+                    elif k2 == "lon":
+                        lon = _f64(_decimal_of(x))
+                a, b = ("geo_lat", "geo_lon") if f == "geo" else ("merchant_lat", "merchant_lon")
+                out[a], out[b] = lat, lon
+            elif f in ("weekend", "fraud"):
+                if v is None:
+                    continue
+                if isinstance(v, bool):
+                    x = int(v)
+                elif isinstance(v, str) and v in ("true", "false"):
+                    x = int(v == "true")
+                elif isinstance(v, Num) and v.is_int:
+                    x = int(Decimal(v.text) != 0)
+                else:
+                    raise Malformed("boolean")
+                out["weekend" if f == "weekend" else "is_fraud"] = x
+            elif f == "hour":
+                d = _decimal_of(v)
+                if d is None:
+                    continue
+                if d < 0 and d != 0:
+                    raise Malformed("negative hour")
+                iv = int(d)  # truncation toward zero
+                if iv > 254:
+                    raise Malformed("hour")
+                out["hour"] = iv
+        if "card_key" not in out or "amount_cents" not in out or "ts_ms" not in out:
+            return dict(DEFAULT, status=MISSING)
+    except (Malformed, ValueError, KeyError, UnicodeDecodeError, RecursionError, TypeError):
+        return dict(DEFAULT, status=MALFORMED)
+    row.update(out)
+    row["status"] = status
+    return row
+
+
+def parse_batch(messages: List[bytes], merchants: Dict[str, int], vocabs: List[Dict[str, int]]) -> dict:
+    rows = [parse_message(m, merchants, vocabs) for m in messages]
+    dt = dict(card_key=np.uint64, ts_ms=np.int64, amount_cents=np.int64, merchant=np.int32, device_fp=np.uint64,
+              ip_class=np.uint8, hour=np.uint8, weekend=np.uint8, geo_lat=np.float64, geo_lon=np.float64,
+              merchant_lat=np.float64, merchant_lon=np.float64, payment_method=np.uint8, transaction_type=np.uint8,
+              card_type=np.uint8, user_agent_flag=np.uint8, fraud_score=np.float64, is_fraud=np.uint8,
+              txn_hash=np.uint64, status=np.uint8)
+    return {k: np.array([r[k] for r in rows], dtype=t) for k, t in dt.items()}

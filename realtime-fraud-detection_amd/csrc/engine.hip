@@ -6,6 +6,7 @@
 #include <string>
 
 #include "fd_internal.h"
+#include "ingest_parse.h"
 
 namespace fd {
 
@@ -715,6 +716,128 @@ int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, i
   if (watermark) *watermark = e.windows.wm;
   if (user_events) *user_events = e.windows.ucount;
   if (merchant_events) *merchant_events = e.windows.mcount;
+  FD_API_END
+}
+
+int fd_hash64(const uint8_t* bytes, int64_t n, uint64_t* out) {
+  FD_API_BEGIN
+  FD_REQUIRE(out && n >= 0 && (n == 0 || bytes), FD_ERR_INVALID_ARG, "bad arguments");
+  *out = fd::hash_bytes(bytes, n);
+  FD_API_END
+}
+
+int fd_ingest_set_vocab(fd_engine* eng, int32_t which, const uint8_t* bytes, const int64_t* offsets, int64_t n) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::ingest_set_vocab(e, which, bytes, offsets, n);
+  FD_API_END
+}
+
+int fd_ingest_set_merchants(fd_engine* eng, const uint8_t* bytes, const int64_t* offsets, int64_t n) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::ingest_set_merchants(e, bytes, offsets, n);
+  FD_API_END
+}
+
+int fd_ingest_json_device(fd_engine* eng, const uint8_t* d_bytes, const int64_t* d_offsets, int64_t n,
+                          const fd_ingest_out* d_out) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(d_out, FD_ERR_INVALID_ARG, "null outputs");
+  fd::launch_ingest(e, d_bytes, d_offsets, n, *d_out);
+  FD_API_END
+}
+
+int fd_ingest_json_host(fd_engine* eng, const uint8_t* bytes, const int64_t* offsets, int64_t n,
+                        const fd_ingest_out* out) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(out && offsets && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  if (n == 0) return FD_OK;
+  FD_REQUIRE(offsets[0] == 0 && offsets[n] >= 0, FD_ERR_INVALID_ARG, "offsets must start at 0");
+  const size_t nb = (size_t)offsets[n];
+  fd::IngestTables& t = e.ingest;
+  t.stage_bytes.ensure(std::max<size_t>(nb, 16));
+  t.stage_offsets.ensure((size_t)(n + 1) * 8);
+  if (nb) FD_HIP(hipMemcpyAsync(t.stage_bytes.ptr, bytes, nb, hipMemcpyHostToDevice, e.stream));
+  FD_HIP(hipMemcpyAsync(t.stage_offsets.ptr, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, e.stream));
+  // device columns: one staging block, 8-byte columns first
+  struct Col { void* host; size_t w; };
+  const Col cols[] = {{out->card_key, 8}, {out->ts_ms, 8}, {out->amount_cents, 8}, {out->device_fp, 8},
+                      {out->geo_lat, 8}, {out->geo_lon, 8}, {out->merchant_lat, 8}, {out->merchant_lon, 8},
+                      {out->fraud_score, 8}, {out->txn_hash, 8}, {out->merchant, 4}, {out->ip_class, 1},
+                      {out->hour, 1}, {out->weekend, 1}, {out->payment_method, 1}, {out->transaction_type, 1},
+                      {out->card_type, 1}, {out->user_agent_flag, 1}, {out->is_fraud, 1}, {out->status, 1}};
+  constexpr int NC = sizeof(cols) / sizeof(cols[0]);
+  size_t offs[NC], total = 0;
+  for (int c = 0; c < NC; ++c) {
+    offs[c] = total;
+    if (cols[c].host) total += ((size_t)n * cols[c].w + 15) & ~(size_t)15;
+  }
+  t.stage_out.ensure(std::max<size_t>(total, 16));
+  char* base = t.stage_out.as<char>();
+  auto dev = [&](int c) -> void* { return cols[c].host ? base + offs[c] : nullptr; };
+  fd_ingest_out d{};
+  d.card_key = (uint64_t*)dev(0);
+  d.ts_ms = (int64_t*)dev(1);
+  d.amount_cents = (int64_t*)dev(2);
+  d.device_fp = (uint64_t*)dev(3);
+  d.geo_lat = (double*)dev(4);
+  d.geo_lon = (double*)dev(5);
+  d.merchant_lat = (double*)dev(6);
+  d.merchant_lon = (double*)dev(7);
+  d.fraud_score = (double*)dev(8);
+  d.txn_hash = (uint64_t*)dev(9);
+  d.merchant = (int32_t*)dev(10);
+  d.ip_class = (uint8_t*)dev(11);
+  d.hour = (uint8_t*)dev(12);
+  d.weekend = (uint8_t*)dev(13);
+  d.payment_method = (uint8_t*)dev(14);
+  d.transaction_type = (uint8_t*)dev(15);
+  d.card_type = (uint8_t*)dev(16);
+  d.user_agent_flag = (uint8_t*)dev(17);
+  d.is_fraud = (uint8_t*)dev(18);
+  d.status = (uint8_t*)dev(19);
+  fd::launch_ingest(e, t.stage_bytes.as<const uint8_t>(), t.stage_offsets.as<const int64_t>(), n, d);
+  for (int c = 0; c < NC; ++c)
+    if (cols[c].host)
+      FD_HIP(hipMemcpyAsync(cols[c].host, base + offs[c], (size_t)n * cols[c].w, hipMemcpyDeviceToHost, e.stream));
+  FD_HIP(hipStreamSynchronize(e.stream));
+  FD_API_END
+}
+
+int fd_ingest_scalar_host(int32_t kind, const uint8_t* text, int32_t n, double* f64_out, int64_t* i64_out,
+                          int32_t* flags_out) {
+  FD_API_BEGIN
+  FD_REQUIRE(text && n >= 0 && flags_out, FD_ERR_INVALID_ARG, "bad arguments");
+  *flags_out = 0;
+  if (kind == 0 || kind == 1) {
+    fd::Decimal d;
+    const int end = fd::scan_number(text, 0, n, d);
+    if (end != n) {
+      *flags_out = 1;
+      return FD_OK;
+    }
+    if (kind == 0) {
+      bool amb = false;
+      const double v = fd::decimal_to_double(d.w, d.q, d.neg, d.many, &amb);
+      if (f64_out) *f64_out = v;
+      if (amb) *flags_out |= 2;
+    } else {
+      bool inexact = false;
+      int64_t c = 0;
+      if (!fd::decimal_to_cents(d, &c, &inexact)) *flags_out |= 1;
+      if (inexact) *flags_out |= 2;
+      if (i64_out) *i64_out = c;
+    }
+  } else if (kind == 2) {
+    int64_t ms = 0;
+    if (!fd::parse_iso_instant(text, 0, n, &ms)) *flags_out = 1;
+    if (i64_out) *i64_out = ms;
+  } else {
+    throw fd::Error(FD_ERR_INVALID_ARG, "unknown scalar kind");
+  }
   FD_API_END
 }
 

@@ -154,6 +154,14 @@ struct WindowState {
   DeviceBuffer keys, vals, sort_tmp, uout, mout, scalars, stage;
 };
 
+// JSON ingest codec lookup tables (ingest.hip): merchant ids and the three vocabularies, hash -> index
+struct IngestTables {
+  DeviceBuffer mkeys, mvals, vkeys[3], vvals[3];
+  unsigned long long mmask = 0, vmask[3] = {0, 0, 0};
+  bool mloaded = false, vloaded[3] = {false, false, false};
+  DeviceBuffer stage_bytes, stage_offsets, stage_out;  // host-API staging
+};
+
 inline int64_t floor_div_host(int64_t a, int64_t b) {
   int64_t q = a / b;
   if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
@@ -168,6 +176,7 @@ struct Engine {
   CardStore state;
   LstmModel lstm;
   WindowState windows;
+  IngestTables ingest;
   hipStream_t aux_stream = nullptr;            // LSTM head runs here, concurrent with the forests
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   hipStream_t aux2_stream = nullptr;           // small batches: the second forest, concurrent with the first
@@ -217,6 +226,10 @@ void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, 
                   fd_user_window* u_out, int64_t u_cap, int64_t* n_user, fd_merchant_window* m_out, int64_t m_cap,
                   int64_t* n_merch);
 void windows_release(Engine& e);
+// ingest.hip
+void ingest_set_vocab(Engine& e, int which, const uint8_t* bytes, const int64_t* offsets, int64_t n);
+void ingest_set_merchants(Engine& e, const uint8_t* bytes, const int64_t* offsets, int64_t n);
+void launch_ingest(Engine& e, const uint8_t* d_bytes, const int64_t* d_offsets, int64_t n, const fd_ingest_out& out);
 // snapshot.hip
 void state_snapshot(Engine& e, const char* path, int shard, int n_shards, int64_t* bytes_written);
 void state_restore(Engine& e, const char* path, int shard, int n_shards, int flags, int64_t* cards_restored);

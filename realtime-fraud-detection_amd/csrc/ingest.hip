@@ -1,0 +1,835 @@
+// ingest.hip — the Kafka JSON codec on the device: a micro-batch of raw transaction
+// messages -> the engine's SoA batch (fd_txn_batch + fd_txn_context + window inputs), in HBM.
+//
+// Reference: the simulator writes each transaction as json.dumps(asdict(Transaction), default=str)
+// (services/data-simulator/src/main/python/simulator.py:77-101 fields, :186 serializer, :376-385 send); the
+// Flink job reads it with TransactionDeserializationSchema.deserialize (fl/serialization/
+// TransactionDeserializationSchema.java:28-49: Jackson ObjectMapper + JavaTimeModule; on any exception an
+// ERROR placeholder transaction goes downstream). The derived codes follow FeatureExtractor
+// (fl/features/FeatureExtractor.java:300-325 device / IP / user agent, :434-451 isPrivateIP /
+// analyzeSuspiciousUserAgent, :366-381 payment / type / card). Declared semantics: DESIGN.md "Ingest".
+//
+// One wavefront per message, four per workgroup:
+//   stage      : 16-B coalesced loads of the message into LDS (<= 4 KiB; longer -> FD_INGEST_TOO_LONG)
+//   structure  : lane i owns bytes [64i, 64i+64): unescaped-quote parity -> wave prefix XOR (ballot) gives
+//                the in-string state at every segment start; bracket depth deltas -> wave prefix sum; the
+//                depth-1 ':' of every top-level member is recorded; balance / closure validated
+//   members    : lane j parses member j sequentially from LDS: key (decoded, FNV-1a -> field), value by the
+//                field's type (strings streamed through the hash / IP-prefix / user-agent matchers without
+//                materialising them, numbers by the exact decimal -> binary64 conversion of
+//                ingest_parse.h, ISO-8601 instants, the nested geolocation objects)
+//   resolve    : duplicate keys -> the last one wins (Jackson); missing / null fields -> defaults; lane f
+//                writes output column f for the message
+// HBM traffic per message: its bytes + 16 B of offsets in, ~100 B of SoA out.
+#include <cstring>
+
+#include "fd_internal.h"
+#include "ingest_parse.h"
+
+namespace fd {
+namespace {
+
+constexpr int kWaves = 4;
+constexpr int kMaxMsg = 4096;      // staged bytes per message (64 lanes x 64-byte segments)
+constexpr int kMaxMembers = 64;    // top-level members per message (one per lane; more -> malformed)
+constexpr int kStage = kMaxMsg + 32;
+
+enum Field : int {
+  F_TXN_ID, F_USER_ID, F_MERCHANT_ID, F_AMOUNT, F_TIMESTAMP, F_IP, F_DEVICE_FP, F_UA, F_GEO, F_MLOC,
+  F_WEEKEND, F_HOUR, F_FRAUD, F_SCORE, F_PAY, F_TTYPE, F_CTYPE, F_COUNT
+};
+
+// simulator (snake_case, simulator.py:77-101) and Java bean (camelCase) property names
+__device__ int field_of_key(uint64_t h) {
+#define FD_K(name, f) \
+  if (h == key_hash(name)) return f;
+  FD_K("transaction_id", F_TXN_ID) FD_K("transactionId", F_TXN_ID)
+  FD_K("user_id", F_USER_ID) FD_K("userId", F_USER_ID)
+  FD_K("merchant_id", F_MERCHANT_ID) FD_K("merchantId", F_MERCHANT_ID)
+  FD_K("amount", F_AMOUNT)
+  FD_K("timestamp", F_TIMESTAMP)
+  FD_K("ip_address", F_IP) FD_K("ipAddress", F_IP)
+  FD_K("device_fingerprint", F_DEVICE_FP) FD_K("deviceFingerprint", F_DEVICE_FP)
+  FD_K("user_agent", F_UA) FD_K("userAgent", F_UA)
+  FD_K("geolocation", F_GEO)
+  FD_K("merchant_location", F_MLOC) FD_K("merchantLocation", F_MLOC)
+  FD_K("is_weekend", F_WEEKEND) FD_K("isWeekend", F_WEEKEND)
+  FD_K("hour_of_day", F_HOUR) FD_K("hourOfDay", F_HOUR)
+  FD_K("is_fraud", F_FRAUD) FD_K("isFraud", F_FRAUD)
+  FD_K("fraud_score", F_SCORE) FD_K("fraudScore", F_SCORE)
+  FD_K("payment_method", F_PAY) FD_K("paymentMethod", F_PAY)
+  FD_K("transaction_type", F_TTYPE) FD_K("transactionType", F_TTYPE)
+  FD_K("card_type", F_CTYPE) FD_K("cardType", F_CTYPE)
+#undef FD_K
+  return -1;
+}
+
+struct LdsBytes {  // byte view of a wave's staged message
+  const unsigned char* p;
+  __device__ __forceinline__ int operator[](int i) const { return p[i]; }
+};
+
+__device__ __forceinline__ bool is_ws(int c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+__device__ __forceinline__ int hexval(int c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+// streaming view of one decoded JSON string: FNV-1a, UTF-16 length (Java String.length()), the first 8
+// decoded bytes, and the "bot" / "crawler" substring matchers (FeatureExtractor.java:447-451)
+struct StrStats {
+  uint64_t fnv = kFnvBasis;
+  uint64_t head = 0;  // first 8 decoded bytes, little-endian
+  uint64_t roll = 0;  // last 8 decoded bytes
+  int nbytes = 0;
+  int units = 0;
+  bool bot = false, crawler = false;
+  bool escaped = false;
+  __device__ __forceinline__ void byte(unsigned c) {
+    fnv = fnv_step(fnv, (unsigned char)c);
+    if (nbytes < 8) head |= (uint64_t)c << (8 * nbytes);
+    ++nbytes;
+    roll = (roll << 8) | c;
+    if ((roll & 0xFFFFFFull) == 0x626F74ull) bot = true;                 // "bot"
+    if ((roll & 0xFFFFFFFFFFFFFFull) == 0x637261776C6572ull) crawler = true;  // "crawler"
+  }
+  __device__ __forceinline__ void utf8(unsigned cp) {
+    if (cp < 0x80) {
+      byte(cp);
+    } else if (cp < 0x800) {
+      byte(0xC0 | (cp >> 6));
+      byte(0x80 | (cp & 0x3F));
+    } else if (cp < 0x10000) {
+      byte(0xE0 | (cp >> 12));
+      byte(0x80 | ((cp >> 6) & 0x3F));
+      byte(0x80 | (cp & 0x3F));
+    } else {
+      byte(0xF0 | (cp >> 18));
+      byte(0x80 | ((cp >> 12) & 0x3F));
+      byte(0x80 | ((cp >> 6) & 0x3F));
+      byte(0x80 | (cp & 0x3F));
+    }
+  }
+};
+
+// decode the string whose opening quote is at s[pos]; returns the index after the closing quote, -1 if malformed
+__device__ int scan_string(LdsBytes s, int pos, int end, StrStats& st) {
+  int i = pos + 1;
+  while (i < end) {
+    const int c = s[i];
+    if (c == '"') return i + 1;
+    if (c < 0x20) return -1;  // unescaped control character
+    if (c != '\\') {
+      st.byte((unsigned)c);
+      // UTF-16 units of raw UTF-8: one per lead byte, two for a 4-byte sequence
+      if ((c & 0xC0) != 0x80) st.units += (c >= 0xF0) ? 2 : 1;
+      ++i;
+      continue;
+    }
+    st.escaped = true;
+    if (i + 1 >= end) return -1;
+    const int e = s[i + 1];
+    i += 2;
+    unsigned cp;
+    switch (e) {
+      case '"': cp = '"'; break;
+      case '\\': cp = '\\'; break;
+      case '/': cp = '/'; break;
+      case 'b': cp = 8; break;
+      case 'f': cp = 12; break;
+      case 'n': cp = 10; break;
+      case 'r': cp = 13; break;
+      case 't': cp = 9; break;
+      case 'u': {
+        if (i + 4 > end) return -1;
+        int v = 0;
+        for (int k = 0; k < 4; ++k) {
+          const int h = hexval(s[i + k]);
+          if (h < 0) return -1;
+          v = v * 16 + h;
+        }
+        i += 4;
+        st.units += 1;
+        if (v >= 0xD800 && v <= 0xDBFF && i + 6 <= end && s[i] == '\\' && s[i + 1] == 'u') {
+          int lo = 0;
+          bool ok = true;
+          for (int k = 0; k < 4; ++k) {
+            const int h = hexval(s[i + 2 + k]);
+            ok = ok && h >= 0;
+            lo = lo * 16 + (h < 0 ? 0 : h);
+          }
+          if (ok && lo >= 0xDC00 && lo <= 0xDFFF) {
+            i += 6;
+            st.units += 1;
+            st.utf8(0x10000u + (((unsigned)v - 0xD800u) << 10) + ((unsigned)lo - 0xDC00u));
+            continue;
+          }
+        }
+        // lone surrogates: Java keeps them; their UTF-8 (CESU) bytes are hashed as is
+        st.utf8((unsigned)v);
+        continue;
+      }
+      default: return -1;
+    }
+    st.units += 1;
+    st.byte(cp);
+  }
+  return -1;
+}
+
+__device__ __forceinline__ bool lit_at(LdsBytes s, int i, int end, const char* w, int n);
+
+// skip one JSON value at s[pos], validated by the RFC 8259 grammar (nesting <= 64); returns the index after
+// it, -1 if malformed
+__device__ int skip_value(LdsBytes s, int pos, int end) {
+  enum { VALUE, VALUE_OR_CLOSE, KEY, KEY_OR_CLOSE, COLON, COMMA_OR_CLOSE };
+  unsigned long long objects = 0ull;  // bit d: level d+1 is an object (else an array)
+  int depth = 0, state = VALUE, i = pos;
+  for (;;) {
+    while (i < end && is_ws(s[i])) ++i;
+    if (i >= end) return -1;
+    const int c = s[i];
+    bool value_done = false;
+    if (state == VALUE || state == VALUE_OR_CLOSE) {
+      if (state == VALUE_OR_CLOSE && c == ']') {
+        --depth;
+        ++i;
+        value_done = true;
+      } else if (c == '{' || c == '[') {
+        if (depth == 64) return -1;
+        if (c == '{') objects |= 1ull << depth; else objects &= ~(1ull << depth);
+        ++depth;
+        ++i;
+        state = c == '{' ? KEY_OR_CLOSE : VALUE_OR_CLOSE;
+        continue;
+      } else if (c == '"') {
+        StrStats st;
+        i = scan_string(s, i, end, st);
+        if (i < 0) return -1;
+        value_done = true;
+      } else if (c == 't' || c == 'f' || c == 'n') {
+        const int n = c == 'f' ? 5 : 4;
+        if (!lit_at(s, i, end, c == 't' ? "true" : (c == 'f' ? "false" : "null"), n)) return -1;
+        i += n;
+        value_done = true;
+      } else {
+        Decimal d;
+        i = scan_number(s, i, end, d);
+        if (i < 0) return -1;
+        value_done = true;
+      }
+    } else if (state == KEY || state == KEY_OR_CLOSE) {
+      if (state == KEY_OR_CLOSE && c == '}') {
+        --depth;
+        ++i;
+        value_done = true;
+      } else {
+        if (c != '"') return -1;
+        StrStats st;
+        i = scan_string(s, i, end, st);
+        if (i < 0) return -1;
+        state = COLON;
+        continue;
+      }
+    } else if (state == COLON) {
+      if (c != ':') return -1;
+      ++i;
+      state = VALUE;
+      continue;
+    } else {  // COMMA_OR_CLOSE
+      const bool obj = (objects >> (depth - 1)) & 1ull;
+      if (c == ',') {
+        ++i;
+        state = obj ? KEY : VALUE;
+        continue;
+      }
+      if (c != (obj ? '}' : ']')) return -1;
+      --depth;
+      ++i;
+      value_done = true;
+    }
+    if (value_done) {
+      if (depth == 0) return i;
+      state = COMMA_OR_CLOSE;
+    }
+  }
+}
+
+__device__ __forceinline__ bool lit_at(LdsBytes s, int i, int end, const char* w, int n) {  // NOLINT
+  if (i + n > end) return false;
+  for (int k = 0; k < n; ++k)
+    if (s[i + k] != w[k]) return false;
+  return true;
+}
+
+// a number or a string holding a JSON number (Jackson's String -> Double coercion), or null
+// kind: 0 = null, 1 = number; returns end index or -1
+__device__ int scan_numeric(LdsBytes s, int pos, int end, Decimal& d, int* kind) {
+  if (lit_at(s, pos, end, "null", 4)) {
+    *kind = 0;
+    return pos + 4;
+  }
+  *kind = 1;
+  if (s[pos] == '"') {
+    int close = pos + 1;
+    while (close < end && s[close] != '"' && s[close] != '\\') ++close;
+    if (close >= end || s[close] != '"') return -1;
+    const int e = scan_number(s, pos + 1, close, d);
+    return e == close ? close + 1 : -1;
+  }
+  return scan_number(s, pos, end, d);
+}
+
+__device__ __forceinline__ double nan_d() { return __builtin_nan(""); }
+
+// geolocation / merchant_location: {"lat": x, "lon": y, ...} or null
+__device__ int scan_latlon(LdsBytes s, int pos, int end, double* lat, double* lon, bool* inexact) {
+  *lat = *lon = nan_d();
+  if (lit_at(s, pos, end, "null", 4)) return pos + 4;
+  if (s[pos] != '{') return -1;
+  int i = pos + 1;
+  while (i < end && is_ws(s[i])) ++i;
+  if (i < end && s[i] == '}') return i + 1;
+  const uint64_t kLat = key_hash("lat"), kLon = key_hash("lon");
+  while (i < end) {
+    if (s[i] != '"') return -1;
+    StrStats k;
+    i = scan_string(s, i, end, k);
+    if (i < 0) return -1;
+    while (i < end && is_ws(s[i])) ++i;
+    if (i >= end || s[i] != ':') return -1;
+    ++i;
+    while (i < end && is_ws(s[i])) ++i;
+    if (i >= end) return -1;
+    if (k.fnv == kLat || k.fnv == kLon) {
+      Decimal d;
+      int kind;
+      i = scan_numeric(s, i, end, d, &kind);
+      if (i < 0) return -1;
+      bool amb = false;
+      const double v = kind ? decimal_to_double(d.w, d.q, d.neg, d.many, &amb) : nan_d();
+      if (amb) *inexact = true;
+      if (k.fnv == kLat) *lat = v; else *lon = v;
+    } else {
+      i = skip_value(s, i, end);
+      if (i < 0) return -1;
+    }
+    while (i < end && is_ws(s[i])) ++i;
+    if (i >= end) return -1;
+    if (s[i] == '}') return i + 1;
+    if (s[i] != ',') return -1;
+    ++i;
+    while (i < end && is_ws(s[i])) ++i;
+  }
+  return -1;
+}
+
+struct Table {  // open addressing: hash -> value (key 0 = empty)
+  const unsigned long long* keys;
+  const int* vals;
+  unsigned long long mask;
+};
+
+__device__ __forceinline__ int table_find(const Table& t, uint64_t h, int miss) {
+  if (!t.keys) return miss;
+  if (h == 0) h = 1;
+  unsigned long long s = fmix64_hd(h ^ 0x9E3779B97F4A7C15ull) & t.mask;
+  for (unsigned long long p = 0; p <= t.mask; ++p) {
+    const unsigned long long k = t.keys[s];
+    if (k == h) return t.vals[s];
+    if (k == 0) return miss;
+    s = (s + 1) & t.mask;
+  }
+  return miss;
+}
+
+struct Tables {
+  Table merchants, vocab[3];
+};
+
+// a parsed field value (the lane's member)
+struct Val {
+  uint64_t u = 0;                // hashes, cents, ts, codes
+  double a = 0.0, b = 0.0;       // f64 values (score, lat, lon)
+  bool null = true;
+};
+
+__global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* __restrict__ buf,
+                                                          const int64_t* __restrict__ offsets, int64_t n, Tables T,
+                                                          fd_ingest_out out) {
+  __shared__ __attribute__((aligned(16))) unsigned char stage[kWaves][kStage];
+  __shared__ int colon[kWaves][kMaxMembers];
+  __shared__ int nmem[kWaves], ncomma[kWaves];
+  __shared__ unsigned status_s[kWaves];
+  __shared__ int win[kWaves][F_COUNT];
+
+  const int wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * kWaves + wv;
+  const bool live = m < n;
+  int64_t off = 0, len = 0;
+  if (live) {
+    off = offsets[m];
+    len = offsets[m + 1] - off;
+  }
+  const int64_t total_bytes = offsets[n];
+  if (lane == 0) {
+    nmem[wv] = 0;
+    ncomma[wv] = 0;
+    status_s[wv] = (live && (len > kMaxMsg || len < 0)) ? FD_INGEST_TOO_LONG : 0u;
+  }
+  if (lane < F_COUNT) win[wv][lane] = -1;
+  const bool go = live && len >= 0 && len <= kMaxMsg;
+  const int L = go ? (int)len : 0;
+  // ---- stage (aligned 16-B loads; the tail beyond the input buffer byte by byte)
+  const int64_t a0 = off & ~15ll;
+  const int shift = (int)(off - a0);
+  const int span = shift + L;
+  for (int k = lane; k * 16 < span; k += 64) {
+    const int64_t g = a0 + 16ll * k;
+    uint4 v;
+    if (g + 16 <= total_bytes) {
+      v = *reinterpret_cast<const uint4*>(buf + g);
+    } else {
+      unsigned char tmp[16];
+      for (int q = 0; q < 16; ++q) tmp[q] = (g + q < total_bytes) ? buf[g + q] : 0;
+      memcpy(&v, tmp, 16);
+    }
+    *reinterpret_cast<uint4*>(&stage[wv][16 * k]) = v;
+  }
+  __syncthreads();
+  const LdsBytes s{&stage[wv][shift]};
+
+  // ---- structure: quote parity per 64-byte segment
+  const int s0 = lane * 64, s1 = min(s0 + 64, L);
+  int bs = 0;
+  for (int p = s0 - 1; p >= 0 && s0 < L && s[p] == '\\'; --p) ++bs;
+  const int bs0 = bs;
+  int par = 0;
+  for (int p = s0; p < s1; ++p) {
+    const int c = s[p];
+    if (c == '"' && !(bs & 1)) par ^= 1;
+    bs = (c == '\\') ? bs + 1 : 0;
+  }
+  const unsigned long long pb = __ballot(par);
+  const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int in0 = __popcll(pb & lt) & 1;
+  const int total_par = __popcll(pb) & 1;
+  // depth deltas outside strings
+  int in = in0, delta = 0, mind = 0;
+  bs = bs0;
+  for (int p = s0; p < s1; ++p) {
+    const int c = s[p];
+    if (c == '"' && !(bs & 1)) {
+      in ^= 1;
+    } else if (!in) {
+      if (c == '{' || c == '[') ++delta;
+      if (c == '}' || c == ']') {
+        --delta;
+        mind = min(mind, delta);
+      }
+    }
+    bs = (c == '\\') ? bs + 1 : 0;
+  }
+  int depth0 = delta;  // exclusive prefix sum over lanes
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(depth0, d);
+    if (lane >= d) depth0 += v;
+  }
+  const int total_depth = __shfl(depth0, 63);
+  depth0 -= delta;
+  // first / last non-whitespace bytes (validation: the message is exactly one object)
+  int first_nw = L, last_nw = -1;
+  for (int p = s0; p < s1; ++p) {
+    if (!is_ws(s[p])) {
+      first_nw = min(first_nw, p);
+      last_nw = p;
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    first_nw = min(first_nw, __shfl_xor(first_nw, d));
+    last_nw = max(last_nw, __shfl_xor(last_nw, d));
+  }
+  bool bad = (depth0 + mind < 0);
+  // depth-1 colons (members) and the first return to depth 0
+  in = in0;
+  bs = bs0;
+  int depth = depth0, zero_at = L;
+  for (int p = s0; p < s1; ++p) {
+    const int c = s[p];
+    if (c == '"' && !(bs & 1)) {
+      in ^= 1;
+    } else if (!in) {
+      if (c == ':' && depth == 1) {
+        const int slot = atomicAdd(&nmem[wv], 1);
+        if (slot < kMaxMembers) colon[wv][slot] = p;
+      } else if (c == ',' && depth == 1) {
+        atomicAdd(&ncomma[wv], 1);
+      } else if (c == '{' || c == '[') {
+        ++depth;
+      } else if (c == '}' || c == ']') {
+        --depth;
+        if (depth == 0) zero_at = min(zero_at, p);
+      }
+    }
+    bs = (c == '\\') ? bs + 1 : 0;
+  }
+  for (int d = 32; d >= 1; d >>= 1) zero_at = min(zero_at, __shfl_xor(zero_at, d));
+  bad = bad || (__ballot(bad) != 0ull);
+  if (go && lane == 0) {
+    const bool ok = !bad && L > 0 && total_par == 0 && total_depth == 0 && first_nw < L && s[first_nw] == '{' &&
+                    zero_at == last_nw;
+    if (!ok) status_s[wv] |= FD_INGEST_MALFORMED;
+  }
+  __syncthreads();
+  const int nm = go ? nmem[wv] : 0;
+  if (go && lane == 0 && status_s[wv] == 0u) {
+    // member skeleton: n members <-> n-1 depth-1 commas; an empty object holds only whitespace
+    bool bad_skel = nm > kMaxMembers || (nm > 0 && ncomma[wv] != nm - 1) || (nm == 0 && ncomma[wv] != 0);
+    if (nm == 0) {
+      int q = first_nw + 1;
+      while (q < L && is_ws(s[q])) ++q;
+      bad_skel = bad_skel || q != zero_at;
+    }
+    if (bad_skel) status_s[wv] |= FD_INGEST_MALFORMED;
+  }
+  __syncthreads();
+  const bool structural_ok = go && status_s[wv] == 0u;
+
+  // ---- members: lane j parses member j
+  int my_field = -1, my_colon = -1;
+  Val my;
+  unsigned my_status = 0;
+  for (int once = 0; once < 1 && structural_ok && lane < nm; ++once) {  // `continue` = member rejected
+    const int c = colon[wv][lane];
+    // key: the string ending right before the colon
+    int kc = c - 1;
+    while (kc >= 0 && is_ws(s[kc])) --kc;
+    if (kc < 1 || s[kc] != '"') {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    int ko = kc - 1;
+    for (;; --ko) {
+      if (ko < 0) break;
+      if (s[ko] == '"') {
+        int r = 0;
+        for (int q = ko - 1; q >= 0 && s[q] == '\\'; --q) ++r;
+        if (!(r & 1)) break;
+      }
+    }
+    int pre = ko - 1;
+    while (pre >= 0 && is_ws(s[pre])) --pre;
+    if (ko < 0 || pre < 0 || (s[pre] != '{' && s[pre] != ',')) {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    StrStats key;
+    if (scan_string(s, ko, L, key) != kc + 1) {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    const int f = field_of_key(key.fnv);
+    int v = c + 1;
+    while (v < L && is_ws(s[v])) ++v;
+    if (v >= L) {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    if (f < 0) {  // unknown property: validated, then ignored (@JsonIgnoreProperties(ignoreUnknown = true))
+      int e = skip_value(s, v, L);
+      while (e >= 0 && e < L && is_ws(s[e])) ++e;
+      if (e < 0 || e >= L || (s[e] != ',' && s[e] != '}')) my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    int e = -1;
+    Val val;
+    val.null = false;
+    const int ch = s[v];
+    switch (f) {
+      case F_TXN_ID: case F_USER_ID: case F_MERCHANT_ID: case F_IP: case F_DEVICE_FP: case F_UA:
+      case F_PAY: case F_TTYPE: case F_CTYPE: {
+        StrStats st;
+        if (ch == '"') {
+          e = scan_string(s, v, L, st);
+        } else if (lit_at(s, v, L, "null", 4)) {
+          e = v + 4;
+          val.null = true;
+        } else {  // scalar -> String coercion: the literal text
+          e = v;
+          while (e < L && !is_ws(s[e]) && s[e] != ',' && s[e] != '}') {
+            const int b = s[e];
+            if (b == '{' || b == '[' || b == '"') {
+              e = -1;
+              break;
+            }
+            st.byte((unsigned)b);
+            ++st.units;
+            ++e;
+          }
+          if (e == v) e = -1;
+        }
+        if (e < 0 || val.null) break;
+        const uint64_t h = hash_finish(st.fnv);
+        if (f == F_IP) {
+          const bool priv = (st.nbytes >= 8 && st.head == 0x2E3836312E323931ull) ||            // "192.168."
+                            (st.nbytes >= 3 && (st.head & 0xFFFFFFull) == 0x2E3031ull) ||       // "10."
+                            (st.nbytes >= 7 && (st.head & 0xFFFFFFFFFFFFFFull) == 0x2E36312E323731ull);  // "172.16."
+          val.u = priv ? 1 : 2;
+        } else if (f == F_UA) {
+          val.u = (st.bot || st.crawler || st.units < 20) ? 1 : 0;
+        } else if (f == F_MERCHANT_ID) {
+          val.u = (uint64_t)(int64_t)table_find(T.merchants, h, -1);
+        } else if (f == F_PAY || f == F_TTYPE || f == F_CTYPE) {
+          const int code = table_find(T.vocab[f - F_PAY], h, FD_VOCAB_OTHER);
+          if (code == FD_VOCAB_OTHER) my_status |= FD_INGEST_UNKNOWN_VOCAB;
+          val.u = (uint64_t)code;
+        } else {
+          val.u = h;
+        }
+        break;
+      }
+      case F_AMOUNT: case F_SCORE: {
+        Decimal d;
+        int kind;
+        e = scan_numeric(s, v, L, d, &kind);
+        if (e < 0) break;
+        if (!kind) {
+          val.null = true;
+          break;
+        }
+        if (f == F_AMOUNT) {
+          bool inexact = false;
+          int64_t cents;
+          if (!decimal_to_cents(d, &cents, &inexact)) {
+            e = -1;
+            break;
+          }
+          if (inexact) my_status |= FD_INGEST_INEXACT;
+          val.u = (uint64_t)cents;
+        } else {
+          bool amb = false;
+          val.a = decimal_to_double(d.w, d.q, d.neg, d.many, &amb);
+          if (amb) my_status |= FD_INGEST_INEXACT;
+        }
+        break;
+      }
+      case F_TIMESTAMP: {
+        if (lit_at(s, v, L, "null", 4)) {
+          e = v + 4;
+          val.null = true;
+          break;
+        }
+        if (ch != '"') break;
+        int close = v + 1;
+        while (close < L && s[close] != '"' && s[close] != '\\') ++close;
+        if (close >= L || s[close] != '"') break;
+        int64_t ms;
+        if (!parse_iso_instant(s, v + 1, close, &ms)) break;
+        val.u = (uint64_t)ms;
+        e = close + 1;
+        break;
+      }
+      case F_GEO: case F_MLOC: {
+        bool inexact = false;
+        e = scan_latlon(s, v, L, &val.a, &val.b, &inexact);
+        if (inexact) my_status |= FD_INGEST_INEXACT;
+        break;
+      }
+      case F_WEEKEND: case F_FRAUD: {
+        if (lit_at(s, v, L, "true", 4)) {
+          val.u = 1;
+          e = v + 4;
+        } else if (lit_at(s, v, L, "false", 5)) {
+          val.u = 0;
+          e = v + 5;
+        } else if (lit_at(s, v, L, "null", 4)) {
+          val.null = true;
+          e = v + 4;
+        } else if (lit_at(s, v, L, "\"true\"", 6)) {
+          val.u = 1;
+          e = v + 6;
+        } else if (lit_at(s, v, L, "\"false\"", 7)) {
+          val.u = 0;
+          e = v + 7;
+        } else {  // integer coercion: 0 -> false, other -> true
+          Decimal d;
+          e = scan_number(s, v, L, d);
+          if (e >= 0 && d.frac_or_exp) e = -1;
+          if (e >= 0) val.u = d.w != 0 ? 1 : 0;
+        }
+        break;
+      }
+      case F_HOUR: {
+        Decimal d;
+        int kind;
+        e = scan_numeric(s, v, L, d, &kind);
+        if (e < 0) break;
+        if (!kind) {
+          val.null = true;
+          break;
+        }
+        // integer value (a fraction truncates toward zero, Jackson ACCEPT_FLOAT_AS_INT); hours 0..254
+        int64_t iv = 0;
+        bool ok = !d.neg || d.w == 0;
+        if (ok && d.w) {
+          if (d.q >= 0) {
+            ok = d.w <= 254 && d.q <= 3;
+            iv = (int64_t)d.w;
+            for (int k = 0; ok && k < d.q; ++k) iv *= 10;
+          } else if (-d.q <= 19) {
+            uint64_t p = 1;
+            for (int k = 0; k < -d.q; ++k) p *= 10;
+            iv = (int64_t)(d.w / p);
+          }
+        }
+        if (!ok || iv > 254) {
+          e = -1;
+          break;
+        }
+        val.u = (uint64_t)iv;
+        break;
+      }
+      default: break;
+    }
+    if (e < 0) {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    while (e < L && is_ws(s[e])) ++e;
+    if (e >= L || (s[e] != ',' && s[e] != '}')) {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    my_field = f;
+    my_colon = c;
+    my = val;
+    atomicMax(&win[wv][f], c);
+  }
+  if (my_status) atomicOr(&status_s[wv], my_status);
+  __syncthreads();
+  // ---- resolve: the winner of each field publishes its value to LDS, then lane f writes column f
+  __shared__ unsigned long long vu[kWaves][F_COUNT];
+  __shared__ double va[kWaves][F_COUNT], vb[kWaves][F_COUNT];
+  __shared__ unsigned char vnull[kWaves][F_COUNT];
+  if (go && my_field >= 0 && win[wv][my_field] == my_colon) {
+    vu[wv][my_field] = my.u;
+    va[wv][my_field] = my.a;
+    vb[wv][my_field] = my.b;
+    vnull[wv][my_field] = my.null ? 1 : 0;
+  }
+  __syncthreads();
+  if (!live) return;
+  unsigned st = status_s[wv];
+  const bool valid_struct = (st & (FD_INGEST_MALFORMED | FD_INGEST_TOO_LONG)) == 0;
+  auto present = [&](int f) { return valid_struct && win[wv][f] >= 0 && !vnull[wv][f]; };
+  if (valid_struct && (!present(F_USER_ID) || !present(F_AMOUNT) || !present(F_TIMESTAMP))) st |= FD_INGEST_MISSING;
+  const bool ok = (st & (FD_INGEST_MALFORMED | FD_INGEST_TOO_LONG | FD_INGEST_MISSING)) == 0;
+  if (!ok) st &= (FD_INGEST_MALFORMED | FD_INGEST_TOO_LONG | FD_INGEST_MISSING);  // an invalid row: its class only
+  const int f = lane;
+  if (f < F_COUNT) {
+    const bool p = ok && present(f);
+    const unsigned long long u = p ? vu[wv][f] : 0ull;
+    const double A = p ? va[wv][f] : nan_d(), B = p ? vb[wv][f] : nan_d();
+    switch (f) {
+      case F_TXN_ID: if (out.txn_hash) out.txn_hash[m] = u; break;
+      case F_USER_ID: if (out.card_key) out.card_key[m] = u; break;
+      case F_MERCHANT_ID: if (out.merchant) out.merchant[m] = p ? (int)(long long)u : -1; break;
+      case F_AMOUNT: if (out.amount_cents) out.amount_cents[m] = (long long)u; break;
+      case F_TIMESTAMP: if (out.ts_ms) out.ts_ms[m] = (long long)u; break;
+      case F_IP: if (out.ip_class) out.ip_class[m] = p ? (unsigned char)u : 0; break;
+      case F_DEVICE_FP: if (out.device_fp) out.device_fp[m] = u; break;
+      case F_UA: if (out.user_agent_flag) out.user_agent_flag[m] = p ? (unsigned char)u : 255; break;
+      case F_GEO:
+        if (out.geo_lat) out.geo_lat[m] = A;
+        if (out.geo_lon) out.geo_lon[m] = B;
+        break;
+      case F_MLOC:
+        if (out.merchant_lat) out.merchant_lat[m] = A;
+        if (out.merchant_lon) out.merchant_lon[m] = B;
+        break;
+      case F_WEEKEND: if (out.weekend) out.weekend[m] = p ? (unsigned char)u : 255; break;
+      case F_HOUR: if (out.hour) out.hour[m] = p ? (unsigned char)u : 255; break;
+      case F_FRAUD: if (out.is_fraud) out.is_fraud[m] = p ? (unsigned char)u : 0; break;
+      case F_SCORE: if (out.fraud_score) out.fraud_score[m] = A; break;
+      case F_PAY: if (out.payment_method) out.payment_method[m] = p ? (unsigned char)u : 255; break;
+      case F_TTYPE: if (out.transaction_type) out.transaction_type[m] = p ? (unsigned char)u : 255; break;
+      case F_CTYPE: if (out.card_type) out.card_type[m] = p ? (unsigned char)u : 255; break;
+      default: break;
+    }
+  } else if (f == 63 && out.status) {
+    out.status[m] = (unsigned char)st;
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host side
+
+namespace {
+
+void build_table(DeviceBuffer& keys, DeviceBuffer& vals, unsigned long long* mask, const uint8_t* bytes,
+                 const int64_t* offsets, int64_t n, hipStream_t stream) {
+  uint64_t cap = 16;
+  while (cap < (uint64_t)std::max<int64_t>(n, 1) * 2) cap <<= 1;
+  std::vector<unsigned long long> k(cap, 0ull);
+  std::vector<int> v(cap, -1);
+  for (int64_t i = 0; i < n; ++i) {
+    FD_REQUIRE(offsets[i + 1] >= offsets[i], FD_ERR_INVALID_ARG, "vocabulary offsets must be non-decreasing");
+    uint64_t h = hash_bytes(bytes + offsets[i], offsets[i + 1] - offsets[i]);
+    if (h == 0) h = 1;
+    uint64_t s = fmix64_hd(h ^ 0x9E3779B97F4A7C15ull) & (cap - 1);
+    while (k[s] != 0ull && k[s] != h) s = (s + 1) & (cap - 1);
+    if (k[s] == h) continue;  // duplicate string: the first position keeps its index
+    k[s] = h;
+    v[s] = (int)i;
+  }
+  keys.ensure(cap * 8);
+  vals.ensure(cap * 4);
+  FD_HIP(hipMemcpyAsync(keys.ptr, k.data(), cap * 8, hipMemcpyHostToDevice, stream));
+  FD_HIP(hipMemcpyAsync(vals.ptr, v.data(), cap * 4, hipMemcpyHostToDevice, stream));
+  FD_HIP(hipStreamSynchronize(stream));
+  *mask = cap - 1;
+}
+
+}  // namespace
+
+void ingest_set_vocab(Engine& e, int which, const uint8_t* bytes, const int64_t* offsets, int64_t n) {
+  FD_REQUIRE(which >= 0 && which < 3, FD_ERR_INVALID_ARG, "unknown vocabulary");
+  FD_REQUIRE(n >= 0 && n <= FD_VOCAB_OTHER, FD_ERR_INVALID_ARG, "a vocabulary holds at most 254 strings");
+  FD_REQUIRE(n == 0 || (bytes && offsets), FD_ERR_INVALID_ARG, "null vocabulary");
+  IngestTables& t = e.ingest;
+  build_table(t.vkeys[which], t.vvals[which], &t.vmask[which], bytes, offsets, n, e.stream);
+  t.vloaded[which] = true;
+}
+
+void ingest_set_merchants(Engine& e, const uint8_t* bytes, const int64_t* offsets, int64_t n) {
+  FD_REQUIRE(n >= 0 && n < (1ll << 31), FD_ERR_INVALID_ARG, "merchant count out of range");
+  FD_REQUIRE(n == 0 || (bytes && offsets), FD_ERR_INVALID_ARG, "null merchant ids");
+  IngestTables& t = e.ingest;
+  build_table(t.mkeys, t.mvals, &t.mmask, bytes, offsets, n, e.stream);
+  t.mloaded = true;
+}
+
+void launch_ingest(Engine& e, const uint8_t* d_bytes, const int64_t* d_offsets, int64_t n, const fd_ingest_out& out) {
+  FD_REQUIRE(n >= 0 && n <= (1ll << 30), FD_ERR_INVALID_ARG, "message count out of range (<= 2^30 per call)");
+  FD_REQUIRE(d_offsets, FD_ERR_INVALID_ARG, "null offsets");
+  if (n == 0) return;
+  FD_REQUIRE(d_bytes, FD_ERR_INVALID_ARG, "null message bytes");
+  IngestTables& t = e.ingest;
+  Tables T{};
+  if (t.mloaded) T.merchants = Table{t.mkeys.as<const unsigned long long>(), t.mvals.as<const int>(), t.mmask};
+  for (int w = 0; w < 3; ++w)
+    if (t.vloaded[w]) T.vocab[w] = Table{t.vkeys[w].as<const unsigned long long>(), t.vvals[w].as<const int>(), t.vmask[w]};
+  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_INGEST) : nullptr;
+  if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
+  const int64_t blocks = (n + kWaves - 1) / kWaves;
+  hipLaunchKernelGGL(ingest_json_kernel, dim3((unsigned)blocks), dim3(256), 0, e.stream, d_bytes, d_offsets, n, T, out);
+  FD_HIP(hipGetLastError());
+  if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
+}
+
+}  // namespace fd

@@ -146,6 +146,22 @@ FD_TIMING_ALL, FD_TIMING_XGB, FD_TIMING_IFOREST, FD_TIMING_FEATURES, FD_TIMING_B
 FD_TIMING_ROUTE = 4
 FD_TIMING_LSTM = 5
 FD_TIMING_WINDOWS = 6
+FD_TIMING_INGEST = 7
+
+# JSON ingest codec (fd_ingest_out column order and dtypes)
+INGEST_FIELDS = (("card_key", "<u8"), ("ts_ms", "<i8"), ("amount_cents", "<i8"), ("merchant", "<i4"),
+                 ("device_fp", "<u8"), ("ip_class", "u1"), ("hour", "u1"), ("weekend", "u1"), ("geo_lat", "<f8"),
+                 ("geo_lon", "<f8"), ("merchant_lat", "<f8"), ("merchant_lon", "<f8"), ("payment_method", "u1"),
+                 ("transaction_type", "u1"), ("card_type", "u1"), ("user_agent_flag", "u1"),
+                 ("fraud_score", "<f8"), ("is_fraud", "u1"), ("txn_hash", "<u8"), ("status", "u1"))
+FD_VOCAB_OTHER = 254
+FD_VOCAB_PAYMENT_METHOD, FD_VOCAB_TRANSACTION_TYPE, FD_VOCAB_CARD_TYPE = 0, 1, 2
+FD_INGEST_MALFORMED, FD_INGEST_TOO_LONG, FD_INGEST_UNKNOWN_VOCAB, FD_INGEST_INEXACT, FD_INGEST_MISSING = 1, 2, 4, 8, 16
+FD_INGEST_INVALID = FD_INGEST_MALFORMED | FD_INGEST_TOO_LONG | FD_INGEST_MISSING
+
+
+class fd_ingest_out(C.Structure):
+    _fields_ = [(name, C.c_void_p) for name, _ in INGEST_FIELDS]
 
 
 class fd_window_params(C.Structure):
@@ -236,6 +252,12 @@ SIGNATURES = {
     "fd_windows_stats": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64)]),
     "fd_state_snapshot": (C.c_int, [_vp, C.c_char_p, _i32, _i32, C.POINTER(_i64)]),
     "fd_state_restore": (C.c_int, [_vp, C.c_char_p, _i32, _i32, _i32, C.POINTER(_i64)]),
+    "fd_hash64": (C.c_int, [_vp, _i64, C.POINTER(C.c_uint64)]),
+    "fd_ingest_set_vocab": (C.c_int, [_vp, _i32, _vp, _vp, _i64]),
+    "fd_ingest_set_merchants": (C.c_int, [_vp, _vp, _vp, _i64]),
+    "fd_ingest_json_device": (C.c_int, [_vp, _vp, _vp, _i64, C.POINTER(fd_ingest_out)]),
+    "fd_ingest_json_host": (C.c_int, [_vp, _vp, _vp, _i64, C.POINTER(fd_ingest_out)]),
+    "fd_ingest_scalar_host": (C.c_int, [_i32, _vp, _i32, _dp, C.POINTER(_i64), C.POINTER(_i32)]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
     "fd_timing_read": (C.c_int, [_vp, C.c_int, _dp, C.POINTER(_i64)]),

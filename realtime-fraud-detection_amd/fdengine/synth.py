@@ -428,3 +428,94 @@ def window_stream(n_batches: int, batch: int, n_cards: int, n_merchants: int, se
         out.append(dict(key=keys[idx], ts_ms=ts.astype(np.int64), amount_cents=cents, merchant=merchant,
                         payment_method=pm, is_fraud=fraud, fraud_score=score))
     return out
+
+
+# ------------------------------------------------------------------ Kafka JSON messages (ingest codec)
+SIM_PAYMENT_METHODS = ("credit_card", "debit_card", "digital_wallet", "bank_transfer")   # simulator.py:331
+SIM_TXN_TYPES = ("purchase", "refund", "authorization")                                   # simulator.py:330
+SIM_CARD_TYPES = ("visa", "mastercard", "amex", "discover")                               # simulator.py:332
+USER_AGENTS = (
+    "Mozilla/5.0 (Windows NT 10.0; Win64; x64) AppleWebKit/537.36 (KHTML, like Gecko) Chrome/120.0 Safari/537.36",
+    "Mozilla/5.0 (Macintosh; Intel Mac OS X 10_15_7) AppleWebKit/605.1.15 (KHTML, like Gecko) Version/17.1 Safari/605.1.15",
+    "Mozilla/5.0 (iPhone; CPU iPhone OS 17_0 like Mac OS X) AppleWebKit/605.1.15 Mobile/15E148",
+    "Mozilla/5.0 (compatible; Googlebot/2.1; +http://www.google.com/bot.html)",
+    "Opera/9.80 (X11; Linux x86_64) Presto/2.12.388 Version/12.16",
+    "curl/8.4.0",
+    "python-requests/2.31",
+    "Mozilla/5.0 (X11; Linux x86_64; rv:121.0) Gecko/20100101 Firefox/121.0 crawler-test",
+    "Mozilla/5.0 (Linux; Android 14; Pixel 8) AppleWebKit/537.36 Chrome/120.0 Mobile Safari/537.36 é中",
+)
+
+
+def _uuid(rng) -> str:
+    import uuid
+    return str(uuid.UUID(bytes=rng.bytes(16), version=4))
+
+
+def sim_population(n_users: int, n_merchants: int, seed: int = 42) -> dict:
+    """User / merchant id strings in the simulator's formats (simulator.py:215, 231, 272)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    users = [f"user_{_uuid(rng)[:8]}" for _ in range(n_users)]
+    fps = [[_uuid(rng) for _ in range(int(rng.integers(1, 4)))] for _ in range(n_users)]
+    merchants = [f"merchant_{_uuid(rng)[:8]}" for _ in range(n_merchants)]
+    avg = rng.lognormal(4.0, 1.0, n_users)
+    return {"user_ids": users, "device_fps": fps, "merchant_ids": merchants, "avg_amount": avg}
+
+
+def json_messages(sp: dict, n: int, seed: int = 7, t0_us: int = 1_757_030_400_000_000, rate_per_s: float = 50.0):
+    """n transaction messages exactly as the simulator produces them: json.dumps(asdict(Transaction),
+    default=str) (simulator.py:186, 319-374) — uuid transaction ids, isoformat() timestamps (microseconds,
+    omitted when zero), Faker-style lat/lon (geolocation floats; merchant_location Decimals -> strings),
+    booleans, fraud_type null / string, fraud_score floats with full repr."""
+    import datetime as dt
+    import json
+    from decimal import Decimal
+    rng = np.random.Generator(np.random.PCG64(seed))
+    t = t0_us + np.cumsum(rng.exponential(1e6 / rate_per_s, n)).astype(np.int64)
+    t[::97] = (t[::97] // 1_000_000) * 1_000_000  # some whole seconds: isoformat drops the fraction
+    out = []
+    nu, nm = len(sp["user_ids"]), len(sp["merchant_ids"])
+    for i in range(n):
+        u = int(rng.integers(0, nu))
+        m = int(rng.integers(0, nm))
+        when = dt.datetime(1970, 1, 1) + dt.timedelta(microseconds=int(t[i]))
+        amount = max(1.0, round(float(sp["avg_amount"][u] * rng.normal(1.0, 0.3) * rng.normal(1.0, 0.2)), 2))
+        roll = rng.random()
+        fraud = roll < 0.055
+        if roll < 0.02:
+            amount = round(float(rng.uniform(1.0, 5.0)), 2)
+        elif 0.03 <= roll < 0.035:
+            amount = round(float(rng.uniform(1000.0, 5000.0)), 2)
+        ip = (f"192.168.{rng.integers(0, 256)}.{rng.integers(1, 255)}" if rng.random() < 0.05 else
+              f"10.{rng.integers(0, 256)}.{rng.integers(0, 256)}.{rng.integers(1, 255)}" if rng.random() < 0.03 else
+              f"{rng.integers(1, 224)}.{rng.integers(0, 256)}.{rng.integers(0, 256)}.{rng.integers(1, 255)}")
+        fps = sp["device_fps"][u]
+        fp = fps[int(rng.integers(0, len(fps)))] if roll >= 0.03 or roll < 0.02 else _uuid(rng)
+        glat, glon = round(float(rng.uniform(-90, 90)), 6), round(float(rng.uniform(-180, 180)), 6)
+        mloc = {"lat": Decimal(f"{rng.uniform(-90, 90):.6f}"), "lon": Decimal(f"{rng.uniform(-180, 180):.6f}")}
+        txn = {
+            "transaction_id": _uuid(rng),
+            "user_id": sp["user_ids"][u],
+            "merchant_id": sp["merchant_ids"][m] if rng.random() > 0.01 else f"merchant_{_uuid(rng)[:8]}",
+            "amount": amount,
+            "currency": "USD",
+            "transaction_type": SIM_TXN_TYPES[int(rng.integers(0, 3))],
+            "payment_method": SIM_PAYMENT_METHODS[int(rng.integers(0, 4))],
+            "card_type": SIM_CARD_TYPES[int(rng.integers(0, 4))],
+            "card_last_four": str(int(rng.integers(1000, 10000))),
+            "timestamp": when.isoformat(),
+            "ip_address": ip,
+            "device_id": fps[0],
+            "device_fingerprint": fp,
+            "user_agent": USER_AGENTS[int(rng.integers(0, len(USER_AGENTS)))],
+            "geolocation": {"lat": glat, "lon": glon},
+            "merchant_location": mloc,
+            "is_weekend": when.weekday() >= 5,
+            "hour_of_day": when.hour,
+            "is_fraud": bool(fraud),
+            "fraud_type": ("card_testing" if roll < 0.02 else "velocity_fraud") if fraud else None,
+            "fraud_score": float(rng.uniform(0.7, 0.95)) if fraud else float(rng.uniform(0.0, 0.3)),
+            "processing_time_ms": int(rng.integers(50, 501)),
+        }
+        out.append(json.dumps(txn, default=str).encode("utf-8"))
+    return out
