@@ -301,7 +301,8 @@ class Config3:
         N = self.N
         names = {N.FD_TIMING_XGB: "xgboost_forest", N.FD_TIMING_IFOREST: "iforest_forest",
                  N.FD_TIMING_FEATURES: "features (assign+process)", N.FD_TIMING_BLEND: "blend",
-                 N.FD_TIMING_ROUTE: "route_partition (count+scan+scatter)", N.FD_TIMING_LSTM: "lstm_head"}
+                 N.FD_TIMING_ROUTE: "route_partition (count+scan+scatter)", N.FD_TIMING_LSTM: "lstm_head",
+                 N.FD_TIMING_WINDOWS: "windows", N.FD_TIMING_INGEST: "ingest_json"}
         return {names[k]: round(ms / max(1, c) * 1e3, 3) for k, (ms, c) in timing.items() if c}
 
     def config(self, world):
@@ -555,7 +556,276 @@ class Config4(Config3):
                           f"{dt:.2f} s, CPU: {cpu_model()}"}
 
 
-WORKLOADS = {"config2": Config2, "config3": Config3, "config4": Config4, "config5": Config5}
+# --------------------------------------------------------------------------------------- ingest
+class Ingest:
+    """The Kafka JSON codec alone: 64k simulator-format messages (~790 B) resident in
+    HBM -> SoA columns in HBM, one fd_ingest_json_device per step. A pool of distinct batches is cycled so the
+    256 MB MALL cannot hold the input."""
+    name = "ingest"
+    dtype = "u8 (bytes; f64 for parsed decimals)"
+    OUT_BYTES = 8 * 10 + 4 + 1 * 10  # the 20 output columns per message
+
+    def __init__(self, args, rank, dev, eng):
+        import numpy as np
+        import torch
+        from fdengine import _native as N
+        from fdengine import synth
+        from fdengine.ingest import IngestCodec, device_columns, pack
+        self.np, self.torch, self.N = np, torch, N
+        self.B = args.batch
+        self.eng = eng
+        t = time.time()
+        self.merchant_ids = [f"merchant_{i:08x}" for i in range(5000)]
+        self.codec = IngestCodec(eng, self.merchant_ids, synth.SIM_PAYMENT_METHODS, synth.SIM_TXN_TYPES,
+                                 synth.SIM_CARD_TYPES)
+        self.msgs = synth.json_messages_fast(self.B, 10_000_000, self.merchant_ids, seed=300 + rank)
+        buf, off = pack(self.msgs)
+        self.nbytes = int(off[-1])
+        self.pool = max(1, args.pool)
+        # pool copies at distinct addresses (same content; 16-B aligned strides)
+        stride = (self.nbytes + 4095) & ~4095
+        host = np.zeros(self.pool * stride, np.uint8)
+        for p in range(self.pool):
+            host[p * stride:p * stride + self.nbytes] = buf
+        self.stride = stride
+        self.buf = torch.from_numpy(host).to(dev)
+        self.off = torch.from_numpy(off).to(dev)
+        self.offsets = off
+        self.cols, self.ptrs = device_columns(self.B, dev.index)
+        self.h_status = torch.empty(self.B, dtype=torch.uint8, pin_memory=True)
+        log(f"[rank {rank}] ingest setup {time.time() - t:.1f}s: {self.B} messages, {self.nbytes / self.B:.0f} B avg, "
+            f"pool {self.pool}")
+
+    def step(self, i):
+        s = i % self.pool
+        self.codec.parse_device(self.buf.data_ptr() + s * self.stride, self.off.data_ptr(), self.B, self.ptrs)
+
+    def fetch(self, i):
+        self.h_status.copy_(self.cols["status"], non_blocking=True)
+
+    def parity(self):
+        from oracle import ingest_ref as R
+        from fdengine import synth
+        np = self.np
+        self.step(0)
+        self.torch.cuda.synchronize()
+        k = 4096
+        exp = R.parse_batch(self.msgs[:k], {m: i for i, m in enumerate(self.merchant_ids)},
+                            [{s: i for i, s in enumerate(v)} for v in (synth.SIM_PAYMENT_METHODS, synth.SIM_TXN_TYPES,
+                                                                      synth.SIM_CARD_TYPES)])
+        bad = 0
+        for name, dt in self.N.INGEST_FIELDS:
+            g = self.cols[name][:k].cpu().numpy().view(dt)
+            e = exp[name]
+            if g.dtype.kind == "f":
+                bad += int((~((g.view(np.uint64) == e.view(np.uint64)) | (np.isnan(g) & np.isnan(e)))).sum())
+            else:
+                bad += int((g != e).sum())
+        return {"messages_checked": k, "mismatched_values": bad,
+                "invalid_rows": int((exp["status"] & R.INVALID != 0).sum())}
+
+    def _avg(self, timing):
+        ms, launches = timing[self.N.FD_TIMING_INGEST]
+        return (ms / 1e3) / max(1, launches)
+
+    def roofline(self, timing):
+        avg = self._avg(timing)
+        per_launch = self.nbytes + 8 * (self.B + 1) + self.OUT_BYTES * self.B
+        achieved = per_launch / avg / 1e9
+        return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(self.name, self.B),
+                "kernel": "ingest_json_kernel (wave per message, LDS-staged)", "kernel_avg_us": round(avg * 1e6, 3),
+                "algorithmic_bytes_per_launch": per_launch,
+                "bytes_per_txn": round(per_launch / self.B, 1)}
+
+    def kernels(self, timing):
+        return {"ingest_json": round(self._avg(timing) * 1e6, 3)}
+
+    def config(self, world):
+        return {"workload": "ingest: Kafka JSON codec — 64k simulator-format transaction messages "
+                            "(json.dumps(asdict(Transaction), default=str)) resident in HBM -> SoA columns",
+                "batch": self.B, "avg_message_bytes": round(self.nbytes / self.B, 1),
+                "parallelism": f"replicas x{world}"}
+
+    def cpu_baseline(self, seconds):
+        """The reference's CPU path for this step restated: Python json.loads + the field mapping
+        (oracle/ingest_ref.py) on one core, over the batch's messages."""
+        from oracle import ingest_ref as R
+        from fdengine import synth
+        merch = {m: i for i, m in enumerate(self.merchant_ids)}
+        voc = [{s: i for i, s in enumerate(v)} for v in (synth.SIM_PAYMENT_METHODS, synth.SIM_TXN_TYPES,
+                                                          synth.SIM_CARD_TYPES)]
+        done, a = 0, time.perf_counter()
+        while time.perf_counter() - a < seconds:
+            R.parse_message(self.msgs[done % self.B], merch, voc)
+            done += 1
+        dt = time.perf_counter() - a
+        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": 1, "kind": "port",
+                "sample": f"{done} messages of the batch through oracle/ingest_ref.py (json.loads + field mapping, "
+                          f"1 core), {dt:.2f} s, CPU: {cpu_model()}"}
+
+
+# --------------------------------------------------------------------------------------- config 3 from JSON
+class Config3J(Config3):
+    """config 3 fed from the wire format: per step one micro-batch of 64k raw Kafka JSON messages (resident in
+    HBM) -> ingest codec -> card-state features (10M cards) -> XGBoost 500x8 + IsolationForest -> blend.
+    Cards are keyed by fd_hash64(user_id) as the codec keys them."""
+    name = "config3j"
+
+    def __init__(self, args, rank, dev, eng):
+        import numpy as np
+        import torch
+        import fdengine
+        from fdengine import _native as N
+        from fdengine import synth
+        from fdengine.ingest import IngestCodec, device_columns, pack
+        from oracle.features_c import OracleFeatureState
+        from oracle import scoring_ref as S
+        self.np, self.torch, self.N, self.S = np, torch, N, S
+        self.B, self.T, self.D = args.batch, args.trees, args.depth
+        self.cards, self.mode, self.K = args.cards, (1 if args.window == "sliding" else 0), args.ring_k
+        self.eng = eng
+        t = time.time()
+        spop = synth.population(20000, 500, seed=11)
+        stx = synth.txn_stream(spop, 40000, seed=12, rate_per_s=20.0)
+        so = OracleFeatureState(1 << 16, self.mode, self.K)
+        so.load_users(spop["users"]["key"], spop["users"]["avg_amount"], spop["users"]["account_age_days"],
+                      spop["users"]["device_fp"])
+        so.load_merchants(spop["merchants"]["fraud_rate"], spop["merchants"]["risk_multiplier"])
+        _, Xref = so.run(stx, want_raw=False)
+        self.xgb = fdengine.xgboost_from_json_doc(synth.xgboost_doc(self.T, self.D, 64, Xref[-8192:], seed=13))
+        self.ifm = fdengine.iforest_from_sklearn(synth.isolation_forest(Xref[-8192:].astype(np.float64)))
+        eng.load_forest(0, self.xgb)
+        eng.load_forest(1, self.ifm)
+        self.names = ["xgboost_primary", "isolation_forest"]
+        self.slots = [0, 1]
+        w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
+        self.weights = [w[n] for n in self.names]
+        self.mults = [S.CONF_MULT[n] for n in self.names]
+        self.params = fdengine.FraudEngine.blend_params(self.weights, self.mults)
+        # users keyed as the codec keys them: fd_hash64("user_xxxxxxxx"), fingerprints fd_hash64("fp-xxxxxxxx")
+        idx = np.arange(self.cards, dtype=np.uint64)
+        self.ukeys = synth.hash64_fixed(synth.fixed_ids("user_", idx))
+        self.uavg = np.exp(4.0 + np.sqrt(2) * synth._erfinv(2 * synth._u01(idx, 42, 0) - 1))
+        self.uage = (synth._u01(idx, 42, 1) * 730).astype(np.int32)
+        self.ufp = np.stack([synth.hash64_fixed(synth.fixed_ids("fp-", idx * np.uint64(3) + np.uint64(k)))
+                             for k in range(3)], axis=1)
+        self.merchant_ids = [f"merchant_{i:08x}" for i in range(5000)]
+        self.merchants = synth.merchants_table(5000, seed=100 + rank)
+        cap = 1
+        while cap < int(self.cards * 1.6):
+            cap *= 2
+        self.cap = cap
+        eng.state_init(cap, self.mode, self.K)
+        eng.load_users(self.ukeys, self.uavg, self.uage, self.ufp)
+        eng.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
+        self.codec = IngestCodec(eng, self.merchant_ids, synth.SIM_PAYMENT_METHODS, synth.SIM_TXN_TYPES,
+                                 synth.SIM_CARD_TYPES)
+        self.pool = max(1, min(args.pool, 4))
+        self.msgs, bufs, offs = [], [], []
+        for p in range(self.pool):
+            ms = synth.json_messages_fast(self.B, self.cards, self.merchant_ids, seed=400 + 17 * rank + p,
+                                          t0_ms=1_757_030_400_000 + p * 60_000)
+            b, o = pack(ms)
+            self.msgs.append(ms)
+            bufs.append(torch.from_numpy(b.copy()).to(dev))
+            offs.append(torch.from_numpy(o).to(dev))
+        self.bufs, self.offs = bufs, offs
+        self.cols, self.cptrs = device_columns(self.B, dev.index)
+        B = self.B
+        self.fp = torch.empty(B, dtype=torch.float64, device=dev)
+        self.conf = torch.empty(B, dtype=torch.float64, device=dev)
+        self.dec = torch.empty(B, dtype=torch.uint8, device=dev)
+        self.risk = torch.empty(B, dtype=torch.uint8, device=dev)
+        self.mp = torch.empty((len(self.names), B), dtype=torch.float64, device=dev)
+        self.vec = torch.empty((B, 64), dtype=torch.float32, device=dev)
+        self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
+        self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
+        self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
+        self.nbytes = [int(o[-1].item()) for o in offs]
+        log(f"[rank {rank}] config3j setup {time.time() - t:.1f}s: {self.cards} cards, capacity {cap}, "
+            f"{self.pool} JSON batches resident ({self.nbytes[0] / B:.0f} B/message)")
+
+    def step(self, i):
+        s = i % self.pool
+        self.codec.parse_device(self.bufs[s].data_ptr(), self.offs[s].data_ptr(), self.B, self.cptrs)
+        txn = {f: self.cptrs[f] for f in self.N.TXN_FIELDS}
+        self.eng.score_batch_device(self.params, self.slots, txn, self.B, self.fp.data_ptr(),
+                                    self.conf.data_ptr(), self.dec.data_ptr(), self.risk.data_ptr(),
+                                    vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
+
+    def _oracle_state(self):
+        from oracle.features_c import OracleFeatureState
+        o = OracleFeatureState(self.cap, self.mode, self.K)
+        o.load_users(self.ukeys, self.uavg, self.uage, self.ufp)
+        o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
+        return o
+
+    def _oracle_txns(self, msgs):
+        from oracle import ingest_ref as R
+        from fdengine import synth
+        cols = R.parse_batch(msgs, {m: i for i, m in enumerate(self.merchant_ids)},
+                             [{s: i for i, s in enumerate(v)} for v in (synth.SIM_PAYMENT_METHODS,
+                                                                         synth.SIM_TXN_TYPES, synth.SIM_CARD_TYPES)])
+        return {f: cols[f] for f in self.N.TXN_FIELDS}
+
+    def parity(self):
+        """Batch 0 (fresh state): oracle ingest -> oracle features -> forests -> blend, first 8192 rows."""
+        import oracle
+        np = self.np
+        k = 8192
+        o = self._oracle_state()
+        self.step(0)
+        self.torch.cuda.synchronize()
+        part = self._oracle_txns(self.msgs[0][:k])
+        _, rvec = o.run(part, want_raw=False)
+        del o
+        V = self.vec[:k].cpu().numpy()
+        px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
+        pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
+        fp, _, dec, _ = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults)
+        return {"rows_checked": k, "vector_mismatched_elements": int((V != rvec).sum()),
+                "max_abs_prob_diff": float(np.abs(self.fp[:k].cpu().numpy() - fp).max()),
+                "decision_mismatches": int((self.dec[:k].cpu().numpy() != dec).sum())}
+
+    def kernels(self, timing):
+        out = super().kernels(timing)
+        ms, c = timing.get(self.N.FD_TIMING_INGEST, (0.0, 0))
+        if c:
+            out["ingest_json"] = round(ms / c * 1e3, 3)
+        return out
+
+    def config(self, world):
+        d = super().config(world)
+        d["workload"] = ("config3j: config3 fed from the wire format — 64k raw Kafka JSON messages per micro-batch "
+                         "resident in HBM -> ingest codec -> features (HBM card state) -> XGBoost 500x8 + "
+                         "IsolationForest 100 -> blend/decision")
+        d["avg_message_bytes"] = round(self.nbytes[0] / self.B, 1)
+        return d
+
+    def cpu_baseline(self, seconds):
+        """The oracle chain from raw JSON: json.loads + mapping (1 core) -> features (C, sequential) ->
+        forests + blend (OpenMP), on the first messages of batch 0 (bounded sample)."""
+        import oracle
+        np = self.np
+        th = cpu_threads()
+        o = self._oracle_state()
+        chunk, done, a = 2048, 0, time.perf_counter()
+        while time.perf_counter() - a < seconds and done + chunk <= self.B:
+            part = self._oracle_txns(self.msgs[0][done:done + chunk])
+            _, V = o.run(part, want_raw=False)
+            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=th)
+            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=th)
+            oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults, nthreads=th)
+            done += chunk
+        dt = time.perf_counter() - a
+        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
+                "sample": f"first {done} messages of batch 0 through the oracle chain (json.loads + mapping 1 core, "
+                          f"features C 1 core, XGBoost + IsolationForest + blend {th} OpenMP threads), {dt:.2f} s, "
+                          f"CPU: {cpu_model()}"}
+
+
+WORKLOADS = {"config2": Config2, "config3": Config3, "config4": Config4, "config5": Config5, "ingest": Ingest, "config3j": Config3J}
 
 
 def main():

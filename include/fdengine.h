@@ -457,7 +457,7 @@ int fd_state_restore(fd_engine* eng, const char* path, int32_t shard, int32_t n_
 enum fd_vocab_kind { FD_VOCAB_PAYMENT_METHOD = 0, FD_VOCAB_TRANSACTION_TYPE = 1, FD_VOCAB_CARD_TYPE = 2 };
 enum fd_ingest_status {
   FD_INGEST_MALFORMED = 1,     /* not one JSON object / bad member syntax / value of the wrong type */
-  FD_INGEST_TOO_LONG = 2,      /* message longer than 4096 bytes */
+  FD_INGEST_TOO_LONG = 2,      /* message longer than 4080 bytes */
   FD_INGEST_UNKNOWN_VOCAB = 4, /* a payment / type / card string outside its vocabulary (code FD_VOCAB_OTHER) */
   FD_INGEST_INEXACT = 8,       /* sub-cent amount (rounded half-even) or a > 19-digit number at a rounding tie */
   FD_INGEST_MISSING = 16,      /* user_id, amount or timestamp missing / null */

@@ -28,7 +28,7 @@ import numpy as np
 MALFORMED, TOO_LONG, UNKNOWN_VOCAB, INEXACT, MISSING = 1, 2, 4, 8, 16
 INVALID = MALFORMED | TOO_LONG | MISSING
 VOCAB_OTHER = 254
-MAX_MSG, MAX_MEMBERS = 4096, 64
+MAX_MSG, MAX_MEMBERS = 4080, 64
 
 FIELDS = {
     "transaction_id": "txn", "transactionId": "txn", "user_id": "user", "userId": "user",

@@ -275,6 +275,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   if (k == "forest_kernel") {
     FD_REQUIRE(value >= 0 && value <= 6, FD_ERR_INVALID_ARG, "forest_kernel must be in 0..6");
     e.forest_variant = (int)value;
+  } else if (k == "ingest_stop_after") {  // diagnostics: 0 full; 1 stage; 2 + structure; 3 + members
+    FD_REQUIRE(value >= 0 && value <= 3, FD_ERR_INVALID_ARG, "ingest_stop_after must be in 0..3");
+    e.ingest.stop_after = (int)value;
   } else if (k == "rule_fraud_threshold_permille") {  // JobConfig.fraudThreshold x 1000
     FD_REQUIRE(value >= 0 && value <= 1000, FD_ERR_INVALID_ARG, "rule_fraud_threshold_permille must be in 0..1000");
     e.state.tp_threshold = (double)value / 1000.0;

@@ -159,6 +159,7 @@ struct IngestTables {
   DeviceBuffer mkeys, mvals, vkeys[3], vvals[3];
   unsigned long long mmask = 0, vmask[3] = {0, 0, 0};
   bool mloaded = false, vloaded[3] = {false, false, false};
+  int stop_after = 0;  // diagnostics option "ingest_stop_after"
   DeviceBuffer stage_bytes, stage_offsets, stage_out;  // host-API staging
 };
 

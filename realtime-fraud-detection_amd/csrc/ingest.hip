@@ -30,9 +30,9 @@ namespace fd {
 namespace {
 
 constexpr int kWaves = 4;
-constexpr int kMaxMsg = 4096;      // staged bytes per message (64 lanes x 64-byte segments)
+constexpr int kMaxMsg = 4080;      // bytes per message: 64 lanes x 64-byte segments minus the 16-B alignment shift
 constexpr int kMaxMembers = 64;    // top-level members per message (one per lane; more -> malformed)
-constexpr int kStage = kMaxMsg + 32;
+constexpr int kStage = 4096;
 
 enum Field : int {
   F_TXN_ID, F_USER_ID, F_MERCHANT_ID, F_AMOUNT, F_TIMESTAMP, F_IP, F_DEVICE_FP, F_UA, F_GEO, F_MLOC,
@@ -40,7 +40,7 @@ enum Field : int {
 };
 
 // simulator (snake_case, simulator.py:77-101) and Java bean (camelCase) property names
-__device__ int field_of_key(uint64_t h) {
+__device__ __forceinline__ int field_of_key(uint64_t h) {
 #define FD_K(name, f) \
   if (h == key_hash(name)) return f;
   FD_K("transaction_id", F_TXN_ID) FD_K("transactionId", F_TXN_ID)
@@ -64,9 +64,12 @@ __device__ int field_of_key(uint64_t h) {
   return -1;
 }
 
-struct LdsBytes {  // byte view of a wave's staged message
-  const unsigned char* p;
-  __device__ __forceinline__ int operator[](int i) const { return p[i]; }
+// byte view of a wave's staged message (message byte i = stage[shift + i]); one ds_read_u8 per access keeps
+// every access site a single instruction (the kernel must stay small enough for the instruction cache)
+struct Reader {
+  const unsigned char* st;
+  int shift;
+  __device__ __forceinline__ int operator[](int i) const { return st[shift + i]; }
 };
 
 __device__ __forceinline__ bool is_ws(int c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
@@ -116,7 +119,7 @@ struct StrStats {
 };
 
 // decode the string whose opening quote is at s[pos]; returns the index after the closing quote, -1 if malformed
-__device__ int scan_string(LdsBytes s, int pos, int end, StrStats& st) {
+__device__ __forceinline__ int scan_string(const Reader& s, int pos, int end, StrStats& st) {
   int i = pos + 1;
   while (i < end) {
     const int c = s[i];
@@ -180,11 +183,37 @@ __device__ int scan_string(LdsBytes s, int pos, int end, StrStats& st) {
   return -1;
 }
 
-__device__ __forceinline__ bool lit_at(LdsBytes s, int i, int end, const char* w, int n);
+__device__ __forceinline__ bool lit_at(const Reader& s, int i, int end, const char* w, int n);
+
+// the end of the string whose opening quote is at s[pos] (escapes validated, nothing decoded); -1 if malformed
+__device__ __forceinline__ int skip_string(const Reader& s, int pos, int end) {
+  int i = pos + 1;
+  while (i < end) {
+    const int c = s[i];
+    if (c == '"') return i + 1;
+    if (c < 0x20) return -1;
+    if (c == '\\') {
+      if (i + 1 >= end) return -1;
+      const int e = s[i + 1];
+      if (e == 'u') {
+        if (i + 6 > end) return -1;
+        for (int k = 2; k < 6; ++k)
+          if (hexval(s[i + k]) < 0) return -1;
+        i += 6;
+        continue;
+      }
+      if (e != '"' && e != '\\' && e != '/' && e != 'b' && e != 'f' && e != 'n' && e != 'r' && e != 't') return -1;
+      i += 2;
+      continue;
+    }
+    ++i;
+  }
+  return -1;
+}
 
 // skip one JSON value at s[pos], validated by the RFC 8259 grammar (nesting <= 64); returns the index after
 // it, -1 if malformed
-__device__ int skip_value(LdsBytes s, int pos, int end) {
+__device__ __forceinline__ int skip_value(const Reader& s, int pos, int end) {
   enum { VALUE, VALUE_OR_CLOSE, KEY, KEY_OR_CLOSE, COLON, COMMA_OR_CLOSE };
   unsigned long long objects = 0ull;  // bit d: level d+1 is an object (else an array)
   int depth = 0, state = VALUE, i = pos;
@@ -206,8 +235,7 @@ __device__ int skip_value(LdsBytes s, int pos, int end) {
         state = c == '{' ? KEY_OR_CLOSE : VALUE_OR_CLOSE;
         continue;
       } else if (c == '"') {
-        StrStats st;
-        i = scan_string(s, i, end, st);
+        i = skip_string(s, i, end);
         if (i < 0) return -1;
         value_done = true;
       } else if (c == 't' || c == 'f' || c == 'n') {
@@ -228,8 +256,7 @@ __device__ int skip_value(LdsBytes s, int pos, int end) {
         value_done = true;
       } else {
         if (c != '"') return -1;
-        StrStats st;
-        i = scan_string(s, i, end, st);
+        i = skip_string(s, i, end);
         if (i < 0) return -1;
         state = COLON;
         continue;
@@ -258,61 +285,65 @@ __device__ int skip_value(LdsBytes s, int pos, int end) {
   }
 }
 
-__device__ __forceinline__ bool lit_at(LdsBytes s, int i, int end, const char* w, int n) {  // NOLINT
+__device__ __forceinline__ bool lit_at(const Reader& s, int i, int end, const char* w, int n) {  // NOLINT
   if (i + n > end) return false;
   for (int k = 0; k < n; ++k)
     if (s[i + k] != w[k]) return false;
   return true;
 }
 
-// a number or a string holding a JSON number (Jackson's String -> Double coercion), or null
-// kind: 0 = null, 1 = number; returns end index or -1
-__device__ int scan_numeric(LdsBytes s, int pos, int end, Decimal& d, int* kind) {
-  if (lit_at(s, pos, end, "null", 4)) {
-    *kind = 0;
-    return pos + 4;
-  }
-  *kind = 1;
-  if (s[pos] == '"') {
-    int close = pos + 1;
-    while (close < end && s[close] != '"' && s[close] != '\\') ++close;
-    if (close >= end || s[close] != '"') return -1;
-    const int e = scan_number(s, pos + 1, close, d);
-    return e == close ? close + 1 : -1;
-  }
-  return scan_number(s, pos, end, d);
-}
-
 __device__ __forceinline__ double nan_d() { return __builtin_nan(""); }
 
-// geolocation / merchant_location: {"lat": x, "lon": y, ...} or null
-__device__ int scan_latlon(LdsBytes s, int pos, int end, double* lat, double* lon, bool* inexact) {
-  *lat = *lon = nan_d();
+// a location value: {"lat": x, "lon": y, ...} or null, x / y numbers, numeric strings or null. The decimals are
+// returned (conversion happens at the caller's single decimal -> binary64 site); has[t] = 0 absent/null, 1 set.
+__device__ __forceinline__ int scan_latlon(const Reader& s, int pos, int end, Decimal& d0, Decimal& d1, int& has0,
+                                           int& has1) {
+  has0 = has1 = 0;
   if (lit_at(s, pos, end, "null", 4)) return pos + 4;
   if (s[pos] != '{') return -1;
   int i = pos + 1;
   while (i < end && is_ws(s[i])) ++i;
   if (i < end && s[i] == '}') return i + 1;
-  const uint64_t kLat = key_hash("lat"), kLon = key_hash("lon");
   while (i < end) {
     if (s[i] != '"') return -1;
-    StrStats k;
-    i = scan_string(s, i, end, k);
+    const int ks = i;
+    i = skip_string(s, i, end);
     if (i < 0) return -1;
+    // "lat" / "lon" (unescaped spelling)
+    const int t = (i - ks == 5 && s[ks + 1] == 'l' && ((s[ks + 2] == 'a' && s[ks + 3] == 't') ||
+                                                         (s[ks + 2] == 'o' && s[ks + 3] == 'n')))
+                      ? (s[ks + 2] == 'a' ? 0 : 1)
+                      : -1;
     while (i < end && is_ws(s[i])) ++i;
     if (i >= end || s[i] != ':') return -1;
     ++i;
     while (i < end && is_ws(s[i])) ++i;
     if (i >= end) return -1;
-    if (k.fnv == kLat || k.fnv == kLon) {
-      Decimal d;
-      int kind;
-      i = scan_numeric(s, i, end, d, &kind);
-      if (i < 0) return -1;
-      bool amb = false;
-      const double v = kind ? decimal_to_double(d.w, d.q, d.neg, d.many, &amb) : nan_d();
-      if (amb) *inexact = true;
-      if (k.fnv == kLat) *lat = v; else *lon = v;
+    if (t >= 0) {
+      if (lit_at(s, i, end, "null", 4)) {
+        if (t == 0) has0 = 0; else has1 = 0;
+        i += 4;
+      } else {
+        int a = i, b = end;
+        const bool quoted = s[i] == '"';
+        if (quoted) {
+          b = a + 1;
+          while (b < end && s[b] != '"' && s[b] != '\\') ++b;
+          if (b >= end || s[b] != '"') return -1;
+          ++a;
+        }
+        Decimal tmp;
+        const int e = scan_number(s, a, b, tmp);
+        if (e < 0 || (quoted && e != b)) return -1;
+        i = quoted ? b + 1 : e;
+        if (t == 0) {
+          d0 = tmp;
+          has0 = 1;
+        } else {
+          d1 = tmp;
+          has1 = 1;
+        }
+      }
     } else {
       i = skip_value(s, i, end);
       if (i < 0) return -1;
@@ -359,7 +390,7 @@ struct Val {
 
 __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* __restrict__ buf,
                                                           const int64_t* __restrict__ offsets, int64_t n, Tables T,
-                                                          fd_ingest_out out) {
+                                                          fd_ingest_out out, int stop_after) {
   __shared__ __attribute__((aligned(16))) unsigned char stage[kWaves][kStage];
   __shared__ int colon[kWaves][kMaxMembers];
   __shared__ int nmem[kWaves], ncomma[kWaves];
@@ -393,89 +424,130 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
     uint4 v;
     if (g + 16 <= total_bytes) {
       v = *reinterpret_cast<const uint4*>(buf + g);
-    } else {
-      unsigned char tmp[16];
-      for (int q = 0; q < 16; ++q) tmp[q] = (g + q < total_bytes) ? buf[g + q] : 0;
-      memcpy(&v, tmp, 16);
+    } else {  // the buffer's last partial chunk, byte by byte (no read past its end)
+      unsigned wq[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (g + q < total_bytes) wq[q >> 2] |= (unsigned)buf[g + q] << (8 * (q & 3));
+      v = make_uint4(wq[0], wq[1], wq[2], wq[3]);
     }
     *reinterpret_cast<uint4*>(&stage[wv][16 * k]) = v;
   }
   __syncthreads();
-  const LdsBytes s{&stage[wv][shift]};
+  if (stop_after == 1) return;
+  const Reader s{&stage[wv][0], shift};
 
-  // ---- structure: quote parity per 64-byte segment
-  const int s0 = lane * 64, s1 = min(s0 + 64, L);
-  int bs = 0;
-  for (int p = s0 - 1; p >= 0 && s0 < L && s[p] == '\\'; --p) ++bs;
-  const int bs0 = bs;
-  int par = 0;
-  for (int p = s0; p < s1; ++p) {
-    const int c = s[p];
-    if (c == '"' && !(bs & 1)) par ^= 1;
-    bs = (c == '\\') ? bs + 1 : 0;
+  // ---- structure, from registers: lane i owns stage bytes [64i, 64i + 64) (16-B aligned) = message bytes
+  //      [q0, q0 + 64) with q0 = 64i - shift, valid where 0 <= q0 + k < L
+  const unsigned* seg = reinterpret_cast<const unsigned*>(&stage[wv][lane * 64]);
+  const int q0 = lane * 64 - shift;
+  // pass 1: trailing backslash run (escape carry into the next lane), first / last non-whitespace byte, quote
+  // parity assuming an even carry, and the byte after the segment's leading backslash run
+  int run = 0, nvalid = 0, first_nw = L, last_nw = -1, par = 0, lead = 0, after_lead = -1;
+  bool leading = true;
+#pragma unroll 2
+  for (int j = 0; j < 16; ++j) {
+    const unsigned w = seg[j];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int k = 4 * j + b, p = q0 + k;
+      const int c = (int)((w >> (8 * b)) & 0xFFu);
+      if ((unsigned)p < (unsigned)L) {
+        ++nvalid;
+        if (c == '"' && !(run & 1)) par ^= 1;
+        if (leading) {
+          if (c == '\\') {
+            ++lead;
+          } else {
+            leading = false;
+            after_lead = c;
+          }
+        }
+        run = (c == '\\') ? run + 1 : 0;
+        if (!is_ws(c)) {
+          first_nw = min(first_nw, p);
+          last_nw = p;
+        }
+      }
+    }
+  }
+  int bs0 = __shfl_up(run, 1);
+  if (lane == 0) bs0 = 0;
+  if (__ballot(nvalid > 0 && run == nvalid) != 0ull) {  // a segment of only backslashes: exact carry from LDS
+    int b2 = 0;
+    for (int p = q0 - 1; p >= 0 && q0 < L && s[p] == '\\'; --p) ++b2;
+    bs0 = b2;
+  }
+  if ((bs0 & 1) && after_lead == '"') par ^= 1;  // the carry escapes the first quote after the leading run
+  for (int d = 32; d >= 1; d >>= 1) {
+    first_nw = min(first_nw, __shfl_xor(first_nw, d));
+    last_nw = max(last_nw, __shfl_xor(last_nw, d));
   }
   const unsigned long long pb = __ballot(par);
   const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   const int in0 = __popcll(pb & lt) & 1;
   const int total_par = __popcll(pb) & 1;
-  // depth deltas outside strings
-  int in = in0, delta = 0, mind = 0;
-  bs = bs0;
-  for (int p = s0; p < s1; ++p) {
-    const int c = s[p];
-    if (c == '"' && !(bs & 1)) {
-      in ^= 1;
-    } else if (!in) {
-      if (c == '{' || c == '[') ++delta;
-      if (c == '}' || c == ']') {
-        --delta;
-        mind = min(mind, delta);
+  // pass 2: bracket depth deltas outside strings -> wave prefix sum
+  int in = in0, delta = 0, mind = 0, bs = bs0;
+#pragma unroll 2
+  for (int j = 0; j < 16; ++j) {
+    const unsigned w = seg[j];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int p = q0 + 4 * j + b;
+      const int c = (int)((w >> (8 * b)) & 0xFFu);
+      if ((unsigned)p < (unsigned)L) {
+        if (c == '"' && !(bs & 1)) {
+          in ^= 1;
+        } else if (!in) {
+          if (c == '{' || c == '[') ++delta;
+          if (c == '}' || c == ']') {
+            --delta;
+            mind = min(mind, delta);
+          }
+        }
+        bs = (c == '\\') ? bs + 1 : 0;
       }
     }
-    bs = (c == '\\') ? bs + 1 : 0;
   }
-  int depth0 = delta;  // exclusive prefix sum over lanes
+  int depth0 = delta;  // inclusive prefix sum over lanes
   for (int d = 1; d < 64; d <<= 1) {
     const int v = __shfl_up(depth0, d);
     if (lane >= d) depth0 += v;
   }
   const int total_depth = __shfl(depth0, 63);
   depth0 -= delta;
-  // first / last non-whitespace bytes (validation: the message is exactly one object)
-  int first_nw = L, last_nw = -1;
-  for (int p = s0; p < s1; ++p) {
-    if (!is_ws(s[p])) {
-      first_nw = min(first_nw, p);
-      last_nw = p;
-    }
-  }
-  for (int d = 32; d >= 1; d >>= 1) {
-    first_nw = min(first_nw, __shfl_xor(first_nw, d));
-    last_nw = max(last_nw, __shfl_xor(last_nw, d));
-  }
   bool bad = (depth0 + mind < 0);
-  // depth-1 colons (members) and the first return to depth 0
+  // pass 3: depth-1 colons (members), depth-1 commas and the first return to depth 0
   in = in0;
   bs = bs0;
   int depth = depth0, zero_at = L;
-  for (int p = s0; p < s1; ++p) {
-    const int c = s[p];
-    if (c == '"' && !(bs & 1)) {
-      in ^= 1;
-    } else if (!in) {
-      if (c == ':' && depth == 1) {
-        const int slot = atomicAdd(&nmem[wv], 1);
-        if (slot < kMaxMembers) colon[wv][slot] = p;
-      } else if (c == ',' && depth == 1) {
-        atomicAdd(&ncomma[wv], 1);
-      } else if (c == '{' || c == '[') {
-        ++depth;
-      } else if (c == '}' || c == ']') {
-        --depth;
-        if (depth == 0) zero_at = min(zero_at, p);
+#pragma unroll 2
+  for (int j = 0; j < 16; ++j) {
+    const unsigned w = seg[j];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int p = q0 + 4 * j + b;
+      const int c = (int)((w >> (8 * b)) & 0xFFu);
+      if ((unsigned)p < (unsigned)L) {
+        if (c == '"' && !(bs & 1)) {
+          in ^= 1;
+        } else if (!in) {
+          if (c == ':' && depth == 1) {
+            const int slot = atomicAdd(&nmem[wv], 1);
+            if (slot < kMaxMembers) colon[wv][slot] = p;
+          } else if (c == ',' && depth == 1) {
+            atomicAdd(&ncomma[wv], 1);
+          } else if (c == '{' || c == '[') {
+            ++depth;
+          } else if (c == '}' || c == ']') {
+            --depth;
+            if (depth == 0) zero_at = min(zero_at, p);
+          }
+        }
+        bs = (c == '\\') ? bs + 1 : 0;
       }
     }
-    bs = (c == '\\') ? bs + 1 : 0;
   }
   for (int d = 32; d >= 1; d >>= 1) zero_at = min(zero_at, __shfl_xor(zero_at, d));
   bad = bad || (__ballot(bad) != 0ull);
@@ -498,6 +570,7 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
   }
   __syncthreads();
   const bool structural_ok = go && status_s[wv] == 0u;
+  if (stop_after == 2) return;
 
   // ---- members: lane j parses member j
   int my_field = -1, my_colon = -1;
@@ -539,40 +612,75 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
       my_status |= FD_INGEST_MALFORMED;
       continue;
     }
+    int e = -1;
     if (f < 0) {  // unknown property: validated, then ignored (@JsonIgnoreProperties(ignoreUnknown = true))
-      int e = skip_value(s, v, L);
+      e = skip_value(s, v, L);
       while (e >= 0 && e < L && is_ws(s[e])) ++e;
       if (e < 0 || e >= L || (s[e] != ',' && s[e] != '}')) my_status |= FD_INGEST_MALFORMED;
       continue;
     }
-    int e = -1;
+    // ---- one token scan per member: string / literal / number / location object
     Val val;
     val.null = false;
     const int ch = s[v];
+    int kind = -1;  // 0 null, 1 string, 2 number, 3 true, 4 false, 5 location
+    StrStats st;
+    Decimal dec0, dec1;
+    int has0 = 0, has1 = 0;
+    int num_a = -1, num_b = L;
+    if (f == F_GEO || f == F_MLOC) {
+      e = scan_latlon(s, v, L, dec0, dec1, has0, has1);
+      kind = 5;
+    } else if (ch == '"') {
+      e = scan_string(s, v, L, st);
+      kind = 1;
+      if (e >= 0 && (f == F_AMOUNT || f == F_SCORE || f == F_HOUR)) {  // numeric string
+        if (st.escaped) e = -1;
+        num_a = v + 1;
+        num_b = e - 1;
+      }
+    } else if (lit_at(s, v, L, "null", 4)) {
+      e = v + 4;
+      kind = 0;
+    } else if (lit_at(s, v, L, "true", 4)) {
+      e = v + 4;
+      kind = 3;
+    } else if (lit_at(s, v, L, "false", 5)) {
+      e = v + 5;
+      kind = 4;
+    } else if (ch == '-' || (ch >= '0' && ch <= '9')) {
+      kind = 2;
+      num_a = v;
+    }
+    if (e < 0 && kind != 2) {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    if (num_a >= 0 && e >= -1) {  // the single number scan
+      const int ne = scan_number(s, num_a, num_b, dec0);
+      if (kind == 2) e = ne;
+      else if (ne != num_b) e = -1;
+      has0 = e >= 0 ? 1 : 0;
+    }
+    if (e < 0) {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    if (kind == 0) val.null = true;
+    // literal text of a scalar bound to a String property (Jackson's scalar -> String coercion)
+    if ((kind == 2 || kind == 3 || kind == 4) && f != F_AMOUNT && f != F_SCORE && f != F_HOUR && f != F_WEEKEND &&
+        f != F_FRAUD) {
+      for (int q = v; q < e; ++q) {
+        st.byte((unsigned)s[q]);
+        ++st.units;
+      }
+      kind = 1;
+    }
+    bool bad = false;
     switch (f) {
       case F_TXN_ID: case F_USER_ID: case F_MERCHANT_ID: case F_IP: case F_DEVICE_FP: case F_UA:
       case F_PAY: case F_TTYPE: case F_CTYPE: {
-        StrStats st;
-        if (ch == '"') {
-          e = scan_string(s, v, L, st);
-        } else if (lit_at(s, v, L, "null", 4)) {
-          e = v + 4;
-          val.null = true;
-        } else {  // scalar -> String coercion: the literal text
-          e = v;
-          while (e < L && !is_ws(s[e]) && s[e] != ',' && s[e] != '}') {
-            const int b = s[e];
-            if (b == '{' || b == '[' || b == '"') {
-              e = -1;
-              break;
-            }
-            st.byte((unsigned)b);
-            ++st.units;
-            ++e;
-          }
-          if (e == v) e = -1;
-        }
-        if (e < 0 || val.null) break;
+        if (kind != 1) break;  // null
         const uint64_t h = hash_finish(st.fnv);
         if (f == F_IP) {
           const bool priv = (st.nbytes >= 8 && st.head == 0x2E3836312E323931ull) ||            // "192.168."
@@ -592,84 +700,54 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
         }
         break;
       }
-      case F_AMOUNT: case F_SCORE: {
-        Decimal d;
-        int kind;
-        e = scan_numeric(s, v, L, d, &kind);
-        if (e < 0) break;
-        if (!kind) {
-          val.null = true;
+      case F_AMOUNT: {
+        if (kind == 0) break;
+        if (!has0) {
+          bad = true;
           break;
         }
-        if (f == F_AMOUNT) {
-          bool inexact = false;
-          int64_t cents;
-          if (!decimal_to_cents(d, &cents, &inexact)) {
-            e = -1;
-            break;
-          }
-          if (inexact) my_status |= FD_INGEST_INEXACT;
-          val.u = (uint64_t)cents;
-        } else {
-          bool amb = false;
-          val.a = decimal_to_double(d.w, d.q, d.neg, d.many, &amb);
-          if (amb) my_status |= FD_INGEST_INEXACT;
-        }
-        break;
-      }
-      case F_TIMESTAMP: {
-        if (lit_at(s, v, L, "null", 4)) {
-          e = v + 4;
-          val.null = true;
-          break;
-        }
-        if (ch != '"') break;
-        int close = v + 1;
-        while (close < L && s[close] != '"' && s[close] != '\\') ++close;
-        if (close >= L || s[close] != '"') break;
-        int64_t ms;
-        if (!parse_iso_instant(s, v + 1, close, &ms)) break;
-        val.u = (uint64_t)ms;
-        e = close + 1;
-        break;
-      }
-      case F_GEO: case F_MLOC: {
         bool inexact = false;
-        e = scan_latlon(s, v, L, &val.a, &val.b, &inexact);
+        int64_t cents;
+        if (!decimal_to_cents(dec0, &cents, &inexact)) {
+          bad = true;
+          break;
+        }
         if (inexact) my_status |= FD_INGEST_INEXACT;
+        val.u = (uint64_t)cents;
+        break;
+      }
+      case F_SCORE: case F_GEO: case F_MLOC:
+        if (f == F_SCORE && kind != 0 && !has0) bad = true;
+        break;  // decimals converted below
+      case F_TIMESTAMP: {
+        if (kind == 0) break;
+        int64_t ms;
+        if (kind != 1 || st.escaped || !parse_iso_instant(s, v + 1, e - 1, &ms)) {
+          bad = true;
+          break;
+        }
+        val.u = (uint64_t)ms;
         break;
       }
       case F_WEEKEND: case F_FRAUD: {
-        if (lit_at(s, v, L, "true", 4)) {
+        if (kind == 3 || kind == 4) {
+          val.u = kind == 3 ? 1 : 0;
+        } else if (kind == 1 && !st.escaped && st.nbytes == 4 && st.head == 0x65757274ull) {  // "true"
           val.u = 1;
-          e = v + 4;
-        } else if (lit_at(s, v, L, "false", 5)) {
+        } else if (kind == 1 && !st.escaped && st.nbytes == 5 && st.head == 0x65736C6166ull) {  // "false"
           val.u = 0;
-          e = v + 5;
-        } else if (lit_at(s, v, L, "null", 4)) {
-          val.null = true;
-          e = v + 4;
-        } else if (lit_at(s, v, L, "\"true\"", 6)) {
-          val.u = 1;
-          e = v + 6;
-        } else if (lit_at(s, v, L, "\"false\"", 7)) {
-          val.u = 0;
-          e = v + 7;
-        } else {  // integer coercion: 0 -> false, other -> true
-          Decimal d;
-          e = scan_number(s, v, L, d);
-          if (e >= 0 && d.frac_or_exp) e = -1;
-          if (e >= 0) val.u = d.w != 0 ? 1 : 0;
+        } else if (kind == 2 && !dec0.frac_or_exp) {  // integer coercion: 0 -> false, other -> true
+          val.u = dec0.w != 0 ? 1 : 0;
+        } else if (kind != 0) {
+          bad = true;
         }
         break;
       }
       case F_HOUR: {
-        Decimal d;
-        int kind;
-        e = scan_numeric(s, v, L, d, &kind);
-        if (e < 0) break;
-        if (!kind) {
-          val.null = true;
+        if (kind == 0) break;
+        const Decimal& d = dec0;
+        if (!has0) {
+          bad = true;
           break;
         }
         // integer value (a fraction truncates toward zero, Jackson ACCEPT_FLOAT_AS_INT); hours 0..254
@@ -687,7 +765,7 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
           }
         }
         if (!ok || iv > 254) {
-          e = -1;
+          bad = true;
           break;
         }
         val.u = (uint64_t)iv;
@@ -695,7 +773,20 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
       }
       default: break;
     }
-    if (e < 0) {
+    // the single decimal -> binary64 site: fraud score, or the two coordinates of a location
+    if (!bad && (f == F_SCORE || f == F_GEO || f == F_MLOC)) {
+      val.a = val.b = nan_d();
+      for (int t = 0; t < 2; ++t) {
+        const bool h = t == 0 ? has0 : (f != F_SCORE && has1);
+        if (!h) continue;
+        const Decimal d = t == 0 ? dec0 : dec1;
+        bool amb = false;
+        const double x = decimal_to_double(d.w, d.q, d.neg, d.many, &amb);
+        if (amb) my_status |= FD_INGEST_INEXACT;
+        if (t == 0) val.a = x; else val.b = x;
+      }
+    }
+    if (bad) {
       my_status |= FD_INGEST_MALFORMED;
       continue;
     }
@@ -711,6 +802,10 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
   }
   if (my_status) atomicOr(&status_s[wv], my_status);
   __syncthreads();
+  if (stop_after == 3) {
+    if (live && lane == 0 && out.status) out.status[m] = (unsigned char)(my_field + my_colon);  // keep the work
+    return;
+  }
   // ---- resolve: the winner of each field publishes its value to LDS, then lane f writes column f
   __shared__ unsigned long long vu[kWaves][F_COUNT];
   __shared__ double va[kWaves][F_COUNT], vb[kWaves][F_COUNT];
@@ -827,7 +922,8 @@ void launch_ingest(Engine& e, const uint8_t* d_bytes, const int64_t* d_offsets, 
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_INGEST) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
   const int64_t blocks = (n + kWaves - 1) / kWaves;
-  hipLaunchKernelGGL(ingest_json_kernel, dim3((unsigned)blocks), dim3(256), 0, e.stream, d_bytes, d_offsets, n, T, out);
+  hipLaunchKernelGGL(ingest_json_kernel, dim3((unsigned)blocks), dim3(256), 0, e.stream, d_bytes, d_offsets, n, T, out,
+                     t.stop_after);
   FD_HIP(hipGetLastError());
   if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
 }

@@ -272,8 +272,9 @@ FD_HD bool parse_iso_instant(const Bytes& s, int pos, int end, int64_t* ms) {
     return false;
   if (M < 1 || M > 12 || D < 1 || h > 23 || mi > 59 || sec > 59) return false;
   const bool leap = (Y % 4 == 0 && Y % 100 != 0) || Y % 400 == 0;
-  const int mdays[12] = {31, leap ? 29 : 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
-  if (D > mdays[M - 1]) return false;
+  // month lengths - 28, two bits per month (Jan .. Dec: 3 0 3 2 3 2 3 3 2 3 2 3); no array (no scratch)
+  const int mdays = 28 + (int)((0xeefbb3u >> (2 * (M - 1))) & 3u) + ((M == 2 && leap) ? 1 : 0);
+  if (D > mdays) return false;
   int i = pos + 19;
   int frac_ms = 0;
   if (i < end && s[i] == '.') {

@@ -68,7 +68,7 @@ class FraudEngine:
         N.call("fd_engine_set_option", self._h, key.encode(), int(value))
 
     def read_timing(self, kinds=(N.FD_TIMING_XGB, N.FD_TIMING_IFOREST, N.FD_TIMING_FEATURES, N.FD_TIMING_BLEND,
-                                 N.FD_TIMING_ROUTE, N.FD_TIMING_LSTM),
+                                 N.FD_TIMING_ROUTE, N.FD_TIMING_LSTM, N.FD_TIMING_WINDOWS, N.FD_TIMING_INGEST),
                     reset: bool = True):
         """-> {kind: (total kernel ms, timed launches)} since the last reset (then resets).
         With a single int `kinds`, returns just that (ms, launches) pair."""

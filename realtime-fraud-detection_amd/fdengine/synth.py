@@ -519,3 +519,88 @@ def json_messages(sp: dict, n: int, seed: int = 7, t0_us: int = 1_757_030_400_00
         }
         out.append(json.dumps(txn, default=str).encode("utf-8"))
     return out
+
+
+def fixed_ids(prefix: str, idx: np.ndarray) -> np.ndarray:
+    """Id strings `prefix` + 8 hex digits (the simulator's f"user_{uuid[:8]}" shape) as a fixed-width
+    uint8 matrix [n, len(prefix) + 8] (vectorised; no Python strings)."""
+    idx = np.asarray(idx, np.uint64)
+    mixed = _fmix64(idx ^ np.uint64(0x5DEECE66D)) & np.uint64(0xFFFFFFFF)
+    hexd = np.frombuffer(b"0123456789abcdef", np.uint8)
+    out = np.empty((len(idx), len(prefix) + 8), np.uint8)
+    out[:, :len(prefix)] = np.frombuffer(prefix.encode(), np.uint8)
+    for k in range(8):
+        out[:, len(prefix) + k] = hexd[((mixed >> np.uint64(28 - 4 * k)) & np.uint64(15)).astype(np.int64)]
+    return out
+
+
+def hash64_fixed(mat: np.ndarray) -> np.ndarray:
+    """fd_hash64 (fmix64(FNV-1a-64)) of every row of a fixed-width uint8 matrix, vectorised."""
+    h = np.full(mat.shape[0], 0xcbf29ce484222325, np.uint64)
+    prime = np.uint64(0x100000001b3)
+    with np.errstate(over="ignore"):
+        for k in range(mat.shape[1]):
+            h = (h ^ mat[:, k].astype(np.uint64)) * prime
+    return _fmix64(h)
+
+
+def json_messages_fast(n: int, n_users: int, merchant_ids, seed: int = 7, t0_ms: int = 1_757_030_400_000,
+                       rate_per_s: float = 2000.0, user_prefix: str = "user_", fp_prefix: str = "fp-"):
+    """Simulator-format messages (the key order, separators and value forms of json.dumps(asdict(Transaction),
+    default=str)) at bench scale: users are fixed_ids(user_prefix, i) with device fingerprints
+    fixed_ids(fp_prefix, 3 i + k); the values follow json_messages' distributions."""
+    import datetime as dt
+    rng = np.random.Generator(np.random.PCG64(seed))
+    u = rng.integers(0, n_users, n)
+    m = rng.integers(0, len(merchant_ids), n)
+    ts_us = (t0_ms * 1000 + np.cumsum(rng.exponential(1e6 / rate_per_s, n))).astype(np.int64)
+    uid = fixed_ids(user_prefix, u)
+    fpk = rng.integers(0, 3, n)
+    fid = fixed_ids(fp_prefix, u * 3 + fpk)
+    base = _u01(u.astype(np.uint64), 42, 0)
+    avg = np.exp(4.0 + 1.0 * np.sqrt(2) * _erfinv(2 * base - 1))
+    amount = np.maximum(1.0, np.round(avg * rng.normal(1.0, 0.3, n) * rng.normal(1.0, 0.2, n), 2))
+    roll = rng.random(n)
+    amount = np.where(roll < 0.02, np.round(rng.uniform(1, 5, n), 2), amount)
+    amount = np.where((roll >= 0.03) & (roll < 0.035), np.round(rng.uniform(1000, 5000, n), 2), amount)
+    fraud = roll < 0.055
+    score = np.where(fraud, rng.uniform(0.7, 0.95, n), rng.uniform(0.0, 0.3, n))
+    tt, pm, ct = rng.integers(0, 3, n), rng.integers(0, 4, n), rng.integers(0, 4, n)
+    glat, glon = np.round(rng.uniform(-90, 90, n), 6), np.round(rng.uniform(-180, 180, n), 6)
+    mlat, mlon = rng.uniform(-90, 90, n), rng.uniform(-180, 180, n)
+    ua = rng.integers(0, len(USER_AGENTS), n)
+    ip = rng.integers(0, 256, (n, 4))
+    priv = rng.random(n) < 0.05
+    txid = rng.integers(0, 1 << 62, n)
+    uas = [json_str(a) for a in USER_AGENTS]
+    out = []
+    epoch = dt.datetime(1970, 1, 1)
+    for i in range(n):
+        when = epoch + dt.timedelta(microseconds=int(ts_us[i]))
+        ipstr = f"192.168.{ip[i, 2]}.{ip[i, 3]}" if priv[i] else f"{ip[i, 0] or 1}.{ip[i, 1]}.{ip[i, 2]}.{ip[i, 3]}"
+        f = bool(fraud[i])
+        fpstr = fid[i].tobytes().decode()
+        out.append((
+            f'{{"transaction_id": "{txid[i]:016x}-tx", "user_id": "{uid[i].tobytes().decode()}", '
+            f'"merchant_id": "{merchant_ids[m[i]]}", "amount": {float(amount[i])!r}, "currency": "USD", '
+            f'"transaction_type": "{SIM_TXN_TYPES[tt[i]]}", "payment_method": "{SIM_PAYMENT_METHODS[pm[i]]}", '
+            f'"card_type": "{SIM_CARD_TYPES[ct[i]]}", "card_last_four": "{1000 + txid[i] % 9000}", '
+            f'"timestamp": "{when.isoformat()}", "ip_address": "{ipstr}", "device_id": "{fpstr}", '
+            f'"device_fingerprint": "{fpstr}", "user_agent": {uas[ua[i]]}, '
+            f'"geolocation": {{"lat": {float(glat[i])!r}, "lon": {float(glon[i])!r}}}, '
+            f'"merchant_location": {{"lat": "{mlat[i]:.6f}", "lon": "{mlon[i]:.6f}"}}, '
+            f'"is_weekend": {"true" if when.weekday() >= 5 else "false"}, "hour_of_day": {when.hour}, '
+            f'"is_fraud": {"true" if f else "false"}, '
+            f'"fraud_type": {chr(34) + "card_testing" + chr(34) if f else "null"}, '
+            f'"fraud_score": {float(score[i])!r}, "processing_time_ms": {50 + txid[i] % 451}}}').encode())
+    return out
+
+
+def json_str(s: str) -> str:
+    import json
+    return json.dumps(s)
+
+
+def _erfinv(y):
+    from scipy.special import erfinv
+    return erfinv(y)

@@ -1,0 +1,30 @@
+"""Per-phase timing of the ingest kernel (option "ingest_stop_after"): stage / + structure / + members / full."""
+import sys
+import time
+sys.path[:0] = [".", "realtime-fraud-detection_amd"]
+import numpy as np
+import torch
+import fdengine
+from fdengine import synth
+from fdengine.ingest import IngestCodec, device_columns, pack
+
+eng = fdengine.FraudEngine(0)
+mids = [f"merchant_{i:08x}" for i in range(5000)]
+codec = IngestCodec(eng, mids, synth.SIM_PAYMENT_METHODS, synth.SIM_TXN_TYPES, synth.SIM_CARD_TYPES)
+B = 65536
+msgs = synth.json_messages_fast(B, 10_000_000, mids, seed=1)
+buf, off = pack(msgs)
+dbuf, doff = torch.from_numpy(buf.copy()).cuda(), torch.from_numpy(off).cuda()
+cols, ptrs = device_columns(B)
+eng.set_stream(torch.cuda.current_stream().cuda_stream)
+for stop in (1, 2, 3, 0):
+    eng.set_option("ingest_stop_after", stop)
+    for _ in range(3):
+        codec.parse_device(dbuf.data_ptr(), doff.data_ptr(), B, ptrs)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(20):
+        codec.parse_device(dbuf.data_ptr(), doff.data_ptr(), B, ptrs)
+    torch.cuda.synchronize()
+    print(f"stop_after={stop}: {(time.perf_counter() - t) / 20 * 1e6:.1f} us / 64k messages", flush=True)
+eng.close()
