@@ -39,29 +39,53 @@ enum Field : int {
   F_WEEKEND, F_HOUR, F_FRAUD, F_SCORE, F_PAY, F_TTYPE, F_CTYPE, F_COUNT
 };
 
-// simulator (snake_case, simulator.py:77-101) and Java bean (camelCase) property names
+// simulator (snake_case, simulator.py:77-101) and Java bean (camelCase) property names, as compile-time
+// FNV-1a constants (namespace-scope constexpr: never evaluated on the device)
+struct KeyName {
+  uint64_t h;
+  int field;
+};
+constexpr KeyName kKeys[] = {
+    {key_hash("transaction_id"), F_TXN_ID},
+    {key_hash("transactionId"), F_TXN_ID},
+    {key_hash("user_id"), F_USER_ID},
+    {key_hash("userId"), F_USER_ID},
+    {key_hash("merchant_id"), F_MERCHANT_ID},
+    {key_hash("merchantId"), F_MERCHANT_ID},
+    {key_hash("amount"), F_AMOUNT},
+    {key_hash("timestamp"), F_TIMESTAMP},
+    {key_hash("ip_address"), F_IP},
+    {key_hash("ipAddress"), F_IP},
+    {key_hash("device_fingerprint"), F_DEVICE_FP},
+    {key_hash("deviceFingerprint"), F_DEVICE_FP},
+    {key_hash("user_agent"), F_UA},
+    {key_hash("userAgent"), F_UA},
+    {key_hash("geolocation"), F_GEO},
+    {key_hash("merchant_location"), F_MLOC},
+    {key_hash("merchantLocation"), F_MLOC},
+    {key_hash("is_weekend"), F_WEEKEND},
+    {key_hash("isWeekend"), F_WEEKEND},
+    {key_hash("hour_of_day"), F_HOUR},
+    {key_hash("hourOfDay"), F_HOUR},
+    {key_hash("is_fraud"), F_FRAUD},
+    {key_hash("isFraud"), F_FRAUD},
+    {key_hash("fraud_score"), F_SCORE},
+    {key_hash("fraudScore"), F_SCORE},
+    {key_hash("payment_method"), F_PAY},
+    {key_hash("paymentMethod"), F_PAY},
+    {key_hash("transaction_type"), F_TTYPE},
+    {key_hash("transactionType"), F_TTYPE},
+    {key_hash("card_type"), F_CTYPE},
+    {key_hash("cardType"), F_CTYPE},
+};
+constexpr int kNumKeys = 31;
+
 __device__ __forceinline__ int field_of_key(uint64_t h) {
-#define FD_K(name, f) \
-  if (h == key_hash(name)) return f;
-  FD_K("transaction_id", F_TXN_ID) FD_K("transactionId", F_TXN_ID)
-  FD_K("user_id", F_USER_ID) FD_K("userId", F_USER_ID)
-  FD_K("merchant_id", F_MERCHANT_ID) FD_K("merchantId", F_MERCHANT_ID)
-  FD_K("amount", F_AMOUNT)
-  FD_K("timestamp", F_TIMESTAMP)
-  FD_K("ip_address", F_IP) FD_K("ipAddress", F_IP)
-  FD_K("device_fingerprint", F_DEVICE_FP) FD_K("deviceFingerprint", F_DEVICE_FP)
-  FD_K("user_agent", F_UA) FD_K("userAgent", F_UA)
-  FD_K("geolocation", F_GEO)
-  FD_K("merchant_location", F_MLOC) FD_K("merchantLocation", F_MLOC)
-  FD_K("is_weekend", F_WEEKEND) FD_K("isWeekend", F_WEEKEND)
-  FD_K("hour_of_day", F_HOUR) FD_K("hourOfDay", F_HOUR)
-  FD_K("is_fraud", F_FRAUD) FD_K("isFraud", F_FRAUD)
-  FD_K("fraud_score", F_SCORE) FD_K("fraudScore", F_SCORE)
-  FD_K("payment_method", F_PAY) FD_K("paymentMethod", F_PAY)
-  FD_K("transaction_type", F_TTYPE) FD_K("transactionType", F_TTYPE)
-  FD_K("card_type", F_CTYPE) FD_K("cardType", F_CTYPE)
-#undef FD_K
-  return -1;
+  int f = -1;
+#pragma unroll
+  for (int k = 0; k < kNumKeys; ++k)
+    if (h == kKeys[k].h) f = kKeys[k].field;
+  return f;
 }
 
 // byte view of a wave's staged message (message byte i = stage[shift + i]); one ds_read_u8 per access keeps
