@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 8
+#define FD_ABI_VERSION 9
 
 enum fd_status {
   FD_OK = 0,
@@ -422,6 +422,33 @@ int fd_windows_step_host(fd_engine* eng, const fd_txn_batch* txns, const fd_wind
                          fd_merchant_window* merchant_out, int64_t merchant_cap, int64_t* n_merchant);
 /* current watermark (INT64_MIN before the first) and events held in the user / merchant logs */
 int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, int64_t* merchant_events);
+
+/* ---------------------------------------------------------------- sink aggregates */
+/* RedisTransactionSink.updateAggregations (fl/sinks/RedisTransactionSink.java:140-262): per transaction the
+   hourly:{ts/3600000}, daily:{ts/86400000} and merchant:{merchant}:{ts/3600000} summaries (count, amount,
+   fraud count, high-risk count (hourly, fraudScore > 0.7), distinct users (merchant)), HBM-resident.
+   Amounts are exact integer cents (reported / 100); the reference's 30-min Redis TTL is wall-clock, so
+   retention here is explicit (fd_sink_evict_before). Declared semantics: DESIGN.md §4.8. */
+typedef struct {
+  int64_t capacity;      /* aggregate entries (hourly + daily + merchant-hour buckets held at once) */
+  int64_t user_capacity; /* distinct (merchant, hour, card) members held at once */
+} fd_sink_params;
+enum fd_agg_kind { FD_AGG_HOURLY = 1, FD_AGG_DAILY = 2, FD_AGG_MERCHANT = 3 };
+typedef struct { /* the stored aggregation map (updateHourly/Daily/MerchantAggregations :165-262); 64 B */
+  int64_t total_count, fraud_count, high_risk_count, unique_user_count;
+  double total_amount, fraud_rate, avg_amount;
+  int32_t found, pad;
+} fd_aggregate;
+int fd_sink_init(fd_engine* eng, const fd_sink_params* params);
+/* apply one micro-batch (device pointers; card_key, ts_ms, amount_cents, merchant of fd_txn_batch; is_fraud /
+   fraud_score of fd_window_inputs, NULL = false / null). Synchronous (error check). */
+int fd_sink_update_device(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n);
+int fd_sink_update_host(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n);
+/* RedisService.getAggregation: bucket = hour or day key, merchant index for FD_AGG_MERCHANT (else ignored) */
+int fd_sink_query_host(fd_engine* eng, int32_t kind, const int64_t* bucket, const int32_t* merchant, int64_t n,
+                       fd_aggregate* out);
+/* drop every bucket older than hour_key (a day is kept while any of its hours is) */
+int fd_sink_evict_before(fd_engine* eng, int64_t hour_key, int64_t* kept_entries, int64_t* kept_users);
 
 /* ---------------------------------------------------------------- state snapshot / restore */
 /* Durable image of the HBM keyed state: the counterpart of Flink's keyed-state checkpoints

@@ -209,6 +209,7 @@ int fd_engine_destroy(fd_engine* eng) {
   e.feat_vec.release();
   e.feat_in.release();
   fd::windows_release(e);
+  fd::sink_release(e);
   for (auto* b : {&e.route_blk, &e.route_soa, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.bias,
                   &e.lstm.wout, &e.lstm.bout, &e.state.seq})
     b->release();
@@ -719,6 +720,73 @@ int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, i
   if (watermark) *watermark = e.windows.wm;
   if (user_events) *user_events = e.windows.ucount;
   if (merchant_events) *merchant_events = e.windows.mcount;
+  FD_API_END
+}
+
+int fd_sink_init(fd_engine* eng, const fd_sink_params* params) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
+  FD_HIP(hipStreamSynchronize(e.stream));
+  fd::sink_init(e, *params);
+  FD_API_END
+}
+
+int fd_sink_update_device(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null batch");
+  const fd_window_inputs none{nullptr, nullptr, nullptr};
+  fd::sink_update(e, *txns, in ? *in : none, n);
+  FD_API_END
+}
+
+int fd_sink_update_host(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  if (n == 0) return FD_OK;
+  FD_REQUIRE(txns->card_key && txns->ts_ms && txns->amount_cents && txns->merchant, FD_ERR_INVALID_ARG,
+             "batch needs card_key, ts_ms, amount_cents and merchant");
+  const size_t nn = (size_t)n;
+  const size_t fo = ((nn * 4 + 15) & ~(size_t)15), so = fo + ((nn + 15) & ~(size_t)15);
+  e.stage_in.ensure(nn * 24 + so + nn * 8 + 64);
+  char* b = e.stage_in.as<char>();
+  FD_HIP(hipMemcpyAsync(b, txns->card_key, nn * 8, hipMemcpyHostToDevice, e.stream));
+  FD_HIP(hipMemcpyAsync(b + nn * 8, txns->ts_ms, nn * 8, hipMemcpyHostToDevice, e.stream));
+  FD_HIP(hipMemcpyAsync(b + nn * 16, txns->amount_cents, nn * 8, hipMemcpyHostToDevice, e.stream));
+  char* x = b + nn * 24;
+  FD_HIP(hipMemcpyAsync(x, txns->merchant, nn * 4, hipMemcpyHostToDevice, e.stream));
+  fd_window_inputs din{nullptr, nullptr, nullptr};
+  if (in && in->is_fraud) {
+    FD_HIP(hipMemcpyAsync(x + fo, in->is_fraud, nn, hipMemcpyHostToDevice, e.stream));
+    din.is_fraud = reinterpret_cast<const uint8_t*>(x + fo);
+  }
+  if (in && in->fraud_score) {
+    FD_HIP(hipMemcpyAsync(x + so, in->fraud_score, nn * 8, hipMemcpyHostToDevice, e.stream));
+    din.fraud_score = reinterpret_cast<const double*>(x + so);
+  }
+  fd_txn_batch d{};
+  d.card_key = reinterpret_cast<const uint64_t*>(b);
+  d.ts_ms = reinterpret_cast<const int64_t*>(b + nn * 8);
+  d.amount_cents = reinterpret_cast<const int64_t*>(b + nn * 16);
+  d.merchant = reinterpret_cast<const int32_t*>(x);
+  fd::sink_update(e, d, din, n);
+  FD_API_END
+}
+
+int fd_sink_query_host(fd_engine* eng, int32_t kind, const int64_t* bucket, const int32_t* merchant, int64_t n,
+                       fd_aggregate* out) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::sink_query(e, kind, bucket, merchant, n, out);
+  FD_API_END
+}
+
+int fd_sink_evict_before(fd_engine* eng, int64_t hour_key, int64_t* kept_entries, int64_t* kept_users) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::sink_evict_before(e, hour_key, kept_entries, kept_users);
   FD_API_END
 }
 

@@ -154,6 +154,13 @@ struct WindowState {
   DeviceBuffer keys, vals, sort_tmp, uout, mout, scalars, stage;
 };
 
+// RedisTransactionSink bucket aggregates (sink.hip)
+struct SinkState {
+  bool ready = false;
+  unsigned long long cap = 0, ucap = 0;
+  DeviceBuffer table, users, err;
+};
+
 // JSON ingest codec lookup tables (ingest.hip): merchant ids and the three vocabularies, hash -> index
 struct IngestTables {
   DeviceBuffer mkeys, mvals, vkeys[3], vvals[3];
@@ -178,6 +185,7 @@ struct Engine {
   LstmModel lstm;
   WindowState windows;
   IngestTables ingest;
+  SinkState sink;
   hipStream_t aux_stream = nullptr;            // LSTM head runs here, concurrent with the forests
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   hipStream_t aux2_stream = nullptr;           // small batches: the second forest, concurrent with the first
@@ -231,6 +239,12 @@ void windows_release(Engine& e);
 void ingest_set_vocab(Engine& e, int which, const uint8_t* bytes, const int64_t* offsets, int64_t n);
 void ingest_set_merchants(Engine& e, const uint8_t* bytes, const int64_t* offsets, int64_t n);
 void launch_ingest(Engine& e, const uint8_t* d_bytes, const int64_t* d_offsets, int64_t n, const fd_ingest_out& out);
+// sink.hip
+void sink_init(Engine& e, const fd_sink_params& p);
+void sink_update(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, int64_t n);
+void sink_query(Engine& e, int kind, const int64_t* bucket, const int32_t* merchant, int64_t n, fd_aggregate* out);
+void sink_evict_before(Engine& e, int64_t hour, int64_t* kept_entries, int64_t* kept_users);
+void sink_release(Engine& e);
 // snapshot.hip
 void state_snapshot(Engine& e, const char* path, int shard, int n_shards, int64_t* bytes_written);
 void state_restore(Engine& e, const char* path, int shard, int n_shards, int flags, int64_t* cards_restored);

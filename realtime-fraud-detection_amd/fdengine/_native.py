@@ -160,6 +160,16 @@ FD_INGEST_MALFORMED, FD_INGEST_TOO_LONG, FD_INGEST_UNKNOWN_VOCAB, FD_INGEST_INEX
 FD_INGEST_INVALID = FD_INGEST_MALFORMED | FD_INGEST_TOO_LONG | FD_INGEST_MISSING
 
 
+class fd_sink_params(C.Structure):
+    _fields_ = [("capacity", C.c_int64), ("user_capacity", C.c_int64)]
+
+
+FD_AGG_HOURLY, FD_AGG_DAILY, FD_AGG_MERCHANT = 1, 2, 3
+AGGREGATE_DTYPE = [("total_count", "<i8"), ("fraud_count", "<i8"), ("high_risk_count", "<i8"),
+                   ("unique_user_count", "<i8"), ("total_amount", "<f8"), ("fraud_rate", "<f8"),
+                   ("avg_amount", "<f8"), ("found", "<i4"), ("pad", "<i4")]
+
+
 class fd_ingest_out(C.Structure):
     _fields_ = [(name, C.c_void_p) for name, _ in INGEST_FIELDS]
 
@@ -253,6 +263,11 @@ SIGNATURES = {
     "fd_state_snapshot": (C.c_int, [_vp, C.c_char_p, _i32, _i32, C.POINTER(_i64)]),
     "fd_state_restore": (C.c_int, [_vp, C.c_char_p, _i32, _i32, _i32, C.POINTER(_i64)]),
     "fd_hash64": (C.c_int, [_vp, _i64, C.POINTER(C.c_uint64)]),
+    "fd_sink_init": (C.c_int, [_vp, C.POINTER(fd_sink_params)]),
+    "fd_sink_update_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_window_inputs), _i64]),
+    "fd_sink_update_host": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_window_inputs), _i64]),
+    "fd_sink_query_host": (C.c_int, [_vp, _i32, _vp, _vp, _i64, _vp]),
+    "fd_sink_evict_before": (C.c_int, [_vp, _i64, C.POINTER(_i64), C.POINTER(_i64)]),
     "fd_ingest_set_vocab": (C.c_int, [_vp, _i32, _vp, _vp, _i64]),
     "fd_ingest_set_merchants": (C.c_int, [_vp, _vp, _vp, _i64]),
     "fd_ingest_json_device": (C.c_int, [_vp, _vp, _vp, _i64, C.POINTER(fd_ingest_out)]),

@@ -19,7 +19,7 @@ LIB_DIR = PKG_ROOT / "lib"
 ORACLE_DIR = REPO_ROOT / "oracle"
 
 HIP_SOURCES = ["engine.hip", "forest.hip", "blend.hip", "features.hip", "route.hip", "lstm.hip",
-               "windows.hip", "snapshot.hip", "ingest.hip"]
+               "windows.hip", "snapshot.hip", "ingest.hip", "sink.hip"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-result"]
 

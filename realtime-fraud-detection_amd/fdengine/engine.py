@@ -291,6 +291,42 @@ class FraudEngine:
         N.call("fd_windows_stats", self._h, C.byref(wm), C.byref(ue), C.byref(me))
         return {"watermark": wm.value, "user_events": ue.value, "merchant_events": me.value}
 
+    # ------------------------------------------------------------------ RedisTransactionSink aggregates
+    def sink_init(self, capacity: int, user_capacity: int) -> None:
+        """Hourly / daily / merchant-hour summaries of RedisTransactionSink.updateAggregations
+        (fl/sinks/RedisTransactionSink.java:140-262), HBM-resident."""
+        p = N.fd_sink_params(int(capacity), int(user_capacity))
+        N.call("fd_sink_init", self._h, C.byref(p))
+
+    def sink_update_host(self, key, ts_ms, amount_cents, merchant, is_fraud=None, fraud_score=None) -> None:
+        keep = [np.ascontiguousarray(key, np.uint64), np.ascontiguousarray(ts_ms, np.int64),
+                np.ascontiguousarray(amount_cents, np.int64), np.ascontiguousarray(merchant, np.int32)]
+        b = N.fd_txn_batch(*[a.ctypes.data for a in keep], None, None, None, None)
+        fr = None if is_fraud is None else np.ascontiguousarray(is_fraud, np.uint8)
+        fs = None if fraud_score is None else np.ascontiguousarray(fraud_score, np.float64)
+        wi = N.fd_window_inputs(None, None if fr is None else fr.ctypes.data, None if fs is None else fs.ctypes.data)
+        N.call("fd_sink_update_host", self._h, C.byref(b), C.byref(wi), len(keep[0]))
+
+    def sink_update_device(self, txn_ptrs: dict, n: int, in_ptrs: Optional[dict] = None) -> None:
+        b = N.fd_txn_batch(*[int(txn_ptrs.get(f) or 0) or None for f in N.TXN_FIELDS])
+        wi = N.fd_window_inputs(None, *[int(in_ptrs[f]) if in_ptrs and in_ptrs.get(f) else None
+                                        for f in ("is_fraud", "fraud_score")])
+        N.call("fd_sink_update_device", self._h, C.byref(b), C.byref(wi), int(n))
+
+    def sink_query(self, kind: int, buckets, merchants=None) -> np.ndarray:
+        """RedisService.getAggregation for hourly / daily (bucket) or merchant (merchant, hour) keys."""
+        bk = np.ascontiguousarray(buckets, np.int64)
+        mk = None if merchants is None else np.ascontiguousarray(merchants, np.int32)
+        out = np.zeros(len(bk), N.AGGREGATE_DTYPE)
+        N.call("fd_sink_query_host", self._h, int(kind), _ptr(bk) if len(bk) else None,
+               _ptr(mk) if mk is not None and len(mk) else None, len(bk), out.ctypes.data if len(bk) else None)
+        return out
+
+    def sink_evict_before(self, hour_key: int):
+        a, b = C.c_int64(), C.c_int64()
+        N.call("fd_sink_evict_before", self._h, int(hour_key), C.byref(a), C.byref(b))
+        return a.value, b.value
+
     # ------------------------------------------------------------------ state snapshot / restore
     def state_snapshot(self, path, shard: int = 0, n_shards: int = 1) -> int:
         """Durable key-addressed image of the HBM keyed state (+ replicated tables, window logs);
