@@ -225,6 +225,14 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipEventDestroy(e.join2_ev);
   }
   for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
+  {  // ingest codec tables and staging
+    fd::IngestTables& t = e.ingest;
+    for (auto* b : {&t.mkeys, &t.mvals, &t.stage_bytes, &t.stage_offsets, &t.stage_out}) b->release();
+    for (int w = 0; w < 3; ++w) {
+      t.vkeys[w].release();
+      t.vvals[w].release();
+    }
+  }
   for (auto* b : {&e.state.headers, &e.state.fps, &e.state.ring, &e.state.merchants, &e.state.slot,
                   &e.state.next, &e.state.err})
     b->release();

@@ -463,14 +463,17 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
 
   // ---- structure, from registers: lane i owns stage bytes [64i, 64i + 64) (16-B aligned) = message bytes
   //      [q0, q0 + 64) with q0 = 64i - shift, valid where 0 <= q0 + k < L
-  const unsigned* seg = reinterpret_cast<const unsigned*>(&stage[wv][lane * 64]);
-  const int q0 = lane * 64 - shift;
+  // segment width: the staged bytes [0, shift + L) over 64 lanes, a multiple of 4 (4..64); a 750-B message
+  // costs 12 bytes per lane instead of a fixed 64
+  const int seg_words = max(1, (shift + L + 255) / 256);
+  const unsigned* seg = reinterpret_cast<const unsigned*>(&stage[wv][lane * 4 * seg_words]);
+  const int q0 = lane * 4 * seg_words - shift;
   // pass 1: trailing backslash run (escape carry into the next lane), first / last non-whitespace byte, quote
   // parity assuming an even carry, and the byte after the segment's leading backslash run
   int run = 0, nvalid = 0, first_nw = L, last_nw = -1, par = 0, lead = 0, after_lead = -1;
   bool leading = true;
 #pragma unroll 2
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < seg_words; ++j) {
     const unsigned w = seg[j];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -514,7 +517,7 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
   // pass 2: bracket depth deltas outside strings -> wave prefix sum
   int in = in0, delta = 0, mind = 0, bs = bs0;
 #pragma unroll 2
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < seg_words; ++j) {
     const unsigned w = seg[j];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -547,7 +550,7 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
   bs = bs0;
   int depth = depth0, zero_at = L;
 #pragma unroll 2
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < seg_words; ++j) {
     const unsigned w = seg[j];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
