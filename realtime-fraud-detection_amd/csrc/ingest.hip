@@ -30,6 +30,7 @@ namespace fd {
 namespace {
 
 constexpr int kWaves = 4;
+constexpr int kSlots = 2 * kWaves;  // messages per workgroup
 constexpr int kMaxMsg = 4080;      // bytes per message: 64 lanes x 64-byte segments minus the 16-B alignment shift
 constexpr int kMaxMembers = 64;    // top-level members per message (one per lane; more -> malformed)
 constexpr int kStage = 4096;
@@ -415,196 +416,216 @@ struct Val {
 __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* __restrict__ buf,
                                                           const int64_t* __restrict__ offsets, int64_t n, Tables T,
                                                           fd_ingest_out out, int stop_after) {
-  __shared__ __attribute__((aligned(16))) unsigned char stage[kWaves][kStage];
-  __shared__ int colon[kWaves][kMaxMembers];
-  __shared__ int nmem[kWaves], ncomma[kWaves];
-  __shared__ unsigned status_s[kWaves];
-  __shared__ int win[kWaves][F_COUNT];
+  __shared__ __attribute__((aligned(16))) unsigned char stage[kSlots][kStage];
+  __shared__ int colon[kSlots][kMaxMembers];
+  __shared__ int nmem[kSlots], ncomma[kSlots], shift_s[kSlots], len_s[kSlots];
+  __shared__ unsigned status_s[kSlots];
+  __shared__ int win[kSlots][F_COUNT];
 
   const int wv = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  const int64_t m = (int64_t)blockIdx.x * kWaves + wv;
-  const bool live = m < n;
-  int64_t off = 0, len = 0;
-  if (live) {
-    off = offsets[m];
-    len = offsets[m + 1] - off;
-  }
-  const int64_t total_bytes = offsets[n];
-  if (lane == 0) {
-    nmem[wv] = 0;
-    ncomma[wv] = 0;
-    status_s[wv] = (live && (len > kMaxMsg || len < 0)) ? FD_INGEST_TOO_LONG : 0u;
-  }
-  if (lane < F_COUNT) win[wv][lane] = -1;
-  const bool go = live && len >= 0 && len <= kMaxMsg;
-  const int L = go ? (int)len : 0;
-  // ---- stage (aligned 16-B loads; the tail beyond the input buffer byte by byte)
-  const int64_t a0 = off & ~15ll;
-  const int shift = (int)(off - a0);
-  const int span = shift + L;
-  for (int k = lane; k * 16 < span; k += 64) {
-    const int64_t g = a0 + 16ll * k;
-    uint4 v;
-    if (g + 16 <= total_bytes) {
-      v = *reinterpret_cast<const uint4*>(buf + g);
-    } else {  // the buffer's last partial chunk, byte by byte (no read past its end)
-      unsigned wq[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int q = 0; q < 16; ++q)
-        if (g + q < total_bytes) wq[q >> 2] |= (unsigned)buf[g + q] << (8 * (q & 3));
-      v = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+  // ---- staging and structure: wave w indexes messages 2w and 2w+1 of the block's 8, one after the other
+  for (int h = 0; h < 2; ++h) {
+    const int ms = 2 * wv + h;
+    const int64_t m = (int64_t)blockIdx.x * kSlots + ms;
+    const bool live = m < n;
+    int64_t off = 0, len = 0;
+    if (live) {
+      off = offsets[m];
+      len = offsets[m + 1] - off;
     }
-    *reinterpret_cast<uint4*>(&stage[wv][16 * k]) = v;
-  }
-  __syncthreads();
-  if (stop_after == 1) return;
-  const Reader s{&stage[wv][0], shift};
+    const int64_t total_bytes = offsets[n];
+    if (lane == 0) {
+      nmem[ms] = 0;
+      ncomma[ms] = 0;
+      status_s[ms] = (live && (len > kMaxMsg || len < 0)) ? FD_INGEST_TOO_LONG : 0u;
+    }
+    if (lane < F_COUNT) win[ms][lane] = -1;
+    const bool go = live && len >= 0 && len <= kMaxMsg;
+    const int L = go ? (int)len : 0;
+    // ---- stage (aligned 16-B loads; the tail beyond the input buffer byte by byte)
+    const int64_t a0 = off & ~15ll;
+    const int shift = (int)(off - a0);
+    const int span = shift + L;
+    for (int k = lane; k * 16 < span; k += 64) {
+      const int64_t g = a0 + 16ll * k;
+      uint4 v;
+      if (g + 16 <= total_bytes) {
+        v = *reinterpret_cast<const uint4*>(buf + g);
+      } else {  // the buffer's last partial chunk, byte by byte (no read past its end)
+        unsigned wq[4] = {0u, 0u, 0u, 0u};
+  #pragma unroll
+        for (int q = 0; q < 16; ++q)
+          if (g + q < total_bytes) wq[q >> 2] |= (unsigned)buf[g + q] << (8 * (q & 3));
+        v = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+      }
+      *reinterpret_cast<uint4*>(&stage[ms][16 * k]) = v;
+    }
+    __syncthreads();
+    if (stop_after == 1) continue;
+    const Reader s{&stage[ms][0], shift};
 
-  // ---- structure, from registers: lane i owns stage bytes [64i, 64i + 64) (16-B aligned) = message bytes
-  //      [q0, q0 + 64) with q0 = 64i - shift, valid where 0 <= q0 + k < L
-  // segment width: the staged bytes [0, shift + L) over 64 lanes, a multiple of 4 (4..64); a 750-B message
-  // costs 12 bytes per lane instead of a fixed 64
-  const int seg_words = max(1, (shift + L + 255) / 256);
-  const unsigned* seg = reinterpret_cast<const unsigned*>(&stage[wv][lane * 4 * seg_words]);
-  const int q0 = lane * 4 * seg_words - shift;
-  // pass 1: trailing backslash run (escape carry into the next lane), first / last non-whitespace byte, quote
-  // parity assuming an even carry, and the byte after the segment's leading backslash run
-  int run = 0, nvalid = 0, first_nw = L, last_nw = -1, par = 0, lead = 0, after_lead = -1;
-  bool leading = true;
-#pragma unroll 2
-  for (int j = 0; j < seg_words; ++j) {
-    const unsigned w = seg[j];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int k = 4 * j + b, p = q0 + k;
-      const int c = (int)((w >> (8 * b)) & 0xFFu);
-      if ((unsigned)p < (unsigned)L) {
-        ++nvalid;
-        if (c == '"' && !(run & 1)) par ^= 1;
-        if (leading) {
-          if (c == '\\') {
-            ++lead;
-          } else {
-            leading = false;
-            after_lead = c;
+    // ---- structure, from registers: lane i owns stage bytes [64i, 64i + 64) (16-B aligned) = message bytes
+    //      [q0, q0 + 64) with q0 = 64i - shift, valid where 0 <= q0 + k < L
+    // segment width: the staged bytes [0, shift + L) over 64 lanes, a multiple of 4 (4..64); a 750-B message
+    // costs 12 bytes per lane instead of a fixed 64
+    const int seg_words = max(1, (shift + L + 255) / 256);
+    const unsigned* seg = reinterpret_cast<const unsigned*>(&stage[ms][lane * 4 * seg_words]);
+    const int q0 = lane * 4 * seg_words - shift;
+    // pass 1: trailing backslash run (escape carry into the next lane), first / last non-whitespace byte, quote
+    // parity assuming an even carry, and the byte after the segment's leading backslash run
+    int run = 0, nvalid = 0, first_nw = L, last_nw = -1, par = 0, lead = 0, after_lead = -1;
+    bool leading = true;
+  #pragma unroll 2
+    for (int j = 0; j < seg_words; ++j) {
+      const unsigned w = seg[j];
+  #pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int k = 4 * j + b, p = q0 + k;
+        const int c = (int)((w >> (8 * b)) & 0xFFu);
+        if ((unsigned)p < (unsigned)L) {
+          ++nvalid;
+          if (c == '"' && !(run & 1)) par ^= 1;
+          if (leading) {
+            if (c == '\\') {
+              ++lead;
+            } else {
+              leading = false;
+              after_lead = c;
+            }
           }
-        }
-        run = (c == '\\') ? run + 1 : 0;
-        if (!is_ws(c)) {
-          first_nw = min(first_nw, p);
-          last_nw = p;
+          run = (c == '\\') ? run + 1 : 0;
+          if (!is_ws(c)) {
+            first_nw = min(first_nw, p);
+            last_nw = p;
+          }
         }
       }
     }
-  }
-  int bs0 = __shfl_up(run, 1);
-  if (lane == 0) bs0 = 0;
-  if (__ballot(nvalid > 0 && run == nvalid) != 0ull) {  // a segment of only backslashes: exact carry from LDS
-    int b2 = 0;
-    for (int p = q0 - 1; p >= 0 && q0 < L && s[p] == '\\'; --p) ++b2;
-    bs0 = b2;
-  }
-  if ((bs0 & 1) && after_lead == '"') par ^= 1;  // the carry escapes the first quote after the leading run
-  for (int d = 32; d >= 1; d >>= 1) {
-    first_nw = min(first_nw, __shfl_xor(first_nw, d));
-    last_nw = max(last_nw, __shfl_xor(last_nw, d));
-  }
-  const unsigned long long pb = __ballot(par);
-  const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  const int in0 = __popcll(pb & lt) & 1;
-  const int total_par = __popcll(pb) & 1;
-  // pass 2: bracket depth deltas outside strings -> wave prefix sum
-  int in = in0, delta = 0, mind = 0, bs = bs0;
-#pragma unroll 2
-  for (int j = 0; j < seg_words; ++j) {
-    const unsigned w = seg[j];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int p = q0 + 4 * j + b;
-      const int c = (int)((w >> (8 * b)) & 0xFFu);
-      if ((unsigned)p < (unsigned)L) {
-        if (c == '"' && !(bs & 1)) {
-          in ^= 1;
-        } else if (!in) {
-          if (c == '{' || c == '[') ++delta;
-          if (c == '}' || c == ']') {
-            --delta;
-            mind = min(mind, delta);
+    int bs0 = __shfl_up(run, 1);
+    if (lane == 0) bs0 = 0;
+    if (__ballot(nvalid > 0 && run == nvalid) != 0ull) {  // a segment of only backslashes: exact carry from LDS
+      int b2 = 0;
+      for (int p = q0 - 1; p >= 0 && q0 < L && s[p] == '\\'; --p) ++b2;
+      bs0 = b2;
+    }
+    if ((bs0 & 1) && after_lead == '"') par ^= 1;  // the carry escapes the first quote after the leading run
+    for (int d = 32; d >= 1; d >>= 1) {
+      first_nw = min(first_nw, __shfl_xor(first_nw, d));
+      last_nw = max(last_nw, __shfl_xor(last_nw, d));
+    }
+    const unsigned long long pb = __ballot(par);
+    const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const int in0 = __popcll(pb & lt) & 1;
+    const int total_par = __popcll(pb) & 1;
+    // pass 2: bracket depth deltas outside strings -> wave prefix sum
+    int in = in0, delta = 0, mind = 0, bs = bs0;
+  #pragma unroll 2
+    for (int j = 0; j < seg_words; ++j) {
+      const unsigned w = seg[j];
+  #pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int p = q0 + 4 * j + b;
+        const int c = (int)((w >> (8 * b)) & 0xFFu);
+        if ((unsigned)p < (unsigned)L) {
+          if (c == '"' && !(bs & 1)) {
+            in ^= 1;
+          } else if (!in) {
+            if (c == '{' || c == '[') ++delta;
+            if (c == '}' || c == ']') {
+              --delta;
+              mind = min(mind, delta);
+            }
           }
+          bs = (c == '\\') ? bs + 1 : 0;
         }
-        bs = (c == '\\') ? bs + 1 : 0;
       }
     }
-  }
-  int depth0 = delta;  // inclusive prefix sum over lanes
-  for (int d = 1; d < 64; d <<= 1) {
-    const int v = __shfl_up(depth0, d);
-    if (lane >= d) depth0 += v;
-  }
-  const int total_depth = __shfl(depth0, 63);
-  depth0 -= delta;
-  bool bad = (depth0 + mind < 0);
-  // pass 3: depth-1 colons (members), depth-1 commas and the first return to depth 0
-  in = in0;
-  bs = bs0;
-  int depth = depth0, zero_at = L;
-#pragma unroll 2
-  for (int j = 0; j < seg_words; ++j) {
-    const unsigned w = seg[j];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int p = q0 + 4 * j + b;
-      const int c = (int)((w >> (8 * b)) & 0xFFu);
-      if ((unsigned)p < (unsigned)L) {
-        if (c == '"' && !(bs & 1)) {
-          in ^= 1;
-        } else if (!in) {
-          if (c == ':' && depth == 1) {
-            const int slot = atomicAdd(&nmem[wv], 1);
-            if (slot < kMaxMembers) colon[wv][slot] = p;
-          } else if (c == ',' && depth == 1) {
-            atomicAdd(&ncomma[wv], 1);
-          } else if (c == '{' || c == '[') {
-            ++depth;
-          } else if (c == '}' || c == ']') {
-            --depth;
-            if (depth == 0) zero_at = min(zero_at, p);
+    int depth0 = delta;  // inclusive prefix sum over lanes
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(depth0, d);
+      if (lane >= d) depth0 += v;
+    }
+    const int total_depth = __shfl(depth0, 63);
+    depth0 -= delta;
+    bool bad = (depth0 + mind < 0);
+    // pass 3: depth-1 colons (members), depth-1 commas and the first return to depth 0
+    in = in0;
+    bs = bs0;
+    int depth = depth0, zero_at = L;
+  #pragma unroll 2
+    for (int j = 0; j < seg_words; ++j) {
+      const unsigned w = seg[j];
+  #pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int p = q0 + 4 * j + b;
+        const int c = (int)((w >> (8 * b)) & 0xFFu);
+        if ((unsigned)p < (unsigned)L) {
+          if (c == '"' && !(bs & 1)) {
+            in ^= 1;
+          } else if (!in) {
+            if (c == ':' && depth == 1) {
+              const int slot = atomicAdd(&nmem[ms], 1);
+              if (slot < kMaxMembers) colon[ms][slot] = p;
+            } else if (c == ',' && depth == 1) {
+              atomicAdd(&ncomma[ms], 1);
+            } else if (c == '{' || c == '[') {
+              ++depth;
+            } else if (c == '}' || c == ']') {
+              --depth;
+              if (depth == 0) zero_at = min(zero_at, p);
+            }
           }
+          bs = (c == '\\') ? bs + 1 : 0;
         }
-        bs = (c == '\\') ? bs + 1 : 0;
       }
     }
-  }
-  for (int d = 32; d >= 1; d >>= 1) zero_at = min(zero_at, __shfl_xor(zero_at, d));
-  bad = bad || (__ballot(bad) != 0ull);
-  if (go && lane == 0) {
-    const bool ok = !bad && L > 0 && total_par == 0 && total_depth == 0 && first_nw < L && s[first_nw] == '{' &&
-                    zero_at == last_nw;
-    if (!ok) status_s[wv] |= FD_INGEST_MALFORMED;
+    for (int d = 32; d >= 1; d >>= 1) zero_at = min(zero_at, __shfl_xor(zero_at, d));
+    bad = bad || (__ballot(bad) != 0ull);
+    if (go && lane == 0) {
+      const bool ok = !bad && L > 0 && total_par == 0 && total_depth == 0 && first_nw < L && s[first_nw] == '{' &&
+                      zero_at == last_nw;
+      if (!ok) status_s[ms] |= FD_INGEST_MALFORMED;
+    }
+    __syncthreads();
+    const int nm = go ? nmem[ms] : 0;
+    if (go && lane == 0 && status_s[ms] == 0u) {
+      // member skeleton: n members <-> n-1 depth-1 commas; an empty object holds only whitespace
+      bool bad_skel = nm > kMaxMembers || (nm > 0 && ncomma[ms] != nm - 1) || (nm == 0 && ncomma[ms] != 0);
+      if (nm == 0) {
+        int q = first_nw + 1;
+        while (q < L && is_ws(s[q])) ++q;
+        bad_skel = bad_skel || q != zero_at;
+      }
+      if (bad_skel) status_s[ms] |= FD_INGEST_MALFORMED;
+    }
+    __syncthreads();
+    const bool structural_ok = go && status_s[ms] == 0u;
+    if (lane == 0) {
+      shift_s[ms] = shift;
+      len_s[ms] = go ? L : -1;
+    }
   }
   __syncthreads();
-  const int nm = go ? nmem[wv] : 0;
-  if (go && lane == 0 && status_s[wv] == 0u) {
-    // member skeleton: n members <-> n-1 depth-1 commas; an empty object holds only whitespace
-    bool bad_skel = nm > kMaxMembers || (nm > 0 && ncomma[wv] != nm - 1) || (nm == 0 && ncomma[wv] != 0);
-    if (nm == 0) {
-      int q = first_nw + 1;
-      while (q < L && is_ws(s[q])) ++q;
-      bad_skel = bad_skel || q != zero_at;
-    }
-    if (bad_skel) status_s[wv] |= FD_INGEST_MALFORMED;
-  }
-  __syncthreads();
-  const bool structural_ok = go && status_s[wv] == 0u;
   if (stop_after == 2) return;
 
-  // ---- members: lane j parses member j
-  int my_field = -1, my_colon = -1;
-  Val my;
+  // ---- members: two messages per wave — half h = lane >> 5 parses message 2w+h, lane j = lane & 31 its members
+  //      j and j + 32 (the divergent member code is paid once for both messages)
+  const int ms = 2 * wv + (lane >> 5);
+  const int64_t m = (int64_t)blockIdx.x * kSlots + ms;
+  const bool live = m < n;
+  const int L = len_s[ms] < 0 ? 0 : len_s[ms];
+  const bool go = live && len_s[ms] >= 0;
+  const Reader s{&stage[ms][0], shift_s[ms]};
+  const int nm = go ? min(nmem[ms], kMaxMembers) : 0;
+  const bool structural_ok = go && status_s[ms] == 0u;
+  int my_field0 = -1, my_colon0 = -1, my_field1 = -1, my_colon1 = -1;
+  Val my0, my1;
   unsigned my_status = 0;
-  for (int once = 0; once < 1 && structural_ok && lane < nm; ++once) {  // `continue` = member rejected
-    const int c = colon[wv][lane];
+  for (int r = 0; r < 2; ++r) {
+  const int mi = 32 * r + (lane & 31);
+  for (int once = 0; once < 1 && structural_ok && mi < nm; ++once) {  // `continue` = member rejected
+    const int c = colon[ms][mi];
     // key: the string ending right before the colon
     int kc = c - 1;
     while (kc >= 0 && is_ws(s[kc])) --kc;
@@ -822,40 +843,53 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
       my_status |= FD_INGEST_MALFORMED;
       continue;
     }
-    my_field = f;
-    my_colon = c;
-    my = val;
-    atomicMax(&win[wv][f], c);
+    if (r == 0) {
+      my_field0 = f;
+      my_colon0 = c;
+      my0 = val;
+    } else {
+      my_field1 = f;
+      my_colon1 = c;
+      my1 = val;
+    }
+    atomicMax(&win[ms][f], c);
   }
-  if (my_status) atomicOr(&status_s[wv], my_status);
+  }
+  if (my_status) atomicOr(&status_s[ms], my_status);
   __syncthreads();
   if (stop_after == 3) {
-    if (live && lane == 0 && out.status) out.status[m] = (unsigned char)(my_field + my_colon);  // keep the work
+    if (live && (lane & 31) == 0 && out.status) out.status[m] = (unsigned char)(my_field0 + my_colon1);  // keep the work
     return;
   }
   // ---- resolve: the winner of each field publishes its value to LDS, then lane f writes column f
-  __shared__ unsigned long long vu[kWaves][F_COUNT];
-  __shared__ double va[kWaves][F_COUNT], vb[kWaves][F_COUNT];
-  __shared__ unsigned char vnull[kWaves][F_COUNT];
-  if (go && my_field >= 0 && win[wv][my_field] == my_colon) {
-    vu[wv][my_field] = my.u;
-    va[wv][my_field] = my.a;
-    vb[wv][my_field] = my.b;
-    vnull[wv][my_field] = my.null ? 1 : 0;
+  __shared__ unsigned long long vu[kSlots][F_COUNT];
+  __shared__ double va[kSlots][F_COUNT], vb[kSlots][F_COUNT];
+  __shared__ unsigned char vnull[kSlots][F_COUNT];
+  if (go && my_field0 >= 0 && win[ms][my_field0] == my_colon0) {
+    vu[ms][my_field0] = my0.u;
+    va[ms][my_field0] = my0.a;
+    vb[ms][my_field0] = my0.b;
+    vnull[ms][my_field0] = my0.null ? 1 : 0;
+  }
+  if (go && my_field1 >= 0 && win[ms][my_field1] == my_colon1) {
+    vu[ms][my_field1] = my1.u;
+    va[ms][my_field1] = my1.a;
+    vb[ms][my_field1] = my1.b;
+    vnull[ms][my_field1] = my1.null ? 1 : 0;
   }
   __syncthreads();
   if (!live) return;
-  unsigned st = status_s[wv];
+  unsigned st = status_s[ms];
   const bool valid_struct = (st & (FD_INGEST_MALFORMED | FD_INGEST_TOO_LONG)) == 0;
-  auto present = [&](int f) { return valid_struct && win[wv][f] >= 0 && !vnull[wv][f]; };
+  auto present = [&](int f) { return valid_struct && win[ms][f] >= 0 && !vnull[ms][f]; };
   if (valid_struct && (!present(F_USER_ID) || !present(F_AMOUNT) || !present(F_TIMESTAMP))) st |= FD_INGEST_MISSING;
   const bool ok = (st & (FD_INGEST_MALFORMED | FD_INGEST_TOO_LONG | FD_INGEST_MISSING)) == 0;
   if (!ok) st &= (FD_INGEST_MALFORMED | FD_INGEST_TOO_LONG | FD_INGEST_MISSING);  // an invalid row: its class only
-  const int f = lane;
+  const int f = lane & 31;
   if (f < F_COUNT) {
     const bool p = ok && present(f);
-    const unsigned long long u = p ? vu[wv][f] : 0ull;
-    const double A = p ? va[wv][f] : nan_d(), B = p ? vb[wv][f] : nan_d();
+    const unsigned long long u = p ? vu[ms][f] : 0ull;
+    const double A = p ? va[ms][f] : nan_d(), B = p ? vb[ms][f] : nan_d();
     switch (f) {
       case F_TXN_ID: if (out.txn_hash) out.txn_hash[m] = u; break;
       case F_USER_ID: if (out.card_key) out.card_key[m] = u; break;
@@ -882,7 +916,7 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
       case F_CTYPE: if (out.card_type) out.card_type[m] = p ? (unsigned char)u : 255; break;
       default: break;
     }
-  } else if (f == 63 && out.status) {
+  } else if (f == 31 && out.status) {
     out.status[m] = (unsigned char)st;
   }
 }
@@ -948,7 +982,7 @@ void launch_ingest(Engine& e, const uint8_t* d_bytes, const int64_t* d_offsets, 
     if (t.vloaded[w]) T.vocab[w] = Table{t.vkeys[w].as<const unsigned long long>(), t.vvals[w].as<const int>(), t.vmask[w]};
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_INGEST) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
-  const int64_t blocks = (n + kWaves - 1) / kWaves;
+  const int64_t blocks = (n + kSlots - 1) / kSlots;
   hipLaunchKernelGGL(ingest_json_kernel, dim3((unsigned)blocks), dim3(256), 0, e.stream, d_bytes, d_offsets, n, T, out,
                      t.stop_after);
   FD_HIP(hipGetLastError());
