@@ -462,9 +462,11 @@ int fd_state_snapshot(fd_engine* eng, const char* path, int32_t shard, int32_t n
    must match fd_state_init's) keeping only the cards with shard_of(key, n_shards) == shard — restoring
    every old shard's image on every new shard re-shards the state onto a different GPU count. Replicated
    tables are replaced. Window logs are appended (fd_windows_init first) unless FD_RESTORE_SKIP_WINDOWS;
-   images merged onto one engine must share the window watermark. On FD_ERR_IO / FD_ERR_OOM the state is
-   unspecified until fd_state_clear. */
+   images merged onto one engine must share the window watermark. The image also carries the sink aggregates
+   (replaced on restore; same shard / shard count only, else FD_RESTORE_SKIP_SINK) and the ingest codec's merchant /
+   vocabulary tables (replaced). On FD_ERR_IO / FD_ERR_OOM the state is unspecified until fd_state_clear. */
 #define FD_RESTORE_SKIP_WINDOWS 1
+#define FD_RESTORE_SKIP_SINK 2 /* sink aggregates (fd_sink_*) resume only on the same shard / shard count */
 int fd_state_restore(fd_engine* eng, const char* path, int32_t shard, int32_t n_shards, int32_t flags,
                      int64_t* cards_restored);
 

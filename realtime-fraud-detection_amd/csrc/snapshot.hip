@@ -33,6 +33,7 @@ constexpr int kFpWords = 2;        // 4 x u64 fingerprints per slot
 constexpr int kUextWords = 3;      // 48-B UserExt
 constexpr size_t kMerchantBytes = 16, kMerchExtBytes = 16, kWinEventBytes = 40, kVocabBytes = 512;
 constexpr int64_t kChunkSlots = 1 << 18;
+constexpr size_t kSinkEntryBytes = 48, kSinkUserBytes = 16;  // sink.hip AggEntry / UserEntry
 
 struct __attribute__((packed)) SnapHeader {  // 256 B, little-endian
   char magic[8];
@@ -43,7 +44,10 @@ struct __attribute__((packed)) SnapHeader {  // 256 B, little-endian
   double tp_threshold;
   int64_t win_ooo, win_wm, win_min_seen, win_max_seen, ucount, mcount;
   uint64_t checksum[6];  // cards, merchants, mext, vocab, user log, merchant log
-  uint8_t pad[72];
+  int32_t ext_flags;      // trailing extension sections: bit 0 sink aggregates, bit 1 ingest tables
+  int32_t ext_pad;
+  uint64_t ext_checksum;
+  uint8_t pad[56];
 };
 static_assert(sizeof(SnapHeader) == 256, "SnapHeader must be 256 B");
 constexpr char kMagic[8] = {'F', 'D', 'S', 'N', 'A', 'P', 0, 1};
@@ -339,6 +343,31 @@ void state_snapshot(Engine& e, const char* path, int shard, int n_shards, int64_
   if (hd.vocab_loaded) dump_device(e, out.f, st.vocab.ptr, kVocabBytes, pin, &h_v);
   if (hd.ucount) dump_device(e, out.f, w.ulog[w.ucur].ptr, (size_t)hd.ucount * kWinEventBytes, pin, &h_u);
   if (hd.mcount) dump_device(e, out.f, w.mlog[w.mcur].ptr, (size_t)hd.mcount * kWinEventBytes, pin, &h_l);
+  // extension sections: sink aggregates (raw tables; resume on the same shard), ingest lookup tables
+  Fnv h_ext;
+  SinkState& sk = e.sink;
+  if (sk.ready) {
+    hd.ext_flags |= 1;
+    const int64_t meta[4] = {(int64_t)sk.cap, (int64_t)sk.ucap, shard, n_shards};
+    write_all(out.f, meta, sizeof meta, &h_ext);
+    dump_device(e, out.f, sk.table.ptr, sk.cap * kSinkEntryBytes, pin, &h_ext);
+    dump_device(e, out.f, sk.users.ptr, sk.ucap * kSinkUserBytes, pin, &h_ext);
+  }
+  IngestTables& it = e.ingest;
+  if (it.mloaded || it.vloaded[0] || it.vloaded[1] || it.vloaded[2]) {
+    hd.ext_flags |= 2;
+    const int64_t meta[4] = {it.mloaded ? (int64_t)it.mmask + 1 : 0, it.vloaded[0] ? (int64_t)it.vmask[0] + 1 : 0,
+                             it.vloaded[1] ? (int64_t)it.vmask[1] + 1 : 0, it.vloaded[2] ? (int64_t)it.vmask[2] + 1 : 0};
+    write_all(out.f, meta, sizeof meta, &h_ext);
+    for (int t = 0; t < 4; ++t) {
+      if (!meta[t]) continue;
+      DeviceBuffer& kb = t == 0 ? it.mkeys : it.vkeys[t - 1];
+      DeviceBuffer& vb = t == 0 ? it.mvals : it.vvals[t - 1];
+      dump_device(e, out.f, kb.ptr, (size_t)meta[t] * 8, pin, &h_ext);
+      dump_device(e, out.f, vb.ptr, (size_t)meta[t] * 4, pin, &h_ext);
+    }
+  }
+  hd.ext_checksum = h_ext.h;
   hd.checksum[1] = h_m.h;
   hd.checksum[2] = h_x.h;
   hd.checksum[3] = h_v.h;
@@ -490,6 +519,59 @@ void state_restore(Engine& e, const char* path, int shard, int n_shards, int fla
   } else if (has_events && !skip_windows) {
     // windows_present == 0 but events recorded: corrupt
     throw Error(FD_ERR_IO, "restore: corrupt header (window events without window state)");
+  }
+  // extension sections
+  if (hd.ext_flags) {
+    Fnv h_ext;
+    std::vector<char> tmp;
+    auto read_to_device = [&](DeviceBuffer& d, size_t bytes) {
+      tmp.resize(bytes);
+      read_all(in.f, tmp.data(), bytes, &h_ext);
+      d.ensure(std::max<size_t>(bytes, 16));
+      FD_HIP(hipMemcpy(d.ptr, tmp.data(), bytes, hipMemcpyHostToDevice));
+    };
+    if (hd.ext_flags & 1) {
+      int64_t meta[4];
+      read_all(in.f, meta, sizeof meta, &h_ext);
+      FD_REQUIRE(meta[0] > 0 && meta[1] > 0 && (meta[0] & (meta[0] - 1)) == 0 && (meta[1] & (meta[1] - 1)) == 0,
+                 FD_ERR_IO, "restore: corrupt sink section");
+      const bool skip_sink = (flags_in & FD_RESTORE_SKIP_SINK) != 0;
+      if (!skip_sink) {
+        FD_REQUIRE(meta[2] == shard && meta[3] == n_shards, FD_ERR_INVALID_ARG,
+                   "restore: sink aggregates resume only on the same shard of the same shard count "
+                   "(FD_RESTORE_SKIP_SINK to re-shard without them)");
+        SinkState& sk = e.sink;
+        read_to_device(sk.table, (size_t)meta[0] * kSinkEntryBytes);
+        read_to_device(sk.users, (size_t)meta[1] * kSinkUserBytes);
+        sk.cap = (unsigned long long)meta[0];
+        sk.ucap = (unsigned long long)meta[1];
+        sk.err.ensure(16);
+        FD_HIP(hipMemset(sk.err.ptr, 0, 16));
+        sk.ready = true;
+      } else {
+        tmp.resize((size_t)meta[0] * kSinkEntryBytes + (size_t)meta[1] * kSinkUserBytes);
+        read_all(in.f, tmp.data(), tmp.size(), &h_ext);
+      }
+    }
+    if (hd.ext_flags & 2) {
+      int64_t meta[4];
+      read_all(in.f, meta, sizeof meta, &h_ext);
+      IngestTables& it = e.ingest;
+      for (int t = 0; t < 4; ++t) {
+        if (!meta[t]) continue;
+        FD_REQUIRE(meta[t] > 0 && (meta[t] & (meta[t] - 1)) == 0, FD_ERR_IO, "restore: corrupt ingest section");
+        read_to_device(t == 0 ? it.mkeys : it.vkeys[t - 1], (size_t)meta[t] * 8);
+        read_to_device(t == 0 ? it.mvals : it.vvals[t - 1], (size_t)meta[t] * 4);
+        if (t == 0) {
+          it.mmask = (unsigned long long)meta[t] - 1;
+          it.mloaded = true;
+        } else {
+          it.vmask[t - 1] = (unsigned long long)meta[t] - 1;
+          it.vloaded[t - 1] = true;
+        }
+      }
+    }
+    FD_REQUIRE(h_ext.h == hd.ext_checksum, FD_ERR_IO, "restore: extension section checksum mismatch");
   }
   unsigned err = 0;
   FD_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, e.stream));

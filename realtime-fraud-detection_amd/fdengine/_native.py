@@ -22,6 +22,7 @@ FD_ERR_UNSUPPORTED = 4
 FD_ERR_OOM = 5
 FD_ERR_IO = 6
 FD_RESTORE_SKIP_WINDOWS = 1
+FD_RESTORE_SKIP_SINK = 2
 
 FD_FOREST_XGB_BINARY_LOGISTIC = 1
 FD_FOREST_SKLEARN_IFOREST = 2

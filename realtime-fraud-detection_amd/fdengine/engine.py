@@ -335,12 +335,14 @@ class FraudEngine:
         N.call("fd_state_snapshot", self._h, os.fsencode(str(path)), int(shard), int(n_shards), C.byref(nb))
         return nb.value
 
-    def state_restore(self, path, shard: int = 0, n_shards: int = 1, skip_windows: bool = False) -> int:
+    def state_restore(self, path, shard: int = 0, n_shards: int = 1, skip_windows: bool = False,
+                      skip_sink: bool = False) -> int:
         """Re-insert an image's cards owned by `shard` of `n_shards` (any table capacity); returns the
         number of cards restored. Restore every old shard's image on each new shard to re-shard."""
         nc = C.c_int64()
         N.call("fd_state_restore", self._h, os.fsencode(str(path)), int(shard), int(n_shards),
-               N.FD_RESTORE_SKIP_WINDOWS if skip_windows else 0, C.byref(nc))
+               (N.FD_RESTORE_SKIP_WINDOWS if skip_windows else 0) | (N.FD_RESTORE_SKIP_SINK if skip_sink else 0),
+               C.byref(nc))
         return nc.value
 
     # ------------------------------------------------------------------ LSTM head

@@ -63,7 +63,7 @@ class EngineShardBackend:
         return self.eng.state_snapshot(path, rank, world)
 
     def restore(self, path: str, rank: int, world: int) -> int:
-        return self.eng.state_restore(path, rank, world, skip_windows=True)
+        return self.eng.state_restore(path, rank, world, skip_windows=True, skip_sink=True)
 
     def scatter_results(self, res, n: int):
         t = self.torch

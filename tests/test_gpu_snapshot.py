@@ -248,3 +248,57 @@ def test_image_deterministic_and_corruption_detected(engine, tmp_path):
         assert fresh.state_restore(a, skip_windows=True) == engine.state_info()["cards"]
     finally:
         fresh.close()
+
+
+def test_image_carries_sink_and_ingest_tables(engine, tmp_path):
+    """The image also holds the RedisTransactionSink aggregates (resume on the same shard) and the ingest codec's
+    merchant / vocabulary tables: a fresh engine restored from it continues both exactly."""
+    from fdengine._native import FD_AGG_HOURLY, FD_AGG_MERCHANT
+    from fdengine.ingest import IngestCodec
+    from oracle.sink_ref import SinkOracle
+    batches = synth.window_stream(6, 3000, 300, 40, seed=17, batch_span_ms=900_000)
+    engine.state_init(1 << 14, 1, 8)
+    engine.sink_init(1 << 13, 1 << 15)
+    sp = synth.sim_population(100, 30, seed=2)
+    codec = IngestCodec(engine, sp["merchant_ids"], synth.SIM_PAYMENT_METHODS, synth.SIM_TXN_TYPES,
+                        synth.SIM_CARD_TYPES)
+    msgs = synth.json_messages(sp, 300, seed=3)
+    before = codec.parse(msgs)
+    o = SinkOracle()
+
+    def feed(eng, b):
+        eng.sink_update_host(b["key"], b["ts_ms"], b["amount_cents"], b["merchant"], b["is_fraud"], b["fraud_score"])
+        o.run_batch(b)
+
+    for b in batches[:3]:
+        feed(engine, b)
+    path = tmp_path / "full.fdsnap"
+    engine.state_snapshot(path)
+    fresh = FraudEngine(0)
+    try:
+        fresh.state_init(1 << 12, 1, 8)
+        fresh.state_restore(path)
+        for b in batches[3:]:
+            fresh.sink_update_host(b["key"], b["ts_ms"], b["amount_cents"], b["merchant"], b["is_fraud"],
+                                   b["fraud_score"])
+            o.run_batch(b)
+        hours = sorted(int(k.split(":")[1]) for k in o.redis if k.startswith("hourly:"))
+        got = fresh.sink_query(FD_AGG_HOURLY, hours)
+        assert [int(x) for x in got["total_count"]] == [o.redis[f"hourly:{h}"]["total_count"] for h in hours]
+        mk = sorted((int(k.split(":")[1]), int(k.split(":")[2])) for k in o.redis if k.startswith("merchant:"))
+        got = fresh.sink_query(FD_AGG_MERCHANT, [h for _, h in mk], [m for m, _ in mk])
+        assert [int(x) for x in got["unique_user_count"]] == \
+               [o.redis[f"merchant:{m}:{h}"]["unique_user_count"] for m, h in mk]
+        # the codec tables came with the image (no set_merchants / set_vocab on the fresh engine)
+        c2 = IngestCodec.__new__(IngestCodec)
+        c2.eng = fresh
+        c2.vocab = [list(v) for v in codec.vocab]
+        after = c2._parse_packed(*__import__("fdengine.ingest", fromlist=["pack"]).pack(msgs))
+        for k in ("merchant", "payment_method", "transaction_type", "card_type", "card_key", "status"):
+            np.testing.assert_array_equal(after[k], before[k])
+        with pytest.raises(NativeError, match="same shard"):
+            fresh.state_restore(path, 1, 2)
+        fresh.state_init(1 << 12, 1, 8)
+        fresh.state_restore(path, 1, 2, skip_sink=True)
+    finally:
+        fresh.close()
