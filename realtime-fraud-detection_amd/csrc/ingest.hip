@@ -116,13 +116,14 @@ struct StrStats {
   int units = 0;
   bool bot = false, crawler = false;
   bool escaped = false;
-  __device__ __forceinline__ void byte(unsigned c) {
+  __device__ __forceinline__ void byte(unsigned c) {  // branchless: selects, no divergent branches per byte
     fnv = fnv_step(fnv, (unsigned char)c);
-    if (nbytes < 8) head |= (uint64_t)c << (8 * nbytes);
+    const uint64_t sh = (uint64_t)c << (8 * (nbytes & 7));
+    head |= (nbytes < 8) ? sh : 0ull;
     ++nbytes;
     roll = (roll << 8) | c;
-    if ((roll & 0xFFFFFFull) == 0x626F74ull) bot = true;                 // "bot"
-    if ((roll & 0xFFFFFFFFFFFFFFull) == 0x637261776C6572ull) crawler = true;  // "crawler"
+    bot = bot | ((roll & 0xFFFFFFull) == 0x626F74ull);                     // "bot"
+    crawler = crawler | ((roll & 0xFFFFFFFFFFFFFFull) == 0x637261776C6572ull);  // "crawler"
   }
   __device__ __forceinline__ void utf8(unsigned cp) {
     if (cp < 0x80) {
@@ -147,16 +148,17 @@ struct StrStats {
 __device__ __forceinline__ int scan_string(const Reader& s, int pos, int end, StrStats& st) {
   int i = pos + 1;
   while (i < end) {
-    const int c = s[i];
-    if (c == '"') return i + 1;
-    if (c < 0x20) return -1;  // unescaped control character
-    if (c != '\\') {
+    // the raw run: one tight loop, no per-byte branches besides the loop exit
+    int c = s[i];
+    while (c >= 0x20 && c != '"' && c != '\\') {
       st.byte((unsigned)c);
       // UTF-16 units of raw UTF-8: one per lead byte, two for a 4-byte sequence
-      if ((c & 0xC0) != 0x80) st.units += (c >= 0xF0) ? 2 : 1;
+      st.units += (int)((c & 0xC0) != 0x80) + (int)(c >= 0xF0);
       ++i;
-      continue;
+      c = i < end ? s[min(i, end - 1)] : -1;
     }
+    if (c == '"') return i + 1;
+    if (c != '\\') return -1;  // unescaped control character, or the end
     st.escaped = true;
     if (i + 1 >= end) return -1;
     const int e = s[i + 1];
