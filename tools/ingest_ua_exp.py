@@ -22,6 +22,8 @@ def sub(pat, rep):
 variants = {
     "full": base,
     "short_ua": sub(rb'"user_agent": "[^"]*"', b'"user_agent": "x"'),
+    "ua_110_ascii": sub(rb'"user_agent": "[^"]*"', b'"user_agent": "' + b"a" * 110 + b'"'),
+    "ua_no_escapes": [m.replace(b"\\u00e9\\u4e2d", b"ee") for m in base],
     "no_locations": sub(rb', "(geolocation|merchant_location)": \{[^}]*\}', b''),
     "no_unknown": sub(rb', "(currency|card_last_four|device_id|fraud_type|processing_time_ms)": ("[^"]*"|null|\d+)', b''),
     "no_timestamp_str": sub(rb'"timestamp": "[^"]*"', b'"timestamp": "2025-09-05T00:00:00"'),
