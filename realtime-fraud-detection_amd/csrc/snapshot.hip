@@ -519,6 +519,10 @@ void state_restore(Engine& e, const char* path, int shard, int n_shards, int fla
   } else if (has_events && !skip_windows) {
     // windows_present == 0 but events recorded: corrupt
     throw Error(FD_ERR_IO, "restore: corrupt header (window events without window state)");
+  } else if (has_events) {
+    // skipped window logs: step over them so the extension sections that follow are read in place
+    const long skip = (long)((hd.ucount + hd.mcount) * (int64_t)kWinEventBytes);
+    FD_REQUIRE(std::fseek(in.f, skip, SEEK_CUR) == 0, FD_ERR_IO, "restore: truncated snapshot (window logs)");
   }
   // extension sections
   if (hd.ext_flags) {
