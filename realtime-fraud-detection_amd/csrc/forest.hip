@@ -710,6 +710,98 @@ __device__ __forceinline__ void walk4(uint32_t buf, int gg, uint32_t lane4, uint
   for (int j = 0; j < TPG; ++j) slot[j] = ((P[j] - tb[j]) >> 3) - NL;  // leaf heap slot - 2^D
 }
 
+// walk4 with the top three levels taken from registers: `top` holds heap slots 0-7 (the root, its two
+// children and four grandchildren) of each chain's tree, loaded from global memory one chunk ahead
+// (uniform 32-B vector loads, no LDS traffic), so levels 0-2 issue only the feature read and select
+// the next node with v_cndmask; the first children-pair read is that of the level-2 node. Per tree
+// this drops 3 of walk4's 16 LDS reads (the root word and the two top children pairs). Measured
+// SLOWER on config 2 (103.6 vs 87.6 us, tools/forest_sweep.py, interleaved): the walk is bound by
+// issue / latency, not by LDS cycles, and the register selects add VALU work. Kept as option 7 (A/B).
+template <int D, int TPG, typename LeafT, bool NAN_AWARE>
+__device__ __forceinline__ void walk4t(uint32_t buf, int gg, uint32_t lane4, const uint32_t (&top)[TPG][8],
+                                       uint32_t (&slot)[TPG]) {
+  static_assert(D >= 3, "walk4t needs three levels");
+  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
+  constexpr uint32_t NL = 1u << D;
+  uint32_t tb[TPG], c0[TPG], c8[TPG], P[TPG], node[TPG], kl[TPG], kr[TPG], xw[TPG];
+  bool r0[TPG];
+  auto go_right = [](uint32_t x, uint32_t nd) {
+    bool right = x > nd;  // bin > j  <=>  !(x < t_j)
+    if (NAN_AWARE) {
+      if (x == 0xFFFF0000u) right = (nd & 1u) == 0u;  // missing: default direction
+    }
+    return right;
+  };
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) {
+    tb[j] = buf + (uint32_t)(gg * TPG + j) * TB;
+    c0[j] = 0u - tb[j];
+    c8[j] = 8u - tb[j];
+    asm volatile("" : "+v"(c0[j]), "+v"(c8[j]));
+    node[j] = top[j][1];
+    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+  }
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) {  // level 0 -> slot 2 + r0
+    r0[j] = go_right(xw[j], node[j]);
+    node[j] = r0[j] ? top[j][3] : top[j][2];
+    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+  }
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) {  // level 1 -> slot 4 + 2 r0 + r1
+    const bool r1 = go_right(xw[j], node[j]);
+    const uint32_t lo = r1 ? top[j][5] : top[j][4], hi = r1 ? top[j][7] : top[j][6];
+    node[j] = r0[j] ? hi : lo;
+    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+    P[j] = tb[j] + 8u * (4u + (r0[j] ? 2u : 0u) + (r1 ? 1u : 0u));  // children pair of the level-2 node
+    if (D > 3) {
+      const u32x2 k = lds_load<u32x2>(P[j]);
+      kl[j] = k.x;
+      kr[j] = k.y;
+    }
+  }
+#pragma unroll
+  for (int l = 2; l < D; ++l) {
+#pragma unroll
+    for (int j = 0; j < TPG; ++j) {
+      const bool right = go_right(xw[j], node[j]);
+      P[j] = (P[j] << 1) + (right ? c8[j] : c0[j]);
+      if (l + 1 < D) {
+        uint32_t a = kl[j], b = kr[j];
+        asm volatile("" : "+v"(a), "+v"(b));
+        node[j] = right ? b : a;
+        xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+        if (l + 2 < D) {
+          const u32x2 k = lds_load<u32x2>(P[j]);
+          kl[j] = k.x;
+          kr[j] = k.y;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) slot[j] = ((P[j] - tb[j]) >> 3) - NL;  // leaf heap slot - 2^D
+}
+
+// heap slots 0-7 of the TPG trees a tree group walks in chunk k (global blob; global vector loads so
+// that they are counted by vmcnt only and never hold up the LDS pipeline's lgkmcnt waits). Loaded one
+// chunk ahead into VGPRs, moved to SGPRs (readfirstlane: the values are wave-uniform) when consumed.
+template <int TPG, typename LeafT, int D>
+__device__ __forceinline__ void load_top(const char* __restrict__ blob, int k, int chunk_stride, int gg,
+                                         uint32_t (&top)[TPG][8]) {
+  constexpr size_t TB = (4u + sizeof(LeafT)) << D;
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) {
+    uint64_t a = (uint64_t)(blob + (size_t)k * chunk_stride + (size_t)(gg * TPG + j) * TB);
+    asm volatile("" : "+v"(a));  // a per-lane (VGPR) address: a vector load, not s_load
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const __attribute__((address_space(1))) v4u* g = (const __attribute__((address_space(1))) v4u*)a;
+    const v4u x = g[0], y = g[1];
+    top[j][0] = x.x; top[j][1] = x.y; top[j][2] = x.z; top[j][3] = x.w;
+    top[j][4] = y.x; top[j][5] = y.y; top[j][6] = y.z; top[j][7] = y.w;
+  }
+}
+
 // bin(v) = #{t in tbl[0, cnt) : t <= v}, tbl ascending; steps = largest power of two <= max count.
 template <bool IN_LDS>
 __device__ __forceinline__ uint32_t bin_of(float v, const float* __restrict__ gt, uint32_t lt, int cnt, int steps) {
@@ -724,7 +816,7 @@ __device__ __forceinline__ uint32_t bin_of(float v, const float* __restrict__ gt
   return (uint32_t)pos;
 }
 
-template <int D, int CH, typename LeafT, int KIND>
+template <int D, int CH, typename LeafT, int KIND, bool TOP>
 __global__ void __launch_bounds__(kWG3)
 forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
                int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
@@ -733,6 +825,7 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
                double* __restrict__ out_raw, int32_t* __restrict__ out_leaf) {
   constexpr int TPG = CH / 4;
   constexpr int NL = 1 << D;
+  constexpr bool kTop = TOP && D >= 3;  // walk4t: top three levels from registers
   constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
@@ -755,6 +848,8 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
   FD_PROF_T(p_t0);
 
   stage_chunk_asm(blob, bufA, chunk_stride, kWG3 / 64);  // chunk 0 lands while the tile is binned
+  uint32_t topc[kTop ? TPG : 1][8], topn[kTop ? TPG : 1][8];
+  if constexpr (kTop) load_top<TPG, LeafT, D>(blob, 0, chunk_stride, gg, topn);
   // threshold tables: into LDS over bufB + lv (dead until chunk 1 / the first leaf store) if they fit
   const int n_thr = thr_off[nf];
   const bool tbl_lds = (uint32_t)n_thr * 4u <= accL - bufB;
@@ -797,8 +892,17 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
   for (int k = 0; k < n_chunks; ++k) {
     FD_PROF_T(q0);
     const uint32_t cur = (k & 1) ? bufB : bufA;
+    if constexpr (kTop) {  // chunk k's top levels (loaded during chunk k-1; complete after its dma_wait)
+#pragma unroll
+      for (int j = 0; j < TPG; ++j)
+#pragma unroll
+        for (int u = 1; u < 8; ++u) topc[j][u] = __builtin_amdgcn_readfirstlane(topn[j][u]);
+    }
     if (k + 1 < n_chunks)
       stage_chunk_asm(blob + (size_t)(k + 1) * chunk_stride, (k & 1) ? bufA : bufB, chunk_stride, kWG3 / 64);
+    if constexpr (kTop) {
+      if (k + 1 < n_chunks) load_top<TPG, LeafT, D>(blob, k + 1, chunk_stride, gg, topn);
+    }
     if (k > 0 && gg == ((k - 1) & 3)) {  // owner of chunk k-1 adds its leaf values in tree order
       const uint32_t lv = ((k - 1) & 1) ? lvB : lvA;
       LeafT acc = lds_load<LeafT>(accL + txn * sizeof(LeafT));
@@ -808,10 +912,17 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
     }
     FD_PROF_T(q1);
     uint32_t slots[TPG];
-    if (tile_nan)
-      walk4<D, TPG, LeafT, true>(cur, gg, lane4, slots);
-    else
-      walk4<D, TPG, LeafT, false>(cur, gg, lane4, slots);
+    if constexpr (kTop) {
+      if (tile_nan)
+        walk4t<D, TPG, LeafT, true>(cur, gg, lane4, topc, slots);
+      else
+        walk4t<D, TPG, LeafT, false>(cur, gg, lane4, topc, slots);
+    } else {
+      if (tile_nan)
+        walk4<D, TPG, LeafT, true>(cur, gg, lane4, slots);
+      else
+        walk4<D, TPG, LeafT, false>(cur, gg, lane4, slots);
+    }
 #ifdef FD_FOREST_PROFILE
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -1278,30 +1389,36 @@ KernelFn pick3(int D, int CH) {
 using KernelFn4 = void (*)(const float*, int64_t, int, int, const char*, int, int, const int32_t*, int,
                            const float*, const int32_t*, int, float, double, double, double*, double*, int32_t*);
 
-template <typename LeafT, int KIND, int CH>
+template <typename LeafT, int KIND, int CH, bool TOP>
 KernelFn4 pick4_ch(int D) {
   switch (D) {
-    case 1: return forest_kernel4<1, CH, LeafT, KIND>;
-    case 2: return forest_kernel4<2, CH, LeafT, KIND>;
-    case 3: return forest_kernel4<3, CH, LeafT, KIND>;
-    case 4: return forest_kernel4<4, CH, LeafT, KIND>;
-    case 5: return forest_kernel4<5, CH, LeafT, KIND>;
-    case 6: return forest_kernel4<6, CH, LeafT, KIND>;
-    case 7: return forest_kernel4<7, CH, LeafT, KIND>;
-    case 8: return forest_kernel4<8, CH, LeafT, KIND>;
+    case 1: return forest_kernel4<1, CH, LeafT, KIND, TOP>;
+    case 2: return forest_kernel4<2, CH, LeafT, KIND, TOP>;
+    case 3: return forest_kernel4<3, CH, LeafT, KIND, TOP>;
+    case 4: return forest_kernel4<4, CH, LeafT, KIND, TOP>;
+    case 5: return forest_kernel4<5, CH, LeafT, KIND, TOP>;
+    case 6: return forest_kernel4<6, CH, LeafT, KIND, TOP>;
+    case 7: return forest_kernel4<7, CH, LeafT, KIND, TOP>;
+    case 8: return forest_kernel4<8, CH, LeafT, KIND, TOP>;
     default: return nullptr;
   }
 }
 
-template <typename LeafT, int KIND>
-KernelFn4 pick4(int D, int CH) {
+template <typename LeafT, int KIND, bool TOP>
+KernelFn4 pick4_top(int D, int CH) {
   switch (CH) {
-    case 4: return pick4_ch<LeafT, KIND, 4>(D);
-    case 8: return pick4_ch<LeafT, KIND, 8>(D);
-    case 12: return pick4_ch<LeafT, KIND, 12>(D);
-    case 16: return pick4_ch<LeafT, KIND, 16>(D);
+    case 4: return pick4_ch<LeafT, KIND, 4, TOP>(D);
+    case 8: return pick4_ch<LeafT, KIND, 8, TOP>(D);
+    case 12: return pick4_ch<LeafT, KIND, 12, TOP>(D);
+    case 16: return pick4_ch<LeafT, KIND, 16, TOP>(D);
     default: return nullptr;
   }
+}
+
+// top: walk4t (top three levels from registers; option 7, A/B only) or the plain walk4 (the default)
+template <typename LeafT, int KIND>
+KernelFn4 pick4(int D, int CH, bool top) {
+  return top ? pick4_top<LeafT, KIND, true>(D, CH) : pick4_top<LeafT, KIND, false>(D, CH);
 }
 
 template <typename LeafT, int KIND, int CH>
@@ -1419,7 +1536,8 @@ extern "C" __attribute__((visibility("default"))) int fd_debug_forest_profile(un
 
 // Kernel choice (option "forest_kernel"): 0 auto = kernel 4 when the binned layout exists (depth <= 8,
 // <= 65534 distinct thresholds per feature), else kernel 3 (depth <= 8), else kernel 1; 1/2/3 force
-// kernel 1/3/4, 4/5 force kernel 5 (plain / speculative-children walk), 6 forces the tree-split
+// kernel 1/3/4 (7: kernel 4 with walk4t, A/B only), 4/5 force kernel 5 (plain /
+// speculative-children walk), 6 forces the tree-split
 // small-batch path, which auto also takes below kSplitTiles tiles (FD_ERR_UNSUPPORTED when the forest
 // cannot use it).
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
@@ -1431,7 +1549,7 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   const int64_t blocks = (n + kTile - 1) / kTile;
   FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
   const int v = e.forest_variant;
-  FD_REQUIRE(v >= 0 && v <= 6, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..6");
+  FD_REQUIRE(v >= 0 && v <= 7, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..7");
   Engine::Timed* ev = nullptr;
 
   // small batches: tree-split latency path (option 6 forces it; auto below 128 tiles)
@@ -1472,10 +1590,10 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
 
   const size_t lds4 = pf.binned ? lds_bytes_kernel4(pf.num_feature, pf.b_chunk_stride, pf.b_chunk, leaf_sz) : 0;
   const bool ok4 = pf.binned && pf.depth <= 8 && pf.b_chunk % 4 == 0 && lds4 <= kLdsBudget;
-  if (v == 3) FD_REQUIRE(ok4, FD_ERR_UNSUPPORTED, "forest kernel 4 needs the binned layout (depth <= 8)");
-  if ((v == 0 || v == 3) && ok4) {
-    KernelFn4 fn = xgb ? pick4<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.b_chunk)
-                       : pick4<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.b_chunk);
+  if (v == 3 || v == 7) FD_REQUIRE(ok4, FD_ERR_UNSUPPORTED, "forest kernel 4 needs the binned layout (depth <= 8)");
+  if ((v == 0 || v == 3 || v == 7) && ok4) {
+    KernelFn4 fn = xgb ? pick4<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.b_chunk, v == 7)
+                       : pick4<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.b_chunk, v == 7);
     FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel 4 for this depth/chunk");
     FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4));
     ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
