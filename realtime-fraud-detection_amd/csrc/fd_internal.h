@@ -95,6 +95,12 @@ struct PackedForest {
   DeviceBuffer b_thr;      // distinct thresholds, feature-major ascending (f32)
   DeviceBuffer b_thr_off;  // num_feature + 1 offsets (int32)
   int b_n_thr = 0;         // distinct thresholds in b_thr
+  // node-only chunks of the binned layout (forest_kernel6): CH trees' node words per chunk, leaf
+  // values in a separate [tree][2^D] array read from global memory
+  int n_chunk = 0, n_n_chunks = 0;
+  size_t n_chunk_stride = 0;
+  DeviceBuffer n_blob;    // n_n_chunks * n_chunk_stride
+  DeviceBuffer n_leaves;  // n_n_chunks * n_chunk * 2^D leaf values (f32 XGBoost / f64 IsolationForest)
   mutable SplitScratch split;
 };
 
@@ -224,6 +230,10 @@ struct HostPack {
   std::vector<int32_t> b_thr_off;
   int b_chunk = 0, b_n_chunks = 0, bin_steps = 0;
   size_t b_tree_bytes = 0, b_chunk_stride = 0;
+  // node-only chunks (forest_kernel6); n_chunk == 0 when no supported chunk size fits
+  std::vector<char> n_blob, n_leaves;
+  int n_chunk = 0, n_n_chunks = 0;
+  size_t n_chunk_stride = 0;
 };
 HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t);
 void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);

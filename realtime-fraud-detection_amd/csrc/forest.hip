@@ -223,6 +223,26 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
       hp.leaf_ids[(size_t)i * NL + s] = o;
     }
   }
+  if (binnable) {  // node-only chunks for forest_kernel6: the largest supported CH whose LDS image fits
+    for (int ch : {32, 24, 16})
+      if (lds_bytes_kernel3(nf, round1k((size_t)ch * NL * 4), ch, leaf_sz) <= kLdsBudget) {
+        hp.n_chunk = ch;
+        break;
+      }
+    if (hp.n_chunk) {
+      const int NC = hp.n_chunk;
+      hp.n_chunk_stride = round1k((size_t)NC * NL * 4);
+      hp.n_n_chunks = (T + NC - 1) / NC;
+      hp.n_blob.assign((size_t)hp.n_n_chunks * hp.n_chunk_stride, 0);
+      hp.n_leaves.assign((size_t)hp.n_n_chunks * NC * NL * leaf_sz, 0);  // padding trees: zero leaves
+      for (int i = 0; i < T; ++i) {
+        const char* btb = hp.b_blob.data() + (size_t)(i / BCH) * hp.b_chunk_stride + (size_t)(i % BCH) * b_tree_bytes;
+        std::memcpy(hp.n_blob.data() + (size_t)(i / NC) * hp.n_chunk_stride + (size_t)(i % NC) * NL * 4, btb,
+                    (size_t)NL * 4);
+        std::memcpy(hp.n_leaves.data() + (size_t)i * NL * leaf_sz, btb + (size_t)NL * 4, (size_t)NL * leaf_sz);
+      }
+    }
+  }
   hp.kind = p.kind;
   hp.n_trees = T;
   hp.n_chunks = n_chunks;
@@ -274,6 +294,13 @@ void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_ar
     pf.b_chunk_stride = hp.b_chunk_stride;
     pf.bin_steps = hp.bin_steps;
     pf.b_n_thr = (int)hp.b_thr.size();
+    pf.n_chunk = hp.n_chunk;
+    pf.n_n_chunks = hp.n_n_chunks;
+    pf.n_chunk_stride = hp.n_chunk_stride;
+    if (hp.n_chunk) {
+      upload(pf.n_blob, hp.n_blob);
+      upload(pf.n_leaves, hp.n_leaves);
+    }
   }
   pf.loaded = true;
 }
@@ -657,9 +684,10 @@ forest_kernel3(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 // word(x) <= node, the feature-row address is (node & 0xFC00) | lane, and a node's two children are
 // one 8-byte pair read: per level one ds_read_b32 (feature) and one ds_read_b64 (children).
 
-template <int D, int TPG, typename LeafT, bool NAN_AWARE>
+template <int D, int TPG, typename LeafT, bool NAN_AWARE, bool NODE_ONLY = false>
 __device__ __forceinline__ void walk4(uint32_t buf, int gg, uint32_t lane4, uint32_t (&slot)[TPG]) {
-  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
+  // tree stride in the staged chunk: node words + leaf values, or node words only (kernel 6)
+  constexpr uint32_t TB = NODE_ONLY ? (4u << D) : (4u + (uint32_t)sizeof(LeafT)) << D;
   constexpr uint32_t NL = 1u << D;
   // P = LDS address of the children pair of the current node (heap slot i: tb + 8 i). Chosen child
   // c = 2i + r has its pair at tb + 8c = 2P - tb + 8r = (P << 1) + (r ? 8 - tb : -tb).
@@ -934,6 +962,147 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
       const uint32_t tb = cur + (uint32_t)c * TB;
       lds_store<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT),
                        lds_load<LeafT>(tb + NL * 4u + slots[j] * sizeof(LeafT)));
+      if (out_leaf != nullptr && valid) {
+        const int tg = k * CH + c;
+        if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slots[j]];
+      }
+    }
+    FD_PROF_T(q3);
+    dma_wait();
+    __syncthreads();  // chunk k+1 landed; lv[k&1] complete; owner of k-1 done with lv[(k-1)&1]
+    FD_PROF_T(q4);
+    FD_PROF_ADD(p_own, q0, q1);
+    FD_PROF_ADD(p_walk, q1, q2);
+    FD_PROF_ADD(p_leaf, q2, q3);
+    FD_PROF_ADD(p_sync, q3, q4);
+  }
+#ifdef FD_FOREST_PROFILE
+  if (lane == 0 && blockIdx.x < 256) {
+    FD_PROF_T(p_t2);
+    unsigned long long* o = g_prof + ((size_t)blockIdx.x * 16 + wave) * 8;
+    o[0] = p_t1 - p_t0; o[1] = p_walk; o[2] = p_leaf; o[3] = p_own; o[4] = p_sync; o[5] = p_t2 - p_t0;
+    o[6] = p_t0; o[7] = 0;
+  }
+#endif
+  const int last = n_chunks - 1;
+  if (gg != (last & 3)) return;
+  LeafT acc = lds_load<LeafT>(accL + txn * sizeof(LeafT));
+  {
+    const uint32_t lv = (last & 1) ? lvB : lvA;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) acc += lds_load<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT));
+  }
+  if (valid) write_outputs<KIND, LeafT>(acc, row, if_offset, if_denom, out_prob, out_raw);
+}
+
+// ------------------------------------------------------------------------------------------------
+// forest_kernel6 (depth <= 8, binned nodes): kernel 4 with node-only chunks. The staged chunk holds
+// only the CH trees' node words (1 KiB per depth-8 tree instead of 2-3 KiB with the leaves), so the
+// same LDS budget stages more trees per chunk: CH = 24 for XGBoost (TPG = 6 independent walks per
+// wave instead of 4) and 16 for the f64-leaf IsolationForest (instead of 8). The walk is bound by the
+// LDS round-trip latency of its dependent chains, not by LDS cycles (PMC: LDS array ~50 % busy, VALU
+// ~35 %), so more chains per wave is the lever. After the walk each lane reads its TPG leaf values
+// from the global [tree][2^D] array (L2-resident: 0.5 MiB for 500 x depth 8) with all loads in
+// flight together; the owner pass and the tree-order sum are kernel 4's.
+template <int D, int CH, typename LeafT, int KIND>
+__global__ void __launch_bounds__(kWG3)
+forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
+               int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
+               const float* __restrict__ thr, const int32_t* __restrict__ thr_off, int bin_steps,
+               float base_margin, double if_offset, double if_denom, double* __restrict__ out_prob,
+               double* __restrict__ out_raw, int32_t* __restrict__ out_leaf, const LeafT* __restrict__ leaves) {
+  constexpr int TPG = CH / 4;
+  constexpr int NL = 1 << D;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
+  const uint32_t s0 = (sdyn + 1023u) & ~1023u;
+  char* const lbase = smem + (s0 - sdyn);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int gg = wave >> 2;
+  const int txn = ((wave & 3) << 6) + lane;
+  const uint32_t lane4 = s0 + (uint32_t)txn * 4u;
+  const uint32_t xbytes = (uint32_t)nf * 1024u;
+  const uint32_t bufA = s0 + xbytes, bufB = bufA + (uint32_t)chunk_stride;
+  const uint32_t lvA = bufB + (uint32_t)chunk_stride;
+  const uint32_t lvB = lvA + CH * kTile * sizeof(LeafT);
+  const uint32_t accL = lvB + CH * kTile * sizeof(LeafT);
+  const int64_t row = (int64_t)blockIdx.x * kTile + txn;
+  const bool valid = row < n;
+#ifdef FD_FOREST_PROFILE
+  unsigned long long p_walk = 0, p_leaf = 0, p_own = 0, p_sync = 0;
+#endif
+  FD_PROF_T(p_t0);
+
+  stage_chunk_asm(blob, bufA, chunk_stride, kWG3 / 64);  // chunk 0 lands while the tile is binned
+  // threshold tables: into LDS over bufB + lv (dead until chunk 1 / the first leaf store) if they fit
+  const int n_thr = thr_off[nf];
+  const bool tbl_lds = (uint32_t)n_thr * 4u <= accL - bufB;
+  if (tbl_lds) {
+    float* tl = reinterpret_cast<float*>(lbase + (bufB - s0));
+    for (int i = tid; i < n_thr; i += kWG3) tl[i] = thr[i];
+    __syncthreads();
+  }
+  int anynan = 0;
+  const int ncopy = ld < nf ? ld : nf;
+  {
+    const int q = tid >> 8;  // the four threads sharing `txn` bin every 4th column
+    uint32_t* Xs = reinterpret_cast<uint32_t*>(lbase);
+    const float* xr = X + row * (int64_t)ld;
+    for (int f = q; f < nf; f += 4) {
+      uint32_t w = 0;
+      if (valid) {
+        const float v = f < ncopy ? xr[f] : __builtin_nanf("");  // DMatrix: missing column = NaN
+        if (v != v) {
+          w = 0xFFFF0000u;
+          anynan = 1;
+        } else {
+          const int o = thr_off[f], cnt = thr_off[f + 1] - o;
+          const uint32_t b = tbl_lds ? bin_of<true>(v, nullptr, bufB + (uint32_t)o * 4u, cnt, bin_steps)
+                                     : bin_of<false>(v, thr + o, 0u, cnt, bin_steps);
+          w = b << 16;
+        }
+      }
+      Xs[f * kTile + txn] = w;
+    }
+    if (gg == 0)
+      lds_store<LeafT>(accL + txn * sizeof(LeafT),
+                       (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0);
+  }
+  dma_wait();  // chunk 0 (published by tile_any's barrier)
+  const bool tile_nan =
+      tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (accL - s0) + kTile * sizeof(LeafT)), kWG3 / 64);
+  FD_PROF_T(p_t1);
+
+  for (int k = 0; k < n_chunks; ++k) {
+    FD_PROF_T(q0);
+    const uint32_t cur = (k & 1) ? bufB : bufA;
+    if (k + 1 < n_chunks)
+      stage_chunk_asm(blob + (size_t)(k + 1) * chunk_stride, (k & 1) ? bufA : bufB, chunk_stride, kWG3 / 64);
+    if (k > 0 && gg == ((k - 1) & 3)) {  // owner of chunk k-1 adds its leaf values in tree order
+      const uint32_t lv = ((k - 1) & 1) ? lvB : lvA;
+      LeafT acc = lds_load<LeafT>(accL + txn * sizeof(LeafT));
+#pragma unroll
+      for (int c = 0; c < CH; ++c) acc += lds_load<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT));
+      lds_store<LeafT>(accL + txn * sizeof(LeafT), acc);
+    }
+    FD_PROF_T(q1);
+    uint32_t slots[TPG];
+    if (tile_nan)
+      walk4<D, TPG, LeafT, true, true>(cur, gg, lane4, slots);
+    else
+      walk4<D, TPG, LeafT, false, true>(cur, gg, lane4, slots);
+#ifdef FD_FOREST_PROFILE
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    FD_PROF_T(q2);
+    const uint32_t lv = (k & 1) ? lvB : lvA;
+    LeafT lval[TPG];  // leaf values from global memory (L2-resident), all TPG loads in flight together
+#pragma unroll
+    for (int j = 0; j < TPG; ++j) lval[j] = leaves[((size_t)k * CH + gg * TPG + j) * NL + slots[j]];
+#pragma unroll
+    for (int j = 0; j < TPG; ++j) {
+      const int c = gg * TPG + j;
+      lds_store<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT), lval[j]);
       if (out_leaf != nullptr && valid) {
         const int tg = k * CH + c;
         if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slots[j]];
@@ -1484,6 +1653,35 @@ void* pick_split(int D, int CH) {
   }
 }
 
+using KernelFn6 = void (*)(const float*, int64_t, int, int, const char*, int, int, const int32_t*, int,
+                           const float*, const int32_t*, int, float, double, double, double*, double*, int32_t*,
+                           const void*);
+
+template <typename LeafT, int KIND, int CH>
+KernelFn6 pick6_ch(int D) {
+  switch (D) {
+    case 1: return (KernelFn6)forest_kernel6<1, CH, LeafT, KIND>;
+    case 2: return (KernelFn6)forest_kernel6<2, CH, LeafT, KIND>;
+    case 3: return (KernelFn6)forest_kernel6<3, CH, LeafT, KIND>;
+    case 4: return (KernelFn6)forest_kernel6<4, CH, LeafT, KIND>;
+    case 5: return (KernelFn6)forest_kernel6<5, CH, LeafT, KIND>;
+    case 6: return (KernelFn6)forest_kernel6<6, CH, LeafT, KIND>;
+    case 7: return (KernelFn6)forest_kernel6<7, CH, LeafT, KIND>;
+    case 8: return (KernelFn6)forest_kernel6<8, CH, LeafT, KIND>;
+    default: return nullptr;
+  }
+}
+
+template <typename LeafT, int KIND>
+KernelFn6 pick6(int D, int CH) {
+  switch (CH) {
+    case 16: return pick6_ch<LeafT, KIND, 16>(D);
+    case 24: return pick6_ch<LeafT, KIND, 24>(D);
+    case 32: return pick6_ch<LeafT, KIND, 32>(D);
+    default: return nullptr;
+  }
+}
+
 // small-batch launch: bin once, walk (tiles x chunk groups), sequential sum
 template <typename LeafT, int KIND>
 void launch_split(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld, double* d_prob,
@@ -1534,8 +1732,10 @@ extern "C" __attribute__((visibility("default"))) int fd_debug_forest_profile(un
 }
 #endif
 
-// Kernel choice (option "forest_kernel"): 0 auto = kernel 4 when the binned layout exists (depth <= 8,
-// <= 65534 distinct thresholds per feature), else kernel 3 (depth <= 8), else kernel 1; 1/2/3 force
+// Kernel choice (option "forest_kernel"): 0 auto = kernel 6 when the binned node-only layout exists
+// (depth <= 8, <= 65534 distinct thresholds per feature; config 2: 84.1 vs kernel 4's 88.2 us, config-3
+// IsolationForest 38.1 vs 38.7 us, tools/forest_sweep.py), else kernel 4 (binned), else kernel 3
+// (depth <= 8), else kernel 1; 8 forces kernel 6; 1/2/3 force
 // kernel 1/3/4 (7: kernel 4 with walk4t, A/B only), 4/5 force kernel 5 (plain /
 // speculative-children walk), 6 forces the tree-split
 // small-batch path, which auto also takes below kSplitTiles tiles (FD_ERR_UNSUPPORTED when the forest
@@ -1549,7 +1749,7 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   const int64_t blocks = (n + kTile - 1) / kTile;
   FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
   const int v = e.forest_variant;
-  FD_REQUIRE(v >= 0 && v <= 7, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..7");
+  FD_REQUIRE(v >= 0 && v <= 8, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..8");
   Engine::Timed* ev = nullptr;
 
   // small batches: tree-split latency path (option 6 forces it; auto below 128 tiles)
@@ -1583,6 +1783,26 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
                        pf.leaf_ids.as<const int32_t>(), pf.n_trees, pf.b_thr.as<const float>(),
                        pf.b_thr_off.as<const int32_t>(), pf.bin_steps, pf.base_margin, pf.if_offset,
                        pf.if_denominator, d_prob, d_raw, d_leaf);
+    FD_HIP(hipGetLastError());
+    if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
+    return;
+  }
+
+  const size_t lds6 = pf.n_chunk ? lds_bytes_kernel3(pf.num_feature, pf.n_chunk_stride, pf.n_chunk, leaf_sz) : 0;
+  const bool ok6 = pf.binned && pf.n_chunk > 0 && pf.depth <= 8 && lds6 <= kLdsBudget;
+  if (v == 8) FD_REQUIRE(ok6, FD_ERR_UNSUPPORTED, "forest kernel 6 needs the binned node-only layout (depth <= 8)");
+  if ((v == 0 || v == 8) && ok6) {
+    KernelFn6 fn = xgb ? pick6<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.n_chunk)
+                       : pick6<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.n_chunk);
+    FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel 6 for this depth/chunk");
+    FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds6));
+    ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
+    if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
+    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kWG3), lds6, e.stream, d_X, n, (int)ld, pf.num_feature,
+                       pf.n_blob.as<const char>(), pf.n_n_chunks, (int)pf.n_chunk_stride,
+                       pf.leaf_ids.as<const int32_t>(), pf.n_trees, pf.b_thr.as<const float>(),
+                       pf.b_thr_off.as<const int32_t>(), pf.bin_steps, pf.base_margin, pf.if_offset,
+                       pf.if_denominator, d_prob, d_raw, d_leaf, (const void*)pf.n_leaves.ptr);
     FD_HIP(hipGetLastError());
     if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
     return;

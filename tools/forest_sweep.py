@@ -18,7 +18,11 @@ B = int(os.environ.get("B", 65536)); F = 50; T = int(os.environ.get("T", 500)); 
 variants = [int(v) for v in os.environ.get("VARIANTS", "1,2").split(",")]
 rounds, reps = 5, 20
 X = synth.feature_matrix(4 * B, F, seed=1000)
-forest = fdengine.xgboost_from_json_doc(synth.xgboost_doc(T, D, F, synth.feature_matrix(2048, F, seed=7), seed=8))
+if os.environ.get("IF"):  # the config-3 IsolationForest (100 trees, max_samples 256, f64 leaves)
+    forest = fdengine.iforest_from_sklearn(
+        synth.isolation_forest(synth.feature_matrix(20000, F, seed=7).astype(np.float64), n_estimators=100))
+else:
+    forest = fdengine.xgboost_from_json_doc(synth.xgboost_doc(T, D, F, synth.feature_matrix(2048, F, seed=7), seed=8))
 eng = fdengine.FraudEngine(0)
 eng.load_forest(0, forest)
 print("forest", eng.forest_info(0))
@@ -38,7 +42,7 @@ for r in range(rounds):
             eng.predict_device(0, dX.data_ptr() + (i % 4) * B * F * 4, B, F, dp.data_ptr() + (i % 4) * B * 8)
         torch.cuda.synchronize()
         eng.set_timing(False)
-        ms, n = eng.read_timing(0)
+        ms, n = eng.read_timing(1 if os.environ.get("IF") else 0)
         res[v].append(ms / n * 1e3)
         out = dp[:B].cpu().numpy()
         if ref is None:
