@@ -801,6 +801,18 @@ class Config3J(Config3):
             out["ingest_json"] = round(ms / c * 1e3, 3)
         return out
 
+    def roofline(self, timing):
+        """The dominant kernel of this line is the JSON codec (≈1.1 ms of the ≈1.35 ms step), not the forest."""
+        ms, launches = timing[self.N.FD_TIMING_INGEST]
+        avg = (ms / 1e3) / max(1, launches)
+        per_launch = self.nbytes[0] + 8 * (self.B + 1) + Ingest.OUT_BYTES * self.B
+        achieved = per_launch / avg / 1e9
+        return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(self.name, self.B),
+                "kernel": "ingest_json_kernel (wave per message, LDS-staged; dominant)",
+                "kernel_avg_us": round(avg * 1e6, 3), "algorithmic_bytes_per_launch": per_launch,
+                "bytes_per_txn": round(per_launch / self.B, 1)}
+
     def config(self, world):
         d = super().config(world)
         d["workload"] = ("config3j: config3 fed from the wire format — 64k raw Kafka JSON messages per micro-batch "
