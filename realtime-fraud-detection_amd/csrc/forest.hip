@@ -738,6 +738,55 @@ __device__ __forceinline__ void walk4(uint32_t buf, int gg, uint32_t lane4, uint
   for (int j = 0; j < TPG; ++j) slot[j] = ((P[j] - tb[j]) >> 3) - NL;  // leaf heap slot - 2^D
 }
 
+// walk4 over G independently chosen (tree, transaction group) items: per-chain tree base tb[j] and
+// feature-row lane address l4[j] (forest_kernel6's dynamic item loop).
+template <int D, int G, bool NAN_AWARE>
+__device__ __forceinline__ void walk4d(const uint32_t (&tb)[G], const uint32_t (&l4)[G], uint32_t (&slot)[G]) {
+  constexpr uint32_t NL = 1u << D;
+  uint32_t c0[G], c8[G], P[G], node[G], kl[G], kr[G], xw[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    c0[j] = 0u - tb[j];
+    c8[j] = 8u - tb[j];
+    asm volatile("" : "+v"(c0[j]), "+v"(c8[j]));
+    node[j] = lds_load<uint32_t>(tb[j] + 4u);
+    P[j] = tb[j] + 8u;
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | l4[j]);
+    if (D > 1) {
+      const u32x2 k = lds_load<u32x2>(P[j]);
+      kl[j] = k.x;
+      kr[j] = k.y;
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < D; ++l) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      bool right = xw[j] > node[j];
+      if (NAN_AWARE) {
+        if (xw[j] == 0xFFFF0000u) right = (node[j] & 1u) == 0u;
+      }
+      P[j] = (P[j] << 1) + (right ? c8[j] : c0[j]);
+      if (l + 1 < D) {
+        uint32_t a = kl[j], b = kr[j];
+        asm volatile("" : "+v"(a), "+v"(b));
+        node[j] = right ? b : a;
+        xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | l4[j]);
+        if (l + 2 < D) {
+          const u32x2 k = lds_load<u32x2>(P[j]);
+          kl[j] = k.x;
+          kr[j] = k.y;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) slot[j] = ((P[j] - tb[j]) >> 3) - NL;
+}
+
 // walk4 with the top three levels taken from registers: `top` holds heap slots 0-7 (the root, its two
 // children and four grandchildren) of each chain's tree, loaded from global memory one chunk ahead
 // (uniform 32-B vector loads, no LDS traffic), so levels 0-2 issue only the feature read and select
@@ -1004,7 +1053,7 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 // ~35 %), so more chains per wave is the lever. After the walk each lane reads its TPG leaf values
 // from the global [tree][2^D] array (L2-resident: 0.5 MiB for 500 x depth 8) with all loads in
 // flight together; the owner pass and the tree-order sum are kernel 4's.
-template <int D, int CH, typename LeafT, int KIND>
+template <int D, int CH, typename LeafT, int KIND, bool DYN>
 __global__ void __launch_bounds__(kWG3)
 forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
                int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
@@ -1068,6 +1117,9 @@ forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
       lds_store<LeafT>(accL + txn * sizeof(LeafT),
                        (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0);
   }
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  lds_u32* const ctr = (lds_u32*)(size_t)(accL + kTile * (uint32_t)sizeof(LeafT) + 64u);  // 2 item counters
+  if (DYN && tid == 0) ctr[0] = 0u;
   dma_wait();  // chunk 0 (published by tile_any's barrier)
   const bool tile_nan =
       tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (accL - s0) + kTile * sizeof(LeafT)), kWG3 / 64);
@@ -1086,28 +1138,69 @@ forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
       lds_store<LeafT>(accL + txn * sizeof(LeafT), acc);
     }
     FD_PROF_T(q1);
-    uint32_t slots[TPG];
-    if (tile_nan)
-      walk4<D, TPG, LeafT, true, true>(cur, gg, lane4, slots);
-    else
-      walk4<D, TPG, LeafT, false, true>(cur, gg, lane4, slots);
+    if constexpr (DYN) {
+      // dynamic items: a wave takes G (tree, transaction group) items at a time from the chunk's LDS
+      // counter until all 4 CH are taken, so waves the SIMD arbiter starves take fewer items and the
+      // end-of-chunk barrier waits less; results go to the same lv slots, the owner sum is unchanged
+      constexpr int G = 2;
+      constexpr uint32_t NI = 4u * CH;  // a multiple of G: every grab is G valid items
+      if (tid == 0) ctr[(k + 1) & 1] = 0u;  // chunk k+1's counter, last used in chunk k-1
+      const uint32_t lv = (k & 1) ? lvB : lvA;
+      for (;;) {
+        uint32_t base = 0u;
+        if (lane == 0) base = __hip_atomic_fetch_add(&ctr[k & 1], (uint32_t)G, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (base >= NI) break;
+        uint32_t tbv[G], l4[G], sl[G], cc[G], tx[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const uint32_t it = base + (uint32_t)j;
+          cc[j] = it >> 2;
+          tx[j] = ((it & 3u) << 6) + (uint32_t)lane;
+          tbv[j] = cur + cc[j] * (4u << D);
+          l4[j] = s0 + tx[j] * 4u;
+        }
+        if (tile_nan)
+          walk4d<D, G, true>(tbv, l4, sl);
+        else
+          walk4d<D, G, false>(tbv, l4, sl);
+        LeafT lval[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) lval[j] = leaves[((size_t)k * CH + cc[j]) * NL + sl[j]];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          lds_store<LeafT>(lv + (cc[j] * kTile + tx[j]) * sizeof(LeafT), lval[j]);
+          const int64_t r = (int64_t)blockIdx.x * kTile + tx[j];
+          if (out_leaf != nullptr && r < n) {
+            const int tg = k * CH + (int)cc[j];
+            if (tg < n_trees) out_leaf[r * n_trees + tg] = leaf_ids[(size_t)tg * NL + sl[j]];
+          }
+        }
+      }
+    } else {
+      uint32_t slots[TPG];
+      if (tile_nan)
+        walk4<D, TPG, LeafT, true, true>(cur, gg, lane4, slots);
+      else
+        walk4<D, TPG, LeafT, false, true>(cur, gg, lane4, slots);
 #ifdef FD_FOREST_PROFILE
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
-    FD_PROF_T(q2);
-    const uint32_t lv = (k & 1) ? lvB : lvA;
-    LeafT lval[TPG];  // leaf values from global memory (L2-resident), all TPG loads in flight together
+      const uint32_t lv = (k & 1) ? lvB : lvA;
+      LeafT lval[TPG];  // leaf values from global memory (L2-resident), all TPG loads in flight together
 #pragma unroll
-    for (int j = 0; j < TPG; ++j) lval[j] = leaves[((size_t)k * CH + gg * TPG + j) * NL + slots[j]];
+      for (int j = 0; j < TPG; ++j) lval[j] = leaves[((size_t)k * CH + gg * TPG + j) * NL + slots[j]];
 #pragma unroll
-    for (int j = 0; j < TPG; ++j) {
-      const int c = gg * TPG + j;
-      lds_store<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT), lval[j]);
-      if (out_leaf != nullptr && valid) {
-        const int tg = k * CH + c;
-        if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slots[j]];
+      for (int j = 0; j < TPG; ++j) {
+        const int c = gg * TPG + j;
+        lds_store<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT), lval[j]);
+        if (out_leaf != nullptr && valid) {
+          const int tg = k * CH + c;
+          if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slots[j]];
+        }
       }
     }
+    FD_PROF_T(q2);  // DYN: walk + leaf in one phase
     FD_PROF_T(q3);
     dma_wait();
     __syncthreads();  // chunk k+1 landed; lv[k&1] complete; owner of k-1 done with lv[(k-1)&1]
@@ -1657,29 +1750,35 @@ using KernelFn6 = void (*)(const float*, int64_t, int, int, const char*, int, in
                            const float*, const int32_t*, int, float, double, double, double*, double*, int32_t*,
                            const void*);
 
-template <typename LeafT, int KIND, int CH>
+template <typename LeafT, int KIND, int CH, bool DYN>
 KernelFn6 pick6_ch(int D) {
   switch (D) {
-    case 1: return (KernelFn6)forest_kernel6<1, CH, LeafT, KIND>;
-    case 2: return (KernelFn6)forest_kernel6<2, CH, LeafT, KIND>;
-    case 3: return (KernelFn6)forest_kernel6<3, CH, LeafT, KIND>;
-    case 4: return (KernelFn6)forest_kernel6<4, CH, LeafT, KIND>;
-    case 5: return (KernelFn6)forest_kernel6<5, CH, LeafT, KIND>;
-    case 6: return (KernelFn6)forest_kernel6<6, CH, LeafT, KIND>;
-    case 7: return (KernelFn6)forest_kernel6<7, CH, LeafT, KIND>;
-    case 8: return (KernelFn6)forest_kernel6<8, CH, LeafT, KIND>;
+    case 1: return (KernelFn6)forest_kernel6<1, CH, LeafT, KIND, DYN>;
+    case 2: return (KernelFn6)forest_kernel6<2, CH, LeafT, KIND, DYN>;
+    case 3: return (KernelFn6)forest_kernel6<3, CH, LeafT, KIND, DYN>;
+    case 4: return (KernelFn6)forest_kernel6<4, CH, LeafT, KIND, DYN>;
+    case 5: return (KernelFn6)forest_kernel6<5, CH, LeafT, KIND, DYN>;
+    case 6: return (KernelFn6)forest_kernel6<6, CH, LeafT, KIND, DYN>;
+    case 7: return (KernelFn6)forest_kernel6<7, CH, LeafT, KIND, DYN>;
+    case 8: return (KernelFn6)forest_kernel6<8, CH, LeafT, KIND, DYN>;
     default: return nullptr;
   }
 }
 
-template <typename LeafT, int KIND>
-KernelFn6 pick6(int D, int CH) {
+template <typename LeafT, int KIND, bool DYN>
+KernelFn6 pick6_dyn(int D, int CH) {
   switch (CH) {
-    case 16: return pick6_ch<LeafT, KIND, 16>(D);
-    case 24: return pick6_ch<LeafT, KIND, 24>(D);
-    case 32: return pick6_ch<LeafT, KIND, 32>(D);
+    case 16: return pick6_ch<LeafT, KIND, 16, DYN>(D);
+    case 24: return pick6_ch<LeafT, KIND, 24, DYN>(D);
+    case 32: return pick6_ch<LeafT, KIND, 32, DYN>(D);
     default: return nullptr;
   }
+}
+
+// dyn: dynamic (tree, transaction group) items per wave (option 9) instead of static tree groups
+template <typename LeafT, int KIND>
+KernelFn6 pick6(int D, int CH, bool dyn) {
+  return dyn ? pick6_dyn<LeafT, KIND, true>(D, CH) : pick6_dyn<LeafT, KIND, false>(D, CH);
 }
 
 // small-batch launch: bin once, walk (tiles x chunk groups), sequential sum
@@ -1749,7 +1848,7 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   const int64_t blocks = (n + kTile - 1) / kTile;
   FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
   const int v = e.forest_variant;
-  FD_REQUIRE(v >= 0 && v <= 8, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..8");
+  FD_REQUIRE(v >= 0 && v <= 9, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..9");
   Engine::Timed* ev = nullptr;
 
   // small batches: tree-split latency path (option 6 forces it; auto below 128 tiles)
@@ -1788,12 +1887,14 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
     return;
   }
 
-  const size_t lds6 = pf.n_chunk ? lds_bytes_kernel3(pf.num_feature, pf.n_chunk_stride, pf.n_chunk, leaf_sz) : 0;
+  // + 64 B: kernel 6's two item counters after the tile_any flags
+  const size_t lds6 = pf.n_chunk ? lds_bytes_kernel3(pf.num_feature, pf.n_chunk_stride, pf.n_chunk, leaf_sz) + 64 : 0;
   const bool ok6 = pf.binned && pf.n_chunk > 0 && pf.depth <= 8 && lds6 <= kLdsBudget;
-  if (v == 8) FD_REQUIRE(ok6, FD_ERR_UNSUPPORTED, "forest kernel 6 needs the binned node-only layout (depth <= 8)");
-  if ((v == 0 || v == 8) && ok6) {
-    KernelFn6 fn = xgb ? pick6<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.n_chunk)
-                       : pick6<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.n_chunk);
+  if (v == 8 || v == 9)
+    FD_REQUIRE(ok6, FD_ERR_UNSUPPORTED, "forest kernel 6 needs the binned node-only layout (depth <= 8)");
+  if ((v == 0 || v == 8 || v == 9) && ok6) {
+    KernelFn6 fn = xgb ? pick6<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.n_chunk, v == 9)
+                       : pick6<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.n_chunk, v == 9);
     FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel 6 for this depth/chunk");
     FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds6));
     ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
