@@ -879,7 +879,11 @@ __device__ __forceinline__ void load_top(const char* __restrict__ blob, int k, i
   }
 }
 
-// bin(v) = #{t in tbl[0, cnt) : t <= v}, tbl ascending; steps = largest power of two <= max count.
+// largest power of two <= cnt (0 for cnt == 0): binary lifting over cnt entries needs exactly these
+// steps (a feature no split uses — the 64-wide vector's pad slots — costs none)
+__device__ __forceinline__ int lift_steps(int cnt) { return cnt > 0 ? (int)(1u << (31 - __clz(cnt))) : 0; }
+
+// bin(v) = #{t in tbl[0, cnt) : t <= v}, tbl ascending; steps = largest power of two <= cnt.
 template <bool IN_LDS>
 __device__ __forceinline__ uint32_t bin_of(float v, const float* __restrict__ gt, uint32_t lt, int cnt, int steps) {
   int pos = 0;
@@ -950,8 +954,8 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
           anynan = 1;
         } else {
           const int o = thr_off[f], cnt = thr_off[f + 1] - o;
-          const uint32_t b = tbl_lds ? bin_of<true>(v, nullptr, bufB + (uint32_t)o * 4u, cnt, bin_steps)
-                                     : bin_of<false>(v, thr + o, 0u, cnt, bin_steps);
+          const uint32_t b = tbl_lds ? bin_of<true>(v, nullptr, bufB + (uint32_t)o * 4u, cnt, lift_steps(cnt))
+                                     : bin_of<false>(v, thr + o, 0u, cnt, lift_steps(cnt));
           w = b << 16;
         }
       }
@@ -1106,8 +1110,8 @@ forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
           anynan = 1;
         } else {
           const int o = thr_off[f], cnt = thr_off[f + 1] - o;
-          const uint32_t b = tbl_lds ? bin_of<true>(v, nullptr, bufB + (uint32_t)o * 4u, cnt, bin_steps)
-                                     : bin_of<false>(v, thr + o, 0u, cnt, bin_steps);
+          const uint32_t b = tbl_lds ? bin_of<true>(v, nullptr, bufB + (uint32_t)o * 4u, cnt, lift_steps(cnt))
+                                     : bin_of<false>(v, thr + o, 0u, cnt, lift_steps(cnt));
           w = b << 16;
         }
       }
@@ -1460,7 +1464,7 @@ split_bin_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, 
   if (ok) v = f < ld ? X[r * (int64_t)ld + f] : __builtin_nanf("");  // DMatrix: missing column = NaN
   const int o = thr_off[f], cnt = thr_off[f + 1] - o;
   int pos = 0;
-  for (int st = bin_steps; st > 0; st >>= 1) {
+  for (int st = lift_steps(cnt); st > 0; st >>= 1) {
     const int np = pos + st;
     if (np <= cnt && thr[o + np - 1] <= v) pos = np;
   }
