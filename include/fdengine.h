@@ -547,7 +547,8 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      tree-split small-batch path (auto takes it below 128 tiles of 256 transactions), 7 force the
      binned 1024-thread kernel with its top three tree levels read from registers (A/B: slower), 8 force
      the binned node-only-chunk kernel (auto's choice when the forest has that layout), 9 force it with
-     dynamic per-wave (tree, transaction group) work items (A/B: slower) */
+     dynamic per-wave (tree, transaction group) work items (A/B: slower), 10 force it with more trees for
+     the older tree groups (A/B: slower) */
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
 int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches);
 int fd_timing_reset(fd_engine* eng);

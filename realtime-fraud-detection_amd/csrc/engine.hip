@@ -282,7 +282,7 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   FD_REQUIRE(key, FD_ERR_INVALID_ARG, "null key");
   const std::string k(key);
   if (k == "forest_kernel") {
-    FD_REQUIRE(value >= 0 && value <= 9, FD_ERR_INVALID_ARG, "forest_kernel must be in 0..9");
+    FD_REQUIRE(value >= 0 && value <= 10, FD_ERR_INVALID_ARG, "forest_kernel must be in 0..10");
     e.forest_variant = (int)value;
   } else if (k == "ingest_stop_after") {  // diagnostics: 0 full; 1 stage; 2 + structure; 3 + members
     FD_REQUIRE(value >= 0 && value <= 3, FD_ERR_INVALID_ARG, "ingest_stop_after must be in 0..3");

@@ -1048,6 +1048,52 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
   if (valid) write_outputs<KIND, LeafT>(acc, row, if_offset, if_denom, out_prob, out_raw);
 }
 
+// Trees of a CH-tree chunk walked by tree group g in kernel 6's skewed mode (MODE 2). The SIMD arbiter
+// issues by age, so the four tree groups (waves 4g..4g+3, launched in that order) walk equal shares in
+// 62k / 77k / 96k / 114k cycles (tools/forest_phases.py per-wave medians) and the older groups then
+// idle at the chunk barrier: the skew gives the older groups more trees.
+__host__ __device__ constexpr int skew_trees(int CH, int g) {
+  return CH == 24 ? (g == 0 ? 8 : g == 1 ? 7 : g == 2 ? 5 : 4)
+       : CH == 16 ? (g == 0 ? 5 : g == 1 ? 4 : g == 2 ? 4 : 3)
+       : CH == 32 ? (g == 0 ? 10 : g == 1 ? 9 : g == 2 ? 7 : 6)
+                  : CH / 4;
+}
+__host__ __device__ constexpr int skew_first(int CH, int g) {
+  return g == 0 ? 0 : skew_first(CH, g - 1) + skew_trees(CH, g - 1);
+}
+static_assert(skew_first(24, 4) == 24 && skew_first(16, 4) == 16 && skew_first(32, 4) == 32, "skew covers the chunk");
+
+// walk NT trees [c0, c0 + NT) of the staged node-only chunk for this lane's transaction, then store
+// their leaf values (global [tree][2^D] array) into the chunk's lv tile
+template <int D, int NT, int CH, typename LeafT>
+__device__ __forceinline__ void walk_group6(uint32_t cur, int c0, uint32_t lane4, bool tile_nan, int k,
+                                            const LeafT* __restrict__ leaves, uint32_t lv, int txn, int64_t row,
+                                            bool valid, int32_t* __restrict__ out_leaf,
+                                            const int32_t* __restrict__ leaf_ids, int n_trees) {
+  constexpr int NL = 1 << D;
+  uint32_t tb[NT], l4[NT], sl[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    tb[j] = cur + (uint32_t)(c0 + j) * (4u << D);
+    l4[j] = lane4;
+  }
+  if (tile_nan)
+    walk4d<D, NT, true>(tb, l4, sl);
+  else
+    walk4d<D, NT, false>(tb, l4, sl);
+  LeafT lval[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) lval[j] = leaves[((size_t)k * CH + c0 + j) * NL + sl[j]];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    lds_store<LeafT>(lv + ((c0 + j) * kTile + txn) * sizeof(LeafT), lval[j]);
+    if (out_leaf != nullptr && valid) {
+      const int tg = k * CH + c0 + j;
+      if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + sl[j]];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // forest_kernel6 (depth <= 8, binned nodes): kernel 4 with node-only chunks. The staged chunk holds
 // only the CH trees' node words (1 KiB per depth-8 tree instead of 2-3 KiB with the leaves), so the
@@ -1057,7 +1103,7 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 // ~35 %), so more chains per wave is the lever. After the walk each lane reads its TPG leaf values
 // from the global [tree][2^D] array (L2-resident: 0.5 MiB for 500 x depth 8) with all loads in
 // flight together; the owner pass and the tree-order sum are kernel 4's.
-template <int D, int CH, typename LeafT, int KIND, bool DYN>
+template <int D, int CH, typename LeafT, int KIND, int MODE>
 __global__ void __launch_bounds__(kWG3)
 forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
                int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
@@ -1123,6 +1169,7 @@ forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
   }
   typedef __attribute__((address_space(3))) uint32_t lds_u32;
   lds_u32* const ctr = (lds_u32*)(size_t)(accL + kTile * (uint32_t)sizeof(LeafT) + 64u);  // 2 item counters
+  constexpr bool DYN = MODE == 1;
   if (DYN && tid == 0) ctr[0] = 0u;
   dma_wait();  // chunk 0 (published by tile_any's barrier)
   const bool tile_nan =
@@ -1181,6 +1228,20 @@ forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
           }
         }
       }
+    } else if constexpr (MODE == 2) {  // static, skewed tree groups (older waves walk more trees)
+      const uint32_t lv = (k & 1) ? lvB : lvA;
+#define FD_K6_GROUP(g)                                                                                      \
+  walk_group6<D, skew_trees(CH, g), CH, LeafT>(cur, skew_first(CH, g), lane4, tile_nan, k, leaves, lv, txn, row, \
+                                              valid, out_leaf, leaf_ids, n_trees)
+      if (gg == 0)
+        FD_K6_GROUP(0);
+      else if (gg == 1)
+        FD_K6_GROUP(1);
+      else if (gg == 2)
+        FD_K6_GROUP(2);
+      else
+        FD_K6_GROUP(3);
+#undef FD_K6_GROUP
     } else {
       uint32_t slots[TPG];
       if (tile_nan)
@@ -1754,35 +1815,38 @@ using KernelFn6 = void (*)(const float*, int64_t, int, int, const char*, int, in
                            const float*, const int32_t*, int, float, double, double, double*, double*, int32_t*,
                            const void*);
 
-template <typename LeafT, int KIND, int CH, bool DYN>
+template <typename LeafT, int KIND, int CH, int MODE>
 KernelFn6 pick6_ch(int D) {
   switch (D) {
-    case 1: return (KernelFn6)forest_kernel6<1, CH, LeafT, KIND, DYN>;
-    case 2: return (KernelFn6)forest_kernel6<2, CH, LeafT, KIND, DYN>;
-    case 3: return (KernelFn6)forest_kernel6<3, CH, LeafT, KIND, DYN>;
-    case 4: return (KernelFn6)forest_kernel6<4, CH, LeafT, KIND, DYN>;
-    case 5: return (KernelFn6)forest_kernel6<5, CH, LeafT, KIND, DYN>;
-    case 6: return (KernelFn6)forest_kernel6<6, CH, LeafT, KIND, DYN>;
-    case 7: return (KernelFn6)forest_kernel6<7, CH, LeafT, KIND, DYN>;
-    case 8: return (KernelFn6)forest_kernel6<8, CH, LeafT, KIND, DYN>;
+    case 1: return (KernelFn6)forest_kernel6<1, CH, LeafT, KIND, MODE>;
+    case 2: return (KernelFn6)forest_kernel6<2, CH, LeafT, KIND, MODE>;
+    case 3: return (KernelFn6)forest_kernel6<3, CH, LeafT, KIND, MODE>;
+    case 4: return (KernelFn6)forest_kernel6<4, CH, LeafT, KIND, MODE>;
+    case 5: return (KernelFn6)forest_kernel6<5, CH, LeafT, KIND, MODE>;
+    case 6: return (KernelFn6)forest_kernel6<6, CH, LeafT, KIND, MODE>;
+    case 7: return (KernelFn6)forest_kernel6<7, CH, LeafT, KIND, MODE>;
+    case 8: return (KernelFn6)forest_kernel6<8, CH, LeafT, KIND, MODE>;
     default: return nullptr;
   }
 }
 
-template <typename LeafT, int KIND, bool DYN>
-KernelFn6 pick6_dyn(int D, int CH) {
+template <typename LeafT, int KIND, int MODE>
+KernelFn6 pick6_mode(int D, int CH) {
   switch (CH) {
-    case 16: return pick6_ch<LeafT, KIND, 16, DYN>(D);
-    case 24: return pick6_ch<LeafT, KIND, 24, DYN>(D);
-    case 32: return pick6_ch<LeafT, KIND, 32, DYN>(D);
+    case 16: return pick6_ch<LeafT, KIND, 16, MODE>(D);
+    case 24: return pick6_ch<LeafT, KIND, 24, MODE>(D);
+    case 32: return pick6_ch<LeafT, KIND, 32, MODE>(D);
     default: return nullptr;
   }
 }
 
-// dyn: dynamic (tree, transaction group) items per wave (option 9) instead of static tree groups
+// mode: 0 equal static tree groups (option 8), 1 dynamic (tree, transaction group) items per wave
+// (option 9), 2 skewed static tree groups (option 10)
 template <typename LeafT, int KIND>
-KernelFn6 pick6(int D, int CH, bool dyn) {
-  return dyn ? pick6_dyn<LeafT, KIND, true>(D, CH) : pick6_dyn<LeafT, KIND, false>(D, CH);
+KernelFn6 pick6(int D, int CH, int mode) {
+  return mode == 1 ? pick6_mode<LeafT, KIND, 1>(D, CH)
+       : mode == 2 ? pick6_mode<LeafT, KIND, 2>(D, CH)
+                   : pick6_mode<LeafT, KIND, 0>(D, CH);
 }
 
 // small-batch launch: bin once, walk (tiles x chunk groups), sequential sum
@@ -1852,7 +1916,7 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   const int64_t blocks = (n + kTile - 1) / kTile;
   FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
   const int v = e.forest_variant;
-  FD_REQUIRE(v >= 0 && v <= 9, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..9");
+  FD_REQUIRE(v >= 0 && v <= 10, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..10");
   Engine::Timed* ev = nullptr;
 
   // small batches: tree-split latency path (option 6 forces it; auto below 128 tiles)
@@ -1894,11 +1958,12 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   // + 64 B: kernel 6's two item counters after the tile_any flags
   const size_t lds6 = pf.n_chunk ? lds_bytes_kernel3(pf.num_feature, pf.n_chunk_stride, pf.n_chunk, leaf_sz) + 64 : 0;
   const bool ok6 = pf.binned && pf.n_chunk > 0 && pf.depth <= 8 && lds6 <= kLdsBudget;
-  if (v == 8 || v == 9)
+  if (v >= 8)
     FD_REQUIRE(ok6, FD_ERR_UNSUPPORTED, "forest kernel 6 needs the binned node-only layout (depth <= 8)");
-  if ((v == 0 || v == 8 || v == 9) && ok6) {
-    KernelFn6 fn = xgb ? pick6<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.n_chunk, v == 9)
-                       : pick6<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.n_chunk, v == 9);
+  if ((v == 0 || v >= 8) && ok6) {
+    const int mode = v == 9 ? 1 : v == 10 ? 2 : 0;
+    KernelFn6 fn = xgb ? pick6<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.n_chunk, mode)
+                       : pick6<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.n_chunk, mode);
     FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel 6 for this depth/chunk");
     FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds6));
     ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;

@@ -130,7 +130,7 @@ def test_kernel5_depths(engine, depth):
 
 
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 6, 8])
-@pytest.mark.parametrize("variant", [3, 7, 8, 9])
+@pytest.mark.parametrize("variant", [3, 7, 8, 9, 10])
 def test_kernel4_depths(engine, depth, variant):
     """The binned 1024-thread kernel with the plain walk (option 3), with the top three levels from
     registers (option 7, walk4t; depth >= 3) and with node-only chunks + leaves from global memory
@@ -148,7 +148,7 @@ def test_kernel4_depths(engine, depth, variant):
 
 
 @pytest.mark.parametrize("max_bin", [256, None])
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_kernel_variants_agree(engine, variant, max_bin):
     """Every forest kernel (256-thread; 1024-thread tree-split on the threshold layout; 1024-thread on
     the binned layout) gives the oracle's bits, for hist-style and raw-valued split thresholds."""

@@ -39,3 +39,8 @@ for i, nm in enumerate(names):
     print(f"  {nm:9s} {np.median(p[:, :, i]):10.0f}   p10 {np.percentile(p[:, :, i], 10):10.0f}  p90 {np.percentile(p[:, :, i], 90):10.0f}")
 start = p[:, 0, 6]
 print("workgroup start spread (cycles):", float(start.max() - start.min()))
+# per wave index (0..15; wave w: tree group w >> 2, transaction group w & 3; SIMD = w mod 4 under the
+# usual round-robin placement): is the walk's spread systematic?
+print("walk / barrier median per wave index:")
+for w in range(16):
+    print(f"  wave {w:2d}  walk {np.median(p[:, w, 1]):9.0f}  barrier {np.median(p[:, w, 4]):9.0f}  owner {np.median(p[:, w, 3]):8.0f}")
