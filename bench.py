@@ -137,7 +137,9 @@ class Config2:
                 "node_steps_per_s": round(self.B * self.T * self.info["depth"] / avg, 1)}
 
     def kernels(self, timing):
-        return {}
+        from fdengine import _native as N
+        ms, c = timing.get(N.FD_TIMING_XGB, (0.0, 0))
+        return {"xgboost_forest": round(ms / c * 1e3, 3)} if c else {}
 
     def config(self, world):
         return {"workload": "config2: XGBoost binary:logistic 500 trees depth 8, 50 features, "
