@@ -1,28 +1,32 @@
 #!/usr/bin/env python3
-"""bench.py — scored transactions/sec on the hot path (BASELINE.json metric).
+"""bench.py — scored transactions/sec on the hot path (BASELINE.json metric: "scored transactions/sec
+(whole node) at 1/2/4/8 GPUs; p99 micro-batch latency").
 
-Default workload (N=1 headline, BASELINE.json configs[1], "config 2"): XGBoost binary:logistic,
-500 trees x depth 8, 50 features, 64k-transaction micro-batches on one MI355X. One *step* = one
-pass of the hot path (fd_forest_predict_device) over one micro-batch whose features are already
-resident in HBM; output = P(fraud) per transaction in HBM.
+Default workload (BASELINE.json configs[3], "config 4" — the configuration the metric is quoted on):
+card-hash-sharded keyed state + scoring. Each rank (one process per GPU) ingests its own 64k-transaction
+micro-batch per step, drawn over ALL 100M cards of the node, and runs fdengine.sharding.ShardedScorer:
+route partition -> RCCL all-to-all of 48-B records to the owner GPUs -> owner features (HBM card state,
+sliding windows) + XGBoost 500x8 + IsolationForest 100 + blend -> all-to-all of results back -> arrival
+order. At N=1 the same kernels run with no collective (all 100M cards resident on the one GPU).
 
-`--workload config3` (BASELINE configs[2]): the full pipeline per step on one GPU — card-state
-features (10M cards resident in HBM, sliding windows) -> XGBoost 500x8 + IsolationForest 100 ->
-ensemble blend/decision (fd_score_batch_device), 64k transactions per micro-batch, the stream's
-transactions resident in HBM.
+`python bench.py --gpus N` (no torchrun env) starts N ranks itself (torch.distributed.run, spawned before
+anything touches the GPU); under `torch.distributed.run --nproc-per-node N` it joins the given ranks.
 
-Multi-GPU (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`): one process per
-GPU, each scoring its own micro-batches — config 2 has no keyed state, so there is no data-path
-collective ("scaling": "weak"); RCCL carries only the barrier and the max-over-ranks time.
+Other workloads (`--workload`): config2 (XGBoost only on HBM-resident vectors), config3 (10M cards, one
+GPU, no routing), config5 (+ LSTM head, 1k latency batches), ingest (JSON codec), config3j (config3 from
+raw JSON).
 
-Also reported: p50/p99 micro-batch latency (host submit -> scores in host memory), the dominant
-kernel's roofline (algorithmic bytes / HIP-event-timed kernel duration vs 8 TB/s HBM), per-kernel
-times, and the CPU oracle (C restatement, OpenMP) timed on this host on a bounded sample (rank 0,
-N=1 only).
+Reported beside the throughput: p50/p99 micro-batch latency (host submit -> scores in host memory), the
+dominant kernel's roofline against ITS bound (the forest walk: LDS issue, node-steps/s against the
+LDS-array ceiling), the fused pipeline's algorithmic HBM bytes (SURVEY §8(d), 238 B/txn), per-kernel
+times, and the CPU baseline: the oracle C restatement of the whole chain on a config-1-shaped stream
+(100k simulator transactions), at 1 core and at the host threads available (rank 0, N=1 only).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -34,6 +38,10 @@ sys.path.insert(0, str(REPO / "realtime-fraud-detection_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 F32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA peak (MI355X_MICROARCH.md "Peak FP32 (matrix)")
+# Forest walk: per node-step one ds_read_b32 (feature bin) + one ds_read_b64 (children pair) per lane; per
+# 64-lane wave-instruction 2 + 2 LDS-array cycles (MI355X_MICROARCH.md §LDS) = 16 node-steps/clk/CU.
+LDS_NODE_STEPS_PEAK = 256 * 2.4e9 * 16  # 9.83e12 node-steps/s
+FUSED_BYTES_PER_TXN = 238  # txn 36 + card header R/W 96 + profiles 64 + outputs 10 + ring append 32
 
 
 def log(*a):
@@ -79,6 +87,101 @@ def pmc_traffic(workload, B):
         return None
 
 
+def forest_roofline(timing, kind, forest, depth, B, workload, label):
+    """Roofline of a forest launch against its real bound: LDS issue of the dependent walk."""
+    from fdengine import _native as N
+    ms, launches = timing[kind]
+    avg = (ms / 1e3) / max(1, launches)
+    steps = B * forest.n_trees * depth
+    achieved = steps / avg
+    model_bytes = forest_blob_bytes(forest)
+    return {"bound": "lds", "achieved": round(achieved, 1), "peak": LDS_NODE_STEPS_PEAK, "unit": "node-steps/s",
+            "frac": round(achieved / LDS_NODE_STEPS_PEAK, 6), "traffic": pmc_traffic(workload, B),
+            "kernel": label, "kernel_avg_us": round(avg * 1e6, 3), "node_steps_per_launch": steps,
+            "peak_basis": "per node-step 1 ds_read_b32 + 1 ds_read_b64 per lane = 4 LDS-array cycles per 64 "
+                          "node-steps: 16/clk/CU x 256 CUs x 2.4 GHz",
+            "hbm_view": {"algorithmic_bytes_per_launch": B * (64 * 4 + 8) + model_bytes,
+                         "achieved_GBs": round((B * (64 * 4 + 8) + model_bytes) / avg / 1e9, 3), "peak_GBs": HBM_PEAK_GBS}}
+
+
+def product_blend(names):
+    """Blend constants the way the product computes them: EnsemblePredictor._get_model_weights over the
+    enabled models of the registry (fdengine/ensemble.py, ensemble_predictor.py:62-73)."""
+    from fdengine import ensemble as E
+    from fdengine.registry import ScoringConfig
+    cfg = ScoringConfig("/nonexistent-models")
+    for n in list(cfg.models):
+        if n not in names:
+            cfg.disable_model(n)
+    ep = E.EnsemblePredictor(None, cfg)
+    return ep.blend_params(names), [ep.model_weights[n] for n in names], [E._CONF_MULT[n] for n in names]
+
+
+def fit_models(dev_index, T, D, mode, K):
+    """Models in the reference's file formats on realistic scoring vectors: a 20k-card population's stream
+    through the ENGINE's own feature kernel (a scratch engine with a small table), then a random XGBoost
+    500 x depth 8 with hist-style cuts of those vectors and an IsolationForest trained with the reference
+    trainer's recipe (synth.isolation_forest)."""
+    import numpy as np
+    import fdengine
+    from fdengine import synth
+    spop = synth.population(20000, 500, seed=11)
+    stx = synth.txn_stream(spop, 40000, seed=12, rate_per_s=20.0)
+    scratch = fdengine.FraudEngine(dev_index)
+    try:
+        scratch.state_init(1 << 16, mode, K)
+        U, M = spop["users"], spop["merchants"]
+        scratch.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        scratch.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        X = scratch.features(stx)
+    finally:
+        scratch.close()
+    xgb = fdengine.xgboost_from_json_doc(synth.xgboost_doc(T, D, 64, X[-8192:], seed=13))
+    ifm = fdengine.iforest_from_sklearn(synth.isolation_forest(X[-8192:].astype(np.float64)))
+    return xgb, ifm
+
+
+def cpu_chain_baseline(xgb, ifm, weights, mults, mode, K, lstm=None, seq_len=10, n=100_000):
+    """BASELINE config 1 shape: 100k simulator transactions (10k users, 5k merchants: simulator.py:481-482)
+    through the oracle chain — features (C, sequential by definition) -> XGBoost -> IsolationForest
+    (-> LSTM) -> blend (OpenMP) — at 1 thread and at every host thread available. kind "port": the
+    reference's own Python never reaches the GPU box (≈2.8k txn/s/core in the build container)."""
+    import numpy as np
+    import oracle
+    from fdengine import synth
+    from oracle.features_c import OracleFeatureState
+    pop = synth.population(10000, 5000, seed=1)
+    tx = synth.txn_stream(pop, n, seed=2)
+    U, M = pop["users"], pop["merchants"]
+
+    def run(th):
+        import torch
+        torch.set_num_threads(th)
+        o = OracleFeatureState(1 << 15, mode, K)
+        o.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        o.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        a = time.perf_counter()
+        raw, V = o.run(tx, want_raw=lstm is not None)
+        cols = [oracle.xgb_predict(xgb, V, nthreads=th)[0].astype(np.float64),
+                oracle.iforest_predict(ifm, V, nthreads=th)[0]]
+        if lstm is not None:
+            from oracle import lstm_ref
+            cols.append(lstm_ref.lstm_forward(lstm, lstm_ref.SequenceState(seq_len).run(tx["card_key"], raw)))
+        oracle.blend_weighted(np.stack(cols), weights, mults, nthreads=th)
+        return n / (time.perf_counter() - a)
+
+    th = cpu_threads()
+    one = run(1)
+    many = run(th) if th > 1 else one
+    chain = "features C 1 thread -> XGBoost 500x8 -> IsolationForest 100" + (" -> LSTM(128) torch fp32" if lstm else "") \
+        + " -> blend"
+    return {"value": round(many, 1), "unit": "txn/s", "cores": th, "kind": "port",
+            "sample": f"config-1 shape: {n} simulator transactions (10k users, 5k merchants) through the oracle chain "
+                      f"({chain}; forests/blend OpenMP), whole stream, {th} threads; CPU: {cpu_model()}, "
+                      f"os.cpu_count()={os.cpu_count()}",
+            "single_core": {"value": round(one, 1), "cores": 1}}
+
+
 # --------------------------------------------------------------------------------------- config 2
 class Config2:
     name = "config2"
@@ -117,24 +220,19 @@ class Config2:
 
     def parity(self):
         import oracle
-        self.step(0)
-        self.torch.cuda.synchronize()
-        rp, _, _ = oracle.xgb_predict(self.forest, self.Xpool[:512], nthreads=cpu_threads())
-        return float(self.np.abs(self.prob[:512].cpu().numpy() - rp).max())
+        np = self.np
+        worst = 0.0
+        for s in range(min(self.pool, 2)):  # two whole micro-batches
+            self.step(s)
+            self.torch.cuda.synchronize()
+            rp, _, _ = oracle.xgb_predict(self.forest, self.Xpool[s * self.B:(s + 1) * self.B], nthreads=cpu_threads())
+            worst = max(worst, float(np.abs(self.prob[s * self.B:(s + 1) * self.B].cpu().numpy() - rp).max()))
+        return {"batches_checked": min(self.pool, 2), "max_abs_prob_diff": worst}
 
     def roofline(self, timing):
         from fdengine import _native as N
-        ms, launches = timing[N.FD_TIMING_XGB]
-        avg = (ms / 1e3) / max(1, launches)
-        model_bytes = forest_blob_bytes(self.forest)
-        per_launch = self.B * (self.F * 4 + 8) + model_bytes
-        achieved = per_launch / avg / 1e9
-        return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(self.name, self.B),
-                "kernel": FOREST_KERNEL.format(d=self.info['depth'], t="f32", k="XGB"), "kernel_avg_us": round(avg * 1e6, 3),
-                "algorithmic_bytes_per_launch": per_launch, "bytes_per_txn": self.F * 4 + 8,
-                "model_bytes_per_launch": model_bytes,
-                "node_steps_per_s": round(self.B * self.T * self.info["depth"] / avg, 1)}
+        return forest_roofline(timing, N.FD_TIMING_XGB, self.forest, self.info["depth"], self.B, self.name,
+                               FOREST_KERNEL.format(d=self.info['depth'], t="f32", k="XGB"))
 
     def kernels(self, timing):
         from fdengine import _native as N
@@ -149,25 +247,19 @@ class Config2:
 
     def cpu_baseline(self, seconds):
         import oracle
+
+        def rate(th, rows):
+            a = time.perf_counter()
+            oracle.xgb_predict(self.forest, self.Xpool[:rows], nthreads=th)
+            return rows / (time.perf_counter() - a)
+
         th = cpu_threads()
-        n0 = min(len(self.Xpool), 256 * th)
-        a = time.perf_counter()
-        oracle.xgb_predict(self.forest, self.Xpool[:n0], nthreads=th)
-        dt = time.perf_counter() - a
-        reps = max(1, int(seconds / max(dt, 1e-6) * n0 / len(self.Xpool)))
-        n = min(len(self.Xpool), max(n0, int(n0 * seconds / max(dt, 1e-6))))
-        a = time.perf_counter()
-        done = 0
-        while True:
-            oracle.xgb_predict(self.forest, self.Xpool[:n], nthreads=th)
-            done += n
-            if time.perf_counter() - a >= seconds or done >= reps * len(self.Xpool):
-                break
-        dt = time.perf_counter() - a
-        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
-                "sample": f"{done} txns of the config-2 workload (500 trees x depth 8, 50 features) through "
-                          f"oracle/oracle_forest.c orc_xgb_predict, {th} OpenMP threads, {dt:.2f} s, "
-                          f"CPU: {cpu_model()}"}
+        one = rate(1, 16384)
+        many = rate(th, min(len(self.Xpool), max(16384, int(one * th * seconds / 2))))
+        return {"value": round(many, 1), "unit": "txn/s", "cores": th, "kind": "port",
+                "sample": f"config-2 vectors (500 trees x depth 8, 50 features) through oracle/oracle_forest.c "
+                          f"orc_xgb_predict, {th} OpenMP threads; CPU: {cpu_model()}, os.cpu_count()={os.cpu_count()}",
+                "single_core": {"value": round(one, 1), "cores": 1}}
 
 
 # --------------------------------------------------------------------------------------- config 3
@@ -180,42 +272,25 @@ class Config3:
     def __init__(self, args, rank, dev, eng):
         import numpy as np
         import torch
-        import fdengine
         from fdengine import _native as N
         from fdengine import synth
-        from oracle.features_c import OracleFeatureState
-        from oracle import scoring_ref as S
-        self.np, self.torch, self.N, self.S = np, torch, N, S
+        self.np, self.torch, self.N = np, torch, N
         self.B, self.T, self.D = args.batch, args.trees, args.depth
         self.cards, self.mode, self.K = args.cards, (1 if args.window == "sliding" else 0), args.ring_k
         self.eng = eng
         t = time.time()
-        # models on realistic scoring vectors: a small population through the CPU feature oracle
-        spop = synth.population(20000, 500, seed=11)
-        stx = synth.txn_stream(spop, 40000, seed=12, rate_per_s=20.0)
-        so = OracleFeatureState(1 << 16, self.mode, self.K)
-        so.load_users(spop["users"]["key"], spop["users"]["avg_amount"], spop["users"]["account_age_days"],
-                      spop["users"]["device_fp"])
-        so.load_merchants(spop["merchants"]["fraud_rate"], spop["merchants"]["risk_multiplier"])
-        _, Xref = so.run(stx, want_raw=False)
-        self.xgb = fdengine.xgboost_from_json_doc(synth.xgboost_doc(self.T, self.D, 64, Xref[-8192:], seed=13))
-        self.ifm = fdengine.iforest_from_sklearn(synth.isolation_forest(Xref[-8192:].astype(np.float64)))
+        self.xgb, self.ifm = fit_models(dev.index, self.T, self.D, self.mode, self.K)
         eng.load_forest(0, self.xgb)
         eng.load_forest(1, self.ifm)
         self.names = ["xgboost_primary", "isolation_forest"]
         self.slots = [0, 1]
-        reg = {"xgboost_primary": 0.4, "isolation_forest": 0.05}
         if self.with_lstm:
             from fdengine import lstm as L
             self.lw = L.random_weights(16, 128, 1, seed=14)
             eng.load_lstm(self.lw)
             self.names.append("lstm_sequential")
             self.slots.append(N.FD_SLOT_LSTM)
-            reg["lstm_sequential"] = 0.25
-        w = S.normalized_weights(reg)
-        self.weights = [w[n] for n in self.names]
-        self.mults = [S.CONF_MULT[n] for n in self.names]
-        self.params = fdengine.FraudEngine.blend_params(self.weights, self.mults)
+        self.params, self.weights, self.mults = product_blend(self.names)
         # population: cards resident in HBM
         self.pop = synth.population(self.cards, 5000, seed=100 + rank)
         cap = 1
@@ -226,7 +301,7 @@ class Config3:
         U, M = self.pop["users"], self.pop["merchants"]
         eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
         eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
-        self.n_batches = args.warmup + args.steps + args.latency_iters + 1
+        self.n_batches = args.warmup + args.steps + args.latency_iters + args.parity_batches + 1
         self.tx = synth.txn_stream(self.pop, self.n_batches * self.B, seed=200 + rank)
         self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
         self.elem = {f: self.tx[f].dtype.itemsize for f in N.TXN_FIELDS}
@@ -241,7 +316,8 @@ class Config3:
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.next_batch = 0
-        log(f"[rank {rank}] config3 setup {time.time() - t:.1f}s: {self.cards} cards, capacity {cap}, "
+        self.parity_batches = args.parity_batches
+        log(f"[rank {rank}] {self.name} setup {time.time() - t:.1f}s: {self.cards} cards, capacity {cap}, "
             f"{self.n_batches} batches resident, window={'sliding' if self.mode else 'redis_compat'}")
 
     def _ptrs(self, b):
@@ -262,7 +338,7 @@ class Config3:
         self.h_risk.copy_(self.risk, non_blocking=True)
 
     def parity(self):
-        """Batch 0 through the oracle chain (fresh oracle state == fresh engine state)."""
+        """The first parity_batches micro-batches (fresh state, carried across them) through the oracle chain."""
         import oracle
         from oracle.features_c import OracleFeatureState
         np = self.np
@@ -270,45 +346,42 @@ class Config3:
         o = OracleFeatureState(self.cap, self.mode, self.K)
         o.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
         o.load_merchants(M["fraud_rate"], M["risk_multiplier"])
-        part = {f: self.tx[f][:self.B] for f in self.N.TXN_FIELDS}
-        self.step(0)
-        self.torch.cuda.synchronize()
-        rraw, rvec = o.run(part, want_raw=self.with_lstm)
-        del o
-        V = self.vec.cpu().numpy()
-        px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
-        pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
-        cols = [px.astype(np.float64), pi]
-        out = {}
+        hist = None
         if self.with_lstm:
             from oracle import lstm_ref
-            pl = lstm_ref.lstm_forward(self.lw, lstm_ref.SequenceState(self.seq_len).run(part["card_key"], rraw))
-            cols.append(pl)
-            out["lstm_max_abs_prob_diff"] = float(np.abs(self.mp[2].cpu().numpy() - pl).max())
-        fp, _, dec, _ = oracle.blend_weighted(np.stack(cols), self.weights, self.mults)
-        vec_diff = int((V != rvec).sum())
-        out.update({"vector_mismatched_elements": vec_diff,
-                    "max_abs_prob_diff": float(np.abs(self.fp.cpu().numpy() - fp).max()),
-                    "decision_mismatches": int((self.dec.cpu().numpy() != dec).sum())})
+            hist = lstm_ref.SequenceState(self.seq_len)
+        out = {"batches_checked": self.parity_batches, "vector_mismatched_elements": 0, "max_abs_prob_diff": 0.0,
+               "decision_mismatches": 0}
+        for b in range(self.parity_batches):
+            part = {f: self.tx[f][b * self.B:(b + 1) * self.B] for f in self.N.TXN_FIELDS}
+            self.step(b)
+            self.torch.cuda.synchronize()
+            rraw, rvec = o.run(part, want_raw=self.with_lstm)
+            V = self.vec.cpu().numpy()
+            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
+            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
+            cols = [px.astype(np.float64), pi]
+            if self.with_lstm:
+                from oracle import lstm_ref
+                pl = lstm_ref.lstm_forward(self.lw, hist.run(part["card_key"], rraw))
+                cols.append(pl)
+                out["lstm_max_abs_prob_diff"] = max(out.get("lstm_max_abs_prob_diff", 0.0),
+                                                    float(np.abs(self.mp[2].cpu().numpy() - pl).max()))
+            fp, _, dec, _ = oracle.blend_weighted(np.stack(cols), self.weights, self.mults)
+            out["vector_mismatched_elements"] += int((V != rvec).sum())
+            out["max_abs_prob_diff"] = max(out["max_abs_prob_diff"], float(np.abs(self.fp.cpu().numpy() - fp).max()))
+            out["decision_mismatches"] += int((self.dec.cpu().numpy() != dec).sum())
+        del o
         return out
 
     def roofline(self, timing):
-        N = self.N
-        ms, launches = timing[N.FD_TIMING_XGB]
-        avg = (ms / 1e3) / max(1, launches)
-        model_bytes = forest_blob_bytes(self.xgb)
-        per_launch = self.B * (64 * 4 + 8) + model_bytes
-        achieved = per_launch / avg / 1e9
-        return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(self.name, self.B),
-                "kernel": FOREST_KERNEL.format(d=8, t="f32", k="XGB") + " dominant", "kernel_avg_us": round(avg * 1e6, 3),
-                "algorithmic_bytes_per_launch": per_launch, "bytes_per_txn": 64 * 4 + 8,
-                "model_bytes_per_launch": model_bytes}
+        return forest_roofline(timing, self.N.FD_TIMING_XGB, self.xgb, 8, self.B, self.name,
+                               FOREST_KERNEL.format(d=8, t="f32", k="XGB") + " dominant")
 
     def kernels(self, timing):
         N = self.N
         names = {N.FD_TIMING_XGB: "xgboost_forest", N.FD_TIMING_IFOREST: "iforest_forest",
-                 N.FD_TIMING_FEATURES: "features (assign+process)", N.FD_TIMING_BLEND: "blend",
+                 N.FD_TIMING_FEATURES: "features", N.FD_TIMING_BLEND: "blend",
                  N.FD_TIMING_ROUTE: "route_partition (count+scan+scatter)", N.FD_TIMING_LSTM: "lstm_head",
                  N.FD_TIMING_WINDOWS: "windows", N.FD_TIMING_INGEST: "ingest_json"}
         return {names[k]: round(ms / max(1, c) * 1e3, 3) for k, (ms, c) in timing.items() if c}
@@ -321,30 +394,8 @@ class Config3:
                 "parallelism": f"replicas x{world}"}
 
     def cpu_baseline(self, seconds):
-        """Oracle chain on the first transactions of the same stream: features (sequential by
-        definition), both forests and the blend (OpenMP)."""
-        import oracle
-        from oracle.features_c import OracleFeatureState
-        np = self.np
-        th = cpu_threads()
-        U, M = self.pop["users"], self.pop["merchants"]
-        o = OracleFeatureState(self.cap, self.mode, self.K)
-        o.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
-        o.load_merchants(M["fraud_rate"], M["risk_multiplier"])
-        chunk = 16384
-        done, a = 0, time.perf_counter()
-        while time.perf_counter() - a < seconds and done + chunk <= len(self.tx["ts_ms"]):
-            part = {f: self.tx[f][done:done + chunk] for f in self.N.TXN_FIELDS}
-            _, V = o.run(part, want_raw=False)
-            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=th)
-            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=th)
-            oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults, nthreads=th)
-            done += chunk
-        dt = time.perf_counter() - a
-        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
-                "sample": f"first {done} txns of the config-3 stream through the oracle chain (features C "
-                          f"single-threaded + XGBoost + IsolationForest + blend, {th} OpenMP threads), "
-                          f"{dt:.2f} s, CPU: {cpu_model()}"}
+        return cpu_chain_baseline(self.xgb, self.ifm, self.weights, self.mults, self.mode, self.K,
+                                  lstm=self.lw if self.with_lstm else None, seq_len=self.seq_len)
 
 
 # --------------------------------------------------------------------------------------- config 5
@@ -365,10 +416,9 @@ class Config5(Config3):
         achieved = flops / avg / 1e12
         return {"bound": "mfma", "achieved": round(achieved, 4), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 6), "traffic": pmc_traffic(self.name, self.B),
-                "kernel": "lstm_kernel (v_mfma_f32_16x16x4_f32, 16 txn x 512 gates per workgroup)",
+                "kernel": "lstm_kernel (v_mfma_f32_16x16x4_f32)",
                 "kernel_avg_us": round(avg * 1e6, 3), "flops_per_launch": flops, "flops_per_txn": flops // self.B,
-                "workgroups": (self.B + 15) // 16,
-                "note": "latency-bound: a 1k batch fills (B/16) of 256 CUs; f32 MFMA = reference fp32 precision"}
+                "note": "latency-bound 1k batch; f32 MFMA = reference fp32 precision"}
 
     def config(self, world):
         c = super().config(world)
@@ -378,57 +428,22 @@ class Config5(Config3):
         c["lstm"] = {"hidden": 128, "seq_len": self.seq_len, "input": 16, "head": "dense(1)+sigmoid"}
         return c
 
-    def cpu_baseline(self, seconds):
-        """Oracle chain incl. the LSTM head (PyTorch fp32 CPU forward) on the first txns of the stream."""
-        import torch
-
-        import oracle
-        from oracle import lstm_ref
-        from oracle.features_c import OracleFeatureState
-        np = self.np
-        th = cpu_threads()
-        torch.set_num_threads(th)
-        U, M = self.pop["users"], self.pop["merchants"]
-        o = OracleFeatureState(self.cap, self.mode, self.K)
-        o.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
-        o.load_merchants(M["fraud_rate"], M["risk_multiplier"])
-        hist = lstm_ref.SequenceState(self.seq_len)
-        chunk = 4096
-        done, a = 0, time.perf_counter()
-        while time.perf_counter() - a < seconds and done + chunk <= len(self.tx["ts_ms"]):
-            part = {f: self.tx[f][done:done + chunk] for f in self.N.TXN_FIELDS}
-            raw, V = o.run(part, want_raw=True)
-            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=th)
-            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=th)
-            pl = lstm_ref.lstm_forward(self.lw, hist.run(part["card_key"], raw))
-            oracle.blend_weighted(np.stack([px.astype(np.float64), pi, pl]), self.weights, self.mults, nthreads=th)
-            done += chunk
-        dt = time.perf_counter() - a
-        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
-                "sample": f"first {done} txns of the config-5 stream through the oracle chain (features C + card "
-                          f"history single-threaded, XGBoost + IsolationForest + blend {th} OpenMP threads, LSTM "
-                          f"torch fp32 CPU {th} threads), {dt:.2f} s, CPU: {cpu_model()}"}
-
 
 # --------------------------------------------------------------------------------------- config 4
 class Config4(Config3):
-    """BASELINE configs[3]: card-hash-sharded keyed state + scoring, RCCL all-to-all routing.
-    Each rank ingests its own 64k-txn micro-batch per step (drawn over ALL cards), routes every
-    transaction to the GPU owning its card (fdengine.sharding.ShardedScorer: partition kernel ->
-    all-to-all of 48-B records -> owner scores features + XGBoost + IsolationForest + blend ->
-    all-to-all of 24-B results back -> scatter to arrival order). Cards: 100M over the node (each GPU
-    holds only the cards it owns). At N=1 the same kernels run with no collective."""
+    """BASELINE configs[3] (the metric's configuration): card-hash-sharded keyed state + scoring, RCCL
+    all-to-all routing. Each rank ingests its own 64k-txn micro-batch per step (drawn over ALL cards) and
+    routes every transaction to the GPU owning its card (fdengine.sharding.ShardedScorer). Cards: 100M
+    over the node (each GPU holds only the cards it owns). At N=1 the same kernels run with no collective."""
     name = "config4"
 
     def __init__(self, args, rank, dev, eng):
         import numpy as np
         import torch
-        import fdengine
         from fdengine import _native as N
         from fdengine import synth
         from fdengine.sharding import EngineShardBackend, ShardedScorer
-        from oracle import scoring_ref as S
-        self.np, self.torch, self.N, self.S = np, torch, N, S
+        self.np, self.torch, self.N = np, torch, N
         self.B, self.T, self.D = args.batch, args.trees, args.depth
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = rank
@@ -437,27 +452,13 @@ class Config4(Config3):
         self.eng = eng
         t = time.time()
         self.merchants = synth.merchants_table(5000, seed=100)
-        # models fitted on realistic scoring vectors (same recipe as config 3)
-        from oracle.features_c import OracleFeatureState
-        spop = synth.population(20000, 500, seed=11)
-        stx = synth.txn_stream(spop, 40000, seed=12, rate_per_s=20.0)
-        so = OracleFeatureState(1 << 16, self.mode, self.K)
-        so.load_users(spop["users"]["key"], spop["users"]["avg_amount"], spop["users"]["account_age_days"],
-                      spop["users"]["device_fp"])
-        so.load_merchants(spop["merchants"]["fraud_rate"], spop["merchants"]["risk_multiplier"])
-        _, Xref = so.run(stx, want_raw=False)
-        del so
-        self.xgb = fdengine.xgboost_from_json_doc(synth.xgboost_doc(self.T, self.D, 64, Xref[-8192:], seed=13))
-        self.ifm = fdengine.iforest_from_sklearn(synth.isolation_forest(Xref[-8192:].astype(np.float64)))
+        self.xgb, self.ifm = fit_models(dev.index, self.T, self.D, self.mode, self.K)
         eng.load_forest(0, self.xgb)
         eng.load_forest(1, self.ifm)
         self.names = ["xgboost_primary", "isolation_forest"]
-        w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
-        self.weights = [w[n] for n in self.names]
-        self.mults = [S.CONF_MULT[n] for n in self.names]
-        self.params = fdengine.FraudEngine.blend_params(self.weights, self.mults)
-        # this GPU's cards
-        own = synth.owned_cards(self.cards, rank, self.world, seed=42)
+        self.with_lstm = False
+        self.params, self.weights, self.mults = product_blend(self.names)
+        own = synth.owned_cards(self.cards, rank, self.world, seed=42)  # this GPU's cards
         self.n_owned = len(own["key"])
         cap = 1
         while cap < int(self.n_owned * 1.6) + 65536:
@@ -468,7 +469,8 @@ class Config4(Config3):
         del own
         eng.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
         # this rank's ingest stream (over all cards), resident in HBM
-        self.n_batches = args.warmup + args.steps + args.latency_iters + 1
+        self.parity_batches = args.parity_batches
+        self.n_batches = args.warmup + args.steps + args.latency_iters + args.parity_batches + 1
         self.tx = synth.txn_stream_cards(self.cards, self.merchants, self.n_batches * self.B, seed=200 + rank,
                                          card_seed=42, rate_per_s=2000.0)
         self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
@@ -498,33 +500,38 @@ class Config4(Config3):
         self.h_risk.copy_(risk, non_blocking=True)
 
     def parity(self):
-        """N=1 only: batch 0 (fresh state) through the oracle chain. The oracle state holds just the
-        profiles of the cards batch 0 touches (identical results, bounded host memory at 100M cards).
-        The N>1 exchange is checked by tests/test_sharding.py (gloo) and tests/test_gpu_sharding.py."""
+        """N=1: the first parity_batches micro-batches (fresh state carried across them) through the oracle
+        chain. The oracle state holds just the profiles of the cards those batches touch (identical results,
+        bounded host memory at 100M cards). N>1: every rank steps the same number of batches (the exchange
+        is checked by tests/test_sharding.py, gloo, and tests/test_gpu_sharding.py)."""
         if self.world > 1:
-            self.step(0)
+            for _ in range(self.parity_batches):
+                self.step(0)
             return None
         import oracle
         from fdengine import synth
         from oracle.features_c import OracleFeatureState
         np = self.np
-        part = {f: self.tx[f][:self.B] for f in self.N.TXN_FIELDS}
-        self.step(0)
-        self.torch.cuda.synchronize()
-        o = OracleFeatureState(1 << 18, self.mode, self.K)
-        ids_keys = np.unique(part["card_key"])
-        at = synth.card_attrs(self.tx["card_id"][:self.B], 42)  # the profiles of the cards batch 0 touches
+        P, B = self.parity_batches, self.B
+        o = OracleFeatureState(1 << 20, self.mode, self.K)
+        at = synth.card_attrs(self.tx["card_id"][:P * B], 42)  # the profiles of the cards these batches touch
         _, first = np.unique(at["key"], return_index=True)
         o.load_users(at["key"][first], at["avg_amount"][first], at["account_age_days"][first], at["device_fp"][first])
         o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
-        _, V = o.run(part, want_raw=False)
+        out = {"batches_checked": P, "max_abs_prob_diff": 0.0, "decision_mismatches": 0, "risk_mismatches": 0}
+        for b in range(P):
+            part = {f: self.tx[f][b * B:(b + 1) * B] for f in self.N.TXN_FIELDS}
+            self.step(b)
+            self.torch.cuda.synchronize()
+            _, V = o.run(part, want_raw=False)
+            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
+            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
+            fp, _, dec, risk = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults)
+            out["max_abs_prob_diff"] = max(out["max_abs_prob_diff"], float(np.abs(self.out[0].cpu().numpy() - fp).max()))
+            out["decision_mismatches"] += int((self.out[2].cpu().numpy() != dec).sum())
+            out["risk_mismatches"] += int((self.out[3].cpu().numpy() != risk).sum())
         del o
-        px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
-        pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
-        fp, _, dec, _ = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults)
-        got_fp, got_dec = self.out[0].cpu().numpy(), self.out[2].cpu().numpy()
-        return {"max_abs_prob_diff": float(np.abs(got_fp - fp).max()),
-                "decision_mismatches": int((got_dec != dec).sum()), "cards_touched": int(len(ids_keys))}
+        return out
 
     def config(self, world):
         return {"workload": "config4: card-hash-sharded keyed state (fmix64 owner) + RCCL all-to-all routing "
@@ -532,36 +539,9 @@ class Config4(Config3):
                             "IsolationForest 100 + blend on the owner, 64k-txn micro-batch per GPU per step",
                 "cards": self.cards, "cards_per_gpu": self.n_owned, "window_mode": "sliding" if self.mode else
                 "redis_compat", "ring_k": self.K, "trees": self.T, "depth": self.D, "features": 64,
-                "batch_per_gpu": self.B, "parallelism": f"card-hash shards x{world}, RCCL all-to-all"}
-
-    def cpu_baseline(self, seconds):
-        """Oracle chain on the first transactions of this rank's stream (N=1)."""
-        import oracle
-        from fdengine import synth
-        from oracle.features_c import OracleFeatureState
-        np = self.np
-        th = cpu_threads()
-        o = OracleFeatureState(1 << 22, self.mode, self.K)
-        chunk = 16384
-        done, a = 0, time.perf_counter()
-        u = self.tx["card_id"][:1 << 21]
-        at = synth.card_attrs(u, 42)
-        _, first = np.unique(at["key"], return_index=True)
-        o.load_users(at["key"][first], at["avg_amount"][first], at["account_age_days"][first], at["device_fp"][first])
-        o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
-        a = time.perf_counter()
-        while time.perf_counter() - a < seconds and done + chunk <= len(u):
-            part = {f: self.tx[f][done:done + chunk] for f in self.N.TXN_FIELDS}
-            _, V = o.run(part, want_raw=False)
-            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=th)
-            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=th)
-            oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults, nthreads=th)
-            done += chunk
-        dt = time.perf_counter() - a
-        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
-                "sample": f"first {done} txns of the config-4 stream through the oracle chain (features C "
-                          f"single-threaded + XGBoost + IsolationForest + blend, {th} OpenMP threads), "
-                          f"{dt:.2f} s, CPU: {cpu_model()}"}
+                "batch_per_gpu": self.B, "global_batch": self.B * world,
+                "parallelism": f"card-hash shards x{world}, RCCL all-to-all" if world > 1 else
+                "1 shard (all cards on one GPU; routing kernels, no collective)"}
 
 
 # --------------------------------------------------------------------------------------- ingest
@@ -590,8 +570,7 @@ class Ingest:
         buf, off = pack(self.msgs)
         self.nbytes = int(off[-1])
         self.pool = max(1, args.pool)
-        # pool copies at distinct addresses (same content; 16-B aligned strides)
-        stride = (self.nbytes + 4095) & ~4095
+        stride = (self.nbytes + 4095) & ~4095  # pool copies at distinct addresses (16-B aligned strides)
         host = np.zeros(self.pool * stride, np.uint8)
         for p in range(self.pool):
             host[p * stride:p * stride + self.nbytes] = buf
@@ -683,34 +662,21 @@ class Config3J(Config3):
     def __init__(self, args, rank, dev, eng):
         import numpy as np
         import torch
-        import fdengine
         from fdengine import _native as N
         from fdengine import synth
         from fdengine.ingest import IngestCodec, device_columns, pack
-        from oracle.features_c import OracleFeatureState
-        from oracle import scoring_ref as S
-        self.np, self.torch, self.N, self.S = np, torch, N, S
+        self.np, self.torch, self.N = np, torch, N
         self.B, self.T, self.D = args.batch, args.trees, args.depth
         self.cards, self.mode, self.K = args.cards, (1 if args.window == "sliding" else 0), args.ring_k
         self.eng = eng
+        self.with_lstm = False
         t = time.time()
-        spop = synth.population(20000, 500, seed=11)
-        stx = synth.txn_stream(spop, 40000, seed=12, rate_per_s=20.0)
-        so = OracleFeatureState(1 << 16, self.mode, self.K)
-        so.load_users(spop["users"]["key"], spop["users"]["avg_amount"], spop["users"]["account_age_days"],
-                      spop["users"]["device_fp"])
-        so.load_merchants(spop["merchants"]["fraud_rate"], spop["merchants"]["risk_multiplier"])
-        _, Xref = so.run(stx, want_raw=False)
-        self.xgb = fdengine.xgboost_from_json_doc(synth.xgboost_doc(self.T, self.D, 64, Xref[-8192:], seed=13))
-        self.ifm = fdengine.iforest_from_sklearn(synth.isolation_forest(Xref[-8192:].astype(np.float64)))
+        self.xgb, self.ifm = fit_models(dev.index, self.T, self.D, self.mode, self.K)
         eng.load_forest(0, self.xgb)
         eng.load_forest(1, self.ifm)
         self.names = ["xgboost_primary", "isolation_forest"]
         self.slots = [0, 1]
-        w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
-        self.weights = [w[n] for n in self.names]
-        self.mults = [S.CONF_MULT[n] for n in self.names]
-        self.params = fdengine.FraudEngine.blend_params(self.weights, self.mults)
+        self.params, self.weights, self.mults = product_blend(self.names)
         # users keyed as the codec keys them: fd_hash64("user_xxxxxxxx"), fingerprints fd_hash64("fp-xxxxxxxx")
         idx = np.arange(self.cards, dtype=np.uint64)
         self.ukeys = synth.hash64_fixed(synth.fixed_ids("user_", idx))
@@ -762,31 +728,23 @@ class Config3J(Config3):
                                     self.conf.data_ptr(), self.dec.data_ptr(), self.risk.data_ptr(),
                                     vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
 
-    def _oracle_state(self):
-        from oracle.features_c import OracleFeatureState
-        o = OracleFeatureState(self.cap, self.mode, self.K)
-        o.load_users(self.ukeys, self.uavg, self.uage, self.ufp)
-        o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
-        return o
-
-    def _oracle_txns(self, msgs):
-        from oracle import ingest_ref as R
-        from fdengine import synth
-        cols = R.parse_batch(msgs, {m: i for i, m in enumerate(self.merchant_ids)},
-                             [{s: i for i, s in enumerate(v)} for v in (synth.SIM_PAYMENT_METHODS,
-                                                                         synth.SIM_TXN_TYPES, synth.SIM_CARD_TYPES)])
-        return {f: cols[f] for f in self.N.TXN_FIELDS}
-
     def parity(self):
         """Batch 0 (fresh state): oracle ingest -> oracle features -> forests -> blend, first 8192 rows."""
         import oracle
+        from fdengine import synth
+        from oracle import ingest_ref as R
+        from oracle.features_c import OracleFeatureState
         np = self.np
         k = 8192
-        o = self._oracle_state()
+        o = OracleFeatureState(self.cap, self.mode, self.K)
+        o.load_users(self.ukeys, self.uavg, self.uage, self.ufp)
+        o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
         self.step(0)
         self.torch.cuda.synchronize()
-        part = self._oracle_txns(self.msgs[0][:k])
-        _, rvec = o.run(part, want_raw=False)
+        cols = R.parse_batch(self.msgs[0][:k], {m: i for i, m in enumerate(self.merchant_ids)},
+                             [{s: i for i, s in enumerate(v)} for v in (synth.SIM_PAYMENT_METHODS,
+                                                                         synth.SIM_TXN_TYPES, synth.SIM_CARD_TYPES)])
+        _, rvec = o.run({f: cols[f] for f in self.N.TXN_FIELDS}, want_raw=False)
         del o
         V = self.vec[:k].cpu().numpy()
         px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
@@ -804,7 +762,7 @@ class Config3J(Config3):
         return out
 
     def roofline(self, timing):
-        """The dominant kernel of this line is the JSON codec (≈1.1 ms of the ≈1.35 ms step), not the forest."""
+        """The dominant kernel of this line is the JSON codec, not the forest."""
         ms, launches = timing[self.N.FD_TIMING_INGEST]
         avg = (ms / 1e3) / max(1, launches)
         per_launch = self.nbytes[0] + 8 * (self.B + 1) + Ingest.OUT_BYTES * self.B
@@ -823,29 +781,31 @@ class Config3J(Config3):
         d["avg_message_bytes"] = round(self.nbytes[0] / self.B, 1)
         return d
 
-    def cpu_baseline(self, seconds):
-        """The oracle chain from raw JSON: json.loads + mapping (1 core) -> features (C, sequential) ->
-        forests + blend (OpenMP), on the first messages of batch 0 (bounded sample)."""
-        import oracle
-        np = self.np
-        th = cpu_threads()
-        o = self._oracle_state()
-        chunk, done, a = 2048, 0, time.perf_counter()
-        while time.perf_counter() - a < seconds and done + chunk <= self.B:
-            part = self._oracle_txns(self.msgs[0][done:done + chunk])
-            _, V = o.run(part, want_raw=False)
-            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=th)
-            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=th)
-            oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults, nthreads=th)
-            done += chunk
-        dt = time.perf_counter() - a
-        return {"value": round(done / dt, 1), "unit": "txn/s", "cores": th, "kind": "port",
-                "sample": f"first {done} messages of batch 0 through the oracle chain (json.loads + mapping 1 core, "
-                          f"features C 1 core, XGBoost + IsolationForest + blend {th} OpenMP threads), {dt:.2f} s, "
-                          f"CPU: {cpu_model()}"}
+
+WORKLOADS = {"config2": Config2, "config3": Config3, "config4": Config4, "config5": Config5, "ingest": Ingest,
+             "config3j": Config3J}
 
 
-WORKLOADS = {"config2": Config2, "config3": Config3, "config4": Config4, "config5": Config5, "ingest": Ingest, "config3j": Config3J}
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside torchrun: start N ranks (one process per GPU) with torch.distributed.run
+    as children — before this process touches the GPU — and return their exit code."""
+    import torch  # device_count() does not initialise the GPU on this image
+    visible = torch.cuda.device_count()
+    if n > visible:
+        log(f"--gpus {n} but only {visible} GPU(s) visible: refusing to oversubscribe")
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    log("[bench] launching ranks:", " ".join(cmd))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -853,28 +813,33 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
-    ap.add_argument("--batch", type=int, default=None, help="micro-batch (default 64k; config5: 1k)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config4")
+    ap.add_argument("--batch", type=int, default=None, help="micro-batch per GPU (default 64k; config5: 1k)")
     ap.add_argument("--trees", type=int, default=500)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--features", type=int, default=50)
-    ap.add_argument("--pool", type=int, default=8, help="config2: distinct HBM-resident micro-batches cycled")
+    ap.add_argument("--pool", type=int, default=8, help="config2/ingest: distinct HBM-resident micro-batches cycled")
     ap.add_argument("--cards", type=int, default=None,
-                    help="cards resident in HBM (config3 default 10M; config4 default 100M over the node)")
+                    help="cards resident in HBM (config4 default 100M over the node; config3 default 10M)")
     ap.add_argument("--window", choices=["sliding", "redis"], default="sliding")
     ap.add_argument("--ring-k", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=200)
+    ap.add_argument("--parity-batches", type=int, default=2)
     args = ap.parse_args()
     if args.batch is None:
         args.batch = 1024 if args.workload == "config5" else 65536
     if args.cards is None:
         args.cards = 100_000_000 if args.workload == "config4" else 10_000_000
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[rank {rank}] note: --gpus {args.gpus} but WORLD_SIZE={world}; n_gpus reports the ranks running")
 
     import numpy as np
     import torch
@@ -885,7 +850,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank)
+        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
+                                device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -898,9 +864,7 @@ def main():
     try:
         parity = wl.parity()
     except Exception as e:  # the oracle is only a checker; report, never fall back
-        log(f"[rank {rank}] parity spot-check unavailable: {e}")
-    if args.workload == "config3":  # parity consumed batch 0 of the stream with fresh state
-        pass
+        log(f"[rank {rank}] parity spot-check unavailable: {e!r}")
 
     for i in range(args.warmup):
         wl.step(i)
@@ -935,6 +899,11 @@ def main():
         stream.synchronize()
         lat.append(time.perf_counter() - a)
     lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
+    p99 = float(np.percentile(lat_ms, 99))
+    if dist:  # the node's p99: the worst rank's
+        t = torch.tensor([p99], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        p99 = float(t.item())
 
     value = world * args.steps * args.batch / elapsed
     cpu = None
@@ -942,6 +911,7 @@ def main():
         cpu = wl.cpu_baseline(args.cpu_seconds)
 
     if rank == 0:
+        roof = wl.roofline(timing)
         line = {
             "metric": "scored transactions/sec (whole node)",
             "value": round(value, 1),
@@ -958,12 +928,19 @@ def main():
                     "reference's file formats)",
             "config": wl.config(world),
             "p50_batch_latency_ms": round(float(np.percentile(lat_ms, 50)), 4),
-            "p99_batch_latency_ms": round(float(np.percentile(lat_ms, 99)), 4),
-            "roofline": wl.roofline(timing),
+            "p99_batch_latency_ms": round(p99, 4),
+            "roofline": roof,
             "kernel_avg_us": wl.kernels(timing),
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
         }
+        if wl.name in ("config3", "config4", "config5"):
+            per_gpu = value / world
+            line["pipeline_hbm"] = {"bytes_per_txn": FUSED_BYTES_PER_TXN,
+                                    "achieved_GBs_per_gpu": round(per_gpu * FUSED_BYTES_PER_TXN / 1e9, 3),
+                                    "peak_GBs": HBM_PEAK_GBS,
+                                    "frac": round(per_gpu * FUSED_BYTES_PER_TXN / 1e9 / HBM_PEAK_GBS, 6),
+                                    "basis": "SURVEY §8(d) fused-pipeline algorithmic bytes x txn/s per GPU"}
         print(json.dumps(line), flush=True)
     eng.close()
     if dist:

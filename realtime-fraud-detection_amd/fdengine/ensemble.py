@@ -5,7 +5,7 @@
   failing models dropped (:150-183), clamp + confidence (:185-219, 325-342), weighted-average /
   voting / stacking (:252-323), decision / risk level (:344-369), explanation (:371-435).
 * `predict_batch(features_list)` is the micro-batch path the reference lacks (its /batch-predict
-  loops one transaction at a time, ml/main.py:235-249): one scoring-vector matrix, every
+  loops one transaction at a time, ml/main.py:235-249): one scoring-vector matrix per vector width, every
   device-resident forest scores it in one launch each, and the blend/decision/risk epilogue runs
   on the GPU (fd_score_matrix_host). Results equal per-transaction `predict` for the same inputs
   (host stand-in models aside, which are random in the reference too); the cache is bypassed.
@@ -250,6 +250,8 @@ class EnsemblePredictor:
                 ok, slot = 0, -1  # flat vectors carry no sequence: dropped, as the reference's LSTM is
             elif mm.models[name].kind == "xgboost" and X.shape[1] > mm.models[name].num_feature:
                 ok = 0  # XGBoost rejects wider matrices; the reference drops the model
+            elif mm.models[name].kind == "isolation_forest" and X.shape[1] != mm.models[name].num_feature:
+                ok = 0  # sklearn's n_features_in_ check raises ValueError; the reference drops the model
             slots.append(slot)
             ext.append(col)
             present.append(ok)
@@ -264,20 +266,39 @@ class EnsemblePredictor:
         t0 = time.time()
         if not features_list:
             return []
-        X = prepare_matrix(features_list)
-        r = self.score_matrix(X)
+        # The reference scores each transaction's own vector: rows are grouped by their unpadded width (one
+        # group in practice, 64), so a wide row only changes which models score THAT row.
+        rows = [prepare_features(f)[0] for f in features_list]
+        groups: Dict[int, List[int]] = {}
+        for i, r in enumerate(rows):
+            groups.setdefault(len(r), []).append(i)
+        scored = {}
+        for width, idx in groups.items():
+            X = np.stack([rows[i] for i in idx])
+            try:
+                r = self.score_matrix(X)
+            except ValueError:
+                if len(groups) == 1:
+                    raise
+                r = None  # no model could score this width: those rows fail below, as predict() would
+            for j, i in enumerate(idx):
+                scored[i] = (r, j)
         per_txn_ms = (time.time() - t0) * 1000 / len(features_list)
         out = []
-        live = [i for i, ok in enumerate(r["present"]) if ok]
         for i, f in enumerate(features_list):
+            r, j = scored[i]
+            if r is None:
+                raise ValueError("No model predictions available")
             preds = []
-            for m in live:
-                p = max(0.0, min(1.0, float(r["model_probs"][m, i])))
+            for m, ok in enumerate(r["present"]):
+                if not ok:
+                    continue
+                p = max(0.0, min(1.0, float(r["model_probs"][m, j])))
                 preds.append((r["models"][m], p, self._calculate_model_confidence(p, r["models"][m])))
-            fp = float(r["fraud_probability"][i])
+            fp = float(r["fraud_probability"][j])
             out.append({
-                "fraud_probability": fp, "fraud_score": fp, "confidence": float(r["confidence"][i]),
-                "risk_level": N.RISK_LEVELS[r["risk"][i]], "decision": N.DECISIONS[r["decision"][i]],
+                "fraud_probability": fp, "fraud_score": fp, "confidence": float(r["confidence"][j]),
+                "risk_level": N.RISK_LEVELS[r["risk"][j]], "decision": N.DECISIONS[r["decision"][j]],
                 "model_predictions": {n: p for n, p, _ in preds}, "model_confidences": {n: c for n, _, c in preds},
                 "explanation": self._generate_explanation(preds, f) if self.enable_explanation else {},
                 "ensemble_strategy": self.strategy.value, "processing_time_ms": per_txn_ms,

@@ -27,6 +27,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import os
+from concurrent.futures import ThreadPoolExecutor
 from datetime import datetime
 from typing import Any, Dict, Optional
 
@@ -100,6 +101,9 @@ class ModelManager:
         self.model_load_times: Dict[str, datetime] = {}
         self.model_lock = asyncio.Lock()
         self.engine = engine if engine is not None else FraudEngine(_default_device() if device is None else device)
+        # GPU round trips run off the event loop (uvicorn's single loop stays responsive); one
+        # worker thread serialises the calls on this engine (ctypes releases the GIL for their duration)
+        self._executor = ThreadPoolExecutor(max_workers=1, thread_name_prefix="fdengine")
         names = list(config.models.keys())
         self._slot_of = {name: i for i, name in enumerate(names)}  # one engine slot per registry entry
 
@@ -167,7 +171,9 @@ class ModelManager:
         model = self.models[model_name]
         cfg = self.config.get_model_config(model_name)
         try:
-            return self.predict_sync(model_name, model, cfg.model_type, features)
+            loop = asyncio.get_running_loop()
+            return await loop.run_in_executor(self._executor, self.predict_sync, model_name, model, cfg.model_type,
+                                              features)
         except Exception as e:
             self.logger.error(f"prediction failed: {e}", extra={"model_name": model_name, "model_type": cfg.model_type,
                                                                 "features_shape": getattr(features, "shape", None)})
@@ -187,6 +193,9 @@ class ModelManager:
                 if X.shape[1] > model.num_feature:  # XGBoost's Learner::ValidateDMatrix
                     raise ValueError(f"Feature shape mismatch, expected: {model.num_feature}, got {X.shape[1]}")
                 return self.engine.predict(model.slot, X).astype(np.float32)
+            if X.shape[1] != model.num_feature:  # sklearn's validate_data(reset=False) n_features_in_ check
+                raise ValueError(f"X has {X.shape[1]} features, but IsolationForest is expecting "
+                                 f"{model.num_feature} features as input.")
             return self.engine.predict(model.slot, X)
         # reference branches for the DummyModel stand-ins (model_manager.py:288-300, 313-336)
         if model_type == "xgboost":

@@ -43,6 +43,9 @@ class EngineShardBackend:
         self.torch = torch
         self.eng, self.params, self.slots, self.present = eng, params, list(slots), present
         self.device = torch.device("cuda", eng.device)
+        # The engine's kernels and the collectives must be ordered on ONE stream: bind the engine to the
+        # stream torch (and so RCCL's all_to_all and .cpu()) uses on this device.
+        eng.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
     def partition(self, txns: dict, n: int, G: int):
         t = self.torch
@@ -65,12 +68,19 @@ class EngineShardBackend:
     def restore(self, path: str, rank: int, world: int) -> int:
         return self.eng.state_restore(path, rank, world, skip_windows=True, skip_sink=True)
 
-    def scatter_results(self, res, n: int):
+    def scatter_results(self, res, n: int, sentinel: bool = False):
+        """sentinel: pre-fill the outputs (NaN probability, decision/risk 255) so a row no result record
+        reached (a mismatched exchange) cannot pass for a score."""
         t = self.torch
-        fp = t.empty(n, dtype=t.float64, device=self.device)
+        if sentinel:
+            fp = t.full((n,), float("nan"), dtype=t.float64, device=self.device)
+            dec = t.full((n,), 255, dtype=t.uint8, device=self.device)
+            risk = t.full((n,), 255, dtype=t.uint8, device=self.device)
+        else:
+            fp = t.empty(n, dtype=t.float64, device=self.device)
+            dec = t.empty(n, dtype=t.uint8, device=self.device)
+            risk = t.empty(n, dtype=t.uint8, device=self.device)
         conf = t.empty(n, dtype=t.float64, device=self.device)
-        dec = t.empty(n, dtype=t.uint8, device=self.device)
-        risk = t.empty(n, dtype=t.uint8, device=self.device)
         if n:
             self.eng.route_scatter_results_device(res.data_ptr(), n, fp.data_ptr(), conf.data_ptr(),
                                                   dec.data_ptr(), risk.data_ptr())
@@ -109,7 +119,7 @@ class ShardedScorer:
         res = self.be.score_records(inbox, m)
         back = torch.empty((n, RES), dtype=torch.uint8, device=rec.device)
         self._a2a(back, res, send, recv)
-        return self.be.scatter_results(back, n)
+        return self.be.scatter_results(back, n, sentinel=True)
 
     # ------------------------------------------------------------------ checkpoint / rescale
     # Counterpart of Flink's externalized keyed-state checkpoints (fl/FraudDetectionJob.java:112-136):

@@ -93,3 +93,53 @@ def test_model_manager_contract(model_dir):
     assert info["total_models"] == 3
     asyncio.run(mm.cleanup())
     assert not mm.is_model_loaded("xgboost_primary")
+
+
+def test_wide_vectors_drop_models_per_row(model_dir):
+    """A Flink `features` sub-dict can push a row's vector past 64 columns. The reference scores each
+    transaction's own vector: XGBoost rejects > num_feature columns and sklearn's IsolationForest any
+    width != n_features_in_, so for THAT row both are dropped (-> "No model predictions available"), while
+    the batch's 64-wide rows keep both models (per-row, not per-batch, width handling)."""
+    cfg, mm, ep = _stack(model_dir)
+    xgb, ifm = _oracle_models(model_dir)
+    cases = [c for c in json.loads((GOLDEN / "feature_processor_cases.json").read_text()) if "vector" in c][:20]
+    processed = [FR.process_features(c["raw"]) for c in cases]
+    X = np.array([c["vector"] for c in cases])
+    narrow = asyncio.run(ep.predict_batch(processed))
+    wide = dict(processed[0], features={f"flink_{k}": 0.25 for k in range(40)})
+    from fdengine.ensemble import prepare_features
+    assert prepare_features(wide).shape[1] > 64
+    with pytest.raises(ValueError):
+        asyncio.run(ep.predict(dict(wide, transaction_id="wide-single")))  # every model dropped
+    with pytest.raises(ValueError):
+        asyncio.run(ep.predict_batch(processed[:5] + [wide]))  # that row has no model, as predict() raises
+    # a 64-wide row whose sub-dict keeps it <= 64 columns is unaffected; the others score as before
+    px, _, _ = oracle.xgb_predict(xgb, X)
+    pi, _, _ = oracle.iforest_predict(ifm, X)
+    for i, r in enumerate(narrow):
+        fp, _, _, _ = S.blend_row(["xgboost_primary", "isolation_forest"], [float(px[i]), float(pi[i])],
+                                  ep.model_weights)
+        assert abs(r["fraud_probability"] - fp) <= 1e-5
+    with pytest.raises(ValueError):  # IsolationForest: any width != n_features_in_
+        asyncio.run(mm.predict("isolation_forest", np.zeros((2, 63))))
+
+
+def test_predict_runs_off_the_event_loop(model_dir):
+    """ModelManager.predict awaits the GPU call in an executor: other coroutines progress meanwhile."""
+    cfg, mm, ep = _stack(model_dir)
+    X = np.zeros((4096, 64))
+    ticks = []
+
+    async def ticker():
+        for _ in range(50):
+            ticks.append(1)
+            await asyncio.sleep(0)
+
+    async def main():
+        t = asyncio.create_task(ticker())
+        p = await mm.predict("xgboost_primary", X)
+        await t
+        return p
+
+    p = asyncio.run(main())
+    assert p.shape == (4096,) and len(ticks) == 50

@@ -110,7 +110,7 @@ class OracleShardBackend:
         self.scored += m
         return self.torch.from_numpy(res.view(np.uint8).reshape(m, 24).copy())
 
-    def scatter_results(self, res, n):
+    def scatter_results(self, res, n, sentinel=False):
         out = R.scatter_results(res.numpy().reshape(-1).view(R.RESULT))
         return tuple(self.torch.from_numpy(a) for a in out)
 
