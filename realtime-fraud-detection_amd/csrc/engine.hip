@@ -210,7 +210,7 @@ int fd_engine_destroy(fd_engine* eng) {
   e.feat_in.release();
   fd::windows_release(e);
   fd::sink_release(e);
-  for (auto* b : {&e.route_blk, &e.route_soa, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.bias,
+  for (auto* b : {&e.route_blk, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.bias,
                   &e.lstm.wout, &e.lstm.bout, &e.state.seq})
     b->release();
   if (e.aux_stream) {
@@ -233,8 +233,8 @@ int fd_engine_destroy(fd_engine* eng) {
       t.vvals[w].release();
     }
   }
-  for (auto* b : {&e.state.headers, &e.state.fps, &e.state.ring, &e.state.merchants, &e.state.slot,
-                  &e.state.next, &e.state.err})
+  for (auto* b : {&e.state.headers, &e.state.ring, &e.state.merchants, &e.state.slot, &e.state.err,
+                  &e.state.bucket_cnt, &e.state.bucket_fill, &e.state.bucket_base, &e.state.pairs})
     b->release();
   for (auto& ev : e.events) {
     (void)hipEventDestroy(ev.a);
@@ -1015,8 +1015,6 @@ int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const
     FD_REQUIRE(slots[m] >= 0 || (present && !present[m]), FD_ERR_INVALID_ARG,
                "routed scoring needs every present model in a forest slot or FD_SLOT_LSTM");
   if (n == 0) return FD_OK;
-  unsigned* seq = nullptr;
-  const fd_txn_batch t = fd::launch_route_unpack(e, d_records, n, &seq);
   e.feat_vec.ensure((size_t)n * FD_VECTOR_WIDTH * 4);
   e.route_out.ensure((size_t)n * (2 * sizeof(double) + 2));
   double* fp = e.route_out.as<double>();
@@ -1024,10 +1022,10 @@ int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const
   uint8_t* dec = reinterpret_cast<uint8_t*>(conf + n);
   uint8_t* risk = dec + n;
   float* sq = lstm_seq_buffer(e, *params, slots, present, n);
-  fd::launch_features(e, t, n, e.feat_vec.as<float>(), nullptr, sq);
+  fd::launch_features_records(e, d_records, n, e.feat_vec.as<float>(), sq);  // reads the records in place
   score_matrix(e, *params, slots, nullptr, present, e.feat_vec.as<float>(), n, FD_VECTOR_WIDTH, nullptr, fp, conf,
                dec, risk, sq, e.state.S);
-  fd::launch_result_pack(e, fp, conf, dec, risk, seq, n, d_results);
+  fd::launch_result_pack(e, fp, conf, dec, risk, static_cast<const fd::RouteRecord*>(d_records), n, d_results);
   FD_API_END
 }
 

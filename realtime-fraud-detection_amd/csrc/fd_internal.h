@@ -130,6 +130,30 @@ struct LstmModel {
   DeviceBuffer wpk, bias, wout, bout;
 };
 
+// One card's keyed state header (features.hip): 128 B = one L2 line, so a transaction's state read and
+// write-back touch one line. Line 0 is what every mode reads (key, profile, ring cursor, window counts,
+// device fingerprints); line 1 the sliding-window sums / oldest times and the redis_compat session.
+struct __attribute__((aligned(128))) CardHeader {
+  unsigned long long key;          // 0 = empty slot
+  long long last_ts;               // time of the card's last event (sliding: last appended; redis: last write)
+  double avg;                      // profile: avg_transaction_amount (NaN = null)
+  int age;                         // profile: account_age_days
+  unsigned flags;                  // bit 0 user profile; bit 1 redis session live; bits 8-15 LSTM events held;
+                                   // bits 16-23 LSTM history write position
+  unsigned char ring_n, ring_head; // sliding: events held (<= K), next write position
+  unsigned char unsorted;          // sliding: appends left before the ring is time-sorted again (0 = sorted)
+  unsigned char pad0;
+  unsigned char wc[3], pad1;       // sliding: events of the ring's newest suffix inside the 5m / 1h / 24h window
+  unsigned long long fp[3];        // profile: device fingerprints (0 = none)
+  long long ws[3];                 // sliding: window sums (cents)
+  long long wo[3];                 // sliding: time of the oldest in-window event (valid when wc > 0)
+  long long rc_sum;                // redis_compat: session amount (cents)
+  int rc_cnt;                      // redis_compat: session count
+  int pad2;
+};
+static_assert(sizeof(CardHeader) == 128, "CardHeader must be one 128-B line");
+constexpr int kCardHeaderBytes = (int)sizeof(CardHeader);
+
 // HBM-resident keyed card state (features.hip)
 struct CardStore {
   bool ready = false;
@@ -137,9 +161,9 @@ struct CardStore {
   int mode = 0;      // fd_window_mode
   int K = 1;         // ring events per card (sliding)
   int S = 0;         // LSTM history events per card (0 = off)
-  unsigned epoch = 0;
   int64_t n_merchants = 0;
-  DeviceBuffer headers, fps, ring, merchants, slot, next, err, seq;
+  DeviceBuffer headers, ring, merchants, slot, err, seq;
+  DeviceBuffer bucket_cnt, bucket_fill, bucket_base, pairs;  // per-batch card grouping (feat_slot/scatter/bucket)
   DeviceBuffer uext, mext, vocab;  // extended profiles + vocabulary flags (feature map, rule scores)
   int64_t n_mext = 0;
   bool vocab_loaded = false;
@@ -201,7 +225,7 @@ struct Engine {
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
-  DeviceBuffer route_blk, route_soa, route_out, route_err;  // card-hash routing scratch (route.hip)
+  DeviceBuffer route_blk, route_out, route_err;  // card-hash routing scratch (route.hip)
   bool route_err_live = false;
   // optional per-launch kernel timing (HIP events on the launch stream)
   int forest_variant = 0;  // "forest_kernel" option
@@ -266,6 +290,8 @@ void load_users(Engine& e, const fd_users& u);
 void load_merchants(Engine& e, const fd_merchants& m);
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw,
                      float* d_seq = nullptr, double* d_vel5 = nullptr);
+// the same over received 48-B route records (route.hip), no unpack pass; also returns nothing else
+void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq);
 void load_users_ext(Engine& e, const fd_users_ext& u);
 void load_merchants_ext(Engine& e, const fd_merchants_ext& m);
 void load_vocab(Engine& e, const uint8_t* pay_high_risk, const uint8_t* type_refund);
@@ -275,9 +301,8 @@ void features_check(Engine& e);
 // route.hip
 unsigned shard_of_host(unsigned long long key, unsigned G);
 void launch_route_partition(Engine& e, const fd_txn_batch& t, int64_t n, int G, void* d_records, int64_t* d_counts);
-fd_txn_batch launch_route_unpack(Engine& e, const void* d_records, int64_t n, unsigned** d_seq);
 void launch_result_pack(Engine& e, const double* fp, const double* conf, const uint8_t* dec, const uint8_t* risk,
-                        const unsigned* seq, int64_t n, void* d_results);
+                        const RouteRecord* records, int64_t n, void* d_results);
 void launch_result_scatter(Engine& e, const void* d_results, int64_t n, double* fp, double* conf, uint8_t* dec,
                            uint8_t* risk);
 void route_check(Engine& e);

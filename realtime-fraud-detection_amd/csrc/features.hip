@@ -10,14 +10,23 @@
 // Declared semantics (window modes, bridge, unknown user/merchant branches): DESIGN.md "Features".
 //
 // Micro-batch semantics = the reference's per-element semantics: transactions of one card are
-// processed in arrival order, each reading the card's velocity before writing it. Two launches:
-//   feat_assign  : per txn, find-or-insert the card slot (open addressing, atomicCAS on the key),
-//                  then atomicExch the txn index into the slot's batch-list head (tagged with the
-//                  batch epoch, so no per-batch reset of the 2^k-slot table is needed);
-//   feat_process : the txn that holds the head owns the card for this batch: it walks the list in
-//                  ascending arrival order (repeated min-selection: lists are short; a card seen L
-//                  times costs O(L^2) index reads), keeps the card's state in registers, and emits
-//                  each transaction's bridged raw features and 64-wide scoring vector.
+// processed in arrival order, each reading the card's velocity before writing it. The batch is
+// sorted and segmented by card (three launches, no per-batch table reset):
+//   feat_slot    : per txn, find-or-insert the card slot (open addressing, atomicCAS on the key) and
+//                  count it into its bucket (slot mod NB; NB ~ n / 256 buckets, LDS histogram per block);
+//   feat_scatter : per txn, its (slot << 32 | arrival index) key into its bucket's range (bases by a
+//                  block-redundant scan of the NB counts);
+//   feat_bucket  : one workgroup per bucket: bitonic sort of the bucket's keys in LDS -> segments = cards
+//                  in arrival order. Segments of <= kSegLong transactions: one thread walks the card with
+//                  its 128-B header in registers; longer ones (hot cards, card-testing bursts): the whole
+//                  workgroup, 256 transactions per tile, each thread computing its transaction's windows
+//                  from an LDS tile of the card's previous K events (positional form of the sequential
+//                  definition) and the redis_compat session by a workgroup scan.
+// Sliding windows are incremental: per window the header keeps how many of the ring's newest events are
+// inside it, their cents sum and the oldest one's time, so a transaction reads ring events only to evict
+// them (canonical state: the windows as of the card's last event). A ring that is not time-sorted (an
+// out-of-order arrival) is scanned in full until the out-of-order event has left it (`unsorted` counts
+// the appends left), then the windows are rebuilt. Both forms equal oracle/oracle_features.c exactly.
 // Velocity sums are integer cents (exact); amounts leave as cents/100.0 (f64, correctly rounded).
 #include <cmath>
 #include <cstring>
@@ -27,20 +36,15 @@
 namespace fd {
 namespace {
 
-struct __attribute__((aligned(16))) CardHeader {  // 64 B: one card's header, AoS (random access per txn)
-  unsigned long long key;   // 0 = empty slot
-  unsigned long long head;  // batch list head: epoch << 32 | txn index
-  long long last_ts;        // redis_compat: time of the last velocity write (ms)
-  long long sum_cents;      // redis_compat: session amount
-  int cnt;                  // redis_compat: session count
-  int has_ts;
-  int ring_n;               // sliding: events held (<= K)
-  int ring_head;            // sliding: next write position
-  double avg;               // profile: avg_transaction_amount (NaN = null)
-  int age;                  // profile: account_age_days
-  unsigned flags;           // bit 0: has a user profile; bits 8-15 seq events held; bits 16-23 seq write pos
-};
-static_assert(sizeof(CardHeader) == 64, "CardHeader must be 64 B");
+constexpr long long kWin[3] = {300000LL, 3600000LL, 86400000LL};  // 5 min / 1 h / 24 h
+constexpr long long kSessionTtl = 3600000LL;                      // RedisService TTL 3600 s (ms)
+constexpr int kBT = 256;          // threads of the slot / scatter / bucket kernels
+constexpr int kSegLong = 16;      // segments longer than this take the cooperative path
+constexpr int kChunkCap = 4096;   // (slot, txn) keys sorted per pass in LDS
+constexpr int kMaxBuckets = 4096;
+constexpr int kMaxBins = 4096;    // arrival-range bins of an oversized bucket
+constexpr int kMaxK = 64;
+constexpr size_t kBucketLds = (size_t)kChunkCap * 8 + (size_t)(kMaxBins + 1) * 4;  // keys | bin prefix sums
 
 struct __attribute__((aligned(16))) RingEvent {
   long long ts;
@@ -76,10 +80,10 @@ __device__ long long find_or_insert(CardHeader* H, long long mask, unsigned long
   return -1;
 }
 
-__global__ void __launch_bounds__(256) users_load_kernel(CardHeader* H, unsigned long long* fps, long long mask,
-                                                         int64_t n, const unsigned long long* key,
-                                                         const double* avg, const int* age,
-                                                         const unsigned long long* dfp, unsigned* err) {
+__global__ void __launch_bounds__(256) users_load_kernel(CardHeader* H, long long mask, int64_t n,
+                                                         const unsigned long long* key, const double* avg,
+                                                         const int* age, const unsigned long long* dfp,
+                                                         unsigned* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const long long s = find_or_insert(H, mask, key[i]);
@@ -90,25 +94,131 @@ __global__ void __launch_bounds__(256) users_load_kernel(CardHeader* H, unsigned
   H[s].avg = avg[i];
   H[s].age = age[i];
   H[s].flags |= 1u;
-  for (int f = 0; f < 3; ++f) fps[s * 4 + f] = dfp[i * 3 + f];
+  for (int f = 0; f < 3; ++f) H[s].fp[f] = dfp[i * 3 + f];
 }
 
-__global__ void __launch_bounds__(256) feat_assign_kernel(CardHeader* H, long long mask, int64_t n,
-                                                          const unsigned long long* key, unsigned epoch,
-                                                          unsigned* slot, int* next, unsigned* err) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const long long s = find_or_insert(H, mask, key[i]);
-  if (s < 0) {
-    atomicOr(err, 1u);
-    slot[i] = 0xffffffffu;
-    return;
+// ------------------------------------------------------------------------------------------------
+// transaction sources: the SoA batch (fd_txn_batch) or received 48-B route records (route.hip)
+struct Txn {
+  long long ts, cents;
+  unsigned long long dfp;
+  int merchant;
+  unsigned char ipc, hour, wk;
+};
+
+struct TxnSrc {
+  const unsigned long long* key;
+  const long long* ts;
+  const long long* cents;
+  const int* merchant;
+  const unsigned long long* dfp;
+  const unsigned char* ipc;
+  const unsigned char* hour;
+  const unsigned char* wk;
+  const RouteRecord* rec;  // non-null: every field comes from the records
+  __device__ __forceinline__ unsigned long long get_key(int64_t i) const { return rec ? rec[i].key : key[i]; }
+  __device__ __forceinline__ Txn get(int64_t i) const {
+    Txn t;
+    if (rec) {
+      const RouteRecord r = rec[i];
+      t.ts = r.ts;
+      t.cents = r.cents;
+      t.dfp = r.dfp;
+      t.merchant = r.merchant;
+      t.ipc = r.ipc;
+      t.hour = r.hour;
+      t.wk = r.wk;
+    } else {
+      t.ts = ts[i];
+      t.cents = cents[i];
+      t.dfp = dfp[i];
+      t.merchant = merchant[i];
+      t.ipc = ipc[i];
+      t.hour = hour[i];
+      t.wk = wk[i];
+    }
+    return t;
   }
-  slot[i] = (unsigned)s;
-  const unsigned long long prev =
-      atomicExch(&H[s].head, ((unsigned long long)epoch << 32) | (unsigned long long)(unsigned)i);
-  next[i] = ((unsigned)(prev >> 32) == epoch) ? (int)(unsigned)(prev & 0xffffffffull) : -1;
+};
+
+// ------------------------------------------------------------------------------------------------
+// per-batch card grouping
+__global__ void __launch_bounds__(kBT) feat_slot_kernel(CardHeader* H, long long mask, int64_t n, TxnSrc src,
+                                                        unsigned nbm, unsigned* __restrict__ slot,
+                                                        unsigned* __restrict__ bucket_cnt, unsigned* err) {
+  extern __shared__ unsigned hist[];  // nbm + 1 counters
+  for (unsigned b = threadIdx.x; b <= nbm; b += kBT) hist[b] = 0u;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kBT + threadIdx.x;
+  if (i < n) {
+    const long long s = find_or_insert(H, mask, src.get_key(i));
+    if (s < 0) {
+      atomicOr(err, 1u);
+      slot[i] = 0xffffffffu;
+    } else {
+      slot[i] = (unsigned)s;
+      atomicAdd(&hist[(unsigned)s & nbm], 1u);
+    }
+  }
+  __syncthreads();
+  for (unsigned b = threadIdx.x; b <= nbm; b += kBT)
+    if (hist[b]) atomicAdd(&bucket_cnt[b], hist[b]);
 }
+
+// exclusive scan of NB counters into LDS base[] (NB <= kMaxBuckets; every block computes it)
+__device__ void block_bucket_scan(const unsigned* __restrict__ cnt, unsigned nb, unsigned* base, unsigned* part) {
+  const unsigned per = (nb + kBT - 1) / kBT, a = threadIdx.x * per;
+  unsigned s = 0;
+  for (unsigned q = 0; q < per; ++q)
+    if (a + q < nb) s += cnt[a + q];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < kBT; d <<= 1) {
+    const unsigned v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  unsigned run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+  for (unsigned q = 0; q < per; ++q)
+    if (a + q < nb) {
+      base[a + q] = run;
+      run += cnt[a + q];
+    }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kBT) feat_scatter_kernel(int64_t n, const unsigned* __restrict__ slot, unsigned nbm,
+                                                           const unsigned* __restrict__ bucket_cnt,
+                                                           unsigned* __restrict__ bucket_fill,
+                                                           unsigned* __restrict__ bucket_base,
+                                                           unsigned long long* __restrict__ pairs) {
+  extern __shared__ unsigned sh[];  // base[NB] | lcnt[NB] | lbase[NB]
+  __shared__ unsigned part[kBT];
+  const unsigned nb = nbm + 1;
+  unsigned* base = sh;
+  unsigned* lcnt = sh + nb;
+  unsigned* lbase = sh + 2 * nb;
+  for (unsigned b = threadIdx.x; b < nb; b += kBT) lcnt[b] = 0u;
+  block_bucket_scan(bucket_cnt, nb, base, part);
+  if (blockIdx.x == 0)
+    for (unsigned b = threadIdx.x; b < nb; b += kBT) bucket_base[b] = base[b];
+  const int64_t i = (int64_t)blockIdx.x * kBT + threadIdx.x;
+  const unsigned s = i < n ? slot[i] : 0xffffffffu;
+  unsigned local = 0, b = 0;
+  if (s != 0xffffffffu) {
+    b = s & nbm;
+    local = atomicAdd(&lcnt[b], 1u);
+  }
+  __syncthreads();
+  for (unsigned q = threadIdx.x; q < nb; q += kBT)
+    if (lcnt[q]) lbase[q] = atomicAdd(&bucket_fill[q], lcnt[q]);
+  __syncthreads();
+  if (s != 0xffffffffu) pairs[base[b] + lbase[b] + local] = ((unsigned long long)s << 32) | (unsigned long long)i;
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-transaction feature arithmetic (shared by the sequential and the cooperative path)
 
 // Python max(x, lo) / min(x, hi) (feature_processor.py:231-234): NaN propagates like the reference
 __device__ __forceinline__ double pmax(double x, double lo) { return (lo > x) ? lo : x; }
@@ -193,169 +303,690 @@ __device__ __forceinline__ float seq_input(double x) {
   return (float)(x < 0 ? -a : a);
 }
 
-struct TxnArgs {
-  const unsigned long long* key;
-  const long long* ts;
-  const long long* cents;
-  const int* merchant;
-  const unsigned long long* dfp;
-  const unsigned char* ipc;
-  const unsigned char* hour;
-  const unsigned char* wk;
+// the card's profile as the sequential and cooperative paths read it
+struct Profile {
+  bool has_user;
+  double avg;
+  int age;
+  unsigned long long fp[3];
 };
 
-__global__ void __launch_bounds__(256) feat_process_kernel(CardHeader* H, const unsigned long long* fps,
-                                                           RingEvent* ring, const Merchant* merchants, int nm,
-                                                           int mode, int K, int64_t n, TxnArgs t,
-                                                           const unsigned* slot, const int* next,
-                                                           float* __restrict__ vec_out,
-                                                           double* __restrict__ raw_out, float* seq_ring,
-                                                           int S, float* __restrict__ seq_out,
-                                                           double* __restrict__ vel5_out) {
+// raw features 0-8, 14, 15 of one transaction (FeatureExtractor.java:92-325 for the bridged names)
+__device__ __forceinline__ void base_raw(const Txn& t, const Profile& p, const Merchant* __restrict__ merchants, int nm,
+                                         double* r) {
 #pragma clang fp contract(off)
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const unsigned s = slot[i];
-  if (s == 0xffffffffu) return;
-  CardHeader* h = &H[s];
-  if ((unsigned)(h->head & 0xffffffffull) != (unsigned)i) return;  // not this card's owner
-  // card state in registers for the whole list
-  int cnt = h->cnt, has_ts = h->has_ts, ring_n = h->ring_n, ring_head = h->ring_head;
-  long long last_ts = h->last_ts, sum_cents = h->sum_cents;
-  unsigned flags = h->flags;
-  const bool has_user = (flags & 1u) != 0u;
-  int seq_n = (int)((flags >> 8) & 0xffu), seq_head = (int)((flags >> 16) & 0xffu);
-  float* sr = S ? seq_ring + (size_t)s * S * kSeqInput : nullptr;
-  const double uavg_raw = h->avg;
-  const int uage = h->age;
-  const unsigned long long fp0 = fps[(size_t)s * 4], fp1 = fps[(size_t)s * 4 + 1], fp2 = fps[(size_t)s * 4 + 2];
-  RingEvent* rg = ring + (size_t)s * K;
-  int last = -1;
-  for (;;) {
-    int j = (int)i, best = 0x7fffffff;  // next transaction of this card in arrival order
-    while (j >= 0) {
-      if (j > last && j < best) best = j;
-      j = next[j];
-    }
-    if (best == 0x7fffffff) break;
-    last = best;
-    const long long ts = t.ts[best];
-    const long long cents = t.cents[best];
-    double r[FD_RAW_FEATURES];
-    const double amount = (double)cents / 100.0;
-    long long days = ts / 86400000LL;
-    if (ts % 86400000LL < 0) days -= 1;
-    int hour = (int)((ts - days * 86400000LL) / 3600000LL);
-    long long dw = (days + 3) % 7;
-    if (dw < 0) dw += 7;
-    const int dow = (int)dw + 1;
-    if (t.hour[best] != 255) hour = t.hour[best];
-    const int weekend = (t.wk[best] == 255) ? (dow >= 6) : (t.wk[best] != 0);
-    const int m = t.merchant[best];
-    double mfr, mult;
-    if (m >= 0 && m < nm) {
-      const double f = merchants[m].fraud_rate;
-      mfr = isnan(f) ? 0.05 : f;
-      mult = merchants[m].mult;
-    } else {
-      mfr = 0.1;
-      mult = 2.0;
-    }
-    const unsigned long long d = t.dfp[best];
-    const bool known = has_user && d != 0ull && (d == fp0 || d == fp1 || d == fp2);
-    const unsigned char ipc = t.ipc[best];
-    r[0] = amount;
-    r[1] = (amount + 1 > 0) ? log(amount + 1) : ((amount + 1 == 0) ? -INFINITY : NAN);
-    r[2] = hour;
-    r[3] = dow;
-    r[4] = weekend ? 1.0 : 0.0;
-    r[5] = mfr;
-    r[6] = known ? 0.0 : 1.0;
-    r[7] = ipc == 0 ? NAN : (ipc == 1 ? 0.1 : 0.3);
-    r[8] = has_user ? (isnan(uavg_raw) ? 0.0 : uavg_raw) : NAN;
-    long long c0 = 0, c1 = 0, c2 = 0, s0 = 0, s1 = 0, s2 = 0;
-    if (mode == FD_WINDOW_REDIS_COMPAT) {
-      const bool live = has_ts && (ts - last_ts <= 3600000LL);
-      const long long cc = live ? cnt : 0, ss = live ? sum_cents : 0;
-      c0 = c1 = c2 = cc;
-      s0 = s1 = s2 = ss;
-      cnt = (int)(cc + 1);
-      sum_cents = ss + cents;
-      last_ts = ts;
-      has_ts = 1;
-    } else {
-      // 8 events per round trip: the loads of a group are independent (slots past ring_n are read
-      // from the allocated ring and ignored)
-      for (int e0 = 0; e0 < ring_n; e0 += 8) {
-        RingEvent ev[8];
+  const double amount = (double)t.cents / 100.0;
+  long long days = t.ts / 86400000LL;
+  if (t.ts % 86400000LL < 0) days -= 1;
+  int hour = (int)((t.ts - days * 86400000LL) / 3600000LL);
+  long long dw = (days + 3) % 7;
+  if (dw < 0) dw += 7;
+  const int dow = (int)dw + 1;
+  if (t.hour != 255) hour = t.hour;
+  const int weekend = (t.wk == 255) ? (dow >= 6) : (t.wk != 0);
+  double mfr, mult;
+  if (t.merchant >= 0 && t.merchant < nm) {
+    const double f = merchants[t.merchant].fraud_rate;
+    mfr = isnan(f) ? 0.05 : f;
+    mult = merchants[t.merchant].mult;
+  } else {
+    mfr = 0.1;
+    mult = 2.0;
+  }
+  const bool known = p.has_user && t.dfp != 0ull && (t.dfp == p.fp[0] || t.dfp == p.fp[1] || t.dfp == p.fp[2]);
+  r[0] = amount;
+  r[1] = (amount + 1 > 0) ? log(amount + 1) : ((amount + 1 == 0) ? -INFINITY : NAN);
+  r[2] = hour;
+  r[3] = dow;
+  r[4] = weekend ? 1.0 : 0.0;
+  r[5] = mfr;
+  r[6] = known ? 0.0 : 1.0;
+  r[7] = t.ipc == 0 ? NAN : (t.ipc == 1 ? 0.1 : 0.3);
+  r[8] = p.has_user ? (isnan(p.avg) ? 0.0 : p.avg) : NAN;
+  r[14] = mult;
+  r[15] = p.has_user ? (double)p.age : 0.0;
+}
+
+__device__ __forceinline__ void velocity_raw(const long long (&c)[3], const long long (&s)[3], double* r) {
+  r[9] = (double)c[0];
+  r[10] = (double)c[1];
+  r[11] = (double)c[2];
+  r[12] = (double)s[1] / 100.0;
+  r[13] = (double)s[2] / 100.0;
+}
+
+struct Outputs {
+  float* vec;     // [n][64]
+  double* raw;    // [n][16] or null
+  double* vel5;   // [n] velocity_5min_amount (feature map) or null
+  float* seq;     // [n][S][16] LSTM input sequences or null
+  float* seq_ring;  // [cap][S][16] per-card LSTM history (S > 0)
+  int S;
+};
+
+__device__ __forceinline__ void emit(const Outputs& o, int64_t i, const double* r, long long s5) {
+  if (o.raw) {
+    double2* ro = reinterpret_cast<double2*>(o.raw + (size_t)i * FD_RAW_FEATURES);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) ev[u] = rg[min(e0 + u, K - 1)];
+    for (int c = 0; c < FD_RAW_FEATURES / 2; ++c) ro[c] = make_double2(r[2 * c], r[2 * c + 1]);
+  }
+  write_vector(r, o.vec + (size_t)i * FD_VECTOR_WIDTH);
+  if (o.vel5) o.vel5[i] = (double)s5 / 100.0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// the sequential path: one thread, one card, its header in registers
+
+struct CardRegs {
+  long long last_ts;
+  unsigned flags;
+  int rn, rh, us;
+  int wc[3];
+  long long ws[3], wo[3];
+  long long rc_sum;
+  int rc_cnt;
+};
+
+__device__ __forceinline__ long long ll2(unsigned lo, unsigned hi) {
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+__device__ __forceinline__ void load_card(const CardHeader* __restrict__ h, CardRegs& c, Profile& p) {
+  const uint4* q = reinterpret_cast<const uint4*>(h);
+  uint4 w[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (e0 + u < ring_n && ev[u].ts <= ts) {
-            if (ts - 300000LL < ev[u].ts) {
-              c0 += 1;
-              s0 += ev[u].cents;
-            }
-            if (ts - 3600000LL < ev[u].ts) {
-              c1 += 1;
-              s1 += ev[u].cents;
-            }
-            if (ts - 86400000LL < ev[u].ts) {
-              c2 += 1;
-              s2 += ev[u].cents;
-            }
-          }
-        }
+  for (int k = 0; k < 8; ++k) w[k] = q[k];
+  // field offsets: see CardHeader (fd_internal.h)
+  c.last_ts = ll2(w[0].z, w[0].w);
+  p.avg = __longlong_as_double(ll2(w[1].x, w[1].y));
+  p.age = (int)w[1].z;
+  c.flags = w[1].w;
+  c.rn = (int)(w[2].x & 0xffu);
+  c.rh = (int)((w[2].x >> 8) & 0xffu);
+  c.us = (int)((w[2].x >> 16) & 0xffu);
+  c.wc[0] = (int)(w[2].y & 0xffu);
+  c.wc[1] = (int)((w[2].y >> 8) & 0xffu);
+  c.wc[2] = (int)((w[2].y >> 16) & 0xffu);
+  p.fp[0] = (unsigned long long)ll2(w[2].z, w[2].w);
+  p.fp[1] = (unsigned long long)ll2(w[3].x, w[3].y);
+  p.fp[2] = (unsigned long long)ll2(w[3].z, w[3].w);
+  c.ws[0] = ll2(w[4].x, w[4].y);
+  c.ws[1] = ll2(w[4].z, w[4].w);
+  c.ws[2] = ll2(w[5].x, w[5].y);
+  c.wo[0] = ll2(w[5].z, w[5].w);
+  c.wo[1] = ll2(w[6].x, w[6].y);
+  c.wo[2] = ll2(w[6].z, w[6].w);
+  c.rc_sum = ll2(w[7].x, w[7].y);
+  c.rc_cnt = (int)w[7].z;
+  p.has_user = (c.flags & 1u) != 0u;
+}
+
+// write back the mutable fields (line 0: last_ts, flags, ring cursor + window counts; line 1 whole)
+__device__ __forceinline__ void store_card(CardHeader* h, const CardRegs& c) {
+  h->last_ts = c.last_ts;
+  h->flags = c.flags;
+  unsigned long long cur = (unsigned long long)(unsigned)c.rn | ((unsigned long long)(unsigned)c.rh << 8) |
+                           ((unsigned long long)(unsigned)c.us << 16) | ((unsigned long long)(unsigned)c.wc[0] << 32) |
+                           ((unsigned long long)(unsigned)c.wc[1] << 40) | ((unsigned long long)(unsigned)c.wc[2] << 48);
+  *reinterpret_cast<unsigned long long*>(&h->ring_n) = cur;
+  const long long l1[8] = {c.ws[0], c.ws[1], c.ws[2], c.wo[0], c.wo[1], c.wo[2], c.rc_sum, (long long)(unsigned)c.rc_cnt};
+  uint4* q = reinterpret_cast<uint4*>(h->ws);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    q[k] = make_uint4((unsigned)l1[2 * k], (unsigned)((unsigned long long)l1[2 * k] >> 32), (unsigned)l1[2 * k + 1],
+                      (unsigned)((unsigned long long)l1[2 * k + 1] >> 32));
+}
+
+// windows as of time t from the (time-sorted) ring: the newest events with ts > t - W
+__device__ void rebuild_windows(CardRegs& c, const RingEvent* __restrict__ rg, int K, long long t) {
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    c.wc[w] = 0;
+    c.ws[w] = 0;
+    c.wo[w] = LLONG_MAX;
+  }
+  for (int e = 0; e < c.rn; ++e) {
+    const RingEvent ev = rg[e];
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+      if (ev.ts > t - kWin[w]) {
+        c.wc[w] += 1;
+        c.ws[w] += ev.cents;
+        c.wo[w] = ev.ts < c.wo[w] ? ev.ts : c.wo[w];
       }
-      rg[ring_head] = RingEvent{ts, cents};
-      ring_head = (ring_head + 1 == K) ? 0 : ring_head + 1;
-      if (ring_n < K) ++ring_n;
-    }
-    r[9] = (double)c0;
-    r[10] = (double)c1;
-    r[11] = (double)c2;
-    r[12] = (double)s1 / 100.0;
-    r[13] = (double)s2 / 100.0;
-    r[14] = mult;
-    r[15] = has_user ? (double)uage : 0.0;
-    if (raw_out) {
-      double2* ro = reinterpret_cast<double2*>(raw_out + (size_t)best * FD_RAW_FEATURES);
+  }
 #pragma unroll
-      for (int c = 0; c < FD_RAW_FEATURES / 2; ++c) ro[c] = make_double2(r[2 * c], r[2 * c + 1]);
-    }
-    write_vector(r, vec_out + (size_t)best * FD_VECTOR_WIDTH);
-    if (vel5_out) vel5_out[best] = (double)s0 / 100.0;  // velocity_5min_amount (feature map only)
-    if (S) {  // LSTM head input: this event appended to the card's history, last S events emitted
-      float* slot_ev = sr + (size_t)seq_head * kSeqInput;
+  for (int w = 0; w < 3; ++w)
+    if (c.wc[w] == 0) c.wo[w] = 0;
+}
+
+// one transaction of the card: velocity read (before write), then the write
+template <int MODE>
+__device__ __forceinline__ void velocity_step(CardRegs& c, RingEvent* __restrict__ rg, int K, long long ts,
+                                              long long cents, long long (&cw)[3], long long (&sw)[3]) {
+  if (MODE == FD_WINDOW_REDIS_COMPAT) {
+    const bool live = (c.flags & 2u) && (ts - c.last_ts <= kSessionTtl);
+    const long long cc = live ? c.rc_cnt : 0, ss = live ? c.rc_sum : 0;
 #pragma unroll
-      for (int c = 0; c < kSeqInput; ++c) slot_ev[c] = seq_input(r[c]);
-      seq_head = (seq_head + 1 == S) ? 0 : seq_head + 1;
-      if (seq_n < S) ++seq_n;
-      if (seq_out) {  // oldest -> newest, left-padded with zero events (Keras pad_sequences 'pre')
-        float* so = seq_out + (size_t)best * S * kSeqInput;
-        const int pad = S - seq_n;
-        for (int q = 0; q < S; ++q) {
-          float4* dst = reinterpret_cast<float4*>(so + (size_t)q * kSeqInput);
-          if (q < pad) {
-            for (int c = 0; c < kSeqInput / 4; ++c) dst[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-          } else {
-            int src = seq_head - seq_n + (q - pad);
-            if (src < 0) src += S;
-            const float4* sp = reinterpret_cast<const float4*>(sr + (size_t)src * kSeqInput);
-            for (int c = 0; c < kSeqInput / 4; ++c) dst[c] = sp[c];
-          }
+    for (int w = 0; w < 3; ++w) {
+      cw[w] = cc;
+      sw[w] = ss;
+    }
+    c.rc_cnt = (int)(cc + 1);
+    c.rc_sum = ss + cents;
+    c.last_ts = ts;
+    c.flags |= 2u;
+    return;
+  }
+  const bool descent = c.rn > 0 && ts < c.last_ts;
+  const bool inc = c.us == 0 && !descent;
+  if (inc) {  // time-sorted ring: evict each window's too-old events from its oldest end
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      while (c.wc[w] > 0 && c.wo[w] <= ts - kWin[w]) {
+        int idx = c.rh - c.wc[w];
+        if (idx < 0) idx += K;
+        c.ws[w] -= rg[idx].cents;
+        c.wc[w] -= 1;
+        if (c.wc[w] > 0) c.wo[w] = rg[idx + 1 == K ? 0 : idx + 1].ts;
+      }
+      cw[w] = c.wc[w];
+      sw[w] = c.ws[w];
+    }
+  } else {  // full scan (the definition): prior events e with t - W < e.ts <= t
+#pragma unroll
+    for (int w = 0; w < 3; ++w) cw[w] = sw[w] = 0;
+    for (int e0 = 0; e0 < c.rn; e0 += 8) {
+      RingEvent ev[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) ev[u] = rg[min(e0 + u, K - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + u < c.rn && ev[u].ts <= ts) {
+#pragma unroll
+          for (int w = 0; w < 3; ++w)
+            if (ts - kWin[w] < ev[u].ts) {
+              cw[w] += 1;
+              sw[w] += ev[u].cents;
+            }
         }
+    }
+  }
+  // append: a full ring overwrites its oldest event, which leaves every window spanning the whole ring
+  if (inc && c.rn == K && (c.wc[0] == K || c.wc[1] == K || c.wc[2] == K)) {
+    const long long oc = rg[c.rh].cents;
+    const long long nts = rg[c.rh + 1 == K ? 0 : c.rh + 1].ts;
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+      if (c.wc[w] == K) {
+        c.ws[w] -= oc;
+        c.wc[w] -= 1;
+        if (c.wc[w] > 0) c.wo[w] = nts;
+      }
+  }
+  rg[c.rh] = RingEvent{ts, cents};
+  c.rh = c.rh + 1 == K ? 0 : c.rh + 1;
+  if (c.rn < K) ++c.rn;
+  c.us = descent ? K : (c.us > 0 ? c.us - 1 : 0);
+  c.last_ts = ts;
+  if (c.us == 0) {
+    if (inc) {
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        if (c.wc[w] == 0) c.wo[w] = ts;
+        c.wc[w] += 1;
+        c.ws[w] += cents;
+      }
+    } else {
+      rebuild_windows(c, rg, K, ts);  // the ring just became time-sorted again
+    }
+  } else {
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      c.wc[w] = 0;
+      c.ws[w] = 0;
+      c.wo[w] = 0;
+    }
+  }
+}
+
+// LSTM head input: this event appended to the card's history, the last S events emitted
+__device__ __forceinline__ void seq_step(const Outputs& o, unsigned s, unsigned& flags, int64_t i, const double* r) {
+  const int S = o.S;
+  int seq_n = (int)((flags >> 8) & 0xffu), seq_head = (int)((flags >> 16) & 0xffu);
+  float* sr = o.seq_ring + (size_t)s * S * kSeqInput;
+  float* slot_ev = sr + (size_t)seq_head * kSeqInput;
+#pragma unroll
+  for (int c = 0; c < kSeqInput; ++c) slot_ev[c] = seq_input(r[c]);
+  seq_head = (seq_head + 1 == S) ? 0 : seq_head + 1;
+  if (seq_n < S) ++seq_n;
+  if (o.seq) {  // oldest -> newest, left-padded with zero events (Keras pad_sequences 'pre')
+    float* so = o.seq + (size_t)i * S * kSeqInput;
+    const int pad = S - seq_n;
+    for (int q = 0; q < S; ++q) {
+      float4* dst = reinterpret_cast<float4*>(so + (size_t)q * kSeqInput);
+      if (q < pad) {
+        for (int c = 0; c < kSeqInput / 4; ++c) dst[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        int src = seq_head - seq_n + (q - pad);
+        if (src < 0) src += S;
+        const float4* sp = reinterpret_cast<const float4*>(sr + (size_t)src * kSeqInput);
+        for (int c = 0; c < kSeqInput / 4; ++c) dst[c] = sp[c];
       }
     }
   }
-  h->flags = (flags & 0xffu) | ((unsigned)seq_n << 8) | ((unsigned)seq_head << 16);
-  h->cnt = cnt;
-  h->has_ts = has_ts;
-  h->ring_n = ring_n;
-  h->ring_head = ring_head;
-  h->last_ts = last_ts;
-  h->sum_cents = sum_cents;
+  flags = (flags & 0xffu) | ((unsigned)seq_n << 8) | ((unsigned)seq_head << 16);
+}
+
+struct BucketArgs {
+  CardHeader* H;
+  RingEvent* ring;
+  const Merchant* merchants;
+  int nm, K;
+  int64_t n;
+  TxnSrc src;
+  Outputs out;
+  unsigned* bucket_cnt;
+  unsigned* bucket_fill;
+  const unsigned* bucket_base;
+  const unsigned long long* pairs;
+};
+
+template <int MODE>
+__device__ void process_short(const BucketArgs& a, unsigned s, const unsigned long long* keys, int len) {
+  CardHeader* h = a.H + s;
+  CardRegs c;
+  Profile p;
+  Txn t = a.src.get((unsigned)keys[0]);  // in flight with the header
+  load_card(h, c, p);
+  RingEvent* rg = a.ring + (size_t)s * a.K;
+  for (int q = 0; q < len; ++q) {
+    const int64_t i = (int64_t)(unsigned)keys[q];
+    if (q > 0) t = a.src.get(i);
+    double r[FD_RAW_FEATURES];
+    base_raw(t, p, a.merchants, a.nm, r);
+    long long cw[3], sw[3];
+    velocity_step<MODE>(c, rg, a.K, t.ts, t.cents, cw, sw);
+    velocity_raw(cw, sw, r);
+    emit(a.out, i, r, sw[0]);
+    if (a.out.S) seq_step(a.out, s, c.flags, i, r);
+  }
+  store_card(h, c);
+}
+
+// ------------------------------------------------------------------------------------------------
+// the cooperative path: a long segment (hot card) processed by the whole workgroup, kBT per tile
+
+struct LongLds {
+  long long ev_ts[kMaxK + kBT];   // [0, K): the K events before the tile (hist_n valid at the top); [K, K+T): tile
+  long long ev_c[kMaxK + kBT];
+  long long pre[kBT];             // redis: inclusive prefix sum of the tile's cents
+  int rst[kBT];                   // redis: last reset index <= j (-1 none); sliding: last descent index <= j
+  float seqb[(FD_MAX_SEQ_LEN + kBT) * kSeqInput];  // LSTM inputs: [0, S) history, [S, S+T) tile
+  CardHeader hdr;
+  long long carry_c, carry_s;     // redis session after the previous tile
+  int hist_n, us, seq_n, pad;
+};
+
+__device__ void block_scan_sum(long long* v) {  // inclusive, kBT entries
+  for (int d = 1; d < kBT; d <<= 1) {
+    const long long x = threadIdx.x >= (unsigned)d ? v[threadIdx.x - d] : 0;
+    __syncthreads();
+    v[threadIdx.x] += x;
+    __syncthreads();
+  }
+}
+
+__device__ void block_scan_max(int* v) {  // inclusive, kBT entries
+  for (int d = 1; d < kBT; d <<= 1) {
+    const int x = threadIdx.x >= (unsigned)d ? v[threadIdx.x - d] : -1;
+    __syncthreads();
+    v[threadIdx.x] = max(v[threadIdx.x], x);
+    __syncthreads();
+  }
+}
+
+template <int MODE>
+__device__ void process_long(const BucketArgs& a, unsigned s, const unsigned long long* keys, int L, LongLds& sm) {
+  const int tid = threadIdx.x, K = a.K, S = a.out.S;
+  CardHeader* h = a.H + s;
+  RingEvent* rg = a.ring + (size_t)s * K;
+  if (tid == 0) {
+    sm.hdr = *h;
+    sm.carry_c = sm.hdr.rc_cnt;
+    sm.carry_s = sm.hdr.rc_sum;
+    sm.hist_n = MODE == FD_WINDOW_SLIDING ? sm.hdr.ring_n : 0;
+    sm.us = sm.hdr.unsorted;
+    sm.seq_n = (int)((sm.hdr.flags >> 8) & 0xffu);
+  }
+  __syncthreads();
+  const int rn0 = sm.hdr.ring_n, rh0 = sm.hdr.ring_head;
+  const long long ts0 = sm.hdr.last_ts;
+  const bool has_ts0 = (sm.hdr.flags & 2u) != 0u;
+  Profile p;
+  p.has_user = (sm.hdr.flags & 1u) != 0u;
+  p.avg = sm.hdr.avg;
+  p.age = sm.hdr.age;
+  for (int k = 0; k < 3; ++k) p.fp[k] = sm.hdr.fp[k];
+  if (MODE == FD_WINDOW_SLIDING && tid < rn0) {  // the ring, oldest first, at the top of [0, K)
+    int src = rh0 - rn0 + tid;
+    if (src < 0) src += K;
+    const RingEvent ev = rg[src];
+    sm.ev_ts[K - rn0 + tid] = ev.ts;
+    sm.ev_c[K - rn0 + tid] = ev.cents;
+  }
+  const int seq_n0 = sm.seq_n, seq_h0 = (int)((sm.hdr.flags >> 16) & 0xffu);
+  const float* sr = S ? a.out.seq_ring + (size_t)s * S * kSeqInput : nullptr;
+  if (S && tid < seq_n0 * kSeqInput) {  // the LSTM history, oldest first, at the top of [0, S)
+    const int e = tid / kSeqInput, c = tid % kSeqInput;
+    int src = seq_h0 - seq_n0 + e;
+    if (src < 0) src += S;
+    sm.seqb[(S - seq_n0 + e) * kSeqInput + c] = sr[(size_t)src * kSeqInput + c];
+  }
+  __syncthreads();
+  for (int t0 = 0; t0 < L; t0 += kBT) {
+    const int T = min(kBT, L - t0), j = tid;
+    const bool act = j < T;
+    const int64_t i = act ? (int64_t)(unsigned)keys[t0 + j] : 0;
+    Txn t{};
+    if (act) {
+      t = a.src.get(i);
+      sm.ev_ts[K + j] = t.ts;
+      sm.ev_c[K + j] = t.cents;
+    }
+    __syncthreads();
+    // the previous event's time in the card's order (ring / previous tile / this tile)
+    const bool first = t0 == 0 && j == 0;
+    const long long prev_ts = (j > 0 || t0 > 0) ? sm.ev_ts[K + j - 1] : ts0;
+    const bool has_prev = !first || (MODE == FD_WINDOW_SLIDING ? rn0 > 0 : has_ts0);
+    long long cw[3] = {0, 0, 0}, sw[3] = {0, 0, 0};
+    if (MODE == FD_WINDOW_REDIS_COMPAT) {
+      const bool live = act && has_prev && (t.ts - prev_ts <= kSessionTtl);
+      sm.pre[j] = act ? t.cents : 0;
+      sm.rst[j] = (act && !live) ? j : -1;
+      __syncthreads();
+      block_scan_sum(sm.pre);
+      block_scan_max(sm.rst);
+      if (act && live) {  // the session after the previous transaction
+        long long cc, ss;
+        if (j == 0) {
+          cc = sm.carry_c;
+          ss = sm.carry_s;
+        } else {
+          const int R = sm.rst[j - 1];
+          cc = R < 0 ? sm.carry_c + j : j - R;
+          ss = R < 0 ? sm.carry_s + sm.pre[j - 1] : sm.pre[j - 1] - (R > 0 ? sm.pre[R - 1] : 0);
+        }
+        for (int w = 0; w < 3; ++w) {
+          cw[w] = cc;
+          sw[w] = ss;
+        }
+      }
+    } else {
+      // positional windows: the card's previous K events are buffer slots [max(K - hist_n, j), K + j)
+      if (act) {
+        for (int e = max(K - sm.hist_n, j); e < K + j; ++e) {
+          const long long et = sm.ev_ts[e];
+          if (et <= t.ts)
+            for (int w = 0; w < 3; ++w)
+              if (t.ts - kWin[w] < et) {
+                cw[w] += 1;
+                sw[w] += sm.ev_c[e];
+              }
+        }
+      }
+      sm.rst[j] = (act && has_prev && t.ts < prev_ts) ? j : -1;  // descents (out-of-order arrivals)
+      __syncthreads();
+      block_scan_max(sm.rst);
+    }
+    double r[FD_RAW_FEATURES];
+    if (act) {
+      base_raw(t, p, a.merchants, a.nm, r);
+      velocity_raw(cw, sw, r);
+      emit(a.out, i, r, sw[0]);
+      if (S)
+        for (int c = 0; c < kSeqInput; ++c) sm.seqb[(S + j) * kSeqInput + c] = seq_input(r[c]);
+    }
+    __syncthreads();
+    if (S && act && a.out.seq) {  // txn j's sequence: the last S events up to and including itself
+      const int have = min(S, sm.seq_n + j + 1), pad = S - have;
+      float* so = a.out.seq + (size_t)i * S * kSeqInput;
+      for (int q = 0; q < S; ++q) {
+        float4* dst = reinterpret_cast<float4*>(so + (size_t)q * kSeqInput);
+        const float4* src = reinterpret_cast<const float4*>(&sm.seqb[(j + 1 + q) * kSeqInput]);
+        for (int c = 0; c < kSeqInput / 4; ++c) dst[c] = q < pad ? make_float4(0.f, 0.f, 0.f, 0.f) : src[c];
+      }
+    }
+    // carries for the next tile (values read before the barrier, written after it)
+    long long nts = 0, nc = 0;
+    if (tid < K) {
+      const int src = T + tid;  // the last K of [prior | tile]
+      nts = sm.ev_ts[src];
+      nc = sm.ev_c[src];
+    }
+    float sv[kSeqInput];
+    const bool seq_mover = S && tid < S;
+    if (seq_mover)
+      for (int c = 0; c < kSeqInput; ++c) sv[c] = sm.seqb[(T + tid) * kSeqInput + c];
+    long long ncc = 0, nss = 0;
+    int nus = 0;
+    if (tid == 0) {
+      if (MODE == FD_WINDOW_REDIS_COMPAT) {
+        const int R = sm.rst[T - 1];
+        ncc = R < 0 ? sm.carry_c + T : T - R;
+        nss = R < 0 ? sm.carry_s + sm.pre[T - 1] : sm.pre[T - 1] - (R > 0 ? sm.pre[R - 1] : 0);
+      } else {
+        const int d = sm.rst[T - 1];
+        nus = d >= 0 ? max(0, K - (T - 1 - d)) : max(0, sm.us - T);
+      }
+    }
+    __syncthreads();
+    if (tid < K) {
+      sm.ev_ts[tid] = nts;
+      sm.ev_c[tid] = nc;
+    }
+    if (seq_mover)
+      for (int c = 0; c < kSeqInput; ++c) sm.seqb[tid * kSeqInput + c] = sv[c];
+    if (tid == 0) {
+      sm.hist_n = min(K, sm.hist_n + T);
+      sm.seq_n = min(S, sm.seq_n + T);
+      sm.carry_c = ncc;
+      sm.carry_s = nss;
+      sm.us = nus;
+    }
+    __syncthreads();
+  }
+  // final state: ring = the card's last K events, header rebuilt as the sequential path leaves it
+  const long long last = sm.ev_ts[K - 1];
+  if (MODE == FD_WINDOW_SLIDING) {
+    const int rn = min(K, rn0 + L), rh = (rh0 + L) % K;
+    if (tid < rn) {
+      int dst = rh - rn + tid;
+      if (dst < 0) dst += K;
+      rg[dst] = RingEvent{sm.ev_ts[K - rn + tid], sm.ev_c[K - rn + tid]};
+    }
+  }
+  if (S && tid < sm.seq_n * kSeqInput) {
+    const int e = tid / kSeqInput, c = tid % kSeqInput;
+    const int sh = (seq_h0 + L) % S;
+    int dst = sh - sm.seq_n + e;
+    if (dst < 0) dst += S;
+    a.out.seq_ring[((size_t)s * S + dst) * kSeqInput + c] = sm.seqb[(S - sm.seq_n + e) * kSeqInput + c];
+  }
+  if (tid == 0) {
+    CardRegs c;
+    c.last_ts = last;
+    c.flags = sm.hdr.flags;
+    if (S) c.flags = (c.flags & 0xffu) | ((unsigned)sm.seq_n << 8) | ((unsigned)((seq_h0 + L) % S) << 16);
+    c.rn = sm.hdr.ring_n;
+    c.rh = sm.hdr.ring_head;
+    c.us = sm.hdr.unsorted;
+    for (int w = 0; w < 3; ++w) {
+      c.wc[w] = sm.hdr.wc[w];
+      c.ws[w] = sm.hdr.ws[w];
+      c.wo[w] = sm.hdr.wo[w];
+    }
+    c.rc_sum = sm.hdr.rc_sum;
+    c.rc_cnt = sm.hdr.rc_cnt;
+    if (MODE == FD_WINDOW_REDIS_COMPAT) {
+      c.rc_cnt = (int)sm.carry_c;
+      c.rc_sum = sm.carry_s;
+      c.flags |= 2u;
+    } else {
+      c.rn = min(K, rn0 + L);
+      c.rh = (rh0 + L) % K;
+      c.us = sm.us;
+      for (int w = 0; w < 3; ++w) {
+        c.wc[w] = 0;
+        c.ws[w] = 0;
+        c.wo[w] = 0;
+      }
+      if (c.us == 0) {  // windows as of the last event, from the newest events (time-sorted ring)
+        for (int w = 0; w < 3; ++w) c.wo[w] = LLONG_MAX;
+        for (int e = K - c.rn; e < K; ++e) {
+          const long long et = sm.ev_ts[e];
+          for (int w = 0; w < 3; ++w)
+            if (et > last - kWin[w]) {
+              c.wc[w] += 1;
+              c.ws[w] += sm.ev_c[e];
+              c.wo[w] = et < c.wo[w] ? et : c.wo[w];
+            }
+        }
+        for (int w = 0; w < 3; ++w)
+          if (c.wc[w] == 0) c.wo[w] = 0;
+      }
+    }
+    store_card(h, c);
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// the bucket kernel
+
+__device__ void bitonic_sort(unsigned long long* k, int N) {  // ascending, N a power of two, in LDS
+  for (int size = 2; size <= N; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int idx = threadIdx.x; idx < (N >> 1); idx += kBT) {
+        const int lo = 2 * stride * (idx / stride) + (idx % stride), hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const unsigned long long x = k[lo], y = k[hi];
+        if ((x > y) == asc) {
+          k[lo] = y;
+          k[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// m keys (slot << 32 | arrival index) already in LDS skeys[0, m): sort, then process every segment
+template <int MODE>
+__device__ void process_sorted(const BucketArgs& a, unsigned long long* skeys, int m, LongLds& sm, int* long_list,
+                               int* n_long) {
+  int N = 2;
+  while (N < m) N <<= 1;
+  for (int q = m + threadIdx.x; q < N; q += kBT) skeys[q] = ~0ull;
+  if (threadIdx.x == 0) *n_long = 0;
+  __syncthreads();
+  if (m > 1) bitonic_sort(skeys, N);
+  for (int pos = threadIdx.x; pos < m; pos += kBT) {
+    const unsigned s = (unsigned)(skeys[pos] >> 32);
+    if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;  // not the first txn of its card
+    int len = 1;
+    while (pos + len < m && (unsigned)(skeys[pos + len] >> 32) == s && len <= kSegLong) ++len;
+    if (len > kSegLong) {
+      long_list[atomicAdd(n_long, 1)] = pos;
+      continue;
+    }
+    process_short<MODE>(a, s, skeys + pos, len);
+  }
+  __syncthreads();
+  const int nl = *n_long;
+  for (int q = 0; q < nl; ++q) {
+    const int pos = long_list[q];
+    const unsigned s = (unsigned)(skeys[pos] >> 32);
+    int len = 1;  // every thread finds the same length
+    while (pos + len < m && (unsigned)(skeys[pos + len] >> 32) == s) ++len;
+    process_long<MODE>(a, s, skeys + pos, len, sm);
+  }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
+  extern __shared__ unsigned long long skeys[];  // kChunkCap keys | kMaxBins + 1 bin prefix sums
+  __shared__ LongLds sm;
+  __shared__ int long_list[kChunkCap / (kSegLong + 1) + 1];
+  __shared__ int n_long, chunk_m;
+  unsigned* bins = reinterpret_cast<unsigned*>(skeys + kChunkCap);
+  const int b = blockIdx.x;
+  const unsigned m = a.bucket_cnt[b];
+  const unsigned long long* src = a.pairs + a.bucket_base[b];
+  if (m <= (unsigned)kChunkCap) {
+    for (unsigned q = threadIdx.x; q < m; q += kBT) skeys[q] = src[q];
+    __syncthreads();
+    process_sorted<MODE>(a, skeys, (int)m, sm, long_list, &n_long);
+  } else {
+    // Oversized bucket (a hot card): pass by arrival range so each pass's keys fit the LDS sort and every
+    // card's transactions of pass c precede its transactions of pass c + 1 (state carried in HBM; the
+    // workgroup barrier orders it: all passes run on this CU).
+    const long long binw = (a.n + kMaxBins - 1) / kMaxBins;  // <= kChunkCap for n <= 16M (launch check)
+    for (int q = threadIdx.x; q < kMaxBins; q += kBT) bins[q] = 0u;
+    __syncthreads();
+    for (unsigned q = threadIdx.x; q < m; q += kBT) atomicAdd(&bins[(unsigned)(src[q] & 0xffffffffull) / binw], 1u);
+    __syncthreads();
+    {  // exclusive prefix over the bins, in place; bins[kMaxBins] = m
+      constexpr int per = kMaxBins / kBT;
+      unsigned v[per], sum = 0;
+      for (int q = 0; q < per; ++q) {
+        v[q] = bins[threadIdx.x * per + q];
+        sum += v[q];
+      }
+      sm.rst[threadIdx.x] = (int)sum;
+      __syncthreads();
+      for (int d = 1; d < kBT; d <<= 1) {
+        const int x = threadIdx.x >= (unsigned)d ? sm.rst[threadIdx.x - d] : 0;
+        __syncthreads();
+        sm.rst[threadIdx.x] += x;
+        __syncthreads();
+      }
+      unsigned run = threadIdx.x ? (unsigned)sm.rst[threadIdx.x - 1] : 0u;
+      for (int q = 0; q < per; ++q) {
+        bins[threadIdx.x * per + q] = run;
+        run += v[q];
+      }
+      if (threadIdx.x == 0) bins[kMaxBins] = m;
+      __syncthreads();
+    }
+    int lo = 0;
+    while (lo < kMaxBins) {
+      // the widest bin range [lo, hi) holding <= kChunkCap keys (a single bin always fits)
+      int l = lo + 1, r = kMaxBins;
+      while (l < r) {
+        const int mid = (l + r + 1) >> 1;
+        if (bins[mid] - bins[lo] <= (unsigned)kChunkCap) l = mid; else r = mid - 1;
+      }
+      const int hi = l;
+      const unsigned i_lo = (unsigned)(lo * binw), i_hi = (unsigned)min((long long)hi * binw, a.n);
+      if (threadIdx.x == 0) chunk_m = 0;
+      __syncthreads();
+      for (unsigned q = threadIdx.x; q < m; q += kBT) {
+        const unsigned long long k = src[q];
+        const unsigned i = (unsigned)(k & 0xffffffffull);
+        if (i >= i_lo && i < i_hi) skeys[atomicAdd(&chunk_m, 1)] = k;
+      }
+      __syncthreads();
+      process_sorted<MODE>(a, skeys, chunk_m, sm, long_list, &n_long);
+      __syncthreads();
+      lo = hi;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the next batch's counters (it runs after this launch on the same stream)
+    a.bucket_cnt[b] = 0u;
+    a.bucket_fill[b] = 0u;
+  }
 }
 
 __global__ void __launch_bounds__(256) count_cards_kernel(const CardHeader* H, int64_t cap,
@@ -366,10 +997,9 @@ __global__ void __launch_bounds__(256) count_cards_kernel(const CardHeader* H, i
   atomicAdd(out, c);
 }
 
-
 // ------------------------------------------------------------------------------------------------
 // Full FeatureExtractor map (a3) and the Flink rule scores ((f) rank 2), elementwise per transaction
-// after feat_process (same batch: the card slots of feat_assign, the raw features of feat_process).
+// after feat_bucket (same batch: the card slots of feat_slot, the raw features of feat_bucket).
 //   fmap[n][64] f64 in FeatureStore.getRegisteredFeatures order (fl/features/FeatureStore.java:325-365),
 //     FeatureExtractor.extractAllFeatures semantics (fl/features/FeatureExtractor.java:50-493): NaN
 //     where the Java map has no key; strings as the host's vocabulary codes, "unknown" = 254.
@@ -436,12 +1066,11 @@ __device__ __forceinline__ bool operating_at(const MerchExt& me, int h) {
 __device__ __forceinline__ double to_rad(double d) { return d * 0.017453292519943295; }  // Math.toRadians
 
 __global__ void __launch_bounds__(256) feat_ext_kernel(const CardHeader* __restrict__ H,
-                                                       const unsigned long long* __restrict__ fps,
                                                        const UserExt* __restrict__ uext,
                                                        const Merchant* __restrict__ merchants,
                                                        const MerchExt* __restrict__ mext, int nm, int n_mext,
                                                        int64_t n,
-                                                       TxnArgs t, CtxArgs c, const unsigned* __restrict__ slot,
+                                                       TxnSrc t, CtxArgs c, const unsigned* __restrict__ slot,
                                                        const double* __restrict__ raw, const double* __restrict__ vel5,
                                                        const unsigned char* __restrict__ vocab, double tp_threshold,
                                                        double* __restrict__ fmap, fd_rule_scores* __restrict__ rules) {
@@ -723,13 +1352,20 @@ __global__ void __launch_bounds__(256) users_ext_load_kernel(CardHeader* H, User
 
 unsigned grid_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+// buckets of a batch of n: NB = the power of two nearest n / 256 (one 256-thread workgroup per ~256 txns)
+unsigned buckets_for(int64_t n, int64_t cap) {
+  unsigned nb = 1;
+  while ((int64_t)nb * 256 < n && nb < (unsigned)kMaxBuckets && (int64_t)nb < cap) nb <<= 1;
+  return nb;
+}
+
 }  // namespace
 
 void state_init(Engine& e, const fd_state_params& p) {
   FD_REQUIRE(p.capacity > 0 && p.capacity <= (1ll << 31), FD_ERR_INVALID_ARG, "capacity must be in [1, 2^31]");
   FD_REQUIRE(p.window_mode == FD_WINDOW_REDIS_COMPAT || p.window_mode == FD_WINDOW_SLIDING, FD_ERR_INVALID_ARG,
              "unknown window_mode");
-  FD_REQUIRE(p.ring_k >= 1 && p.ring_k <= 64, FD_ERR_INVALID_ARG, "ring_k must be in [1, 64]");
+  FD_REQUIRE(p.ring_k >= 1 && p.ring_k <= kMaxK, FD_ERR_INVALID_ARG, "ring_k must be in [1, 64]");
   FD_REQUIRE(p.seq_len >= 0 && p.seq_len <= FD_MAX_SEQ_LEN, FD_ERR_INVALID_ARG, "seq_len must be in [0, 16]");
   int64_t cap = 1;
   while (cap < p.capacity) cap <<= 1;
@@ -738,7 +1374,6 @@ void state_init(Engine& e, const fd_state_params& p) {
   st.mode = p.window_mode;
   st.K = p.window_mode == FD_WINDOW_SLIDING ? p.ring_k : 1;
   st.headers.ensure((size_t)cap * sizeof(CardHeader));
-  st.fps.ensure((size_t)cap * 4 * sizeof(unsigned long long));
   st.ring.ensure((size_t)cap * st.K * sizeof(RingEvent));
   st.S = p.seq_len;
   if (st.S) st.seq.ensure((size_t)cap * st.S * kSeqInput * sizeof(float));
@@ -746,6 +1381,9 @@ void state_init(Engine& e, const fd_state_params& p) {
   // allocates for the new capacity)
   st.uext.release();
   st.err.ensure(16);
+  st.bucket_cnt.ensure(kMaxBuckets * sizeof(unsigned));
+  st.bucket_fill.ensure(kMaxBuckets * sizeof(unsigned));
+  st.bucket_base.ensure(kMaxBuckets * sizeof(unsigned));
   st.ready = true;
   state_clear(e);
 }
@@ -754,11 +1392,11 @@ void state_clear(Engine& e) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
   FD_HIP(hipMemsetAsync(st.headers.ptr, 0, (size_t)st.cap * sizeof(CardHeader), e.stream));
-  FD_HIP(hipMemsetAsync(st.fps.ptr, 0, (size_t)st.cap * 4 * sizeof(unsigned long long), e.stream));
   if (st.uext.ptr) FD_HIP(hipMemsetAsync(st.uext.ptr, 0, (size_t)st.cap * sizeof(UserExt), e.stream));
   FD_HIP(hipMemsetAsync(st.err.ptr, 0, 16, e.stream));
+  FD_HIP(hipMemsetAsync(st.bucket_cnt.ptr, 0, kMaxBuckets * sizeof(unsigned), e.stream));
+  FD_HIP(hipMemsetAsync(st.bucket_fill.ptr, 0, kMaxBuckets * sizeof(unsigned), e.stream));
   FD_HIP(hipStreamSynchronize(e.stream));
-  st.epoch = 0;
   // the window event logs hold card-table slots: clearing the table empties them too
   WindowState& w = e.windows;
   w.ucount = w.mcount = 0;
@@ -809,8 +1447,8 @@ void load_users(Engine& e, const fd_users& u) {
   FD_HIP(hipMemcpyAsync(g.ptr, u.account_age_days, u.n * 4, hipMemcpyHostToDevice, e.stream));
   FD_HIP(hipMemcpyAsync(f.ptr, u.device_fp, u.n * 24, hipMemcpyHostToDevice, e.stream));
   hipLaunchKernelGGL(users_load_kernel, dim3(grid_for(u.n)), dim3(256), 0, e.stream, st.headers.as<CardHeader>(),
-                     st.fps.as<unsigned long long>(), (long long)(st.cap - 1), u.n, k.as<const unsigned long long>(),
-                     a.as<const double>(), g.as<const int>(), f.as<const unsigned long long>(), st.err.as<unsigned>());
+                     (long long)(st.cap - 1), u.n, k.as<const unsigned long long>(), a.as<const double>(),
+                     g.as<const int>(), f.as<const unsigned long long>(), st.err.as<unsigned>());
   FD_HIP(hipGetLastError());
   check_err(e);  // synchronises before the staging buffers are freed
 }
@@ -826,6 +1464,61 @@ void load_merchants(Engine& e, const fd_merchants& m) {
   st.n_merchants = m.n;
 }
 
+namespace {
+
+// The three grouping launches + the bucket kernel over any transaction source.
+void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, double* d_raw, float* d_seq,
+                    double* d_vel5) {
+  CardStore& st = e.state;
+  FD_REQUIRE(n <= (int64_t)kMaxBins * kChunkCap, FD_ERR_INVALID_ARG, "micro-batch larger than 16M transactions");
+  st.slot.ensure((size_t)n * 4);
+  st.pairs.ensure((size_t)n * 8);
+  if (st.merchants.ptr == nullptr) st.merchants.ensure(16);
+  const unsigned nb = buckets_for(n, st.cap);
+  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
+  if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
+  hipLaunchKernelGGL(feat_slot_kernel, dim3(grid_for(n)), dim3(kBT), nb * sizeof(unsigned), e.stream,
+                     st.headers.as<CardHeader>(), (long long)(st.cap - 1), n, src, nb - 1, st.slot.as<unsigned>(),
+                     st.bucket_cnt.as<unsigned>(), st.err.as<unsigned>());
+  FD_HIP(hipGetLastError());
+  static bool attrs = false;
+  if (!attrs) {  // > 48 KiB of dynamic LDS at the largest bucket counts
+    FD_HIP(hipFuncSetAttribute((const void*)feat_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               3 * kMaxBuckets * (int)sizeof(unsigned)));
+    FD_HIP(hipFuncSetAttribute((const void*)feat_bucket_kernel<FD_WINDOW_SLIDING>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLds));
+    FD_HIP(hipFuncSetAttribute((const void*)feat_bucket_kernel<FD_WINDOW_REDIS_COMPAT>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLds));
+    attrs = true;
+  }
+  hipLaunchKernelGGL(feat_scatter_kernel, dim3(grid_for(n)), dim3(kBT), 3 * nb * sizeof(unsigned), e.stream, n,
+                     st.slot.as<const unsigned>(), nb - 1, st.bucket_cnt.as<const unsigned>(),
+                     st.bucket_fill.as<unsigned>(), st.bucket_base.as<unsigned>(), st.pairs.as<unsigned long long>());
+  FD_HIP(hipGetLastError());
+  BucketArgs a{};
+  a.H = st.headers.as<CardHeader>();
+  a.ring = st.ring.as<RingEvent>();
+  a.merchants = st.merchants.as<const Merchant>();
+  a.nm = (int)st.n_merchants;
+  a.K = st.K;
+  a.n = n;
+  a.src = src;
+  a.out = Outputs{d_vec, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S};
+  a.bucket_cnt = st.bucket_cnt.as<unsigned>();
+  a.bucket_fill = st.bucket_fill.as<unsigned>();
+  a.bucket_base = st.bucket_base.as<const unsigned>();
+  a.pairs = st.pairs.as<const unsigned long long>();
+  const size_t lds = kBucketLds;
+  if (st.mode == FD_WINDOW_SLIDING)
+    hipLaunchKernelGGL(feat_bucket_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), lds, e.stream, a);
+  else
+    hipLaunchKernelGGL(feat_bucket_kernel<FD_WINDOW_REDIS_COMPAT>, dim3(nb), dim3(kBT), lds, e.stream, a);
+  FD_HIP(hipGetLastError());
+  if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
+}
+
+}  // namespace
+
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw, float* d_seq,
                      double* d_vel5) {
   CardStore& st = e.state;
@@ -837,25 +1530,22 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
   FD_REQUIRE(t.card_key && t.ts_ms && t.amount_cents && t.merchant && t.device_fp && t.ip_class && t.hour &&
                  t.weekend,
              FD_ERR_INVALID_ARG, "incomplete transaction batch");
-  st.slot.ensure((size_t)n * 4);
-  st.next.ensure((size_t)n * 4);
-  if (st.merchants.ptr == nullptr) st.merchants.ensure(16);
-  st.epoch = (st.epoch == 0xffffffffu) ? 1u : st.epoch + 1u;
-  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
-  if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
-  hipLaunchKernelGGL(feat_assign_kernel, dim3(grid_for(n)), dim3(256), 0, e.stream, st.headers.as<CardHeader>(),
-                     (long long)(st.cap - 1), n, reinterpret_cast<const unsigned long long*>(t.card_key), st.epoch,
-                     st.slot.as<unsigned>(), st.next.as<int>(), st.err.as<unsigned>());
-  FD_HIP(hipGetLastError());
-  TxnArgs a{reinterpret_cast<const unsigned long long*>(t.card_key), reinterpret_cast<const long long*>(t.ts_ms),
-            reinterpret_cast<const long long*>(t.amount_cents), reinterpret_cast<const int*>(t.merchant),
-            reinterpret_cast<const unsigned long long*>(t.device_fp), t.ip_class, t.hour, t.weekend};
-  hipLaunchKernelGGL(feat_process_kernel, dim3(grid_for(n)), dim3(256), 0, e.stream, st.headers.as<CardHeader>(),
-                     st.fps.as<const unsigned long long>(), st.ring.as<RingEvent>(), st.merchants.as<const Merchant>(),
-                     (int)st.n_merchants, st.mode, st.K, n, a, st.slot.as<const unsigned>(), st.next.as<const int>(),
-                     d_vec, d_raw, st.S ? st.seq.as<float>() : nullptr, st.S, d_seq, d_vel5);
-  FD_HIP(hipGetLastError());
-  if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
+  TxnSrc src{reinterpret_cast<const unsigned long long*>(t.card_key), reinterpret_cast<const long long*>(t.ts_ms),
+             reinterpret_cast<const long long*>(t.amount_cents), reinterpret_cast<const int*>(t.merchant),
+             reinterpret_cast<const unsigned long long*>(t.device_fp), t.ip_class, t.hour, t.weekend, nullptr};
+  launch_grouped(e, src, n, d_vec, d_raw, d_seq, d_vel5);
+}
+
+void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq) {
+  CardStore& st = e.state;
+  FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
+  FD_REQUIRE(d_vec != nullptr && (n == 0 || d_records != nullptr), FD_ERR_INVALID_ARG, "null records / output");
+  FD_REQUIRE(d_seq == nullptr || st.S > 0, FD_ERR_INVALID_ARG, "sequence output needs fd_state_params.seq_len > 0");
+  FD_REQUIRE(n >= 0 && n < (1ll << 31), FD_ERR_INVALID_ARG, "batch size out of range");
+  if (n == 0) return;
+  TxnSrc src{};
+  src.rec = static_cast<const RouteRecord*>(d_records);
+  launch_grouped(e, src, n, d_vec, nullptr, d_seq, nullptr);
 }
 
 void features_check(Engine& e) { check_err(e); }
@@ -944,13 +1634,13 @@ void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context
   launch_features(e, t, n, d_vec, raw, nullptr, vel5);
   if (!st.vocab_loaded) load_vocab(e, nullptr, nullptr);
   if (st.merchants.ptr == nullptr) st.merchants.ensure(16);
-  TxnArgs a{reinterpret_cast<const unsigned long long*>(t.card_key), reinterpret_cast<const long long*>(t.ts_ms),
-            reinterpret_cast<const long long*>(t.amount_cents), reinterpret_cast<const int*>(t.merchant),
-            reinterpret_cast<const unsigned long long*>(t.device_fp), t.ip_class, t.hour, t.weekend};
+  TxnSrc a{reinterpret_cast<const unsigned long long*>(t.card_key), reinterpret_cast<const long long*>(t.ts_ms),
+           reinterpret_cast<const long long*>(t.amount_cents), reinterpret_cast<const int*>(t.merchant),
+           reinterpret_cast<const unsigned long long*>(t.device_fp), t.ip_class, t.hour, t.weekend, nullptr};
   CtxArgs ca{c.geo_lat, c.geo_lon, c.merchant_lat, c.merchant_lon, c.payment_method, c.transaction_type,
              c.card_type, c.user_agent_flag, c.fraud_score};
   hipLaunchKernelGGL(feat_ext_kernel, dim3(grid_for(n)), dim3(256), 0, e.stream, st.headers.as<const CardHeader>(),
-                     st.fps.as<const unsigned long long>(), st.uext.ptr ? st.uext.as<const UserExt>() : nullptr,
+                     st.uext.ptr ? st.uext.as<const UserExt>() : nullptr,
                      st.merchants.as<const Merchant>(), st.mext.ptr ? st.mext.as<const MerchExt>() : nullptr,
                      (int)st.n_merchants, (int)st.n_mext, n, a, ca,
                      st.slot.as<const unsigned>(), raw, vel5, st.vocab.as<const unsigned char>(), st.tp_threshold,

@@ -14,7 +14,7 @@
 //   route_scan    : one workgroup, exclusive scan of blk in shard-major order -> offsets, counts[s]
 //   route_scatter : per txn, pos = offset[s][b] + rank among same-shard txns before it in the block;
 //                   writes the 48-B transaction record at pos (seq = ingest index)
-//   route_unpack  : owner side, records -> the SoA columns the feature kernel reads
+//   (owner side: the feature kernels read the received records in place, features.hip TxnSrc)
 //   result_pack   : owner side, per scored txn a 24-B result record {fp, conf, seq, decision, risk}
 //   result_scatter: ingest side, out[seq] = record (inverse permutation)
 #include "fd_internal.h"
@@ -130,37 +130,18 @@ __global__ void __launch_bounds__(kRouteBlock) route_scatter_kernel(
   out[pos] = r;
 }
 
-__global__ void __launch_bounds__(256) route_unpack_kernel(const RouteRecord* __restrict__ in, int64_t n,
-                                                           unsigned long long* key, long long* ts, long long* cents,
-                                                           unsigned long long* dfp, int* merchant, unsigned* seq,
-                                                           unsigned char* ipc, unsigned char* hour,
-                                                           unsigned char* wk) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const RouteRecord r = in[i];
-  key[i] = r.key;
-  ts[i] = r.ts;
-  cents[i] = r.cents;
-  dfp[i] = r.dfp;
-  merchant[i] = r.merchant;
-  seq[i] = r.seq;
-  ipc[i] = r.ipc;
-  hour[i] = r.hour;
-  wk[i] = r.wk;
-}
-
 __global__ void __launch_bounds__(256) result_pack_kernel(const double* __restrict__ fp,
                                                           const double* __restrict__ conf,
                                                           const unsigned char* __restrict__ dec,
                                                           const unsigned char* __restrict__ risk,
-                                                          const unsigned* __restrict__ seq, int64_t n,
+                                                          const RouteRecord* __restrict__ rec, int64_t n,
                                                           ResultRecord* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   ResultRecord r;
   r.fraud_prob = fp[i];
   r.confidence = conf[i];
-  r.seq = seq[i];
+  r.seq = rec[i].seq;
   r.decision = dec[i];
   r.risk = risk[i];
   r.pad = 0;
@@ -230,46 +211,11 @@ void launch_route_partition(Engine& e, const fd_txn_batch& t, int64_t n, int G, 
   if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
 }
 
-// Unpack received records into the engine's routed-SoA scratch; returns the batch view and the seq column.
-fd_txn_batch launch_route_unpack(Engine& e, const void* d_records, int64_t n, unsigned** d_seq) {
-  FD_REQUIRE(n >= 0 && n < (1ll << 31), FD_ERR_INVALID_ARG, "batch size out of range");
-  const size_t a8 = (size_t)n * 8, a4 = ((size_t)n * 4 + 15) / 16 * 16, a1 = ((size_t)n + 15) / 16 * 16;
-  e.route_soa.ensure(std::max<size_t>(64, 4 * a8 + 2 * a4 + 3 * a1));
-  char* b = e.route_soa.as<char>();
-  auto* key = reinterpret_cast<unsigned long long*>(b);
-  auto* ts = reinterpret_cast<long long*>(b + a8);
-  auto* cents = reinterpret_cast<long long*>(b + 2 * a8);
-  auto* dfp = reinterpret_cast<unsigned long long*>(b + 3 * a8);
-  auto* merchant = reinterpret_cast<int*>(b + 4 * a8);
-  auto* seq = reinterpret_cast<unsigned*>(b + 4 * a8 + a4);
-  auto* ipc = reinterpret_cast<unsigned char*>(b + 4 * a8 + 2 * a4);
-  auto* hour = ipc + a1;
-  auto* wk = hour + a1;
-  if (n) {
-    FD_REQUIRE(d_records != nullptr, FD_ERR_INVALID_ARG, "null records");
-    hipLaunchKernelGGL(route_unpack_kernel, dim3(grid256(n)), dim3(256), 0, e.stream,
-                       static_cast<const RouteRecord*>(d_records), n, key, ts, cents, dfp, merchant, seq, ipc, hour,
-                       wk);
-    FD_HIP(hipGetLastError());
-  }
-  fd_txn_batch t{};
-  t.card_key = reinterpret_cast<const uint64_t*>(key);
-  t.ts_ms = reinterpret_cast<const int64_t*>(ts);
-  t.amount_cents = reinterpret_cast<const int64_t*>(cents);
-  t.merchant = reinterpret_cast<const int32_t*>(merchant);
-  t.device_fp = reinterpret_cast<const uint64_t*>(dfp);
-  t.ip_class = ipc;
-  t.hour = hour;
-  t.weekend = wk;
-  *d_seq = seq;
-  return t;
-}
-
 void launch_result_pack(Engine& e, const double* fp, const double* conf, const uint8_t* dec, const uint8_t* risk,
-                        const unsigned* seq, int64_t n, void* d_results) {
+                        const RouteRecord* records, int64_t n, void* d_results) {
   if (n == 0) return;
   FD_REQUIRE(d_results != nullptr, FD_ERR_INVALID_ARG, "null result records");
-  hipLaunchKernelGGL(result_pack_kernel, dim3(grid256(n)), dim3(256), 0, e.stream, fp, conf, dec, risk, seq, n,
+  hipLaunchKernelGGL(result_pack_kernel, dim3(grid256(n)), dim3(256), 0, e.stream, fp, conf, dec, risk, records, n,
                      static_cast<ResultRecord*>(d_results));
   FD_HIP(hipGetLastError());
 }

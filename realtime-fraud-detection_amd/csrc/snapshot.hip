@@ -6,7 +6,7 @@
 // on the hot path, so resume / failover needs its own durable image.
 //
 // The image is KEY-addressed, not a dump of the hash table: one record per occupied card slot
-//   { 64-B card header (batch-list head zeroed) | 4 x u64 device fingerprints | K ring events |
+//   { 128-B card header (key, profile + device fingerprints, ring cursor, windows, session) | K ring events |
 //     S x 16 f32 LSTM history | 48-B extended user profile (when loaded) }
 // followed by the replicated tables (merchants, extended merchants, vocabulary) and the Flink window event
 // logs (40-B events, card slots stripped). Restore re-inserts every record by key, so an image restores into
@@ -28,8 +28,7 @@
 namespace fd {
 namespace {
 
-constexpr int kHeaderWords = 4;    // 64-B CardHeader (features.hip): key @0, batch-list head @8
-constexpr int kFpWords = 2;        // 4 x u64 fingerprints per slot
+constexpr int kHeaderWords = kCardHeaderBytes / 16;  // CardHeader (fd_internal.h): key @0
 constexpr int kUextWords = 3;      // 48-B UserExt
 constexpr size_t kMerchantBytes = 16, kMerchExtBytes = 16, kWinEventBytes = 40, kVocabBytes = 512;
 constexpr int64_t kChunkSlots = 1 << 18;
@@ -51,7 +50,7 @@ struct __attribute__((packed)) SnapHeader {  // 256 B, little-endian
 };
 static_assert(sizeof(SnapHeader) == 256, "SnapHeader must be 256 B");
 constexpr char kMagic[8] = {'F', 'D', 'S', 'N', 'A', 'P', 0, 1};
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;  // 2: 128-B card header with the fingerprints folded in (1: 64-B + fps plane)
 
 struct Fnv {
   uint64_t h = 0xcbf29ce484222325ull;
@@ -67,15 +66,14 @@ struct Fnv {
   }
 };
 
-// per-record word map (16-B words): header | fps | ring | seq | uext
+// per-record word map (16-B words): header | ring | seq | uext
 struct RecMap {
   int K, S, uext;
-  int w_fp, w_ring, w_seq, w_uext, words;
+  int w_ring, w_seq, w_uext, words;
 };
 RecMap rec_map(int K, int S, bool uext) {
-  RecMap m{K, S, uext ? 1 : 0, 0, 0, 0, 0, 0};
-  m.w_fp = kHeaderWords;
-  m.w_ring = m.w_fp + kFpWords;
+  RecMap m{K, S, uext ? 1 : 0, 0, 0, 0, 0};
+  m.w_ring = kHeaderWords;
   m.w_seq = m.w_ring + K;
   m.w_uext = m.w_seq + S * 4;
   m.words = m.w_uext + (uext ? kUextWords : 0);
@@ -84,7 +82,6 @@ RecMap rec_map(int K, int S, bool uext) {
 
 struct Planes {  // the per-slot state arrays as 16-B words
   uint4* headers;
-  uint4* fps;
   uint4* ring;
   uint4* seq;
   uint4* uext;
@@ -92,8 +89,7 @@ struct Planes {  // the per-slot state arrays as 16-B words
 
 // the word of `slot`'s state that record word w maps to
 __device__ __forceinline__ uint4* plane_word(const Planes& P, const RecMap& m, long long slot, int w) {
-  if (w < m.w_fp) return P.headers + slot * kHeaderWords + w;
-  if (w < m.w_ring) return P.fps + slot * kFpWords + (w - m.w_fp);
+  if (w < m.w_ring) return P.headers + slot * kHeaderWords + w;
   if (w < m.w_seq) return P.ring + slot * m.K + (w - m.w_ring);
   if (w < m.w_uext) return P.seq + slot * (m.S * 4) + (w - m.w_seq);
   return P.uext + slot * kUextWords + (w - m.w_uext);
@@ -146,9 +142,7 @@ __global__ void __launch_bounds__(256) snap_gather_kernel(Planes P, RecMap m, co
   if (t >= n_words) return;
   const long long r = t / m.words;
   const int w = (int)(t - r * m.words);
-  uint4 v = *plane_word(P, m, (long long)slots[r], w);
-  if (w == 0) v.z = v.w = 0u;  // batch-list head: engine-epoch scoped, meaningless after restore
-  out[t] = v;
+  out[t] = *plane_word(P, m, (long long)slots[r], w);
 }
 
 __global__ void __launch_bounds__(256) restore_slot_kernel(unsigned long long* keys, long long mask,
@@ -161,7 +155,7 @@ __global__ void __launch_bounds__(256) restore_slot_kernel(unsigned long long* k
   const unsigned long long key = ((unsigned long long)h.y << 32) | h.x;
   long long s = -1;
   if (owned(key, shard, G)) {
-    s = slot_of(keys, 64, mask, key);
+    s = slot_of(keys, kCardHeaderBytes, mask, key);
     if (s < 0)
       atomicOr(err, 1u);
     else
@@ -192,7 +186,7 @@ __global__ void __launch_bounds__(256) restore_events_kernel(unsigned long long*
   const unsigned char* ev = in + i * kWinEventBytes;
   const unsigned long long key = *reinterpret_cast<const unsigned long long*>(ev + 16);
   if (!owned(key, shard, G)) return;
-  const long long s = slot_of(keys, 64, mask, key);
+  const long long s = slot_of(keys, kCardHeaderBytes, mask, key);
   if (s < 0) {
     atomicOr(err, 1u);
     return;
@@ -242,7 +236,7 @@ void read_all(FILE* f, void* p, size_t bytes, Fnv* h) {
 }
 
 Planes planes_of(CardStore& st) {
-  return Planes{st.headers.as<uint4>(), st.fps.as<uint4>(), st.ring.as<uint4>(),
+  return Planes{st.headers.as<uint4>(), st.ring.as<uint4>(),
                 st.seq.ptr ? st.seq.as<uint4>() : nullptr, st.uext.ptr ? st.uext.as<uint4>() : nullptr};
 }
 

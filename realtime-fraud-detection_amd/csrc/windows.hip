@@ -420,7 +420,7 @@ void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, 
     WinEvent* ul = w.ulog[w.ucur].as<WinEvent>() + w.ucount;
     WinEvent* ml = w.mlog[w.mcur].as<WinEvent>() + w.mcount;
     hipLaunchKernelGGL(win_append_kernel, dim3(g256(n)), dim3(256), 0, e.stream,
-                       reinterpret_cast<unsigned long long*>(st.headers.ptr), (size_t)64, (long long)(st.cap - 1), n,
+                       reinterpret_cast<unsigned long long*>(st.headers.ptr), (size_t)kCardHeaderBytes, (long long)(st.cap - 1), n,
                        reinterpret_cast<const unsigned long long*>(t.card_key),
                        reinterpret_cast<const long long*>(t.ts_ms), reinterpret_cast<const long long*>(t.amount_cents),
                        reinterpret_cast<const int*>(t.merchant), in.payment_method, in.is_fraud, in.fraud_score, ul,
