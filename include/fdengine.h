@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 9
+#define FD_ABI_VERSION 10
 
 enum fd_status {
   FD_OK = 0,
@@ -109,6 +109,20 @@ int fd_engine_sync(fd_engine* eng);
    (:197-200): repacks the original trees into the engine's depth-major layout and uploads them. */
 int fd_load_forest(fd_engine* eng, int slot, const fd_forest_params* params, const fd_tree_arrays* trees);
 int fd_unload_forest(fd_engine* eng, int slot);
+
+/* Load the reference's XGBoost model FILE unchanged into `slot` (replaces ModelManager._load_xgboost_model,
+   services/ml-models/src/models/model_manager.py:157-161: XGBClassifier().load_model(path); the file is
+   XGBClassifier.save_model's XGBoost 2.0.3 JSON, model_trainer.py:95-108). Parsed in C++ — a C / C++ / JNI
+   host needs no Python — then repacked exactly as fd_load_forest. FD_ERR_IO: unreadable file;
+   FD_ERR_UNSUPPORTED: objective other than binary:logistic, booster other than gbtree, multi-class,
+   categorical splits or vector leaves; FD_ERR_INVALID_ARG: malformed JSON / tree arrays. */
+int fd_load_xgboost_json(fd_engine* eng, int slot, const char* path);
+
+/* Host-only (no device): the same file flattened into caller arrays, the parity hook for the reader.
+   Call with trees == NULL to get *n_trees / *n_nodes, then with trees' arrays sized n_trees + 1 (offsets)
+   and n_nodes (the rest); params receives kind, num_feature and base_score. */
+int fd_xgboost_json_read(const char* path, fd_forest_params* params, int32_t* n_trees, int64_t* n_nodes,
+                         fd_tree_arrays* trees);
 int fd_forest_info(fd_engine* eng, int slot, int32_t* n_trees, int32_t* depth, int32_t* num_feature);
 
 /* Replaces _predict_xgboost (:309-311) / _predict_sklearn (:338-346) for a batch.
@@ -538,7 +552,8 @@ int fd_ingest_scalar_host(int32_t kind, const uint8_t* text, int32_t n, double* 
    count of the timed launches of `kind` (FD_TIMING_ALL: every kind) since the last fd_timing_reset. */
 enum fd_timing_kind { FD_TIMING_ALL = -1, FD_TIMING_XGB = 0, FD_TIMING_IFOREST = 1, FD_TIMING_FEATURES = 2,
                       FD_TIMING_BLEND = 3, FD_TIMING_ROUTE = 4, FD_TIMING_LSTM = 5,
-                      FD_TIMING_WINDOWS = 6, FD_TIMING_INGEST = 7 };
+                      FD_TIMING_WINDOWS = 6, FD_TIMING_INGEST = 7,
+                      FD_TIMING_ENSEMBLE = 8 /* fused XGBoost + IsolationForest + blend kernel */ };
 int fd_engine_set_timing(fd_engine* eng, int enable);
 /* Engine tuning knobs (for A/B measurement; defaults are the tuned choices):
      "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel

@@ -65,13 +65,19 @@ static fd::PackedForest& slot_of(Engine& e, int slot) {
 // Score the same feature matrix with every forest model, then blend (all on e.stream). A model in slot
 // FD_SLOT_LSTM runs the LSTM head over d_seq (n x T x 16) on the auxiliary stream, forked after
 // everything already queued on e.stream (the feature kernel that wrote d_seq) and joined before the blend.
-static void score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slots, const double* const* ext,
+// Returns true when the route result records were written too (the fused ensemble kernel writes them in its
+// epilogue); otherwise the caller packs them from the columns.
+static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slots, const double* const* ext,
                          const uint8_t* present, const float* dX, int64_t n, int32_t ld, double* dMP,
                          double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk, const float* d_seq = nullptr,
-                         int T = 0) {
+                         int T = 0, const fd::RouteRecord* records = nullptr, fd::ResultRecord* results = nullptr) {
   FD_REQUIRE(p.n_models > 0 && p.n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "n_models out of range");
-  FD_REQUIRE(slots != nullptr && dfp != nullptr, FD_ERR_INVALID_ARG, "null slots/output");
-  if (n == 0) return;
+  FD_REQUIRE(slots != nullptr && (dfp != nullptr || results != nullptr), FD_ERR_INVALID_ARG, "null slots/output");
+  if (n == 0) return false;
+  // one XGBoost + one IsolationForest, large batch: both forests and the blend in one kernel
+  if (fd::launch_ensemble(e, p, slots, present, dX, n, ld, dMP, dfp, dconf, ddec, drisk, records, results))
+    return results != nullptr;
+  FD_REQUIRE(dfp != nullptr, FD_ERR_INVALID_ARG, "null output");
   const int M = p.n_models;
   if (!dMP) {
     e.scratch_probs.ensure((size_t)n * M * sizeof(double));
@@ -134,6 +140,7 @@ static void score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     FD_HIP(hipStreamWaitEvent(e.stream, e.join2_ev, 0));
   }
   fd::launch_blend(e, p, n, cols, present, dfp, dconf, ddec, drisk);
+  return false;
 }
 
 // engine scratch for the fused path's LSTM input sequences, when a present model is the LSTM head
@@ -225,6 +232,8 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipEventDestroy(e.join2_ev);
   }
   for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
+  for (auto* b : {&e.ens.nodes[0], &e.ens.nodes[1], &e.ens.leaves[0], &e.ens.leaves[1], &e.ens.thr, &e.ens.thr_off})
+    b->release();
   {  // ingest codec tables and staging
     fd::IngestTables& t = e.ingest;
     for (auto* b : {&t.mkeys, &t.mvals, &t.stage_bytes, &t.stage_offsets, &t.stage_out}) b->release();
@@ -284,6 +293,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   if (k == "forest_kernel") {
     FD_REQUIRE(value >= 0 && value <= 10, FD_ERR_INVALID_ARG, "forest_kernel must be in 0..10");
     e.forest_variant = (int)value;
+  } else if (k == "ensemble") {  // 1 (default): fused forests + blend when applicable; 0: per-model kernels
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble must be 0 or 1");
+    e.ensemble_on = value != 0;
   } else if (k == "ingest_stop_after") {  // diagnostics: 0 full; 1 stage; 2 + structure; 3 + members
     FD_REQUIRE(value >= 0 && value <= 3, FD_ERR_INVALID_ARG, "ingest_stop_after must be in 0..3");
     e.ingest.stop_after = (int)value;
@@ -393,6 +405,63 @@ int fd_pack_forest_binned_host(const fd_forest_params* params, const fd_tree_arr
   FD_API_END
 }
 
+int fd_load_xgboost_json(fd_engine* eng, int slot, const char* path) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  fd::PackedForest& pf = slot_of(e, slot);
+  fd::XgbModel m;
+  fd::read_xgboost_json(path, m);
+  fd_forest_params p{};
+  p.kind = FD_FOREST_XGB_BINARY_LOGISTIC;
+  p.num_feature = m.num_feature;
+  p.base_score = m.base_score;
+  fd_tree_arrays t{};
+  t.n_trees = (int32_t)(m.offsets.size() - 1);
+  t.tree_offsets = m.offsets.data();
+  t.left = m.left.data();
+  t.right = m.right.data();
+  t.feature = m.feature.data();
+  t.threshold = m.threshold.data();
+  t.default_left = m.default_left.data();
+  t.leaf_value = m.leaf_value.data();
+  FD_REQUIRE(t.n_trees > 0, FD_ERR_INVALID_ARG, "xgboost json: no trees");
+  FD_HIP(hipStreamSynchronize(e.stream));  // a reload must not race an in-flight predict
+  pf.loaded = false;
+  fd::repack_forest(pf, p, t);
+  FD_API_END
+}
+
+int fd_xgboost_json_read(const char* path, fd_forest_params* params, int32_t* n_trees, int64_t* n_nodes,
+                         fd_tree_arrays* trees) {
+  FD_API_BEGIN
+  fd::XgbModel m;
+  fd::read_xgboost_json(path, m);
+  const int32_t T = (int32_t)(m.offsets.size() - 1);
+  const int64_t M = (int64_t)m.left.size();
+  if (params) {
+    *params = fd_forest_params{};
+    params->kind = FD_FOREST_XGB_BINARY_LOGISTIC;
+    params->num_feature = m.num_feature;
+    params->base_score = m.base_score;
+  }
+  if (n_trees) *n_trees = T;
+  if (n_nodes) *n_nodes = M;
+  if (trees) {
+    FD_REQUIRE(trees->tree_offsets && trees->left && trees->right && trees->feature && trees->threshold &&
+                   trees->default_left && trees->leaf_value,
+               FD_ERR_INVALID_ARG, "incomplete output arrays");
+    trees->n_trees = T;
+    std::memcpy(const_cast<int64_t*>(trees->tree_offsets), m.offsets.data(), (size_t)(T + 1) * 8);
+    std::memcpy(const_cast<int32_t*>(trees->left), m.left.data(), (size_t)M * 4);
+    std::memcpy(const_cast<int32_t*>(trees->right), m.right.data(), (size_t)M * 4);
+    std::memcpy(const_cast<int32_t*>(trees->feature), m.feature.data(), (size_t)M * 4);
+    std::memcpy(const_cast<double*>(trees->threshold), m.threshold.data(), (size_t)M * 8);
+    std::memcpy(const_cast<uint8_t*>(trees->default_left), m.default_left.data(), (size_t)M);
+    std::memcpy(const_cast<double*>(trees->leaf_value), m.leaf_value.data(), (size_t)M * 8);
+  }
+  FD_API_END
+}
+
 int fd_unload_forest(fd_engine* eng, int slot) {
   FD_API_BEGIN
   Engine& e = E(eng);
@@ -407,6 +476,7 @@ int fd_unload_forest(fd_engine* eng, int slot) {
   pf.split.epoch = 0;
   pf.binned = false;
   pf.loaded = false;
+  pf.gen = 0;  // any ensemble plan built over this slot is stale
   FD_API_END
 }
 
@@ -1023,9 +1093,10 @@ int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const
   uint8_t* risk = dec + n;
   float* sq = lstm_seq_buffer(e, *params, slots, present, n);
   fd::launch_features_records(e, d_records, n, e.feat_vec.as<float>(), sq);  // reads the records in place
-  score_matrix(e, *params, slots, nullptr, present, e.feat_vec.as<float>(), n, FD_VECTOR_WIDTH, nullptr, fp, conf,
-               dec, risk, sq, e.state.S);
-  fd::launch_result_pack(e, fp, conf, dec, risk, static_cast<const fd::RouteRecord*>(d_records), n, d_results);
+  const auto* rec = static_cast<const fd::RouteRecord*>(d_records);
+  if (!score_matrix(e, *params, slots, nullptr, present, e.feat_vec.as<float>(), n, FD_VECTOR_WIDTH, nullptr, fp,
+                    conf, dec, risk, sq, e.state.S, rec, static_cast<fd::ResultRecord*>(d_results)))
+    fd::launch_result_pack(e, fp, conf, dec, risk, rec, n, d_results);
   FD_API_END
 }
 

@@ -102,6 +102,30 @@ struct PackedForest {
   DeviceBuffer n_blob;    // n_n_chunks * n_chunk_stride
   DeviceBuffer n_leaves;  // n_n_chunks * n_chunk * 2^D leaf values (f32 XGBoost / f64 IsolationForest)
   mutable SplitScratch split;
+  // the model as loaded (host copy): the fused ensemble kernel repacks it jointly with the other forest
+  uint64_t gen = 0;  // changes on every load / unload (ensemble plan cache key)
+  fd_forest_params params{};
+  std::vector<int64_t> t_off;
+  std::vector<int32_t> t_left, t_right, t_feature;
+  std::vector<double> t_threshold, t_leaf;
+  std::vector<uint8_t> t_dleft;
+};
+
+// The fused ensemble kernel's joint repack of one XGBoost and/or one IsolationForest (ensemble.hip): both
+// padded to one depth D, node words rewritten against the MERGED per-feature threshold tables, so one bin
+// tile serves both forests; chunks of CH[k] node-only trees, leaf values [tree][2^D] per forest.
+struct EnsemblePlan {
+  bool valid = false;
+  int slot[2] = {-1, -1};   // forest A = the XGBoost model (or the only forest), forest B = the IsolationForest
+  uint64_t gen[2] = {0, 0};
+  int n_forests = 0, D = 0, nf = 0;
+  int kind[2] = {0, 0}, n_trees[2] = {0, 0}, CH[2] = {0, 0}, n_chunks[2] = {0, 0};
+  size_t stride[2] = {0, 0};
+  float base_margin = 0.f;
+  double if_offset = 0.0, if_denominator = 0.0;
+  DeviceBuffer nodes[2], leaves[2], thr, thr_off;
+  std::vector<int32_t> h_thr_off;  // merged table offsets (host copy: binning pass plan)
+  int max_feature_thr = 0;
 };
 
 // card-hash routing records (route.hip): one transaction (48 B) / one result (24 B)
@@ -226,9 +250,11 @@ struct Engine {
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
   DeviceBuffer route_blk, route_out, route_err;  // card-hash routing scratch (route.hip)
+  EnsemblePlan ens;                              // fused XGBoost + IsolationForest + blend (ensemble.hip)
   bool route_err_live = false;
   // optional per-launch kernel timing (HIP events on the launch stream)
   int forest_variant = 0;  // "forest_kernel" option
+  bool ensemble_on = true;  // "ensemble" option: the fused XGBoost + IsolationForest + blend kernel (auto)
   bool timing = false;
   struct Timed {
     hipEvent_t a, b;
@@ -258,8 +284,10 @@ struct HostPack {
   std::vector<char> n_blob, n_leaves;
   int n_chunk = 0, n_n_chunks = 0;
   size_t n_chunk_stride = 0;
+  std::vector<uint8_t> pad;  // [tree][2^D] heap slot is a pad node (a leaf above depth D): either way is right
 };
-HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t);
+// min_depth: pad every tree to at least this depth (the ensemble kernel's common depth)
+HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t, int min_depth = 0);
 void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
                    double* d_prob, double* d_raw, int32_t* d_leaf, hipStream_t stream = nullptr);
@@ -309,6 +337,23 @@ void route_check(Engine& e);
 // lstm.hip
 void load_lstm(Engine& e, const fd_lstm_params& p);
 void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, int T, double* d_prob);
+// model_io.hip: the unchanged XGBoost 2.0.3 JSON model file, flattened (fdengine/forest.py semantics)
+struct XgbModel {
+  int num_feature = 0;
+  double base_score = 0.5;
+  std::vector<int64_t> offsets;
+  std::vector<int32_t> left, right, feature;
+  std::vector<double> threshold, leaf_value;
+  std::vector<uint8_t> default_left;
+};
+void read_xgboost_json(const char* path, XgbModel& out);
+// ensemble.hip: the fused path when the present models are one XGBoost and/or one IsolationForest in engine
+// slots and the batch is large (false: not applicable, the caller runs the per-model kernels + blend).
+// results != nullptr: write route result records (seq from records[i]) instead of the columns.
+bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
+                     const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
+                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results);
+void forest_loaded(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);
 // blend.hip
 void launch_blend(Engine& e, const fd_blend_params& p, int64_t n, const double* const* d_probs,
                   const uint8_t* present, double* d_fp, double* d_conf, uint8_t* d_dec, uint8_t* d_risk);

@@ -38,13 +38,26 @@ namespace {
 
 constexpr long long kWin[3] = {300000LL, 3600000LL, 86400000LL};  // 5 min / 1 h / 24 h
 constexpr long long kSessionTtl = 3600000LL;                      // RedisService TTL 3600 s (ms)
-constexpr int kBT = 256;          // threads of the slot / scatter / bucket kernels
+constexpr int kBT = 256;          // threads of the bucket kernel (and its scans)
+constexpr int kGT = 1024;         // threads of the slot / scatter kernels (one global atomic per bucket per block)
 constexpr int kSegLong = 16;      // segments longer than this take the cooperative path
 constexpr int kChunkCap = 4096;   // (slot, txn) keys sorted per pass in LDS
 constexpr int kMaxBuckets = 4096;
 constexpr int kMaxBins = 4096;    // arrival-range bins of an oversized bucket
 constexpr int kMaxK = 64;
 constexpr size_t kBucketLds = (size_t)kChunkCap * 8 + (size_t)(kMaxBins + 1) * 4;  // keys | bin prefix sums
+
+#ifdef FD_FOREST_PROFILE
+// Phase stamps of the bucket kernel (profiling build only): per workgroup b < 4096 {start, keys loaded,
+// sorted, short segments done (workgroup barrier), end} plus each wave's own end of the short loop.
+__device__ unsigned long long g_fprof[4096 * 8];
+#define FD_FSTAMP(k)                                                                              \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_fprof[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define FD_FSTAMP(k)
+#endif
 
 struct __attribute__((aligned(16))) RingEvent {
   long long ts;
@@ -143,13 +156,13 @@ struct TxnSrc {
 
 // ------------------------------------------------------------------------------------------------
 // per-batch card grouping
-__global__ void __launch_bounds__(kBT) feat_slot_kernel(CardHeader* H, long long mask, int64_t n, TxnSrc src,
+__global__ void __launch_bounds__(kGT) feat_slot_kernel(CardHeader* H, long long mask, int64_t n, TxnSrc src,
                                                         unsigned nbm, unsigned* __restrict__ slot,
                                                         unsigned* __restrict__ bucket_cnt, unsigned* err) {
   extern __shared__ unsigned hist[];  // nbm + 1 counters
-  for (unsigned b = threadIdx.x; b <= nbm; b += kBT) hist[b] = 0u;
+  for (unsigned b = threadIdx.x; b <= nbm; b += kGT) hist[b] = 0u;
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * kBT + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kGT + threadIdx.x;
   if (i < n) {
     const long long s = find_or_insert(H, mask, src.get_key(i));
     if (s < 0) {
@@ -161,19 +174,19 @@ __global__ void __launch_bounds__(kBT) feat_slot_kernel(CardHeader* H, long long
     }
   }
   __syncthreads();
-  for (unsigned b = threadIdx.x; b <= nbm; b += kBT)
+  for (unsigned b = threadIdx.x; b <= nbm; b += kGT)
     if (hist[b]) atomicAdd(&bucket_cnt[b], hist[b]);
 }
 
 // exclusive scan of NB counters into LDS base[] (NB <= kMaxBuckets; every block computes it)
 __device__ void block_bucket_scan(const unsigned* __restrict__ cnt, unsigned nb, unsigned* base, unsigned* part) {
-  const unsigned per = (nb + kBT - 1) / kBT, a = threadIdx.x * per;
+  const unsigned per = (nb + kGT - 1) / kGT, a = threadIdx.x * per;
   unsigned s = 0;
   for (unsigned q = 0; q < per; ++q)
     if (a + q < nb) s += cnt[a + q];
   part[threadIdx.x] = s;
   __syncthreads();
-  for (int d = 1; d < kBT; d <<= 1) {
+  for (int d = 1; d < kGT; d <<= 1) {
     const unsigned v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0u;
     __syncthreads();
     part[threadIdx.x] += v;
@@ -188,22 +201,22 @@ __device__ void block_bucket_scan(const unsigned* __restrict__ cnt, unsigned nb,
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(kBT) feat_scatter_kernel(int64_t n, const unsigned* __restrict__ slot, unsigned nbm,
+__global__ void __launch_bounds__(kGT) feat_scatter_kernel(int64_t n, const unsigned* __restrict__ slot, unsigned nbm,
                                                            const unsigned* __restrict__ bucket_cnt,
                                                            unsigned* __restrict__ bucket_fill,
                                                            unsigned* __restrict__ bucket_base,
                                                            unsigned long long* __restrict__ pairs) {
   extern __shared__ unsigned sh[];  // base[NB] | lcnt[NB] | lbase[NB]
-  __shared__ unsigned part[kBT];
+  __shared__ unsigned part[kGT];
   const unsigned nb = nbm + 1;
   unsigned* base = sh;
   unsigned* lcnt = sh + nb;
   unsigned* lbase = sh + 2 * nb;
-  for (unsigned b = threadIdx.x; b < nb; b += kBT) lcnt[b] = 0u;
+  for (unsigned b = threadIdx.x; b < nb; b += kGT) lcnt[b] = 0u;
   block_bucket_scan(bucket_cnt, nb, base, part);
   if (blockIdx.x == 0)
-    for (unsigned b = threadIdx.x; b < nb; b += kBT) bucket_base[b] = base[b];
-  const int64_t i = (int64_t)blockIdx.x * kBT + threadIdx.x;
+    for (unsigned b = threadIdx.x; b < nb; b += kGT) bucket_base[b] = base[b];
+  const int64_t i = (int64_t)blockIdx.x * kGT + threadIdx.x;
   const unsigned s = i < n ? slot[i] : 0xffffffffu;
   unsigned local = 0, b = 0;
   if (s != 0xffffffffu) {
@@ -211,7 +224,7 @@ __global__ void __launch_bounds__(kBT) feat_scatter_kernel(int64_t n, const unsi
     local = atomicAdd(&lcnt[b], 1u);
   }
   __syncthreads();
-  for (unsigned q = threadIdx.x; q < nb; q += kBT)
+  for (unsigned q = threadIdx.x; q < nb; q += kGT)
     if (lcnt[q]) lbase[q] = atomicAdd(&bucket_fill[q], lcnt[q]);
   __syncthreads();
   if (s != 0xffffffffu) pairs[base[b] + lbase[b] + local] = ((unsigned long long)s << 32) | (unsigned long long)i;
@@ -864,11 +877,16 @@ __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned lon
 // ------------------------------------------------------------------------------------------------
 // the bucket kernel
 
-__device__ void bitonic_sort(unsigned long long* k, int N) {  // ascending, N a power of two, in LDS
+// Ascending bitonic sort of N (a power of two) keys in LDS. Pair idx of a stage touches positions
+// lo = 2*stride*(idx / stride) + idx % stride and lo + stride; the 64 pairs of one wave span 128 consecutive
+// positions, so stages with stride <= 64 stay inside the wave (no workgroup barrier, only wave order).
+__device__ void bitonic_sort(unsigned long long* k, int N) {
   for (int size = 2; size <= N; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int sh = 31 - __clz(stride);
+      if (stride >= 128) __syncthreads();  // other waves' positions: their previous stages must be done
       for (int idx = threadIdx.x; idx < (N >> 1); idx += kBT) {
-        const int lo = 2 * stride * (idx / stride) + (idx % stride), hi = lo + stride;
+        const int lo = ((idx >> sh) << (sh + 1)) + (idx & (stride - 1)), hi = lo + stride;
         const bool asc = (lo & size) == 0;
         const unsigned long long x = k[lo], y = k[hi];
         if ((x > y) == asc) {
@@ -876,9 +894,11 @@ __device__ void bitonic_sort(unsigned long long* k, int N) {  // ascending, N a 
           k[hi] = x;
         }
       }
-      __syncthreads();
+      if (stride >= 128) __syncthreads();
+      else __builtin_amdgcn_wave_barrier();
     }
   }
+  __syncthreads();
 }
 
 // m keys (slot << 32 | arrival index) already in LDS skeys[0, m): sort, then process every segment
@@ -890,7 +910,9 @@ __device__ void process_sorted(const BucketArgs& a, unsigned long long* skeys, i
   for (int q = m + threadIdx.x; q < N; q += kBT) skeys[q] = ~0ull;
   if (threadIdx.x == 0) *n_long = 0;
   __syncthreads();
+  FD_FSTAMP(1);
   if (m > 1) bitonic_sort(skeys, N);
+  FD_FSTAMP(2);
   for (int pos = threadIdx.x; pos < m; pos += kBT) {
     const unsigned s = (unsigned)(skeys[pos] >> 32);
     if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;  // not the first txn of its card
@@ -902,7 +924,12 @@ __device__ void process_sorted(const BucketArgs& a, unsigned long long* skeys, i
     }
     process_short<MODE>(a, s, skeys + pos, len);
   }
+#ifdef FD_FOREST_PROFILE
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)
+    g_fprof[blockIdx.x * 8 + 4 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();
+#endif
   __syncthreads();
+  FD_FSTAMP(3);
   const int nl = *n_long;
   for (int q = 0; q < nl; ++q) {
     const int pos = long_list[q];
@@ -921,6 +948,7 @@ __global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
   __shared__ int n_long, chunk_m;
   unsigned* bins = reinterpret_cast<unsigned*>(skeys + kChunkCap);
   const int b = blockIdx.x;
+  FD_FSTAMP(0);
   const unsigned m = a.bucket_cnt[b];
   const unsigned long long* src = a.pairs + a.bucket_base[b];
   if (m <= (unsigned)kChunkCap) {
@@ -1352,10 +1380,11 @@ __global__ void __launch_bounds__(256) users_ext_load_kernel(CardHeader* H, User
 
 unsigned grid_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
-// buckets of a batch of n: NB = the power of two nearest n / 256 (one 256-thread workgroup per ~256 txns)
+// buckets of a batch of n: NB = the power of two >= n / 128, so a 256-thread bucket workgroup holds ~128
+// cards: one segment per thread (a second round would double the dependent-load chain)
 unsigned buckets_for(int64_t n, int64_t cap) {
   unsigned nb = 1;
-  while ((int64_t)nb * 256 < n && nb < (unsigned)kMaxBuckets && (int64_t)nb < cap) nb <<= 1;
+  while ((int64_t)nb * 128 < n && nb < (unsigned)kMaxBuckets && (int64_t)nb < cap) nb <<= 1;
   return nb;
 }
 
@@ -1477,7 +1506,8 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   const unsigned nb = buckets_for(n, st.cap);
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
-  hipLaunchKernelGGL(feat_slot_kernel, dim3(grid_for(n)), dim3(kBT), nb * sizeof(unsigned), e.stream,
+  const unsigned gblocks = (unsigned)((n + kGT - 1) / kGT);
+  hipLaunchKernelGGL(feat_slot_kernel, dim3(gblocks), dim3(kGT), nb * sizeof(unsigned), e.stream,
                      st.headers.as<CardHeader>(), (long long)(st.cap - 1), n, src, nb - 1, st.slot.as<unsigned>(),
                      st.bucket_cnt.as<unsigned>(), st.err.as<unsigned>());
   FD_HIP(hipGetLastError());
@@ -1491,7 +1521,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLds));
     attrs = true;
   }
-  hipLaunchKernelGGL(feat_scatter_kernel, dim3(grid_for(n)), dim3(kBT), 3 * nb * sizeof(unsigned), e.stream, n,
+  hipLaunchKernelGGL(feat_scatter_kernel, dim3(gblocks), dim3(kGT), 3 * nb * sizeof(unsigned), e.stream, n,
                      st.slot.as<const unsigned>(), nb - 1, st.bucket_cnt.as<const unsigned>(),
                      st.bucket_fill.as<unsigned>(), st.bucket_base.as<unsigned>(), st.pairs.as<unsigned long long>());
   FD_HIP(hipGetLastError());
@@ -1647,5 +1677,11 @@ void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context
                      d_fmap, d_rules);
   FD_HIP(hipGetLastError());
 }
+
+#ifdef FD_FOREST_PROFILE
+extern "C" __attribute__((visibility("default"))) int fd_debug_feat_profile(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprof), sizeof(unsigned long long) * (size_t)n);
+}
+#endif
 
 }  // namespace fd

@@ -24,6 +24,7 @@
 #include <cstring>
 
 #include "fd_internal.h"
+#include "walk_common.h"
 
 namespace fd {
 
@@ -95,7 +96,7 @@ int choose_chunk(int D, int nf, size_t tree_bytes, size_t leaf_sz) {
 
 }  // namespace
 
-HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
+HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t, int min_depth) {
   FD_REQUIRE(p.kind == FD_FOREST_XGB_BINARY_LOGISTIC || p.kind == FD_FOREST_SKLEARN_IFOREST,
              FD_ERR_INVALID_ARG, "unknown forest kind");
   FD_REQUIRE(t.n_trees > 0 && t.tree_offsets && t.left && t.right && t.feature && t.threshold &&
@@ -111,6 +112,8 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
     FD_REQUIRE(b > a, FD_ERR_INVALID_ARG, "empty tree");
     D = std::max(D, tree_depth(t.left + a, t.right + a, b - a));
   }
+  FD_REQUIRE(min_depth <= kMaxDepth, FD_ERR_UNSUPPORTED, "min_depth beyond the supported depth");
+  D = std::max(D, min_depth);
   // engine threshold of an internal node: the f32 t with "go left <=> x < t"
   auto engine_thr = [&](int64_t g) { return xgb ? (float)t.threshold[g] : sklearn_threshold_to_lt(t.threshold[g]); };
 
@@ -168,6 +171,7 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
   }
 
   std::vector<int32_t> cur(2 * NL);
+  hp.pad.assign((size_t)T * NL, 0);
   for (int i = 0; i < T; ++i) {
     const int64_t a = t.tree_offsets[i], m = t.tree_offsets[i + 1] - a;
     const int32_t* L = t.left + a;
@@ -186,6 +190,7 @@ HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t) {
     for (int s = 1; s < NL; ++s) {
       const int32_t o = cur[s];
       if (L[o] < 0) {  // leaf above depth D: pad node, both subtrees resolve to the same leaf
+        hp.pad[(size_t)i * NL + s] = 1;
         nodes[2 * s] = 0;
         nodes[2 * s + 1] = 0;
         if (binnable) bnodes[s] = 0;
@@ -270,6 +275,7 @@ void upload(DeviceBuffer& d, const std::vector<T>& h) {
 
 void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t) {
   const HostPack hp = pack_forest_host(p, t);
+  forest_loaded(pf, p, t);
   upload(pf.blob, hp.blob);
   upload(pf.leaf_ids, hp.leaf_ids);
   pf.kind = hp.kind;
@@ -309,84 +315,6 @@ void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_ar
 // device side
 
 namespace {
-
-typedef __attribute__((address_space(3))) char lds_char;
-typedef __attribute__((address_space(3))) void* lds_ptr;
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-template <typename T>
-__device__ __forceinline__ T lds_load(uint32_t addr) {
-  return *reinterpret_cast<const __attribute__((address_space(3))) T*>((size_t)addr);
-}
-template <typename T>
-__device__ __forceinline__ void lds_store(uint32_t addr, T v) {
-  *reinterpret_cast<__attribute__((address_space(3))) T*>((size_t)addr) = v;
-}
-
-// Tile-wide OR that is also the prologue barrier. Hand-rolled (per-wave ballot -> one LDS word per
-// wave) because __syncthreads_or pulls 256 B of STATIC LDS into the kernel, which shifts the
-// dynamic-LDS base and breaks the 1 KiB-aligned feature-tile addressing of forest_kernel3.
-__device__ __forceinline__ bool tile_any(int pred, uint32_t* flags, int nwaves) {
-  const unsigned long long b = __ballot(pred);
-  if ((threadIdx.x & 63) == 0) flags[threadIdx.x >> 6] = (b != 0ull) ? 1u : 0u;
-  __syncthreads();
-  uint32_t r = 0;
-  for (int i = 0; i < nwaves; ++i) r |= flags[i];
-  return r != 0u;
-}
-
-// Stage one chunk (stride bytes, a multiple of 1 KiB) global -> LDS with LDS-DMA: each
-// wave-instruction moves one 1 KiB piece (64 lanes x 16 B), pieces dealt round-robin to waves.
-__device__ __forceinline__ void stage_chunk(const char* __restrict__ src, char* dst, int stride, int nwaves) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pieces = stride >> 10;
-  for (int p = wave; p < pieces; p += nwaves)
-    __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16), (lds_ptr)(dst + (p << 10)), 16,
-                                     0, 0);
-}
-
-// Same staging, issued through inline asm. While an LDS-DMA issued by the builtin is outstanding,
-// LLVM's waitcnt insertion cannot count LDS reads and emits lgkmcnt(0) before every use, which
-// serialises the walk's independent chains. Hidden from the compiler, the DMA must be completed by
-// the caller: dma_wait() (vmcnt(0)) before the barrier that publishes the chunk.
-__device__ __forceinline__ void stage_chunk_asm(const char* __restrict__ src, uint32_t dst, int stride, int nwaves) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pieces = stride >> 10;
-  for (int p = wave; p < pieces; p += nwaves) {
-    const char* g = src + (p << 10) + lane * 16;
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane(dst + ((uint32_t)p << 10));
-    asm volatile(
-        "s_mov_b32 m0, %0\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off"
-        :
-        : "s"(m0), "v"(g)
-        : "memory", "m0");
-  }
-}
-__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// XGBoost common::Sigmoid (src/common/math.h) in f32 / sklearn score -> decision -> the
-// reference's 1/(1+exp(s)) in f64.
-template <int KIND, typename LeafT>
-__device__ __forceinline__ void write_outputs(LeafT acc, int64_t row, double if_offset, double if_denom,
-                                              double* out_prob, double* out_raw) {
-  if (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) {
-    const float m = (float)acc;
-    const float xm = fminf(-m, 88.7f);
-    const float denom = expf(xm) + 1.0f + 1e-16f;
-    out_prob[row] = (double)(1.0f / denom);
-    if (out_raw) out_raw[row] = (double)m;
-  } else {
-    const double d = (double)acc;
-    const double q = (if_denom != 0.0) ? d / if_denom : 1.0;
-    const double score = pow(2.0, -q);
-    const double decision = -score - if_offset;
-    out_prob[row] = 1.0 / (1.0 + exp(decision));
-    if (out_raw) out_raw[row] = d;
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
 // forest_kernel1: 256 threads = 256 transactions, thread per transaction, CH trees interleaved.
@@ -684,60 +612,6 @@ forest_kernel3(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 // word(x) <= node, the feature-row address is (node & 0xFC00) | lane, and a node's two children are
 // one 8-byte pair read: per level one ds_read_b32 (feature) and one ds_read_b64 (children).
 
-template <int D, int TPG, typename LeafT, bool NAN_AWARE, bool NODE_ONLY = false>
-__device__ __forceinline__ void walk4(uint32_t buf, int gg, uint32_t lane4, uint32_t (&slot)[TPG]) {
-  // tree stride in the staged chunk: node words + leaf values, or node words only (kernel 6)
-  constexpr uint32_t TB = NODE_ONLY ? (4u << D) : (4u + (uint32_t)sizeof(LeafT)) << D;
-  constexpr uint32_t NL = 1u << D;
-  // P = LDS address of the children pair of the current node (heap slot i: tb + 8 i). Chosen child
-  // c = 2i + r has its pair at tb + 8c = 2P - tb + 8r = (P << 1) + (r ? 8 - tb : -tb).
-  uint32_t tb[TPG], c0[TPG], c8[TPG], P[TPG], node[TPG], kl[TPG], kr[TPG], xw[TPG];
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {
-    tb[j] = buf + (uint32_t)(gg * TPG + j) * TB;
-    c0[j] = 0u - tb[j];
-    c8[j] = 8u - tb[j];
-    asm volatile("" : "+v"(c0[j]), "+v"(c8[j]));  // keep the two-term form (one cndmask + one lshl_add)
-    node[j] = lds_load<uint32_t>(tb[j] + 4u);     // heap slot 1
-    P[j] = tb[j] + 8u;                            // slots 2, 3
-  }
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {
-    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
-    if (D > 1) {
-      const u32x2 k = lds_load<u32x2>(P[j]);
-      kl[j] = k.x;
-      kr[j] = k.y;
-    }
-  }
-  // software-pipelined over the TPG chains: chain j's next reads are issued right after its step, so
-  // the wave keeps ~2 (TPG - 1) LDS reads in flight while it steps the other chains
-#pragma unroll
-  for (int l = 0; l < D; ++l) {
-#pragma unroll
-    for (int j = 0; j < TPG; ++j) {
-      bool right = xw[j] > node[j];  // bin > j  <=>  !(x < t_j)
-      if (NAN_AWARE) {
-        if (xw[j] == 0xFFFF0000u) right = (node[j] & 1u) == 0u;  // missing: default direction
-      }
-      P[j] = (P[j] << 1) + (right ? c8[j] : c0[j]);
-      if (l + 1 < D) {
-        uint32_t a = kl[j], b = kr[j];
-        asm volatile("" : "+v"(a), "+v"(b));
-        node[j] = right ? b : a;
-        xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
-        if (l + 2 < D) {
-          const u32x2 k = lds_load<u32x2>(P[j]);
-          kl[j] = k.x;
-          kr[j] = k.y;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) slot[j] = ((P[j] - tb[j]) >> 3) - NL;  // leaf heap slot - 2^D
-}
-
 // walk4 over G independently chosen (tree, transaction group) items: per-chain tree base tb[j] and
 // feature-row lane address l4[j] (forest_kernel6's dynamic item loop).
 template <int D, int G, bool NAN_AWARE>
@@ -877,24 +751,6 @@ __device__ __forceinline__ void load_top(const char* __restrict__ blob, int k, i
     top[j][0] = x.x; top[j][1] = x.y; top[j][2] = x.z; top[j][3] = x.w;
     top[j][4] = y.x; top[j][5] = y.y; top[j][6] = y.z; top[j][7] = y.w;
   }
-}
-
-// largest power of two <= cnt (0 for cnt == 0): binary lifting over cnt entries needs exactly these
-// steps (a feature no split uses — the 64-wide vector's pad slots — costs none)
-__device__ __forceinline__ int lift_steps(int cnt) { return cnt > 0 ? (int)(1u << (31 - __clz(cnt))) : 0; }
-
-// bin(v) = #{t in tbl[0, cnt) : t <= v}, tbl ascending; steps = largest power of two <= cnt.
-template <bool IN_LDS>
-__device__ __forceinline__ uint32_t bin_of(float v, const float* __restrict__ gt, uint32_t lt, int cnt, int steps) {
-  int pos = 0;
-  for (int st = steps; st > 0; st >>= 1) {
-    const int np = pos + st;
-    if (np <= cnt) {
-      const float t = IN_LDS ? lds_load<float>(lt + (uint32_t)(np - 1) * 4u) : gt[np - 1];
-      if (t <= v) pos = np;
-    }
-  }
-  return (uint32_t)pos;
 }
 
 template <int D, int CH, typename LeafT, int KIND, bool TOP>

@@ -148,6 +148,7 @@ FD_TIMING_ROUTE = 4
 FD_TIMING_LSTM = 5
 FD_TIMING_WINDOWS = 6
 FD_TIMING_INGEST = 7
+FD_TIMING_ENSEMBLE = 8
 
 # JSON ingest codec (fd_ingest_out column order and dtypes)
 INGEST_FIELDS = (("card_key", "<u8"), ("ts_ms", "<i8"), ("amount_cents", "<i8"), ("merchant", "<i4"),
@@ -223,6 +224,9 @@ SIGNATURES = {
     "fd_engine_sync": (C.c_int, [_vp]),
     "fd_load_forest": (C.c_int, [_vp, C.c_int, C.POINTER(fd_forest_params), C.POINTER(fd_tree_arrays)]),
     "fd_unload_forest": (C.c_int, [_vp, C.c_int]),
+    "fd_load_xgboost_json": (C.c_int, [_vp, C.c_int, C.c_char_p]),
+    "fd_xgboost_json_read": (C.c_int, [C.c_char_p, C.POINTER(fd_forest_params), C.POINTER(_i32), C.POINTER(_i64),
+                                       C.POINTER(fd_tree_arrays)]),
     "fd_forest_info": (C.c_int, [_vp, C.c_int, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
     "fd_forest_predict_device": (C.c_int, [_vp, C.c_int, _vp, _i64, _i32, _vp, _vp, _vp]),
     "fd_forest_predict_host": (C.c_int, [_vp, C.c_int, _vp, _i64, _i32, _vp, _vp, _vp]),

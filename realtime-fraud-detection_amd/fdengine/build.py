@@ -18,8 +18,8 @@ CSRC = PKG_ROOT / "csrc"
 LIB_DIR = PKG_ROOT / "lib"
 ORACLE_DIR = REPO_ROOT / "oracle"
 
-HIP_SOURCES = ["engine.hip", "forest.hip", "blend.hip", "features.hip", "route.hip", "lstm.hip",
-               "windows.hip", "snapshot.hip", "ingest.hip", "sink.hip"]
+HIP_SOURCES = ["engine.hip", "forest.hip", "ensemble.hip", "blend.hip", "features.hip", "route.hip", "lstm.hip",
+               "windows.hip", "snapshot.hip", "ingest.hip", "sink.hip", "model_io.hip"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-result"]
 
@@ -40,8 +40,9 @@ def _stale(out: Path, inputs) -> bool:
 
 def build_engine(force: bool = False, verbose: bool = True, profile: bool = False) -> Path:
     """One object per translation unit (compiled in parallel, rebuilt only when stale), then one link.
-    profile=True builds lib/libfdengine_prof.so with the forest kernel's phase-cycle
-    instrumentation (-DFD_FOREST_PROFILE; tools/forest_phases.py loads it via FDENGINE_LIB)."""
+    profile=True builds lib/libfdengine_prof.so with the forest and feature kernels' phase-cycle
+    instrumentation (-DFD_FOREST_PROFILE; tools/forest_phases.py / tools/feat_phases.py load it via
+    FDENGINE_LIB)."""
     from concurrent.futures import ThreadPoolExecutor
     LIB_DIR.mkdir(exist_ok=True)
     obj_dir = LIB_DIR / ("obj_prof" if profile else "obj")

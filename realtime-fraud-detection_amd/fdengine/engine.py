@@ -68,7 +68,8 @@ class FraudEngine:
         N.call("fd_engine_set_option", self._h, key.encode(), int(value))
 
     def read_timing(self, kinds=(N.FD_TIMING_XGB, N.FD_TIMING_IFOREST, N.FD_TIMING_FEATURES, N.FD_TIMING_BLEND,
-                                 N.FD_TIMING_ROUTE, N.FD_TIMING_LSTM, N.FD_TIMING_WINDOWS, N.FD_TIMING_INGEST),
+                                 N.FD_TIMING_ROUTE, N.FD_TIMING_LSTM, N.FD_TIMING_WINDOWS, N.FD_TIMING_INGEST,
+                                 N.FD_TIMING_ENSEMBLE),
                     reset: bool = True):
         """-> {kind: (total kernel ms, timed launches)} since the last reset (then resets).
         With a single int `kinds`, returns just that (ms, launches) pair."""
@@ -91,6 +92,14 @@ class FraudEngine:
         nt, d, nf = C.c_int32(), C.c_int32(), C.c_int32()
         N.call("fd_forest_info", self._h, int(slot), C.byref(nt), C.byref(d), C.byref(nf))
         self.forests[slot] = {"kind": fa.kind, "n_trees": nt.value, "depth": d.value, "num_feature": nf.value}
+
+    def load_xgboost_file(self, slot: int, path) -> None:
+        """The reference's XGBoost JSON model file, parsed by the engine itself (fd_load_xgboost_json)."""
+        N.call("fd_load_xgboost_json", self._h, int(slot), os.fsencode(str(path)))
+        nt, d, nf = C.c_int32(), C.c_int32(), C.c_int32()
+        N.call("fd_forest_info", self._h, int(slot), C.byref(nt), C.byref(d), C.byref(nf))
+        self.forests[slot] = {"kind": N.FD_FOREST_XGB_BINARY_LOGISTIC, "n_trees": nt.value, "depth": d.value,
+                              "num_feature": nf.value}
 
     def unload_forest(self, slot: int) -> None:
         N.call("fd_unload_forest", self._h, int(slot))
@@ -496,6 +505,24 @@ def pack_forest_binned_host(fa: ForestArrays):
            C.c_void_p(thr.ctypes.data), info.n_thresholds, C.c_void_p(off.ctypes.data), C.byref(info))
     del keep
     return blob.tobytes(), thr, off, info
+
+
+def read_xgboost_json_native(path) -> ForestArrays:
+    """Host-only: the engine's C++ reader of the XGBoost JSON file (fd_xgboost_json_read), as ForestArrays."""
+    p = N.fd_forest_params()
+    nt, nn = C.c_int32(), C.c_int64()
+    N.call("fd_xgboost_json_read", os.fsencode(str(path)), C.byref(p), C.byref(nt), C.byref(nn), None)
+    T, M = nt.value, nn.value
+    fa = ForestArrays(kind=p.kind, num_feature=p.num_feature, offsets=np.zeros(T + 1, np.int64),
+                      left=np.zeros(M, np.int32), right=np.zeros(M, np.int32), feature=np.zeros(M, np.int32),
+                      threshold=np.zeros(M, np.float64), default_left=np.zeros(M, np.uint8),
+                      leaf_value=np.zeros(M, np.float64), base_score=p.base_score)
+    _, t, keep = fa.c_structs()
+    N.call("fd_xgboost_json_read", os.fsencode(str(path)), C.byref(p), C.byref(nt), C.byref(nn), C.byref(t))
+    out = ForestArrays(kind=fa.kind, num_feature=fa.num_feature, offsets=keep["offsets"], left=keep["left"],
+                       right=keep["right"], feature=keep["feature"], threshold=keep["threshold"],
+                       default_left=keep["default_left"], leaf_value=keep["leaf_value"], base_score=p.base_score)
+    return out
 
 
 def shard_of(keys, n_shards: int) -> np.ndarray:

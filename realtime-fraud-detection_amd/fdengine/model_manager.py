@@ -34,7 +34,7 @@ from typing import Any, Dict, Optional
 import numpy as np
 
 from .engine import FraudEngine
-from .forest import UnsupportedModel, iforest_from_sklearn, load_xgboost_json
+from .forest import UnsupportedModel, iforest_from_sklearn
 
 log = logging.getLogger("fdengine.model_manager")
 
@@ -142,9 +142,10 @@ class ModelManager:
 
     def _load_by_type(self, name: str, cfg):
         slot = self._slot_of.setdefault(name, len(self._slot_of))
-        if cfg.model_type == "xgboost":
-            fa = load_xgboost_json(cfg.model_path)
-            return self._upload(slot, fa, "xgboost")
+        if cfg.model_type == "xgboost":  # the unchanged JSON file, parsed by the engine (fd_load_xgboost_json)
+            self.engine.load_xgboost_file(slot, cfg.model_path)
+            info = self.engine.forest_info(slot)
+            return EngineForest(slot, "xgboost", info["num_feature"], info["n_trees"], info["depth"])
         if cfg.model_type == "sklearn":
             import joblib
             model = joblib.load(cfg.model_path)

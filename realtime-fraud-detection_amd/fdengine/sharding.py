@@ -16,7 +16,8 @@ gloo in the CPU tests):
   5. all_to_all of the 24-B result records back (splits reversed);
   6. fd_route_scatter_results_device: results in the ingest batch's original order.
 Records from one source keep their arrival order and all_to_all concatenates sources in rank order,
-so every card sees its transactions in (step, ingest rank, ingest index) order.
+so every card sees its transactions in (step, ingest rank, ingest index) order. With one shard (world 1)
+the step is the fused hot path on the ingest batch itself (fd_score_batch_device): nothing to route.
 
 The exchange logic is backend-agnostic: `EngineShardBackend` drives libfdengine.so (the product path);
 the CPU tests plug an oracle-backed backend into the same `ShardedScorer` to check the protocol.
@@ -62,6 +63,19 @@ class EngineShardBackend:
             self.eng.score_records_device(self.params, self.slots, rec.data_ptr(), m, res.data_ptr(), self.present)
         return res
 
+    def score_batch(self, txns: dict, n: int):
+        """One shard: the whole hot path on the ingest GPU in arrival order (nothing to route)."""
+        t = self.torch
+        fp = t.empty(n, dtype=t.float64, device=self.device)
+        conf = t.empty(n, dtype=t.float64, device=self.device)
+        dec = t.empty(n, dtype=t.uint8, device=self.device)
+        risk = t.empty(n, dtype=t.uint8, device=self.device)
+        if n:
+            self.eng.score_batch_device(self.params, self.slots, {f: txns[f].data_ptr() for f in N.TXN_FIELDS}, n,
+                                        fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
+                                        present=self.present)
+        return fp, conf, dec, risk
+
     def snapshot(self, path: str, rank: int, world: int) -> int:
         return self.eng.state_snapshot(path, rank, world)
 
@@ -103,11 +117,13 @@ class ShardedScorer:
         -> (fraud_prob f64, confidence f64, decision u8, risk u8) tensors in the same order."""
         import torch
         G = self.world
-        rec, counts = self.be.partition(txns, n, G)
-        if G == 1:
-            res = self.be.score_records(rec, n)
+        if G == 1:  # one shard owns every card: no partition, no exchange
             self.last_counts = ([n], [n])
-            return self.be.scatter_results(res, n)
+            if hasattr(self.be, "score_batch"):
+                return self.be.score_batch(txns, n)
+            rec, _ = self.be.partition(txns, n, 1)
+            return self.be.scatter_results(self.be.score_records(rec, n), n)
+        rec, counts = self.be.partition(txns, n, G)
         recv_counts = torch.empty_like(counts)
         self._a2a(recv_counts, counts)
         both = torch.cat([counts, recv_counts]).cpu().tolist()
