@@ -14,10 +14,11 @@
 // the merged table is staged in LDS in feature ranges (passes) that fit the space of chunk buffer B + the
 // leaf tiles (dead until chunk 1), each transaction's 64-wide vector is binned into the [f][256] u32 tile.
 // Then the chunk stream is XGBoost's CHA-tree chunks followed by the IsolationForest's CHB-tree chunks
-// (node-only, double-buffered by LDS-DMA); per chunk each wave walks its TPG trees for its 64 transactions
-// (walk_common.h walk4), stores the leaf values to the chunk's LDS leaf tile, and a rotating owner tree
-// group adds the previous chunk's values in tree order into the f32 margin (XGBoost) or the f64 path-length
-// sum (IsolationForest): both the reference's sequential sums, bit for bit. Epilogue (tree group 0, one
+// (node-only, one 1 KiB block per tree, double-buffered by LDS-DMA); per chunk each wave walks its TPG trees
+// for its 64 transactions (walk_ens: 4 VALU + 2 LDS reads per node step), loads the leaf values (stored to
+// the chunk's LDS leaf tile one iteration later, so the L2 latency overlaps the barrier), and a rotating
+// owner tree group adds a completed chunk's values in tree order into the f32 margin (XGBoost) or the f64
+// path-length sum (IsolationForest): both the reference's sequential sums, bit for bit. Epilogue (tree group 0, one
 // thread per transaction): sigmoid / IsolationForest transform, blend_row, outputs (columns, or the 24-B
 // route result records of the owner GPU).
 #include <algorithm>
@@ -54,9 +55,7 @@ constexpr int kCHA = 16;  // XGBoost trees per chunk (TPG 4)
 constexpr int kCHB = 12;  // IsolationForest trees per chunk (TPG 3; f64 leaf tiles)
 constexpr int kMaxPass = 64;
 
-size_t round1k_e(size_t b) { return (b + 1023) / 1024 * 1024; }
-
-constexpr uint32_t ens_cs(int D) { return (uint32_t)((kCHA * (4 << D) + 1023) / 1024 * 1024); }
+constexpr uint32_t ens_cs(int) { return (uint32_t)kCHA * 1024u; }  // every tree in a 1 KiB block (walk_ens)
 constexpr uint32_t kEnsLV = (uint32_t)(kCHA * kTile * 4 > kCHB * kTile * 8 ? kCHA * kTile * 4 : kCHB * kTile * 8);
 
 // LDS bytes of the kernel: Xs | bufA | bufB | lvA | lvB | accA (f32) | accB (f64) | flags, + 1 KiB alignment
@@ -69,7 +68,8 @@ struct EnsArgs {
   int64_t n;
   int ld, nf;
   const float* thr;
-  const int32_t* thr_off;
+  int thr_off[kMaxFeatures + 1];  // per-feature table offsets into thr (kernel arguments: scalar loads)
+  int vec4;                       // rows 16-B aligned (ld % 4 == 0, aligned X): float4 row loads
   int n_pass;
   int pass_f[kMaxPass + 1];
   unsigned long long pass_global;  // bit p: pass p bins from global memory (its table does not fit LDS)
@@ -92,20 +92,87 @@ struct EnsArgs {
   ResultRecord* res;
 };
 
+// Ensemble node word: j << 16 | feature << 10 | link << 3 | default_left. `link` makes the next pair address
+// one AND-OR: for a node at heap slot i above the last split level, link = i (its children pair is at byte
+// 8 i of the tree's 1 KiB block); at the last split level link = i - 2^(D-1), so the leaf is 2 link + right.
+// One step is then v_cmp + v_cndmask (child) + v_and_or (bin address) + v_and_or (pair address): 4 VALU, 2 LDS
+// reads (the forest kernels' walk4 needs 5 VALU: it tracks the heap position separately).
+constexpr uint32_t kLinkMask = 0x3F8u;
+
+template <int D, int TPG, bool NAN_AWARE>
+__device__ __forceinline__ void walk_ens(uint32_t buf, int gg, uint32_t lane4, uint32_t (&leaf)[TPG]) {
+  uint32_t tb[TPG], node[TPG], kl[TPG], kr[TPG], xw[TPG];
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) {
+    tb[j] = buf + (uint32_t)(gg * TPG + j) * 1024u;  // 1 KiB aligned: the link OR is exact
+    // in a VGPR: v_and_or_b32 takes one scalar operand on gfx9 (the mask literal), else it splits in two
+    asm volatile("" : "+v"(tb[j]));
+    node[j] = lds_load<uint32_t>(tb[j] + 4u);
+  }
+#pragma unroll
+  for (int j = 0; j < TPG; ++j) {
+    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+    if (D > 1) {
+      const u32x2 k = lds_load<u32x2>(tb[j] + 8u);
+      kl[j] = k.x;
+      kr[j] = k.y;
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < D; ++l) {
+#pragma unroll
+    for (int j = 0; j < TPG; ++j) {
+      bool right = xw[j] > node[j];  // bin > j  <=>  !(x < t_j)
+      if (NAN_AWARE) {
+        if (xw[j] == 0xFFFF0000u) right = (node[j] & 1u) == 0u;  // missing: default direction
+      }
+      if (l + 1 < D) {
+        uint32_t a = kl[j], b = kr[j];
+        asm volatile("" : "+v"(a), "+v"(b));
+        node[j] = right ? b : a;
+        xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+        if (l + 2 < D) {
+          const u32x2 k = lds_load<u32x2>((node[j] & kLinkMask) | tb[j]);
+          kl[j] = k.x;
+          kr[j] = k.y;
+        }
+      } else {
+        leaf[j] = ((node[j] & kLinkMask) >> 2) + (right ? 1u : 0u);
+      }
+    }
+  }
+}
+
+// Walk chunk k of one forest for this wave's TPG trees and issue the leaf-value loads (L2-resident
+// [tree][2^D] table, scalar base + 32-bit lane offset). The values are consumed one iteration later, so
+// their latency overlaps the chunk barrier instead of stalling in front of it.
 template <int D, int TPG, int CH, typename LeafT>
 __device__ __forceinline__ void walk_chunk(uint32_t cur, int gg, uint32_t lane4, bool tile_nan,
-                                           const LeafT* __restrict__ leaves, int k, uint32_t lv, int txn) {
+                                           const LeafT* __restrict__ leaves, int k, LeafT (&lval)[TPG]) {
   constexpr int NL = 1 << D;
-  uint32_t slots[TPG];
+  uint32_t leaf[TPG];
   if (tile_nan)
-    walk4<D, TPG, LeafT, true, true>(cur, gg, lane4, slots);
+    walk_ens<D, TPG, true>(cur, gg, lane4, leaf);
   else
-    walk4<D, TPG, LeafT, false, true>(cur, gg, lane4, slots);
-  LeafT lval[TPG];  // leaf values from global memory (L2-resident), all TPG loads in flight together
+    walk_ens<D, TPG, false>(cur, gg, lane4, leaf);
+  const LeafT* lb = leaves + (size_t)(k * CH + gg * TPG) * NL;  // gg is wave-uniform: a scalar base
 #pragma unroll
-  for (int j = 0; j < TPG; ++j) lval[j] = leaves[((size_t)k * CH + gg * TPG + j) * NL + slots[j]];
+  for (int j = 0; j < TPG; ++j) lval[j] = lb[j * NL + leaf[j]];
+}
+
+template <int TPG, typename LeafT>
+__device__ __forceinline__ void store_leaves(uint32_t lv, int gg, int txn, const LeafT (&lval)[TPG]) {
+  const uint32_t base = lv + ((uint32_t)(gg * TPG) * kTile + (uint32_t)txn) * (uint32_t)sizeof(LeafT);
 #pragma unroll
-  for (int j = 0; j < TPG; ++j) lds_store<LeafT>(lv + ((gg * TPG + j) * kTile + txn) * sizeof(LeafT), lval[j]);
+  for (int j = 0; j < TPG; ++j) lds_store<LeafT>(base + (uint32_t)(j * kTile * sizeof(LeafT)), lval[j]);
+}
+
+// the chunk's LDS-DMA has landed once only the n newest vector-memory operations (its leaf loads) are left
+template <int N>
+__device__ __forceinline__ void dma_wait_but() {
+  if (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // chunk c's leaf values added, in tree order, to its forest's running sum (one transaction)
@@ -125,6 +192,19 @@ __device__ __forceinline__ void owner_add(int c, int nA, uint32_t lvA, uint32_t 
   }
 }
 
+// Staged threshold tables hold element g at word g + g / 32: the binary search's power-of-two strides would
+// otherwise put every lane of a step on one LDS bank (up to 32-way conflicts); one pad word per 32 spreads them.
+__device__ __forceinline__ int thr_pad(int g) { return g + (g >> 5); }
+
+#ifdef FD_FOREST_PROFILE
+// per (workgroup < 256, wave): cycles in prologue, loop top (leaf stores, DMA issue, owner add), walk + leaf
+// loads, DMA wait + barrier, epilogue (s_memtime; read by fd_debug_ens_profile)
+__device__ unsigned long long g_eprof[256 * 16 * 16];
+#define FD_ESTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#else
+#define FD_ESTAMP(var)
+#endif
+
 template <int D, int OUT>
 __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   constexpr int TPGA = kCHA / 4, TPGB = kCHB / 4;
@@ -134,7 +214,7 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   const uint32_t s0 = (sdyn + 1023u) & ~1023u;
   char* const lbase = smem + (s0 - sdyn);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int gg = wave >> 2;
+  const int gg = __builtin_amdgcn_readfirstlane(wave >> 2);  // wave-uniform: scalar addressing
   const int txn = ((wave & 3) << 6) + lane;
   const uint32_t lane4 = s0 + (uint32_t)txn * 4u;
   const uint32_t bufA = s0 + (uint32_t)a.nf * 1024u, bufB = bufA + CS;
@@ -145,40 +225,131 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   const bool valid = row < a.n;
   const int nA = a.n_chunks[0], G = nA + a.n_chunks[1];
 
+#ifdef FD_FOREST_PROFILE
+  unsigned long long pr_top = 0, pr_walk = 0, pr_sync = 0, pr_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  FD_ESTAMP(pr_t0);
   stage_chunk_asm(a.nodes[0], bufA, a.stride[0], kEnsWG / 64);  // chunk 0 lands while the tile is binned
   int anynan = 0;
   {
     uint32_t* Xs = reinterpret_cast<uint32_t*>(lbase);
-    const float* xr = a.X + row * (int64_t)a.ld;
-    const int ncopy = a.ld < a.nf ? a.ld : a.nf;
-    const int q = tid >> 8;  // the four threads sharing `txn` bin every 4th feature of a pass
+    const int q = __builtin_amdgcn_readfirstlane(tid >> 8);  // wave-uniform: the four threads sharing `txn`
+    // (1) raw values: thread (q, txn) loads features [16 q, 16 q + 16) of its row in one go (all loads in
+    // flight together) and stores them transposed into the [f][256] tile (lane = txn: conflict-free)
+    if (valid) {
+      const float* xr = a.X + row * (int64_t)a.ld;
+      const int ncopy = a.ld < a.nf ? a.ld : a.nf;
+      const int fq = q * 16;
+      float v[16];
+      if (a.vec4 && fq + 16 <= ncopy) {
+        const float4* x4 = reinterpret_cast<const float4*>(xr + fq);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float4 t = x4[k];
+          v[4 * k] = t.x;
+          v[4 * k + 1] = t.y;
+          v[4 * k + 2] = t.z;
+          v[4 * k + 3] = t.w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = fq + k < ncopy ? xr[fq + k] : __builtin_nanf("");  // missing: NaN
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (fq + k < a.nf) Xs[(fq + k) * kTile + txn] = __float_as_uint(v[k]);
+    }
+    __syncthreads();
+#ifdef FD_FOREST_PROFILE
+    pr_st[0] = __builtin_amdgcn_s_memtime();
+#endif
+    // (2) per pass: stage its tables, then bin in place four features at a time (independent searches in
+    // lockstep, so four LDS reads are in flight per step)
     for (int p = 0; p < a.n_pass; ++p) {
       const int f0 = a.pass_f[p], f1 = a.pass_f[p + 1];
       const bool glob = (a.pass_global >> p) & 1ull;
       const int o0 = a.thr_off[f0];
-      if (!glob) {  // this pass's tables into bufB + lvA + lvB (dead until chunk 1 / the first leaf store)
-        float* tl = reinterpret_cast<float*>(lbase + (bufB - s0));
+      const uint32_t tl = bufB;  // this pass's tables: bufB + lvA + lvB (dead until chunk 1 / the first leaf store)
+      if (!glob) {
+        float* tp = reinterpret_cast<float*>(lbase + (bufB - s0));
         const int cnt = a.thr_off[f1] - o0;
-        for (int i = tid; i < cnt; i += kEnsWG) tl[i] = a.thr[o0 + i];
+        int i = tid;  // element g at word g + g / 32 (thr_pad)
+        for (; i + 3 * kEnsWG < cnt; i += 4 * kEnsWG) {
+          const float t0 = a.thr[o0 + i], t1 = a.thr[o0 + i + kEnsWG], t2 = a.thr[o0 + i + 2 * kEnsWG],
+                      t3 = a.thr[o0 + i + 3 * kEnsWG];
+          tp[thr_pad(i)] = t0;
+          tp[thr_pad(i + kEnsWG)] = t1;
+          tp[thr_pad(i + 2 * kEnsWG)] = t2;
+          tp[thr_pad(i + 3 * kEnsWG)] = t3;
+        }
+        for (; i < cnt; i += kEnsWG) tp[thr_pad(i)] = a.thr[o0 + i];
         __syncthreads();
       }
-      for (int f = f0 + q; f < f1; f += 4) {
-        uint32_t w = 0;
-        if (valid) {
-          const float v = f < ncopy ? xr[f] : __builtin_nanf("");  // DMatrix: missing column = NaN
-          if (v != v) {
-            w = 0xFFFF0000u;
-            anynan = 1;
+#ifdef FD_FOREST_PROFILE
+      if (p < 3) pr_st[1 + 2 * p] = __builtin_amdgcn_s_memtime();
+#endif
+      if (valid) {
+        for (int fb = f0 + q; fb < f1; fb += 16) {
+          float v[4];
+          int o[4], cnt[4], pos[4];
+          int steps = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int f = fb + 4 * k;
+            const bool act = f < f1;
+            v[k] = act ? __uint_as_float(Xs[f * kTile + txn]) : 0.f;
+            o[k] = act ? a.thr_off[f] : o0;
+            cnt[k] = act ? a.thr_off[f + 1] - o[k] : 0;
+            pos[k] = 0;
+            steps = max(steps, lift_steps(cnt[k]));
+          }
+          // bin = #{t <= v} by binary lifting, as bin_of; branch-free (clamped index + select), so the four
+          // reads of a step issue back to back
+          if (!glob) {
+            for (int st = steps; st > 0; st >>= 1) {
+              float t[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int np = pos[k] + st;
+                const int idx = np <= cnt[k] ? np - 1 : 0;
+                t[k] = lds_load<float>(tl + (uint32_t)thr_pad(o[k] - o0 + idx) * 4u);
+              }
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int np = pos[k] + st;
+                pos[k] = (np <= cnt[k] && t[k] <= v[k]) ? np : pos[k];
+              }
+            }
           } else {
-            const int o = a.thr_off[f], cnt = a.thr_off[f + 1] - o;
-            const uint32_t b = glob ? bin_of<false>(v, a.thr + o, 0u, cnt, lift_steps(cnt))
-                                    : bin_of<true>(v, nullptr, bufB + (uint32_t)(o - o0) * 4u, cnt, lift_steps(cnt));
-            w = b << 16;
+            for (int st = steps; st > 0; st >>= 1) {
+              float t[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int np = pos[k] + st;
+                t[k] = a.thr[o[k] + (np <= cnt[k] ? np - 1 : 0)];
+              }
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int np = pos[k] + st;
+                pos[k] = (np <= cnt[k] && t[k] <= v[k]) ? np : pos[k];
+              }
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int f = fb + 4 * k;
+            if (f < f1) {
+              const bool nan = v[k] != v[k];
+              anynan |= nan ? 1 : 0;
+              Xs[f * kTile + txn] = nan ? 0xFFFF0000u : ((uint32_t)pos[k] << 16);
+            }
           }
         }
-        Xs[f * kTile + txn] = w;
       }
       __syncthreads();  // the staged tables are overwritten by the next pass / chunk 1
+#ifdef FD_FOREST_PROFILE
+      if (p < 3) pr_st[2 + 2 * p] = __builtin_amdgcn_s_memtime();
+#endif
     }
   }
   if (gg == 0) {
@@ -188,24 +359,65 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   dma_wait();  // chunk 0 (published by tile_any's barrier)
   const bool tile_nan = tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (flags - s0)), kEnsWG / 64);
 
-  for (int g = 0; g < G; ++g) {
-    const uint32_t cur = (g & 1) ? bufB : bufA;
+  // Iteration g: store chunk g-1's leaf values (loaded during iteration g-1) to lv[(g-1)&1], stage chunk g+1,
+  // the owner group of chunk g-2 adds lv[g&1] into the sums, walk chunk g and issue its leaf loads; the
+  // barrier then publishes chunk g+1 and lv[(g-1)&1]. Iteration G only drains.
+  float la[TPGA];
+  double lb[TPGB];
+  FD_ESTAMP(pr_t1);
+  for (int g = 0; g <= G; ++g) {
+    FD_ESTAMP(q0);
+    if (g > 0) {
+      const uint32_t lvp = ((g - 1) & 1) ? lvB : lvA;
+      if (g - 1 < nA) store_leaves<TPGA, float>(lvp, gg, txn, la);
+      else store_leaves<TPGB, double>(lvp, gg, txn, lb);
+    }
     if (g + 1 < G) {
       const int h = g + 1, fb = h >= nA ? 1 : 0;
       stage_chunk_asm(a.nodes[fb] + (size_t)(fb ? h - nA : h) * a.stride[fb], (g & 1) ? bufA : bufB, a.stride[fb],
                       kEnsWG / 64);
     }
-    if (g > 0 && gg == ((g - 1) & 3)) owner_add(g - 1, nA, lvA, lvB, accA, accB, txn);
-    const uint32_t lv = (g & 1) ? lvB : lvA;
-    if (g < nA)
-      walk_chunk<D, TPGA, kCHA, float>(cur, gg, lane4, tile_nan, a.leaves_a, g, lv, txn);
-    else
-      walk_chunk<D, TPGB, kCHB, double>(cur, gg, lane4, tile_nan, a.leaves_b, g - nA, lv, txn);
-    dma_wait();
-    __syncthreads();  // chunk g+1 landed; lv[g&1] complete; owner of g-1 done with lv[(g-1)&1]
+    if (g > 1 && gg == ((g - 2) & 3)) owner_add(g - 2, nA, lvA, lvB, accA, accB, txn);
+    const uint32_t cur = (g & 1) ? bufB : bufA;
+    FD_ESTAMP(q1);
+#ifdef FD_FOREST_PROFILE
+    unsigned long long q2 = q1;
+#endif
+    if (g < nA) {
+      walk_chunk<D, TPGA, kCHA, float>(cur, gg, lane4, tile_nan, a.leaves_a, g, la);
+#ifdef FD_FOREST_PROFILE
+      q2 = __builtin_amdgcn_s_memtime();
+#endif
+      dma_wait_but<TPGA>();
+    } else if (g < G) {
+      walk_chunk<D, TPGB, kCHB, double>(cur, gg, lane4, tile_nan, a.leaves_b, g - nA, lb);
+#ifdef FD_FOREST_PROFILE
+      q2 = __builtin_amdgcn_s_memtime();
+#endif
+      dma_wait_but<TPGB>();
+    }
+    __syncthreads();
+#ifdef FD_FOREST_PROFILE
+    const unsigned long long q3 = __builtin_amdgcn_s_memtime();
+    pr_top += q1 - q0;
+    pr_walk += q2 - q1;
+    pr_sync += q3 - q2;
+#endif
   }
   if (G > 0 && gg == ((G - 1) & 3)) owner_add(G - 1, nA, lvA, lvB, accA, accB, txn);
   __syncthreads();
+#ifdef FD_FOREST_PROFILE
+  if (lane == 0 && blockIdx.x < 256) {
+    unsigned long long* o = g_eprof + ((size_t)blockIdx.x * 16 + wave) * 16;
+    for (int k = 0; k < 7; ++k) o[6 + k] = pr_st[k] ? pr_st[k] - pr_t0 : 0;
+    o[0] = pr_t1 - pr_t0;
+    o[1] = pr_top;
+    o[2] = pr_walk;
+    o[3] = pr_sync;
+    o[4] = pr_t0;
+    o[5] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   if (gg != 0 || !valid) return;
 
   // epilogue: the two models' probabilities, then the blend (blend_row.h)
@@ -314,14 +526,14 @@ bool build_plan(Engine& e, int sa, int sb) {
   for (int k = 0; k < 2; ++k) {
     const HostPack& h = hp[k];
     const int T = h.n_trees, nc = (T + CH[k] - 1) / CH[k];
-    const size_t stride = round1k_e((size_t)CH[k] * NL * 4);
+    const size_t stride = (size_t)CH[k] * 1024;  // one 1 KiB block per tree (walk_ens link addressing)
     std::vector<char> nodes((size_t)nc * stride, 0);
     std::vector<char> leaves((size_t)nc * CH[k] * NL * leaf_sz[k], 0);  // padding trees: zero leaves
     for (int i = 0; i < T; ++i) {
       const char* src = h.b_blob.data() + (size_t)(i / h.b_chunk) * h.b_chunk_stride + (size_t)(i % h.b_chunk) *
                                                                                           h.b_tree_bytes;
       uint32_t* dst = reinterpret_cast<uint32_t*>(nodes.data() + (size_t)(i / CH[k]) * stride +
-                                                  (size_t)(i % CH[k]) * NL * 4);
+                                                  (size_t)(i % CH[k]) * 1024);
       for (int s = 1; s < NL; ++s) {
         uint32_t w;
         std::memcpy(&w, src + (size_t)s * 4, 4);
@@ -331,7 +543,8 @@ bool build_plan(Engine& e, int sa, int sb) {
           const uint32_t jm = (uint32_t)(std::lower_bound(merged[f].begin(), merged[f].end(), t) - merged[f].begin());
           w = (jm << 16) | (w & 0xFFFFu);
         }
-        dst[s] = w;
+        const uint32_t link = s < (NL >> 1) ? (uint32_t)s : (uint32_t)(s - (NL >> 1));
+        dst[s] = (w & ~0x3FEu) | (link << 3);  // walk_ens node word
       }
       std::memcpy(leaves.data() + (size_t)i * NL * leaf_sz[k], src + (size_t)NL * 4, (size_t)NL * leaf_sz[k]);
     }
@@ -367,6 +580,12 @@ bool build_plan(Engine& e, int sa, int sb) {
 }
 
 }  // namespace
+
+#ifdef FD_FOREST_PROFILE
+extern "C" __attribute__((visibility("default"))) int fd_debug_ens_profile(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eprof), sizeof(unsigned long long) * (size_t)n);
+}
+#endif
 
 bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
                      const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
@@ -405,7 +624,9 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
   a.ld = ld;
   a.nf = P.nf;
   a.thr = P.thr.as<const float>();
-  a.thr_off = P.thr_off.as<const int32_t>();
+  FD_REQUIRE(P.nf <= kMaxFeatures, FD_ERR_UNSUPPORTED, "ensemble: more than 64 features");
+  for (int f = 0; f <= P.nf; ++f) a.thr_off[f] = P.h_thr_off[f];
+  a.vec4 = (ld % 4 == 0 && (reinterpret_cast<uintptr_t>(dX) & 15u) == 0) ? 1 : 0;
   // binning passes: consecutive features whose tables fit bufB + the leaf tiles; a larger table alone,
   // searched in global memory
   const size_t stage_floats = (ens_cs(P.D) + 2 * (size_t)kEnsLV) / 4;
@@ -414,7 +635,7 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
   while (f < P.nf) {
     const int32_t* o = P.h_thr_off.data();
     int g = f;
-    while (g < P.nf && (size_t)(o[g + 1] - o[f]) <= stage_floats) ++g;
+    while (g < P.nf && (size_t)(o[g + 1] - o[f]) + (size_t)(o[g + 1] - o[f]) / 32 + 1 <= stage_floats) ++g;  // thr_pad
     if (g == f) {  // one feature's table exceeds the LDS space
       a.pass_global |= 1ull << np;
       g = f + 1;

@@ -187,7 +187,7 @@ struct CardStore {
   int S = 0;         // LSTM history events per card (0 = off)
   int64_t n_merchants = 0;
   DeviceBuffer headers, ring, merchants, slot, err, seq;
-  DeviceBuffer bucket_cnt, bucket_fill, bucket_base, pairs;  // per-batch card grouping (feat_slot/scatter/bucket)
+  DeviceBuffer bucket_cnt, bucket_fill, bucket_base, pairs, prep;  // per-batch card grouping (feat_slot/scatter/bucket)
   DeviceBuffer uext, mext, vocab;  // extended profiles + vocabulary flags (feature map, rule scores)
   int64_t n_mext = 0;
   bool vocab_loaded = false;
