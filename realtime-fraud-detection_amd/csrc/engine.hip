@@ -232,7 +232,7 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipEventDestroy(e.join2_ev);
   }
   for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
-  for (auto* b : {&e.ens.nodes[0], &e.ens.nodes[1], &e.ens.leaves[0], &e.ens.leaves[1], &e.ens.thr, &e.ens.thr_off})
+  for (auto* b : {&e.ens.nodes[0], &e.ens.nodes[1], &e.ens.thr})
     b->release();
   {  // ingest codec tables and staging
     fd::IngestTables& t = e.ingest;
@@ -296,6 +296,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "ensemble") {  // 1 (default): fused forests + blend when applicable; 0: per-model kernels
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble must be 0 or 1");
     e.ensemble_on = value != 0;
+  } else if (k == "ensemble_owner") {  // fused kernel: 0 owner tree group rotates per chunk; 1 always group 0
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_owner must be 0 or 1");
+    e.ens_owner_fixed = value != 0;
   } else if (k == "ingest_stop_after") {  // diagnostics: 0 full; 1 stage; 2 + structure; 3 + members
     FD_REQUIRE(value >= 0 && value <= 3, FD_ERR_INVALID_ARG, "ingest_stop_after must be in 0..3");
     e.ingest.stop_after = (int)value;

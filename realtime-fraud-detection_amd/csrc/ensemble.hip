@@ -52,15 +52,19 @@ namespace {
 
 constexpr int kEnsWG = 1024;
 constexpr int kCHA = 16;  // XGBoost trees per chunk (TPG 4)
-constexpr int kCHB = 12;  // IsolationForest trees per chunk (TPG 3; f64 leaf tiles)
+constexpr int kCHB = 12;  // IsolationForest trees per chunk (TPG 3)
 constexpr int kMaxPass = 64;
 
-constexpr uint32_t ens_cs(int) { return (uint32_t)kCHA * 1024u; }  // every tree in a 1 KiB block (walk_ens)
-constexpr uint32_t kEnsLV = (uint32_t)(kCHA * kTile * 4 > kCHB * kTile * 8 ? kCHA * kTile * 4 : kCHB * kTile * 8);
+// A chunk in LDS: CH node blocks of 1 KiB (walk_ens link addressing), then the CH trees' leaf values
+// [CH][2^D]; its LDS buffer is sized for depth 8: max(16 x (1 KiB + 1 KiB f32), 12 x (1 KiB + 2 KiB f64)).
+constexpr uint32_t kEnsBuf = (uint32_t)(kCHA * (1024 + 256 * 4) > kCHB * (1024 + 256 * 8) ? kCHA * (1024 + 256 * 4)
+                                                                                          : kCHB * (1024 + 256 * 8));
+constexpr uint32_t kEnsTile = 4u * kTile * 4u;  // leaf indices of one chunk: [tree group][txn] u32, a byte per tree
 
-// LDS bytes of the kernel: Xs | bufA | bufB | lvA | lvB | accA (f32) | accB (f64) | flags, + 1 KiB alignment
-size_t ens_lds(int nf, int D) {
-  return (size_t)nf * 1024 + 2 * ens_cs(D) + 2 * (size_t)kEnsLV + kTile * 4 + kTile * 8 + 64 + 1024;
+// LDS bytes of the kernel: Xs | bufA | bufB | tile0 | tile1 | accA (f32) | accB (f64) | flags + owner counter,
+// + 1 KiB alignment
+size_t ens_lds(int nf, int /*D*/) {
+  return (size_t)nf * 1024 + 2 * (size_t)kEnsBuf + 2 * (size_t)kEnsTile + kTile * 4 + kTile * 8 + 128 + 1024;
 }
 
 struct EnsArgs {
@@ -70,14 +74,13 @@ struct EnsArgs {
   const float* thr;
   int thr_off[kMaxFeatures + 1];  // per-feature table offsets into thr (kernel arguments: scalar loads)
   int vec4;                       // rows 16-B aligned (ld % 4 == 0, aligned X): float4 row loads
+  int owner_fixed;                // chunk owner: tree group 0 (the oldest waves: highest issue priority), else rotating
   int n_pass;
   int pass_f[kMaxPass + 1];
   unsigned long long pass_global;  // bit p: pass p bins from global memory (its table does not fit LDS)
   const char* nodes[2];
   int n_chunks[2];
   int stride[2];
-  const float* leaves_a;   // XGBoost [tree][2^D] f32
-  const double* leaves_b;  // IsolationForest [tree][2^D] f64
   float base_margin;
   double if_offset, if_denom;
   int pos[2];   // blend position (present-model order) of forest A / B
@@ -100,11 +103,11 @@ struct EnsArgs {
 constexpr uint32_t kLinkMask = 0x3F8u;
 
 template <int D, int TPG, bool NAN_AWARE>
-__device__ __forceinline__ void walk_ens(uint32_t buf, int gg, uint32_t lane4, uint32_t (&leaf)[TPG]) {
+__device__ __forceinline__ void walk_ens(uint32_t buf, int t0, uint32_t lane4, uint32_t (&leaf)[TPG]) {
   uint32_t tb[TPG], node[TPG], kl[TPG], kr[TPG], xw[TPG];
 #pragma unroll
   for (int j = 0; j < TPG; ++j) {
-    tb[j] = buf + (uint32_t)(gg * TPG + j) * 1024u;  // 1 KiB aligned: the link OR is exact
+    tb[j] = buf + (uint32_t)(t0 + j) * 1024u;  // 1 KiB aligned: the link OR is exact
     // in a VGPR: v_and_or_b32 takes one scalar operand on gfx9 (the mask literal), else it splits in two
     asm volatile("" : "+v"(tb[j]));
     node[j] = lds_load<uint32_t>(tb[j] + 4u);
@@ -143,52 +146,59 @@ __device__ __forceinline__ void walk_ens(uint32_t buf, int gg, uint32_t lane4, u
   }
 }
 
-// Walk chunk k of one forest for this wave's TPG trees and issue the leaf-value loads (L2-resident
-// [tree][2^D] table, scalar base + 32-bit lane offset). The values are consumed one iteration later, so
-// their latency overlaps the chunk barrier instead of stalling in front of it.
-template <int D, int TPG, int CH, typename LeafT>
-__device__ __forceinline__ void walk_chunk(uint32_t cur, int gg, uint32_t lane4, bool tile_nan,
-                                           const LeafT* __restrict__ leaves, int k, LeafT (&lval)[TPG]) {
-  constexpr int NL = 1 << D;
+// Walk this wave's TPG trees of the chunk at `cur` (trees gg*TPG ...) for its 64 transactions; the leaf
+// indices (< 2^D <= 256) packed a byte per tree, in tree order, stored as one u32 per (tree group, txn).
+// (Measured: byte-per-tree stores of a [txn][16] tile cost ~5 us more per 64k batch; skewing the split
+// towards tree group 0 was slower still.)
+template <int D, int TPG>
+__device__ __forceinline__ uint32_t walk_pack(uint32_t cur, int gg, uint32_t lane4, bool tile_nan) {
   uint32_t leaf[TPG];
   if (tile_nan)
-    walk_ens<D, TPG, true>(cur, gg, lane4, leaf);
+    walk_ens<D, TPG, true>(cur, gg * TPG, lane4, leaf);
   else
-    walk_ens<D, TPG, false>(cur, gg, lane4, leaf);
-  const LeafT* lb = leaves + (size_t)(k * CH + gg * TPG) * NL;  // gg is wave-uniform: a scalar base
+    walk_ens<D, TPG, false>(cur, gg * TPG, lane4, leaf);
+  uint32_t w = 0;
 #pragma unroll
-  for (int j = 0; j < TPG; ++j) lval[j] = lb[j * NL + leaf[j]];
+  for (int j = 0; j < TPG; ++j) w |= leaf[j] << (8 * j);
+  return w;
 }
 
-template <int TPG, typename LeafT>
-__device__ __forceinline__ void store_leaves(uint32_t lv, int gg, int txn, const LeafT (&lval)[TPG]) {
-  const uint32_t base = lv + ((uint32_t)(gg * TPG) * kTile + (uint32_t)txn) * (uint32_t)sizeof(LeafT);
+// One transaction's share of a finished chunk: its CH leaf values (indices from the tile, values from the
+// chunk's leaf block in LDS) added in tree order to the forest's running sum — the reference's sequential
+// f32 margin / f64 path-length sum, bit for bit.
+template <int D, int TPG, int CH, typename LeafT>
+__device__ __forceinline__ void owner_sum(uint32_t buf, uint32_t tile, uint32_t acc, int txn) {
+  constexpr int NL = 1 << D;
+  uint32_t w[4];
 #pragma unroll
-  for (int j = 0; j < TPG; ++j) lds_store<LeafT>(base + (uint32_t)(j * kTile * sizeof(LeafT)), lval[j]);
+  for (int q = 0; q < 4; ++q) w[q] = lds_load<uint32_t>(tile + (uint32_t)(q * kTile + txn) * 4u);
+  LeafT v[CH];
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const uint32_t idx = (w[t / TPG] >> (8 * (t % TPG))) & 0xFFu;
+    v[t] = lds_load<LeafT>(buf + (uint32_t)(CH * 1024) + ((uint32_t)(t * NL) + idx) * (uint32_t)sizeof(LeafT));
+  }
+  LeafT s = lds_load<LeafT>(acc + (uint32_t)txn * (uint32_t)sizeof(LeafT));
+#pragma unroll
+  for (int t = 0; t < CH; ++t) s += v[t];
+  lds_store<LeafT>(acc + (uint32_t)txn * (uint32_t)sizeof(LeafT), s);
 }
 
-// the chunk's LDS-DMA has landed once only the n newest vector-memory operations (its leaf loads) are left
-template <int N>
-__device__ __forceinline__ void dma_wait_but() {
-  if (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// chunk c's leaf values added, in tree order, to its forest's running sum (one transaction)
-__device__ __forceinline__ void owner_add(int c, int nA, uint32_t lvA, uint32_t lvB, uint32_t accA, uint32_t accB,
-                                          int txn) {
-  const uint32_t lv = (c & 1) ? lvB : lvA;
-  if (c < nA) {
-    float acc = lds_load<float>(accA + txn * 4);
-#pragma unroll
-    for (int t = 0; t < kCHA; ++t) acc += lds_load<float>(lv + (t * kTile + txn) * 4);
-    lds_store<float>(accA + txn * 4, acc);
-  } else {
-    double acc = lds_load<double>(accB + txn * 8);
-#pragma unroll
-    for (int t = 0; t < kCHB; ++t) acc += lds_load<double>(lv + (t * kTile + txn) * 8);
-    lds_store<double>(accB + txn * 8, acc);
+// LDS-DMA of one chunk by the four waves of one tree group (part = transaction group): 1 KiB pieces dealt
+// round-robin; completed by dma_wait() in the issuing waves before the chunk barrier
+__device__ __forceinline__ void stage_chunk_part(const char* __restrict__ src, uint32_t dst, int stride, int part) {
+  const int lane = threadIdx.x & 63;
+  const int pieces = stride >> 10;
+  for (int p = part; p < pieces; p += 4) {
+    const char* g = src + (p << 10) + lane * 16;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(dst + ((uint32_t)p << 10));
+    asm volatile(
+        "s_mov_b32 m0, %0\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off"
+        :
+        : "s"(m0), "v"(g)
+        : "memory", "m0");
   }
 }
 
@@ -208,7 +218,6 @@ __device__ unsigned long long g_eprof[256 * 16 * 16];
 template <int D, int OUT>
 __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   constexpr int TPGA = kCHA / 4, TPGB = kCHB / 4;
-  constexpr uint32_t CS = ens_cs(D);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
   const uint32_t s0 = (sdyn + 1023u) & ~1023u;
@@ -217,10 +226,10 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   const int gg = __builtin_amdgcn_readfirstlane(wave >> 2);  // wave-uniform: scalar addressing
   const int txn = ((wave & 3) << 6) + lane;
   const uint32_t lane4 = s0 + (uint32_t)txn * 4u;
-  const uint32_t bufA = s0 + (uint32_t)a.nf * 1024u, bufB = bufA + CS;
-  const uint32_t lvA = bufB + CS, lvB = lvA + kEnsLV;
-  const uint32_t accA = lvB + kEnsLV, accB = accA + kTile * 4;
-  const uint32_t flags = accB + kTile * 8;
+  const uint32_t bufA = s0 + (uint32_t)a.nf * 1024u, bufB = bufA + kEnsBuf;
+  const uint32_t tile0 = bufB + kEnsBuf, tile1 = tile0 + kEnsTile;
+  const uint32_t accA = tile1 + kEnsTile, accB = accA + kTile * 4;
+  const uint32_t flags = accB + kTile * 8, owner_cnt = flags + 64;
   const int64_t row = (int64_t)blockIdx.x * kTile + txn;
   const bool valid = row < a.n;
   const int nA = a.n_chunks[0], G = nA + a.n_chunks[1];
@@ -229,7 +238,6 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   unsigned long long pr_top = 0, pr_walk = 0, pr_sync = 0, pr_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   FD_ESTAMP(pr_t0);
-  stage_chunk_asm(a.nodes[0], bufA, a.stride[0], kEnsWG / 64);  // chunk 0 lands while the tile is binned
   int anynan = 0;
   {
     uint32_t* Xs = reinterpret_cast<uint32_t*>(lbase);
@@ -269,9 +277,9 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
       const int f0 = a.pass_f[p], f1 = a.pass_f[p + 1];
       const bool glob = (a.pass_global >> p) & 1ull;
       const int o0 = a.thr_off[f0];
-      const uint32_t tl = bufB;  // this pass's tables: bufB + lvA + lvB (dead until chunk 1 / the first leaf store)
+      const uint32_t tl = bufA;  // this pass's tables: bufA + bufB + the tiles (free until chunk 0 is staged)
       if (!glob) {
-        float* tp = reinterpret_cast<float*>(lbase + (bufB - s0));
+        float* tp = reinterpret_cast<float*>(lbase + (bufA - s0));
         const int cnt = a.thr_off[f1] - o0;
         int i = tid;  // element g at word g + g / 32 (thr_pad)
         for (; i + 3 * kEnsWG < cnt; i += 4 * kEnsWG) {
@@ -352,50 +360,49 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
 #endif
     }
   }
+  if (G > 0) stage_chunk_asm(a.nodes[0], bufA, a.stride[0], kEnsWG / 64);  // chunk 0 (the tables are dead)
   if (gg == 0) {
     lds_store<float>(accA + txn * 4, a.base_margin);
     lds_store<double>(accB + txn * 8, 0.0);
   }
+  if (tid == 0) lds_store<uint32_t>(owner_cnt, 0u);
   dma_wait();  // chunk 0 (published by tile_any's barrier)
   const bool tile_nan = tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (flags - s0)), kEnsWG / 64);
 
-  // Iteration g: store chunk g-1's leaf values (loaded during iteration g-1) to lv[(g-1)&1], stage chunk g+1,
-  // the owner group of chunk g-2 adds lv[g&1] into the sums, walk chunk g and issue its leaf loads; the
-  // barrier then publishes chunk g+1 and lv[(g-1)&1]. Iteration G only drains.
-  float la[TPGA];
-  double lb[TPGB];
+  // Iteration g: the owner tree group (0, or (g - 1) & 3 with the rotating schedule) sums chunk g-1 (leaf indices from tile[(g-1)&1], values
+  // from its LDS buffer), waits until all four of its waves are done reading that buffer (LDS counter),
+  // then stages chunk g+1 into it; every wave walks chunk g and stores its packed leaf indices to
+  // tile[g&1]; the owners complete their DMA; the barrier publishes chunk g+1 and tile[g&1].
   FD_ESTAMP(pr_t1);
-  for (int g = 0; g <= G; ++g) {
+  for (int g = 0; g < G; ++g) {
     FD_ESTAMP(q0);
-    if (g > 0) {
-      const uint32_t lvp = ((g - 1) & 1) ? lvB : lvA;
-      if (g - 1 < nA) store_leaves<TPGA, float>(lvp, gg, txn, la);
-      else store_leaves<TPGB, double>(lvp, gg, txn, lb);
+    const bool owner = gg == (a.owner_fixed ? 0 : ((g - 1) & 3));
+    if (owner) {
+      if (g > 0) {
+        const int c = g - 1;
+        const uint32_t bp = (c & 1) ? bufB : bufA, tp = (c & 1) ? tile1 : tile0;
+        if (c < nA) owner_sum<D, TPGA, kCHA, float>(bp, tp, accA, txn);
+        else owner_sum<D, TPGB, kCHB, double>(bp, tp, accB, txn);
+        // the leaf reads of all four owner waves are complete before any of them overwrites the buffer
+        if (lane == 0)
+          __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lbase + (owner_cnt - s0)), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(reinterpret_cast<uint32_t*>(lbase + (owner_cnt - s0)), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP) < 4u * (uint32_t)g)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      if (g + 1 < G) {
+        const int h = g + 1, fb = h >= nA ? 1 : 0;
+        stage_chunk_part(a.nodes[fb] + (size_t)(fb ? h - nA : h) * a.stride[fb], (g & 1) ? bufA : bufB, a.stride[fb],
+                         wave & 3);
+      }
     }
-    if (g + 1 < G) {
-      const int h = g + 1, fb = h >= nA ? 1 : 0;
-      stage_chunk_asm(a.nodes[fb] + (size_t)(fb ? h - nA : h) * a.stride[fb], (g & 1) ? bufA : bufB, a.stride[fb],
-                      kEnsWG / 64);
-    }
-    if (g > 1 && gg == ((g - 2) & 3)) owner_add(g - 2, nA, lvA, lvB, accA, accB, txn);
-    const uint32_t cur = (g & 1) ? bufB : bufA;
+    const uint32_t cur = (g & 1) ? bufB : bufA, tw = (g & 1) ? tile1 : tile0;
     FD_ESTAMP(q1);
-#ifdef FD_FOREST_PROFILE
-    unsigned long long q2 = q1;
-#endif
-    if (g < nA) {
-      walk_chunk<D, TPGA, kCHA, float>(cur, gg, lane4, tile_nan, a.leaves_a, g, la);
-#ifdef FD_FOREST_PROFILE
-      q2 = __builtin_amdgcn_s_memtime();
-#endif
-      dma_wait_but<TPGA>();
-    } else if (g < G) {
-      walk_chunk<D, TPGB, kCHB, double>(cur, gg, lane4, tile_nan, a.leaves_b, g - nA, lb);
-#ifdef FD_FOREST_PROFILE
-      q2 = __builtin_amdgcn_s_memtime();
-#endif
-      dma_wait_but<TPGB>();
-    }
+    const uint32_t w = g < nA ? walk_pack<D, TPGA>(cur, gg, lane4, tile_nan) : walk_pack<D, TPGB>(cur, gg, lane4, tile_nan);
+    lds_store<uint32_t>(tw + (uint32_t)(gg * kTile + txn) * 4u, w);
+    FD_ESTAMP(q2);
+    if (owner) dma_wait();
     __syncthreads();
 #ifdef FD_FOREST_PROFILE
     const unsigned long long q3 = __builtin_amdgcn_s_memtime();
@@ -404,7 +411,12 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     pr_sync += q3 - q2;
 #endif
   }
-  if (G > 0 && gg == ((G - 1) & 3)) owner_add(G - 1, nA, lvA, lvB, accA, accB, txn);
+  if (G > 0 && gg == (a.owner_fixed ? 0 : ((G - 1) & 3))) {
+    const int c = G - 1;
+    const uint32_t bp = (c & 1) ? bufB : bufA, tp = (c & 1) ? tile1 : tile0;
+    if (c < nA) owner_sum<D, TPGA, kCHA, float>(bp, tp, accA, txn);
+    else owner_sum<D, TPGB, kCHB, double>(bp, tp, accB, txn);
+  }
   __syncthreads();
 #ifdef FD_FOREST_PROFILE
   if (lane == 0 && blockIdx.x < 256) {
@@ -526,14 +538,17 @@ bool build_plan(Engine& e, int sa, int sb) {
   for (int k = 0; k < 2; ++k) {
     const HostPack& h = hp[k];
     const int T = h.n_trees, nc = (T + CH[k] - 1) / CH[k];
-    const size_t stride = (size_t)CH[k] * 1024;  // one 1 KiB block per tree (walk_ens link addressing)
-    std::vector<char> nodes((size_t)nc * stride, 0);
-    std::vector<char> leaves((size_t)nc * CH[k] * NL * leaf_sz[k], 0);  // padding trees: zero leaves
+    // chunk: CH node blocks of 1 KiB (walk_ens link addressing), then the CH trees' leaf values [CH][NL];
+    // padding trees (a partial last chunk) keep zero nodes and zero leaves
+    const size_t leaf_bytes = (size_t)CH[k] * NL * leaf_sz[k];
+    const size_t stride = ((size_t)CH[k] * 1024 + leaf_bytes + 1023) / 1024 * 1024;
+    FD_REQUIRE(stride <= kEnsBuf, FD_ERR_UNSUPPORTED, "ensemble chunk exceeds its LDS buffer");
+    std::vector<char> blob((size_t)nc * stride, 0);
     for (int i = 0; i < T; ++i) {
       const char* src = h.b_blob.data() + (size_t)(i / h.b_chunk) * h.b_chunk_stride + (size_t)(i % h.b_chunk) *
                                                                                           h.b_tree_bytes;
-      uint32_t* dst = reinterpret_cast<uint32_t*>(nodes.data() + (size_t)(i / CH[k]) * stride +
-                                                  (size_t)(i % CH[k]) * 1024);
+      char* chunk = blob.data() + (size_t)(i / CH[k]) * stride;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(chunk + (size_t)(i % CH[k]) * 1024);
       for (int s = 1; s < NL; ++s) {
         uint32_t w;
         std::memcpy(&w, src + (size_t)s * 4, 4);
@@ -546,12 +561,11 @@ bool build_plan(Engine& e, int sa, int sb) {
         const uint32_t link = s < (NL >> 1) ? (uint32_t)s : (uint32_t)(s - (NL >> 1));
         dst[s] = (w & ~0x3FEu) | (link << 3);  // walk_ens node word
       }
-      std::memcpy(leaves.data() + (size_t)i * NL * leaf_sz[k], src + (size_t)NL * 4, (size_t)NL * leaf_sz[k]);
+      std::memcpy(chunk + (size_t)CH[k] * 1024 + (size_t)(i % CH[k]) * NL * leaf_sz[k], src + (size_t)NL * 4,
+                  (size_t)NL * leaf_sz[k]);
     }
-    P.nodes[k].ensure(nodes.size());
-    FD_HIP(hipMemcpy(P.nodes[k].ptr, nodes.data(), nodes.size(), hipMemcpyHostToDevice));
-    P.leaves[k].ensure(leaves.size());
-    FD_HIP(hipMemcpy(P.leaves[k].ptr, leaves.data(), leaves.size(), hipMemcpyHostToDevice));
+    P.nodes[k].ensure(blob.size());
+    FD_HIP(hipMemcpy(P.nodes[k].ptr, blob.data(), blob.size(), hipMemcpyHostToDevice));
     P.n_trees[k] = T;
     P.CH[k] = CH[k];
     P.n_chunks[k] = nc;
@@ -559,8 +573,6 @@ bool build_plan(Engine& e, int sa, int sb) {
   }
   P.thr.ensure(std::max<size_t>(4, thr.size() * sizeof(float)));
   if (!thr.empty()) FD_HIP(hipMemcpy(P.thr.ptr, thr.data(), thr.size() * sizeof(float), hipMemcpyHostToDevice));
-  P.thr_off.ensure(off.size() * sizeof(int32_t));
-  FD_HIP(hipMemcpy(P.thr_off.ptr, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   P.h_thr_off = off;
   P.max_feature_thr = maxc;
   P.slot[0] = sa;
@@ -626,10 +638,11 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
   a.thr = P.thr.as<const float>();
   FD_REQUIRE(P.nf <= kMaxFeatures, FD_ERR_UNSUPPORTED, "ensemble: more than 64 features");
   for (int f = 0; f <= P.nf; ++f) a.thr_off[f] = P.h_thr_off[f];
+  a.owner_fixed = e.ens_owner_fixed ? 1 : 0;
   a.vec4 = (ld % 4 == 0 && (reinterpret_cast<uintptr_t>(dX) & 15u) == 0) ? 1 : 0;
-  // binning passes: consecutive features whose tables fit bufB + the leaf tiles; a larger table alone,
+  // binning passes: consecutive features whose tables fit bufA + bufB + the tiles; a larger table alone,
   // searched in global memory
-  const size_t stage_floats = (ens_cs(P.D) + 2 * (size_t)kEnsLV) / 4;
+  const size_t stage_floats = (2 * (size_t)kEnsBuf + 2 * (size_t)kEnsTile) / 4;  // bufA + bufB + the tiles
   int np = 0, f = 0;
   a.pass_f[0] = 0;
   while (f < P.nf) {
@@ -650,8 +663,6 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
     a.n_chunks[q] = P.n_chunks[q];
     a.stride[q] = (int)P.stride[q];
   }
-  a.leaves_a = P.leaves[0].as<const float>();
-  a.leaves_b = P.leaves[1].as<const double>();
   a.base_margin = P.base_margin;
   a.if_offset = P.if_offset;
   a.if_denom = P.if_denominator;

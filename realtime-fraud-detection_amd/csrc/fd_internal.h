@@ -123,7 +123,7 @@ struct EnsemblePlan {
   size_t stride[2] = {0, 0};
   float base_margin = 0.f;
   double if_offset = 0.0, if_denominator = 0.0;
-  DeviceBuffer nodes[2], leaves[2], thr, thr_off;
+  DeviceBuffer nodes[2], thr;  // per forest: chunk blobs (node blocks + leaf values); merged threshold tables
   std::vector<int32_t> h_thr_off;  // merged table offsets (host copy: binning pass plan)
   int max_feature_thr = 0;
 };
@@ -254,6 +254,8 @@ struct Engine {
   bool route_err_live = false;
   // optional per-launch kernel timing (HIP events on the launch stream)
   int forest_variant = 0;  // "forest_kernel" option
+  bool ens_owner_fixed = true;
+  int ens_split = 0;  // "ensemble_split" option: trees per tree group of the fused kernel  // "ensemble_owner" option (A/B of the fused kernel's chunk-owner schedule)
   bool ensemble_on = true;  // "ensemble" option: the fused XGBoost + IsolationForest + blend kernel (auto)
   bool timing = false;
   struct Timed {
