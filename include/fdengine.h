@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 10
+#define FD_ABI_VERSION 11
 
 enum fd_status {
   FD_OK = 0,
@@ -357,6 +357,13 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
                           int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
                           double* d_confidence, uint8_t* d_decision, uint8_t* d_risk);
 
+/* per-transaction window / sink inputs beyond fd_txn_batch; any pointer may be NULL */
+typedef struct fd_window_inputs_s {
+  const uint8_t* payment_method; /* vocabulary code, 255 = null (NULL: all null) */
+  const uint8_t* is_fraud;       /* Transaction.isFraud, nonzero = TRUE (NULL: all false) */
+  const double* fraud_score;     /* Transaction.fraudScore, NaN = null (NULL: all null) */
+} fd_window_inputs;
+
 /* ---------------------------------------------------------------- card-hash sharding */
 /* The reference partitions per-card work by key (Kafka key / Flink keyBy(userId),
    fl/FraudDetectionJob.java; velocity state in one Redis, fl/services/RedisService.java:178-207).
@@ -377,6 +384,16 @@ int fd_shard_of_host(const uint64_t* keys, int64_t n, int32_t n_shards, int32_t*
 /* d_records: n x FD_ROUTE_RECORD_BYTES, owner-major, stable; d_counts: n_shards int64 (device) */
 int fd_route_partition_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, int32_t n_shards,
                               void* d_records, int64_t* d_counts);
+/* same, the records also carrying the window / sink inputs the owner needs (extra may be NULL; its
+   payment_method and is_fraud are read, fraud_score is produced by the owner) */
+int fd_route_partition_ex_device(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* extra,
+                                 int64_t n, int32_t n_shards, void* d_records, int64_t* d_counts);
+/* owner side: received records (+ their result records, may be NULL) back to columns for the window /
+   sink kernels: out's non-NULL fields (card_key, ts_ms, amount_cents, merchant, device_fp, ip_class, hour,
+   weekend) and payment_method / is_fraud / fraud_score (the result's fraud_prob; NaN without results) */
+int fd_route_unpack_device(fd_engine* eng, const void* d_records, const void* d_results, int64_t n,
+                           const fd_txn_batch* out, uint8_t* d_payment_method, uint8_t* d_is_fraud,
+                           double* d_fraud_score);
 /* the whole hot path (fd_score_batch_device) over received records; d_results: n x FD_RESULT_RECORD_BYTES
    {f64 fraud_prob, f64 confidence, u32 seq, u8 decision, u8 risk, u16 pad} in the records' order */
 int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
@@ -399,12 +416,7 @@ typedef struct {
   int64_t log_capacity;            /* events kept per log (user / merchant), 40 B each, device-resident */
   int64_t max_out_of_orderness_ms; /* watermark lag: forBoundedOutOfOrderness(10 s) = 10000 */
 } fd_window_params;
-/* per-transaction window inputs beyond fd_txn_batch; any pointer may be NULL */
-typedef struct {
-  const uint8_t* payment_method; /* vocabulary code, 255 = null (NULL: all null) */
-  const uint8_t* is_fraud;       /* Transaction.isFraud, nonzero = TRUE (NULL: all false) */
-  const double* fraud_score;     /* Transaction.fraudScore, NaN = null (NULL: all null) */
-} fd_window_inputs;
+
 /* UserVelocityAggregate (getResult :292-311) + the Flink window bounds; 96 B */
 typedef struct {
   uint64_t user_key;
@@ -413,12 +425,16 @@ typedef struct {
   int32_t count, fraud_count, high_risk_count, unique_merchants, unique_payment_methods, pad;
   double total_amount, avg_amount, fraud_rate, velocity_score;
 } fd_user_window;
-/* MerchantAggregate (getResult :403-424) + the Flink window bounds; 104 B */
+/* MerchantAggregate (getResult :403-424) + the Flink window bounds + the exact moments it is derived from
+   (what fd_merchant_windows_merge combines across shards); 168 B */
 typedef struct {
   int32_t merchant, count;
   int64_t window_start, window_end, first_ts, last_ts;
   int32_t fraud_count, high_risk_count, unique_users, unique_payment_methods;
   double total_amount, fraud_amount, avg_amount, fraud_rate, amount_stddev, risk_score;
+  int64_t cents, fraud_cents;   /* exact amount sums (integer cents) */
+  uint64_t sq_lo, sq_hi;        /* sum of cents^2, 128-bit */
+  uint64_t pm_mask[4];          /* payment-method codes seen (bit per code) */
 } fd_merchant_window;
 /* allocate the event logs and reset the watermark (needs fd_state_init: cards are keyed by its table;
    fd_state_init / fd_state_clear empty the logs and reset the watermark too). After a failed step
@@ -436,6 +452,17 @@ int fd_windows_step_host(fd_engine* eng, const fd_txn_batch* txns, const fd_wind
                          fd_merchant_window* merchant_out, int64_t merchant_cap, int64_t* n_merchant);
 /* current watermark (INT64_MIN before the first) and events held in the user / merchant logs */
 int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, int64_t* merchant_events);
+/* Sharded windows: every shard advances ONE watermark — before its step, each shard reports the
+   largest event time of the whole node's micro-batch (an all-reduce MAX of the ingest batches); the next step
+   then advances the watermark from it even when this shard received no transaction. Each shard's user
+   windows are complete (cards are owned); its merchant windows are partials over its cards. */
+int fd_windows_observe(fd_engine* eng, int64_t max_event_ts);
+/* Merge merchant-window partials of several shards (host memory, any order): records with the same
+   (merchant, window_start) are combined from their exact moments (counts, cents, cents^2, payment-method
+   set, first / last time; distinct users add: a card lives on one shard) and the derived fields recomputed
+   exactly as the device does. out: capacity n; *n_out merged records sorted by (window_start, merchant).
+   Host only (no GPU needed). */
+int fd_merchant_windows_merge(const fd_merchant_window* parts, int64_t n, fd_merchant_window* out, int64_t* n_out);
 
 /* ---------------------------------------------------------------- sink aggregates */
 /* RedisTransactionSink.updateAggregations (fl/sinks/RedisTransactionSink.java:140-262): per transaction the

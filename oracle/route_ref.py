@@ -14,7 +14,7 @@ from __future__ import annotations
 import numpy as np
 
 RECORD = np.dtype([("key", "<u8"), ("ts", "<i8"), ("cents", "<i8"), ("dfp", "<u8"), ("merchant", "<i4"),
-                   ("seq", "<u4"), ("ipc", "u1"), ("hour", "u1"), ("wk", "u1"), ("pad0", "u1"), ("pad1", "<u4")])
+                   ("seq", "<u4"), ("ipc", "u1"), ("hour", "u1"), ("wk", "u1"), ("pm", "u1"), ("flags", "<u4")])
 RESULT = np.dtype([("fraud_prob", "<f8"), ("confidence", "<f8"), ("seq", "<u4"), ("decision", "u1"),
                    ("risk", "u1"), ("pad", "<u2")])
 assert RECORD.itemsize == 48 and RESULT.itemsize == 24
@@ -42,8 +42,9 @@ def shard_of(keys, G: int) -> np.ndarray:
         return ((hi * np.uint64(G)) >> np.uint64(32)).astype(np.int32)
 
 
-def partition(txns: dict, G: int):
-    """-> (records [n] RECORD, owner-major and stable; counts [G] int64)."""
+def partition(txns: dict, G: int, payment_method=None, is_fraud=None):
+    """-> (records [n] RECORD, owner-major and stable; counts [G] int64). payment_method / is_fraud (optional)
+    ride in the records for the owner's windows and sink (fd_route_partition_ex_device)."""
     owner = shard_of(txns["card_key"], G)
     order = np.argsort(owner, kind="stable")
     n = len(owner)
@@ -57,6 +58,8 @@ def partition(txns: dict, G: int):
     rec["ipc"] = np.asarray(txns["ip_class"], np.uint8)[order]
     rec["hour"] = np.asarray(txns["hour"], np.uint8)[order]
     rec["wk"] = np.asarray(txns["weekend"], np.uint8)[order]
+    rec["pm"] = 255 if payment_method is None else np.asarray(payment_method, np.uint8)[order]
+    rec["flags"] = 0 if is_fraud is None else (np.asarray(is_fraud) != 0).astype(np.uint32)[order]
     return rec, np.bincount(owner, minlength=G).astype(np.int64)
 
 

@@ -96,6 +96,12 @@ class WindowOracle:
         self.wm = None          # None = no watermark yet (Long.MIN_VALUE)
         self.max_seen = None
         self.events = []        # retained events, arrival order
+        self.observed = False   # observe() since the last step (sharded: advance on the node-wide max)
+
+    def observe(self, max_event_ts: int):
+        """fd_windows_observe: the node-wide batch's largest event time (sharded runs)."""
+        self.max_seen = max_event_ts if self.max_seen is None else max(self.max_seen, max_event_ts)
+        self.observed = True
 
     def _fires(self, end: int, w_prev, w_new) -> bool:
         return (w_prev is None or end - 1 > w_prev) and end - 1 <= w_new
@@ -107,9 +113,10 @@ class WindowOracle:
             self.max_seen = e["ts"] if self.max_seen is None else max(self.max_seen, e["ts"])
         w_prev = self.wm
         w_new = w_prev
-        if batch:
+        if (batch or self.observed) and self.max_seen is not None:
             cand = self.max_seen - self.ooo - 1
             w_new = cand if w_new is None else max(w_new, cand)
+        self.observed = False
         if flush and self.max_seen is not None:
             cand = self.max_seen + MERCH_SIZE
             w_new = cand if w_new is None else max(w_new, cand)
@@ -170,4 +177,7 @@ class WindowOracle:
                     first_ts=first, last_ts=last, count=cnt, fraud_count=fraud, high_risk_count=high,
                     unique_users=uniq_u, unique_payment_methods=npm, total_amount=total,
                     fraud_amount=fcents / 100.0, avg_amount=avg, fraud_rate=rate, amount_stddev=sd,
-                    risk_score=merchant_risk(cnt, rate, avg, sd, uniq_u))
+                    risk_score=merchant_risk(cnt, rate, avg, sd, uniq_u),
+                    # the exact moments (fd_merchant_window's merge fields)
+                    cents=cents, fraud_cents=fcents, s2=sum(e["cents"] * e["cents"] for e in evs),
+                    pm_set={e["pm"] for e in evs if e["pm"] != 255})

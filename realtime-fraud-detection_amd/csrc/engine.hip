@@ -804,6 +804,18 @@ int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, i
   FD_API_END
 }
 
+int fd_windows_observe(fd_engine* eng, int64_t max_event_ts) {
+  FD_API_BEGIN
+  fd::windows_observe(E(eng), max_event_ts);
+  FD_API_END
+}
+
+int fd_merchant_windows_merge(const fd_merchant_window* parts, int64_t n, fd_merchant_window* out, int64_t* n_out) {
+  FD_API_BEGIN
+  fd::merchant_windows_merge(parts, n, out, n_out);
+  FD_API_END
+}
+
 int fd_sink_init(fd_engine* eng, const fd_sink_params* params) {
   FD_API_BEGIN
   Engine& e = E(eng);
@@ -1075,7 +1087,26 @@ int fd_route_partition_device(fd_engine* eng, const fd_txn_batch* txns, int64_t 
   FD_API_BEGIN
   Engine& e = E(eng);
   FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
-  fd::launch_route_partition(e, *txns, n, n_shards, d_records, d_counts);
+  fd::launch_route_partition(e, *txns, nullptr, n, n_shards, d_records, d_counts);
+  FD_API_END
+}
+
+int fd_route_partition_ex_device(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* extra, int64_t n,
+                                 int32_t n_shards, void* d_records, int64_t* d_counts) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
+  fd::launch_route_partition(e, *txns, extra, n, n_shards, d_records, d_counts);
+  FD_API_END
+}
+
+int fd_route_unpack_device(fd_engine* eng, const void* d_records, const void* d_results, int64_t n,
+                           const fd_txn_batch* out, uint8_t* d_payment_method, uint8_t* d_is_fraud,
+                           double* d_fraud_score) {
+  FD_API_BEGIN
+  Engine& e = E(eng);
+  FD_REQUIRE(out, FD_ERR_INVALID_ARG, "null output columns");
+  fd::launch_route_unpack(e, d_records, d_results, n, *out, d_payment_method, d_is_fraud, d_fraud_score);
   FD_API_END
 }
 

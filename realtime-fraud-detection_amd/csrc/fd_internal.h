@@ -136,8 +136,9 @@ struct __attribute__((aligned(16))) RouteRecord {
   unsigned long long dfp;
   int merchant;
   unsigned seq;  // index in the ingest rank's micro-batch
-  unsigned char ipc, hour, wk, pad0;
-  unsigned pad1;
+  unsigned char ipc, hour, wk;
+  unsigned char pm;  // payment-method code for the owner's windows (255 = null)
+  unsigned flags;    // bit 0: Transaction.isFraud (owner's windows / sink)
 };
 struct __attribute__((aligned(8))) ResultRecord {
   double fraud_prob;
@@ -201,7 +202,8 @@ struct WindowState {
   int64_t ooo = 10000;                    // watermark lag (ms)
   int64_t wm = INT64_MIN;                 // current watermark
   int64_t min_seen = INT64_MAX;           // smallest event time added (bases the first firing's keys)
-  int64_t max_seen = INT64_MIN;           // largest event time added (flush)
+  int64_t max_seen = INT64_MIN;           // largest event time added (flush) or observed (sharded)
+  bool observed = false;                  // fd_windows_observe since the last step: advance even with n == 0
   DeviceBuffer ulog[2], mlog[2];
   int ucur = 0, mcur = 0;
   int64_t ucount = 0, mcount = 0;
@@ -299,6 +301,8 @@ void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, 
                   fd_user_window* u_out, int64_t u_cap, int64_t* n_user, fd_merchant_window* m_out, int64_t m_cap,
                   int64_t* n_merch);
 void windows_release(Engine& e);
+void windows_observe(Engine& e, int64_t max_event_ts);
+void merchant_windows_merge(const fd_merchant_window* p, int64_t n, fd_merchant_window* out, int64_t* n_out);
 // ingest.hip
 void ingest_set_vocab(Engine& e, int which, const uint8_t* bytes, const int64_t* offsets, int64_t n);
 void ingest_set_merchants(Engine& e, const uint8_t* bytes, const int64_t* offsets, int64_t n);
@@ -330,7 +334,10 @@ void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context
 void features_check(Engine& e);
 // route.hip
 unsigned shard_of_host(unsigned long long key, unsigned G);
-void launch_route_partition(Engine& e, const fd_txn_batch& t, int64_t n, int G, void* d_records, int64_t* d_counts);
+void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_inputs* extra, int64_t n, int G,
+                            void* d_records, int64_t* d_counts);
+void launch_route_unpack(Engine& e, const void* d_records, const void* d_results, int64_t n, const fd_txn_batch& out,
+                         uint8_t* pm, uint8_t* fraud, double* score);
 void launch_result_pack(Engine& e, const double* fp, const double* conf, const uint8_t* dec, const uint8_t* risk,
                         const RouteRecord* records, int64_t n, void* d_results);
 void launch_result_scatter(Engine& e, const void* d_results, int64_t n, double* fp, double* conf, uint8_t* dec,

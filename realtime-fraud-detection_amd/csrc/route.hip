@@ -98,7 +98,8 @@ __global__ void __launch_bounds__(1024) route_scan_kernel(int* __restrict__ blk,
 __global__ void __launch_bounds__(kRouteBlock) route_scatter_kernel(
     const unsigned long long* __restrict__ key, const long long* __restrict__ ts, const long long* __restrict__ cents,
     const int* __restrict__ merchant, const unsigned long long* __restrict__ dfp, const unsigned char* __restrict__ ipc,
-    const unsigned char* __restrict__ hour, const unsigned char* __restrict__ wk, int64_t n, unsigned G, int nblk,
+    const unsigned char* __restrict__ hour, const unsigned char* __restrict__ wk,
+    const unsigned char* __restrict__ pm, const unsigned char* __restrict__ fraud, int64_t n, unsigned G, int nblk,
     const int* __restrict__ blk, RouteRecord* __restrict__ out) {
   __shared__ int wcnt[kRouteBlock / 64][64];
   const int64_t i = (int64_t)blockIdx.x * kRouteBlock + threadIdx.x;
@@ -125,9 +126,32 @@ __global__ void __launch_bounds__(kRouteBlock) route_scatter_kernel(
   r.ipc = ipc[i];
   r.hour = hour[i];
   r.wk = wk[i];
-  r.pad0 = 0;
-  r.pad1 = 0;
+  r.pm = pm ? pm[i] : (unsigned char)255;
+  r.flags = (fraud && fraud[i]) ? 1u : 0u;
   out[pos] = r;
+}
+
+// owner side: records (+ their result records) back to columns for the window / sink kernels
+__global__ void __launch_bounds__(256) route_unpack_kernel(const RouteRecord* __restrict__ rec,
+                                                           const ResultRecord* __restrict__ res, int64_t n,
+                                                           unsigned long long* key, long long* ts, long long* cents,
+                                                           int* merchant, unsigned long long* dfp, unsigned char* ipc,
+                                                           unsigned char* hour, unsigned char* wk, unsigned char* pm,
+                                                           unsigned char* fraud, double* score) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const RouteRecord r = rec[i];
+  if (key) key[i] = r.key;
+  if (ts) ts[i] = r.ts;
+  if (cents) cents[i] = r.cents;
+  if (merchant) merchant[i] = r.merchant;
+  if (dfp) dfp[i] = r.dfp;
+  if (ipc) ipc[i] = r.ipc;
+  if (hour) hour[i] = r.hour;
+  if (wk) wk[i] = r.wk;
+  if (pm) pm[i] = r.pm;
+  if (fraud) fraud[i] = (unsigned char)(r.flags & 1u);
+  if (score) score[i] = res ? res[i].fraud_prob : __builtin_nan("");
 }
 
 __global__ void __launch_bounds__(256) result_pack_kernel(const double* __restrict__ fp,
@@ -178,8 +202,8 @@ unsigned shard_of_host(unsigned long long key, unsigned G) {
   return (unsigned)(((key >> 32) * (unsigned long long)G) >> 32);
 }
 
-void launch_route_partition(Engine& e, const fd_txn_batch& t, int64_t n, int G, void* d_records,
-                            int64_t* d_counts) {
+void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_inputs* extra, int64_t n, int G,
+                            void* d_records, int64_t* d_counts) {
   FD_REQUIRE(G >= 1 && G <= FD_MAX_SHARDS, FD_ERR_INVALID_ARG, "n_shards must be in [1, 64]");
   FD_REQUIRE(n >= 0 && n < (1ll << 31), FD_ERR_INVALID_ARG, "batch size out of range");
   FD_REQUIRE(d_counts != nullptr, FD_ERR_INVALID_ARG, "null counts");
@@ -205,10 +229,28 @@ void launch_route_partition(Engine& e, const fd_txn_batch& t, int64_t n, int G, 
   hipLaunchKernelGGL(route_scatter_kernel, dim3(nblk), dim3(kRouteBlock), 0, e.stream, key,
                      reinterpret_cast<const long long*>(t.ts_ms), reinterpret_cast<const long long*>(t.amount_cents),
                      reinterpret_cast<const int*>(t.merchant), reinterpret_cast<const unsigned long long*>(t.device_fp),
-                     t.ip_class, t.hour, t.weekend, n, (unsigned)G, nblk, e.route_blk.as<const int>(),
+                     t.ip_class, t.hour, t.weekend, extra ? extra->payment_method : nullptr,
+                     extra ? extra->is_fraud : nullptr, n, (unsigned)G, nblk, e.route_blk.as<const int>(),
                      static_cast<RouteRecord*>(d_records));
   FD_HIP(hipGetLastError());
   if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
+}
+
+void launch_route_unpack(Engine& e, const void* d_records, const void* d_results, int64_t n, const fd_txn_batch& out,
+                         uint8_t* pm, uint8_t* fraud, double* score) {
+  FD_REQUIRE(n >= 0 && n < (1ll << 31), FD_ERR_INVALID_ARG, "batch size out of range");
+  if (n == 0) return;
+  FD_REQUIRE(d_records != nullptr, FD_ERR_INVALID_ARG, "null records");
+  hipLaunchKernelGGL(route_unpack_kernel, dim3(grid256(n)), dim3(256), 0, e.stream,
+                     static_cast<const RouteRecord*>(d_records), static_cast<const ResultRecord*>(d_results), n,
+                     reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(out.card_key)),
+                     reinterpret_cast<long long*>(const_cast<int64_t*>(out.ts_ms)),
+                     reinterpret_cast<long long*>(const_cast<int64_t*>(out.amount_cents)),
+                     const_cast<int32_t*>(out.merchant),
+                     reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(out.device_fp)),
+                     const_cast<uint8_t*>(out.ip_class), const_cast<uint8_t*>(out.hour),
+                     const_cast<uint8_t*>(out.weekend), pm, fraud, score);
+  FD_HIP(hipGetLastError());
 }
 
 void launch_result_pack(Engine& e, const double* fp, const double* conf, const uint8_t* dec, const uint8_t* risk,

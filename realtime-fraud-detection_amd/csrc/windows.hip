@@ -26,7 +26,10 @@
 //   win_reduce_* : one thread per window segment (contiguous after the sort): counts, cents, distinct
 //                  merchants / users (key changes), payment-method bitmask, min / max event time -> result
 //   win_compact  : drop events no open window can still contain
+#include <algorithm>
 #include <cstring>
+#include <numeric>
+#include <vector>
 
 #include <rocprim/rocprim.hpp>
 
@@ -237,6 +240,38 @@ __global__ void __launch_bounds__(256) win_reduce_user_kernel(const WinEvent* __
   out[o] = r;
 }
 
+// MerchantAggregateFunction.getResult (:403-424) from the exact moments: avg, fraud rate, population
+// stddev (calculateStandardDeviation :447-457 as the integer-moment formula) and calculateMerchantRiskScore
+// (:459-483). Shared by the reduce kernel and the host merge of shard partials (fd_merchant_windows_merge),
+// so a merged window is bit-identical to one reduced whole.
+__host__ __device__ inline void merchant_window_finalize(fd_merchant_window& r) {
+#pragma clang fp contract(off)
+  const int cnt = r.count;
+  r.unique_payment_methods = __builtin_popcountll(r.pm_mask[0]) + __builtin_popcountll(r.pm_mask[1]) +
+                             __builtin_popcountll(r.pm_mask[2]) + __builtin_popcountll(r.pm_mask[3]);
+  r.total_amount = (double)r.cents / 100.0;
+  r.fraud_amount = (double)r.fraud_cents / 100.0;
+  r.avg_amount = cnt > 0 ? r.total_amount / cnt : 0.0;
+  r.fraud_rate = cnt > 0 ? (double)r.fraud_count / cnt : 0.0;
+  // population stddev, exact moments: (n S2 - S1^2) / n^2 cents^2
+  double sd = 0.0;
+  if (cnt >= 2) {
+    const unsigned __int128 s2 = ((unsigned __int128)r.sq_hi << 64) | (unsigned __int128)r.sq_lo;
+    const __int128 num = (__int128)cnt * (__int128)s2 - (__int128)r.cents * (__int128)r.cents;
+    const double var = (double)num / ((double)cnt * (double)cnt);
+    sd = sqrt(var) / 100.0;
+  }
+  r.amount_stddev = sd;
+  double score = 0.0;
+  score += r.fraud_rate * 0.5;
+  if (cnt > 1000) score += 0.2;
+  else if (cnt > 500) score += 0.1;
+  if (r.avg_amount > 0 && sd / r.avg_amount > 2.0) score += 0.2;
+  const double diversity = cnt > 0 ? (double)r.unique_users / cnt : 0.0;
+  if (diversity < 0.1) score += 0.3;
+  r.risk_score = fmin(1.0, score);
+}
+
 __global__ void __launch_bounds__(256) win_reduce_merchant_kernel(const WinEvent* __restrict__ log,
                                                                   const unsigned long long* __restrict__ keys,
                                                                   const unsigned* __restrict__ vals, unsigned n,
@@ -282,28 +317,12 @@ __global__ void __launch_bounds__(256) win_reduce_merchant_kernel(const WinEvent
   r.fraud_count = fraud;
   r.high_risk_count = high;
   r.unique_users = uniq_u;
-  r.unique_payment_methods = __popcll(pm[0]) + __popcll(pm[1]) + __popcll(pm[2]) + __popcll(pm[3]);
-  r.total_amount = (double)cents / 100.0;
-  r.fraud_amount = (double)fcents / 100.0;
-  r.avg_amount = cnt > 0 ? r.total_amount / cnt : 0.0;
-  r.fraud_rate = cnt > 0 ? (double)fraud / cnt : 0.0;
-  // population stddev (calculateStandardDeviation :447-457), exact moments: (n S2 - S1^2) / n^2 cents^2
-  double sd = 0.0;
-  if (cnt >= 2) {
-    const __int128 num = (__int128)cnt * (__int128)s2 - (__int128)cents * (__int128)cents;
-    const double var = (double)num / ((double)cnt * (double)cnt);
-    sd = sqrt(var) / 100.0;
-  }
-  r.amount_stddev = sd;
-  // calculateMerchantRiskScore (:459-483)
-  double score = 0.0;
-  score += r.fraud_rate * 0.5;
-  if (cnt > 1000) score += 0.2;
-  else if (cnt > 500) score += 0.1;
-  if (r.avg_amount > 0 && sd / r.avg_amount > 2.0) score += 0.2;
-  const double diversity = cnt > 0 ? (double)uniq_u / cnt : 0.0;
-  if (diversity < 0.1) score += 0.3;
-  r.risk_score = fmin(1.0, score);
+  r.cents = cents;
+  r.fraud_cents = fcents;
+  r.sq_lo = (unsigned long long)s2;
+  r.sq_hi = (unsigned long long)(s2 >> 64);
+  for (int q = 0; q < 4; ++q) r.pm_mask[q] = pm[q];
+  merchant_window_finalize(r);
   const unsigned o = atomicAdd(out_count, 1u);
   if (o >= cap) {
     atomicOr(err, 8u);
@@ -439,7 +458,9 @@ void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, 
   }
   const long long w_prev = w.wm;
   long long w_new = w_prev;
-  if (n > 0 && w.max_seen - w.ooo - 1 > w_new) w_new = w.max_seen - w.ooo - 1;  // BoundedOutOfOrdernessWatermarks
+  // BoundedOutOfOrdernessWatermarks; a sharded step also advances on the node-wide max (fd_windows_observe)
+  if ((n > 0 || w.observed) && w.max_seen - w.ooo - 1 > w_new) w_new = w.max_seen - w.ooo - 1;
+  w.observed = false;
   if (flush && w.max_seen != INT64_MIN && w.max_seen + kMerchSize > w_new) w_new = w.max_seen + kMerchSize;
   if (w_new == w_prev) return;  // no window can fire
   w.wm = w_new;
@@ -512,6 +533,47 @@ void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, 
     cur ^= 1;
   }
   FD_HIP(hipStreamSynchronize(e.stream));
+}
+
+void windows_observe(Engine& e, int64_t max_event_ts) {
+  WindowState& w = e.windows;
+  FD_REQUIRE(w.ready, FD_ERR_NOT_LOADED, "windows not initialised (fd_windows_init)");
+  w.max_seen = std::max<int64_t>(w.max_seen, max_event_ts);
+  w.observed = true;
+}
+
+void merchant_windows_merge(const fd_merchant_window* p, int64_t n, fd_merchant_window* out, int64_t* n_out) {
+  FD_REQUIRE(n >= 0 && (n == 0 || (p && out)) && n_out, FD_ERR_INVALID_ARG, "bad arguments");
+  std::vector<int64_t> idx((size_t)n);
+  std::iota(idx.begin(), idx.end(), (int64_t)0);
+  std::stable_sort(idx.begin(), idx.end(), [p](int64_t a, int64_t b) {
+    return p[a].window_start != p[b].window_start ? p[a].window_start < p[b].window_start
+                                                  : p[a].merchant < p[b].merchant;
+  });
+  int64_t m = 0;
+  for (int64_t k : idx) {
+    const fd_merchant_window& b = p[k];
+    if (m > 0 && out[m - 1].window_start == b.window_start && out[m - 1].merchant == b.merchant) {
+      fd_merchant_window& a = out[m - 1];
+      a.count += b.count;
+      a.fraud_count += b.fraud_count;
+      a.high_risk_count += b.high_risk_count;
+      a.unique_users += b.unique_users;  // a card (user) lives on one shard: the sets are disjoint
+      a.cents += b.cents;
+      a.fraud_cents += b.fraud_cents;
+      const unsigned __int128 s2 = (((unsigned __int128)a.sq_hi << 64) | a.sq_lo) +
+                                   (((unsigned __int128)b.sq_hi << 64) | b.sq_lo);
+      a.sq_lo = (uint64_t)s2;
+      a.sq_hi = (uint64_t)(s2 >> 64);
+      for (int q = 0; q < 4; ++q) a.pm_mask[q] |= b.pm_mask[q];
+      if (a.first_ts == 0 || (b.first_ts != 0 && b.first_ts < a.first_ts)) a.first_ts = b.first_ts;  // add() rule
+      if (b.last_ts > a.last_ts) a.last_ts = b.last_ts;
+    } else {
+      out[m++] = b;
+    }
+  }
+  for (int64_t i = 0; i < m; ++i) merchant_window_finalize(out[i]);
+  *n_out = m;
 }
 
 void windows_release(Engine& e) {

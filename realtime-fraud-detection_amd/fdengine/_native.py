@@ -194,7 +194,9 @@ MERCHANT_WINDOW_DTYPE = [("merchant", "<i4"), ("count", "<i4"), ("window_start",
                          ("first_ts", "<i8"), ("last_ts", "<i8"), ("fraud_count", "<i4"),
                          ("high_risk_count", "<i4"), ("unique_users", "<i4"), ("unique_payment_methods", "<i4"),
                          ("total_amount", "<f8"), ("fraud_amount", "<f8"), ("avg_amount", "<f8"),
-                         ("fraud_rate", "<f8"), ("amount_stddev", "<f8"), ("risk_score", "<f8")]
+                         ("fraud_rate", "<f8"), ("amount_stddev", "<f8"), ("risk_score", "<f8"),
+                         ("cents", "<i8"), ("fraud_cents", "<i8"), ("sq_lo", "<u8"), ("sq_hi", "<u8"),
+                         ("pm_mask", "<u8", (4,))]  # the exact moments fd_merchant_windows_merge combines
 FD_MAX_SEQ_LEN = 16
 FD_SLOT_LSTM = 64
 FD_SEQ_INPUT = 16
@@ -257,6 +259,11 @@ SIGNATURES = {
     "fd_features_seq_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp]),
     "fd_shard_of_host": (C.c_int, [_vp, _i64, _i32, _vp]),
     "fd_route_partition_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), _i64, _i32, _vp, _vp]),
+    "fd_route_partition_ex_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_window_inputs), _i64, _i32,
+                                               _vp, _vp]),
+    "fd_route_unpack_device": (C.c_int, [_vp, _vp, _vp, _i64, C.POINTER(fd_txn_batch), _vp, _vp, _vp]),
+    "fd_windows_observe": (C.c_int, [_vp, _i64]),
+    "fd_merchant_windows_merge": (C.c_int, [_vp, _i64, _vp, C.POINTER(_i64)]),
     "fd_score_records_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, _vp, _vp, _i64, _vp]),
     "fd_route_scatter_results_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "fd_windows_init": (C.c_int, [_vp, C.POINTER(fd_window_params)]),

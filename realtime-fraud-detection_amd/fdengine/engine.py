@@ -300,6 +300,11 @@ class FraudEngine:
         N.call("fd_windows_stats", self._h, C.byref(wm), C.byref(ue), C.byref(me))
         return {"watermark": wm.value, "user_events": ue.value, "merchant_events": me.value}
 
+    def windows_observe(self, max_event_ts: int) -> None:
+        """Sharded windows: the node-wide micro-batch's largest event time (all-reduce MAX), so every shard
+        advances one watermark (fd_windows_observe)."""
+        N.call("fd_windows_observe", self._h, int(max_event_ts))
+
     # ------------------------------------------------------------------ RedisTransactionSink aggregates
     def sink_init(self, capacity: int, user_capacity: int) -> None:
         """Hourly / daily / merchant-hour summaries of RedisTransactionSink.updateAggregations
@@ -391,6 +396,25 @@ class FraudEngine:
         b = N.fd_txn_batch(*[int(txn_ptrs[f]) for f in N.TXN_FIELDS])
         N.call("fd_route_partition_device", self._h, C.byref(b), int(n), int(n_shards),
                C.c_void_p(records_ptr) if records_ptr else None, C.c_void_p(counts_ptr))
+
+    def route_partition_ex_device(self, txn_ptrs: dict, extra_ptrs: Optional[dict], n: int, n_shards: int,
+                                  records_ptr: int, counts_ptr: int) -> None:
+        """route_partition_device with the owner's window / sink inputs riding in the records:
+        extra_ptrs = {"payment_method": u8*, "is_fraud": u8*} device pointers (missing: null / false)."""
+        b = N.fd_txn_batch(*[int(txn_ptrs[f]) for f in N.TXN_FIELDS])
+        wi = N.fd_window_inputs(*[int(extra_ptrs[f]) if extra_ptrs and extra_ptrs.get(f) else None
+                                  for f in ("payment_method", "is_fraud")], None)
+        N.call("fd_route_partition_ex_device", self._h, C.byref(b), C.byref(wi), int(n), int(n_shards),
+               C.c_void_p(records_ptr) if records_ptr else None, C.c_void_p(counts_ptr))
+
+    def route_unpack_device(self, records_ptr: int, results_ptr: int, n: int, out_ptrs: dict, pm_ptr: int = 0,
+                            fraud_ptr: int = 0, score_ptr: int = 0) -> None:
+        """Owner side: received records (+ their result records) back to device columns (out_ptrs: any of
+        TXN_FIELDS), payment method, isFraud and the fraud score (the result's fraud probability)."""
+        opt = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        b = N.fd_txn_batch(*[int(out_ptrs.get(f) or 0) or None for f in N.TXN_FIELDS])
+        N.call("fd_route_unpack_device", self._h, opt(records_ptr), opt(results_ptr), int(n), C.byref(b),
+               opt(pm_ptr), opt(fraud_ptr), opt(score_ptr))
 
     def score_records_device(self, params: N.fd_blend_params, slots: Sequence[int], records_ptr: int, n: int,
                              results_ptr: int, present: Optional[Sequence[int]] = None) -> None:
@@ -537,3 +561,16 @@ def device_count() -> int:
     c = C.c_int()
     rc = N.lib.fd_device_count(C.byref(c))
     return c.value if rc == N.FD_OK else 0
+
+
+def merge_merchant_windows(parts) -> np.ndarray:
+    """Combine merchant-window partials of several shards (N.MERCHANT_WINDOW_DTYPE arrays) into whole windows,
+    sorted by (window_start, merchant): exact moments summed, derived fields recomputed by the library's own
+    finalisation (fd_merchant_windows_merge, host only), so the result is bit-identical to an unsharded run."""
+    a = np.concatenate([np.asarray(p, N.MERCHANT_WINDOW_DTYPE) for p in parts]) if len(parts) else \
+        np.zeros(0, N.MERCHANT_WINDOW_DTYPE)
+    a = np.ascontiguousarray(a)
+    out = np.zeros(max(len(a), 1), N.MERCHANT_WINDOW_DTYPE)
+    m = C.c_int64()
+    N.call("fd_merchant_windows_merge", a.ctypes.data if len(a) else None, len(a), out.ctypes.data, C.byref(m))
+    return out[:m.value].copy()

@@ -21,6 +21,19 @@ the step is the fused hot path on the ingest batch itself (fd_score_batch_device
 
 The exchange logic is backend-agnostic: `EngineShardBackend` drives libfdengine.so (the product path);
 the CPU tests plug an oracle-backed backend into the same `ShardedScorer` to check the protocol.
+
+Keyed aggregates across shards (step(..., windows=True, sink=True)): the payment method and isFraud ride in
+the transaction records; after scoring, each owner runs the Flink window aggregates (WindowProcessor, a5) and
+the sink aggregates (RedisTransactionSink, f3) on the transactions it owns, with the ML fraud score as
+Transaction.fraudScore. Cards are owned, so user windows are complete on their owner. Merchant-keyed state
+spans shards: (1) ONE watermark — an all-reduce MAX of the ingest batches' largest event time, given to every
+shard before its window step (fd_windows_observe), so all shards fire the same windows at the same step;
+(2) each shard's fired merchant windows are exact-moment partials (counts, integer cents, cents^2, the
+payment-method set; distinct users add because a card lives on one shard), all-gathered and merged with the
+library's own finalisation (fd_merchant_windows_merge): bit-identical to an unsharded run. The sink's
+hourly / daily / merchant-hour aggregates stay as per-shard integer partials and are summed at query time
+(an all-reduce of counts and cents, `sink_query`). Nothing on the scoring path reads these aggregates
+(merchant features come from the replicated merchant table), so no "as of batch start" snapshot is needed.
 """
 from __future__ import annotations
 
@@ -33,6 +46,7 @@ from .engine import FraudEngine, shard_of  # noqa: F401  (shard_of re-exported f
 
 REC = N.FD_ROUTE_RECORD_BYTES
 RES = N.FD_RESULT_RECORD_BYTES
+INT64_MIN = -(1 << 63)
 
 
 class EngineShardBackend:
@@ -48,13 +62,55 @@ class EngineShardBackend:
         # stream torch (and so RCCL's all_to_all and .cpu()) uses on this device.
         eng.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def partition(self, txns: dict, n: int, G: int):
+    def partition(self, txns: dict, n: int, G: int, extras: Optional[dict] = None):
         t = self.torch
         rec = t.empty((n, REC), dtype=t.uint8, device=self.device)
         counts = t.empty(G, dtype=t.int64, device=self.device)
-        self.eng.route_partition_device({f: txns[f].data_ptr() for f in N.TXN_FIELDS}, n, G,
-                                        rec.data_ptr() if n else 0, counts.data_ptr())
+        ptrs = {f: txns[f].data_ptr() for f in N.TXN_FIELDS}
+        if extras:
+            self.eng.route_partition_ex_device(ptrs, {k: v.data_ptr() for k, v in extras.items()}, n, G,
+                                               rec.data_ptr() if n else 0, counts.data_ptr())
+        else:
+            self.eng.route_partition_device(ptrs, n, G, rec.data_ptr() if n else 0, counts.data_ptr())
         return rec, counts
+
+    # ---- owner-side keyed aggregates (windows a5, sink f3)
+    def unpack(self, rec, res, m: int) -> dict:
+        """received records (+ result records) -> device columns for the window / sink kernels"""
+        t = self.torch
+        cols = {"card_key": t.empty(m, dtype=t.uint64, device=self.device),
+                "ts_ms": t.empty(m, dtype=t.int64, device=self.device),
+                "amount_cents": t.empty(m, dtype=t.int64, device=self.device),
+                "merchant": t.empty(m, dtype=t.int32, device=self.device),
+                "payment_method": t.empty(m, dtype=t.uint8, device=self.device),
+                "is_fraud": t.empty(m, dtype=t.uint8, device=self.device),
+                "fraud_score": t.empty(m, dtype=t.float64, device=self.device)}
+        if m:
+            self.eng.route_unpack_device(rec.data_ptr(), res.data_ptr() if res is not None else 0, m,
+                                         {f: cols[f].data_ptr() for f in ("card_key", "ts_ms", "amount_cents",
+                                                                          "merchant")},
+                                         cols["payment_method"].data_ptr(), cols["is_fraud"].data_ptr(),
+                                         cols["fraud_score"].data_ptr())
+        return cols
+
+    @staticmethod
+    def _ins(cols):
+        return {k: cols[k].data_ptr() for k in ("payment_method", "is_fraud", "fraud_score") if k in cols}
+
+    def windows_observe(self, max_event_ts: int) -> None:
+        self.eng.windows_observe(max_event_ts)
+
+    def windows_step(self, cols: dict, m: int, flush: bool):
+        return self.eng.windows_step_device({f: cols[f].data_ptr() for f in cols if f in N.TXN_FIELDS}, m,
+                                            in_ptrs=self._ins(cols), flush=flush)
+
+    def sink_update(self, cols: dict, m: int) -> None:
+        if m:
+            self.eng.sink_update_device({f: cols[f].data_ptr() for f in cols if f in N.TXN_FIELDS}, m,
+                                        in_ptrs=self._ins(cols))
+
+    def sink_query(self, kind: int, buckets, merchants=None):
+        return self.eng.sink_query(kind, buckets, merchants)
 
     def score_records(self, rec, m: int):
         t = self.torch
@@ -107,23 +163,56 @@ class ShardedScorer:
     def __init__(self, backend, rank: int, world: int, group=None):
         self.be, self.rank, self.world, self.group = backend, int(rank), int(world), group
         self.last_counts = None  # (send, recv) split sizes of the last step, for diagnostics
+        self.last_windows = None  # (user windows, merged merchant windows) fired by the last windows step
+
+    def _staged(self) -> bool:
+        """gloo moves host memory only: device tensors are staged through the host (several ranks sharing one
+        GPU in tests; RCCL — the product path — exchanges device memory directly)."""
+        import torch.distributed as dist
+        return dist.get_backend(self.group) == "gloo"
 
     def _a2a(self, out, inp, out_splits=None, in_splits=None):
         import torch.distributed as dist
+        if self._staged() and (out.is_cuda or inp.is_cuda):
+            o = out.cpu()
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+            out.copy_(o)
+            return
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def step(self, txns: dict, n: int):
+    def _allreduce_max(self, t):
+        import torch.distributed as dist
+        g = t.cpu() if self._staged() else t.clone()
+        dist.all_reduce(g, op=dist.ReduceOp.MAX, group=self.group)
+        return int(g.cpu()[0])
+
+    def step(self, txns: dict, n: int, extras: Optional[dict] = None, windows: bool = False, sink: bool = False,
+             flush: bool = False):
         """txns: field -> tensor (n rows) on the backend's device, in arrival order.
-        -> (fraud_prob f64, confidence f64, decision u8, risk u8) tensors in the same order."""
+        -> (fraud_prob f64, confidence f64, decision u8, risk u8) tensors in the same order.
+        extras: {"payment_method": u8, "is_fraud": u8} tensors (n rows) for the keyed aggregates.
+        windows / sink: after scoring, run the Flink window aggregates / the sink aggregates on the owned
+        transactions (module docstring); the fired windows are left in self.last_windows =
+        (this shard's user windows, the node's merged merchant windows); flush: end of input."""
         import torch
         G = self.world
+        aux = windows or sink
         if G == 1:  # one shard owns every card: no partition, no exchange
             self.last_counts = ([n], [n])
             if hasattr(self.be, "score_batch"):
-                return self.be.score_batch(txns, n)
-            rec, _ = self.be.partition(txns, n, 1)
-            return self.be.scatter_results(self.be.score_records(rec, n), n)
-        rec, counts = self.be.partition(txns, n, G)
+                out = self.be.score_batch(txns, n)
+                if aux:
+                    cols = {f: txns[f] for f in ("card_key", "ts_ms", "amount_cents", "merchant")}
+                    cols.update(extras or {})
+                    cols["fraud_score"] = out[0]
+                    self._aggregates(cols, n, None, windows, sink, flush)
+                return out
+            rec, _ = self.be.partition(txns, n, 1, extras) if aux else self.be.partition(txns, n, 1)
+            res = self.be.score_records(rec, n)
+            if aux:
+                self._aggregates(self.be.unpack(rec, res, n), n, None, windows, sink, flush)
+            return self.be.scatter_results(res, n)
+        rec, counts = self.be.partition(txns, n, G, extras) if aux else self.be.partition(txns, n, G)
         recv_counts = torch.empty_like(counts)
         self._a2a(recv_counts, counts)
         both = torch.cat([counts, recv_counts]).cpu().tolist()
@@ -135,7 +224,54 @@ class ShardedScorer:
         res = self.be.score_records(inbox, m)
         back = torch.empty((n, RES), dtype=torch.uint8, device=rec.device)
         self._a2a(back, res, send, recv)
+        if aux:
+            tmax = txns["ts_ms"].max().reshape(1) if n else torch.full((1,), INT64_MIN, dtype=torch.int64,
+                                                                        device=rec.device)
+            self._aggregates(self.be.unpack(inbox, res, m), m, tmax, windows, sink, flush)
         return self.be.scatter_results(back, n, sentinel=True)
+
+    def _aggregates(self, cols: dict, m: int, tmax, windows: bool, sink: bool, flush: bool):
+        import torch.distributed as dist
+        if windows:
+            if tmax is not None:  # one watermark for the node: the largest event time of all ingest batches
+                gmax = self._allreduce_max(tmax)
+                if gmax != INT64_MIN:
+                    self.be.windows_observe(gmax)
+            uw, mw = self.be.windows_step(cols, m, flush)
+            if self.world > 1:
+                parts = [None] * self.world
+                dist.all_gather_object(parts, mw, group=self.group)
+            else:
+                parts = [mw]
+            from .engine import merge_merchant_windows
+            self.last_windows = (uw, merge_merchant_windows(parts))
+        if sink:
+            self.be.sink_update(cols, m)
+
+    def sink_query(self, kind: int, buckets, merchants=None) -> np.ndarray:
+        """RedisService.getAggregation over the whole node: this shard's integer partials summed over all
+        shards (counts, distinct users — a card lives on one shard — and exact cents), then the reference's
+        derived fields with the device's own operations (rate = fraud / count, avg = (cents / 100) / count)."""
+        import torch
+        import torch.distributed as dist
+        a = self.be.sink_query(kind, buckets, merchants)
+        if self.world == 1:
+            return a
+        cents = np.rint(a["total_amount"] * 100.0).astype(np.int64)  # exact: |cents| < 2^50
+        ints = np.stack([a["total_count"], a["fraud_count"], a["high_risk_count"], a["unique_user_count"], cents,
+                         a["found"].astype(np.int64)])
+        t = torch.from_numpy(np.ascontiguousarray(ints))
+        if not self._staged():
+            t = t.to(self.be.device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        tot = t.cpu().numpy()
+        out = np.zeros(len(a), N.AGGREGATE_DTYPE)
+        for i in range(len(a)):
+            cnt, fr, hi, uu, c, found = (int(v) for v in tot[:, i])
+            if found:
+                total = c / 100
+                out[i] = (cnt, fr, hi, uu, total, fr / cnt, total / cnt, 1, 0)
+        return out
 
     # ------------------------------------------------------------------ checkpoint / rescale
     # Counterpart of Flink's externalized keyed-state checkpoints (fl/FraudDetectionJob.java:112-136):
