@@ -19,7 +19,8 @@ The IsolationForest is a real sklearn 1.7.2 model trained with the reference tra
 
 Outputs:
   feature_processor_cases.json  raw request dicts -> processed numeric key order + 64-wide vector
-  ensemble_cases.json           raw request + stand-in probabilities -> reference predict() outputs
+  ensemble_cases.json           raw request + stand-in probabilities -> reference predict() outputs, incl. the
+                                processed request, the explanation dict and the prediction-cache key (a14)
   iforest_golden.npz            IF flattened arrays, inputs, sklearn apply/decision_function and the
                                 reference _predict_sklearn probabilities
 """
@@ -229,7 +230,12 @@ def main():
                 "expected": {k: jsonable(out[k]) for k in ("fraud_probability", "confidence", "decision",
                                                             "risk_level")},
                 "model_predictions": {k: float(v) for k, v in out["model_predictions"].items()},
+                "model_confidences": {k: float(v) for k, v in out["model_confidences"].items()},
                 "model_weights": {k: float(v) for k, v in ep.model_weights.items()},
+                # a14: the explanation and the prediction-cache key the reference derives from this request
+                "processed": processed,
+                "explanation": out["explanation"],
+                "cache_key": ep._generate_cache_key(processed),
             })
     (HERE / "ensemble_cases.json").write_text(json.dumps(ens_cases, default=jsonable))
     print(f"wrote {len(fp_cases)} feature cases, {len(ens_cases)} ensemble cases, IF golden {Xif.shape}")
