@@ -19,12 +19,14 @@ velocity/feature semantics are parity-unpinned (no JDK, no tests in the referenc
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 import numpy as np
 
 ORACLE_DIR = Path(__file__).resolve().parent
-LIB_PATH = ORACLE_DIR / "build" / "liboracle.so"
+# FD_ORACLE_LIB: another build of the same sources (the sanitizer build of tests/test_oracle_sanitizers.py)
+LIB_PATH = Path(os.environ.get("FD_ORACLE_LIB") or ORACLE_DIR / "build" / "liboracle.so")
 
 _lib = None
 
