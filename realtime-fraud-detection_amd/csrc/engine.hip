@@ -243,7 +243,7 @@ int fd_engine_destroy(fd_engine* eng) {
     }
   }
   for (auto* b : {&e.state.headers, &e.state.ring, &e.state.merchants, &e.state.slot, &e.state.err,
-                  &e.state.bucket_cnt, &e.state.bucket_fill, &e.state.bucket_base, &e.state.pairs, &e.state.prep})
+                  &e.state.bucket_fill, &e.state.pairs, &e.state.ovf_cnt, &e.state.ovf_key, &e.state.ovf_b, &e.state.prep})
     b->release();
   for (auto& ev : e.events) {
     (void)hipEventDestroy(ev.a);

@@ -188,7 +188,10 @@ struct CardStore {
   int S = 0;         // LSTM history events per card (0 = off)
   int64_t n_merchants = 0;
   DeviceBuffer headers, ring, merchants, slot, err, seq;
-  DeviceBuffer bucket_cnt, bucket_fill, bucket_base, pairs, prep;  // per-batch card grouping (feat_slot/scatter/bucket)
+  // per-batch card grouping (feat_slot -> feat_bucket): keys per bucket, [NB][C] bucket regions, overflow
+  // counters by batch parity + the overflow list (key, bucket), prep records
+  DeviceBuffer bucket_fill, pairs, ovf_cnt, ovf_key, ovf_b, prep;
+  int batch_parity = 0;
   DeviceBuffer uext, mext, vocab;  // extended profiles + vocabulary flags (feature map, rule scores)
   int64_t n_mext = 0;
   bool vocab_loaded = false;

@@ -11,17 +11,18 @@
 //
 // Micro-batch semantics = the reference's per-element semantics: transactions of one card are
 // processed in arrival order, each reading the card's velocity before writing it. The batch is
-// sorted and segmented by card (three launches, no per-batch table reset):
-//   feat_slot    : per txn, find-or-insert the card slot (open addressing, atomicCAS on the key) and
-//                  count it into its bucket (slot mod NB; NB ~ n / 256 buckets, LDS histogram per block);
-//   feat_scatter : per txn, its (slot << 32 | arrival index) key into its bucket's range (bases by a
-//                  block-redundant scan of the NB counts);
-//   feat_bucket  : one workgroup per bucket: bitonic sort of the bucket's keys in LDS -> segments = cards
-//                  in arrival order. Segments of <= kSegLong transactions: one thread walks the card with
-//                  its 128-B header in registers; longer ones (hot cards, card-testing bursts): the whole
-//                  workgroup, 256 transactions per tile, each thread computing its transaction's windows
-//                  from an LDS tile of the card's previous K events (positional form of the sequential
-//                  definition) and the redis_compat session by a workgroup scan.
+// sorted and segmented by card (two launches, no per-batch table reset):
+//   feat_slot    : per txn, find-or-insert the card slot (open addressing, atomicCAS on the key), write its
+//                  48-B prep record (fields + the merchant row already joined) and append its
+//                  (slot << 32 | arrival index) key to its bucket's fixed-capacity region (bucket = slot mod
+//                  NB, NB ~ n / 128; per block an LDS histogram and one global atomic per bucket; a bucket
+//                  past its capacity spills to an overflow list its bucket kernel scans);
+//   feat_bucket  : one workgroup per bucket: the bucket's keys sorted in LDS (rank counting up to 512 keys,
+//                  bitonic beyond) -> segments = cards in arrival order. Segments of <= kSegLong transactions:
+//                  one thread walks the card with its 128-B header in registers; longer ones (hot cards,
+//                  card-testing bursts): the whole workgroup, 256 transactions per tile, each thread computing
+//                  its transaction's windows from an LDS tile of the card's previous K events (positional
+//                  form of the sequential definition) and the redis_compat session by a workgroup scan.
 // Sliding windows are incremental: per window the header keeps how many of the ring's newest events are
 // inside it, their cents sum and the oldest one's time, so a transaction reads ring events only to evict
 // them (canonical state: the windows as of the card's last event). A ring that is not time-sorted (an
@@ -39,7 +40,6 @@ namespace {
 constexpr long long kWin[3] = {300000LL, 3600000LL, 86400000LL};  // 5 min / 1 h / 24 h
 constexpr long long kSessionTtl = 3600000LL;                      // RedisService TTL 3600 s (ms)
 constexpr int kBT = 256;          // threads of the bucket kernel (and its scans)
-constexpr int kGT = 1024;         // threads of the scatter kernel (one global atomic per bucket per block)
 constexpr int kST = 256;          // threads of the slot kernel (latency-bound probes: spread over every CU)
 constexpr int kSegLong = 16;      // segments longer than this take the cooperative path
 constexpr int kChunkCap = 4096;   // (slot, txn) keys sorted per pass in LDS
@@ -155,21 +155,37 @@ struct TxnSrc {
   }
 };
 
+// Python max(x, lo) / min(x, hi) (feature_processor.py:231-234): NaN propagates like the reference
+__device__ __forceinline__ double pmax(double x, double lo) { return (lo > x) ? lo : x; }
+__device__ __forceinline__ double pmin(double x, double hi) { return (hi < x) ? hi : x; }
+__device__ __forceinline__ float clip10(double x) {
+  if (x < -10.0) x = -10.0;
+  if (x > 10.0) x = 10.0;
+  return (float)x;
+}
+
 // One transaction as the bucket kernel reads it, written by the slot kernel in arrival order: the fields the
-// card-independent features need with the merchant row already looked up, so the bucket kernel's random
-// read of transaction i is ONE 48-B record (three 16-B loads in flight with the card header) whatever the
-// source layout (eight SoA columns or a route record) and no merchant-table round trip follows it.
+// card-independent features need with the merchant row already looked up and the card-independent
+// arithmetic done (log, log1p, sqrt, calendar fields), so the bucket kernel's random read of transaction i is
+// ONE 64-B record (four 16-B loads in flight with the card header) whatever the source layout (eight SoA
+// columns or a route record), no merchant-table round trip follows it and its dependent chain is shorter.
 struct __attribute__((aligned(16))) Prep {
   long long ts, cents;
   unsigned long long dfp;
   double mfr;   // merchant fraud rate as the feature reads it (unknown merchant 0.1, null rate 0.05)
   double mult;  // merchant risk multiplier (unknown merchant 2.0)
+  double r1;    // raw feature 1: log(amount + 1) (Java Math.log; the card-independent transcendental)
+  float o1;     // vector slot 1: clip10(log1p(amount)) (FeatureProcessor amount_log)
+  float dv0;    // derived amount_sqrt: clip10(sqrt(amount)) (used when amount > 0)
   int merchant;
-  unsigned char ipc, hour, wk, pad;
+  unsigned char ipc, hour, dow, weekend;  // hour / day of week / weekend as the features read them
 };
-static_assert(sizeof(Prep) == 48, "Prep must be 48 B");
+static_assert(sizeof(Prep) == 64, "Prep must be 64 B");
 
+// The card-independent part of a transaction's features, computed here where it hides under the slot
+// probe's latency (base_raw / write_vector read the results; same operations, so the same bits).
 __device__ __forceinline__ Prep make_prep(const Txn& t, const Merchant* __restrict__ merchants, int nm) {
+#pragma clang fp contract(off)
   Prep p;
   p.ts = t.ts;
   p.cents = t.cents;
@@ -182,11 +198,26 @@ __device__ __forceinline__ Prep make_prep(const Txn& t, const Merchant* __restri
     p.mfr = 0.1;
     p.mult = 2.0;
   }
+  const double r0 = (double)t.cents / 100.0;
+  p.r1 = (r0 + 1 > 0) ? log(r0 + 1) : ((r0 + 1 == 0) ? -INFINITY : NAN);
+  const double amount = pmax(r0, 0.0);  // write_vector's amount
+  double alog = p.r1;
+  if (isnan(alog) || isinf(alog)) alog = 0.0;
+  if (amount > 0) alog = log1p(amount);
+  p.o1 = clip10(alog);
+  p.dv0 = clip10(sqrt(amount));
+  long long days = t.ts / 86400000LL;  // event time -> hour / ISO day of week (1 = Monday) in UTC
+  if (t.ts % 86400000LL < 0) days -= 1;
+  int hour = (int)((t.ts - days * 86400000LL) / 3600000LL);
+  long long dw = (days + 3) % 7;
+  if (dw < 0) dw += 7;
+  const int dow = (int)dw + 1;
+  if (t.hour != 255) hour = t.hour;
+  p.hour = (unsigned char)hour;
+  p.dow = (unsigned char)dow;
+  p.weekend = ((t.wk == 255) ? (dow >= 6) : (t.wk != 0)) ? 1 : 0;
   p.merchant = t.merchant;
   p.ipc = t.ipc;
-  p.hour = t.hour;
-  p.wk = t.wk;
-  p.pad = 0;
   return p;
 }
 
@@ -194,40 +225,57 @@ __device__ __forceinline__ void store_prep(Prep* dst, const Prep& p) {
   uint4* q = reinterpret_cast<uint4*>(dst);
   const unsigned long long a = (unsigned long long)p.ts, b = (unsigned long long)p.cents;
   const unsigned long long c = __double_as_longlong(p.mfr), d = __double_as_longlong(p.mult);
+  const unsigned long long e = __double_as_longlong(p.r1);
   q[0] = make_uint4((unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32));
   q[1] = make_uint4((unsigned)p.dfp, (unsigned)(p.dfp >> 32), (unsigned)c, (unsigned)(c >> 32));
-  q[2] = make_uint4((unsigned)d, (unsigned)(d >> 32), (unsigned)p.merchant,
-                    (unsigned)p.ipc | ((unsigned)p.hour << 8) | ((unsigned)p.wk << 16));
+  q[2] = make_uint4((unsigned)d, (unsigned)(d >> 32), (unsigned)e, (unsigned)(e >> 32));
+  q[3] = make_uint4(__float_as_uint(p.o1), __float_as_uint(p.dv0), (unsigned)p.merchant,
+                    (unsigned)p.ipc | ((unsigned)p.hour << 8) | ((unsigned)p.dow << 16) | ((unsigned)p.weekend << 24));
 }
 
 __device__ __forceinline__ Prep load_prep(const Prep* __restrict__ src) {
   const uint4* q = reinterpret_cast<const uint4*>(src);
-  const uint4 w0 = q[0], w1 = q[1], w2 = q[2];
+  const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
   Prep p;
   p.ts = (long long)(((unsigned long long)w0.y << 32) | w0.x);
   p.cents = (long long)(((unsigned long long)w0.w << 32) | w0.z);
   p.dfp = ((unsigned long long)w1.y << 32) | w1.x;
   p.mfr = __longlong_as_double((long long)(((unsigned long long)w1.w << 32) | w1.z));
   p.mult = __longlong_as_double((long long)(((unsigned long long)w2.y << 32) | w2.x));
-  p.merchant = (int)w2.z;
-  p.ipc = (unsigned char)(w2.w & 0xffu);
-  p.hour = (unsigned char)((w2.w >> 8) & 0xffu);
-  p.wk = (unsigned char)((w2.w >> 16) & 0xffu);
-  p.pad = 0;
+  p.r1 = __longlong_as_double((long long)(((unsigned long long)w2.w << 32) | w2.z));
+  p.o1 = __uint_as_float(w3.x);
+  p.dv0 = __uint_as_float(w3.y);
+  p.merchant = (int)w3.z;
+  p.ipc = (unsigned char)(w3.w & 0xffu);
+  p.hour = (unsigned char)((w3.w >> 8) & 0xffu);
+  p.dow = (unsigned char)((w3.w >> 16) & 0xffu);
+  p.weekend = (unsigned char)((w3.w >> 24) & 0xffu);
   return p;
 }
 
 // ------------------------------------------------------------------------------------------------
 // per-batch card grouping
+// Per transaction: card slot (find-or-insert), prep record, and its (slot, arrival index) key appended to its
+// bucket's fixed-capacity region (bucket = slot & nbm): per block an LDS histogram, one global atomic per
+// (block, bucket) reserving the block's run, then each key at its rank in the run. A bucket that outgrows its
+// capacity C spills the rest to an overflow list (bucket id + key) its bucket kernel scans. No count / scan /
+// scatter passes: the bucket kernel's inputs are complete when this kernel ends.
 __global__ void __launch_bounds__(kST) feat_slot_kernel(CardHeader* H, long long mask, int64_t n, TxnSrc src,
                                                         const Merchant* __restrict__ merchants, int nm,
-                                                        unsigned nbm, unsigned* __restrict__ slot,
-                                                        Prep* __restrict__ prep, unsigned* __restrict__ bucket_cnt,
-                                                        unsigned* err) {
-  extern __shared__ unsigned hist[];  // nbm + 1 counters
+                                                        unsigned nbm, unsigned C, unsigned* __restrict__ slot,
+                                                        Prep* __restrict__ prep, unsigned* __restrict__ fill,
+                                                        unsigned long long* __restrict__ pairs,
+                                                        unsigned* __restrict__ ovf_cnt,
+                                                        unsigned long long* __restrict__ ovf_key,
+                                                        unsigned* __restrict__ ovf_b, unsigned* err) {
+  extern __shared__ unsigned hist[];  // [nbm + 1] block counts | [nbm + 1] reserved run starts
+  unsigned* run = hist + nbm + 1;
   for (unsigned b = threadIdx.x; b <= nbm; b += kST) hist[b] = 0u;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kST + threadIdx.x;
+  unsigned local = 0, b = 0;
+  unsigned long long key = 0;
+  bool have = false;
   if (i < n) {
     const Txn t = src.get(i);  // in flight with the probe
     const long long s = find_or_insert(H, mask, src.get_key(i));
@@ -237,86 +285,37 @@ __global__ void __launch_bounds__(kST) feat_slot_kernel(CardHeader* H, long long
       slot[i] = 0xffffffffu;
     } else {
       slot[i] = (unsigned)s;
-      atomicAdd(&hist[(unsigned)s & nbm], 1u);
+      b = (unsigned)s & nbm;
+      key = ((unsigned long long)s << 32) | (unsigned long long)i;
+      local = atomicAdd(&hist[b], 1u);
+      have = true;
     }
   }
   __syncthreads();
-  for (unsigned b = threadIdx.x; b <= nbm; b += kST)
-    if (hist[b]) atomicAdd(&bucket_cnt[b], hist[b]);
-}
-
-// exclusive scan of NB counters into LDS base[] (NB <= kMaxBuckets; every block computes it)
-__device__ void block_bucket_scan(const unsigned* __restrict__ cnt, unsigned nb, unsigned* base, unsigned* part) {
-  const unsigned per = (nb + kGT - 1) / kGT, a = threadIdx.x * per;
-  unsigned s = 0;
-  for (unsigned q = 0; q < per; ++q)
-    if (a + q < nb) s += cnt[a + q];
-  part[threadIdx.x] = s;
+  for (unsigned q = threadIdx.x; q <= nbm; q += kST)
+    if (hist[q]) run[q] = atomicAdd(&fill[q], hist[q]);
   __syncthreads();
-  for (int d = 1; d < kGT; d <<= 1) {
-    const unsigned v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0u;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  unsigned run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
-  for (unsigned q = 0; q < per; ++q)
-    if (a + q < nb) {
-      base[a + q] = run;
-      run += cnt[a + q];
+  if (have) {
+    const unsigned pos = run[b] + local;
+    if (pos < C) {
+      pairs[(size_t)b * C + pos] = key;
+    } else {
+      const unsigned j = atomicAdd(ovf_cnt, 1u);
+      ovf_key[j] = key;
+      ovf_b[j] = b;
     }
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(kGT) feat_scatter_kernel(int64_t n, const unsigned* __restrict__ slot, unsigned nbm,
-                                                           const unsigned* __restrict__ bucket_cnt,
-                                                           unsigned* __restrict__ bucket_fill,
-                                                           unsigned* __restrict__ bucket_base,
-                                                           unsigned long long* __restrict__ pairs) {
-  extern __shared__ unsigned sh[];  // base[NB] | lcnt[NB] | lbase[NB]
-  __shared__ unsigned part[kGT];
-  const unsigned nb = nbm + 1;
-  unsigned* base = sh;
-  unsigned* lcnt = sh + nb;
-  unsigned* lbase = sh + 2 * nb;
-  for (unsigned b = threadIdx.x; b < nb; b += kGT) lcnt[b] = 0u;
-  block_bucket_scan(bucket_cnt, nb, base, part);
-  if (blockIdx.x == 0)
-    for (unsigned b = threadIdx.x; b < nb; b += kGT) bucket_base[b] = base[b];
-  const int64_t i = (int64_t)blockIdx.x * kGT + threadIdx.x;
-  const unsigned s = i < n ? slot[i] : 0xffffffffu;
-  unsigned local = 0, b = 0;
-  if (s != 0xffffffffu) {
-    b = s & nbm;
-    local = atomicAdd(&lcnt[b], 1u);
   }
-  __syncthreads();
-  for (unsigned q = threadIdx.x; q < nb; q += kGT)
-    if (lcnt[q]) lbase[q] = atomicAdd(&bucket_fill[q], lcnt[q]);
-  __syncthreads();
-  if (s != 0xffffffffu) pairs[base[b] + lbase[b] + local] = ((unsigned long long)s << 32) | (unsigned long long)i;
 }
 
 // ------------------------------------------------------------------------------------------------
 // per-transaction feature arithmetic (shared by the sequential and the cooperative path)
 
-// Python max(x, lo) / min(x, hi) (feature_processor.py:231-234): NaN propagates like the reference
-__device__ __forceinline__ double pmax(double x, double lo) { return (lo > x) ? lo : x; }
-__device__ __forceinline__ double pmin(double x, double hi) { return (hi < x) ? hi : x; }
-__device__ __forceinline__ float clip10(double x) {
-  if (x < -10.0) x = -10.0;
-  if (x > 10.0) x = 10.0;
-  return (float)x;
-}
-
 // bridged raw features -> scoring vector: FeatureProcessor.process_features (41 definitions, derived
 // features appended when present) + _prepare_features (pad to 64, clip +-10), then the f32 cast the
 // models apply. Mirrors oracle/oracle_features.c orc_vector_from_raw.
-__device__ void write_vector(const double* r, float* __restrict__ out) {
+__device__ void write_vector(const double* r, float o1, float dv0, float* __restrict__ out) {
 #pragma clang fp contract(off)
   const double amount = pmax(r[0], 0.0);
-  double alog = r[1];
-  if (isnan(alog) || isinf(alog)) alog = 0.0;
   const double hour = pmin(pmax(r[2], 0.0), 23.0);
   const double dow = pmin(pmax(r[3], 0.0), 6.0);
   double mfr = pmin(pmax(r[5], 0.0), 1.0);
@@ -328,14 +327,13 @@ __device__ void write_vector(const double* r, float* __restrict__ out) {
   double mrisk = pmin(pmax(r[14], 0.0), 1.0);
   if (isnan(mrisk)) mrisk = 0.5;
   const double age = pmax(r[15], 0.0);
-  if (amount > 0) alog = log1p(amount);
   // the 41 definitions in declaration order (feature_processor.py:66-147); built in registers
   // (compile-time indices only) and stored as 16 x 16 B
   float o[FD_VECTOR_WIDTH];
 #pragma unroll
   for (int k = 0; k < FD_VECTOR_WIDTH; ++k) o[k] = 0.f;
   o[0] = clip10(amount);
-  o[1] = clip10(alog);
+  o[1] = o1;  // clip10(log1p(amount)), or the sanitised log(amount + 1) when amount <= 0 (make_prep)
   o[5] = clip10(hour);
   o[6] = clip10(dow);
   o[7] = r[4] > 0.5 ? 1.f : 0.f;
@@ -358,7 +356,7 @@ __device__ void write_vector(const double* r, float* __restrict__ out) {
   // derived, appended in order when present (feature_processor.py:330-363); merchant_avg_amount is 0 on
   // this path, so there is no amount_to_merchant_avg_ratio
   const bool pres[6] = {amount > 0, uavg > 0, c24 > 0, true, true, true};
-  const float dv[6] = {clip10(sqrt(amount)), clip10(amount / uavg), clip10(c1 / (c24 / 24)), clip10((0.5 + ip) / 2),
+  const float dv[6] = {dv0, clip10(amount / uavg), clip10(c1 / (c24 / 24)), clip10((0.5 + ip) / 2),
                        (9 <= hour && hour <= 17) ? 1.f : 0.f, (hour < 6 || hour > 22) ? 1.f : 0.f};
   int k = 0;
 #pragma unroll
@@ -394,27 +392,17 @@ struct Profile {
 // raw features 0-8, 14, 15 of one transaction (FeatureExtractor.java:92-325 for the bridged names)
 __device__ __forceinline__ void base_raw(const Prep& t, const Profile& p, double* r) {
 #pragma clang fp contract(off)
-  const double amount = (double)t.cents / 100.0;
-  long long days = t.ts / 86400000LL;
-  if (t.ts % 86400000LL < 0) days -= 1;
-  int hour = (int)((t.ts - days * 86400000LL) / 3600000LL);
-  long long dw = (days + 3) % 7;
-  if (dw < 0) dw += 7;
-  const int dow = (int)dw + 1;
-  if (t.hour != 255) hour = t.hour;
-  const int weekend = (t.wk == 255) ? (dow >= 6) : (t.wk != 0);
-  const double mfr = t.mfr, mult = t.mult;  // merchant row looked up by the slot kernel (make_prep)
   const bool known = p.has_user && t.dfp != 0ull && (t.dfp == p.fp[0] || t.dfp == p.fp[1] || t.dfp == p.fp[2]);
-  r[0] = amount;
-  r[1] = (amount + 1 > 0) ? log(amount + 1) : ((amount + 1 == 0) ? -INFINITY : NAN);
-  r[2] = hour;
-  r[3] = dow;
-  r[4] = weekend ? 1.0 : 0.0;
-  r[5] = mfr;
+  r[0] = (double)t.cents / 100.0;
+  r[1] = t.r1;  // card-independent fields: make_prep (slot kernel)
+  r[2] = t.hour;
+  r[3] = t.dow;
+  r[4] = t.weekend ? 1.0 : 0.0;
+  r[5] = t.mfr;
   r[6] = known ? 0.0 : 1.0;
   r[7] = t.ipc == 0 ? NAN : (t.ipc == 1 ? 0.1 : 0.3);
   r[8] = p.has_user ? (isnan(p.avg) ? 0.0 : p.avg) : NAN;
-  r[14] = mult;
+  r[14] = t.mult;
   r[15] = p.has_user ? (double)p.age : 0.0;
 }
 
@@ -435,13 +423,13 @@ struct Outputs {
   int S;
 };
 
-__device__ __forceinline__ void emit(const Outputs& o, int64_t i, const double* r, long long s5) {
+__device__ __forceinline__ void emit(const Outputs& o, int64_t i, const double* r, long long s5, float o1, float dv0) {
   if (o.raw) {
     double2* ro = reinterpret_cast<double2*>(o.raw + (size_t)i * FD_RAW_FEATURES);
 #pragma unroll
     for (int c = 0; c < FD_RAW_FEATURES / 2; ++c) ro[c] = make_double2(r[2 * c], r[2 * c + 1]);
   }
-  write_vector(r, o.vec + (size_t)i * FD_VECTOR_WIDTH);
+  write_vector(r, o1, dv0, o.vec + (size_t)i * FD_VECTOR_WIDTH);
   if (o.vel5) o.vel5[i] = (double)s5 / 100.0;
 }
 
@@ -656,10 +644,13 @@ struct BucketArgs {
   int64_t n;
   const Prep* prep;  // [n] in arrival order (feat_slot_kernel)
   Outputs out;
-  unsigned* bucket_cnt;
-  unsigned* bucket_fill;
-  const unsigned* bucket_base;
-  const unsigned long long* pairs;
+  unsigned* fill;                     // keys per bucket (this batch); reset here for the next batch
+  const unsigned long long* pairs;    // [NB][C] bucket regions
+  unsigned C;
+  unsigned* ovf_cnt;                  // [2] overflow counts by batch parity
+  int par;
+  const unsigned long long* ovf_key;  // overflow list: key, bucket
+  const unsigned* ovf_b;
 };
 
 template <int MODE>
@@ -678,7 +669,7 @@ __device__ void process_short(const BucketArgs& a, unsigned s, const unsigned lo
     long long cw[3], sw[3];
     velocity_step<MODE>(c, rg, a.K, t.ts, t.cents, cw, sw);
     velocity_raw(cw, sw, r);
-    emit(a.out, i, r, sw[0]);
+    emit(a.out, i, r, sw[0], t.o1, t.dv0);
     if (a.out.S) seq_step(a.out, s, c.flags, i, r);
   }
   store_card(h, c);
@@ -813,7 +804,7 @@ __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned lon
     if (act) {
       base_raw(t, p, r);
       velocity_raw(cw, sw, r);
-      emit(a.out, i, r, sw[0]);
+      emit(a.out, i, r, sw[0], t.o1, t.dv0);
       if (S)
         for (int c = 0; c < kSeqInput; ++c) sm.seqb[(S + j) * kSeqInput + c] = seq_input(r[c]);
     }
@@ -1047,10 +1038,18 @@ __global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
   unsigned* bins = reinterpret_cast<unsigned*>(skeys + kChunkCap);
   const int b = blockIdx.x;
   FD_FSTAMP(0);
-  const unsigned m = a.bucket_cnt[b];
-  const unsigned long long* src = a.pairs + a.bucket_base[b];
+  const unsigned m = a.fill[b];  // region (min(m, C)) + overflow entries (m - C) of this bucket
+  const unsigned long long* src = a.pairs + (size_t)b * a.C;
+  const unsigned in_region = m < a.C ? m : a.C;
+  const unsigned n_ovf = m > a.C ? a.ovf_cnt[a.par] : 0u;  // the whole list is scanned for this bucket's entries
   if (m <= (unsigned)kChunkCap) {
-    for (unsigned q = threadIdx.x; q < m; q += kBT) skeys[q] = src[q];
+    for (unsigned q = threadIdx.x; q < in_region; q += kBT) skeys[q] = src[q];
+    if (n_ovf) {
+      if (threadIdx.x == 0) chunk_m = (int)in_region;
+      __syncthreads();
+      for (unsigned q = threadIdx.x; q < n_ovf; q += kBT)
+        if (a.ovf_b[q] == (unsigned)b) skeys[atomicAdd(&chunk_m, 1)] = a.ovf_key[q];
+    }
     __syncthreads();
     process_sorted<MODE>(a, skeys, (int)m, sm, long_list, &n_long);
   } else {
@@ -1060,7 +1059,10 @@ __global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
     const long long binw = (a.n + kMaxBins - 1) / kMaxBins;  // <= kChunkCap for n <= 16M (launch check)
     for (int q = threadIdx.x; q < kMaxBins; q += kBT) bins[q] = 0u;
     __syncthreads();
-    for (unsigned q = threadIdx.x; q < m; q += kBT) atomicAdd(&bins[(unsigned)(src[q] & 0xffffffffull) / binw], 1u);
+    for (unsigned q = threadIdx.x; q < in_region; q += kBT)
+      atomicAdd(&bins[(unsigned)(src[q] & 0xffffffffull) / binw], 1u);
+    for (unsigned q = threadIdx.x; q < n_ovf; q += kBT)
+      if (a.ovf_b[q] == (unsigned)b) atomicAdd(&bins[(unsigned)(a.ovf_key[q] & 0xffffffffull) / binw], 1u);
     __syncthreads();
     {  // exclusive prefix over the bins, in place; bins[kMaxBins] = m
       constexpr int per = kMaxBins / kBT;
@@ -1077,10 +1079,10 @@ __global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
         sm.rst[threadIdx.x] += x;
         __syncthreads();
       }
-      unsigned run = threadIdx.x ? (unsigned)sm.rst[threadIdx.x - 1] : 0u;
+      unsigned acc = threadIdx.x ? (unsigned)sm.rst[threadIdx.x - 1] : 0u;
       for (int q = 0; q < per; ++q) {
-        bins[threadIdx.x * per + q] = run;
-        run += v[q];
+        bins[threadIdx.x * per + q] = acc;
+        acc += v[q];
       }
       if (threadIdx.x == 0) bins[kMaxBins] = m;
       __syncthreads();
@@ -1097,8 +1099,14 @@ __global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
       const unsigned i_lo = (unsigned)(lo * binw), i_hi = (unsigned)min((long long)hi * binw, a.n);
       if (threadIdx.x == 0) chunk_m = 0;
       __syncthreads();
-      for (unsigned q = threadIdx.x; q < m; q += kBT) {
+      for (unsigned q = threadIdx.x; q < in_region; q += kBT) {
         const unsigned long long k = src[q];
+        const unsigned i = (unsigned)(k & 0xffffffffull);
+        if (i >= i_lo && i < i_hi) skeys[atomicAdd(&chunk_m, 1)] = k;
+      }
+      for (unsigned q = threadIdx.x; q < n_ovf; q += kBT) {
+        if (a.ovf_b[q] != (unsigned)b) continue;
+        const unsigned long long k = a.ovf_key[q];
         const unsigned i = (unsigned)(k & 0xffffffffull);
         if (i >= i_lo && i < i_hi) skeys[atomicAdd(&chunk_m, 1)] = k;
       }
@@ -1110,8 +1118,8 @@ __global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {  // the next batch's counters (it runs after this launch on the same stream)
-    a.bucket_cnt[b] = 0u;
-    a.bucket_fill[b] = 0u;
+    a.fill[b] = 0u;
+    if (b == 0) a.ovf_cnt[a.par ^ 1] = 0u;  // the next batch's overflow list (this batch's is reset by the next)
   }
 }
 
@@ -1508,9 +1516,8 @@ void state_init(Engine& e, const fd_state_params& p) {
   // allocates for the new capacity)
   st.uext.release();
   st.err.ensure(16);
-  st.bucket_cnt.ensure(kMaxBuckets * sizeof(unsigned));
   st.bucket_fill.ensure(kMaxBuckets * sizeof(unsigned));
-  st.bucket_base.ensure(kMaxBuckets * sizeof(unsigned));
+  st.ovf_cnt.ensure(2 * sizeof(unsigned));
   st.ready = true;
   state_clear(e);
 }
@@ -1521,8 +1528,8 @@ void state_clear(Engine& e) {
   FD_HIP(hipMemsetAsync(st.headers.ptr, 0, (size_t)st.cap * sizeof(CardHeader), e.stream));
   if (st.uext.ptr) FD_HIP(hipMemsetAsync(st.uext.ptr, 0, (size_t)st.cap * sizeof(UserExt), e.stream));
   FD_HIP(hipMemsetAsync(st.err.ptr, 0, 16, e.stream));
-  FD_HIP(hipMemsetAsync(st.bucket_cnt.ptr, 0, kMaxBuckets * sizeof(unsigned), e.stream));
   FD_HIP(hipMemsetAsync(st.bucket_fill.ptr, 0, kMaxBuckets * sizeof(unsigned), e.stream));
+  FD_HIP(hipMemsetAsync(st.ovf_cnt.ptr, 0, 2 * sizeof(unsigned), e.stream));
   FD_HIP(hipStreamSynchronize(e.stream));
   // the window event logs hold card-table slots: clearing the table empties them too
   WindowState& w = e.windows;
@@ -1593,38 +1600,40 @@ void load_merchants(Engine& e, const fd_merchants& m) {
 
 namespace {
 
-// The three grouping launches + the bucket kernel over any transaction source.
+// The grouping launch (feat_slot) + the bucket kernel over any transaction source.
 void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, double* d_raw, float* d_seq,
                     double* d_vel5) {
   CardStore& st = e.state;
   FD_REQUIRE(n <= (int64_t)kMaxBins * kChunkCap, FD_ERR_INVALID_ARG, "micro-batch larger than 16M transactions");
   st.slot.ensure((size_t)n * 4);
-  st.pairs.ensure((size_t)n * 8);
   st.prep.ensure((size_t)n * sizeof(Prep));
   if (st.merchants.ptr == nullptr) st.merchants.ensure(16);
   const unsigned nb = buckets_for(n, st.cap);
+  // bucket capacity: 4x the mean (Poisson tail beyond it is negligible for hashed cards; skewed batches spill
+  // to the overflow list), a multiple of 64
+  const unsigned C = (unsigned)std::max<int64_t>(512, ((4 * ((n + nb - 1) / nb)) + 63) / 64 * 64);
+  st.pairs.ensure((size_t)nb * C * 8);
+  st.ovf_key.ensure((size_t)n * 8);
+  st.ovf_b.ensure((size_t)n * 4);
+  const int par = st.batch_parity;
+  st.batch_parity ^= 1;
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
-  const unsigned gblocks = (unsigned)((n + kGT - 1) / kGT);
-  hipLaunchKernelGGL(feat_slot_kernel, dim3((unsigned)((n + kST - 1) / kST)), dim3(kST), nb * sizeof(unsigned),
+  hipLaunchKernelGGL(feat_slot_kernel, dim3((unsigned)((n + kST - 1) / kST)), dim3(kST), 2 * nb * sizeof(unsigned),
                      e.stream, st.headers.as<CardHeader>(), (long long)(st.cap - 1), n, src,
-                     st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, st.slot.as<unsigned>(),
-                     st.prep.as<Prep>(), st.bucket_cnt.as<unsigned>(), st.err.as<unsigned>());
+                     st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, C, st.slot.as<unsigned>(),
+                     st.prep.as<Prep>(), st.bucket_fill.as<unsigned>(), st.pairs.as<unsigned long long>(),
+                     st.ovf_cnt.as<unsigned>() + par, st.ovf_key.as<unsigned long long>(), st.ovf_b.as<unsigned>(),
+                     st.err.as<unsigned>());
   FD_HIP(hipGetLastError());
   static bool attrs = false;
-  if (!attrs) {  // > 48 KiB of dynamic LDS at the largest bucket counts
-    FD_HIP(hipFuncSetAttribute((const void*)feat_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               3 * kMaxBuckets * (int)sizeof(unsigned)));
+  if (!attrs) {  // > 48 KiB of dynamic LDS
     FD_HIP(hipFuncSetAttribute((const void*)feat_bucket_kernel<FD_WINDOW_SLIDING>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLds));
     FD_HIP(hipFuncSetAttribute((const void*)feat_bucket_kernel<FD_WINDOW_REDIS_COMPAT>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLds));
     attrs = true;
   }
-  hipLaunchKernelGGL(feat_scatter_kernel, dim3(gblocks), dim3(kGT), 3 * nb * sizeof(unsigned), e.stream, n,
-                     st.slot.as<const unsigned>(), nb - 1, st.bucket_cnt.as<const unsigned>(),
-                     st.bucket_fill.as<unsigned>(), st.bucket_base.as<unsigned>(), st.pairs.as<unsigned long long>());
-  FD_HIP(hipGetLastError());
   BucketArgs a{};
   a.H = st.headers.as<CardHeader>();
   a.ring = st.ring.as<RingEvent>();
@@ -1632,10 +1641,13 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.n = n;
   a.prep = st.prep.as<const Prep>();
   a.out = Outputs{d_vec, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S};
-  a.bucket_cnt = st.bucket_cnt.as<unsigned>();
-  a.bucket_fill = st.bucket_fill.as<unsigned>();
-  a.bucket_base = st.bucket_base.as<const unsigned>();
+  a.fill = st.bucket_fill.as<unsigned>();
   a.pairs = st.pairs.as<const unsigned long long>();
+  a.C = C;
+  a.ovf_cnt = st.ovf_cnt.as<unsigned>();
+  a.par = par;
+  a.ovf_key = st.ovf_key.as<const unsigned long long>();
+  a.ovf_b = st.ovf_b.as<const unsigned>();
   const size_t lds = kBucketLds;
   if (st.mode == FD_WINDOW_SLIDING)
     hipLaunchKernelGGL(feat_bucket_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), lds, e.stream, a);
