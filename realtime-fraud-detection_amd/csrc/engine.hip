@@ -217,7 +217,7 @@ int fd_engine_destroy(fd_engine* eng) {
   e.feat_in.release();
   fd::windows_release(e);
   fd::sink_release(e);
-  for (auto* b : {&e.route_blk, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.bias,
+  for (auto* b : {&e.route_blk, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.wpk4, &e.lstm.bias,
                   &e.lstm.wout, &e.lstm.bout, &e.state.seq})
     b->release();
   if (e.aux_stream) {
@@ -299,6 +299,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "ensemble_owner") {  // fused kernel: 0 owner tree group rotates per chunk; 1 always group 0
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_owner must be 0 or 1");
     e.ens_owner_fixed = value != 0;
+  } else if (k == "lstm_rows") {  // LSTM tile: 0 auto (4 below 4096 transactions, else 16), 4 or 16
+    FD_REQUIRE(value == 0 || value == 4 || value == 16, FD_ERR_INVALID_ARG, "lstm_rows must be 0, 4 or 16");
+    e.lstm_rows = (int)value;
   } else if (k == "ingest_stop_after") {  // diagnostics: 0 full; 1 stage; 2 + structure; 3 + members
     FD_REQUIRE(value >= 0 && value <= 3, FD_ERR_INVALID_ARG, "ingest_stop_after must be in 0..3");
     e.ingest.stop_after = (int)value;
@@ -1037,7 +1040,7 @@ int fd_unload_lstm(fd_engine* eng) {
   Engine& e = E(eng);
   FD_HIP(hipStreamSynchronize(e.stream));
   if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
-  for (auto* b : {&e.lstm.wpk, &e.lstm.bias, &e.lstm.wout, &e.lstm.bout}) b->release();
+  for (auto* b : {&e.lstm.wpk, &e.lstm.wpk4, &e.lstm.bias, &e.lstm.wout, &e.lstm.bout}) b->release();
   e.lstm.loaded = false;
   FD_API_END
 }

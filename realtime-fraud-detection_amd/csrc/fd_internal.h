@@ -152,7 +152,7 @@ struct __attribute__((aligned(8))) ResultRecord {
 struct LstmModel {
   bool loaded = false;
   int input_size = 0, n_out = 0;
-  DeviceBuffer wpk, bias, wout, bout;
+  DeviceBuffer wpk, wpk4, bias, wout, bout;  // wpk: 16-row kernel's B operands; wpk4: the 4-row kernel's
 };
 
 // One card's keyed state header (features.hip): 128 B = one L2 line, so a transaction's state read and
@@ -259,8 +259,8 @@ struct Engine {
   bool route_err_live = false;
   // optional per-launch kernel timing (HIP events on the launch stream)
   int forest_variant = 0;  // "forest_kernel" option
-  bool ens_owner_fixed = true;
-  int ens_split = 0;  // "ensemble_split" option: trees per tree group of the fused kernel  // "ensemble_owner" option (A/B of the fused kernel's chunk-owner schedule)
+  bool ens_owner_fixed = true;  // "ensemble_owner" option (A/B of the fused kernel's chunk-owner schedule)
+  int lstm_rows = 0;  // "lstm_rows" option: transactions per LSTM workgroup tile (0 auto, 4 or 16)
   bool ensemble_on = true;  // "ensemble" option: the fused XGBoost + IsolationForest + blend kernel (auto)
   bool timing = false;
   struct Timed {

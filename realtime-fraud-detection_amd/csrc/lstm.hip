@@ -18,7 +18,21 @@
 // the preload is coalesced); h_t goes through a double-buffered LDS tile laid out so each lane reads
 // its 32 A-operand values with 8 ds_read_b128; one barrier per time step.
 // Per 16-txn tile and step: 4 tiles x 36 k-steps = 144 MFMAs per wave = 2.36 MFLOP per workgroup.
+//
+// Small batches (the latency path, config 5's 1 k micro-batches) would leave most CUs idle with 16-row
+// tiles (64 workgroups for 1 k), and the recurrence cannot be split across CUs without a per-step
+// exchange of h_t. lstm_kernel4 therefore takes 4 transactions per workgroup on the 16-block form
+// v_mfma_f32_4x4x1_16b_f32 (the same f32 rate per instruction-cycle, a quarter of the rows): all 16
+// blocks share the A operand — the CBSZ/ABID broadcast of one block's 4 values, so a single VGPR holding
+// h[txn][k0 + block] feeds 16 instructions and a lane reads all of h_t with two ds_read_b128 — and each
+// block takes 4 gate columns, so one instruction is 4 txn x 64 columns x 1 k. Lane l of wave w accumulates column (gate l >> 4, unit
+// 16 w + (l & 15)) for the 4 transactions (one register each); a 4 x 4 transpose across the 16-lane
+// rows (two v_permlane32_swap + two v_permlane16_swap) then gives lane (q, unit) the i, f, g, o gates
+// of transaction q, so each lane updates ONE cell (5 transcendentals instead of 20). The workgroup
+// loops over tiles (persistent grid) with the weights resident in VGPRs.
+#include <algorithm>
 #include <cmath>
+#include <utility>
 
 #include "fd_internal.h"
 
@@ -29,10 +43,19 @@ constexpr int kH = kLstmHidden;  // 128
 constexpr int kI = kSeqInput;    // 16
 constexpr int kRows = 16;        // transactions per workgroup
 constexpr int kKS = kI / 4 + kH / 4;  // 36 k-steps of 4
+constexpr int kKT = kI + kH;          // 144 k values: one 4x4x1 MFMA each
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// Gate nonlinearities on the hardware transcendentals (v_exp_f32, v_rcp_f32: ~1 ulp each) instead of
+// the correctly rounded libm sequences: the per-step cell update is the serial tail between two MFMA
+// chains. sigm(x) = 1 / (1 + 2^(-x log2 e)) saturates to exactly 0 / 1; tanh(x) = 2 sigm(2x) - 1 has an
+// absolute error of a few 1e-8 near 0. The head's probabilities stay within the 1e-5 north-star bar
+// of the PyTorch fp32 forward (tests/test_gpu_lstm.py).
+__device__ __forceinline__ float sigm(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504088896341f));
+}
+__device__ __forceinline__ float tanh_g(float x) { return 2.0f * sigm(2.0f * x) - 1.0f; }
 
 __global__ void __launch_bounds__(512) lstm_kernel(const float* __restrict__ seq, int64_t n, int T,
                                                    const float* __restrict__ wpk, const float* __restrict__ bias,
@@ -88,9 +111,9 @@ __global__ void __launch_bounds__(512) lstm_kernel(const float* __restrict__ seq
     float* hn = &hbuf[(t + 1) & 1][0][0][0];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float ig = sigm(acc[0][j]), fg = sigm(acc[1][j]), gg = tanhf(acc[2][j]), og = sigm(acc[3][j]);
+      const float ig = sigm(acc[0][j]), fg = sigm(acc[1][j]), gg = tanh_g(acc[2][j]), og = sigm(acc[3][j]);
       c[j] = fg * c[j] + ig * gg;
-      const float hv = og * tanhf(c[j]);
+      const float hv = og * tanh_g(c[j]);
       const int r = 4 * (l >> 4) + j;
       hn[(r * 4 + (unit & 3)) * (kH / 4) + (unit >> 2)] = hv;
     }
@@ -116,6 +139,104 @@ __global__ void __launch_bounds__(512) lstm_kernel(const float* __restrict__ seq
       p = e1 / (e0 + e1);
     }
     prob[row0 + tid] = (double)p;
+  }
+}
+
+// lane row g (16 lanes), register j holds M[j][g] -> register j holds M[g][j]
+__device__ __forceinline__ void xpose_rows4(float& a0, float& a1, float& a2, float& a3) {
+  const auto r02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a2), false, false);
+  const auto r13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a1), __float_as_uint(a3), false, false);
+  const auto r01 = __builtin_amdgcn_permlane16_swap(r02[0], r13[0], false, false);
+  const auto r23 = __builtin_amdgcn_permlane16_swap(r02[1], r13[1], false, false);
+  a0 = __uint_as_float(r01[0]);
+  a1 = __uint_as_float(r01[1]);
+  a2 = __uint_as_float(r23[0]);
+  a3 = __uint_as_float(r23[1]);
+}
+
+// acc[J & 3] += A(block J, broadcast to all 16 blocks: CBSZ 4, ABID J) x B(b[J]) for J = 0..15: lanes
+// 4J..4J+3 of `a` hold the 4 transactions' values at k = k0 + J, so one VGPR feeds 16 k-steps
+template <int... J>
+__device__ __forceinline__ void mfma_abid16(float a, const float* b, f32x4* acc, std::integer_sequence<int, J...>) {
+  ((acc[J & 3] = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b[J], acc[J & 3], 4, J, 0)), ...);
+}
+
+__global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ seq, int64_t n, int T,
+                                                    const float* __restrict__ wpk4, const float* __restrict__ bias,
+                                                    const float* __restrict__ wout, const float* __restrict__ bout,
+                                                    int n_out, double* __restrict__ prob) {
+#pragma clang fp contract(off)
+  // h_t and x_t in the A-operand order: (txn i, k) at lane i + 4 (k & 15), register k >> 4
+  __shared__ __attribute__((aligned(16))) float hbuf[2][64][kH / 16];       // 4 KB
+  __shared__ __attribute__((aligned(16))) float xs[FD_MAX_SEQ_LEN][64];     // 4 KB
+  __shared__ float hT[4][kH];
+  __shared__ float zs[4][2];
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63;
+  // B operands: lane l holds W[(l >> 4) * 128 + 16 w + (l & 15)][k] for k = 0..143 (W_ih, then W_hh)
+  float bw[kKT];
+#pragma unroll
+  for (int k = 0; k < kKT; ++k) bw[k] = wpk4[((size_t)w * kKT + k) * 64 + l];
+  const int q = l >> 4, unit = 16 * w + (l & 15);
+  const float bcol = bias[q * kH + unit];
+  const int64_t ntiles = (n + 3) / 4;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row0 = tile * 4;
+    for (int idx = tid; idx < 4 * T * kI; idx += 512) {
+      const int r = idx / (T * kI), rem = idx - r * (T * kI), t = rem / kI, k = rem - t * kI;
+      xs[t][r + 4 * k] = (row0 + r < n) ? seq[(size_t)(row0 + r) * T * kI + rem] : 0.f;
+    }
+    (&hbuf[0][0][0])[tid] = 0.f;  // 512 threads = 4 x 128
+    float c = 0.f, h = 0.f;
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+      f32x4 acc[4] = {f32x4{bcol, bcol, bcol, bcol}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                      f32x4{0.f, 0.f, 0.f, 0.f}};
+      const f32x4 h0 = *reinterpret_cast<const f32x4*>(&hbuf[t & 1][l][0]);
+      const f32x4 h1 = *reinterpret_cast<const f32x4*>(&hbuf[t & 1][l][4]);
+      mfma_abid16(xs[t][l], &bw[0], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(h0[0], &bw[kI + 0], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(h0[1], &bw[kI + 16], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(h0[2], &bw[kI + 32], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(h0[3], &bw[kI + 48], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(h1[0], &bw[kI + 64], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(h1[1], &bw[kI + 80], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(h1[2], &bw[kI + 96], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(h1[3], &bw[kI + 112], acc, std::make_integer_sequence<int, 16>{});
+      // register r = transaction r of this lane's gate column; after the transpose register j = gate j of
+      // transaction q
+      float g0 = (acc[0][0] + acc[1][0]) + (acc[2][0] + acc[3][0]);
+      float g1 = (acc[0][1] + acc[1][1]) + (acc[2][1] + acc[3][1]);
+      float g2 = (acc[0][2] + acc[1][2]) + (acc[2][2] + acc[3][2]);
+      float g3 = (acc[0][3] + acc[1][3]) + (acc[2][3] + acc[3][3]);
+      xpose_rows4(g0, g1, g2, g3);
+      const float ig = sigm(g0), fg = sigm(g1), gg = tanh_g(g2), og = sigm(g3);
+      c = fg * c + ig * gg;
+      h = og * tanh_g(c);
+      hbuf[(t + 1) & 1][q + 4 * (unit & 15)][unit >> 4] = h;
+      __syncthreads();
+    }
+    hT[q][unit] = h;
+    __syncthreads();
+    if (tid < 4 * n_out) {  // dense head over h_T, fixed k order
+      const int r = tid / n_out, o = tid - r * n_out;
+      float z = bout[o];
+      for (int k = 0; k < kH; ++k) z = z + wout[o * kH + k] * hT[r][k];
+      zs[r][o] = z;
+    }
+    __syncthreads();
+    if (tid < 4 && row0 + tid < n) {
+      float p;
+      if (n_out == 1) {
+        p = sigm(zs[tid][0]);
+      } else {
+        const float m = fmaxf(zs[tid][0], zs[tid][1]);
+        const float e0 = expf(zs[tid][0] - m), e1 = expf(zs[tid][1] - m);
+        p = e1 / (e0 + e1);
+      }
+      prob[row0 + tid] = (double)p;
+    }
+    __syncthreads();  // xs / hbuf / hT / zs are rewritten by the next tile
   }
 }
 
@@ -145,6 +266,15 @@ void load_lstm(Engine& e, const fd_lstm_params& p) {
           }
           pk[(((size_t)w * 4 + g) * kKS + s) * 64 + l] = v;
         }
+  // 4-row kernel: [wave][k][lane] = W[(lane >> 4) * 128 + 16 wave + (lane & 15)][k], k < 16 from W_ih
+  std::vector<float> pk4((size_t)8 * kKT * 64);
+  for (int w = 0; w < 8; ++w)
+    for (int k = 0; k < kKT; ++k)
+      for (int l = 0; l < 64; ++l) {
+        const int row = (l >> 4) * kH + 16 * w + (l & 15);
+        const float v = k < kI ? (k < I ? p.w_ih[(size_t)row * I + k] : 0.f) : p.w_hh[(size_t)row * kH + (k - kI)];
+        pk4[((size_t)w * kKT + k) * 64 + l] = v;
+      }
   std::vector<float> b(4 * kH);
   for (int i = 0; i < 4 * kH; ++i) b[i] = (p.b_ih ? p.b_ih[i] : 0.f) + (p.b_hh ? p.b_hh[i] : 0.f);
   std::vector<float> wo((size_t)p.n_out * kH), bo(p.n_out);
@@ -152,10 +282,12 @@ void load_lstm(Engine& e, const fd_lstm_params& p) {
   for (int i = 0; i < p.n_out; ++i) bo[i] = p.b_out ? p.b_out[i] : 0.f;
   LstmModel& m = e.lstm;
   m.wpk.ensure(pk.size() * 4);
+  m.wpk4.ensure(pk4.size() * 4);
   m.bias.ensure(b.size() * 4);
   m.wout.ensure(wo.size() * 4);
   m.bout.ensure(16);
   FD_HIP(hipMemcpy(m.wpk.ptr, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
+  FD_HIP(hipMemcpy(m.wpk4.ptr, pk4.data(), pk4.size() * 4, hipMemcpyHostToDevice));
   FD_HIP(hipMemcpy(m.bias.ptr, b.data(), b.size() * 4, hipMemcpyHostToDevice));
   FD_HIP(hipMemcpy(m.wout.ptr, wo.data(), wo.size() * 4, hipMemcpyHostToDevice));
   FD_HIP(hipMemcpy(m.bout.ptr, bo.data(), bo.size() * 4, hipMemcpyHostToDevice));
@@ -173,9 +305,17 @@ void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, i
   FD_REQUIRE(d_seq && d_prob, FD_ERR_INVALID_ARG, "null sequence / output");
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_LSTM) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, stream));
-  hipLaunchKernelGGL(lstm_kernel, dim3((unsigned)((n + kRows - 1) / kRows)), dim3(512), 0, stream, d_seq, n, T,
-                     m.wpk.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),
-                     m.bout.as<const float>(), m.n_out, d_prob);
+  const int rows = e.lstm_rows ? e.lstm_rows : (n < 4096 ? 4 : 16);
+  if (rows == 4) {  // one 512-thread workgroup per CU (bw[] holds 144 VGPRs), looping over 4-row tiles
+    const int64_t tiles = (n + 3) / 4;
+    hipLaunchKernelGGL(lstm_kernel4, dim3((unsigned)std::min<int64_t>(tiles, 256)), dim3(512), 0, stream, d_seq, n,
+                       T, m.wpk4.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),
+                       m.bout.as<const float>(), m.n_out, d_prob);
+  } else {
+    hipLaunchKernelGGL(lstm_kernel, dim3((unsigned)((n + kRows - 1) / kRows)), dim3(512), 0, stream, d_seq, n, T,
+                       m.wpk.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),
+                       m.bout.as<const float>(), m.n_out, d_prob);
+  }
   FD_HIP(hipGetLastError());
   if (ev) FD_HIP(hipEventRecord(ev->b, stream));
 }

@@ -28,6 +28,22 @@ def test_lstm_matches_torch(engine, n, T, n_out):
     assert np.abs(p - ref).max() <= TOL, np.abs(p - ref).max()
 
 
+@pytest.mark.parametrize("rows", [4, 16])
+@pytest.mark.parametrize("n,T", [(5, 10), (1000, 10), (1029, 13)])
+def test_lstm_tile_kernels_match_torch(engine, rows, n, T):
+    """both tile forms (4 rows on v_mfma_f32_4x4x1_16b_f32, persistent; 16 rows on 16x16x4) forced through
+    the "lstm_rows" option, whatever the batch size"""
+    w = L.random_weights(16, 128, 2, seed=3 * n + T)
+    engine.load_lstm(w)
+    seq = np.random.default_rng(n + 1).normal(0, 1.5, (n, T, 16)).astype(np.float32)
+    engine.set_option("lstm_rows", rows)
+    try:
+        p = engine.lstm_predict(seq)
+    finally:
+        engine.set_option("lstm_rows", 0)
+    assert np.abs(p - R.lstm_forward(w, seq)).max() <= TOL
+
+
 def test_lstm_narrow_input_and_saturation(engine):
     w = L.random_weights(7, 128, 1, seed=9)
     w.w_hh *= 4.0  # strongly saturating gates
