@@ -624,6 +624,9 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
   int my_field0 = -1, my_colon0 = -1, my_field1 = -1, my_colon1 = -1;
   Val my0, my1;
   unsigned my_status = 0;
+  // user-agent string members are deferred to the cooperative scan below (r = 0 / 1: member j / j + 32)
+  bool ua_pend0 = false, ua_pend1 = false;
+  int ua_v0 = 0, ua_v1 = 0, ua_c0 = 0, ua_c1 = 0;
   for (int r = 0; r < 2; ++r) {
   const int mi = 32 * r + (lane & 31);
   for (int once = 0; once < 1 && structural_ok && mi < nm; ++once) {  // `continue` = member rejected
@@ -667,6 +670,18 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
       e = skip_value(s, v, L);
       while (e >= 0 && e < L && is_ws(s[e])) ++e;
       if (e < 0 || e >= L || (s[e] != ',' && s[e] != '}')) my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    if (f == F_UA && s[v] == '"') {  // the message's longest string: scanned by the whole wave below
+      if (r == 0) {
+        ua_pend0 = true;
+        ua_v0 = v;
+        ua_c0 = c;
+      } else {
+        ua_pend1 = true;
+        ua_v1 = v;
+        ua_c1 = c;
+      }
       continue;
     }
     // ---- one token scan per member: string / literal / number / location object
@@ -856,6 +871,120 @@ __global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* _
     }
     atomicMax(&win[ms][f], c);
   }
+  }
+  // ---- deferred user-agent strings (FeatureExtractor.analyzeSuspiciousUserAgent needs only the "bot" /
+  //      "crawler" substrings of the decoded string and its UTF-16 length): the whole wave walks each one 64
+  //      bytes per step. Lane p's backslash-run parity (read backwards) marks escape starts and escaped
+  //      characters, the escaped 'u's mark their 4 hex digits; the end is the first unescaped quote or
+  //      control byte (ballot). UTF-16 units = raw lead bytes (+1 for 4-byte leads) + one per escape; a
+  //      substring match starts on a raw byte (escapes decode to non-letters, so they only break matches).
+  //      Escapes the scan cannot price exactly — \u00XX below 0x80 (an ASCII letter could join a match) or
+  //      invalid ones — send the string back to its lane's serial decoder.
+  int ua_e0 = -1, ua_e1 = -1;
+  unsigned ua_f0 = 0, ua_f1 = 0;
+  bool ua_serial0 = false, ua_serial1 = false;
+  for (int r = 0; r < 2; ++r) {
+    unsigned long long pend = __ballot(r == 0 ? ua_pend0 : ua_pend1);
+    while (pend) {
+      const int owner = __ffsll((long long)pend) - 1;
+      pend &= pend - 1;
+      const int vpos = __shfl(r == 0 ? ua_v0 : ua_v1, owner);
+      const int oms = 2 * wv + (owner >> 5);
+      const Reader so{&stage[oms][0], shift_s[oms]};
+      const int oL = len_s[oms];
+      int units = 0, endq = -1, how = 0;  // how: 1 closing quote, 2 serial fallback, 3 control byte / end
+      bool hit = false;
+      unsigned long long u_prev = 0ull;
+      for (int base = vpos + 1;; base += 64) {
+        const int p = base + lane;
+        const int ch = p < oL ? so[p] : 0;
+        int run = 0;  // backslashes right before p, inside the string
+        for (int q = p - 1; q > vpos && so[q] == '\\'; --q) ++run;
+        const bool escaped = run & 1;
+        const bool esc_start = ch == '\\' && !escaped;
+        const unsigned long long U = __ballot(escaped && ch == 'u');
+        const unsigned long long hexcov_m = (U << 1) | (U << 2) | (U << 3) | (U << 4) | (u_prev >> 63) |
+                                            (u_prev >> 62) | (u_prev >> 61) | (u_prev >> 60);
+        u_prev = U;
+        const bool hexcov = (hexcov_m >> lane) & 1ull;
+        const bool covered = escaped || esc_start || hexcov;
+        const bool is_hex = (ch >= '0' && ch <= '9') || (ch >= 'a' && ch <= 'f') || (ch >= 'A' && ch <= 'F');
+        bool odd = hexcov && !is_hex;
+        if (escaped && !hexcov)
+          odd = odd || !(ch == '"' || ch == '\\' || ch == '/' || ch == 'b' || ch == 'f' || ch == 'n' ||
+                         ch == 'r' || ch == 't' || ch == 'u');
+        if (escaped && ch == 'u' && p + 3 < oL)  // \u00XX with XX < 0x80: decodes to ASCII
+          odd = odd || (so[p + 1] == '0' && so[p + 2] == '0' && so[p + 3] >= '0' && so[p + 3] <= '7');
+        const unsigned long long stop = __ballot(ch < 0x20 || (ch == '"' && !escaped && !hexcov));
+        const int first = stop ? __ffsll((long long)stop) - 1 : 64;
+        const bool content = lane < first;
+        if (__ballot(odd && lane <= first) != 0ull) {
+          how = 2;
+          break;
+        }
+        const bool raw = content && !covered;
+        units += __popcll(__ballot(raw && (ch & 0xC0) != 0x80)) + __popcll(__ballot(raw && ch >= 0xF0)) +
+                 __popcll(__ballot(content && esc_start));
+        bool m = false;
+        if (raw && ch == 'b' && p + 2 < oL) m = so[p + 1] == 'o' && so[p + 2] == 't';
+        if (raw && ch == 'c' && p + 6 < oL) {
+          const int c1 = so[p + 1], c2 = so[p + 2], c3 = so[p + 3], c4 = so[p + 4], c5 = so[p + 5], c6 = so[p + 6];
+          m = c1 == 'r' && c2 == 'a' && c3 == 'w' && c4 == 'l' && c5 == 'e' && c6 == 'r';
+        }
+        hit = hit || __ballot(m) != 0ull;
+        if (stop) {
+          endq = base + first;
+          how = __shfl(ch, first) == '"' ? 1 : 3;
+          break;
+        }
+      }
+      if (lane == owner) {
+        const int e = how == 1 ? endq + 1 : -1;
+        const unsigned flag = (hit || units < 20) ? 1u : 0u;
+        if (r == 0) {
+          ua_e0 = e;
+          ua_f0 = flag;
+          ua_serial0 = how == 2;
+        } else {
+          ua_e1 = e;
+          ua_f1 = flag;
+          ua_serial1 = how == 2;
+        }
+      }
+    }
+  }
+  for (int r = 0; r < 2; ++r) {  // each owner finishes its user-agent members as the member loop would
+    if (!(r == 0 ? ua_pend0 : ua_pend1)) continue;
+    const int v = r == 0 ? ua_v0 : ua_v1, c = r == 0 ? ua_c0 : ua_c1;
+    int e = r == 0 ? ua_e0 : ua_e1;
+    unsigned flag = r == 0 ? ua_f0 : ua_f1;
+    if (r == 0 ? ua_serial0 : ua_serial1) {
+      StrStats st;
+      e = scan_string(s, v, L, st);
+      flag = (st.bot || st.crawler || st.units < 20) ? 1u : 0u;
+    }
+    if (e < 0) {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    while (e < L && is_ws(s[e])) ++e;
+    if (e >= L || (s[e] != ',' && s[e] != '}')) {
+      my_status |= FD_INGEST_MALFORMED;
+      continue;
+    }
+    Val val;
+    val.null = false;
+    val.u = flag;
+    if (r == 0) {
+      my_field0 = F_UA;
+      my_colon0 = c;
+      my0 = val;
+    } else {
+      my_field1 = F_UA;
+      my_colon1 = c;
+      my1 = val;
+    }
+    atomicMax(&win[ms][F_UA], c);
   }
   if (my_status) atomicOr(&status_s[ms], my_status);
   __syncthreads();

@@ -103,6 +103,27 @@ def _edge_corpus():
         d(user_agent="Googlebot/2.1"), d(user_agent="short"), d(user_agent="x" * 19), d(user_agent="x" * 20),
         d(user_agent="\U0001F600" * 10), d(user_agent="\U0001F600" * 9 + "a"), d(user_agent="MyCrawler 1.0 crawler"),
         d(user_agent=None), d(device_fingerprint=None), d(transaction_id=None),
+        # the cooperative user-agent scan: matches across its 64-byte steps, long / multi-byte / empty strings,
+        # escapes (serial fallback), control bytes, duplicates, non-string values
+        d(user_agent="A" * 62 + "bot"), d(user_agent="A" * 60 + "crawler" + "B" * 100), d(user_agent="A" * 63 + "crawle"),
+        d(user_agent="b" * 64 + "ot"), d(user_agent="é" * 70), d(user_agent=""), d(user_agent='say "bot" loudly ok'),
+        d(user_agent="tab\there and a long tail of text"), d(user_agent=12345678901234567890123),
+        json.dumps(dict(base, user_agent="😀é中" * 30), ensure_ascii=False).encode(),
+        b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_agent": "\\u0062ot-agent long"}',
+        b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_agent": "x\x01yyyyyyyyyyyyyyyyyyyyy"}',
+        b'{"user_agent": "Mozilla bot", "user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", '
+        b'"userAgent": "Mozilla/5.0 long enough string here"}',
+        b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_agent": "abc',
+        d(user_agent="A" * 60 + "é中" + "bot"), d(user_agent="bo" + "é" + "t and more text here"),
+        d(user_agent="x" * 61 + "\U0001F600" * 3 + "crawler"), d(user_agent="ends with backslashes \\\\"),
+        d(user_agent='quote\\"bot\\\\' + "z" * 70), d(user_agent="é" * 19), d(user_agent="é" * 20),
+        b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_agent": "' + b"y" * 62 +
+        b'\\u00e9\\u4e2dcrawler"}',
+        b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_agent": "ro\\bot yyyyyyyyyyyyyyyy"}',
+        b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_agent": "c\\rawler yyyyyyyyyyyyyy"}',
+        b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_agent": "bad \\x escape yyyyyyyy"}',
+        b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_agent": "bad \\u12G4 hex yyyyyyy"}',
+        b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_agent": "cut \\u12"}',
         d(extra={"deep": [[[{"x": "]}"}]]], "s": "\\\"}"}), d(userId="camel"),
         b'{"user_id": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_id": "b"}',
         b'{"userId": "a", "amount": 1, "timestamp": "2025-01-01T00:00:00", "user_id": "b", "userId": "c"}',
