@@ -11,16 +11,17 @@
 // kernels keep the leaf-id outputs).
 //
 // Kernel: 1024 threads = 16 waves per tile (tree group gg = wave >> 2, transaction group wave & 3). Prologue:
-// the merged table is staged in LDS in feature ranges (passes) that fit the space of chunk buffer B + the
-// leaf tiles (dead until chunk 1), each transaction's 64-wide vector is binned into the [f][256] u32 tile.
-// Then the chunk stream is XGBoost's CHA-tree chunks followed by the IsolationForest's CHB-tree chunks
-// (node-only, one 1 KiB block per tree, double-buffered by LDS-DMA); per chunk each wave walks its TPG trees
-// for its 64 transactions (walk_ens: 4 VALU + 2 LDS reads per node step), loads the leaf values (stored to
-// the chunk's LDS leaf tile one iteration later, so the L2 latency overlaps the barrier), and a rotating
-// owner tree group adds a completed chunk's values in tree order into the f32 margin (XGBoost) or the f64
-// path-length sum (IsolationForest): both the reference's sequential sums, bit for bit. Epilogue (tree group 0, one
-// thread per transaction): sigmoid / IsolationForest transform, blend_row, outputs (columns, or the 24-B
-// route result records of the owner GPU).
+// each thread loads 16 features of its row into registers; the merged table is staged in LDS in feature
+// ranges (passes) that fit the chunk buffers + leaf-index tiles (dead until chunk 0 is staged) and every
+// value is binned into the u16 tile (two features per 1 KiB row, 32 KiB for 64 features). Then the chunk
+// stream is XGBoost's 24-tree chunks followed by the IsolationForest's 16-tree chunks (1 KiB node block per
+// tree + the chunk's leaf values, double-buffered by LDS-DMA); per chunk each wave walks its TPG trees
+// (6 / 4) for its 64 transactions (walk_ens: 4 VALU + 2 LDS reads per node step) and stores the packed leaf
+// indices to the chunk's index tile; the owner tree group (0) then adds each transaction's leaf values of
+// that chunk, read from LDS, in tree order into the f32 margin (XGBoost) or the f64 path-length sum
+// (IsolationForest): both the reference's sequential sums, bit for bit. Epilogue (tree group 0, one thread
+// per transaction): sigmoid / IsolationForest transform, blend_row, outputs (columns, or the 24-B route
+// result records of the owner GPU).
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -51,20 +52,25 @@ void forest_loaded(PackedForest& pf, const fd_forest_params& p, const fd_tree_ar
 namespace {
 
 constexpr int kEnsWG = 1024;
-constexpr int kCHA = 16;  // XGBoost trees per chunk (TPG 4)
-constexpr int kCHB = 12;  // IsolationForest trees per chunk (TPG 3)
+constexpr int kCHA = 24;  // XGBoost trees per chunk (TPG 6)
+constexpr int kCHB = 16;  // IsolationForest trees per chunk (TPG 4)
 constexpr int kMaxPass = 64;
 
 // A chunk in LDS: CH node blocks of 1 KiB (walk_ens link addressing), then the CH trees' leaf values
-// [CH][2^D]; its LDS buffer is sized for depth 8: max(16 x (1 KiB + 1 KiB f32), 12 x (1 KiB + 2 KiB f64)).
+// [CH][2^D]; its LDS buffer is sized for depth 8: max(24 x (1 KiB + 1 KiB f32), 16 x (1 KiB + 2 KiB f64)).
 constexpr uint32_t kEnsBuf = (uint32_t)(kCHA * (1024 + 256 * 4) > kCHB * (1024 + 256 * 8) ? kCHA * (1024 + 256 * 4)
                                                                                           : kCHB * (1024 + 256 * 8));
-constexpr uint32_t kEnsTile = 4u * kTile * 4u;  // leaf indices of one chunk: [tree group][txn] u32, a byte per tree
+constexpr uint32_t kEnsTile = 4u * kTile * 8u;  // leaf indices of one chunk: [tree group][txn] u64, a byte per tree
+
+// The bin tile: u16 bins, two features per 1 KiB row — feature f of transaction t at byte
+// (f >> 1) * 1024 + 4 t + 2 (f & 1) — so a node word's bits [15:10] = f >> 1 and bit 1 = f & 1 address it
+// with one AND-OR, and the 64 lanes of a read hit 64 distinct banks whatever features they ask for.
+__host__ __device__ constexpr uint32_t ens_xs_bytes(int nf) { return (uint32_t)((nf + 1) / 2) * 1024u; }
 
 // LDS bytes of the kernel: Xs | bufA | bufB | tile0 | tile1 | accA (f32) | accB (f64) | flags + owner counter,
 // + 1 KiB alignment
 size_t ens_lds(int nf, int /*D*/) {
-  return (size_t)nf * 1024 + 2 * (size_t)kEnsBuf + 2 * (size_t)kEnsTile + kTile * 4 + kTile * 8 + 128 + 1024;
+  return (size_t)ens_xs_bytes(nf) + 2 * (size_t)kEnsBuf + 2 * (size_t)kEnsTile + kTile * 4 + kTile * 8 + 128 + 1024;
 }
 
 struct EnsArgs {
@@ -95,11 +101,11 @@ struct EnsArgs {
   ResultRecord* res;
 };
 
-// Ensemble node word: j << 16 | feature << 10 | link << 3 | default_left. `link` makes the next pair address
-// one AND-OR: for a node at heap slot i above the last split level, link = i (its children pair is at byte
-// 8 i of the tree's 1 KiB block); at the last split level link = i - 2^(D-1), so the leaf is 2 link + right.
-// One step is then v_cmp + v_cndmask (child) + v_and_or (bin address) + v_and_or (pair address): 4 VALU, 2 LDS
-// reads (the forest kernels' walk4 needs 5 VALU: it tracks the heap position separately).
+// Ensemble node word: j << 16 | (feature >> 1) << 10 | link << 3 | (feature & 1) << 1 | default_left. `link`
+// makes the next pair address one AND-OR: for a node at heap slot i above the last split level, link = i (its
+// children pair is at byte 8 i of the tree's 1 KiB block); at the last split level link = i - 2^(D-1), so the
+// leaf is 2 link + right. One step is then v_cmp (u16 bin against the word's high half: SDWA) + v_cndmask
+// (child) + v_and_or (bin address) + v_and_or (pair address): 4 VALU, 2 LDS reads.
 constexpr uint32_t kLinkMask = 0x3F8u;
 
 template <int D, int TPG, bool NAN_AWARE>
@@ -114,7 +120,7 @@ __device__ __forceinline__ void walk_ens(uint32_t buf, int t0, uint32_t lane4, u
   }
 #pragma unroll
   for (int j = 0; j < TPG; ++j) {
-    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+    xw[j] = lds_load<uint16_t>((node[j] & 0xFC02u) | lane4);
     if (D > 1) {
       const u32x2 k = lds_load<u32x2>(tb[j] + 8u);
       kl[j] = k.x;
@@ -125,15 +131,15 @@ __device__ __forceinline__ void walk_ens(uint32_t buf, int t0, uint32_t lane4, u
   for (int l = 0; l < D; ++l) {
 #pragma unroll
     for (int j = 0; j < TPG; ++j) {
-      bool right = xw[j] > node[j];  // bin > j  <=>  !(x < t_j)
+      bool right = xw[j] > (node[j] >> 16);  // bin > j  <=>  !(x < t_j)
       if (NAN_AWARE) {
-        if (xw[j] == 0xFFFF0000u) right = (node[j] & 1u) == 0u;  // missing: default direction
+        if (xw[j] == 0xFFFFu) right = (node[j] & 1u) == 0u;  // missing: default direction
       }
       if (l + 1 < D) {
         uint32_t a = kl[j], b = kr[j];
         asm volatile("" : "+v"(a), "+v"(b));
         node[j] = right ? b : a;
-        xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
+        xw[j] = lds_load<uint16_t>((node[j] & 0xFC02u) | lane4);
         if (l + 2 < D) {
           const u32x2 k = lds_load<u32x2>((node[j] & kLinkMask) | tb[j]);
           kl[j] = k.x;
@@ -147,20 +153,24 @@ __device__ __forceinline__ void walk_ens(uint32_t buf, int t0, uint32_t lane4, u
 }
 
 // Walk this wave's TPG trees of the chunk at `cur` (trees gg*TPG ...) for its 64 transactions; the leaf
-// indices (< 2^D <= 256) packed a byte per tree, in tree order, stored as one u32 per (tree group, txn).
+// indices (< 2^D <= 256) packed a byte per tree, in tree order, stored as one u64 per (tree group, txn).
 // (Measured: byte-per-tree stores of a [txn][16] tile cost ~5 us more per 64k batch; skewing the split
 // towards tree group 0 was slower still.)
 template <int D, int TPG>
-__device__ __forceinline__ uint32_t walk_pack(uint32_t cur, int gg, uint32_t lane4, bool tile_nan) {
+__device__ __forceinline__ unsigned long long walk_pack(uint32_t cur, int gg, uint32_t lane4, bool tile_nan) {
+  static_assert(TPG <= 8, "a byte per tree in a u64");
   uint32_t leaf[TPG];
   if (tile_nan)
     walk_ens<D, TPG, true>(cur, gg * TPG, lane4, leaf);
   else
     walk_ens<D, TPG, false>(cur, gg * TPG, lane4, leaf);
-  uint32_t w = 0;
+  uint32_t lo = 0, hi = 0;
 #pragma unroll
-  for (int j = 0; j < TPG; ++j) w |= leaf[j] << (8 * j);
-  return w;
+  for (int j = 0; j < TPG; ++j) {
+    if (j < 4) lo |= leaf[j] << (8 * j);
+    else hi |= leaf[j] << (8 * (j - 4));
+  }
+  return ((unsigned long long)hi << 32) | lo;
 }
 
 // One transaction's share of a finished chunk: its CH leaf values (indices from the tile, values from the
@@ -169,13 +179,13 @@ __device__ __forceinline__ uint32_t walk_pack(uint32_t cur, int gg, uint32_t lan
 template <int D, int TPG, int CH, typename LeafT>
 __device__ __forceinline__ void owner_sum(uint32_t buf, uint32_t tile, uint32_t acc, int txn) {
   constexpr int NL = 1 << D;
-  uint32_t w[4];
+  unsigned long long w[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) w[q] = lds_load<uint32_t>(tile + (uint32_t)(q * kTile + txn) * 4u);
+  for (int q = 0; q < 4; ++q) w[q] = lds_load<unsigned long long>(tile + (uint32_t)(q * kTile + txn) * 8u);
   LeafT v[CH];
 #pragma unroll
   for (int t = 0; t < CH; ++t) {
-    const uint32_t idx = (w[t / TPG] >> (8 * (t % TPG))) & 0xFFu;
+    const uint32_t idx = (uint32_t)(w[t / TPG] >> (8 * (t % TPG))) & 0xFFu;
     v[t] = lds_load<LeafT>(buf + (uint32_t)(CH * 1024) + ((uint32_t)(t * NL) + idx) * (uint32_t)sizeof(LeafT));
   }
   LeafT s = lds_load<LeafT>(acc + (uint32_t)txn * (uint32_t)sizeof(LeafT));
@@ -226,7 +236,7 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   const int gg = __builtin_amdgcn_readfirstlane(wave >> 2);  // wave-uniform: scalar addressing
   const int txn = ((wave & 3) << 6) + lane;
   const uint32_t lane4 = s0 + (uint32_t)txn * 4u;
-  const uint32_t bufA = s0 + (uint32_t)a.nf * 1024u, bufB = bufA + kEnsBuf;
+  const uint32_t bufA = s0 + ens_xs_bytes(a.nf), bufB = bufA + kEnsBuf;
   const uint32_t tile0 = bufB + kEnsBuf, tile1 = tile0 + kEnsTile;
   const uint32_t accA = tile1 + kEnsTile, accB = accA + kTile * 4;
   const uint32_t flags = accB + kTile * 8, owner_cnt = flags + 64;
@@ -240,15 +250,15 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   FD_ESTAMP(pr_t0);
   int anynan = 0;
   {
-    uint32_t* Xs = reinterpret_cast<uint32_t*>(lbase);
+    uint16_t* Xs = reinterpret_cast<uint16_t*>(lbase);
     const int q = __builtin_amdgcn_readfirstlane(tid >> 8);  // wave-uniform: the four threads sharing `txn`
+    const int fq = q * 16;
     // (1) raw values: thread (q, txn) loads features [16 q, 16 q + 16) of its row in one go (all loads in
-    // flight together) and stores them transposed into the [f][256] tile (lane = txn: conflict-free)
+    // flight together) and keeps them in registers until they are binned
+    float v[16];
     if (valid) {
       const float* xr = a.X + row * (int64_t)a.ld;
       const int ncopy = a.ld < a.nf ? a.ld : a.nf;
-      const int fq = q * 16;
-      float v[16];
       if (a.vec4 && fq + 16 <= ncopy) {
         const float4* x4 = reinterpret_cast<const float4*>(xr + fq);
 #pragma unroll
@@ -263,16 +273,13 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = fq + k < ncopy ? xr[fq + k] : __builtin_nanf("");  // missing: NaN
       }
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (fq + k < a.nf) Xs[(fq + k) * kTile + txn] = __float_as_uint(v[k]);
     }
-    __syncthreads();
 #ifdef FD_FOREST_PROFILE
     pr_st[0] = __builtin_amdgcn_s_memtime();
 #endif
-    // (2) per pass: stage its tables, then bin in place four features at a time (independent searches in
-    // lockstep, so four LDS reads are in flight per step)
+    // (2) per pass: stage its tables, then bin this thread's features of the pass kLock at a time (independent
+    // searches in lockstep, so kLock LDS reads are in flight per step) into the u16 tile
+    constexpr int kLock = 4;  // 8 measured slower (bank conflicts of the diverging searches, not latency)
     for (int p = 0; p < a.n_pass; ++p) {
       const int f0 = a.pass_f[p], f1 = a.pass_f[p + 1];
       const bool glob = (a.pass_global >> p) & 1ull;
@@ -297,17 +304,21 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
       if (p < 3) pr_st[1 + 2 * p] = __builtin_amdgcn_s_memtime();
 #endif
       if (valid) {
-        for (int fb = f0 + q; fb < f1; fb += 16) {
-          float v[4];
-          int o[4], cnt[4], pos[4];
+#pragma unroll
+        for (int kk = 0; kk < 16; kk += kLock) {
+          const int fb = fq + kk;
+          if (fb + kLock - 1 < f0 || fb >= f1) continue;  // wave-uniform
+          float vv[kLock];
+          int o[kLock], cnt[kLock], pos[kLock];
+          bool act[kLock];
           int steps = 0;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int f = fb + 4 * k;
-            const bool act = f < f1;
-            v[k] = act ? __uint_as_float(Xs[f * kTile + txn]) : 0.f;
-            o[k] = act ? a.thr_off[f] : o0;
-            cnt[k] = act ? a.thr_off[f + 1] - o[k] : 0;
+          for (int k = 0; k < kLock; ++k) {
+            const int f = fb + k;
+            act[k] = f >= f0 && f < f1;
+            vv[k] = act[k] ? v[kk + k] : 0.f;
+            o[k] = act[k] ? a.thr_off[f] : o0;
+            cnt[k] = act[k] ? a.thr_off[f + 1] - o[k] : 0;
             pos[k] = 0;
             steps = max(steps, lift_steps(cnt[k]));
           }
@@ -315,41 +326,41 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
           // reads of a step issue back to back
           if (!glob) {
             for (int st = steps; st > 0; st >>= 1) {
-              float t[4];
+              float t[kLock];
 #pragma unroll
-              for (int k = 0; k < 4; ++k) {
+              for (int k = 0; k < kLock; ++k) {
                 const int np = pos[k] + st;
                 const int idx = np <= cnt[k] ? np - 1 : 0;
                 t[k] = lds_load<float>(tl + (uint32_t)thr_pad(o[k] - o0 + idx) * 4u);
               }
 #pragma unroll
-              for (int k = 0; k < 4; ++k) {
+              for (int k = 0; k < kLock; ++k) {
                 const int np = pos[k] + st;
-                pos[k] = (np <= cnt[k] && t[k] <= v[k]) ? np : pos[k];
+                pos[k] = (np <= cnt[k] && t[k] <= vv[k]) ? np : pos[k];
               }
             }
           } else {
             for (int st = steps; st > 0; st >>= 1) {
-              float t[4];
+              float t[kLock];
 #pragma unroll
-              for (int k = 0; k < 4; ++k) {
+              for (int k = 0; k < kLock; ++k) {
                 const int np = pos[k] + st;
                 t[k] = a.thr[o[k] + (np <= cnt[k] ? np - 1 : 0)];
               }
 #pragma unroll
-              for (int k = 0; k < 4; ++k) {
+              for (int k = 0; k < kLock; ++k) {
                 const int np = pos[k] + st;
-                pos[k] = (np <= cnt[k] && t[k] <= v[k]) ? np : pos[k];
+                pos[k] = (np <= cnt[k] && t[k] <= vv[k]) ? np : pos[k];
               }
             }
           }
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int f = fb + 4 * k;
-            if (f < f1) {
-              const bool nan = v[k] != v[k];
+          for (int k = 0; k < kLock; ++k) {
+            const int f = fb + k;
+            if (act[k]) {
+              const bool nan = vv[k] != vv[k];
               anynan |= nan ? 1 : 0;
-              Xs[f * kTile + txn] = nan ? 0xFFFF0000u : ((uint32_t)pos[k] << 16);
+              Xs[(f >> 1) * 512 + txn * 2 + (f & 1)] = nan ? (uint16_t)0xFFFFu : (uint16_t)pos[k];
             }
           }
         }
@@ -399,8 +410,9 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     }
     const uint32_t cur = (g & 1) ? bufB : bufA, tw = (g & 1) ? tile1 : tile0;
     FD_ESTAMP(q1);
-    const uint32_t w = g < nA ? walk_pack<D, TPGA>(cur, gg, lane4, tile_nan) : walk_pack<D, TPGB>(cur, gg, lane4, tile_nan);
-    lds_store<uint32_t>(tw + (uint32_t)(gg * kTile + txn) * 4u, w);
+    const unsigned long long w =
+        g < nA ? walk_pack<D, TPGA>(cur, gg, lane4, tile_nan) : walk_pack<D, TPGB>(cur, gg, lane4, tile_nan);
+    lds_store<unsigned long long>(tw + (uint32_t)(gg * kTile + txn) * 8u, w);
     FD_ESTAMP(q2);
     if (owner) dma_wait();
     __syncthreads();
@@ -552,14 +564,16 @@ bool build_plan(Engine& e, int sa, int sb) {
       for (int s = 1; s < NL; ++s) {
         uint32_t w;
         std::memcpy(&w, src + (size_t)s * 4, 4);
+        const uint32_t f = (w >> 10) & 63u;
         if (!h.pad[(size_t)i * NL + s]) {  // real split: its threshold's index in the merged table
-          const int f = (int)((w >> 10) & 63u), j = (int)(w >> 16);
+          const int j = (int)(w >> 16);
           const float t = h.b_thr[h.b_thr_off[f] + j];
           const uint32_t jm = (uint32_t)(std::lower_bound(merged[f].begin(), merged[f].end(), t) - merged[f].begin());
           w = (jm << 16) | (w & 0xFFFFu);
         }
         const uint32_t link = s < (NL >> 1) ? (uint32_t)s : (uint32_t)(s - (NL >> 1));
-        dst[s] = (w & ~0x3FEu) | (link << 3);  // walk_ens node word
+        // walk_ens node word: the pair-row of the u16 bin tile in bits [15:10], the feature's half in bit 1
+        dst[s] = (w & 0xFFFF0001u) | ((f >> 1) << 10) | (link << 3) | ((f & 1u) << 1);
       }
       std::memcpy(chunk + (size_t)CH[k] * 1024 + (size_t)(i % CH[k]) * NL * leaf_sz[k], src + (size_t)NL * 4,
                   (size_t)NL * leaf_sz[k]);
