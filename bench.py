@@ -42,6 +42,7 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA peak (MI355X_MICROARCH.md "
 # 64-lane wave-instruction 2 + 2 LDS-array cycles (MI355X_MICROARCH.md §LDS) = 16 node-steps/clk/CU.
 LDS_NODE_STEPS_PEAK = 256 * 2.4e9 * 16  # 9.83e12 node-steps/s
 FUSED_BYTES_PER_TXN = 238  # txn 36 + card header R/W 96 + profiles 64 + outputs 10 + ring append 32
+TIMING_EVERY = 8  # kernel-timing sample period (engine option "timing_every")
 
 
 def log(*a):
@@ -881,6 +882,9 @@ def main():
     if dist:
         dist.barrier()
     eng.read_timing()
+    # kernel durations: HIP events on the launch stream, on one launch in TIMING_EVERY of each kernel (an event
+    # record costs stream time; timing every launch would charge ~10 us per step of instrumentation to `value`)
+    eng.set_option("timing_every", TIMING_EVERY)
     eng.set_timing(True)
     torch.cuda.synchronize()
     if dist:
@@ -940,6 +944,7 @@ def main():
             "p99_batch_latency_ms": round(p99, 4),
             "roofline": roof,
             "kernel_avg_us": wl.kernels(timing),
+            "kernel_timing": f"HIP events on the launch stream, 1 launch in {TIMING_EVERY} of each kernel, timed region",
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
         }

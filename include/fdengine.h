@@ -590,7 +590,11 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      binned 1024-thread kernel with its top three tree levels read from registers (A/B: slower), 8 force
      the binned node-only-chunk kernel (auto's choice when the forest has that layout), 9 force it with
      dynamic per-wave (tree, transaction group) work items (A/B: slower), 10 force it with more trees for
-     the older tree groups (A/B: slower) */
+     the older tree groups (A/B: slower)
+     "ensemble": 1 fused XGBoost + IsolationForest + blend kernel when applicable (default), 0 per-model kernels
+     "lstm_rows": LSTM tile, 0 auto (4 transactions below 4096, else 16), 4 or 16
+     "timing_every": N >= 1, fd_engine_set_timing records HIP events on one launch in N of each timing kind
+     (the others run without event records; fd_timing_read's launch count is the timed ones) */
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
 int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches);
 int fd_timing_reset(fd_engine* eng);

@@ -15,10 +15,13 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 Engine::Timed* Engine::next_event_pair(int kind) {
+  if (timing_every > 1 && kind >= 0 && kind < 16 && (timing_seq[kind]++ % (unsigned)timing_every) != 0)
+    return nullptr;  // sampled timing: this launch runs without event records
   if (events_used == events.size()) {
+    // timing events only: no system-scope fence at record (a fenced record costs ~4 us of stream time)
     hipEvent_t a, b;
-    FD_HIP(hipEventCreate(&a));
-    FD_HIP(hipEventCreate(&b));
+    FD_HIP(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+    FD_HIP(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
     events.push_back({a, b, 0});
   }
   Timed* t = &events[events_used++];
@@ -299,6 +302,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "ensemble_owner") {  // fused kernel: 0 owner tree group rotates per chunk; 1 always group 0
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_owner must be 0 or 1");
     e.ens_owner_fixed = value != 0;
+  } else if (k == "timing_every") {  // kernel timing (fd_timing_*): HIP events on one launch in N of each kind
+    FD_REQUIRE(value >= 1 && value <= 1000000, FD_ERR_INVALID_ARG, "timing_every must be >= 1");
+    e.timing_every = (int)value;
+    for (auto& q : e.timing_seq) q = 0;  // the next launch of every kind is a timed one
   } else if (k == "lstm_rows") {  // LSTM tile: 0 auto (4 below 4096 transactions, else 16), 4 or 16
     FD_REQUIRE(value == 0 || value == 4 || value == 16, FD_ERR_INVALID_ARG, "lstm_rows must be 0, 4 or 16");
     e.lstm_rows = (int)value;

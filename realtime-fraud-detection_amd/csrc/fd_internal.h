@@ -263,6 +263,8 @@ struct Engine {
   int lstm_rows = 0;  // "lstm_rows" option: transactions per LSTM workgroup tile (0 auto, 4 or 16)
   bool ensemble_on = true;  // "ensemble" option: the fused XGBoost + IsolationForest + blend kernel (auto)
   bool timing = false;
+  int timing_every = 1;               // "timing_every" option: time one launch in N of each kind
+  unsigned long long timing_seq[16] = {};
   struct Timed {
     hipEvent_t a, b;
     int kind;

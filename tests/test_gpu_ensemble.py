@@ -13,7 +13,7 @@ import pytest
 
 import oracle
 from fdengine import FraudEngine, iforest_from_sklearn, synth, xgboost_from_json_doc
-from fdengine._native import FD_TIMING_ENSEMBLE
+from fdengine._native import FD_TIMING_ENSEMBLE, NativeError
 from oracle import scoring_ref as S
 
 pytestmark = pytest.mark.gpu
@@ -113,3 +113,27 @@ def test_reload_invalidates_the_joint_repack(engine):
     _check(engine, xgb, ifm, X)
     xgb_b, _ = _models(64, 8, n_trees=70, seed=16)
     _check(engine, xgb_b, ifm, X)  # a different model in slot 0: the cached plan must not be reused
+
+
+def test_sampled_kernel_timing(engine):
+    """engine option "timing_every" = 3: HIP events on launches 0, 3, 6 of each kind; averages unchanged in kind"""
+    xgb, ifm = _models(64, 8, n_trees=40, seed=17)
+    engine.load_forest(0, xgb)
+    engine.load_forest(1, ifm)
+    X = synth.feature_matrix(N, 64, seed=18)
+    params = FraudEngine.blend_params([0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
+    engine.read_timing()
+    engine.set_option("timing_every", 3)
+    try:
+        engine.set_timing(True)
+        outs = [engine.score_matrix(params, [0, 1], X) for _ in range(7)]
+        engine.set_timing(False)
+        ms, launches = engine.read_timing(FD_TIMING_ENSEMBLE)
+    finally:
+        engine.set_option("timing_every", 1)
+    assert launches == 3 and ms > 0.0
+    for o in outs[1:]:
+        for u, v in zip(o, outs[0]):
+            np.testing.assert_array_equal(u, v)
+    with pytest.raises(NativeError):
+        engine.set_option("timing_every", 0)
