@@ -484,7 +484,10 @@ class Config4(Config3):
         self.tx = synth.txn_stream_cards(self.cards, self.merchants, self.n_batches * self.B, seed=200 + rank,
                                          card_seed=42, rate_per_s=2000.0)
         self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
-        self.scorer = ShardedScorer(EngineShardBackend(eng, self.params, [0, 1]), rank, self.world)
+        # world 1: the stream of resident micro-batches goes through fd_score_batch_pipelined (batch i+1's
+        # features overlap batch i's forests); the inputs were complete before the first step (setup sync)
+        self.scorer = ShardedScorer(EngineShardBackend(eng, self.params, [0, 1],
+                                                       pipelined=not args.no_pipeline), rank, self.world)
         self.out = None
         B = self.B
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
@@ -835,6 +838,8 @@ def main():
     ap.add_argument("--ring-k", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="config4 at N=1: fd_score_batch_device per step instead of the pipelined stream")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--parity-batches", type=int, default=2)
     args = ap.parse_args()

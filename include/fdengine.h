@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 11
+#define FD_ABI_VERSION 12
 
 enum fd_status {
   FD_OK = 0,
@@ -356,6 +356,21 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
                           const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
                           int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
                           double* d_confidence, uint8_t* d_decision, uint8_t* d_risk);
+
+/* Streaming form of fd_score_batch_device for a sequence of micro-batches (the Flink operator chain is
+   pipelined record by record; here micro-batch by micro-batch). Same results, same card-state order.
+   The feature launches of batch i run on the engine's feature stream, ordered after batch i-1's feature
+   launches and after `input_ready` (a hipEvent_t the caller recorded once the batch's input columns were
+   in device memory; NULL = they were complete before this call); the scoring launches run on the engine
+   stream after batch i's features, so the outputs are ordered on the engine stream exactly as with
+   fd_score_batch_device. Batch i+1's features therefore overlap batch i's forests. The scoring vectors
+   live in two engine buffers (batch parity); the input columns must stay unchanged until the call's
+   outputs are complete. Any other engine call in between orders the next batch's features after
+   everything queued on the engine stream (no overlap across it). */
+int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                             const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
+                             int64_t n, double* d_model_probs, double* d_fraud_prob, double* d_confidence,
+                             uint8_t* d_decision, uint8_t* d_risk, void* input_ready);
 
 /* per-transaction window / sink inputs beyond fd_txn_batch; any pointer may be NULL */
 typedef struct fd_window_inputs_s {

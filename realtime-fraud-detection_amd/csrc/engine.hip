@@ -54,7 +54,17 @@ struct fd_engine {
   Engine e;
 };
 
+// Engine of an entry point that may queue work on e.stream: the next fd_score_batch_pipelined orders its
+// feature stream after e.stream again (pipe_dirty).
 static Engine& E(fd_engine* p) {
+  FD_REQUIRE(p != nullptr, FD_ERR_INVALID_ARG, "null engine");
+  p->e.activate();
+  p->e.pipe_dirty = true;
+  return p->e;
+}
+
+// Engine of an entry point that queues no device work touching engine state (options, timing reads)
+static Engine& E_quiet(fd_engine* p) {
   FD_REQUIRE(p != nullptr, FD_ERR_INVALID_ARG, "null engine");
   p->e.activate();
   return p->e;
@@ -234,6 +244,13 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipStreamDestroy(e.aux2_stream);
     (void)hipEventDestroy(e.join2_ev);
   }
+  if (e.feat_stream) {
+    (void)hipStreamSynchronize(e.feat_stream);
+    (void)hipStreamDestroy(e.feat_stream);
+    for (hipEvent_t ev : {e.pipe_feat_ev, e.pipe_entry_ev, e.pipe_score_ev[0], e.pipe_score_ev[1]})
+      (void)hipEventDestroy(ev);
+  }
+  for (auto* b : {&e.pipe_vec[0], &e.pipe_vec[1], &e.pipe_seq[0], &e.pipe_seq[1]}) b->release();
   for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
   for (auto* b : {&e.ens.nodes[0], &e.ens.nodes[1], &e.ens.thr})
     b->release();
@@ -246,7 +263,8 @@ int fd_engine_destroy(fd_engine* eng) {
     }
   }
   for (auto* b : {&e.state.headers, &e.state.ring, &e.state.merchants, &e.state.slot, &e.state.err,
-                  &e.state.bucket_fill, &e.state.pairs, &e.state.ovf_cnt, &e.state.ovf_key, &e.state.ovf_b, &e.state.prep})
+                  &e.state.bucket_fill, &e.state.pairs, &e.state.ovf_cnt, &e.state.ovf_key, &e.state.ovf_b, &e.state.prep,
+                  &e.state.defer})
     b->release();
   for (auto& ev : e.events) {
     (void)hipEventDestroy(ev.a);
@@ -275,6 +293,7 @@ int fd_engine_sync(fd_engine* eng) {
   FD_API_BEGIN
   Engine& e = E(eng);
   FD_HIP(hipStreamSynchronize(e.stream));
+  if (e.feat_stream) FD_HIP(hipStreamSynchronize(e.feat_stream));
   if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
   if (e.aux2_stream) FD_HIP(hipStreamSynchronize(e.aux2_stream));
   fd::route_check(e);
@@ -283,14 +302,14 @@ int fd_engine_sync(fd_engine* eng) {
 
 int fd_engine_set_timing(fd_engine* eng, int enable) {
   FD_API_BEGIN
-  Engine& e = E(eng);
+  Engine& e = E_quiet(eng);
   e.timing = enable != 0;
   FD_API_END
 }
 
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   FD_API_BEGIN
-  Engine& e = E(eng);
+  Engine& e = E_quiet(eng);
   FD_REQUIRE(key, FD_ERR_INVALID_ARG, "null key");
   const std::string k(key);
   if (k == "forest_kernel") {
@@ -302,6 +321,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "ensemble_owner") {  // fused kernel: 0 owner tree group rotates per chunk; 1 always group 0
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_owner must be 0 or 1");
     e.ens_owner_fixed = value != 0;
+  } else if (k == "pipeline_lean") {  // fd_score_batch_pipelined's bucket pass: 1 (default) lean + deferred
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "pipeline_lean must be 0 or 1");
+    e.pipe_lean = value != 0;
   } else if (k == "timing_every") {  // kernel timing (fd_timing_*): HIP events on one launch in N of each kind
     FD_REQUIRE(value >= 1 && value <= 1000000, FD_ERR_INVALID_ARG, "timing_every must be >= 1");
     e.timing_every = (int)value;
@@ -323,7 +345,7 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
 
 int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches) {
   FD_API_BEGIN
-  Engine& e = E(eng);
+  Engine& e = E_quiet(eng);
   double tot = 0.0;
   int64_t cnt = 0;
   for (size_t i = 0; i < e.events_used; ++i) {
@@ -341,8 +363,8 @@ int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches
 
 int fd_timing_reset(fd_engine* eng) {
   FD_API_BEGIN
-  Engine& e = E(eng);
-  if (e.events_used) FD_HIP(hipEventSynchronize(e.events[e.events_used - 1].b));
+  Engine& e = E_quiet(eng);
+  for (size_t i = 0; i < e.events_used; ++i) FD_HIP(hipEventSynchronize(e.events[i].b));  // pairs on 2+ streams
   e.events_used = 0;
   FD_API_END
 }
@@ -697,6 +719,53 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
   fd::launch_features(e, *txns, n, vec, nullptr, seq);
   score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
                d_confidence, d_decision, d_risk, seq, e.state.S);
+  FD_API_END
+}
+
+int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                             const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
+                             int64_t n, double* d_model_probs, double* d_fraud_prob, double* d_confidence,
+                             uint8_t* d_decision, uint8_t* d_risk, void* input_ready) {
+  FD_API_BEGIN
+  Engine& e = E_quiet(eng);
+  FD_REQUIRE(params && txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  if (n == 0) return FD_OK;
+  if (!e.feat_stream) {
+    FD_HIP(hipStreamCreateWithFlags(&e.feat_stream, hipStreamNonBlocking));
+    for (hipEvent_t* ev : {&e.pipe_feat_ev, &e.pipe_entry_ev, &e.pipe_score_ev[0], &e.pipe_score_ev[1]})
+      FD_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  }
+  hipStream_t F = e.feat_stream;
+  if (e.pipe_dirty) {  // work queued on e.stream by other calls (state loads, snapshots, ...) comes first
+    FD_HIP(hipEventRecord(e.pipe_entry_ev, e.stream));
+    FD_HIP(hipStreamWaitEvent(F, e.pipe_entry_ev, 0));
+    e.pipe_dirty = false;
+  }
+  if (input_ready) FD_HIP(hipStreamWaitEvent(F, static_cast<hipEvent_t>(input_ready), 0));
+  const int b = e.pipe_parity;
+  // the scoring launches that last read buffer b (batch i-2) must be done before batch i's features write it
+  if (e.pipe_score_live[b]) FD_HIP(hipStreamWaitEvent(F, e.pipe_score_ev[b], 0));
+  e.pipe_vec[b].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
+  float* vec = e.pipe_vec[b].as<float>();
+  float* seq = nullptr;
+  bool want_seq = false;
+  for (int m = 0; m < params->n_models && m < FD_MAX_MODELS; ++m)
+    want_seq = want_seq || (slots && slots[m] == FD_SLOT_LSTM && !(present && !present[m]));
+  if (want_seq) {
+    FD_REQUIRE(e.state.ready && e.state.S > 0, FD_ERR_INVALID_ARG,
+               "the LSTM head needs card history: fd_state_params.seq_len > 0");
+    e.pipe_seq[b].ensure((size_t)n * e.state.S * fd::kSeqInput * sizeof(float));
+    seq = e.pipe_seq[b].as<float>();
+  }
+  fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, F, e.pipe_lean);
+  FD_HIP(hipEventRecord(e.pipe_feat_ev, F));
+  FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_feat_ev, 0));
+  // parity flips only once the launches are queued (a failed call leaves the buffers' order intact)
+  e.pipe_parity ^= 1;
+  score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
+               d_confidence, d_decision, d_risk, seq, e.state.S);
+  FD_HIP(hipEventRecord(e.pipe_score_ev[b], e.stream));
+  e.pipe_score_live[b] = true;
   FD_API_END
 }
 

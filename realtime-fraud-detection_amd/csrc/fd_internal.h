@@ -190,7 +190,7 @@ struct CardStore {
   DeviceBuffer headers, ring, merchants, slot, err, seq;
   // per-batch card grouping (feat_slot -> feat_bucket): keys per bucket, [NB][C] bucket regions, overflow
   // counters by batch parity + the overflow list (key, bucket), prep records
-  DeviceBuffer bucket_fill, pairs, ovf_cnt, ovf_key, ovf_b, prep;
+  DeviceBuffer bucket_fill, pairs, ovf_cnt, ovf_key, ovf_b, prep, defer;
   int batch_parity = 0;
   DeviceBuffer uext, mext, vocab;  // extended profiles + vocabulary flags (feature map, rule scores)
   int64_t n_mext = 0;
@@ -251,6 +251,15 @@ struct Engine {
   hipEvent_t join2_ev = nullptr;
   DeviceBuffer seq_buf;                        // per-txn LSTM input sequences of the fused path
   DeviceBuffer feat_vec, feat_in, feat_ext;  // host-API / fused-pipeline staging for features
+  // fd_score_batch_pipelined: features on feat_stream (batch i+1's overlap batch i's forests on `stream`),
+  // scoring vectors / LSTM sequences double-buffered by batch parity
+  hipStream_t feat_stream = nullptr;
+  hipEvent_t pipe_feat_ev = nullptr, pipe_entry_ev = nullptr, pipe_score_ev[2] = {nullptr, nullptr};
+  bool pipe_score_live[2] = {false, false};
+  bool pipe_dirty = true;  // another engine call since the last pipelined one: order after `stream` first
+  int pipe_parity = 0;
+  bool pipe_lean = true;  // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
+  DeviceBuffer pipe_vec[2], pipe_seq[2];
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
@@ -328,7 +337,8 @@ int64_t state_count(Engine& e);
 void load_users(Engine& e, const fd_users& u);
 void load_merchants(Engine& e, const fd_merchants& m);
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw,
-                     float* d_seq = nullptr, double* d_vel5 = nullptr);
+                     float* d_seq = nullptr, double* d_vel5 = nullptr, hipStream_t stream = nullptr,
+                     bool lean = false);
 // the same over received 48-B route records (route.hip), no unpack pass; also returns nothing else
 void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq);
 void load_users_ext(Engine& e, const fd_users_ext& u);

@@ -201,6 +201,28 @@ class FraudEngine:
         N.call("fd_score_batch_device", self._h, C.byref(params), _ptr(sl), ext, _ptr(pres), C.byref(b), int(n),
                opt(vec_ptr), opt(model_probs_ptr), C.c_void_p(fp_ptr), opt(conf_ptr), opt(dec_ptr), opt(risk_ptr))
 
+    def score_batch_pipelined(self, params: N.fd_blend_params, slots: Sequence[int], txn_ptrs: dict, n: int,
+                              fp_ptr: int, conf_ptr: int = 0, dec_ptr: int = 0, risk_ptr: int = 0,
+                              model_probs_ptr: int = 0, ext_ptrs: Optional[Sequence[Optional[int]]] = None,
+                              present: Optional[Sequence[int]] = None, input_ready: int = 0) -> None:
+        """Streaming form of score_batch_device (fd_score_batch_pipelined): the batch's features run on the
+        engine's feature stream, overlapping the previous batch's forests; outputs are ordered on the engine
+        stream as with score_batch_device. input_ready: a hipEvent_t handle (e.g. torch.cuda.Event's
+        cuda_event) recorded when the input columns were complete; 0 = complete before this call. The input
+        columns must stay unchanged until the outputs are complete."""
+        M = params.n_models
+        sl = np.array(list(slots) + [-1] * (N.FD_MAX_MODELS - len(slots)), np.int32)
+        pres = np.array([1] * M if present is None else list(present), np.uint8)
+        ext = (C.c_void_p * N.FD_MAX_MODELS)()
+        if ext_ptrs:
+            for i, p in enumerate(ext_ptrs):
+                ext[i] = p if p else None
+        b = N.fd_txn_batch(*[int(txn_ptrs[f]) for f in N.TXN_FIELDS])
+        opt = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        N.call("fd_score_batch_pipelined", self._h, C.byref(params), _ptr(sl), ext, _ptr(pres), C.byref(b),
+               int(n), opt(model_probs_ptr), C.c_void_p(fp_ptr), opt(conf_ptr), opt(dec_ptr), opt(risk_ptr),
+               opt(input_ready))
+
     def features_seq_device(self, ptrs: dict, n: int, vec_ptr: int, seq_ptr: int, raw_ptr: int = 0) -> None:
         """features_device plus each transaction's LSTM input sequence (n x seq_len x 16 f32)."""
         b = N.fd_txn_batch(*[int(ptrs[f]) for f in N.TXN_FIELDS])

@@ -53,10 +53,14 @@ class EngineShardBackend:
     """Steps 1, 4 and 6 on one GPU through the C-ABI (device tensors in, device tensors out)."""
 
     def __init__(self, eng: FraudEngine, params: N.fd_blend_params, slots: Sequence[int],
-                 present: Optional[Sequence[int]] = None):
+                 present: Optional[Sequence[int]] = None, pipelined: bool = False):
+        """pipelined: one shard scores through fd_score_batch_pipelined (batch i+1's features overlap batch i's
+        forests). The caller then guarantees each step's input tensors are complete when step() is called
+        (resident in HBM, or pass `input_ready` to score_batch) and unchanged until its outputs are."""
         import torch
         self.torch = torch
         self.eng, self.params, self.slots, self.present = eng, params, list(slots), present
+        self.pipelined = pipelined
         self.device = torch.device("cuda", eng.device)
         # The engine's kernels and the collectives must be ordered on ONE stream: bind the engine to the
         # stream torch (and so RCCL's all_to_all and .cpu()) uses on this device.
@@ -119,17 +123,24 @@ class EngineShardBackend:
             self.eng.score_records_device(self.params, self.slots, rec.data_ptr(), m, res.data_ptr(), self.present)
         return res
 
-    def score_batch(self, txns: dict, n: int):
-        """One shard: the whole hot path on the ingest GPU in arrival order (nothing to route)."""
+    def score_batch(self, txns: dict, n: int, input_ready=None):
+        """One shard: the whole hot path on the ingest GPU in arrival order (nothing to route).
+        input_ready: optional torch.cuda.Event recorded once the input tensors were complete (pipelined)."""
         t = self.torch
         fp = t.empty(n, dtype=t.float64, device=self.device)
         conf = t.empty(n, dtype=t.float64, device=self.device)
         dec = t.empty(n, dtype=t.uint8, device=self.device)
         risk = t.empty(n, dtype=t.uint8, device=self.device)
         if n:
-            self.eng.score_batch_device(self.params, self.slots, {f: txns[f].data_ptr() for f in N.TXN_FIELDS}, n,
-                                        fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
-                                        present=self.present)
+            ptrs = {f: txns[f].data_ptr() for f in N.TXN_FIELDS}
+            if self.pipelined:
+                self.eng.score_batch_pipelined(self.params, self.slots, ptrs, n, fp.data_ptr(), conf.data_ptr(),
+                                               dec.data_ptr(), risk.data_ptr(), present=self.present,
+                                               input_ready=input_ready.cuda_event if input_ready is not None
+                                               else 0)
+            else:
+                self.eng.score_batch_device(self.params, self.slots, ptrs, n, fp.data_ptr(), conf.data_ptr(),
+                                            dec.data_ptr(), risk.data_ptr(), present=self.present)
         return fp, conf, dec, risk
 
     def snapshot(self, path: str, rank: int, world: int) -> int:

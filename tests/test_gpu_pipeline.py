@@ -1,0 +1,129 @@
+"""fd_score_batch_pipelined (the streaming form of fd_score_batch_device: batch i+1's features on the engine's
+feature stream overlap batch i's forests) against fd_score_batch_device on a twin engine with the same state:
+every batch's outputs bit-identical, the card state after the stream identical (the next batch's vectors), with
+other engine calls interleaved and with inputs that arrive on a side stream behind an `input_ready` event.
+Reference chain: FeatureExtractor -> RedisTransactionSink -> FeatureProcessor -> EnsemblePredictor.predict
+(fl/features/FeatureExtractor.java:50-87, ml/models/ensemble_predictor.py:75-148), one micro-batch at a time."""
+import numpy as np
+import pytest
+
+from fdengine import FraudEngine, iforest_from_sklearn, synth, xgboost_from_json_doc
+from fdengine._native import TXN_FIELDS
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(pop, xgb, ifm, K=16):
+    U, M = pop["users"], pop["merchants"]
+    eng = FraudEngine(0)
+    eng.state_init(1 << 17, 1, K)
+    eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+    eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+    eng.load_forest(0, xgb)
+    eng.load_forest(1, ifm)
+    return eng
+
+
+def _params():
+    from oracle import scoring_ref as S
+    names = ["xgboost_primary", "isolation_forest"]
+    w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
+    return FraudEngine.blend_params([w[k] for k in names], [S.CONF_MULT[k] for k in names])
+
+
+def _outs(n):
+    import torch
+    return [torch.empty(n, dtype=t, device="cuda") for t in (torch.float64, torch.float64, torch.uint8, torch.uint8)]
+
+
+@pytest.fixture(scope="module")
+def world():
+    pop = synth.population(20000, 5000, seed=7)
+    tx = synth.txn_stream(pop, 300_000, seed=8)
+    warm = FraudEngine(0)
+    try:
+        U, M = pop["users"], pop["merchants"]
+        warm.state_init(1 << 17, 1, 16)
+        warm.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        warm.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        X = warm.features({k: v[:16384] for k, v in tx.items()})
+    finally:
+        warm.close()
+    xgb = xgboost_from_json_doc(synth.xgboost_doc(200, 8, 64, X[-8192:], seed=3))
+    ifm = iforest_from_sklearn(synth.isolation_forest(X[-8192:].astype(np.float64), n_estimators=60))
+    return pop, tx, xgb, ifm
+
+
+def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1):
+    import torch
+    pop, tx, xgb, ifm = world
+    params = _params()
+    cols = {f: np.array(tx[f][:cuts[-1]]) for f in TXN_FIELDS}
+    if hot:  # batch 1: one card with 2,000 transactions (an oversized bucket), one with 30 (a long segment)
+        k = cols["card_key"]
+        k[cuts[1]:cuts[2]:20] = k[cuts[1]]
+        k[cuts[1] + 7:cuts[1] + 7 + 30 * 97:97] = k[cuts[1] + 7]
+    dev = {f: torch.from_numpy(np.ascontiguousarray(cols[f])).cuda() for f in TXN_FIELDS}
+    torch.cuda.synchronize()
+    ref, pip = _setup(pop, xgb, ifm), _setup(pop, xgb, ifm)
+    pip.set_option("pipeline_lean", lean)
+    try:
+        for e in (ref, pip):
+            e.set_stream(torch.cuda.current_stream().cuda_stream)
+        got, want = [], []
+        side = torch.cuda.Stream() if side_stream else None
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            n = b - a
+            part = {f: t[a:b] for f, t in dev.items()}
+            o_ref = _outs(n)
+            ref.score_batch_device(params, [0, 1], {f: t.data_ptr() for f, t in part.items()}, n,
+                                   *[o.data_ptr() for o in o_ref])
+            ev = None
+            if side is not None:  # inputs produced on another stream: a fresh copy behind an event
+                with torch.cuda.stream(side):
+                    part = {f: t.clone() for f, t in part.items()}
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+            o_pip = _outs(n)
+            pip.score_batch_pipelined(params, [0, 1], {f: t.data_ptr() for f, t in part.items()}, n,
+                                      *[o.data_ptr() for o in o_pip], input_ready=ev.cuda_event if ev else 0)
+            if side is not None:
+                for t in part.values():
+                    t.record_stream(torch.cuda.current_stream())
+            if interleave and a == cuts[1]:  # another engine call between two pipelined batches
+                for e in (ref, pip):
+                    e.load_merchants(pop["merchants"]["fraud_rate"], pop["merchants"]["risk_multiplier"])
+            got.append(o_pip)
+            want.append(o_ref)
+        torch.cuda.synchronize()
+        for g, w in zip(got, want):
+            for x, y in zip(g, w):
+                np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+        # the card state both engines end with: the next batch's vectors
+        nxt = {k: v[cuts[-1]:cuts[-1] + 4096] for k, v in tx.items()}
+        np.testing.assert_array_equal(pip.features(nxt), ref.features(nxt))
+    finally:
+        ref.close()
+        pip.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("lean", [1, 0])
+def test_pipelined_stream_matches_serial(world, lean):
+    _run(world, [0, 40000, 80000, 81000, 121000, 161000, 201000], lean=lean)
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_hot_cards_deferred_buckets(world):
+    """buckets the lean kernel cannot take (> 512 keys, a segment > 16) go to the deferred launch"""
+    _run(world, [0, 40000, 80000, 120000], hot=True)
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_with_interleaved_calls(world):
+    _run(world, [0, 40000, 80000, 120000], interleave=True)
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_input_ready_event(world):
+    _run(world, [0, 40000, 80000, 120000, 160000], side_stream=True)
