@@ -897,6 +897,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         wl.step(i)
+    t_sub = time.perf_counter()  # host submission done (the GPU may still be working through the queue)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -938,6 +939,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "host_submit_ms_per_step": round((t_sub - t0) / args.steps * 1e3, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -70,6 +70,10 @@ static Engine& E_quiet(fd_engine* p) {
   return p->e;
 }
 
+// Events that only order one device's streams: no system-scope release at record (that is an L2 writeback
+// per record, several us of stream time between a kernel and its cross-stream dependents)
+constexpr unsigned kStreamEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
+
 static fd::PackedForest& slot_of(Engine& e, int slot) {
   FD_REQUIRE(slot >= 0 && slot < fd::kMaxSlots, FD_ERR_INVALID_ARG, "slot out of range");
   return e.forests[slot];
@@ -104,8 +108,8 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
                "the LSTM head needs card-history sequences (fd_score_batch_device with seq_len > 0)");
     if (!e.aux_stream) {
       FD_HIP(hipStreamCreateWithFlags(&e.aux_stream, hipStreamNonBlocking));
-      FD_HIP(hipEventCreateWithFlags(&e.fork_ev, hipEventDisableTiming));
-      FD_HIP(hipEventCreateWithFlags(&e.join_ev, hipEventDisableTiming));
+      FD_HIP(hipEventCreateWithFlags(&e.fork_ev, kStreamEventFlags));
+      FD_HIP(hipEventCreateWithFlags(&e.join_ev, kStreamEventFlags));
     }
     FD_HIP(hipEventRecord(e.fork_ev, e.stream));
     FD_HIP(hipStreamWaitEvent(e.aux_stream, e.fork_ev, 0));
@@ -123,8 +127,8 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
   if (small) {
     if (!e.aux2_stream) {
       FD_HIP(hipStreamCreateWithFlags(&e.aux2_stream, hipStreamNonBlocking));
-      FD_HIP(hipEventCreateWithFlags(&e.join2_ev, hipEventDisableTiming));
-      if (!e.fork_ev) FD_HIP(hipEventCreateWithFlags(&e.fork_ev, hipEventDisableTiming));
+      FD_HIP(hipEventCreateWithFlags(&e.join2_ev, kStreamEventFlags));
+      if (!e.fork_ev) FD_HIP(hipEventCreateWithFlags(&e.fork_ev, kStreamEventFlags));
     }
     FD_HIP(hipEventRecord(e.fork_ev, e.stream));
     FD_HIP(hipStreamWaitEvent(e.aux2_stream, e.fork_ev, 0));
@@ -264,7 +268,7 @@ int fd_engine_destroy(fd_engine* eng) {
   }
   for (auto* b : {&e.state.headers, &e.state.ring, &e.state.merchants, &e.state.slot, &e.state.err,
                   &e.state.bucket_fill, &e.state.pairs, &e.state.ovf_cnt, &e.state.ovf_key, &e.state.ovf_b, &e.state.prep,
-                  &e.state.defer})
+                  &e.state.bucket_scr})
     b->release();
   for (auto& ev : e.events) {
     (void)hipEventDestroy(ev.a);
@@ -733,7 +737,7 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
   if (!e.feat_stream) {
     FD_HIP(hipStreamCreateWithFlags(&e.feat_stream, hipStreamNonBlocking));
     for (hipEvent_t* ev : {&e.pipe_feat_ev, &e.pipe_entry_ev, &e.pipe_score_ev[0], &e.pipe_score_ev[1]})
-      FD_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+      FD_HIP(hipEventCreateWithFlags(ev, kStreamEventFlags));
   }
   hipStream_t F = e.feat_stream;
   if (e.pipe_dirty) {  // work queued on e.stream by other calls (state loads, snapshots, ...) comes first

@@ -190,7 +190,8 @@ struct CardStore {
   DeviceBuffer headers, ring, merchants, slot, err, seq;
   // per-batch card grouping (feat_slot -> feat_bucket): keys per bucket, [NB][C] bucket regions, overflow
   // counters by batch parity + the overflow list (key, bucket), prep records
-  DeviceBuffer bucket_fill, pairs, ovf_cnt, ovf_key, ovf_b, prep, defer;
+  DeviceBuffer bucket_fill, pairs, ovf_cnt, ovf_key, ovf_b, prep,
+      bucket_scr;  // lean bucket kernel: per-bucket global working set of its slow path
   int batch_parity = 0;
   DeviceBuffer uext, mext, vocab;  // extended profiles + vocabulary flags (feature map, rule scores)
   int64_t n_mext = 0;

@@ -651,8 +651,6 @@ struct BucketArgs {
   int par;
   const unsigned long long* ovf_key;  // overflow list: key, bucket
   const unsigned* ovf_b;
-  const unsigned* defer;              // deferred buckets (lean + deferred form), nullptr: one bucket per block
-  unsigned* defer_cnt;                // [2] deferred counts by batch parity
 };
 
 template <int MODE>
@@ -1119,64 +1117,57 @@ __device__ void bucket_body(const BucketArgs& a, const int b, unsigned long long
     a.fill[b] = 0u;
     if (b == 0) a.ovf_cnt[a.par ^ 1] = 0u;  // the next batch's overflow list (this batch's is reset by the next)
   }
-  __syncthreads();  // the keys in LDS are the next bucket's (deferred form)
 }
 
-// One workgroup per bucket; deferred form (a.defer != nullptr): the buckets feat_bucket_lean_kernel left, a
-// workgroup per list entry (grid-strided over the count the lean launch wrote).
+// One workgroup per bucket
 template <int MODE>
 __global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long skeys[];  // kChunkCap keys | kMaxBins + 1 bins
   __shared__ LongLds sm;
   __shared__ int long_list[kChunkCap / (kSegLong + 1) + 1];
   __shared__ int n_long, chunk_m;
-  if (a.defer == nullptr) {
-    bucket_body<MODE>(a, blockIdx.x, skeys, sm, long_list, n_long, chunk_m);
-    return;
-  }
-  const unsigned cnt = a.defer_cnt[a.par];
-  for (unsigned q = blockIdx.x; q < cnt; q += gridDim.x) bucket_body<MODE>(a, (int)a.defer[q], skeys, sm, long_list, n_long, chunk_m);
+  bucket_body<MODE>(a, blockIdx.x, skeys, sm, long_list, n_long, chunk_m);
 }
 
-// Lean form of the bucket kernel for the pipelined stream (fd_score_batch_pipelined): ~4.5 KiB of LDS and no
-// cooperative path, so its workgroups fit beside a running ensemble_kernel workgroup (148 KiB of the CU's 160)
-// and batch i+1's card work overlaps batch i's forests. It takes the common bucket — at most kLeanCap keys,
-// none in the overflow list, every card segment short — and defers any other bucket, untouched, to
-// feat_bucket_kernel (deferred form) through a list; buckets hold disjoint cards, so the split keeps every
-// card's arrival order.
+// The bucket kernel's LDS working set, in global memory (one per bucket) for the lean kernel's slow path
+struct BucketScratch {
+  unsigned long long keys[kChunkCap + (kMaxBins + 1 + 1) / 2];  // keys | bin prefix sums (kBucketLds)
+  LongLds sm;
+  int long_list[kChunkCap / (kSegLong + 1) + 1];
+  int n_long, chunk_m;
+};
+
+// Lean form of the bucket kernel for the pipelined stream (fd_score_batch_pipelined): 4 KiB of LDS, so its
+// workgroups fit beside a running ensemble_kernel workgroup (148 KiB of the CU's 160) and batch i+1's card work
+// overlaps batch i's forests. The common bucket — at most kLeanCap keys, none in the overflow list, every card
+// segment short — is sorted and walked in LDS; any other bucket (a hot card) takes the full bucket kernel's
+// code with its working set in a per-bucket global scratch block (L1/L2-resident; same results, no launch
+// that would have to wait for a whole CU).
 constexpr int kLeanCap = 512;
-constexpr int kDeferGrid = 32;  // workgroups of the deferred launch
 template <int MODE>
-__global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a) {
+__global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, BucketScratch* scratch) {
   __shared__ __attribute__((aligned(16))) unsigned long long skeys[kLeanCap];
   __shared__ int any_long;
   const int b = blockIdx.x;
   const unsigned m = a.fill[b];
-  unsigned* defer = const_cast<unsigned*>(a.defer);
-  unsigned* defer_cnt = a.defer_cnt + a.par;
-  if (threadIdx.x == 0) {
-    any_long = 0;
-    if (b == 0) {  // the next batch's overflow list and deferred count
-      a.ovf_cnt[a.par ^ 1] = 0u;
-      a.defer_cnt[a.par ^ 1] = 0u;
+  if (threadIdx.x == 0) any_long = 0;
+  bool slow = m > (unsigned)kLeanCap || m > a.C;
+  if (!slow) {
+    const unsigned long long* src = a.pairs + (size_t)b * a.C;
+    for (unsigned q = threadIdx.x; q < m; q += kBT) skeys[q] = src[q];
+    __syncthreads();
+    if (m > 1) rank_sort(skeys, (int)m);
+    for (int pos = threadIdx.x; pos < (int)m; pos += kBT) {
+      const unsigned s = (unsigned)(skeys[pos] >> 32);
+      if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;
+      if (pos + kSegLong < (int)m && (unsigned)(skeys[pos + kSegLong] >> 32) == s) any_long = 1;
     }
+    __syncthreads();
+    slow = any_long != 0;
   }
-  if (m > (unsigned)kLeanCap || m > a.C) {
-    if (threadIdx.x == 0) defer[atomicAdd(defer_cnt, 1u)] = (unsigned)b;
-    return;
-  }
-  const unsigned long long* src = a.pairs + (size_t)b * a.C;
-  for (unsigned q = threadIdx.x; q < m; q += kBT) skeys[q] = src[q];
-  __syncthreads();
-  if (m > 1) rank_sort(skeys, (int)m);
-  for (int pos = threadIdx.x; pos < (int)m; pos += kBT) {
-    const unsigned s = (unsigned)(skeys[pos] >> 32);
-    if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;
-    if (pos + kSegLong < (int)m && (unsigned)(skeys[pos + kSegLong] >> 32) == s) any_long = 1;
-  }
-  __syncthreads();
-  if (any_long) {
-    if (threadIdx.x == 0) defer[atomicAdd(defer_cnt, 1u)] = (unsigned)b;
+  if (slow) {
+    BucketScratch& w = scratch[b];
+    bucket_body<MODE>(a, b, w.keys, w.sm, w.long_list, w.n_long, w.chunk_m);
     return;
   }
   for (int pos = threadIdx.x; pos < (int)m; pos += kBT) {
@@ -1186,7 +1177,10 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a) {
     while (pos + len < (int)m && (unsigned)(skeys[pos + len] >> 32) == s) ++len;
     process_short<MODE>(a, s, skeys + pos, len);
   }
-  if (threadIdx.x == 0) a.fill[b] = 0u;  // the next batch's counter (it runs after this launch on the stream)
+  if (threadIdx.x == 0) {  // the next batch's counters (it runs after this launch on the stream)
+    a.fill[b] = 0u;
+    if (b == 0) a.ovf_cnt[a.par ^ 1] = 0u;
+  }
 }
 
 __global__ void __launch_bounds__(256) count_cards_kernel(const CardHeader* H, int64_t cap,
@@ -1583,8 +1577,7 @@ void state_init(Engine& e, const fd_state_params& p) {
   st.uext.release();
   st.err.ensure(16);
   st.bucket_fill.ensure(kMaxBuckets * sizeof(unsigned));
-  st.ovf_cnt.ensure(4 * sizeof(unsigned));  // [2] overflow counts | [2] deferred-bucket counts, by parity
-  st.defer.ensure(kMaxBuckets * sizeof(unsigned));
+  st.ovf_cnt.ensure(2 * sizeof(unsigned));
   st.ready = true;
   state_clear(e);
 }
@@ -1596,7 +1589,7 @@ void state_clear(Engine& e) {
   if (st.uext.ptr) FD_HIP(hipMemsetAsync(st.uext.ptr, 0, (size_t)st.cap * sizeof(UserExt), e.stream));
   FD_HIP(hipMemsetAsync(st.err.ptr, 0, 16, e.stream));
   FD_HIP(hipMemsetAsync(st.bucket_fill.ptr, 0, kMaxBuckets * sizeof(unsigned), e.stream));
-  FD_HIP(hipMemsetAsync(st.ovf_cnt.ptr, 0, 4 * sizeof(unsigned), e.stream));
+  FD_HIP(hipMemsetAsync(st.ovf_cnt.ptr, 0, 2 * sizeof(unsigned), e.stream));
   FD_HIP(hipStreamSynchronize(e.stream));
   // the window event logs hold card-table slots: clearing the table empties them too
   WindowState& w = e.windows;
@@ -1668,7 +1661,7 @@ void load_merchants(Engine& e, const fd_merchants& m) {
 namespace {
 
 // The grouping launch (feat_slot) + the bucket kernel over any transaction source.
-// lean: the pipelined stream's bucket pass (feat_bucket_lean_kernel + the deferred form of feat_bucket_kernel)
+// lean: the pipelined stream's bucket pass (feat_bucket_lean_kernel: fits beside the ensemble kernel)
 void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, double* d_raw, float* d_seq,
                     double* d_vel5, hipStream_t stream = nullptr, bool lean = false) {
   CardStore& st = e.state;
@@ -1718,21 +1711,18 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.ovf_key = st.ovf_key.as<const unsigned long long>();
   a.ovf_b = st.ovf_b.as<const unsigned>();
   const size_t lds = kBucketLds;
-  unsigned grid = nb;
   if (lean) {
-    a.defer = st.defer.as<const unsigned>();
-    a.defer_cnt = st.ovf_cnt.as<unsigned>() + 2;
+    st.bucket_scr.ensure((size_t)nb * sizeof(BucketScratch));
+    BucketScratch* scr = st.bucket_scr.as<BucketScratch>();
     if (st.mode == FD_WINDOW_SLIDING)
-      hipLaunchKernelGGL(feat_bucket_lean_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), 0, s, a);
+      hipLaunchKernelGGL(feat_bucket_lean_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), 0, s, a, scr);
     else
-      hipLaunchKernelGGL(feat_bucket_lean_kernel<FD_WINDOW_REDIS_COMPAT>, dim3(nb), dim3(kBT), 0, s, a);
-    FD_HIP(hipGetLastError());
-    grid = std::min(nb, (unsigned)kDeferGrid);  // usually nothing deferred: these workgroups exit at once
+      hipLaunchKernelGGL(feat_bucket_lean_kernel<FD_WINDOW_REDIS_COMPAT>, dim3(nb), dim3(kBT), 0, s, a, scr);
+  } else if (st.mode == FD_WINDOW_SLIDING) {
+    hipLaunchKernelGGL(feat_bucket_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), lds, s, a);
+  } else {
+    hipLaunchKernelGGL(feat_bucket_kernel<FD_WINDOW_REDIS_COMPAT>, dim3(nb), dim3(kBT), lds, s, a);
   }
-  if (st.mode == FD_WINDOW_SLIDING)
-    hipLaunchKernelGGL(feat_bucket_kernel<FD_WINDOW_SLIDING>, dim3(grid), dim3(kBT), lds, s, a);
-  else
-    hipLaunchKernelGGL(feat_bucket_kernel<FD_WINDOW_REDIS_COMPAT>, dim3(grid), dim3(kBT), lds, s, a);
   FD_HIP(hipGetLastError());
   if (ev) FD_HIP(hipEventRecord(ev->b, s));
 }

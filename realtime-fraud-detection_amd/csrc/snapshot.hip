@@ -235,6 +235,53 @@ void read_all(FILE* f, void* p, size_t bytes, Fnv* h) {
   if (h) h->add(p, bytes);
 }
 
+// Checksum pass over the whole image before anything is restored: a truncated or corrupt file (a partial copy
+// during a re-shard) fails here with the engine's state untouched. Leaves the file at the first section.
+void verify_image(FILE* f, const SnapHeader& hd, size_t rec_bytes) {
+  const long start = std::ftell(f);
+  std::vector<char> buf(1 << 20);
+  auto section = [&](size_t bytes, Fnv* h) {
+    for (size_t off = 0; off < bytes;) {
+      const size_t b = std::min(bytes - off, buf.size());
+      read_all(f, buf.data(), b, h);
+      off += b;
+    }
+  };
+  Fnv hc, hm, hx, hv, hu, hl;
+  section((size_t)hd.n_cards * rec_bytes, &hc);
+  section((size_t)hd.n_merchants * kMerchantBytes, &hm);
+  section((size_t)hd.n_mext * kMerchExtBytes, &hx);
+  if (hd.vocab_loaded) section(kVocabBytes, &hv);
+  section((size_t)hd.ucount * kWinEventBytes, &hu);
+  section((size_t)hd.mcount * kWinEventBytes, &hl);
+  FD_REQUIRE(hc.h == hd.checksum[0], FD_ERR_IO, "restore: card section checksum mismatch (nothing restored)");
+  FD_REQUIRE(hm.h == hd.checksum[1] && hx.h == hd.checksum[2] && hv.h == hd.checksum[3], FD_ERR_IO,
+             "restore: table section checksum mismatch (nothing restored)");
+  FD_REQUIRE(hu.h == hd.checksum[4] && hl.h == hd.checksum[5], FD_ERR_IO,
+             "restore: window log checksum mismatch (nothing restored)");
+  if (hd.ext_flags) {
+    Fnv he;
+    if (hd.ext_flags & 1) {
+      int64_t meta[4];
+      read_all(f, meta, sizeof meta, &he);
+      FD_REQUIRE(meta[0] > 0 && meta[1] > 0 && meta[0] < (1ll << 40) && meta[1] < (1ll << 40), FD_ERR_IO,
+                 "restore: corrupt sink section");
+      section((size_t)meta[0] * kSinkEntryBytes + (size_t)meta[1] * kSinkUserBytes, &he);
+    }
+    if (hd.ext_flags & 2) {
+      int64_t meta[4];
+      read_all(f, meta, sizeof meta, &he);
+      for (int t = 0; t < 4; ++t) {
+        FD_REQUIRE(meta[t] >= 0 && meta[t] < (1ll << 40), FD_ERR_IO, "restore: corrupt ingest section");
+        section((size_t)meta[t] * 8, &he);
+        section((size_t)meta[t] * 4, &he);
+      }
+    }
+    FD_REQUIRE(he.h == hd.ext_checksum, FD_ERR_IO, "restore: extension section checksum mismatch (nothing restored)");
+  }
+  FD_REQUIRE(std::fseek(f, start, SEEK_SET) == 0, FD_ERR_IO, "restore: cannot rewind the snapshot");
+}
+
 Planes planes_of(CardStore& st) {
   return Planes{st.headers.as<uint4>(), st.ring.as<uint4>(),
                 st.seq.ptr ? st.seq.as<uint4>() : nullptr, st.uext.ptr ? st.uext.as<uint4>() : nullptr};
@@ -406,6 +453,7 @@ void state_restore(Engine& e, const char* path, int shard, int n_shards, int fla
     FD_REQUIRE(w.ucount + hd.ucount <= w.cap && w.mcount + hd.mcount <= w.cap, FD_ERR_OOM,
                "restore: window event log too small (fd_window_params.log_capacity)");
   }
+  verify_image(in.f, hd, (size_t)m.words * 16);
   FD_HIP(hipStreamSynchronize(e.stream));
   if (m.uext && !st.uext.ptr) {
     st.uext.ensure((size_t)st.cap * kUextWords * 16);

@@ -223,6 +223,12 @@ class FraudEngine:
                int(n), opt(model_probs_ptr), C.c_void_p(fp_ptr), opt(conf_ptr), opt(dec_ptr), opt(risk_ptr),
                opt(input_ready))
 
+    def pipelined_scorer(self, params: N.fd_blend_params, slots: Sequence[int],
+                         present: Optional[Sequence[int]] = None) -> "PipelinedScorer":
+        """A prepared score_batch_pipelined for a fixed model set: per call only the batch's pointers change
+        (the per-step host cost stays well below the GPU step)."""
+        return PipelinedScorer(self, params, slots, present)
+
     def features_seq_device(self, ptrs: dict, n: int, vec_ptr: int, seq_ptr: int, raw_ptr: int = 0) -> None:
         """features_device plus each transaction's LSTM input sequence (n x seq_len x 16 f32)."""
         b = N.fd_txn_batch(*[int(ptrs[f]) for f in N.TXN_FIELDS])
@@ -596,3 +602,28 @@ def merge_merchant_windows(parts) -> np.ndarray:
     m = C.c_int64()
     N.call("fd_merchant_windows_merge", a.ctypes.data if len(a) else None, len(a), out.ctypes.data, C.byref(m))
     return out[:m.value].copy()
+
+
+class PipelinedScorer:
+    """fd_score_batch_pipelined with its model arguments marshalled once (FraudEngine.pipelined_scorer)."""
+
+    def __init__(self, eng: FraudEngine, params: N.fd_blend_params, slots: Sequence[int],
+                 present: Optional[Sequence[int]] = None):
+        M = params.n_models
+        self.eng = eng
+        self.params = params
+        self._sl = np.array(list(slots) + [-1] * (N.FD_MAX_MODELS - len(slots)), np.int32)
+        self._pres = np.array([1] * M if present is None else list(present), np.uint8)
+        self._ext = (C.c_void_p * N.FD_MAX_MODELS)()
+        self._batch = N.fd_txn_batch()
+        self._fn = N.lib.fd_score_batch_pipelined
+        self._args = [C.byref(params), _ptr(self._sl), self._ext, _ptr(self._pres), C.byref(self._batch)]
+
+    def __call__(self, txn_ptrs: dict, n: int, fp_ptr: int, conf_ptr: int = 0, dec_ptr: int = 0, risk_ptr: int = 0,
+                 input_ready: int = 0) -> None:
+        b = self._batch
+        for f in N.TXN_FIELDS:
+            setattr(b, f, txn_ptrs[f])
+        rc = self._fn(self.eng._h, *self._args, int(n), None, fp_ptr, conf_ptr or None, dec_ptr or None,
+                      risk_ptr or None, input_ready or None)
+        N.check(rc, "fd_score_batch_pipelined")

@@ -61,6 +61,7 @@ class EngineShardBackend:
         self.torch = torch
         self.eng, self.params, self.slots, self.present = eng, params, list(slots), present
         self.pipelined = pipelined
+        self._scorer = None
         self.device = torch.device("cuda", eng.device)
         # The engine's kernels and the collectives must be ordered on ONE stream: bind the engine to the
         # stream torch (and so RCCL's all_to_all and .cpu()) uses on this device.
@@ -134,10 +135,10 @@ class EngineShardBackend:
         if n:
             ptrs = {f: txns[f].data_ptr() for f in N.TXN_FIELDS}
             if self.pipelined:
-                self.eng.score_batch_pipelined(self.params, self.slots, ptrs, n, fp.data_ptr(), conf.data_ptr(),
-                                               dec.data_ptr(), risk.data_ptr(), present=self.present,
-                                               input_ready=input_ready.cuda_event if input_ready is not None
-                                               else 0)
+                if self._scorer is None:
+                    self._scorer = self.eng.pipelined_scorer(self.params, self.slots, self.present)
+                self._scorer(ptrs, n, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
+                             input_ready.cuda_event if input_ready is not None else 0)
             else:
                 self.eng.score_batch_device(self.params, self.slots, ptrs, n, fp.data_ptr(), conf.data_ptr(),
                                             dec.data_ptr(), risk.data_ptr(), present=self.present)

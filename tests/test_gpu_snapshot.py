@@ -225,6 +225,13 @@ def test_image_deterministic_and_corruption_detected(engine, tmp_path):
         with pytest.raises(NativeError, match="checksum") as ei:
             fresh.state_restore(tmp_path / "bad.fdsnap")
         assert ei.value.code == FD_ERR_IO
+        assert fresh.state_info()["cards"] == 0  # verified before anything is restored
+        bad = bytearray(blob)
+        bad[len(blob) - 24] ^= 0x01  # a byte in the last section (window logs)
+        (tmp_path / "bad2.fdsnap").write_bytes(bytes(bad))
+        with pytest.raises(NativeError, match="checksum"):
+            fresh.state_restore(tmp_path / "bad2.fdsnap")
+        assert fresh.state_info()["cards"] == 0
         (tmp_path / "short.fdsnap").write_bytes(blob[: len(blob) // 2])
         fresh.state_clear()
         with pytest.raises(NativeError, match="truncated"):
