@@ -949,6 +949,8 @@ def main():
             "config": wl.config(world),
             "p50_batch_latency_ms": round(float(np.percentile(lat_ms, 50)), 4),
             "p99_batch_latency_ms": round(p99, 4),
+            "max_batch_latency_ms": round(float(lat_ms.max()), 4),
+            "latency_samples": len(lat),
             "roofline": roof,
             "kernel_avg_us": wl.kernels(timing),
             "kernel_timing": f"HIP events on the launch stream, 1 launch in {TIMING_EVERY} of each kernel, timed region",

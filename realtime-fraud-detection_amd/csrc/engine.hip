@@ -248,10 +248,12 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipStreamDestroy(e.aux2_stream);
     (void)hipEventDestroy(e.join2_ev);
   }
-  if (e.feat_stream) {
-    (void)hipStreamSynchronize(e.feat_stream);
-    (void)hipStreamDestroy(e.feat_stream);
-    for (hipEvent_t ev : {e.pipe_feat_ev, e.pipe_entry_ev, e.pipe_score_ev[0], e.pipe_score_ev[1]})
+  if (e.pipe_stream[0]) {
+    for (hipStream_t st : e.pipe_stream) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
+    for (hipEvent_t ev : {e.pipe_feat_ev, e.pipe_entry_ev, e.pipe_done_ev[0], e.pipe_done_ev[1]})
       (void)hipEventDestroy(ev);
   }
   for (auto* b : {&e.pipe_vec[0], &e.pipe_vec[1], &e.pipe_seq[0], &e.pipe_seq[1]}) b->release();
@@ -297,7 +299,8 @@ int fd_engine_sync(fd_engine* eng) {
   FD_API_BEGIN
   Engine& e = E(eng);
   FD_HIP(hipStreamSynchronize(e.stream));
-  if (e.feat_stream) FD_HIP(hipStreamSynchronize(e.feat_stream));
+  for (hipStream_t st : e.pipe_stream)
+    if (st) FD_HIP(hipStreamSynchronize(st));
   if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
   if (e.aux2_stream) FD_HIP(hipStreamSynchronize(e.aux2_stream));
   fd::route_check(e);
@@ -734,21 +737,28 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
   Engine& e = E_quiet(eng);
   FD_REQUIRE(params && txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   if (n == 0) return FD_OK;
-  if (!e.feat_stream) {
-    FD_HIP(hipStreamCreateWithFlags(&e.feat_stream, hipStreamNonBlocking));
-    for (hipEvent_t* ev : {&e.pipe_feat_ev, &e.pipe_entry_ev, &e.pipe_score_ev[0], &e.pipe_score_ev[1]})
+  if (!e.pipe_stream[0]) {
+    for (hipStream_t* st : {&e.pipe_stream[0], &e.pipe_stream[1]})
+      FD_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+    for (hipEvent_t* ev : {&e.pipe_feat_ev, &e.pipe_entry_ev, &e.pipe_done_ev[0], &e.pipe_done_ev[1]})
       FD_HIP(hipEventCreateWithFlags(ev, kStreamEventFlags));
   }
-  hipStream_t F = e.feat_stream;
+  // Batch i on stream S = pipe_stream[i & 1]: features then scoring, back to back on one queue (no
+  // cross-stream wait between them). S orders: after batch i-1's features (card-state order), after batch i-2
+  // (stream order: its vectors buffer, its scoring), and the engine stream after S (outputs in stream order).
+  const int b = e.pipe_parity;
+  hipStream_t S = e.pipe_stream[b];
   if (e.pipe_dirty) {  // work queued on e.stream by other calls (state loads, snapshots, ...) comes first
     FD_HIP(hipEventRecord(e.pipe_entry_ev, e.stream));
-    FD_HIP(hipStreamWaitEvent(F, e.pipe_entry_ev, 0));
+    FD_HIP(hipStreamWaitEvent(S, e.pipe_entry_ev, 0));
     e.pipe_dirty = false;
   }
-  if (input_ready) FD_HIP(hipStreamWaitEvent(F, static_cast<hipEvent_t>(input_ready), 0));
-  const int b = e.pipe_parity;
-  // the scoring launches that last read buffer b (batch i-2) must be done before batch i's features write it
-  if (e.pipe_score_live[b]) FD_HIP(hipStreamWaitEvent(F, e.pipe_score_ev[b], 0));
+  if (input_ready) FD_HIP(hipStreamWaitEvent(S, static_cast<hipEvent_t>(input_ready), 0));
+  if (e.pipe_feat_live) FD_HIP(hipStreamWaitEvent(S, e.pipe_feat_ev, 0));
+  // scoring paths other than the fused kernel share engine scratch (per-model columns, tree-split and LSTM
+  // buffers): those batches also wait for the previous batch's scoring
+  if (e.pipe_done_live[b ^ 1] && !fd::ensemble_applies(e, *params, slots, present, n))
+    FD_HIP(hipStreamWaitEvent(S, e.pipe_done_ev[b ^ 1], 0));
   e.pipe_vec[b].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
   float* vec = e.pipe_vec[b].as<float>();
   float* seq = nullptr;
@@ -761,15 +771,23 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
     e.pipe_seq[b].ensure((size_t)n * e.state.S * fd::kSeqInput * sizeof(float));
     seq = e.pipe_seq[b].as<float>();
   }
-  fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, F, e.pipe_lean);
-  FD_HIP(hipEventRecord(e.pipe_feat_ev, F));
-  FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_feat_ev, 0));
-  // parity flips only once the launches are queued (a failed call leaves the buffers' order intact)
+  fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, S, e.pipe_lean);
+  FD_HIP(hipEventRecord(e.pipe_feat_ev, S));
+  e.pipe_feat_live = true;
   e.pipe_parity ^= 1;
-  score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
-               d_confidence, d_decision, d_risk, seq, e.state.S);
-  FD_HIP(hipEventRecord(e.pipe_score_ev[b], e.stream));
-  e.pipe_score_live[b] = true;
+  {  // the scoring launches go on S: score_matrix launches on e.stream
+    struct Swap {
+      Engine& e;
+      hipStream_t saved;
+      ~Swap() { e.stream = saved; }
+    } swap{e, e.stream};
+    e.stream = S;
+    score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
+                 d_confidence, d_decision, d_risk, seq, e.state.S);
+  }
+  FD_HIP(hipEventRecord(e.pipe_done_ev[b], S));
+  e.pipe_done_live[b] = true;
+  FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[b], 0));
   FD_API_END
 }
 

@@ -613,37 +613,58 @@ extern "C" __attribute__((visibility("default"))) int fd_debug_ens_profile(unsig
 }
 #endif
 
-bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
-                     const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
-                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results) {
+namespace {
+struct Pair {
+  int sa = -1, sb = -1, pa = -1, pb = -1, ma = -1, mb = -1;
+};
+
+// The fused kernel applies (and its joint plan is built) when the batch is large and the present models are
+// exactly one XGBoost and one IsolationForest in engine slots.
+bool select_pair(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present, int64_t n,
+                 Pair& q) {
   if (!e.ensemble_on || e.forest_variant != 0 || n <= 0) return false;
   if ((n + kTile - 1) / kTile < kSplitTiles) return false;  // latency batches: the tree-split path
-  // the present models must be exactly one XGBoost and one IsolationForest in engine slots
-  int sa = -1, sb = -1, pa = -1, pb = -1, ma = -1, mb = -1, k = 0;
+  int k = 0;
   for (int m = 0; m < p.n_models; ++m) {
     if (present && !present[m]) continue;
     const int s = slots[m];
     if (s < 0 || s >= kMaxSlots || !e.forests[s].loaded) return false;
     const int kind = e.forests[s].kind;
-    if (kind == FD_FOREST_XGB_BINARY_LOGISTIC && sa < 0) {
-      sa = s;
-      pa = k;
-      ma = m;
-    } else if (kind == FD_FOREST_SKLEARN_IFOREST && sb < 0) {
-      sb = s;
-      pb = k;
-      mb = m;
+    if (kind == FD_FOREST_XGB_BINARY_LOGISTIC && q.sa < 0) {
+      q.sa = s;
+      q.pa = k;
+      q.ma = m;
+    } else if (kind == FD_FOREST_SKLEARN_IFOREST && q.sb < 0) {
+      q.sb = s;
+      q.pb = k;
+      q.mb = m;
     } else {
       return false;
     }
     ++k;
   }
-  if (sa < 0 || sb < 0) return false;
+  if (q.sa < 0 || q.sb < 0) return false;
   EnsemblePlan& P = e.ens;
-  if (!P.valid || P.slot[0] != sa || P.slot[1] != sb || P.gen[0] != e.forests[sa].gen ||
-      P.gen[1] != e.forests[sb].gen) {
-    if (!build_plan(e, sa, sb)) return false;
+  if (!P.valid || P.slot[0] != q.sa || P.slot[1] != q.sb || P.gen[0] != e.forests[q.sa].gen ||
+      P.gen[1] != e.forests[q.sb].gen) {
+    if (!build_plan(e, q.sa, q.sb)) return false;
   }
+  return true;
+}
+}  // namespace
+
+bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present, int64_t n) {
+  Pair q;
+  return select_pair(e, p, slots, present, n, q);
+}
+
+bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
+                     const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
+                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results) {
+  Pair q;
+  if (!select_pair(e, p, slots, present, n, q)) return false;
+  const int pa = q.pa, pb = q.pb, ma = q.ma, mb = q.mb;
+  EnsemblePlan& P = e.ens;
   EnsArgs a{};
   a.X = dX;
   a.n = n;

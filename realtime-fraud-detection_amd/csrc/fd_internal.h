@@ -252,11 +252,12 @@ struct Engine {
   hipEvent_t join2_ev = nullptr;
   DeviceBuffer seq_buf;                        // per-txn LSTM input sequences of the fused path
   DeviceBuffer feat_vec, feat_in, feat_ext;  // host-API / fused-pipeline staging for features
-  // fd_score_batch_pipelined: features on feat_stream (batch i+1's overlap batch i's forests on `stream`),
-  // scoring vectors / LSTM sequences double-buffered by batch parity
-  hipStream_t feat_stream = nullptr;
-  hipEvent_t pipe_feat_ev = nullptr, pipe_entry_ev = nullptr, pipe_score_ev[2] = {nullptr, nullptr};
-  bool pipe_score_live[2] = {false, false};
+  // fd_score_batch_pipelined: batch i runs features + scoring on pipe_stream[i & 1], its features ordered after
+  // batch i-1's (pipe_feat_ev), so batch i+1's features overlap batch i's forests with no cross-stream wait
+  // between a batch's features and its forests; vectors / LSTM sequences double-buffered by batch parity
+  hipStream_t pipe_stream[2] = {nullptr, nullptr};
+  hipEvent_t pipe_feat_ev = nullptr, pipe_entry_ev = nullptr, pipe_done_ev[2] = {nullptr, nullptr};
+  bool pipe_feat_live = false, pipe_done_live[2] = {false, false};
   bool pipe_dirty = true;  // another engine call since the last pipelined one: order after `stream` first
   int pipe_parity = 0;
   bool pipe_lean = true;  // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
@@ -375,6 +376,7 @@ void read_xgboost_json(const char* path, XgbModel& out);
 // ensemble.hip: the fused path when the present models are one XGBoost and/or one IsolationForest in engine
 // slots and the batch is large (false: not applicable, the caller runs the per-model kernels + blend).
 // results != nullptr: write route result records (seq from records[i]) instead of the columns.
+bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present, int64_t n);
 bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
                      const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
                      uint8_t* drisk, const RouteRecord* records, ResultRecord* results);

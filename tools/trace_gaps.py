@@ -1,0 +1,19 @@
+"""Kernel timeline of a rocprofv3 --kernel-trace run: per kernel start/end/duration/queue and the idle gap on
+the queue of the dominant kernel (usage: python tools/trace_gaps.py run_kernel_trace.csv [n] [names...])."""
+import csv
+import sys
+
+path = sys.argv[1]
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+names = sys.argv[3:] or ["ensemble", "feat_slot", "feat_bucket"]
+rows = list(csv.DictReader(open(path)))
+ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]) for r in rows)
+sel = [k for k in ks if any(x in k[2] for x in names)]
+win = sel[-(n + 20):-20] if len(sel) > n + 20 else sel
+t0 = win[0][0]
+last_end = {}
+for s, e, name, q in win:
+    nm = name.replace("void ", "").replace("fd::(anonymous namespace)::", "")[:32]
+    gap = (s - last_end[q]) / 1000 if q in last_end else 0.0
+    last_end[q] = e
+    print(f"{(s - t0) / 1000:9.1f} {(e - t0) / 1000:9.1f} {(e - s) / 1000:7.1f}  qgap {gap:6.1f}  q{q} {nm}")
