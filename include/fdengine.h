@@ -365,8 +365,9 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
    stream after batch i's features, so the outputs are ordered on the engine stream exactly as with
    fd_score_batch_device. Batch i+1's features therefore overlap batch i's forests. The scoring vectors
    live in two engine buffers (batch parity); the input columns must stay unchanged until the call's
-   outputs are complete. Any other engine call in between orders the next batch's features after
-   everything queued on the engine stream (no overlap across it). */
+   outputs are complete, and consecutive calls must not share output buffers (batch i+1's forests may
+   start before batch i's finish). Any other engine call in between orders the next batch's features
+   after everything queued on the engine stream (no overlap across it). */
 int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
                              const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
                              int64_t n, double* d_model_probs, double* d_fraud_prob, double* d_confidence,

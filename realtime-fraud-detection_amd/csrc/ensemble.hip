@@ -248,6 +248,9 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   unsigned long long pr_top = 0, pr_walk = 0, pr_sync = 0, pr_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   FD_ESTAMP(pr_t0);
+  // above the feature kernels of the next micro-batch that share the CU in the pipelined stream (priority 0):
+  // this kernel is the stream's critical path, theirs is latency-bound with slack
+  __builtin_amdgcn_s_setprio(2);
   int anynan = 0;
   {
     uint16_t* Xs = reinterpret_cast<uint16_t*>(lbase);
