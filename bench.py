@@ -276,6 +276,7 @@ class Config3:
     name = "config3"
     dtype = "f32 (features f64, forests f32/f64, blend f64)"
     with_lstm = False
+    pipelined_default = True  # 64k batches: batch i+1's features overlap batch i's forests
     seq_len = 10  # lstm_sequential sequence_length (ml/utils/config.py:152)
 
     def __init__(self, args, rank, dev, eng):
@@ -324,30 +325,50 @@ class Config3:
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
+        # after the parity batches (which need the vectors): the pipelined stream, outputs alternating two sets
+        self.pipe, self.parity_done, self.cur = self.pipelined_default and not args.no_pipeline, False, 0
+        self.outs = [[self.fp, self.conf, self.dec, self.risk],
+                     [torch.empty_like(t) for t in (self.fp, self.conf, self.dec, self.risk)]]
+        self.scorer = eng.pipelined_scorer(self.params, self.slots)
+        self.serial = eng.batch_scorer(self.params, self.slots)
         self.next_batch = 0
         self.parity_batches = args.parity_batches
         log(f"[rank {rank}] {self.name} setup {time.time() - t:.1f}s: {self.cards} cards, capacity {cap}, "
             f"{self.n_batches} batches resident, window={'sliding' if self.mode else 'redis_compat'}")
 
     def _ptrs(self, b):
-        return {f: t.data_ptr() + b * self.B * self.elem[f] for f, t in self.dev.items()}
+        if not hasattr(self, "_base"):
+            self._base = {f: (t.data_ptr(), self.B * self.elem[f]) for f, t in self.dev.items()}
+        return {f: p + b * w for f, (p, w) in self._base.items()}
 
     def step(self, i):
         b = self.next_batch
         if b >= self.n_batches:
             raise RuntimeError("stream exhausted: raise n_batches")
         self.next_batch += 1
-        self.eng.score_batch_device(self.params, self.slots, self._ptrs(b), self.B, self.fp.data_ptr(),
-                                    self.conf.data_ptr(), self.dec.data_ptr(), self.risk.data_ptr(),
-                                    vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
+        if self.pipe and self.parity_done:
+            self.cur = b & 1
+            fp, conf, dec, risk = self.outs[self.cur]
+            self.scorer(self._ptrs(b), self.B, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr())
+            return
+        self.cur = 0
+        self.serial(self._ptrs(b), self.B, self.fp.data_ptr(), self.conf.data_ptr(), self.dec.data_ptr(),
+                    self.risk.data_ptr(), vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
 
     def fetch(self, i):
-        self.h_fp.copy_(self.fp, non_blocking=True)
-        self.h_dec.copy_(self.dec, non_blocking=True)
-        self.h_risk.copy_(self.risk, non_blocking=True)
+        fp, _, dec, risk = self.outs[self.cur]
+        self.h_fp.copy_(fp, non_blocking=True)
+        self.h_dec.copy_(dec, non_blocking=True)
+        self.h_risk.copy_(risk, non_blocking=True)
 
     def parity(self):
         """The first parity_batches micro-batches (fresh state, carried across them) through the oracle chain."""
+        try:
+            return self._parity()
+        finally:
+            self.parity_done = True
+
+    def _parity(self):
         import oracle
         from oracle.features_c import OracleFeatureState
         np = self.np
@@ -416,6 +437,7 @@ class Config5(Config3):
     -> blend/decision. p99 micro-batch latency is the headline here."""
     name = "config5"
     with_lstm = True
+    pipelined_default = False  # 1k latency batches: the per-call cost is the bound, one stream is faster
 
     def roofline(self, timing):
         N = self.N
@@ -729,6 +751,7 @@ class Config3J(Config3):
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
+        self.outs, self.cur = [[self.fp, self.conf, self.dec, self.risk]], 0  # Config3.fetch (serial steps here)
         self.nbytes = [int(o[-1].item()) for o in offs]
         log(f"[rank {rank}] config3j setup {time.time() - t:.1f}s: {self.cards} cards, capacity {cap}, "
             f"{self.pool} JSON batches resident ({self.nbytes[0] / B:.0f} B/message)")
@@ -839,7 +862,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="config4 at N=1: fd_score_batch_device per step instead of the pipelined stream")
+                    help="config3/4 at N=1: fd_score_batch_device per step instead of the pipelined stream")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--parity-batches", type=int, default=2)
     args = ap.parse_args()

@@ -229,6 +229,12 @@ class FraudEngine:
         (the per-step host cost stays well below the GPU step)."""
         return PipelinedScorer(self, params, slots, present)
 
+    def batch_scorer(self, params: N.fd_blend_params, slots: Sequence[int],
+                     present: Optional[Sequence[int]] = None) -> "PipelinedScorer":
+        """The same prepared call over score_batch_device (one stream; small latency batches, where the
+        per-call host cost is the step's bound)."""
+        return PipelinedScorer(self, params, slots, present, pipelined=False)
+
     def features_seq_device(self, ptrs: dict, n: int, vec_ptr: int, seq_ptr: int, raw_ptr: int = 0) -> None:
         """features_device plus each transaction's LSTM input sequence (n x seq_len x 16 f32)."""
         b = N.fd_txn_batch(*[int(ptrs[f]) for f in N.TXN_FIELDS])
@@ -605,10 +611,11 @@ def merge_merchant_windows(parts) -> np.ndarray:
 
 
 class PipelinedScorer:
-    """fd_score_batch_pipelined with its model arguments marshalled once (FraudEngine.pipelined_scorer)."""
+    """fd_score_batch_pipelined (or, pipelined=False, fd_score_batch_device) with its model arguments marshalled
+    once (FraudEngine.pipelined_scorer / batch_scorer)."""
 
     def __init__(self, eng: FraudEngine, params: N.fd_blend_params, slots: Sequence[int],
-                 present: Optional[Sequence[int]] = None):
+                 present: Optional[Sequence[int]] = None, pipelined: bool = True):
         M = params.n_models
         self.eng = eng
         self.params = params
@@ -616,14 +623,20 @@ class PipelinedScorer:
         self._pres = np.array([1] * M if present is None else list(present), np.uint8)
         self._ext = (C.c_void_p * N.FD_MAX_MODELS)()
         self._batch = N.fd_txn_batch()
-        self._fn = N.lib.fd_score_batch_pipelined
+        self.pipelined = pipelined
+        self._fn = N.lib.fd_score_batch_pipelined if pipelined else N.lib.fd_score_batch_device
         self._args = [C.byref(params), _ptr(self._sl), self._ext, _ptr(self._pres), C.byref(self._batch)]
 
     def __call__(self, txn_ptrs: dict, n: int, fp_ptr: int, conf_ptr: int = 0, dec_ptr: int = 0, risk_ptr: int = 0,
-                 input_ready: int = 0) -> None:
+                 input_ready: int = 0, vec_ptr: int = 0, model_probs_ptr: int = 0) -> None:
         b = self._batch
         for f in N.TXN_FIELDS:
             setattr(b, f, txn_ptrs[f])
-        rc = self._fn(self.eng._h, *self._args, int(n), None, fp_ptr, conf_ptr or None, dec_ptr or None,
-                      risk_ptr or None, input_ready or None)
-        N.check(rc, "fd_score_batch_pipelined")
+        if self.pipelined:
+            rc = self._fn(self.eng._h, *self._args, int(n), model_probs_ptr or None, fp_ptr, conf_ptr or None,
+                          dec_ptr or None, risk_ptr or None, input_ready or None)
+            N.check(rc, "fd_score_batch_pipelined")
+        else:
+            rc = self._fn(self.eng._h, *self._args, int(n), vec_ptr or None, model_probs_ptr or None, fp_ptr,
+                          conf_ptr or None, dec_ptr or None, risk_ptr or None)
+            N.check(rc, "fd_score_batch_device")

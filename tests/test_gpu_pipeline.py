@@ -127,3 +127,57 @@ def test_pipelined_with_interleaved_calls(world):
 @pytest.mark.timeout(300)
 def test_pipelined_input_ready_event(world):
     _run(world, [0, 40000, 80000, 120000, 160000], side_stream=True)
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_lstm_and_latency_batches(world):
+    """models [XGBoost, IsolationForest, LSTM] (the per-model scoring path with the LSTM on its second stream and
+    the card histories double-buffered) and latency-size batches (tree-split path): pipelined == serial, model
+    columns included"""
+    import torch
+
+    from fdengine import lstm as L
+    from fdengine._native import FD_SLOT_LSTM
+    from oracle import scoring_ref as S
+    pop, tx, xgb, ifm = world
+    names = ["xgboost_primary", "isolation_forest", "lstm_sequential"]
+    w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05, "lstm_sequential": 0.25})
+    params = FraudEngine.blend_params([w[k] for k in names], [S.CONF_MULT[k] for k in names])
+    lw = L.random_weights(16, 128, 1, seed=5)
+    U, M = pop["users"], pop["merchants"]
+    engines = []
+    for _ in range(2):
+        e = FraudEngine(0)
+        e.state_init(1 << 17, 1, 16, seq_len=10)
+        e.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        e.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        e.load_forest(0, xgb)
+        e.load_forest(1, ifm)
+        e.load_lstm(lw)
+        e.set_stream(torch.cuda.current_stream().cuda_stream)
+        engines.append(e)
+    ref, pip = engines
+    cuts = [0, 1000, 1700, 9000, 9100, 15000]
+    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f][:cuts[-1]])).cuda() for f in TXN_FIELDS}
+    torch.cuda.synchronize()
+    try:
+        got, want = [], []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            n = b - a
+            ptrs = {f: t[a:b].data_ptr() for f, t in dev.items()}
+            o_ref, o_pip = _outs(n), _outs(n)
+            mp_ref = torch.empty((3, n), dtype=torch.float64, device="cuda")
+            mp_pip = torch.empty((3, n), dtype=torch.float64, device="cuda")
+            ref.score_batch_device(params, [0, 1, FD_SLOT_LSTM], ptrs, n, *[o.data_ptr() for o in o_ref],
+                                   model_probs_ptr=mp_ref.data_ptr())
+            pip.score_batch_pipelined(params, [0, 1, FD_SLOT_LSTM], ptrs, n, *[o.data_ptr() for o in o_pip],
+                                      model_probs_ptr=mp_pip.data_ptr())
+            got.append(o_pip + [mp_pip])
+            want.append(o_ref + [mp_ref])
+        torch.cuda.synchronize()
+        for g, w_ in zip(got, want):
+            for x, y in zip(g, w_):
+                np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+    finally:
+        for e in engines:
+            e.close()
