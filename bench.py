@@ -861,6 +861,9 @@ def main():
     ap.add_argument("--ring-k", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline-mode", type=int, choices=[1, 2], default=1,
+                    help="fd_score_batch_pipelined option pipeline_mode (1: features + scoring per stream, 2: one "
+                         "feature stream)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="config3/4 at N=1: fd_score_batch_device per step instead of the pipelined stream")
     ap.add_argument("--latency-iters", type=int, default=200)
@@ -896,6 +899,7 @@ def main():
     eng = fdengine.FraudEngine(dev.index)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
+    eng.set_option("pipeline_mode", args.pipeline_mode)
     wl = WORKLOADS[args.workload](args, rank, dev, eng)
 
     parity = None

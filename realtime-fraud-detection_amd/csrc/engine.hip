@@ -248,15 +248,18 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipStreamDestroy(e.aux2_stream);
     (void)hipEventDestroy(e.join2_ev);
   }
-  if (e.pipe_stream[0]) {
-    for (hipStream_t st : e.pipe_stream) {
+  for (hipStream_t st : e.pipe_stream)
+    if (st) {
       (void)hipStreamSynchronize(st);
       (void)hipStreamDestroy(st);
     }
-    for (hipEvent_t ev : {e.pipe_feat_ev, e.pipe_entry_ev, e.pipe_done_ev[0], e.pipe_done_ev[1]})
-      (void)hipEventDestroy(ev);
+  if (e.pipe_entry_ev) (void)hipEventDestroy(e.pipe_entry_ev);
+  for (int k = 0; k < Engine::kPipeSlots; ++k) {
+    if (e.pipe_feat_ev[k]) (void)hipEventDestroy(e.pipe_feat_ev[k]);
+    if (e.pipe_done_ev[k]) (void)hipEventDestroy(e.pipe_done_ev[k]);
+    e.pipe_vec[k].release();
+    e.pipe_seq[k].release();
   }
-  for (auto* b : {&e.pipe_vec[0], &e.pipe_vec[1], &e.pipe_seq[0], &e.pipe_seq[1]}) b->release();
   for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
   for (auto* b : {&e.ens.nodes[0], &e.ens.nodes[1], &e.ens.thr})
     b->release();
@@ -331,6 +334,16 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "pipeline_lean") {  // fd_score_batch_pipelined's bucket pass: 1 (default) lean + deferred
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "pipeline_lean must be 0 or 1");
     e.pipe_lean = value != 0;
+  } else if (k == "pipeline_mode") {  // fd_score_batch_pipelined: 1 features + scoring of a batch on one of two
+    // streams (default); 2 every batch's features on a third stream, scoring on two
+    FD_REQUIRE(value == 1 || value == 2, FD_ERR_INVALID_ARG, "pipeline_mode must be 1 or 2");
+    if ((int)value != e.pipe_mode) {  // drain the pipeline: its buffer ring changes
+      for (hipStream_t st : e.pipe_stream)
+        if (st) FD_HIP(hipStreamSynchronize(st));
+      for (int q = 0; q < Engine::kPipeSlots; ++q) e.pipe_feat_live[q] = e.pipe_done_live[q] = false;
+      e.pipe_iter = 0;
+      e.pipe_mode = (int)value;
+    }
   } else if (k == "timing_every") {  // kernel timing (fd_timing_*): HIP events on one launch in N of each kind
     FD_REQUIRE(value >= 1 && value <= 1000000, FD_ERR_INVALID_ARG, "timing_every must be >= 1");
     e.timing_every = (int)value;
@@ -737,30 +750,36 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
   Engine& e = E_quiet(eng);
   FD_REQUIRE(params && txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   if (n == 0) return FD_OK;
-  if (!e.pipe_stream[0]) {
-    for (hipStream_t* st : {&e.pipe_stream[0], &e.pipe_stream[1]})
-      FD_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
-    for (hipEvent_t* ev : {&e.pipe_feat_ev, &e.pipe_entry_ev, &e.pipe_done_ev[0], &e.pipe_done_ev[1]})
-      FD_HIP(hipEventCreateWithFlags(ev, kStreamEventFlags));
+  const bool m2 = e.pipe_mode == 2;
+  for (int k = 0; k < (m2 ? 3 : 2); ++k)
+    if (!e.pipe_stream[k]) FD_HIP(hipStreamCreateWithFlags(&e.pipe_stream[k], hipStreamNonBlocking));
+  if (!e.pipe_entry_ev) {
+    FD_HIP(hipEventCreateWithFlags(&e.pipe_entry_ev, kStreamEventFlags));
+    for (int k = 0; k < Engine::kPipeSlots; ++k) {
+      FD_HIP(hipEventCreateWithFlags(&e.pipe_feat_ev[k], kStreamEventFlags));
+      FD_HIP(hipEventCreateWithFlags(&e.pipe_done_ev[k], kStreamEventFlags));
+    }
   }
-  // Batch i on stream S = pipe_stream[i & 1]: features then scoring, back to back on one queue (no
-  // cross-stream wait between them). S orders: after batch i-1's features (card-state order), after batch i-2
-  // (stream order: its vectors buffer, its scoring), and the engine stream after S (outputs in stream order).
-  const int b = e.pipe_parity;
-  hipStream_t S = e.pipe_stream[b];
+  // Batch i: buffer slot s = i mod nbuf, scoring stream Sc = pipe_stream[i & 1], feature stream Sf = Sc
+  // (mode 1) or pipe_stream[2] (mode 2). Card-state order: batch i's features after batch i-1's (same queue in
+  // mode 2, an event in mode 1). Buffer s is free once batch i-nbuf's scoring is done (same queue in mode 1,
+  // an event in mode 2). Outputs: the engine stream waits for batch i's scoring.
+  const int nbuf = m2 ? 3 : 2;
+  const int s = (int)(e.pipe_iter % (unsigned long long)nbuf);
+  const int prev = (s + nbuf - 1) % nbuf;
+  hipStream_t Sc = e.pipe_stream[e.pipe_iter & 1];
+  hipStream_t Sf = m2 ? e.pipe_stream[2] : Sc;
   if (e.pipe_dirty) {  // work queued on e.stream by other calls (state loads, snapshots, ...) comes first
     FD_HIP(hipEventRecord(e.pipe_entry_ev, e.stream));
-    FD_HIP(hipStreamWaitEvent(S, e.pipe_entry_ev, 0));
+    FD_HIP(hipStreamWaitEvent(Sf, e.pipe_entry_ev, 0));
+    if (m2) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_entry_ev, 0));
     e.pipe_dirty = false;
   }
-  if (input_ready) FD_HIP(hipStreamWaitEvent(S, static_cast<hipEvent_t>(input_ready), 0));
-  if (e.pipe_feat_live) FD_HIP(hipStreamWaitEvent(S, e.pipe_feat_ev, 0));
-  // scoring paths other than the fused kernel share engine scratch (per-model columns, tree-split and LSTM
-  // buffers): those batches also wait for the previous batch's scoring
-  if (e.pipe_done_live[b ^ 1] && !fd::ensemble_applies(e, *params, slots, present, n))
-    FD_HIP(hipStreamWaitEvent(S, e.pipe_done_ev[b ^ 1], 0));
-  e.pipe_vec[b].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
-  float* vec = e.pipe_vec[b].as<float>();
+  if (input_ready) FD_HIP(hipStreamWaitEvent(Sf, static_cast<hipEvent_t>(input_ready), 0));
+  if (!m2 && e.pipe_feat_live[prev]) FD_HIP(hipStreamWaitEvent(Sf, e.pipe_feat_ev[prev], 0));
+  if (m2 && e.pipe_done_live[s]) FD_HIP(hipStreamWaitEvent(Sf, e.pipe_done_ev[s], 0));
+  e.pipe_vec[s].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
+  float* vec = e.pipe_vec[s].as<float>();
   float* seq = nullptr;
   bool want_seq = false;
   for (int m = 0; m < params->n_models && m < FD_MAX_MODELS; ++m)
@@ -768,26 +787,31 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
   if (want_seq) {
     FD_REQUIRE(e.state.ready && e.state.S > 0, FD_ERR_INVALID_ARG,
                "the LSTM head needs card history: fd_state_params.seq_len > 0");
-    e.pipe_seq[b].ensure((size_t)n * e.state.S * fd::kSeqInput * sizeof(float));
-    seq = e.pipe_seq[b].as<float>();
+    e.pipe_seq[s].ensure((size_t)n * e.state.S * fd::kSeqInput * sizeof(float));
+    seq = e.pipe_seq[s].as<float>();
   }
-  fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, S, e.pipe_lean);
-  FD_HIP(hipEventRecord(e.pipe_feat_ev, S));
-  e.pipe_feat_live = true;
-  e.pipe_parity ^= 1;
-  {  // the scoring launches go on S: score_matrix launches on e.stream
+  fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean);
+  FD_HIP(hipEventRecord(e.pipe_feat_ev[s], Sf));
+  e.pipe_feat_live[s] = true;
+  if (m2) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_feat_ev[s], 0));
+  // scoring paths other than the fused kernel share engine scratch (per-model columns, tree-split and LSTM
+  // buffers): those batches also wait for the previous batch's scoring
+  if (e.pipe_done_live[prev] && !fd::ensemble_applies(e, *params, slots, present, n))
+    FD_HIP(hipStreamWaitEvent(Sc, e.pipe_done_ev[prev], 0));
+  ++e.pipe_iter;
+  {  // the scoring launches go on Sc: score_matrix launches on e.stream
     struct Swap {
       Engine& e;
       hipStream_t saved;
       ~Swap() { e.stream = saved; }
     } swap{e, e.stream};
-    e.stream = S;
+    e.stream = Sc;
     score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
                  d_confidence, d_decision, d_risk, seq, e.state.S);
   }
-  FD_HIP(hipEventRecord(e.pipe_done_ev[b], S));
-  e.pipe_done_live[b] = true;
-  FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[b], 0));
+  FD_HIP(hipEventRecord(e.pipe_done_ev[s], Sc));
+  e.pipe_done_live[s] = true;
+  FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[s], 0));
   FD_API_END
 }
 

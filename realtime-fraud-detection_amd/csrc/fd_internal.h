@@ -252,16 +252,19 @@ struct Engine {
   hipEvent_t join2_ev = nullptr;
   DeviceBuffer seq_buf;                        // per-txn LSTM input sequences of the fused path
   DeviceBuffer feat_vec, feat_in, feat_ext;  // host-API / fused-pipeline staging for features
-  // fd_score_batch_pipelined: batch i runs features + scoring on pipe_stream[i & 1], its features ordered after
-  // batch i-1's (pipe_feat_ev), so batch i+1's features overlap batch i's forests with no cross-stream wait
-  // between a batch's features and its forests; vectors / LSTM sequences double-buffered by batch parity
-  hipStream_t pipe_stream[2] = {nullptr, nullptr};
-  hipEvent_t pipe_feat_ev = nullptr, pipe_entry_ev = nullptr, pipe_done_ev[2] = {nullptr, nullptr};
-  bool pipe_feat_live = false, pipe_done_live[2] = {false, false};
+  // fd_score_batch_pipelined (engine.hip): scoring of batch i on pipe_stream[i & 1]; its features on the same
+  // stream (mode 1: no cross-stream wait between a batch's features and its forests, batch i-1's features
+  // waited for by event) or on pipe_stream[2] for every batch (mode 2: the feature chain on one queue, the
+  // scoring streams wait for it); vectors / LSTM sequences in a ring of 2 (mode 1) or 3 (mode 2) buffers
+  static constexpr int kPipeSlots = 3;
+  hipStream_t pipe_stream[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t pipe_entry_ev = nullptr, pipe_feat_ev[kPipeSlots] = {}, pipe_done_ev[kPipeSlots] = {};
+  bool pipe_feat_live[kPipeSlots] = {}, pipe_done_live[kPipeSlots] = {};
   bool pipe_dirty = true;  // another engine call since the last pipelined one: order after `stream` first
-  int pipe_parity = 0;
-  bool pipe_lean = true;  // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
-  DeviceBuffer pipe_vec[2], pipe_seq[2];
+  unsigned long long pipe_iter = 0;
+  int pipe_mode = 1;       // "pipeline_mode" option
+  bool pipe_lean = true;   // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
+  DeviceBuffer pipe_vec[kPipeSlots], pipe_seq[kPipeSlots];
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
