@@ -311,7 +311,7 @@ class Config3:
         U, M = self.pop["users"], self.pop["merchants"]
         eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
         eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
-        self.n_batches = args.warmup + args.steps + args.latency_iters + args.parity_batches + 1
+        self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches + 1
         self.tx = synth.txn_stream(self.pop, self.n_batches * self.B, seed=200 + rank)
         self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
         self.elem = {f: self.tx[f].dtype.itemsize for f in N.TXN_FIELDS}
@@ -502,7 +502,7 @@ class Config4(Config3):
         eng.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
         # this rank's ingest stream (over all cards), resident in HBM
         self.parity_batches = args.parity_batches
-        self.n_batches = args.warmup + args.steps + args.latency_iters + args.parity_batches + 1
+        self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches + 1
         self.tx = synth.txn_stream_cards(self.cards, self.merchants, self.n_batches * self.B, seed=200 + rank,
                                          card_seed=42, rate_per_s=2000.0)
         self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
@@ -867,6 +867,9 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="config3/4 at N=1: fd_score_batch_device per step instead of the pipelined stream")
     ap.add_argument("--latency-iters", type=int, default=200)
+    ap.add_argument("--alone-iters", type=int, default=20,
+                    help="steps run one at a time after the latency loop, every launch timed: each kernel's "
+                         "duration with nothing beside it (roofline.alone)")
     ap.add_argument("--parity-batches", type=int, default=2)
     args = ap.parse_args()
     if args.batch is None:
@@ -951,6 +954,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         p99 = float(t.item())
 
+    # the same kernels one micro-batch at a time, nothing beside them (in the pipelined stream the next batch's
+    # feature kernels share the CUs with the forests): each kernel's unshared duration
+    timing_alone = None
+    if args.alone_iters > 0:
+        eng.set_option("timing_every", 1)
+        eng.set_timing(True)
+        for i in range(args.alone_iters):
+            wl.step(i)
+            stream.synchronize()
+        eng.set_timing(False)
+        timing_alone = eng.read_timing()
+
     value = world * args.steps * args.batch / elapsed
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -958,6 +973,14 @@ def main():
 
     if rank == 0:
         roof = wl.roofline(timing)
+        if timing_alone and isinstance(roof, dict):
+            try:
+                ra = wl.roofline(timing_alone)
+                roof["alone"] = {"kernel_avg_us": ra.get("kernel_avg_us"), "achieved": ra.get("achieved"),
+                                 "frac": ra.get("frac"), "basis": f"{args.alone_iters} steps one at a time, "
+                                 "every launch timed (no other kernel on the CUs)"}
+            except Exception as e:  # a workload whose roofline needs the timed region's kernels
+                log(f"[rank {rank}] roofline.alone unavailable: {e!r}")
         line = {
             "metric": "scored transactions/sec (whole node)",
             "value": round(value, 1),
@@ -980,6 +1003,7 @@ def main():
             "latency_samples": len(lat),
             "roofline": roof,
             "kernel_avg_us": wl.kernels(timing),
+            "kernel_avg_us_alone": wl.kernels(timing_alone) if timing_alone else None,
             "kernel_timing": f"HIP events on the launch stream, 1 launch in {TIMING_EVERY} of each kernel, timed region",
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
