@@ -261,6 +261,8 @@ int fd_engine_destroy(fd_engine* eng) {
     e.pipe_seq[k].release();
   }
   for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
+  for (auto& P1 : e.ens1)
+    for (auto* b : {&P1.nodes[0], &P1.nodes[1], &P1.thr}) b->release();
   for (auto* b : {&e.ens.nodes[0], &e.ens.nodes[1], &e.ens.thr})
     b->release();
   {  // ingest codec tables and staging

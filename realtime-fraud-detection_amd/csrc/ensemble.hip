@@ -374,7 +374,8 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
 #endif
     }
   }
-  if (G > 0) stage_chunk_asm(a.nodes[0], bufA, a.stride[0], kEnsWG / 64);  // chunk 0 (the tables are dead)
+  if (G > 0)  // chunk 0 (the tables are dead): forest A's first, or B's when A is absent
+    stage_chunk_asm(nA > 0 ? a.nodes[0] : a.nodes[1], bufA, nA > 0 ? a.stride[0] : a.stride[1], kEnsWG / 64);
   if (gg == 0) {
     lds_store<float>(accA + txn * 4, a.base_margin);
     lds_store<double>(accB + txn * 8, 0.0);
@@ -462,6 +463,10 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     const double decision = -score - a.if_offset;
     pb = 1.0 / (1.0 + exp(decision));
   }
+  if (OUT == 2) {  // one forest: its probability (forest_predict semantics)
+    a.fp[row] = nA > 0 ? pa : pb;
+    return;
+  }
   double raw[FD_MAX_MODELS];  // the two present models at their blend positions (selects: no scratch)
 #pragma unroll
   for (int m = 0; m < FD_MAX_MODELS; ++m) raw[m] = m == a.pos[0] ? pa : (m == a.pos[1] ? pb : 0.0);
@@ -517,24 +522,35 @@ fd_tree_arrays arrays_of(const PackedForest& f) {
   return t;
 }
 
-// joint repack of forest A (XGBoost) and B (IsolationForest); false when not possible (the per-model path runs)
-bool build_plan(Engine& e, int sa, int sb) {
-  EnsemblePlan& P = e.ens;
+// joint repack of forest A (XGBoost, slot sa) and B (IsolationForest, slot sb) into plan P; either slot may be -1
+// (a single forest: the kernel walks only the other one); false when not possible (the per-model path runs)
+bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb) {
   P.valid = false;
-  const PackedForest& A = e.forests[sa];
-  const PackedForest& B = e.forests[sb];
-  if (!A.binned || !B.binned || A.num_feature != B.num_feature || A.t_off.empty() || B.t_off.empty()) return false;
-  const int D = std::max(A.depth, B.depth);
+  const PackedForest* F[2] = {sa >= 0 ? &e.forests[sa] : nullptr, sb >= 0 ? &e.forests[sb] : nullptr};
+  if (!F[0] && !F[1]) return false;
+  int D = 0, nf = -1;
+  for (const PackedForest* f : F) {
+    if (!f) continue;
+    if (!f->binned || f->t_off.empty() || (nf >= 0 && f->num_feature != nf)) return false;
+    nf = f->num_feature;
+    D = std::max(D, f->depth);
+  }
   if (D > 8) return false;
-  const int nf = A.num_feature;
   if (ens_lds(nf, D) > kLdsBudget) return false;
-  HostPack hp[2] = {pack_forest_host(A.params, arrays_of(A), D), pack_forest_host(B.params, arrays_of(B), D)};
-  if (!hp[0].binned || !hp[1].binned || hp[0].depth != D || hp[1].depth != D) return false;
+  HostPack hp[2];
+  for (int k = 0; k < 2; ++k) {
+    if (!F[k]) continue;
+    hp[k] = pack_forest_host(F[k]->params, arrays_of(*F[k]), D);
+    if (!hp[k].binned || hp[k].depth != D) return false;
+  }
   // merged per-feature tables
   std::vector<std::vector<float>> merged(nf);
   for (int f = 0; f < nf; ++f) {
-    for (const HostPack& h : hp)
+    for (int k = 0; k < 2; ++k) {
+      if (!F[k]) continue;
+      const HostPack& h = hp[k];
       merged[f].insert(merged[f].end(), h.b_thr.begin() + h.b_thr_off[f], h.b_thr.begin() + h.b_thr_off[f + 1]);
+    }
     std::sort(merged[f].begin(), merged[f].end());
     merged[f].erase(std::unique(merged[f].begin(), merged[f].end()), merged[f].end());
     if (merged[f].size() > (size_t)kMaxBins) return false;
@@ -551,6 +567,12 @@ bool build_plan(Engine& e, int sa, int sb) {
   const int CH[2] = {kCHA, kCHB};
   const size_t leaf_sz[2] = {sizeof(float), sizeof(double)};
   for (int k = 0; k < 2; ++k) {
+    if (!F[k]) {
+      P.n_trees[k] = P.n_chunks[k] = 0;
+      P.CH[k] = CH[k];
+      P.stride[k] = 0;
+      continue;
+    }
     const HostPack& h = hp[k];
     const int T = h.n_trees, nc = (T + CH[k] - 1) / CH[k];
     // chunk: CH node blocks of 1 KiB (walk_ens link addressing), then the CH trees' leaf values [CH][NL];
@@ -594,18 +616,23 @@ bool build_plan(Engine& e, int sa, int sb) {
   P.max_feature_thr = maxc;
   P.slot[0] = sa;
   P.slot[1] = sb;
-  P.gen[0] = A.gen;
-  P.gen[1] = B.gen;
-  P.n_forests = 2;
+  P.gen[0] = F[0] ? F[0]->gen : 0;
+  P.gen[1] = F[1] ? F[1]->gen : 0;
+  P.n_forests = (F[0] ? 1 : 0) + (F[1] ? 1 : 0);
   P.D = D;
   P.nf = nf;
   P.kind[0] = FD_FOREST_XGB_BINARY_LOGISTIC;
   P.kind[1] = FD_FOREST_SKLEARN_IFOREST;
-  P.base_margin = hp[0].base_margin;
-  P.if_offset = B.if_offset;
-  P.if_denominator = B.if_denominator;
+  P.base_margin = F[0] ? hp[0].base_margin : 0.f;
+  P.if_offset = F[1] ? F[1]->if_offset : 0.0;
+  P.if_denominator = F[1] ? F[1]->if_denominator : 0.0;
   P.valid = true;
   return true;
+}
+
+bool plan_current(const Engine& e, const EnsemblePlan& P, int sa, int sb) {
+  return P.valid && P.slot[0] == sa && P.slot[1] == sb && P.gen[0] == (sa >= 0 ? e.forests[sa].gen : 0) &&
+         P.gen[1] == (sb >= 0 ? e.forests[sb].gen : 0);
 }
 
 }  // namespace
@@ -647,28 +674,13 @@ bool select_pair(Engine& e, const fd_blend_params& p, const int32_t* slots, cons
     ++k;
   }
   if (q.sa < 0 || q.sb < 0) return false;
-  EnsemblePlan& P = e.ens;
-  if (!P.valid || P.slot[0] != q.sa || P.slot[1] != q.sb || P.gen[0] != e.forests[q.sa].gen ||
-      P.gen[1] != e.forests[q.sb].gen) {
-    if (!build_plan(e, q.sa, q.sb)) return false;
-  }
+  if (!plan_current(e, e.ens, q.sa, q.sb) && !build_plan(e, e.ens, q.sa, q.sb)) return false;
   return true;
 }
 }  // namespace
 
-bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present, int64_t n) {
-  Pair q;
-  return select_pair(e, p, slots, present, n, q);
-}
-
-bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
-                     const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
-                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results) {
-  Pair q;
-  if (!select_pair(e, p, slots, present, n, q)) return false;
-  const int pa = q.pa, pb = q.pb, ma = q.ma, mb = q.mb;
-  EnsemblePlan& P = e.ens;
-  EnsArgs a{};
+namespace {
+void plan_args(const EnsemblePlan& P, const float* dX, int64_t n, int32_t ld, bool owner_fixed, EnsArgs& a) {
   a.X = dX;
   a.n = n;
   a.ld = ld;
@@ -676,7 +688,7 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
   a.thr = P.thr.as<const float>();
   FD_REQUIRE(P.nf <= kMaxFeatures, FD_ERR_UNSUPPORTED, "ensemble: more than 64 features");
   for (int f = 0; f <= P.nf; ++f) a.thr_off[f] = P.h_thr_off[f];
-  a.owner_fixed = e.ens_owner_fixed ? 1 : 0;
+  a.owner_fixed = owner_fixed ? 1 : 0;
   a.vec4 = (ld % 4 == 0 && (reinterpret_cast<uintptr_t>(dX) & 15u) == 0) ? 1 : 0;
   // binning passes: consecutive features whose tables fit bufA + bufB + the tiles; a larger table alone,
   // searched in global memory
@@ -704,6 +716,37 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
   a.base_margin = P.base_margin;
   a.if_offset = P.if_offset;
   a.if_denom = P.if_denominator;
+}
+
+// out: 0 blended columns, 1 route result records, 2 the single forest's probability column (a.fp)
+bool run_plan(Engine& e, const EnsemblePlan& P, EnsArgs& a, int out, int timing_kind) {
+  const void* fn = out == 1 ? pick_ensemble<1>(P.D) : out == 2 ? pick_ensemble<2>(P.D) : pick_ensemble<0>(P.D);
+  if (!fn) return false;
+  const size_t lds = ens_lds(P.nf, P.D);
+  FD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int64_t blocks = (a.n + kTile - 1) / kTile;
+  Engine::Timed* ev = e.timing ? e.next_event_pair(timing_kind) : nullptr;
+  if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
+  void* args[] = {&a};
+  FD_HIP(hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kEnsWG), args, lds, e.stream));
+  if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
+  return true;
+}
+}  // namespace
+
+bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present, int64_t n) {
+  Pair q;
+  return select_pair(e, p, slots, present, n, q);
+}
+
+bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
+                     const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
+                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results) {
+  Pair q;
+  if (!select_pair(e, p, slots, present, n, q)) return false;
+  const int pa = q.pa, pb = q.pb, ma = q.ma, mb = q.mb;
+  EnsArgs a{};
+  plan_args(e.ens, dX, n, ld, e.ens_owner_fixed, a);
   a.pos[0] = pa;
   a.pos[1] = pb;
   a.mcol[0] = ma;
@@ -718,17 +761,33 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
   a.res = results;
   const int out = results ? 1 : 0;
   FD_REQUIRE(out == 1 || dfp != nullptr, FD_ERR_INVALID_ARG, "null output");
-  const void* fn = out ? pick_ensemble<1>(P.D) : pick_ensemble<0>(P.D);
-  if (!fn) return false;
-  const size_t lds = ens_lds(P.nf, P.D);
-  FD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const int64_t blocks = (n + kTile - 1) / kTile;
-  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_ENSEMBLE) : nullptr;
-  if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
-  void* args[] = {&a};
-  FD_HIP(hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kEnsWG), args, lds, e.stream));
-  if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
-  return true;
+  return run_plan(e, e.ens, a, out, FD_TIMING_ENSEMBLE);
 }
+
+bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int32_t ld, double* dprob,
+                            hipStream_t stream) {
+  if (!e.ensemble_on || e.forest_variant != 0 || n <= 0) return false;
+  if ((n + kTile - 1) / kTile < kSplitTiles) return false;
+  if (slot < 0 || slot >= kMaxSlots || !e.forests[slot].loaded) return false;
+  const bool xgb = e.forests[slot].kind == FD_FOREST_XGB_BINARY_LOGISTIC;
+  const int sa = xgb ? slot : -1, sb = xgb ? -1 : slot;
+  EnsemblePlan& P = e.ens1[slot];
+  if (!plan_current(e, P, sa, sb) && !build_plan(e, P, sa, sb)) return false;
+  EnsArgs a{};
+  plan_args(P, dX, n, ld, e.ens_owner_fixed, a);
+  a.fp = dprob;
+  const hipStream_t saved = e.stream;
+  if (stream) e.stream = stream;
+  bool ok = false;
+  try {
+    ok = run_plan(e, P, a, 2, xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST);
+  } catch (...) {
+    e.stream = saved;
+    throw;
+  }
+  e.stream = saved;
+  return ok;
+}
+
 
 }  // namespace fd

@@ -270,6 +270,7 @@ struct Engine {
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
   DeviceBuffer route_blk, route_out, route_err;  // card-hash routing scratch (route.hip)
   EnsemblePlan ens;                              // fused XGBoost + IsolationForest + blend (ensemble.hip)
+  EnsemblePlan ens1[kMaxSlots];                  // the same kernel over one forest (forest predict), per slot
   bool route_err_live = false;
   // optional per-launch kernel timing (HIP events on the launch stream)
   int forest_variant = 0;  // "forest_kernel" option
@@ -380,6 +381,9 @@ void read_xgboost_json(const char* path, XgbModel& out);
 // slots and the batch is large (false: not applicable, the caller runs the per-model kernels + blend).
 // results != nullptr: write route result records (seq from records[i]) instead of the columns.
 bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present, int64_t n);
+// one forest's probabilities through the fused kernel (large batches, no raw / leaf outputs); false: not applicable
+bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int32_t ld, double* dprob,
+                            hipStream_t stream);
 bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
                      const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
                      uint8_t* drisk, const RouteRecord* records, ResultRecord* results);

@@ -1811,6 +1811,13 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
     return;
   }
 
+  // large batches, probabilities only: the fused ensemble kernel over this one forest (its u16 merged-bin tile,
+  // link-encoded nodes and LDS-staged leaves; the same f32 margin / f64 path-length sums in tree order)
+  if (v == 0 && !d_raw && !d_leaf) {
+    const int slot = (int)(&pf - e.forests);
+    if (slot >= 0 && slot < kMaxSlots && launch_ensemble_single(e, slot, d_X, n, ld, d_prob, stream)) return;
+  }
+
   // + 64 B: kernel 6's two item counters after the tile_any flags
   const size_t lds6 = pf.n_chunk ? lds_bytes_kernel3(pf.num_feature, pf.n_chunk_stride, pf.n_chunk, leaf_sz) + 64 : 0;
   const bool ok6 = pf.binned && pf.n_chunk > 0 && pf.depth <= 8 && lds6 <= kLdsBudget;

@@ -137,3 +137,41 @@ def test_sampled_kernel_timing(engine):
             np.testing.assert_array_equal(u, v)
     with pytest.raises(NativeError):
         engine.set_option("timing_every", 0)
+
+
+@pytest.mark.parametrize("kind,depth", [("xgb", 8), ("xgb", 6), ("if", 8)])
+def test_single_forest_fused_equals_kernel6(engine, kind, depth):
+    """fd_forest_predict on a large batch without raw / leaf outputs runs the fused kernel over the one forest
+    (_predict_xgboost / _predict_sklearn, ml/models/model_manager.py:309-311, 338-346): probabilities
+    bit-identical to forest kernel 6 (engine option ensemble = 0), NaNs and short rows included; and with raw
+    margins requested the call keeps kernel 6."""
+    nf = 64
+    xgb, ifm = _models(nf, depth, n_trees=150, n_if=50, seed=11 + depth)
+    model = xgb if kind == "xgb" else ifm
+    engine.load_forest(2, model)
+    X = synth.feature_matrix(N, nf, seed=5).astype(np.float32)
+    X[::113, 7] = np.nan
+    X[5::251, :] = np.nan
+    fused = engine.predict(2, X)
+    engine.set_option("ensemble", 0)
+    try:
+        k6, raw = engine.predict(2, X, want_raw=True)
+        k6b = engine.predict(2, X)
+    finally:
+        engine.set_option("ensemble", 1)
+    np.testing.assert_array_equal(fused, k6)
+    np.testing.assert_array_equal(fused, k6b)
+    _, raw1 = engine.predict(2, X, want_raw=True)  # raw requested: kernel 6 even with the option on
+    np.testing.assert_array_equal(raw1, raw)
+    short = np.ascontiguousarray(X[:, :48])  # rows shorter than num_feature: missing columns
+    np.testing.assert_array_equal(engine.predict(2, short), _k6(engine, 2, short))
+    ref = oracle.xgb_predict(model, X)[0].astype(np.float64) if kind == "xgb" else oracle.iforest_predict(model, X)[0]
+    assert np.abs(fused - ref).max() <= 1e-5
+
+
+def _k6(engine, slot, X):
+    engine.set_option("ensemble", 0)
+    try:
+        return engine.predict(slot, X)
+    finally:
+        engine.set_option("ensemble", 1)
