@@ -1,6 +1,6 @@
-# bench lines for the non-default workloads, pipelined and --no-pipeline (one gpurun call)
+# bench lines for non-default workloads (WORKLOADS), pipelined and --no-pipeline (VARIANTS), after the GPU tests in TESTS
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-T=${TAG:-s2w}
+T=${TAG:-wl}
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
 timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_pipeline.py} -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/$T.pytest.log 2>&1; rc=$?; tail -4 gpurun_out/$T.pytest.log; [ $rc -ne 0 ] && exit $rc
 fi

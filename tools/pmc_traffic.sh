@@ -1,6 +1,6 @@
 # HBM traffic (FETCH_SIZE / WRITE_SIZE passes, one rocprofv3 --pmc run each) of the default bench + config5 line
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-T=${TAG:-s2p}
+T=${TAG:-pmc}
 k=0
 for p in FETCH_SIZE WRITE_SIZE; do
   k=$((k + 1))
