@@ -286,17 +286,25 @@ int fd_engine_destroy(fd_engine* eng) {
   FD_API_END
 }
 
+// the new engine stream inherits the order of the old one over pipelined batches: their scoring is complete
+// before anything queued on it (fd_score_batch_pipelined's outputs stay ordered on the engine stream)
+static void rebind_stream(Engine& e, hipStream_t s) {
+  for (int k = 0; k < Engine::kPipeSlots; ++k)
+    if (e.pipe_done_live[k] && s != e.stream) FD_HIP(hipStreamWaitEvent(s, e.pipe_done_ev[k], 0));
+  e.stream = s;
+}
+
 int fd_engine_set_stream(fd_engine* eng, void* hip_stream) {
   FD_API_BEGIN
   Engine& e = E(eng);
-  e.stream = static_cast<hipStream_t>(hip_stream);
+  rebind_stream(e, static_cast<hipStream_t>(hip_stream));
   FD_API_END
 }
 
 int fd_engine_reset_stream(fd_engine* eng) {
   FD_API_BEGIN
   Engine& e = E(eng);
-  e.stream = e.own_stream;
+  rebind_stream(e, e.own_stream);
   FD_API_END
 }
 
