@@ -199,8 +199,10 @@ class ShardedScorer:
         return int(g.cpu()[0])
 
     def step(self, txns: dict, n: int, extras: Optional[dict] = None, windows: bool = False, sink: bool = False,
-             flush: bool = False):
+             flush: bool = False, input_ready=None):
         """txns: field -> tensor (n rows) on the backend's device, in arrival order.
+        input_ready: optional torch.cuda.Event recorded once `txns` were complete (a pipelined backend's features
+        wait for it instead of assuming resident inputs).
         -> (fraud_prob f64, confidence f64, decision u8, risk u8) tensors in the same order.
         extras: {"payment_method": u8, "is_fraud": u8} tensors (n rows) for the keyed aggregates.
         windows / sink: after scoring, run the Flink window aggregates / the sink aggregates on the owned
@@ -212,7 +214,8 @@ class ShardedScorer:
         if G == 1:  # one shard owns every card: no partition, no exchange
             self.last_counts = ([n], [n])
             if hasattr(self.be, "score_batch"):
-                out = self.be.score_batch(txns, n)
+                out = self.be.score_batch(txns, n, input_ready) if input_ready is not None else \
+                    self.be.score_batch(txns, n)
                 if aux:
                     cols = {f: txns[f] for f in ("card_key", "ts_ms", "amount_cents", "merchant")}
                     cols.update(extras or {})
