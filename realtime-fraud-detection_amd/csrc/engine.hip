@@ -273,10 +273,9 @@ int fd_engine_destroy(fd_engine* eng) {
       t.vvals[w].release();
     }
   }
-  for (auto* b : {&e.state.headers, &e.state.ring, &e.state.merchants, &e.state.slot, &e.state.err,
-                  &e.state.bucket_fill, &e.state.pairs, &e.state.ovf_cnt, &e.state.ovf_key, &e.state.ovf_b, &e.state.prep,
-                  &e.state.bucket_scr})
-    b->release();
+  for (auto* b : {&e.state.headers, &e.state.ring, &e.state.merchants, &e.state.err, &e.state.bucket_scr}) b->release();
+  for (auto& g : e.state.gs)
+    for (auto* b : {&g.slot, &g.bucket_fill, &g.pairs, &g.ovf_cnt, &g.ovf_key, &g.ovf_b, &g.prep}) b->release();
   for (auto& ev : e.events) {
     (void)hipEventDestroy(ev.a);
     (void)hipEventDestroy(ev.b);
@@ -786,7 +785,9 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
     e.pipe_dirty = false;
   }
   if (input_ready) FD_HIP(hipStreamWaitEvent(Sf, static_cast<hipEvent_t>(input_ready), 0));
-  if (!m2 && e.pipe_feat_live[prev]) FD_HIP(hipStreamWaitEvent(Sf, e.pipe_feat_ev[prev], 0));
+  // mode 1: the slot pass (scratch set s & 1, untouched by batch i-1) runs at once; the bucket pass waits for
+  // batch i-1's card updates
+  hipEvent_t before_buckets = (!m2 && e.pipe_feat_live[prev]) ? e.pipe_feat_ev[prev] : nullptr;
   if (m2 && e.pipe_done_live[s]) FD_HIP(hipStreamWaitEvent(Sf, e.pipe_done_ev[s], 0));
   e.pipe_vec[s].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
   float* vec = e.pipe_vec[s].as<float>();
@@ -800,7 +801,7 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
     e.pipe_seq[s].ensure((size_t)n * e.state.S * fd::kSeqInput * sizeof(float));
     seq = e.pipe_seq[s].as<float>();
   }
-  fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean);
+  fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, m2 ? 0 : s & 1, before_buckets);
   FD_HIP(hipEventRecord(e.pipe_feat_ev[s], Sf));
   e.pipe_feat_live[s] = true;
   if (m2) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_feat_ev[s], 0));

@@ -187,12 +187,15 @@ struct CardStore {
   int K = 1;         // ring events per card (sliding)
   int S = 0;         // LSTM history events per card (0 = off)
   int64_t n_merchants = 0;
-  DeviceBuffer headers, ring, merchants, slot, err, seq;
-  // per-batch card grouping (feat_slot -> feat_bucket): keys per bucket, [NB][C] bucket regions, overflow
-  // counters by batch parity + the overflow list (key, bucket), prep records
-  DeviceBuffer bucket_fill, pairs, ovf_cnt, ovf_key, ovf_b, prep,
-      bucket_scr;  // lean bucket kernel: per-bucket global working set of its slow path
-  int batch_parity = 0;
+  DeviceBuffer headers, ring, merchants, err, seq;
+  // per-batch card grouping (feat_slot -> feat_bucket): per-txn slots, keys per bucket, [NB][C] bucket regions,
+  // overflow counters by batch parity + the overflow list (key, bucket), prep records. Two sets: the pipelined
+  // stream alternates them, so batch i+1's slot kernel runs while batch i's bucket kernel still reads its set.
+  struct GroupScratch {
+    DeviceBuffer slot, bucket_fill, pairs, ovf_cnt, ovf_key, ovf_b, prep;
+    int batch_parity = 0;
+  } gs[2];
+  DeviceBuffer bucket_scr;  // lean bucket kernel: per-bucket global working set of its slow path
   DeviceBuffer uext, mext, vocab;  // extended profiles + vocabulary flags (feature map, rule scores)
   int64_t n_mext = 0;
   bool vocab_loaded = false;
@@ -344,7 +347,7 @@ void load_users(Engine& e, const fd_users& u);
 void load_merchants(Engine& e, const fd_merchants& m);
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw,
                      float* d_seq = nullptr, double* d_vel5 = nullptr, hipStream_t stream = nullptr,
-                     bool lean = false);
+                     bool lean = false, int set = 0, hipEvent_t before_buckets = nullptr);
 // the same over received 48-B route records (route.hip), no unpack pass; also returns nothing else
 void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq);
 void load_users_ext(Engine& e, const fd_users_ext& u);

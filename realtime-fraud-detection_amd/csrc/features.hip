@@ -1576,8 +1576,10 @@ void state_init(Engine& e, const fd_state_params& p) {
   // allocates for the new capacity)
   st.uext.release();
   st.err.ensure(16);
-  st.bucket_fill.ensure(kMaxBuckets * sizeof(unsigned));
-  st.ovf_cnt.ensure(2 * sizeof(unsigned));
+  for (auto& g : st.gs) {
+    g.bucket_fill.ensure(kMaxBuckets * sizeof(unsigned));
+    g.ovf_cnt.ensure(2 * sizeof(unsigned));
+  }
   st.ready = true;
   state_clear(e);
 }
@@ -1588,8 +1590,10 @@ void state_clear(Engine& e) {
   FD_HIP(hipMemsetAsync(st.headers.ptr, 0, (size_t)st.cap * sizeof(CardHeader), e.stream));
   if (st.uext.ptr) FD_HIP(hipMemsetAsync(st.uext.ptr, 0, (size_t)st.cap * sizeof(UserExt), e.stream));
   FD_HIP(hipMemsetAsync(st.err.ptr, 0, 16, e.stream));
-  FD_HIP(hipMemsetAsync(st.bucket_fill.ptr, 0, kMaxBuckets * sizeof(unsigned), e.stream));
-  FD_HIP(hipMemsetAsync(st.ovf_cnt.ptr, 0, 2 * sizeof(unsigned), e.stream));
+  for (auto& g : st.gs) {
+    FD_HIP(hipMemsetAsync(g.bucket_fill.ptr, 0, kMaxBuckets * sizeof(unsigned), e.stream));
+    FD_HIP(hipMemsetAsync(g.ovf_cnt.ptr, 0, 2 * sizeof(unsigned), e.stream));
+  }
   FD_HIP(hipStreamSynchronize(e.stream));
   // the window event logs hold card-table slots: clearing the table empties them too
   WindowState& w = e.windows;
@@ -1662,32 +1666,37 @@ namespace {
 
 // The grouping launch (feat_slot) + the bucket kernel over any transaction source.
 // lean: the pipelined stream's bucket pass (feat_bucket_lean_kernel: fits beside the ensemble kernel)
+// set: the scratch set (CardStore::gs); before_buckets: an event the bucket pass waits for (the previous batch's
+// card updates, pipelined stream) while the slot pass runs ahead
 void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, double* d_raw, float* d_seq,
-                    double* d_vel5, hipStream_t stream = nullptr, bool lean = false) {
+                    double* d_vel5, hipStream_t stream = nullptr, bool lean = false, int set = 0,
+                    hipEvent_t before_buckets = nullptr) {
   CardStore& st = e.state;
+  CardStore::GroupScratch& g = st.gs[set];
   const hipStream_t s = stream ? stream : e.stream;
   FD_REQUIRE(n <= (int64_t)kMaxBins * kChunkCap, FD_ERR_INVALID_ARG, "micro-batch larger than 16M transactions");
-  st.slot.ensure((size_t)n * 4);
-  st.prep.ensure((size_t)n * sizeof(Prep));
+  g.slot.ensure((size_t)n * 4);
+  g.prep.ensure((size_t)n * sizeof(Prep));
   if (st.merchants.ptr == nullptr) st.merchants.ensure(16);
   const unsigned nb = buckets_for(n, st.cap);
   // bucket capacity: 4x the mean (Poisson tail beyond it is negligible for hashed cards; skewed batches spill
   // to the overflow list), a multiple of 64
   const unsigned C = (unsigned)std::max<int64_t>(512, ((4 * ((n + nb - 1) / nb)) + 63) / 64 * 64);
-  st.pairs.ensure((size_t)nb * C * 8);
-  st.ovf_key.ensure((size_t)n * 8);
-  st.ovf_b.ensure((size_t)n * 4);
-  const int par = st.batch_parity;
-  st.batch_parity ^= 1;
+  g.pairs.ensure((size_t)nb * C * 8);
+  g.ovf_key.ensure((size_t)n * 8);
+  g.ovf_b.ensure((size_t)n * 4);
+  const int par = g.batch_parity;
+  g.batch_parity ^= 1;
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, s));
   hipLaunchKernelGGL(feat_slot_kernel, dim3((unsigned)((n + kST - 1) / kST)), dim3(kST), 2 * nb * sizeof(unsigned),
                      s, st.headers.as<CardHeader>(), (long long)(st.cap - 1), n, src,
-                     st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, C, st.slot.as<unsigned>(),
-                     st.prep.as<Prep>(), st.bucket_fill.as<unsigned>(), st.pairs.as<unsigned long long>(),
-                     st.ovf_cnt.as<unsigned>() + par, st.ovf_key.as<unsigned long long>(), st.ovf_b.as<unsigned>(),
+                     st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, C, g.slot.as<unsigned>(),
+                     g.prep.as<Prep>(), g.bucket_fill.as<unsigned>(), g.pairs.as<unsigned long long>(),
+                     g.ovf_cnt.as<unsigned>() + par, g.ovf_key.as<unsigned long long>(), g.ovf_b.as<unsigned>(),
                      st.err.as<unsigned>());
   FD_HIP(hipGetLastError());
+  if (before_buckets) FD_HIP(hipStreamWaitEvent(s, before_buckets, 0));
   static bool attrs = false;
   if (!attrs) {  // > 48 KiB of dynamic LDS
     FD_HIP(hipFuncSetAttribute((const void*)feat_bucket_kernel<FD_WINDOW_SLIDING>,
@@ -1701,15 +1710,15 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.ring = st.ring.as<RingEvent>();
   a.K = st.K;
   a.n = n;
-  a.prep = st.prep.as<const Prep>();
+  a.prep = g.prep.as<const Prep>();
   a.out = Outputs{d_vec, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S};
-  a.fill = st.bucket_fill.as<unsigned>();
-  a.pairs = st.pairs.as<const unsigned long long>();
+  a.fill = g.bucket_fill.as<unsigned>();
+  a.pairs = g.pairs.as<const unsigned long long>();
   a.C = C;
-  a.ovf_cnt = st.ovf_cnt.as<unsigned>();
+  a.ovf_cnt = g.ovf_cnt.as<unsigned>();
   a.par = par;
-  a.ovf_key = st.ovf_key.as<const unsigned long long>();
-  a.ovf_b = st.ovf_b.as<const unsigned>();
+  a.ovf_key = g.ovf_key.as<const unsigned long long>();
+  a.ovf_b = g.ovf_b.as<const unsigned>();
   const size_t lds = kBucketLds;
   if (lean) {
     st.bucket_scr.ensure((size_t)nb * sizeof(BucketScratch));
@@ -1730,7 +1739,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
 }  // namespace
 
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw, float* d_seq,
-                     double* d_vel5, hipStream_t stream, bool lean) {
+                     double* d_vel5, hipStream_t stream, bool lean, int set, hipEvent_t before_buckets) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
   FD_REQUIRE(d_vec != nullptr, FD_ERR_INVALID_ARG, "null vector output");
@@ -1743,7 +1752,7 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
   TxnSrc src{reinterpret_cast<const unsigned long long*>(t.card_key), reinterpret_cast<const long long*>(t.ts_ms),
              reinterpret_cast<const long long*>(t.amount_cents), reinterpret_cast<const int*>(t.merchant),
              reinterpret_cast<const unsigned long long*>(t.device_fp), t.ip_class, t.hour, t.weekend, nullptr};
-  launch_grouped(e, src, n, d_vec, d_raw, d_seq, d_vel5, stream, lean);
+  launch_grouped(e, src, n, d_vec, d_raw, d_seq, d_vel5, stream, lean, set, before_buckets);
 }
 
 void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq) {
@@ -1853,7 +1862,7 @@ void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context
                      st.uext.ptr ? st.uext.as<const UserExt>() : nullptr,
                      st.merchants.as<const Merchant>(), st.mext.ptr ? st.mext.as<const MerchExt>() : nullptr,
                      (int)st.n_merchants, (int)st.n_mext, n, a, ca,
-                     st.slot.as<const unsigned>(), raw, vel5, st.vocab.as<const unsigned char>(), st.tp_threshold,
+                     st.gs[0].slot.as<const unsigned>(), raw, vel5, st.vocab.as<const unsigned char>(), st.tp_threshold,
                      d_fmap, d_rules);
   FD_HIP(hipGetLastError());
 }
