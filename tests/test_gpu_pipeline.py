@@ -189,3 +189,69 @@ def test_pipelined_lstm_and_latency_batches(world):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_sharded_scorer_with_windows_and_sink():
+    """ShardedScorer at world size 1 over EngineShardBackend(pipelined=True) — the bench's product path — with the
+    Flink window aggregates (a5) and the sink aggregates (f3) run on every step's scores: scores, fired user /
+    merchant windows and sink queries identical to the same scorer over fd_score_batch_device."""
+    import torch
+
+    from fdengine.sharding import EngineShardBackend, ShardedScorer
+    pop = synth.population(20000, 80, seed=71)
+    B, steps = 40000, 4
+    tx = synth.txn_stream(pop, B * steps, seed=72, rate_per_s=20.0)
+    rng = np.random.default_rng(80)
+    pm = rng.integers(0, 6, B * steps).astype(np.uint8)
+    X = synth.feature_matrix(3000, 64, seed=73)
+    xgb = xgboost_from_json_doc(synth.xgboost_doc(80, 8, 64, X, seed=74, p_leaf=0.1))
+    ifm = iforest_from_sklearn(synth.isolation_forest(X.astype(np.float64), n_estimators=30))
+    params = FraudEngine.blend_params([0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
+    U, M = pop["users"], pop["merchants"]
+    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f])).cuda() for f in TXN_FIELDS}
+    extras = {"payment_method": torch.from_numpy(pm).cuda(),
+              "is_fraud": torch.from_numpy(tx["is_fraud"].astype(np.uint8)).cuda()}
+    torch.cuda.synchronize()
+    results, engines = [], []
+    try:
+        for pipelined in (False, True):
+            e = FraudEngine(0)
+            engines.append(e)
+            e.state_init(1 << 17, 1, 16)
+            e.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+            e.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+            e.load_forest(0, xgb)
+            e.load_forest(1, ifm)
+            e.windows_init(1 << 18)
+            e.sink_init(1 << 14, 1 << 18)
+            sc = ShardedScorer(EngineShardBackend(e, params, [0, 1], pipelined=pipelined), 0, 1)
+            scores, users, merchants = [], [], []
+            for s in range(steps):
+                sl = slice(s * B, (s + 1) * B)
+                out = sc.step({f: t[sl] for f, t in dev.items()}, B,
+                              extras={k: v[sl] for k, v in extras.items()}, windows=True, sink=True,
+                              flush=s == steps - 1)
+                scores.append([o.cpu().numpy() for o in out])
+                uw, mw = sc.last_windows
+                users.append(uw)
+                merchants.append(mw)
+            hours = sorted({int(t) // 3_600_000 for t in tx["ts_ms"]})
+            sink = sc.sink_query(1, hours)
+            results.append((scores, users, merchants, sink))
+        (s0, u0, m0, k0), (s1, u1, m1, k1) = results
+        for a, b in zip(s0, s1):
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
+        # fired windows per step as sets (their order follows card-table slots, which concurrent first inserts
+        # of new cards may assign differently)
+        for a, b, key in [(x, y, ("user_key", "window_start")) for x, y in zip(u0, u1)] + \
+                         [(x, y, ("merchant", "window_start")) for x, y in zip(m0, m1)]:
+            assert len(a) == len(b)
+            ia, ib = np.lexsort([a[k] for k in key[::-1]]), np.lexsort([b[k] for k in key[::-1]])
+            assert bool((a[ia].tobytes() == b[ib].tobytes())), "fired windows differ"
+        assert sum(len(w) for w in u0) > 0 and sum(len(w) for w in m0) > 0
+        assert bool(k0.tobytes() == k1.tobytes()), "sink aggregates differ"
+    finally:
+        for e in engines:
+            e.close()
