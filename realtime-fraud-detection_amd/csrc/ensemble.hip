@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   const int nA = a.n_chunks[0], G = nA + a.n_chunks[1];
 
 #ifdef FD_FOREST_PROFILE
-  unsigned long long pr_top = 0, pr_walk = 0, pr_sync = 0, pr_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long pr_top = 0, pr_walk = 0, pr_sync = 0, pr_dma = 0, pr_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   FD_ESTAMP(pr_t0);
   // above the feature kernels of the next micro-batch that share the CU in the pipelined stream (priority 0):
@@ -419,11 +419,15 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     lds_store<unsigned long long>(tw + (uint32_t)(gg * kTile + txn) * 8u, w);
     FD_ESTAMP(q2);
     if (owner) dma_wait();
+#ifdef FD_FOREST_PROFILE
+    const unsigned long long q2d = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
 #ifdef FD_FOREST_PROFILE
     const unsigned long long q3 = __builtin_amdgcn_s_memtime();
     pr_top += q1 - q0;
     pr_walk += q2 - q1;
+    pr_dma += q2d - q2;
     pr_sync += q3 - q2;
 #endif
   }
@@ -442,6 +446,7 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     o[1] = pr_top;
     o[2] = pr_walk;
     o[3] = pr_sync;
+    o[13] = pr_dma;  // of pr_sync: the owner waves' wait for their chunk DMA (0 for the other waves)
     o[4] = pr_t0;
     o[5] = __builtin_amdgcn_s_memtime();
   }

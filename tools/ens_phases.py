@@ -53,6 +53,8 @@ for k, nm in enumerate(["prologue", "loop top", "walk+leaf", "wait+barrier"]):
     print(f"  {nm:13s} {np.median(v):9.0f} {np.percentile(v, 10):9.0f} {np.percentile(v, 90):9.0f}"
           f"   share {np.median(v / tot):.3f}")
 print(f"  {'total':13s} {np.median(tot):9.0f} {np.percentile(tot, 10):9.0f} {np.percentile(tot, 90):9.0f}")
+dm = p[:, :, 13][:, :4]  # tree group 0 (the chunk owner) waits for its LDS-DMA before the barrier
+print(f"  owner DMA wait (group 0, inside wait+barrier): median {np.median(dm):.0f} p90 {np.percentile(dm, 90):.0f}")
 wk = p[:, :, 2]
 print("  walk+leaf by tree group (median):", [float(np.median(wk[:, g * 4:(g + 1) * 4])) for g in range(4)])
 st = p[:, :, 6:13]
