@@ -273,7 +273,8 @@ int fd_engine_destroy(fd_engine* eng) {
       t.vvals[w].release();
     }
   }
-  for (auto* b : {&e.state.headers, &e.state.ring, &e.state.merchants, &e.state.err, &e.state.bucket_scr}) b->release();
+  for (auto* b : {&e.state.headers, &e.state.keys, &e.state.ring, &e.state.merchants, &e.state.err, &e.state.bucket_scr})
+    b->release();
   for (auto& g : e.state.gs)
     for (auto* b : {&g.slot, &g.bucket_fill, &g.pairs, &g.ovf_cnt, &g.ovf_key, &g.ovf_b, &g.prep}) b->release();
   for (auto& ev : e.events) {

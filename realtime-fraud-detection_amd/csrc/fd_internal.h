@@ -179,6 +179,40 @@ struct __attribute__((aligned(128))) CardHeader {
 static_assert(sizeof(CardHeader) == 128, "CardHeader must be one 128-B line");
 constexpr int kCardHeaderBytes = (int)sizeof(CardHeader);
 
+#ifdef __HIP_DEVICE_COMPILE__
+#define FD_CARD_SLOT_QUAL __device__ __forceinline__
+#else
+#define FD_CARD_SLOT_QUAL __device__ inline
+#endif
+// Card-table probe (murmur3 fmix64 home slot, linear probing) over the compact key array `keys` (8 B per slot,
+// CardStore::keys): the probes' random accesses stay inside 8 x capacity bytes, a range the GPU's TLBs reach,
+// instead of the 128-B headers. An insert mirrors the key into the slot's header (snapshots and occupancy read
+// it there). Returns the slot, -1 when the table is full.
+FD_CARD_SLOT_QUAL long long card_slot(unsigned long long* keys, CardHeader* hdr, long long mask, unsigned long long key) {
+  if (key == 0ull) key = 1ull;  // 0 marks an empty slot
+  unsigned long long m = key;
+  m ^= m >> 33;
+  m *= 0xff51afd7ed558ccdULL;
+  m ^= m >> 33;
+  m *= 0xc4ceb9fe1a85ec53ULL;
+  m ^= m >> 33;
+  long long h = (long long)(m & (unsigned long long)mask);
+  for (long long p = 0; p <= mask; ++p) {
+    const unsigned long long k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == key) return h;
+    if (k == 0ull) {
+      const unsigned long long old = atomicCAS(&keys[h], 0ull, key);
+      if (old == 0ull) {
+        hdr[h].key = key;
+        return h;
+      }
+      if (old == key) return h;
+    }
+    h = (h + 1) & mask;
+  }
+  return -1;
+}
+
 // HBM-resident keyed card state (features.hip)
 struct CardStore {
   bool ready = false;
@@ -187,7 +221,7 @@ struct CardStore {
   int K = 1;         // ring events per card (sliding)
   int S = 0;         // LSTM history events per card (0 = off)
   int64_t n_merchants = 0;
-  DeviceBuffer headers, ring, merchants, err, seq;
+  DeviceBuffer headers, keys, ring, merchants, err, seq;  // keys: the compact key array card_slot probes
   // per-batch card grouping (feat_slot -> feat_bucket): per-txn slots, keys per bucket, [NB][C] bucket regions,
   // overflow counters by batch parity + the overflow list (key, bucket), prep records. Two sets: the pipelined
   // stream alternates them, so batch i+1's slot kernel runs while batch i's bucket kernel still reads its set.

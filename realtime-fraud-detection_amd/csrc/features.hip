@@ -79,28 +79,14 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long k) {
   return k;
 }
 
-__device__ long long find_or_insert(CardHeader* H, long long mask, unsigned long long key) {
-  if (key == 0ull) key = 1ull;  // 0 marks an empty slot
-  long long h = (long long)(mix64(key) & (unsigned long long)mask);
-  for (long long p = 0; p <= mask; ++p) {
-    const unsigned long long k = __hip_atomic_load(&H[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k == key) return h;
-    if (k == 0ull) {
-      const unsigned long long old = atomicCAS(&H[h].key, 0ull, key);
-      if (old == 0ull || old == key) return h;
-    }
-    h = (h + 1) & mask;
-  }
-  return -1;
-}
 
-__global__ void __launch_bounds__(256) users_load_kernel(CardHeader* H, long long mask, int64_t n,
+__global__ void __launch_bounds__(256) users_load_kernel(CardHeader* H, unsigned long long* K, long long mask, int64_t n,
                                                          const unsigned long long* key, const double* avg,
                                                          const int* age, const unsigned long long* dfp,
                                                          unsigned* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const long long s = find_or_insert(H, mask, key[i]);
+  const long long s = card_slot(K, H, mask, key[i]);
   if (s < 0) {
     atomicOr(err, 1u);
     return;
@@ -260,7 +246,7 @@ __device__ __forceinline__ Prep load_prep(const Prep* __restrict__ src) {
 // (block, bucket) reserving the block's run, then each key at its rank in the run. A bucket that outgrows its
 // capacity C spills the rest to an overflow list (bucket id + key) its bucket kernel scans. No count / scan /
 // scatter passes: the bucket kernel's inputs are complete when this kernel ends.
-__global__ void __launch_bounds__(kST) feat_slot_kernel(CardHeader* H, long long mask, int64_t n, TxnSrc src,
+__global__ void __launch_bounds__(kST) feat_slot_kernel(CardHeader* H, unsigned long long* K, long long mask, int64_t n, TxnSrc src,
                                                         const Merchant* __restrict__ merchants, int nm,
                                                         unsigned nbm, unsigned C, unsigned* __restrict__ slot,
                                                         Prep* __restrict__ prep, unsigned* __restrict__ fill,
@@ -278,7 +264,7 @@ __global__ void __launch_bounds__(kST) feat_slot_kernel(CardHeader* H, long long
   bool have = false;
   if (i < n) {
     const Txn t = src.get(i);  // in flight with the probe
-    const long long s = find_or_insert(H, mask, src.get_key(i));
+    const long long s = card_slot(K, H, mask, src.get_key(i));
     store_prep(prep + i, make_prep(t, merchants, nm));
     if (s < 0) {
       atomicOr(err, 1u);
@@ -1529,12 +1515,12 @@ __global__ void __launch_bounds__(256) feat_ext_kernel(const CardHeader* __restr
   rules[i] = out;
 }
 
-__global__ void __launch_bounds__(256) users_ext_load_kernel(CardHeader* H, UserExt* U, long long mask, int64_t n,
+__global__ void __launch_bounds__(256) users_ext_load_kernel(CardHeader* H, unsigned long long* K, UserExt* U, long long mask, int64_t n,
                                                              const unsigned long long* key, const UserExt* src,
                                                              unsigned* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const long long s = find_or_insert(H, mask, key[i]);
+  const long long s = card_slot(K, H, mask, key[i]);
   if (s < 0) {
     atomicOr(err, 1u);
     return;
@@ -1569,6 +1555,7 @@ void state_init(Engine& e, const fd_state_params& p) {
   st.mode = p.window_mode;
   st.K = p.window_mode == FD_WINDOW_SLIDING ? p.ring_k : 1;
   st.headers.ensure((size_t)cap * sizeof(CardHeader));
+  st.keys.ensure((size_t)cap * sizeof(unsigned long long));
   st.ring.ensure((size_t)cap * st.K * sizeof(RingEvent));
   st.S = p.seq_len;
   if (st.S) st.seq.ensure((size_t)cap * st.S * kSeqInput * sizeof(float));
@@ -1588,6 +1575,7 @@ void state_clear(Engine& e) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
   FD_HIP(hipMemsetAsync(st.headers.ptr, 0, (size_t)st.cap * sizeof(CardHeader), e.stream));
+  FD_HIP(hipMemsetAsync(st.keys.ptr, 0, (size_t)st.cap * sizeof(unsigned long long), e.stream));
   if (st.uext.ptr) FD_HIP(hipMemsetAsync(st.uext.ptr, 0, (size_t)st.cap * sizeof(UserExt), e.stream));
   FD_HIP(hipMemsetAsync(st.err.ptr, 0, 16, e.stream));
   for (auto& g : st.gs) {
@@ -1645,6 +1633,7 @@ void load_users(Engine& e, const fd_users& u) {
   FD_HIP(hipMemcpyAsync(g.ptr, u.account_age_days, u.n * 4, hipMemcpyHostToDevice, e.stream));
   FD_HIP(hipMemcpyAsync(f.ptr, u.device_fp, u.n * 24, hipMemcpyHostToDevice, e.stream));
   hipLaunchKernelGGL(users_load_kernel, dim3(grid_for(u.n)), dim3(256), 0, e.stream, st.headers.as<CardHeader>(),
+                     st.keys.as<unsigned long long>(),
                      (long long)(st.cap - 1), u.n, k.as<const unsigned long long>(), a.as<const double>(),
                      g.as<const int>(), f.as<const unsigned long long>(), st.err.as<unsigned>());
   FD_HIP(hipGetLastError());
@@ -1690,7 +1679,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, s));
   hipLaunchKernelGGL(feat_slot_kernel, dim3((unsigned)((n + kST - 1) / kST)), dim3(kST), 2 * nb * sizeof(unsigned),
-                     s, st.headers.as<CardHeader>(), (long long)(st.cap - 1), n, src,
+                     s, st.headers.as<CardHeader>(), st.keys.as<unsigned long long>(), (long long)(st.cap - 1), n, src,
                      st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, C, g.slot.as<unsigned>(),
                      g.prep.as<Prep>(), g.bucket_fill.as<unsigned>(), g.pairs.as<unsigned long long>(),
                      g.ovf_cnt.as<unsigned>() + par, g.ovf_key.as<unsigned long long>(), g.ovf_b.as<unsigned>(),
@@ -1799,6 +1788,7 @@ void load_users_ext(Engine& e, const fd_users_ext& u) {
   FD_HIP(hipMemcpyAsync(k.ptr, u.key, u.n * 8, hipMemcpyHostToDevice, e.stream));
   FD_HIP(hipMemcpyAsync(d.ptr, h.data(), h.size() * sizeof(UserExt), hipMemcpyHostToDevice, e.stream));
   hipLaunchKernelGGL(users_ext_load_kernel, dim3(grid_for(u.n)), dim3(256), 0, e.stream, st.headers.as<CardHeader>(),
+                     st.keys.as<unsigned long long>(),
                      st.uext.as<UserExt>(), (long long)(st.cap - 1), u.n, k.as<const unsigned long long>(),
                      d.as<const UserExt>(), st.err.as<unsigned>());
   FD_HIP(hipGetLastError());

@@ -112,21 +112,6 @@ __device__ __forceinline__ bool owned(unsigned long long key, unsigned shard, un
 }
 
 // features.hip find_or_insert over a strided key array
-__device__ long long slot_of(unsigned long long* keys, size_t stride, long long mask, unsigned long long key) {
-  if (key == 0ull) key = 1ull;
-  long long h = (long long)(smix64(key) & (unsigned long long)mask);
-  for (long long p = 0; p <= mask; ++p) {
-    unsigned long long* kp = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(keys) + (size_t)h * stride);
-    const unsigned long long k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k == key) return h;
-    if (k == 0ull) {
-      const unsigned long long old = atomicCAS(kp, 0ull, key);
-      if (old == 0ull || old == key) return h;
-    }
-    h = (h + 1) & mask;
-  }
-  return -1;
-}
 
 __global__ void __launch_bounds__(256) snap_flag_kernel(const uint4* __restrict__ headers, long long lo, long long n,
                                                         unsigned char* __restrict__ flags) {
@@ -145,7 +130,7 @@ __global__ void __launch_bounds__(256) snap_gather_kernel(Planes P, RecMap m, co
   out[t] = *plane_word(P, m, (long long)slots[r], w);
 }
 
-__global__ void __launch_bounds__(256) restore_slot_kernel(unsigned long long* keys, long long mask,
+__global__ void __launch_bounds__(256) restore_slot_kernel(unsigned long long* keys, CardHeader* headers, long long mask,
                                                            const uint4* __restrict__ recs, int words, long long n,
                                                            unsigned shard, unsigned G, long long* __restrict__ slots,
                                                            unsigned long long* restored, unsigned* err) {
@@ -155,7 +140,7 @@ __global__ void __launch_bounds__(256) restore_slot_kernel(unsigned long long* k
   const unsigned long long key = ((unsigned long long)h.y << 32) | h.x;
   long long s = -1;
   if (owned(key, shard, G)) {
-    s = slot_of(keys, kCardHeaderBytes, mask, key);
+    s = card_slot(keys, headers, mask, key);
     if (s < 0)
       atomicOr(err, 1u);
     else
@@ -177,7 +162,7 @@ __global__ void __launch_bounds__(256) restore_scatter_kernel(Planes P, RecMap m
 
 // window events (windows.hip WinEvent: ts @0, cents @8, card key @16, slot @24): filter by owner, re-slot
 // through the card table, append to the log
-__global__ void __launch_bounds__(256) restore_events_kernel(unsigned long long* keys, long long mask,
+__global__ void __launch_bounds__(256) restore_events_kernel(unsigned long long* keys, CardHeader* headers, long long mask,
                                                              const unsigned char* __restrict__ in, long long n,
                                                              unsigned shard, unsigned G, unsigned char* __restrict__ log,
                                                              unsigned long long* count, unsigned* err) {
@@ -186,7 +171,7 @@ __global__ void __launch_bounds__(256) restore_events_kernel(unsigned long long*
   const unsigned char* ev = in + i * kWinEventBytes;
   const unsigned long long key = *reinterpret_cast<const unsigned long long*>(ev + 16);
   if (!owned(key, shard, G)) return;
-  const long long s = slot_of(keys, kCardHeaderBytes, mask, key);
+  const long long s = card_slot(keys, headers, mask, key);
   if (s < 0) {
     atomicOr(err, 1u);
     return;
@@ -478,7 +463,7 @@ void state_restore(Engine& e, const char* path, int shard, int n_shards, int fla
     read_all(in.f, pin.p, (size_t)n * rec_bytes, &h_cards);
     FD_HIP(hipMemcpyAsync(recs.ptr, pin.p, (size_t)n * rec_bytes, hipMemcpyHostToDevice, e.stream));
     hipLaunchKernelGGL(restore_slot_kernel, dim3(blocks(n)), dim3(256), 0, e.stream,
-                       reinterpret_cast<unsigned long long*>(st.headers.ptr), (long long)(st.cap - 1),
+                       st.keys.as<unsigned long long>(), st.headers.as<CardHeader>(), (long long)(st.cap - 1),
                        recs.as<const uint4>(), m.words, (long long)n, (unsigned)shard, (unsigned)n_shards,
                        slots.as<long long>(), d_restored, d_err);
     FD_HIP(hipGetLastError());
@@ -546,7 +531,7 @@ void state_restore(Engine& e, const char* path, int shard, int n_shards, int fla
         read_all(in.f, pin.p, (size_t)n * kWinEventBytes, &hh);
         FD_HIP(hipMemcpyAsync(recs.ptr, pin.p, (size_t)n * kWinEventBytes, hipMemcpyHostToDevice, e.stream));
         hipLaunchKernelGGL(restore_events_kernel, dim3(blocks(n)), dim3(256), 0, e.stream,
-                           reinterpret_cast<unsigned long long*>(st.headers.ptr), (long long)(st.cap - 1),
+                           st.keys.as<unsigned long long>(), st.headers.as<CardHeader>(), (long long)(st.cap - 1),
                            recs.as<const unsigned char>(), (long long)n, (unsigned)shard, (unsigned)n_shards,
                            log.as<unsigned char>(), d_count, d_err);
         FD_HIP(hipGetLastError());

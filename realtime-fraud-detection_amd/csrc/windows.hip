@@ -53,31 +53,8 @@ static_assert(sizeof(WinEvent) == 40, "WinEvent must be 40 B");
 
 constexpr long long kUserSize = 300000, kUserSlide = 60000, kMerchSize = 3600000;
 
-__device__ __forceinline__ unsigned long long wmix64(unsigned long long k) {
-  k ^= k >> 33;
-  k *= 0xff51afd7ed558ccdULL;
-  k ^= k >> 33;
-  k *= 0xc4ceb9fe1a85ec53ULL;
-  k ^= k >> 33;
-  return k;
-}
 
 // the card table's slot of a key (insert when absent, as feat_assign does)
-__device__ long long win_slot(unsigned long long* keys, size_t stride, long long mask, unsigned long long key) {
-  if (key == 0ull) key = 1ull;
-  long long h = (long long)(wmix64(key) & (unsigned long long)mask);
-  for (long long p = 0; p <= mask; ++p) {
-    unsigned long long* kp = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(keys) + (size_t)h * stride);
-    const unsigned long long k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k == key) return h;
-    if (k == 0ull) {
-      const unsigned long long old = atomicCAS(kp, 0ull, key);
-      if (old == 0ull || old == key) return h;
-    }
-    h = (h + 1) & mask;
-  }
-  return -1;
-}
 
 __device__ __forceinline__ long long floor_div(long long a, long long b) {
   long long q = a / b;
@@ -85,7 +62,7 @@ __device__ __forceinline__ long long floor_div(long long a, long long b) {
   return q;
 }
 
-__global__ void __launch_bounds__(256) win_append_kernel(unsigned long long* card_keys, size_t header_stride,
+__global__ void __launch_bounds__(256) win_append_kernel(unsigned long long* card_keys, CardHeader* headers,
                                                          long long mask, int64_t n, const unsigned long long* key,
                                                          const long long* ts, const long long* cents,
                                                          const int* merchant, const unsigned char* pm,
@@ -94,7 +71,7 @@ __global__ void __launch_bounds__(256) win_append_kernel(unsigned long long* car
                                                          unsigned long long* min_ts, unsigned* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const long long s = win_slot(card_keys, header_stride, mask, key[i]);
+  const long long s = card_slot(card_keys, headers, mask, key[i]);
   if (s < 0) {
     atomicOr(err, 1u);
     return;
@@ -439,7 +416,7 @@ void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, 
     WinEvent* ul = w.ulog[w.ucur].as<WinEvent>() + w.ucount;
     WinEvent* ml = w.mlog[w.mcur].as<WinEvent>() + w.mcount;
     hipLaunchKernelGGL(win_append_kernel, dim3(g256(n)), dim3(256), 0, e.stream,
-                       reinterpret_cast<unsigned long long*>(st.headers.ptr), (size_t)kCardHeaderBytes, (long long)(st.cap - 1), n,
+                       st.keys.as<unsigned long long>(), st.headers.as<CardHeader>(), (long long)(st.cap - 1), n,
                        reinterpret_cast<const unsigned long long*>(t.card_key),
                        reinterpret_cast<const long long*>(t.ts_ms), reinterpret_cast<const long long*>(t.amount_cents),
                        reinterpret_cast<const int*>(t.merchant), in.payment_method, in.is_fraud, in.fraud_score, ul,
