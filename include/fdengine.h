@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 12
+#define FD_ABI_VERSION 13
 
 enum fd_status {
   FD_OK = 0,
@@ -610,8 +610,15 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      "ensemble": 1 fused XGBoost + IsolationForest + blend kernel when applicable (default), 0 per-model kernels
      "lstm_rows": LSTM tile, 0 auto (4 transactions below 4096, else 16), 4 or 16
      "timing_every": N >= 1, fd_engine_set_timing records HIP events on one launch in N of each timing kind
-     (the others run without event records; fd_timing_read's launch count is the timed ones) */
+     (the others run without event records; fd_timing_read's launch count is the timed ones)
+     "graphs": 1 fd_score_batch_device runs latency batches (< 32768 transactions, no external probability
+     columns) as a replayed hipGraph per (size, models, outputs, stream, grouping parity): the transaction columns
+     are gathered into engine staging by one kernel, then one graph launch; the first batch of a shape runs
+     directly and captures the graph; any other engine call, a moved engine buffer or a timed (sampled) step
+     falls back to direct launches. 0 (default) direct launches. Same results bit for bit. */
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
+/* Engine counters (diagnostics): "graphs_captured", "graphs_replayed" (fd_score_batch_device graph option). */
+int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value);
 int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches);
 int fd_timing_reset(fd_engine* eng);
 

@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <atomic>
 #include <vector>
 
 #include "fdengine.h"
@@ -43,6 +44,10 @@ void set_error(const std::string& msg);
   } while (0)
 
 // Device allocation owned by the engine; grows, never shrinks.
+// bumped by every device (re)allocation or free: a captured hipGraph bakes buffer pointers in, so graphs
+// captured before a change are dropped (engine.hip score_batch_graph)
+inline std::atomic<unsigned long long> g_alloc_gen{0};
+
 struct DeviceBuffer {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -51,9 +56,13 @@ struct DeviceBuffer {
     release();
     FD_HIP(hipMalloc(&ptr, need));
     bytes = need;
+    ++g_alloc_gen;
   }
   void release() {
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) {
+      (void)hipFree(ptr);
+      ++g_alloc_gen;
+    }
     ptr = nullptr;
     bytes = 0;
   }
@@ -302,6 +311,19 @@ struct Engine {
   int pipe_mode = 1;       // "pipeline_mode" option
   bool pipe_lean = true;   // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
   DeviceBuffer pipe_vec[kPipeSlots], pipe_seq[kPipeSlots];
+  // fd_score_batch_device for latency batches as a replayed hipGraph ("graphs" option, engine.hip): the inputs
+  // are gathered into fixed staging by one kernel, the rest of the step is one graph launch; a graph per
+  // (shape, models, outputs, stream, grouping parity), all dropped by any other engine call (graph_epoch)
+  bool graphs_on = false;
+  struct GraphEntry {
+    std::vector<char> key;
+    hipGraphExec_t exec;
+  };
+  std::vector<GraphEntry> graphs;
+  unsigned long long graph_epoch = 0, graphs_epoch = 0, graphs_gen = 0, graph_seq = 0;
+  DeviceBuffer graph_in;
+  hipStream_t graph_cap_stream = nullptr;
+  unsigned long long graphs_captured = 0, graphs_replayed = 0;
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns

@@ -289,6 +289,7 @@ SIGNATURES = {
     "fd_ingest_scalar_host": (C.c_int, [_i32, _vp, _i32, _dp, C.POINTER(_i64), C.POINTER(_i32)]),
     "fd_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fd_engine_set_option": (C.c_int, [_vp, C.c_char_p, _i64]),
+    "fd_engine_get_counter": (C.c_int, [_vp, C.c_char_p, C.POINTER(_i64)]),
     "fd_timing_read": (C.c_int, [_vp, C.c_int, _dp, C.POINTER(_i64)]),
     "fd_timing_reset": (C.c_int, [_vp]),
     "fd_pack_forest_host": (C.c_int, [C.POINTER(fd_forest_params), C.POINTER(fd_tree_arrays), _vp, _i64, _vp, _i64,

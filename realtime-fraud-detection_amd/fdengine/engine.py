@@ -67,6 +67,12 @@ class FraudEngine:
     def set_option(self, key: str, value: int) -> None:
         N.call("fd_engine_set_option", self._h, key.encode(), int(value))
 
+    def counter(self, key: str) -> int:
+        """fd_engine_get_counter: "graphs_captured" / "graphs_replayed"."""
+        v = N._i64()
+        N.call("fd_engine_get_counter", self._h, key.encode(), C.byref(v))
+        return int(v.value)
+
     def read_timing(self, kinds=(N.FD_TIMING_XGB, N.FD_TIMING_IFOREST, N.FD_TIMING_FEATURES, N.FD_TIMING_BLEND,
                                  N.FD_TIMING_ROUTE, N.FD_TIMING_LSTM, N.FD_TIMING_WINDOWS, N.FD_TIMING_INGEST,
                                  N.FD_TIMING_ENSEMBLE),

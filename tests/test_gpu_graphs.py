@@ -1,0 +1,111 @@
+"""fd_score_batch_device with the "graphs" option (latency batches replayed as captured hipGraphs: inputs gathered
+into fixed staging, the rest of the step one graph launch) against the same calls on a twin engine without it:
+every batch's outputs and vectors bit-identical and the card state identical afterwards, across both grouping
+parities, two output sets, a sampled timed (un-captured) step, a batch size change, a large batch that moves the
+engine's buffers, and another engine call that invalidates the graphs.
+Reference chain: FeatureExtractor -> FeatureProcessor -> EnsemblePredictor.predict one micro-batch at a time
+(fl/features/FeatureExtractor.java:50-87, ml/models/ensemble_predictor.py:75-148)."""
+import numpy as np
+import pytest
+
+from fdengine import FraudEngine, iforest_from_sklearn, synth, xgboost_from_json_doc
+from fdengine import lstm as L
+from fdengine._native import FD_SLOT_LSTM, TXN_FIELDS
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(lstm):
+    from oracle import scoring_ref as S
+    names = ["xgboost_primary", "isolation_forest"] + (["lstm_sequential"] if lstm else [])
+    w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05, "lstm_sequential": 0.3})
+    return FraudEngine.blend_params([w[k] for k in names], [S.CONF_MULT[k] for k in names])
+
+
+def _setup(pop, xgb, ifm, lw, graphs):
+    U, M = pop["users"], pop["merchants"]
+    eng = FraudEngine(0)
+    eng.state_init(1 << 17, 1, 16, seq_len=10 if lw is not None else 0)
+    eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+    eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+    eng.load_forest(0, xgb)
+    eng.load_forest(1, ifm)
+    if lw is not None:
+        eng.load_lstm(lw)
+    eng.set_option("graphs", int(graphs))
+    return eng
+
+
+@pytest.fixture(scope="module")
+def world():
+    pop = synth.population(20000, 5000, seed=11)
+    tx = synth.txn_stream(pop, 120_000, seed=12)
+    X = synth.feature_matrix(8192, 64, seed=13)
+    xgb = xgboost_from_json_doc(synth.xgboost_doc(120, 8, 64, X, seed=14))
+    ifm = iforest_from_sklearn(synth.isolation_forest(X.astype(np.float64), n_estimators=40))
+    return pop, tx, xgb, ifm
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("lstm,side", [(False, False), (True, False), (True, True)])
+def test_graph_replay_matches_direct(world, lstm, side):
+    """side: the engines on a created stream (else torch's null stream, which the capture cannot use directly)"""
+    import torch
+    pop, tx, xgb, ifm = world
+    lw = L.random_weights(seed=5) if lstm else None
+    params = _params(lstm)
+    slots = [0, 1] + ([FD_SLOT_LSTM] if lstm else [])
+    M = len(slots)
+    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f])).cuda() for f in TXN_FIELDS}
+    # 1k latency batches, a 1001 batch, a 40k batch (the large-batch path, new buffer sizes), then 1k again
+    sizes = [1000] * 9 + [1001, 1001, 1001] + [1000] * 3 + [40000] + [1000] * 6
+    cuts = np.cumsum([0] + sizes)
+    assert cuts[-1] <= len(tx["card_key"])
+    ref, gra = _setup(pop, xgb, ifm, lw, False), _setup(pop, xgb, ifm, lw, True)
+    side_stream = torch.cuda.Stream() if side else None
+    ctx = torch.cuda.stream(side_stream) if side else torch.cuda.stream(torch.cuda.current_stream())
+    try:
+        ctx.__enter__()
+        st = torch.cuda.current_stream()
+        for e in (ref, gra):
+            e.set_stream(st.cuda_stream)
+        outs = [[torch.empty(40000, dtype=t, device="cuda") for t in (torch.float64,) * 2 + (torch.uint8,) * 2]
+                for _ in range(2)]
+        vec = torch.empty((40000, 64), dtype=torch.float32, device="cuda")
+        mp = torch.empty((M, 40000), dtype=torch.float64, device="cuda")
+        got, want = [], []
+        for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+            n = int(b - a)
+            ptrs = {f: t[a:b].data_ptr() for f, t in dev.items()}
+            if i == 6:  # a timed stretch: one step in 2 is the sampled, un-captured launch
+                gra.set_option("timing_every", 2)
+                gra.set_timing(True)
+            if i == 10:
+                gra.set_timing(False)
+            if i == 13:  # another engine call: every captured graph is dropped
+                for e in (ref, gra):
+                    e.load_merchants(pop["merchants"]["fraud_rate"], pop["merchants"]["risk_multiplier"])
+            for e, dst in ((ref, want), (gra, got)):
+                fp, conf, dec, risk = outs[i & 1]
+                e.score_batch_device(params, slots, ptrs, n, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(),
+                                     risk.data_ptr(), vec_ptr=vec.data_ptr() if i % 2 == 0 else 0,
+                                     model_probs_ptr=mp.data_ptr())
+                r = [fp[:n].clone(), conf[:n].clone(), dec[:n].clone(), risk[:n].clone(), mp[:, :n].clone()]
+                if i % 2 == 0:
+                    r.append(vec[:n].clone())
+                dst.append(r)
+        torch.cuda.synchronize()
+        for i, (g, w) in enumerate(zip(got, want)):
+            for x, y in zip(g, w):
+                assert np.array_equal(x.cpu().numpy(), y.cpu().numpy()), f"batch {i} differs"
+        nxt = {k: v[cuts[-1]:cuts[-1] + 2048] for k, v in tx.items()}
+        assert np.array_equal(gra.features(nxt), ref.features(nxt)), "card state differs after the stream"
+        # a graph per grouping parity (the output set and vector pointer alternate with it) for each of: 1000,
+        # 1001, 1000 after load_merchants, 1000 after the 40k batch moved buffers; the other untimed steps replay
+        cap, rep = gra.counter("graphs_captured"), gra.counter("graphs_replayed")
+        assert cap >= 6 and rep >= 4, (cap, rep)
+        assert ref.counter("graphs_captured") == 0 and ref.counter("graphs_replayed") == 0
+    finally:
+        ctx.__exit__(None, None, None)
+        ref.close()
+        gra.close()
