@@ -102,11 +102,17 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     dMP = e.scratch_probs.as<double>();
   }
   const double* cols[FD_MAX_MODELS] = {};
-  bool joined = true;
-  for (int m = 0; m < M; ++m) {  // the LSTM first, so it overlaps the forests
-    if ((present && !present[m]) || slots[m] != FD_SLOT_LSTM) continue;
-    FD_REQUIRE(d_seq != nullptr, FD_ERR_INVALID_ARG,
-               "the LSTM head needs card-history sequences (fd_score_batch_device with seq_len > 0)");
+  // small (latency) batches: the LSTM and every forest after the first run beside the first forest, forked after
+  // everything queued so far (the feature kernel). small_streams: 2 the LSTM on aux, the other forests on aux2;
+  // 1 both on aux (one fork / join hop); 0 everything on e.stream
+  int n_forests = 0;
+  for (int m = 0; m < M; ++m) n_forests += (!(present && !present[m]) && slots[m] >= 0 && slots[m] != FD_SLOT_LSTM);
+  const bool latency = (n + fd::kTile - 1) / fd::kTile < fd::kSplitTiles;
+  const int ss = latency ? e.small_streams : 2;
+  const bool small = latency && n_forests > 1;
+  bool aux_forked = false;
+  auto fork_aux = [&]() {
+    if (aux_forked) return;
     if (!e.aux_stream) {
       FD_HIP(hipStreamCreateWithFlags(&e.aux_stream, hipStreamNonBlocking));
       FD_HIP(hipEventCreateWithFlags(&e.fork_ev, kStreamEventFlags));
@@ -114,18 +120,23 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     }
     FD_HIP(hipEventRecord(e.fork_ev, e.stream));
     FD_HIP(hipStreamWaitEvent(e.aux_stream, e.fork_ev, 0));
+    aux_forked = true;
+  };
+  for (int m = 0; m < M; ++m) {  // the LSTM first, so it overlaps the forests
+    if ((present && !present[m]) || slots[m] != FD_SLOT_LSTM) continue;
+    FD_REQUIRE(d_seq != nullptr, FD_ERR_INVALID_ARG,
+               "the LSTM head needs card-history sequences (fd_score_batch_device with seq_len > 0)");
     double* col = dMP + (size_t)m * n;
-    fd::launch_lstm(e, e.aux_stream, d_seq, n, T, col);
-    FD_HIP(hipEventRecord(e.join_ev, e.aux_stream));
-    joined = false;
+    if (ss == 0) {
+      fd::launch_lstm(e, e.stream, d_seq, n, T, col);
+    } else {
+      fork_aux();
+      fd::launch_lstm(e, e.aux_stream, d_seq, n, T, col);
+    }
     cols[m] = col;
   }
-  // small (latency) batches: every forest after the first runs on a second stream, concurrently,
-  // forked after everything queued so far (the feature kernel)
-  int n_forests = 0;
-  for (int m = 0; m < M; ++m) n_forests += (!(present && !present[m]) && slots[m] >= 0 && slots[m] != FD_SLOT_LSTM);
-  const bool small = (n + fd::kTile - 1) / fd::kTile < fd::kSplitTiles && n_forests > 1;
-  if (small) {
+  const bool use2 = small && ss == 2, use1 = small && ss == 1;
+  if (use2) {
     if (!e.aux2_stream) {
       FD_HIP(hipStreamCreateWithFlags(&e.aux2_stream, hipStreamNonBlocking));
       FD_HIP(hipEventCreateWithFlags(&e.join2_ev, kStreamEventFlags));
@@ -134,15 +145,16 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     FD_HIP(hipEventRecord(e.fork_ev, e.stream));
     FD_HIP(hipStreamWaitEvent(e.aux2_stream, e.fork_ev, 0));
   }
+  if (use1) fork_aux();
   int forests_seen = 0;
-  bool joined2 = !small;
   for (int m = 0; m < M; ++m) {
     if ((present && !present[m]) || slots[m] == FD_SLOT_LSTM) continue;
     double* col = dMP + (size_t)m * n;
     if (slots[m] >= 0) {
       const fd::PackedForest& pf = slot_of(e, slots[m]);
       FD_REQUIRE(pf.loaded, FD_ERR_NOT_LOADED, "Model in slot " + std::to_string(slots[m]) + " not loaded");
-      const hipStream_t st = (small && forests_seen++ > 0) ? e.aux2_stream : nullptr;
+      const bool side = small && forests_seen++ > 0;
+      const hipStream_t st = side && use2 ? e.aux2_stream : side && use1 ? e.aux_stream : nullptr;
       fd::launch_forest(e, pf, dX, n, ld, col, nullptr, nullptr, st);
       cols[m] = col;
     } else {
@@ -152,8 +164,11 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
       cols[m] = col;
     }
   }
-  if (!joined) FD_HIP(hipStreamWaitEvent(e.stream, e.join_ev, 0));
-  if (!joined2) {
+  if (aux_forked) {
+    FD_HIP(hipEventRecord(e.join_ev, e.aux_stream));
+    FD_HIP(hipStreamWaitEvent(e.stream, e.join_ev, 0));
+  }
+  if (use2) {
     FD_HIP(hipEventRecord(e.join2_ev, e.aux2_stream));
     FD_HIP(hipStreamWaitEvent(e.stream, e.join2_ev, 0));
   }
@@ -374,6 +389,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
       e.pipe_iter = 0;
       e.pipe_mode = (int)value;
     }
+  } else if (k == "small_streams") {  // latency batches: 2 LSTM | other forests on two side streams, 1 one, 0 none
+    FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "small_streams must be 0, 1 or 2");
+    e.small_streams = (int)value;
   } else if (k == "graphs") {  // fd_score_batch_device: latency batches replayed as captured hipGraphs
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "graphs must be 0 or 1");
     e.graphs_on = value != 0;

@@ -109,3 +109,39 @@ def test_graph_replay_matches_direct(world, lstm, side):
         ctx.__exit__(None, None, None)
         ref.close()
         gra.close()
+
+
+@pytest.mark.timeout(200)
+def test_small_streams_variants_identical(world):
+    """engine option small_streams (latency batches: the LSTM and the second forest on 2 / 1 / 0 side streams):
+    the same outputs bit for bit, batch after batch"""
+    import torch
+    pop, tx, xgb, ifm = world
+    lw = L.random_weights(seed=6)
+    params = _params(True)
+    slots = [0, 1, FD_SLOT_LSTM]
+    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f][:8000])).cuda() for f in TXN_FIELDS}
+    engs = [_setup(pop, xgb, ifm, lw, False) for _ in range(3)]
+    try:
+        res = []
+        for v, e in enumerate(engs):
+            e.set_option("small_streams", v)
+            e.set_stream(torch.cuda.current_stream().cuda_stream)
+            out = []
+            for a in range(0, 8000, 1000):
+                fp, conf = (torch.empty(1000, dtype=torch.float64, device="cuda") for _ in range(2))
+                dec, risk = (torch.empty(1000, dtype=torch.uint8, device="cuda") for _ in range(2))
+                mp = torch.empty((3, 1000), dtype=torch.float64, device="cuda")
+                e.score_batch_device(params, slots, {f: t[a:a + 1000].data_ptr() for f, t in dev.items()}, 1000,
+                                     fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
+                                     model_probs_ptr=mp.data_ptr())
+                out.append([fp, conf, dec, risk, mp])
+            res.append(out)
+        torch.cuda.synchronize()
+        for v in (1, 2):
+            for b, (x, y) in enumerate(zip(res[v], res[0])):
+                for s, t in zip(x, y):
+                    assert np.array_equal(s.cpu().numpy(), t.cpu().numpy()), f"small_streams {v} batch {b}"
+    finally:
+        for e in engs:
+            e.close()
