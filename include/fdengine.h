@@ -611,9 +611,9 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      "lstm_rows": LSTM tile, 0 auto (4 transactions below 4096, else 16), 4 or 16
      "timing_every": N >= 1, fd_engine_set_timing records HIP events on one launch in N of each timing kind
      (the others run without event records; fd_timing_read's launch count is the timed ones)
-     "small_streams": latency batches (< 32768 transactions) with the LSTM head and / or several forests: 2
-     (default) the LSTM and the forests after the first on two side streams, 1 both on one side stream, 0 all on
-     the engine stream (fewer cross-queue hops, no overlap)
+     "small_streams": latency batches (< 32768 transactions) with the LSTM head and / or several forests: 0
+     (default) all on the engine stream (no cross-queue hops; config 5 0.088 ms per 1 k step), 1 the LSTM and the
+     forests after the first on one side stream (0.095), 2 on two side streams (0.095)
      "graphs": 1 fd_score_batch_device runs latency batches (< 32768 transactions, no external probability
      columns) as a replayed hipGraph per (size, models, outputs, stream, grouping parity): the transaction columns
      are gathered into engine staging by one kernel, then one graph launch; the first batch of a shape runs

@@ -102,9 +102,10 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     dMP = e.scratch_probs.as<double>();
   }
   const double* cols[FD_MAX_MODELS] = {};
-  // small (latency) batches: the LSTM and every forest after the first run beside the first forest, forked after
-  // everything queued so far (the feature kernel). small_streams: 2 the LSTM on aux, the other forests on aux2;
-  // 1 both on aux (one fork / join hop); 0 everything on e.stream
+  // small (latency) batches, small_streams: 0 (default) everything on e.stream — the kernels of a 1 k batch are
+  // short and the cross-queue fork / join hops cost more than the overlap gains (config 5: 0.088 vs 0.095 ms);
+  // 1 the LSTM and every forest after the first on aux; 2 the LSTM on aux, the other forests on aux2 (forked
+  // after everything queued so far, i.e. the feature kernel). Large batches: the LSTM on aux.
   int n_forests = 0;
   for (int m = 0; m < M; ++m) n_forests += (!(present && !present[m]) && slots[m] >= 0 && slots[m] != FD_SLOT_LSTM);
   const bool latency = (n + fd::kTile - 1) / fd::kTile < fd::kSplitTiles;

@@ -315,7 +315,7 @@ struct Engine {
   // are gathered into fixed staging by one kernel, the rest of the step is one graph launch; a graph per
   // (shape, models, outputs, stream, grouping parity), all dropped by any other engine call (graph_epoch)
   bool graphs_on = false;
-  int small_streams = 2;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
+  int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
   struct GraphEntry {
     std::vector<char> key;
     hipGraphExec_t exec;
