@@ -1459,9 +1459,9 @@ split_walk_kernel(const uint32_t* __restrict__ bins, int64_t n, int64_t n_pad, i
   }
 }
 
-// 32 transactions per workgroup: all 256 threads stream a [trees][32] block of leaf values into LDS
-// (independent coalesced loads), then 32 threads add them in tree order (the sequential sum)
-constexpr int kSumRows = 32;
+// 8 transactions per workgroup (128 workgroups for a 1 k batch): all 256 threads stream a [trees][8] block of
+// leaf values into LDS (independent 32-B row loads), then 8 threads add them in tree order (the sequential sum)
+constexpr int kSumRows = 8;
 
 template <int KIND, typename LeafT>
 __global__ void __launch_bounds__(256)
