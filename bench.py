@@ -890,6 +890,8 @@ def main():
                     help="config3/4 at N=1: fd_score_batch_device per step instead of the pipelined stream")
     ap.add_argument("--small-streams", type=int, choices=[0, 1, 2], default=None,
                     help="engine option small_streams (latency batches: side streams for the LSTM / other forests)")
+    ap.add_argument("--lstm-rows", type=int, choices=[0, 4, 16], default=None,
+                    help="engine option lstm_rows (LSTM tile: 0 auto, 4 or 16 transactions per workgroup)")
     ap.add_argument("--graphs", action="store_true",
                     help="config5: fd_score_batch_device replays a captured hipGraph per step (engine option "
                          "graphs) instead of launching every kernel")
@@ -938,6 +940,8 @@ def main():
     # --graphs: each fd_score_batch_device latency batch replays a captured hipGraph (one launch for the step)
     graphs_on = bool(args.graphs)
     eng.set_option("graphs", int(graphs_on))
+    if args.lstm_rows is not None:
+        eng.set_option("lstm_rows", args.lstm_rows)
     if args.small_streams is not None:
         eng.set_option("small_streams", args.small_streams)
 
