@@ -147,9 +147,28 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     FD_HIP(hipStreamWaitEvent(e.aux2_stream, e.fork_ev, 0));
   }
   if (use1) fork_aux();
+  // two forests, one stream: one binning launch for both (fd::launch_forest_pair)
+  bool paired = false;
+  if (small && ss == 0 && n_forests == 2) {
+    int fm[2], k = 0;
+    for (int m = 0; m < M && k < 2; ++m)
+      if (!(present && !present[m]) && slots[m] >= 0 && slots[m] != FD_SLOT_LSTM) fm[k++] = m;
+    const fd::PackedForest& pa = slot_of(e, slots[fm[0]]);
+    const fd::PackedForest& pb = slot_of(e, slots[fm[1]]);
+    if (pa.loaded && pb.loaded) {
+      double* ca = dMP + (size_t)fm[0] * n;
+      double* cb = dMP + (size_t)fm[1] * n;
+      paired = fd::launch_forest_pair(e, pa, pb, dX, n, ld, ca, cb);
+      if (paired) {
+        cols[fm[0]] = ca;
+        cols[fm[1]] = cb;
+      }
+    }
+  }
   int forests_seen = 0;
   for (int m = 0; m < M; ++m) {
     if ((present && !present[m]) || slots[m] == FD_SLOT_LSTM) continue;
+    if (paired && slots[m] >= 0) continue;
     double* col = dMP + (size_t)m * n;
     if (slots[m] >= 0) {
       const fd::PackedForest& pf = slot_of(e, slots[m]);

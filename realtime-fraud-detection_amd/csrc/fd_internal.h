@@ -373,6 +373,9 @@ struct HostPack {
 // min_depth: pad every tree to at least this depth (the ensemble kernel's common depth)
 HostPack pack_forest_host(const fd_forest_params& p, const fd_tree_arrays& t, int min_depth = 0);
 void repack_forest(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);
+// two forests of a latency batch, one binning launch (forest.hip); false: not applicable, nothing launched
+bool launch_forest_pair(Engine& e, const PackedForest& pa, const PackedForest& pb, const float* d_X, int64_t n,
+                        int32_t ld, double* d_prob_a, double* d_prob_b);
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
                    double* d_prob, double* d_raw, int32_t* d_leaf, hipStream_t stream = nullptr);
 // windows.hip

@@ -1370,12 +1370,11 @@ forest_kernel5(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 constexpr int kSplitBin = 256;
 
 // one thread per (feature, transaction): the binary search's dependent loads are the only latency
-__global__ void __launch_bounds__(kSplitBin)
-split_bin_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, int nf, const float* __restrict__ thr,
-                 const int32_t* __restrict__ thr_off, int bin_steps, uint32_t* __restrict__ bins,
-                 uint32_t* __restrict__ tile_nan, uint32_t epoch) {
+__device__ __forceinline__ void split_bin_body(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, int f,
+                                               const float* __restrict__ thr, const int32_t* __restrict__ thr_off,
+                                               uint32_t* __restrict__ bins, uint32_t* __restrict__ tile_nan,
+                                               uint32_t epoch) {
   const int64_t r = (int64_t)blockIdx.x * kSplitBin + threadIdx.x;  // row within [0, n_pad)
-  const int f = blockIdx.y;
   const bool ok = r < n;
   float v = 0.f;
   if (ok) v = f < ld ? X[r * (int64_t)ld + f] : __builtin_nanf("");  // DMatrix: missing column = NaN
@@ -1389,6 +1388,33 @@ split_bin_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, 
   bins[(size_t)f * n_pad + r] = !ok ? 0u : (isnan_v ? 0xFFFF0000u : (uint32_t)pos << 16);
   // tile flag = this call's epoch when the tile holds a NaN (no per-call clearing of the flags)
   if (__ballot(isnan_v) != 0ull && (threadIdx.x & 63) == 0) atomicMax(&tile_nan[r / kTile], epoch);
+}
+
+__global__ void __launch_bounds__(kSplitBin)
+split_bin_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, int nf, const float* __restrict__ thr,
+                 const int32_t* __restrict__ thr_off, int bin_steps, uint32_t* __restrict__ bins,
+                 uint32_t* __restrict__ tile_nan, uint32_t epoch) {
+  split_bin_body(X, n, n_pad, ld, (int)blockIdx.y, thr, thr_off, bins, tile_nan, epoch);
+}
+
+// one forest's binning inputs / outputs (split_bin_pair_kernel)
+struct SplitBinArgs {
+  const float* thr;
+  const int32_t* thr_off;
+  uint32_t* bins;
+  uint32_t* tile_nan;
+  uint32_t epoch;
+  int nf;
+};
+
+// both forests of a latency batch binned in one launch: grid.y = nf_a + nf_b
+__global__ void __launch_bounds__(kSplitBin)
+split_bin_pair_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, SplitBinArgs a, SplitBinArgs b) {
+  const int y = (int)blockIdx.y;
+  if (y < a.nf)
+    split_bin_body(X, n, n_pad, ld, y, a.thr, a.thr_off, a.bins, a.tile_nan, a.epoch);
+  else
+    split_bin_body(X, n, n_pad, ld, y - a.nf, b.thr, b.thr_off, b.bins, b.tile_nan, b.epoch);
 }
 
 // Stage `rows` rows of 1 KiB (row r at src + r * row_stride) into LDS at dst + r * 1024 by LDS-DMA.
@@ -1706,9 +1732,9 @@ KernelFn6 pick6(int D, int CH, int mode) {
 }
 
 // small-batch launch: bin once, walk (tiles x chunk groups), sequential sum
-template <typename LeafT, int KIND>
-void launch_split(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld, double* d_prob,
-                  double* d_raw, int32_t* d_leaf, int64_t tiles, hipStream_t stream) {
+// stage 1: the forest's scratch for this batch (the NaN flags' epoch advanced)
+template <typename LeafT>
+SplitBinArgs split_prepare(const PackedForest& pf, int64_t n, int64_t tiles, hipStream_t stream) {
   const int64_t n_pad = tiles * kTile;
   SplitScratch& sc = pf.split;  // per forest: two forests may run concurrently on different streams
   sc.bins.ensure((size_t)pf.num_feature * n_pad * 4);
@@ -1720,11 +1746,16 @@ void launch_split(Engine& e, const PackedForest& pf, const float* d_X, int64_t n
   sc.epoch = (sc.epoch == 0xffffffffu) ? 1u : sc.epoch + 1u;
   if (sc.epoch == 1u) FD_HIP(hipMemsetAsync(sc.nan.ptr, 0, sc.nan.bytes, stream));
   sc.leaves.ensure((size_t)pf.n_trees * n * sizeof(LeafT));
-  hipLaunchKernelGGL(split_bin_kernel, dim3((unsigned)(n_pad / kSplitBin), (unsigned)pf.num_feature), dim3(kSplitBin), 0,
-                     stream, d_X, n, n_pad, (int)ld, pf.num_feature, pf.b_thr.as<const float>(),
-                     pf.b_thr_off.as<const int32_t>(), pf.bin_steps, sc.bins.as<uint32_t>(), sc.nan.as<uint32_t>(),
-                     sc.epoch);
-  FD_HIP(hipGetLastError());
+  return SplitBinArgs{pf.b_thr.as<const float>(), pf.b_thr_off.as<const int32_t>(), sc.bins.as<uint32_t>(),
+                      sc.nan.as<uint32_t>(), sc.epoch, pf.num_feature};
+}
+
+// stage 3: walk (tiles x chunk groups) over the binned rows, then the sequential sum
+template <typename LeafT, int KIND>
+void split_walk_sum(const PackedForest& pf, int64_t n, double* d_prob, double* d_raw, int32_t* d_leaf, int64_t tiles,
+                    hipStream_t stream) {
+  const int64_t n_pad = tiles * kTile;
+  SplitScratch& sc = pf.split;
   // chunk groups: enough workgroups to cover the CUs (tiles x groups >= 256)
   const int want = (int)std::max<int64_t>(1, (256 + tiles - 1) / tiles);
   const int cpg = std::max(1, (pf.b_n_chunks + want - 1) / want);
@@ -1747,6 +1778,24 @@ void launch_split(Engine& e, const PackedForest& pf, const float* d_X, int64_t n
   FD_HIP(hipGetLastError());
 }
 
+template <typename LeafT, int KIND>
+void launch_split(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld, double* d_prob,
+                  double* d_raw, int32_t* d_leaf, int64_t tiles, hipStream_t stream) {
+  (void)e;
+  const SplitBinArgs a = split_prepare<LeafT>(pf, n, tiles, stream);
+  hipLaunchKernelGGL(split_bin_kernel, dim3((unsigned)(tiles * kTile / kSplitBin), (unsigned)pf.num_feature),
+                     dim3(kSplitBin), 0, stream, d_X, n, tiles * kTile, (int)ld, pf.num_feature, a.thr, a.thr_off,
+                     pf.bin_steps, a.bins, a.tile_nan, a.epoch);
+  FD_HIP(hipGetLastError());
+  split_walk_sum<LeafT, KIND>(pf, n, d_prob, d_raw, d_leaf, tiles, stream);
+}
+
+bool split_path(const Engine& e, const PackedForest& pf, int64_t n) {
+  const int64_t blocks = (n + kTile - 1) / kTile;
+  const bool ok_split = pf.binned && pf.depth <= 8 && pf.b_chunk % 4 == 0;
+  return ok_split && (e.forest_variant == 6 || (e.forest_variant == 0 && blocks < kSplitTiles));
+}
+
 }  // namespace
 
 #ifdef FD_FOREST_PROFILE
@@ -1763,6 +1812,37 @@ extern "C" __attribute__((visibility("default"))) int fd_debug_forest_profile(un
 // speculative-children walk), 6 forces the tree-split
 // small-batch path, which auto also takes below kSplitTiles tiles (FD_ERR_UNSUPPORTED when the forest
 // cannot use it).
+// Two forests of a latency batch on one stream (score_matrix, small_streams 0): one binning launch for both,
+// then each forest's walk and sum. false: not applicable (a forest off the split path); nothing launched.
+bool launch_forest_pair(Engine& e, const PackedForest& pa, const PackedForest& pb, const float* d_X, int64_t n,
+                        int32_t ld, double* d_prob_a, double* d_prob_b) {
+  if (n == 0 || !split_path(e, pa, n) || !split_path(e, pb, n) || &pa == &pb) return false;
+  FD_REQUIRE(d_X && d_prob_a && d_prob_b && ld > 0, FD_ERR_INVALID_ARG, "null buffer or bad ld");
+  const int64_t tiles = (n + kTile - 1) / kTile;
+  const hipStream_t st = e.stream;
+  const bool xa = pa.kind == FD_FOREST_XGB_BINARY_LOGISTIC, xb = pb.kind == FD_FOREST_XGB_BINARY_LOGISTIC;
+  Engine::Timed* ev = e.timing ? e.next_event_pair(xa ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
+  if (ev) FD_HIP(hipEventRecord(ev->a, st));  // the first forest's time includes the shared binning
+  const SplitBinArgs a = xa ? split_prepare<float>(pa, n, tiles, st) : split_prepare<double>(pa, n, tiles, st);
+  const SplitBinArgs b = xb ? split_prepare<float>(pb, n, tiles, st) : split_prepare<double>(pb, n, tiles, st);
+  hipLaunchKernelGGL(split_bin_pair_kernel, dim3((unsigned)(tiles * kTile / kSplitBin), (unsigned)(a.nf + b.nf)),
+                     dim3(kSplitBin), 0, st, d_X, n, tiles * kTile, (int)ld, a, b);
+  FD_HIP(hipGetLastError());
+  if (xa)
+    split_walk_sum<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pa, n, d_prob_a, nullptr, nullptr, tiles, st);
+  else
+    split_walk_sum<double, FD_FOREST_SKLEARN_IFOREST>(pa, n, d_prob_a, nullptr, nullptr, tiles, st);
+  if (ev) FD_HIP(hipEventRecord(ev->b, st));
+  ev = e.timing ? e.next_event_pair(xb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
+  if (ev) FD_HIP(hipEventRecord(ev->a, st));
+  if (xb)
+    split_walk_sum<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pb, n, d_prob_b, nullptr, nullptr, tiles, st);
+  else
+    split_walk_sum<double, FD_FOREST_SKLEARN_IFOREST>(pb, n, d_prob_b, nullptr, nullptr, tiles, st);
+  if (ev) FD_HIP(hipEventRecord(ev->b, st));
+  return true;
+}
+
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
                    double* d_prob, double* d_raw, int32_t* d_leaf, hipStream_t stream) {
   FD_REQUIRE(d_X && d_prob && ld > 0, FD_ERR_INVALID_ARG, "null buffer or bad ld");
