@@ -15,8 +15,10 @@
  *   - fd_last_error() returns a thread-local message for the last failure on this thread;
  *   - caller-owned buffers; "_device" functions take device pointers (HBM-resident inputs),
  *     "_host" functions take host pointers and are synchronous;
- *   - one engine per GPU; calls on one engine must be serialised by the caller
- *     (the reference serialises on one asyncio loop, ml/main.py:337-344).
+ *   - one engine per GPU; every entry point taking an engine holds that engine's (recursive) lock, so
+ *     calls from several host threads are serialised per engine (the reference serialises on one
+ *     asyncio loop, ml/main.py:337-344; here ModelManager.predict runs in a worker thread beside the
+ *     loop's own calls). fd_engine_destroy while another thread still uses the engine is undefined.
  * No PyTorch / HIP types appear in these signatures; streams are passed as void*.
  */
 #ifndef FDENGINE_H
@@ -93,6 +95,10 @@ typedef struct {
 /* ---------------------------------------------------------------- engine lifecycle */
 const char* fd_last_error(void);
 int fd_abi_version(void);
+/* "fdengine-build-id:src=<digest>;flags=<hipcc flags>": SHA-256 (first 128 bits) of the HIP sources, the csrc
+   headers and this header the library was built from (fdengine/_buildid.py); the Python loader refuses a
+   library whose digest differs from the tree beside it. */
+const char* fd_build_id(void);
 int fd_device_count(int* out);
 /* ModelManager.__init__ (ml/models/model_manager.py:33-45): one engine per GPU. */
 int fd_engine_create(int device, fd_engine** out);
@@ -359,15 +365,17 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
 
 /* Streaming form of fd_score_batch_device for a sequence of micro-batches (the Flink operator chain is
    pipelined record by record; here micro-batch by micro-batch). Same results, same card-state order.
-   The feature launches of batch i run on the engine's feature stream, ordered after batch i-1's feature
-   launches and after `input_ready` (a hipEvent_t the caller recorded once the batch's input columns were
-   in device memory; NULL = they were complete before this call); the scoring launches run on the engine
-   stream after batch i's features, so the outputs are ordered on the engine stream exactly as with
-   fd_score_batch_device. Batch i+1's features therefore overlap batch i's forests. The scoring vectors
-   live in two engine buffers (batch parity); the input columns must stay unchanged until the call's
-   outputs are complete, and consecutive calls must not share output buffers (batch i+1's forests may
-   start before batch i's finish). Any other engine call in between orders the next batch's features
-   after everything queued on the engine stream (no overlap across it). */
+   Batch i's feature and scoring launches run on one of the engine's two private pipeline streams
+   (alternating by batch), the features ordered after batch i-1's feature launches and after
+   `input_ready` (a hipEvent_t the caller recorded once the batch's input columns were in device memory;
+   NULL = they were complete before this call). Batch i+1's features therefore overlap batch i's forests.
+   The scoring launches write engine-owned staging; the caller's output buffers are written by one copy
+   kernel queued on the ENGINE stream (fd_engine_set_stream) after batch i's scoring: the outputs are
+   ordered on the engine stream exactly as with fd_score_batch_device, and a caller may free or reuse
+   them in that stream's order (e.g. torch's caching allocator on the stream the engine is bound to).
+   The input columns must stay unchanged until the engine stream has passed the call (the engine stream
+   waits for the batch's features and scoring). Any other engine call in between orders the next
+   batch's features after everything queued on the engine stream (no overlap across it). */
 int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
                              const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
                              int64_t n, double* d_model_probs, double* d_fraud_prob, double* d_confidence,

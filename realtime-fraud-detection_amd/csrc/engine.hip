@@ -2,6 +2,7 @@
 // Every entry point catches everything: status codes + a thread-local message cross the ABI,
 // exceptions never do (mirrors the reference's log-and-raise contract, ml/models/model_manager.py:302-307,
 // with the raise done by the Python shim).
+#include <mutex>
 #include <cstring>
 #include <string>
 
@@ -52,7 +53,17 @@ using fd::Engine;
 
 struct fd_engine {
   Engine e;
+  // every entry point on this engine holds it (FD_ENGINE_LOCK): calls from several host threads are serialised
+  // per engine (e.g. ModelManager.predict in an executor thread beside a reload on the event loop's thread);
+  // recursive so an entry point may call another
+  std::recursive_mutex mu;
 };
+
+static std::recursive_mutex& lock_of(fd_engine* p) {
+  static std::recursive_mutex none;  // null engine: E() reports it
+  return p ? p->mu : none;
+}
+#define FD_ENGINE_LOCK(p) std::lock_guard<std::recursive_mutex> fd_engine_guard_(lock_of(p))
 
 // Engine of an entry point that may queue work on e.stream: the next fd_score_batch_pipelined orders its
 // feature stream after e.stream again (pipe_dirty).
@@ -249,6 +260,7 @@ int fd_engine_create(int device, fd_engine** out) {
 int fd_engine_destroy(fd_engine* eng) {
   FD_API_BEGIN
   if (!eng) return FD_OK;
+  { FD_ENGINE_LOCK(eng); }  // wait for a call in flight on another thread (destroying while in use is the caller's bug)
   Engine& e = E(eng);
   (void)hipStreamSynchronize(e.stream);
   for (auto& f : e.forests) {
@@ -293,7 +305,9 @@ int fd_engine_destroy(fd_engine* eng) {
   for (int k = 0; k < Engine::kPipeSlots; ++k) {
     if (e.pipe_feat_ev[k]) (void)hipEventDestroy(e.pipe_feat_ev[k]);
     if (e.pipe_done_ev[k]) (void)hipEventDestroy(e.pipe_done_ev[k]);
+    if (e.pipe_copy_ev[k]) (void)hipEventDestroy(e.pipe_copy_ev[k]);
     e.pipe_vec[k].release();
+    e.pipe_out[k].release();
     e.pipe_seq[k].release();
   }
   for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
@@ -335,6 +349,7 @@ static void rebind_stream(Engine& e, hipStream_t s) {
 
 int fd_engine_set_stream(fd_engine* eng, void* hip_stream) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   rebind_stream(e, static_cast<hipStream_t>(hip_stream));
   FD_API_END
@@ -342,6 +357,7 @@ int fd_engine_set_stream(fd_engine* eng, void* hip_stream) {
 
 int fd_engine_reset_stream(fd_engine* eng) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   rebind_stream(e, e.own_stream);
   FD_API_END
@@ -349,6 +365,7 @@ int fd_engine_reset_stream(fd_engine* eng) {
 
 int fd_engine_sync(fd_engine* eng) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_HIP(hipStreamSynchronize(e.stream));
   for (hipStream_t st : e.pipe_stream)
@@ -361,6 +378,7 @@ int fd_engine_sync(fd_engine* eng) {
 
 int fd_engine_set_timing(fd_engine* eng, int enable) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);
   e.timing = enable != 0;
   FD_API_END
@@ -368,6 +386,7 @@ int fd_engine_set_timing(fd_engine* eng, int enable) {
 
 int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);
   FD_REQUIRE(key && value, FD_ERR_INVALID_ARG, "null key/value");
   const std::string k(key);
@@ -383,6 +402,7 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
 
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);
   FD_REQUIRE(key, FD_ERR_INVALID_ARG, "null key");
   const std::string k(key);
@@ -405,7 +425,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     if ((int)value != e.pipe_mode) {  // drain the pipeline: its buffer ring changes
       for (hipStream_t st : e.pipe_stream)
         if (st) FD_HIP(hipStreamSynchronize(st));
-      for (int q = 0; q < Engine::kPipeSlots; ++q) e.pipe_feat_live[q] = e.pipe_done_live[q] = false;
+      FD_HIP(hipStreamSynchronize(e.stream));  // the output copies of the old ring
+      for (int q = 0; q < Engine::kPipeSlots; ++q)
+        e.pipe_feat_live[q] = e.pipe_done_live[q] = e.pipe_copy_live[q] = false;
       e.pipe_iter = 0;
       e.pipe_mode = (int)value;
     }
@@ -436,6 +458,7 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
 
 int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);
   double tot = 0.0;
   int64_t cnt = 0;
@@ -454,6 +477,7 @@ int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches
 
 int fd_timing_reset(fd_engine* eng) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);
   for (size_t i = 0; i < e.events_used; ++i) FD_HIP(hipEventSynchronize(e.events[i].b));  // pairs on 2+ streams
   e.events_used = 0;
@@ -462,6 +486,7 @@ int fd_timing_reset(fd_engine* eng) {
 
 int fd_load_forest(fd_engine* eng, int slot, const fd_forest_params* params, const fd_tree_arrays* trees) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params && trees, FD_ERR_INVALID_ARG, "null params/trees");
   fd::PackedForest& pf = slot_of(e, slot);
@@ -533,6 +558,7 @@ int fd_pack_forest_binned_host(const fd_forest_params* params, const fd_tree_arr
 
 int fd_load_xgboost_json(fd_engine* eng, int slot, const char* path) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::PackedForest& pf = slot_of(e, slot);
   fd::XgbModel m;
@@ -590,6 +616,7 @@ int fd_xgboost_json_read(const char* path, fd_forest_params* params, int32_t* n_
 
 int fd_unload_forest(fd_engine* eng, int slot) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::PackedForest& pf = slot_of(e, slot);
   FD_HIP(hipStreamSynchronize(e.stream));
@@ -599,7 +626,6 @@ int fd_unload_forest(fd_engine* eng, int slot) {
   pf.b_thr.release();
   pf.b_thr_off.release();
   for (auto* b : {&pf.split.bins, &pf.split.nan, &pf.split.leaves}) b->release();
-  pf.split.epoch = 0;
   pf.binned = false;
   pf.loaded = false;
   pf.gen = 0;  // any ensemble plan built over this slot is stale
@@ -608,6 +634,7 @@ int fd_unload_forest(fd_engine* eng, int slot) {
 
 int fd_forest_info(fd_engine* eng, int slot, int32_t* n_trees, int32_t* depth, int32_t* num_feature) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::PackedForest& pf = slot_of(e, slot);
   FD_REQUIRE(pf.loaded, FD_ERR_NOT_LOADED, "Model in slot " + std::to_string(slot) + " not loaded");
@@ -620,6 +647,7 @@ int fd_forest_info(fd_engine* eng, int slot, int32_t* n_trees, int32_t* depth, i
 int fd_forest_predict_device(fd_engine* eng, int slot, const float* d_X, int64_t n, int32_t ld,
                              double* d_prob, double* d_raw, int32_t* d_leaf) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::PackedForest& pf = slot_of(e, slot);
   FD_REQUIRE(pf.loaded, FD_ERR_NOT_LOADED, "Model in slot " + std::to_string(slot) + " not loaded");
@@ -631,6 +659,7 @@ int fd_forest_predict_device(fd_engine* eng, int slot, const float* d_X, int64_t
 int fd_forest_predict_host(fd_engine* eng, int slot, const float* X, int64_t n, int32_t ld, double* prob,
                            double* raw, int32_t* leaf) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::PackedForest& pf = slot_of(e, slot);
   FD_REQUIRE(pf.loaded, FD_ERR_NOT_LOADED, "Model in slot " + std::to_string(slot) + " not loaded");
@@ -656,6 +685,7 @@ int fd_forest_predict_host(fd_engine* eng, int slot, const float* X, int64_t n, 
 
 int fd_state_init(fd_engine* eng, const fd_state_params* params) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
   FD_HIP(hipStreamSynchronize(e.stream));
@@ -665,6 +695,7 @@ int fd_state_init(fd_engine* eng, const fd_state_params* params) {
 
 int fd_state_clear(fd_engine* eng) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::state_clear(e);
   FD_API_END
@@ -672,6 +703,7 @@ int fd_state_clear(fd_engine* eng) {
 
 int fd_state_info(fd_engine* eng, int64_t* capacity, int64_t* cards) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::features_check(e);
   if (capacity) *capacity = e.state.cap;
@@ -681,6 +713,7 @@ int fd_state_info(fd_engine* eng, int64_t* capacity, int64_t* cards) {
 
 int fd_state_load_users_host(fd_engine* eng, const fd_users* users) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(users, FD_ERR_INVALID_ARG, "null users");
   fd::load_users(e, *users);
@@ -689,6 +722,7 @@ int fd_state_load_users_host(fd_engine* eng, const fd_users* users) {
 
 int fd_load_merchants_host(fd_engine* eng, const fd_merchants* merchants) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(merchants, FD_ERR_INVALID_ARG, "null merchants");
   FD_HIP(hipStreamSynchronize(e.stream));
@@ -698,6 +732,7 @@ int fd_load_merchants_host(fd_engine* eng, const fd_merchants* merchants) {
 
 int fd_features_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* d_vectors, double* d_raw) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
   fd::launch_features(e, *txns, n, d_vectors, d_raw);
@@ -706,6 +741,7 @@ int fd_features_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, floa
 
 int fd_features_host(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* vectors, double* raw) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(txns && vectors && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   if (n == 0) return FD_OK;
@@ -746,6 +782,7 @@ int fd_score_matrix_device(fd_engine* eng, const fd_blend_params* params, const 
                            int64_t n, int32_t ld, double* d_model_probs, double* d_fraud_prob,
                            double* d_confidence, uint8_t* d_decision, uint8_t* d_risk) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params && d_X && ld > 0 && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   score_matrix(e, *params, slots, ext_probs, present, d_X, n, ld, d_model_probs, d_fraud_prob, d_confidence,
@@ -758,6 +795,7 @@ int fd_score_matrix_host(fd_engine* eng, const fd_blend_params* params, const in
                          int32_t ld, double* model_probs, double* fraud_prob, double* confidence,
                          uint8_t* decision, uint8_t* risk) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params && slots && X && fraud_prob && ld > 0 && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   FD_REQUIRE(params->n_models > 0 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "n_models out of range");
@@ -929,6 +967,7 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
                           int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
                           double* d_confidence, uint8_t* d_decision, uint8_t* d_risk) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);  // queues work on e.stream, but changes nothing a captured step depends on
   e.pipe_dirty = true;
   FD_REQUIRE(params && txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
@@ -942,14 +981,33 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
   FD_API_END
 }
 
+// fd_score_batch_pipelined's outputs: engine staging -> the caller's buffers, on the engine stream (one thread per
+// transaction; null destinations are skipped)
+__global__ void __launch_bounds__(256)
+pipe_out_copy_kernel(const double* __restrict__ fp, const double* __restrict__ conf, const uint8_t* __restrict__ dec,
+                     const uint8_t* __restrict__ risk, const double* __restrict__ mp, int n_mp, int64_t n,
+                     double* __restrict__ o_fp, double* __restrict__ o_conf, uint8_t* __restrict__ o_dec,
+                     uint8_t* __restrict__ o_risk, double* __restrict__ o_mp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  o_fp[i] = fp[i];
+  if (o_conf) o_conf[i] = conf[i];
+  if (o_dec) o_dec[i] = dec[i];
+  if (o_risk) o_risk[i] = risk[i];
+  for (int m = 0; m < n_mp; ++m) o_mp[(size_t)m * n + i] = mp[(size_t)m * n + i];
+}
+
 int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
                              const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
                              int64_t n, double* d_model_probs, double* d_fraud_prob, double* d_confidence,
                              uint8_t* d_decision, uint8_t* d_risk, void* input_ready) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);
   FD_REQUIRE(params && txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   if (n == 0) return FD_OK;
+  FD_REQUIRE(d_fraud_prob != nullptr, FD_ERR_INVALID_ARG, "null fraud_prob output");
+  FD_REQUIRE(params->n_models >= 1 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "bad n_models");
   const bool m2 = e.pipe_mode == 2;
   for (int k = 0; k < (m2 ? 3 : 2); ++k)
     if (!e.pipe_stream[k]) FD_HIP(hipStreamCreateWithFlags(&e.pipe_stream[k], hipStreamNonBlocking));
@@ -958,6 +1016,7 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
     for (int k = 0; k < Engine::kPipeSlots; ++k) {
       FD_HIP(hipEventCreateWithFlags(&e.pipe_feat_ev[k], kStreamEventFlags));
       FD_HIP(hipEventCreateWithFlags(&e.pipe_done_ev[k], kStreamEventFlags));
+      FD_HIP(hipEventCreateWithFlags(&e.pipe_copy_ev[k], kStreamEventFlags));
     }
   }
   // Batch i: buffer slot s = i mod nbuf, scoring stream Sc = pipe_stream[i & 1], feature stream Sf = Sc
@@ -1000,6 +1059,17 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
   // buffers): those batches also wait for the previous batch's scoring
   if (e.pipe_done_live[prev] && !fd::ensemble_applies(e, *params, slots, present, n))
     FD_HIP(hipStreamWaitEvent(Sc, e.pipe_done_ev[prev], 0));
+  // this slot's output staging: free once batch i-nbuf's copy to its caller (on e.stream) is done
+  const int n_mp = d_model_probs ? params->n_models : 0;
+  const size_t n8 = (size_t)n * 8, a8 = ((size_t)n + 7) & ~(size_t)7;
+  e.pipe_out[s].ensure((2 + (size_t)n_mp) * n8 + 2 * a8);
+  char* so = e.pipe_out[s].as<char>();
+  double* s_fp = reinterpret_cast<double*>(so);
+  double* s_conf = d_confidence ? reinterpret_cast<double*>(so + n8) : nullptr;
+  double* s_mp = n_mp ? reinterpret_cast<double*>(so + 2 * n8) : nullptr;
+  uint8_t* s_dec = d_decision ? reinterpret_cast<uint8_t*>(so + (2 + (size_t)n_mp) * n8) : nullptr;
+  uint8_t* s_risk = d_risk ? reinterpret_cast<uint8_t*>(so + (2 + (size_t)n_mp) * n8 + a8) : nullptr;
+  if (e.pipe_copy_live[s]) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_copy_ev[s], 0));
   ++e.pipe_iter;
   {  // the scoring launches go on Sc: score_matrix launches on e.stream
     struct Swap {
@@ -1008,17 +1078,23 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
       ~Swap() { e.stream = saved; }
     } swap{e, e.stream};
     e.stream = Sc;
-    score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, d_model_probs, d_fraud_prob,
-                 d_confidence, d_decision, d_risk, seq, e.state.S);
+    score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, s_mp, s_fp, s_conf, s_dec, s_risk,
+                 seq, e.state.S);
   }
   FD_HIP(hipEventRecord(e.pipe_done_ev[s], Sc));
   e.pipe_done_live[s] = true;
   FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[s], 0));
+  hipLaunchKernelGGL(pipe_out_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e.stream, s_fp, s_conf,
+                     s_dec, s_risk, s_mp, n_mp, n, d_fraud_prob, d_confidence, d_decision, d_risk, d_model_probs);
+  FD_HIP(hipGetLastError());
+  FD_HIP(hipEventRecord(e.pipe_copy_ev[s], e.stream));
+  e.pipe_copy_live[s] = true;
   FD_API_END
 }
 
 int fd_state_load_users_ext_host(fd_engine* eng, const fd_users_ext* users) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(users, FD_ERR_INVALID_ARG, "null users");
   fd::load_users_ext(e, *users);
@@ -1027,6 +1103,7 @@ int fd_state_load_users_ext_host(fd_engine* eng, const fd_users_ext* users) {
 
 int fd_load_merchants_ext_host(fd_engine* eng, const fd_merchants_ext* merchants) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(merchants, FD_ERR_INVALID_ARG, "null merchants");
   FD_HIP(hipStreamSynchronize(e.stream));
@@ -1036,6 +1113,7 @@ int fd_load_merchants_ext_host(fd_engine* eng, const fd_merchants_ext* merchants
 
 int fd_load_vocab_host(fd_engine* eng, const uint8_t* payment_high_risk, const uint8_t* type_is_refund) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_HIP(hipStreamSynchronize(e.stream));
   fd::load_vocab(e, payment_high_risk, type_is_refund);
@@ -1045,6 +1123,7 @@ int fd_load_vocab_host(fd_engine* eng, const uint8_t* payment_high_risk, const u
 int fd_features_full_device(fd_engine* eng, const fd_txn_batch* txns, const fd_txn_context* ctx, int64_t n,
                             float* d_vectors, double* d_raw, double* d_fmap, fd_rule_scores* d_rules) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
   const fd_txn_context none{};
@@ -1054,6 +1133,7 @@ int fd_features_full_device(fd_engine* eng, const fd_txn_batch* txns, const fd_t
 
 int fd_windows_init(fd_engine* eng, const fd_window_params* params) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
   FD_HIP(hipStreamSynchronize(e.stream));
@@ -1065,6 +1145,7 @@ int fd_windows_step_device(fd_engine* eng, const fd_txn_batch* txns, const fd_wi
                            int flush, fd_user_window* user_out, int64_t user_cap, int64_t* n_user,
                            fd_merchant_window* merchant_out, int64_t merchant_cap, int64_t* n_merchant) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(n_user && n_merchant, FD_ERR_INVALID_ARG, "null result counts");
   const fd_txn_batch none_t{};
@@ -1082,6 +1163,7 @@ int fd_windows_step_host(fd_engine* eng, const fd_txn_batch* txns, const fd_wind
                          fd_user_window* user_out, int64_t user_cap, int64_t* n_user,
                          fd_merchant_window* merchant_out, int64_t merchant_cap, int64_t* n_merchant) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(n_user && n_merchant, FD_ERR_INVALID_ARG, "null result counts");
   FD_REQUIRE(n >= 0 && (txns || n == 0), FD_ERR_INVALID_ARG, "bad batch");
@@ -1123,6 +1205,7 @@ int fd_windows_step_host(fd_engine* eng, const fd_txn_batch* txns, const fd_wind
 
 int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, int64_t* merchant_events) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(e.windows.ready, FD_ERR_NOT_LOADED, "windows not initialised (fd_windows_init)");
   if (watermark) *watermark = e.windows.wm;
@@ -1133,6 +1216,7 @@ int fd_windows_stats(fd_engine* eng, int64_t* watermark, int64_t* user_events, i
 
 int fd_windows_observe(fd_engine* eng, int64_t max_event_ts) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   fd::windows_observe(E(eng), max_event_ts);
   FD_API_END
 }
@@ -1145,6 +1229,7 @@ int fd_merchant_windows_merge(const fd_merchant_window* parts, int64_t n, fd_mer
 
 int fd_sink_init(fd_engine* eng, const fd_sink_params* params) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
   FD_HIP(hipStreamSynchronize(e.stream));
@@ -1154,6 +1239,7 @@ int fd_sink_init(fd_engine* eng, const fd_sink_params* params) {
 
 int fd_sink_update_device(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null batch");
   const fd_window_inputs none{nullptr, nullptr, nullptr};
@@ -1163,6 +1249,7 @@ int fd_sink_update_device(fd_engine* eng, const fd_txn_batch* txns, const fd_win
 
 int fd_sink_update_host(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* in, int64_t n) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   if (n == 0) return FD_OK;
@@ -1198,6 +1285,7 @@ int fd_sink_update_host(fd_engine* eng, const fd_txn_batch* txns, const fd_windo
 int fd_sink_query_host(fd_engine* eng, int32_t kind, const int64_t* bucket, const int32_t* merchant, int64_t n,
                        fd_aggregate* out) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::sink_query(e, kind, bucket, merchant, n, out);
   FD_API_END
@@ -1205,6 +1293,7 @@ int fd_sink_query_host(fd_engine* eng, int32_t kind, const int64_t* bucket, cons
 
 int fd_sink_evict_before(fd_engine* eng, int64_t hour_key, int64_t* kept_entries, int64_t* kept_users) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::sink_evict_before(e, hour_key, kept_entries, kept_users);
   FD_API_END
@@ -1219,6 +1308,7 @@ int fd_hash64(const uint8_t* bytes, int64_t n, uint64_t* out) {
 
 int fd_ingest_set_vocab(fd_engine* eng, int32_t which, const uint8_t* bytes, const int64_t* offsets, int64_t n) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::ingest_set_vocab(e, which, bytes, offsets, n);
   FD_API_END
@@ -1226,6 +1316,7 @@ int fd_ingest_set_vocab(fd_engine* eng, int32_t which, const uint8_t* bytes, con
 
 int fd_ingest_set_merchants(fd_engine* eng, const uint8_t* bytes, const int64_t* offsets, int64_t n) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::ingest_set_merchants(e, bytes, offsets, n);
   FD_API_END
@@ -1234,6 +1325,7 @@ int fd_ingest_set_merchants(fd_engine* eng, const uint8_t* bytes, const int64_t*
 int fd_ingest_json_device(fd_engine* eng, const uint8_t* d_bytes, const int64_t* d_offsets, int64_t n,
                           const fd_ingest_out* d_out) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(d_out, FD_ERR_INVALID_ARG, "null outputs");
   fd::launch_ingest(e, d_bytes, d_offsets, n, *d_out);
@@ -1243,6 +1335,7 @@ int fd_ingest_json_device(fd_engine* eng, const uint8_t* d_bytes, const int64_t*
 int fd_ingest_json_host(fd_engine* eng, const uint8_t* bytes, const int64_t* offsets, int64_t n,
                         const fd_ingest_out* out) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(out && offsets && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   if (n == 0) return FD_OK;
@@ -1334,6 +1427,7 @@ int fd_ingest_scalar_host(int32_t kind, const uint8_t* text, int32_t n, double* 
 
 int fd_state_snapshot(fd_engine* eng, const char* path, int32_t shard, int32_t n_shards, int64_t* bytes_written) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::features_check(e);
   fd::state_snapshot(e, path, shard, n_shards, bytes_written);
@@ -1343,6 +1437,7 @@ int fd_state_snapshot(fd_engine* eng, const char* path, int32_t shard, int32_t n
 int fd_state_restore(fd_engine* eng, const char* path, int32_t shard, int32_t n_shards, int32_t flags,
                      int64_t* cards_restored) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::features_check(e);
   fd::state_restore(e, path, shard, n_shards, flags, cards_restored);
@@ -1351,6 +1446,7 @@ int fd_state_restore(fd_engine* eng, const char* path, int32_t shard, int32_t n_
 
 int fd_load_lstm(fd_engine* eng, const fd_lstm_params* params) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
   FD_HIP(hipStreamSynchronize(e.stream));
@@ -1361,6 +1457,7 @@ int fd_load_lstm(fd_engine* eng, const fd_lstm_params* params) {
 
 int fd_unload_lstm(fd_engine* eng) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_HIP(hipStreamSynchronize(e.stream));
   if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
@@ -1371,6 +1468,7 @@ int fd_unload_lstm(fd_engine* eng) {
 
 int fd_lstm_predict_device(fd_engine* eng, const float* d_seq, int64_t n, int32_t T, double* d_prob) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::launch_lstm(e, e.stream, d_seq, n, T, d_prob);
   FD_API_END
@@ -1378,6 +1476,7 @@ int fd_lstm_predict_device(fd_engine* eng, const float* d_seq, int64_t n, int32_
 
 int fd_lstm_predict_host(fd_engine* eng, const float* seq, int64_t n, int32_t T, double* prob) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(n >= 0 && T >= 1 && T <= FD_MAX_SEQ_LEN, FD_ERR_INVALID_ARG, "bad arguments");
   if (n == 0) return FD_OK;
@@ -1395,6 +1494,7 @@ int fd_lstm_predict_host(fd_engine* eng, const float* seq, int64_t n, int32_t T,
 int fd_features_seq_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, float* d_vectors, double* d_raw,
                            float* d_seq) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
   fd::launch_features(e, *txns, n, d_vectors, d_raw, d_seq);
@@ -1412,6 +1512,7 @@ int fd_shard_of_host(const uint64_t* keys, int64_t n, int32_t n_shards, int32_t*
 int fd_route_partition_device(fd_engine* eng, const fd_txn_batch* txns, int64_t n, int32_t n_shards,
                               void* d_records, int64_t* d_counts) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
   fd::launch_route_partition(e, *txns, nullptr, n, n_shards, d_records, d_counts);
@@ -1421,6 +1522,7 @@ int fd_route_partition_device(fd_engine* eng, const fd_txn_batch* txns, int64_t 
 int fd_route_partition_ex_device(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* extra, int64_t n,
                                  int32_t n_shards, void* d_records, int64_t* d_counts) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
   fd::launch_route_partition(e, *txns, extra, n, n_shards, d_records, d_counts);
@@ -1431,6 +1533,7 @@ int fd_route_unpack_device(fd_engine* eng, const void* d_records, const void* d_
                            const fd_txn_batch* out, uint8_t* d_payment_method, uint8_t* d_is_fraud,
                            double* d_fraud_score) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(out, FD_ERR_INVALID_ARG, "null output columns");
   fd::launch_route_unpack(e, d_records, d_results, n, *out, d_payment_method, d_is_fraud, d_fraud_score);
@@ -1440,6 +1543,7 @@ int fd_route_unpack_device(fd_engine* eng, const void* d_records, const void* d_
 int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
                             const uint8_t* present, const void* d_records, int64_t n, void* d_results) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params && slots && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   for (int m = 0; m < params->n_models && m < FD_MAX_MODELS; ++m)
@@ -1464,6 +1568,7 @@ int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const
 int fd_route_scatter_results_device(fd_engine* eng, const void* d_results, int64_t n, double* d_fraud_prob,
                                     double* d_confidence, uint8_t* d_decision, uint8_t* d_risk) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   fd::launch_result_scatter(e, d_results, n, d_fraud_prob, d_confidence, d_decision, d_risk);
   FD_API_END
@@ -1473,6 +1578,7 @@ int fd_blend_device(fd_engine* eng, const fd_blend_params* params, int64_t n, co
                     const uint8_t* present, double* d_fraud_prob, double* d_confidence, uint8_t* d_decision,
                     uint8_t* d_risk) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params, FD_ERR_INVALID_ARG, "null params");
   fd::launch_blend(e, *params, n, d_probs, present, d_fraud_prob, d_confidence, d_decision, d_risk);
@@ -1483,6 +1589,7 @@ int fd_blend_host(fd_engine* eng, const fd_blend_params* params, int64_t n, cons
                   const uint8_t* present, double* fraud_prob, double* confidence, uint8_t* decision,
                   uint8_t* risk) {
   FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
   FD_REQUIRE(params && probs && fraud_prob, FD_ERR_INVALID_ARG, "bad arguments");
   FD_REQUIRE(params->n_models >= 0 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG,

@@ -72,8 +72,7 @@ struct DeviceBuffer {
 
 // small-batch tree-split scratch of one forest (forest.hip launch_split)
 struct SplitScratch {
-  DeviceBuffer bins, nan, leaves;
-  uint32_t epoch = 0;
+  DeviceBuffer bins, nan, leaves;  // nan: per-tile "holds a NaN" flags, cleared by the step's sum kernel
 };
 
 // A forest repacked into perfect depth-D trees stored as 1-based heaps (see forest.hip header and
@@ -311,6 +310,12 @@ struct Engine {
   int pipe_mode = 1;       // "pipeline_mode" option
   bool pipe_lean = true;   // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
   DeviceBuffer pipe_vec[kPipeSlots], pipe_seq[kPipeSlots];
+  // the scoring streams write a batch's outputs into pipe_out[slot]; one copy kernel on `stream` moves them to the
+  // caller's buffers, so the caller's memory is written only in the engine stream's order (torch's caching
+  // allocator may hand batch i's freed outputs to batch i+1); batch i+nbuf's scoring waits for pipe_copy_ev[slot]
+  DeviceBuffer pipe_out[kPipeSlots];
+  hipEvent_t pipe_copy_ev[kPipeSlots] = {};
+  bool pipe_copy_live[kPipeSlots] = {};
   // fd_score_batch_device for latency batches as a replayed hipGraph ("graphs" option, engine.hip): the inputs
   // are gathered into fixed staging by one kernel, the rest of the step is one graph launch; a graph per
   // (shape, models, outputs, stream, grouping parity), all dropped by any other engine call (graph_epoch)

@@ -1372,8 +1372,7 @@ constexpr int kSplitBin = 256;
 // one thread per (feature, transaction): the binary search's dependent loads are the only latency
 __device__ __forceinline__ void split_bin_body(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, int f,
                                                const float* __restrict__ thr, const int32_t* __restrict__ thr_off,
-                                               uint32_t* __restrict__ bins, uint32_t* __restrict__ tile_nan,
-                                               uint32_t epoch) {
+                                               uint32_t* __restrict__ bins, uint32_t* __restrict__ tile_nan) {
   const int64_t r = (int64_t)blockIdx.x * kSplitBin + threadIdx.x;  // row within [0, n_pad)
   const bool ok = r < n;
   float v = 0.f;
@@ -1386,15 +1385,16 @@ __device__ __forceinline__ void split_bin_body(const float* __restrict__ X, int6
   }
   const bool isnan_v = ok && v != v;
   bins[(size_t)f * n_pad + r] = !ok ? 0u : (isnan_v ? 0xFFFF0000u : (uint32_t)pos << 16);
-  // tile flag = this call's epoch when the tile holds a NaN (no per-call clearing of the flags)
-  if (__ballot(isnan_v) != 0ull && (threadIdx.x & 63) == 0) atomicMax(&tile_nan[r / kTile], epoch);
+  // tile flag: nonzero when the tile holds a NaN; split_sum_kernel, the step's last launch over this scratch,
+  // clears it again, so a replayed hipGraph of the step starts from clear flags (no host-side epoch)
+  if (__ballot(isnan_v) != 0ull && (threadIdx.x & 63) == 0) tile_nan[r / kTile] = 1u;
 }
 
 __global__ void __launch_bounds__(kSplitBin)
 split_bin_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, int nf, const float* __restrict__ thr,
                  const int32_t* __restrict__ thr_off, int bin_steps, uint32_t* __restrict__ bins,
-                 uint32_t* __restrict__ tile_nan, uint32_t epoch) {
-  split_bin_body(X, n, n_pad, ld, (int)blockIdx.y, thr, thr_off, bins, tile_nan, epoch);
+                 uint32_t* __restrict__ tile_nan) {
+  split_bin_body(X, n, n_pad, ld, (int)blockIdx.y, thr, thr_off, bins, tile_nan);
 }
 
 // one forest's binning inputs / outputs (split_bin_pair_kernel)
@@ -1403,7 +1403,6 @@ struct SplitBinArgs {
   const int32_t* thr_off;
   uint32_t* bins;
   uint32_t* tile_nan;
-  uint32_t epoch;
   int nf;
 };
 
@@ -1412,9 +1411,9 @@ __global__ void __launch_bounds__(kSplitBin)
 split_bin_pair_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, SplitBinArgs a, SplitBinArgs b) {
   const int y = (int)blockIdx.y;
   if (y < a.nf)
-    split_bin_body(X, n, n_pad, ld, y, a.thr, a.thr_off, a.bins, a.tile_nan, a.epoch);
+    split_bin_body(X, n, n_pad, ld, y, a.thr, a.thr_off, a.bins, a.tile_nan);
   else
-    split_bin_body(X, n, n_pad, ld, y - a.nf, b.thr, b.thr_off, b.bins, b.tile_nan, b.epoch);
+    split_bin_body(X, n, n_pad, ld, y - a.nf, b.thr, b.thr_off, b.bins, b.tile_nan);
 }
 
 // Stage `rows` rows of 1 KiB (row r at src + r * row_stride) into LDS at dst + r * 1024 by LDS-DMA.
@@ -1437,7 +1436,7 @@ __device__ __forceinline__ void stage_rows_asm(const char* __restrict__ src, siz
 template <int D, int CH, typename LeafT>
 __global__ void __launch_bounds__(kWG3)
 split_walk_kernel(const uint32_t* __restrict__ bins, int64_t n, int64_t n_pad, int nf,
-                  const uint32_t* __restrict__ tile_nan, uint32_t epoch, const char* __restrict__ blob, int n_chunks,
+                  const uint32_t* __restrict__ tile_nan, const char* __restrict__ blob, int n_chunks,
                   int chunk_stride, int chunks_per_group, const int32_t* __restrict__ leaf_ids, int n_trees,
                   LeafT* __restrict__ leaves, int32_t* __restrict__ out_leaf) {
   constexpr int TPG = CH / 4;
@@ -1458,7 +1457,7 @@ split_walk_kernel(const uint32_t* __restrict__ bins, int64_t n, int64_t n_pad, i
   if (k0 >= k1) return;  // uniform per workgroup
   stage_rows_asm(reinterpret_cast<const char*>(bins + (size_t)tile * kTile), (size_t)n_pad * 4u, s0, nf, kWG3 / 64);
   stage_chunk_asm(blob + (size_t)k0 * chunk_stride, bufA, chunk_stride, kWG3 / 64);
-  const bool tile_has_nan = tile_nan[tile] == epoch;
+  const bool tile_has_nan = tile_nan[tile] != 0u;
   dma_wait();
   __syncthreads();
   for (int k = k0; k < k1; ++k) {
@@ -1492,7 +1491,8 @@ constexpr int kSumRows = 8;
 template <int KIND, typename LeafT>
 __global__ void __launch_bounds__(256)
 split_sum_kernel(const LeafT* __restrict__ leaves, int64_t n, int n_trees, float base_margin, double if_offset,
-                 double if_denom, double* __restrict__ out_prob, double* __restrict__ out_raw) {
+                 double if_denom, double* __restrict__ out_prob, double* __restrict__ out_raw,
+                 uint32_t* __restrict__ tile_nan) {
   constexpr int kTc = 65536 / (kSumRows * (int)sizeof(LeafT));  // trees per LDS block (64 KiB)
   __shared__ LeafT blk[kTc * kSumRows];
   const int tid = threadIdx.x;
@@ -1531,6 +1531,7 @@ split_sum_kernel(const LeafT* __restrict__ leaves, int64_t n, int n_trees, float
     __syncthreads();
   }
   if (tid < rows) write_outputs<KIND, LeafT>(acc, r0 + tid, if_offset, if_denom, out_prob, out_raw);
+  if (tid == 0 && r0 % kTile == 0) tile_nan[r0 / kTile] = 0u;  // every walk of the tile is done (stream order)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1732,7 +1733,7 @@ KernelFn6 pick6(int D, int CH, int mode) {
 }
 
 // small-batch launch: bin once, walk (tiles x chunk groups), sequential sum
-// stage 1: the forest's scratch for this batch (the NaN flags' epoch advanced)
+// stage 1: the forest's scratch for this batch (NaN tile flags zeroed when allocated, cleared after each use)
 template <typename LeafT>
 SplitBinArgs split_prepare(const PackedForest& pf, int64_t n, int64_t tiles, hipStream_t stream) {
   const int64_t n_pad = tiles * kTile;
@@ -1741,13 +1742,10 @@ SplitBinArgs split_prepare(const PackedForest& pf, int64_t n, int64_t tiles, hip
   if (sc.nan.bytes < (size_t)tiles * 4) {
     sc.nan.ensure((size_t)tiles * 4);
     FD_HIP(hipMemsetAsync(sc.nan.ptr, 0, sc.nan.bytes, stream));
-    sc.epoch = 0;
   }
-  sc.epoch = (sc.epoch == 0xffffffffu) ? 1u : sc.epoch + 1u;
-  if (sc.epoch == 1u) FD_HIP(hipMemsetAsync(sc.nan.ptr, 0, sc.nan.bytes, stream));
   sc.leaves.ensure((size_t)pf.n_trees * n * sizeof(LeafT));
   return SplitBinArgs{pf.b_thr.as<const float>(), pf.b_thr_off.as<const int32_t>(), sc.bins.as<uint32_t>(),
-                      sc.nan.as<uint32_t>(), sc.epoch, pf.num_feature};
+                      sc.nan.as<uint32_t>(), pf.num_feature};
 }
 
 // stage 3: walk (tiles x chunk groups) over the binned rows, then the sequential sum
@@ -1765,16 +1763,16 @@ void split_walk_sum(const PackedForest& pf, int64_t n, double* d_prob, double* d
   const size_t lds = (size_t)pf.num_feature * 1024 + 2 * pf.b_chunk_stride + 1024;
   FD_REQUIRE(lds <= kLdsBudget, FD_ERR_UNSUPPORTED, "split forest kernel exceeds the LDS budget");
   FD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  using WalkFn = void (*)(const uint32_t*, int64_t, int64_t, int, const uint32_t*, uint32_t, const char*, int, int, int,
+  using WalkFn = void (*)(const uint32_t*, int64_t, int64_t, int, const uint32_t*, const char*, int, int, int,
                           const int32_t*, int, LeafT*, int32_t*);
   hipLaunchKernelGGL((WalkFn)fn, dim3((unsigned)tiles, (unsigned)groups), dim3(kWG3), lds, stream,
-                     sc.bins.as<const uint32_t>(), n, n_pad, pf.num_feature, sc.nan.as<const uint32_t>(), sc.epoch,
+                     sc.bins.as<const uint32_t>(), n, n_pad, pf.num_feature, sc.nan.as<const uint32_t>(),
                      pf.b_blob.as<const char>(), pf.b_n_chunks, (int)pf.b_chunk_stride, cpg,
                      pf.leaf_ids.as<const int32_t>(), pf.n_trees, sc.leaves.as<LeafT>(), d_leaf);
   FD_HIP(hipGetLastError());
   hipLaunchKernelGGL((split_sum_kernel<KIND, LeafT>), dim3((unsigned)((n + kSumRows - 1) / kSumRows)), dim3(256), 0,
                      stream, sc.leaves.as<const LeafT>(), n, pf.n_trees, pf.base_margin, pf.if_offset,
-                     pf.if_denominator, d_prob, d_raw);
+                     pf.if_denominator, d_prob, d_raw, sc.nan.as<uint32_t>());
   FD_HIP(hipGetLastError());
 }
 
@@ -1785,7 +1783,7 @@ void launch_split(Engine& e, const PackedForest& pf, const float* d_X, int64_t n
   const SplitBinArgs a = split_prepare<LeafT>(pf, n, tiles, stream);
   hipLaunchKernelGGL(split_bin_kernel, dim3((unsigned)(tiles * kTile / kSplitBin), (unsigned)pf.num_feature),
                      dim3(kSplitBin), 0, stream, d_X, n, tiles * kTile, (int)ld, pf.num_feature, a.thr, a.thr_off,
-                     pf.bin_steps, a.bins, a.tile_nan, a.epoch);
+                     pf.bin_steps, a.bins, a.tile_nan);
   FD_HIP(hipGetLastError());
   split_walk_sum<LeafT, KIND>(pf, n, d_prob, d_raw, d_leaf, tiles, stream);
 }

@@ -217,6 +217,7 @@ _dp = C.POINTER(C.c_double)
 # (name, restype, argtypes) for every function the header declares.
 SIGNATURES = {
     "fd_last_error": (C.c_char_p, []),
+    "fd_build_id": (C.c_char_p, []),
     "fd_abi_version": (C.c_int, []),
     "fd_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "fd_engine_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
@@ -336,6 +337,13 @@ def _load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # refuse a library built from other sources than the tree it runs beside (FDENGINE_SRC_ROOT: check against
+    # another copy of the package sources, used by tests)
+    from . import _buildid
+    src_pkg = Path(os.environ.get("FDENGINE_SRC_ROOT", PKG_ROOT))
+    src_repo = Path(os.environ.get("FDENGINE_SRC_REPO", src_pkg.parent))
+    if (src_pkg / "csrc").is_dir():
+        _buildid.check(lib.fd_build_id().decode(), src_pkg, src_repo)
     return lib
 
 

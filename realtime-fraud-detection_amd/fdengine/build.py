@@ -7,6 +7,7 @@ Outputs stay in-tree (git-ignored, but shipped to the GPU box by gpurun):
 """
 from __future__ import annotations
 
+import importlib.util
 import os
 import shutil
 import subprocess
@@ -31,6 +32,14 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm required to build libfdengine.so)")
 
 
+def _buildid():
+    """fdengine/_buildid.py, loaded by path (the package cannot be imported before its library exists)"""
+    spec = importlib.util.spec_from_file_location("fdengine_buildid", Path(__file__).resolve().parent / "_buildid.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def _stale(out: Path, inputs) -> bool:
     if not out.exists():
         return True
@@ -39,27 +48,34 @@ def _stale(out: Path, inputs) -> bool:
 
 
 def build_engine(force: bool = False, verbose: bool = True, profile: bool = False) -> Path:
-    """One object per translation unit (compiled in parallel, rebuilt only when stale), then one link.
-    profile=True builds lib/libfdengine_prof.so with the forest and feature kernels' phase-cycle
-    instrumentation (-DFD_FOREST_PROFILE; tools/forest_phases.py / tools/feat_phases.py load it via
-    FDENGINE_LIB)."""
+    """One object per translation unit (compiled in parallel), then one link with a generated build-id object.
+    Staleness is decided by content, not mtime: the library embeds fd_build_id() (a digest of the HIP sources,
+    the csrc headers and include/fdengine.h, plus the flags; fdengine/_buildid.py) and is rebuilt when that
+    differs from the tree's; each object is rebuilt when the digest of its source + the headers + flags recorded
+    beside it differs. profile=True builds lib/libfdengine_prof.so with the forest and feature kernels'
+    phase-cycle instrumentation (-DFD_FOREST_PROFILE; tools/forest_phases.py / tools/feat_phases.py load it
+    via FDENGINE_LIB)."""
     from concurrent.futures import ThreadPoolExecutor
+    B = _buildid()
     LIB_DIR.mkdir(exist_ok=True)
     obj_dir = LIB_DIR / ("obj_prof" if profile else "obj")
     obj_dir.mkdir(exist_ok=True)
     out = LIB_DIR / ("libfdengine_prof.so" if profile else "libfdengine.so")
     srcs = [CSRC / s for s in HIP_SOURCES if (CSRC / s).exists()]
-    headers = list(CSRC.glob("*.h")) + [REPO_ROOT / "include" / "fdengine.h"]
+    headers = sorted(CSRC.glob("*.h")) + [REPO_ROOT / "include" / "fdengine.h"]
     extra = ["-DFD_FOREST_PROFILE"] if profile else []
-    compile_flags = [f for f in HIPCC_FLAGS if f != "-shared"]
-    if not force and not _stale(out, [*srcs, *headers]):
+    compile_flags = [f for f in HIPCC_FLAGS if f != "-shared"] + extra
+    want_id = B.id_string(B.source_digest(), compile_flags)
+    if not force and B.embedded_id(out) == want_id:
         return out  # (the GPU box gets the library without the objects)
 
     def obj(src: Path) -> Path:
         o = obj_dir / (src.stem + ".o")
-        if force or _stale(o, [src, *headers]):
+        stamp = o.with_suffix(".o.digest")
+        dig = B.digest_files([src, *headers]) + " " + " ".join(compile_flags)
+        if force or not o.exists() or not stamp.exists() or stamp.read_text() != dig:
             tmp = o.with_suffix(".o.tmp")
-            cmd = [_hipcc(), *compile_flags, *extra, f"-I{REPO_ROOT / 'include'}", f"-I{CSRC}", "-c", str(src),
+            cmd = [_hipcc(), *compile_flags, f"-I{REPO_ROOT / 'include'}", f"-I{CSRC}", "-c", str(src),
                    "-o", str(tmp)]
             if verbose:
                 print("[build]", " ".join(cmd), flush=True)
@@ -67,15 +83,20 @@ def build_engine(force: bool = False, verbose: bool = True, profile: bool = Fals
             if r.returncode != 0:
                 raise RuntimeError(f"hipcc failed on {src.name}:\n{r.stderr[-6000:]}")
             tmp.replace(o)
+            stamp.write_text(dig)
         return o
 
     jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(obj, srcs))
-    if not force and not _stale(out, objs):
-        return out
+    # the build id: one C function returning the id string (the marker also lets the build read it from the bytes)
+    idc = obj_dir / "build_id.c"
+    idc.write_text('__attribute__((visibility("default"))) const char* fd_build_id(void) {\n'
+                   f'  return "{want_id}";\n}}\n')
+    ido = obj_dir / "build_id.o"
+    subprocess.run(["gcc", "-O2", "-fPIC", "-c", str(idc), "-o", str(ido)], check=True)
     tmp = out.with_suffix(".so.tmp")
-    cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+    cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *map(str, objs), str(ido), "-o", str(tmp)]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -101,8 +101,10 @@ class ModelManager:
         self.model_load_times: Dict[str, datetime] = {}
         self.model_lock = asyncio.Lock()
         self.engine = engine if engine is not None else FraudEngine(_default_device() if device is None else device)
-        # GPU round trips run off the event loop (uvicorn's single loop stays responsive); one
-        # worker thread serialises the calls on this engine (ctypes releases the GIL for their duration)
+        # GPU round trips run off the event loop (uvicorn's single loop stays responsive). Calls that
+        # stay on the loop's thread (predict_batch, loads, reloads) may overlap one in this worker: the library
+        # serialises every entry point on one engine (a per-engine lock, include/fdengine.h), and an unload syncs
+        # the engine's streams before freeing a forest (ctypes releases the GIL for each call's duration)
         self._executor = ThreadPoolExecutor(max_workers=1, thread_name_prefix="fdengine")
         names = list(config.models.keys())
         self._slot_of = {name: i for i, name in enumerate(names)}  # one engine slot per registry entry

@@ -255,3 +255,42 @@ def test_pipelined_sharded_scorer_with_windows_and_sink():
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_outputs_dropped_each_step(world):
+    """The bench's product path (ShardedScorer at world 1 over EngineShardBackend(pipelined=True)) with a caller that
+    keeps nothing on the device: every step's outputs are fresh torch tensors on the engine's stream, each step
+    queues a non_blocking D2H of them into pinned host memory and drops them. torch's caching allocator hands the
+    freed blocks to the next step at once, so the engine must write the caller's buffers in that stream's order
+    (the pipelined call's copy on the engine stream). Results equal the serial fd_score_batch_device bit for bit."""
+    import torch
+
+    from fdengine.sharding import EngineShardBackend, ShardedScorer
+    pop, tx, xgb, ifm = world
+    params = _params()
+    cuts = list(range(0, 240_001, 24_000))
+    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f][:cuts[-1]])).cuda() for f in TXN_FIELDS}
+    torch.cuda.synchronize()
+    ref, pip = _setup(pop, xgb, ifm), _setup(pop, xgb, ifm)
+    try:
+        sc = ShardedScorer(EngineShardBackend(pip, params, [0, 1], pipelined=True), 0, 1)
+        ref.set_stream(torch.cuda.current_stream().cuda_stream)
+        got = []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            out = sc.step({f: t[a:b] for f, t in dev.items()}, b - a)
+            host = [torch.empty(o.shape, dtype=o.dtype, pin_memory=True) for o in out]
+            for h, o in zip(host, out):
+                h.copy_(o, non_blocking=True)
+            del out
+            got.append(host)
+        torch.cuda.synchronize()
+        for (a, b), host in zip(zip(cuts[:-1], cuts[1:]), got):
+            o_ref = _outs(b - a)
+            ref.score_batch_device(params, [0, 1], {f: t[a:b].data_ptr() for f, t in dev.items()}, b - a,
+                                   *[o.data_ptr() for o in o_ref])
+            for x, y in zip(host, o_ref):
+                np.testing.assert_array_equal(x.numpy(), y.cpu().numpy())
+    finally:
+        ref.close()
+        pip.close()
