@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 13
+#define FD_ABI_VERSION 14
 
 enum fd_status {
   FD_OK = 0,
@@ -373,13 +373,14 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
    kernel queued on the ENGINE stream (fd_engine_set_stream) after batch i's scoring: the outputs are
    ordered on the engine stream exactly as with fd_score_batch_device, and a caller may free or reuse
    them in that stream's order (e.g. torch's caching allocator on the stream the engine is bound to).
+   d_vectors (optional, n x FD_VECTOR_WIDTH f32) receives the batch's scoring vectors the same way.
    The input columns must stay unchanged until the engine stream has passed the call (the engine stream
    waits for the batch's features and scoring). Any other engine call in between orders the next
    batch's features after everything queued on the engine stream (no overlap across it). */
 int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
                              const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
-                             int64_t n, double* d_model_probs, double* d_fraud_prob, double* d_confidence,
-                             uint8_t* d_decision, uint8_t* d_risk, void* input_ready);
+                             int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
+                             double* d_confidence, uint8_t* d_decision, uint8_t* d_risk, void* input_ready);
 
 /* per-transaction window / sink inputs beyond fd_txn_batch; any pointer may be NULL */
 typedef struct fd_window_inputs_s {

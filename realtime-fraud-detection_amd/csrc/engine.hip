@@ -987,8 +987,13 @@ __global__ void __launch_bounds__(256)
 pipe_out_copy_kernel(const double* __restrict__ fp, const double* __restrict__ conf, const uint8_t* __restrict__ dec,
                      const uint8_t* __restrict__ risk, const double* __restrict__ mp, int n_mp, int64_t n,
                      double* __restrict__ o_fp, double* __restrict__ o_conf, uint8_t* __restrict__ o_dec,
-                     uint8_t* __restrict__ o_risk, double* __restrict__ o_mp) {
+                     uint8_t* __restrict__ o_risk, double* __restrict__ o_mp, const float4* __restrict__ vec,
+                     float4* __restrict__ o_vec) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o_vec) {  // the vectors: 16 float4 per row, one float4 per thread over the whole grid
+    const int64_t total = n * (FD_VECTOR_WIDTH / 4);
+    for (int64_t q = i; q < total; q += (int64_t)gridDim.x * blockDim.x) o_vec[q] = vec[q];
+  }
   if (i >= n) return;
   o_fp[i] = fp[i];
   if (o_conf) o_conf[i] = conf[i];
@@ -999,8 +1004,8 @@ pipe_out_copy_kernel(const double* __restrict__ fp, const double* __restrict__ c
 
 int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
                              const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
-                             int64_t n, double* d_model_probs, double* d_fraud_prob, double* d_confidence,
-                             uint8_t* d_decision, uint8_t* d_risk, void* input_ready) {
+                             int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
+                             double* d_confidence, uint8_t* d_decision, uint8_t* d_risk, void* input_ready) {
   FD_API_BEGIN
   FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);
@@ -1035,6 +1040,8 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
     e.pipe_dirty = false;
   }
   if (input_ready) FD_HIP(hipStreamWaitEvent(Sf, static_cast<hipEvent_t>(input_ready), 0));
+  // the slot's vectors are rewritten below: after batch i-nbuf's output copy if that one read them
+  if (e.pipe_copy_live[s] && e.pipe_copy_vec[s]) FD_HIP(hipStreamWaitEvent(Sf, e.pipe_copy_ev[s], 0));
   // mode 1: the slot pass (scratch set s & 1, untouched by batch i-1) runs at once; the bucket pass waits for
   // batch i-1's card updates
   hipEvent_t before_buckets = (!m2 && e.pipe_feat_live[prev]) ? e.pipe_feat_ev[prev] : nullptr;
@@ -1085,10 +1092,12 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
   e.pipe_done_live[s] = true;
   FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[s], 0));
   hipLaunchKernelGGL(pipe_out_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e.stream, s_fp, s_conf,
-                     s_dec, s_risk, s_mp, n_mp, n, d_fraud_prob, d_confidence, d_decision, d_risk, d_model_probs);
+                     s_dec, s_risk, s_mp, n_mp, n, d_fraud_prob, d_confidence, d_decision, d_risk, d_model_probs,
+                     reinterpret_cast<const float4*>(vec), reinterpret_cast<float4*>(d_vectors));
   FD_HIP(hipGetLastError());
   FD_HIP(hipEventRecord(e.pipe_copy_ev[s], e.stream));
   e.pipe_copy_live[s] = true;
+  e.pipe_copy_vec[s] = d_vectors != nullptr;
   FD_API_END
 }
 

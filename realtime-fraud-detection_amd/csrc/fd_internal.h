@@ -316,6 +316,7 @@ struct Engine {
   DeviceBuffer pipe_out[kPipeSlots];
   hipEvent_t pipe_copy_ev[kPipeSlots] = {};
   bool pipe_copy_live[kPipeSlots] = {};
+  bool pipe_copy_vec[kPipeSlots] = {};  // that copy also read the slot's vectors (the slot's next features wait)
   // fd_score_batch_device for latency batches as a replayed hipGraph ("graphs" option, engine.hip): the inputs
   // are gathered into fixed staging by one kernel, the rest of the step is one graph launch; a graph per
   // (shape, models, outputs, stream, grouping parity), all dropped by any other engine call (graph_epoch)

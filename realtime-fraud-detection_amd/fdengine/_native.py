@@ -249,7 +249,7 @@ SIGNATURES = {
     "fd_score_batch_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, C.POINTER(_vp), _vp,
                                         C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "fd_score_batch_pipelined": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, C.POINTER(_vp), _vp,
-                                           C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+                                           C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "fd_state_load_users_ext_host": (C.c_int, [_vp, C.POINTER(fd_users_ext)]),
     "fd_load_merchants_ext_host": (C.c_int, [_vp, C.POINTER(fd_merchants_ext)]),
     "fd_load_vocab_host": (C.c_int, [_vp, _vp, _vp]),

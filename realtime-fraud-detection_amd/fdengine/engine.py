@@ -210,12 +210,14 @@ class FraudEngine:
     def score_batch_pipelined(self, params: N.fd_blend_params, slots: Sequence[int], txn_ptrs: dict, n: int,
                               fp_ptr: int, conf_ptr: int = 0, dec_ptr: int = 0, risk_ptr: int = 0,
                               model_probs_ptr: int = 0, ext_ptrs: Optional[Sequence[Optional[int]]] = None,
-                              present: Optional[Sequence[int]] = None, input_ready: int = 0) -> None:
+                              present: Optional[Sequence[int]] = None, input_ready: int = 0,
+                              vec_ptr: int = 0) -> None:
         """Streaming form of score_batch_device (fd_score_batch_pipelined): the batch's features run on the
         engine's feature stream, overlapping the previous batch's forests; outputs are ordered on the engine
-        stream as with score_batch_device. input_ready: a hipEvent_t handle (e.g. torch.cuda.Event's
-        cuda_event) recorded when the input columns were complete; 0 = complete before this call. The input
-        columns must stay unchanged until the outputs are complete."""
+        stream as with score_batch_device (written there by a copy from engine staging, so the caller may free
+        them in that stream's order). input_ready: a hipEvent_t handle (e.g. torch.cuda.Event's cuda_event)
+        recorded when the input columns were complete; 0 = complete before this call. The input columns must
+        stay unchanged until the engine stream has passed the call."""
         M = params.n_models
         sl = np.array(list(slots) + [-1] * (N.FD_MAX_MODELS - len(slots)), np.int32)
         pres = np.array([1] * M if present is None else list(present), np.uint8)
@@ -226,8 +228,8 @@ class FraudEngine:
         b = N.fd_txn_batch(*[int(txn_ptrs[f]) for f in N.TXN_FIELDS])
         opt = lambda p: C.c_void_p(p) if p else None  # noqa: E731
         N.call("fd_score_batch_pipelined", self._h, C.byref(params), _ptr(sl), ext, _ptr(pres), C.byref(b),
-               int(n), opt(model_probs_ptr), C.c_void_p(fp_ptr), opt(conf_ptr), opt(dec_ptr), opt(risk_ptr),
-               opt(input_ready))
+               int(n), opt(vec_ptr), opt(model_probs_ptr), C.c_void_p(fp_ptr), opt(conf_ptr), opt(dec_ptr),
+               opt(risk_ptr), opt(input_ready))
 
     def pipelined_scorer(self, params: N.fd_blend_params, slots: Sequence[int],
                          present: Optional[Sequence[int]] = None) -> "PipelinedScorer":
@@ -639,8 +641,8 @@ class PipelinedScorer:
         for f in N.TXN_FIELDS:
             setattr(b, f, txn_ptrs[f])
         if self.pipelined:
-            rc = self._fn(self.eng._h, *self._args, int(n), model_probs_ptr or None, fp_ptr, conf_ptr or None,
-                          dec_ptr or None, risk_ptr or None, input_ready or None)
+            rc = self._fn(self.eng._h, *self._args, int(n), vec_ptr or None, model_probs_ptr or None, fp_ptr,
+                          conf_ptr or None, dec_ptr or None, risk_ptr or None, input_ready or None)
             N.check(rc, "fd_score_batch_pipelined")
         else:
             rc = self._fn(self.eng._h, *self._args, int(n), vec_ptr or None, model_probs_ptr or None, fp_ptr,

@@ -124,9 +124,11 @@ class EngineShardBackend:
             self.eng.score_records_device(self.params, self.slots, rec.data_ptr(), m, res.data_ptr(), self.present)
         return res
 
-    def score_batch(self, txns: dict, n: int, input_ready=None):
+    def score_batch(self, txns: dict, n: int, input_ready=None, vectors=None, model_probs=None):
         """One shard: the whole hot path on the ingest GPU in arrival order (nothing to route).
-        input_ready: optional torch.cuda.Event recorded once the input tensors were complete (pipelined)."""
+        input_ready: optional torch.cuda.Event recorded once the input tensors were complete (pipelined).
+        vectors / model_probs: optional device tensors (n x 64 f32 / n_models x n f64) that also receive the
+        batch's scoring vectors / per-model probabilities."""
         t = self.torch
         fp = t.empty(n, dtype=t.float64, device=self.device)
         conf = t.empty(n, dtype=t.float64, device=self.device)
@@ -138,10 +140,15 @@ class EngineShardBackend:
                 if self._scorer is None:
                     self._scorer = self.eng.pipelined_scorer(self.params, self.slots, self.present)
                 self._scorer(ptrs, n, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
-                             input_ready.cuda_event if input_ready is not None else 0)
+                             input_ready.cuda_event if input_ready is not None else 0,
+                             vec_ptr=vectors.data_ptr() if vectors is not None else 0,
+                             model_probs_ptr=model_probs.data_ptr() if model_probs is not None else 0)
             else:
                 self.eng.score_batch_device(self.params, self.slots, ptrs, n, fp.data_ptr(), conf.data_ptr(),
-                                            dec.data_ptr(), risk.data_ptr(), present=self.present)
+                                            dec.data_ptr(), risk.data_ptr(), present=self.present,
+                                            vec_ptr=vectors.data_ptr() if vectors is not None else 0,
+                                            model_probs_ptr=model_probs.data_ptr() if model_probs is not None
+                                            else 0)
         return fp, conf, dec, risk
 
     def snapshot(self, path: str, rank: int, world: int) -> int:
@@ -199,7 +206,7 @@ class ShardedScorer:
         return int(g.cpu()[0])
 
     def step(self, txns: dict, n: int, extras: Optional[dict] = None, windows: bool = False, sink: bool = False,
-             flush: bool = False, input_ready=None):
+             flush: bool = False, input_ready=None, vectors=None, model_probs=None):
         """txns: field -> tensor (n rows) on the backend's device, in arrival order.
         input_ready: optional torch.cuda.Event recorded once `txns` were complete (a pipelined backend's features
         wait for it instead of assuming resident inputs).
@@ -207,15 +214,18 @@ class ShardedScorer:
         extras: {"payment_method": u8, "is_fraud": u8} tensors (n rows) for the keyed aggregates.
         windows / sink: after scoring, run the Flink window aggregates / the sink aggregates on the owned
         transactions (module docstring); the fired windows are left in self.last_windows =
-        (this shard's user windows, the node's merged merchant windows); flush: end of input."""
+        (this shard's user windows, the node's merged merchant windows); flush: end of input.
+        vectors / model_probs (world 1, backends with score_batch): optional device tensors that also receive the
+        batch's scoring vectors (n x 64) / per-model probabilities (n_models x n)."""
         import torch
         G = self.world
         aux = windows or sink
         if G == 1:  # one shard owns every card: no partition, no exchange
             self.last_counts = ([n], [n])
             if hasattr(self.be, "score_batch"):
-                out = self.be.score_batch(txns, n, input_ready) if input_ready is not None else \
-                    self.be.score_batch(txns, n)
+                kw = {k: v for k, v in (("input_ready", input_ready), ("vectors", vectors),
+                                        ("model_probs", model_probs)) if v is not None}
+                out = self.be.score_batch(txns, n, **kw)
                 if aux:
                     cols = {f: txns[f] for f in ("card_key", "ts_ms", "amount_cents", "merchant")}
                     cols.update(extras or {})

@@ -243,7 +243,8 @@ def card_keys(ids, seed: int = 42) -> np.ndarray:
 
 def card_attrs(ids, seed: int = 42) -> dict:
     """Attributes of cards `ids` (int64 in [0, n_cards)) with the simulator's distributions
-    (simulator.py:212-238: avg amount LogNormal(4,1), 1-3 device fingerprints, account age)."""
+    (simulator.py:212-238: avg amount LogNormal(4,1), 1-3 device fingerprints, account age, transactions per day
+    floor(Gamma(2, 2)) + 1 (:229), Gamma(2, 2) drawn as the sum of two Exp(2))."""
     from scipy.special import ndtri
     ids = np.asarray(ids, np.int64).astype(np.uint64)
     key = card_keys(ids, seed)
@@ -251,8 +252,10 @@ def card_attrs(ids, seed: int = 42) -> dict:
     fps = np.stack([_fmix64(ids * np.uint64(4) + np.uint64(j + 1) + np.uint64(seed)) | (np.uint64(1) << np.uint64(63))
                     for j in range(3)], axis=1)
     fps[np.arange(3)[None, :] >= n_fp[:, None]] = 0
+    freq = np.floor(-2.0 * np.log(_u01(ids, seed, 5)) - 2.0 * np.log(_u01(ids, seed, 6))) + 1.0
     return {"key": key, "avg_amount": np.exp(4.0 + ndtri(_u01(ids, seed, 2))),
-            "account_age_days": np.floor(_u01(ids, seed, 3) * 730).astype(np.int32), "device_fp": fps}
+            "account_age_days": np.floor(_u01(ids, seed, 3) * 730).astype(np.int32), "device_fp": fps,
+            "txn_frequency": freq.astype(np.int16)}
 
 
 def merchants_table(n_merchants: int = 5000, seed: int = 42) -> dict:

@@ -127,3 +127,157 @@ def test_config1_simulator_stream(engine):
     cuts = [0, 1000, 33768, 66536, 100_000]  # a latency-size batch, then 32 k + 32 k (fused) + the rest
     for a, b in zip(cuts[:-1], cuts[1:]):
         _score_and_check(engine, orc, xgb, ifm, {k: v[a:b] for k, v in tx.items()}, b - a)
+
+
+def _fit_models_oracle(trees=500, if_trees=100):
+    """Models in the reference's formats fitted on realistic scoring vectors: a 20 k-card population's stream through
+    the CPU oracle's feature path (as bench.fit_models does through a scratch engine)."""
+    from oracle.features_c import OracleFeatureState
+    spop = synth.population(20000, 500, seed=11)
+    stx = synth.txn_stream(spop, 40000, seed=12, rate_per_s=20.0)
+    o = OracleFeatureState(1 << 16, 1, 16)
+    U, M = spop["users"], spop["merchants"]
+    o.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+    o.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+    _, X = o.run(stx)
+    xgb = xgboost_from_json_doc(synth.xgboost_doc(trees, 8, 64, X[-8192:], seed=13))
+    ifm = iforest_from_sklearn(synth.isolation_forest(X[-8192:].astype(np.float64), n_estimators=if_trees))
+    return xgb, ifm
+
+
+@pytest.mark.timeout(900)
+def test_config4_full_size_warm_pipelined():
+    """BASELINE configs[3] at its stated size on one GPU, through the path the bench times: 100 M cards resident,
+    24 h of SURVEY §8(d)-shaped history (floor(Gamma(2,2)) + 1 transactions per card per day, Poisson arrivals;
+    simulator.py:229,302) run through the feature path so the 5 min / 1 h / 24 h windows hold events
+    (RedisService.java:178-207), then three 64 k micro-batches submitted back to back through ShardedScorer at
+    world 1 over EngineShardBackend(pipelined=True) -> fd_score_batch_pipelined (batch i+1's features overlap
+    batch i's forests). Vectors, model probabilities, fraud probability, decision and risk against the oracle chain,
+    which replays the history rows of exactly the cards those batches touch."""
+    import torch
+
+    import oracle
+    from fdengine import synth_gpu
+    from fdengine.sharding import EngineShardBackend, ShardedScorer
+    from oracle import scoring_ref as S
+    from oracle.features_c import OracleFeatureState
+    cards, B, K, P = 100_000_000, 65536, 16, 3
+    merch = synth.merchants_table(5000, seed=100)
+    xgb, ifm = _fit_models_oracle()
+    names = ["xgboost_primary", "isolation_forest"]
+    w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
+    params = FraudEngine.blend_params([w[k] for k in names], [S.CONF_MULT[k] for k in names])
+    eng = FraudEngine(0)
+    try:
+        eng.state_init(1 << 28, 1, K)
+        eng.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
+        sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), 0, 1)  # binds torch's stream
+        dev = torch.device("cuda", 0)
+        wk = synth_gpu.warm_workload(eng, dev, cards, 0, 1, n_batches=P, batch=B, hours=24.0, keep_batches=P)
+        assert wk["history_transactions"] > 4e8  # ~4.5 per card per day
+        eng.load_forest(0, xgb)
+        eng.load_forest(1, ifm)
+        assert eng.state_info()["cards"] >= cards
+        res = wk["resident"]
+        got = []
+        for b in range(P):  # back to back: no sync between the pipelined steps
+            vec = torch.empty((B, 64), dtype=torch.float32, device=dev)
+            mp = torch.empty((2, B), dtype=torch.float64, device=dev)
+            out = sc.step({f: t[b * B:(b + 1) * B] for f, t in res.items()}, B, vectors=vec, model_probs=mp)
+            got.append((vec, mp, out))
+        torch.cuda.synchronize()
+        o = OracleFeatureState(1 << 22, 1, K)
+        pr = wk["profiles"]
+        o.load_users(pr["key"], pr["avg_amount"], pr["account_age_days"], pr["device_fp"])
+        o.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
+        o.run(wk["history_rows"])
+        raws = []
+        for b, (vec, mp, out) in enumerate(got):
+            part = {f: v[b * B:(b + 1) * B] for f, v in wk["head"].items()}
+            raw, rvec = o.run(part, want_raw=True)
+            raws.append(raw)
+            V = vec.cpu().numpy()
+            _check_vectors(V, rvec)
+            px, _, _ = oracle.xgb_predict(xgb, V)
+            pi, _, _ = oracle.iforest_predict(ifm, V)
+            M = mp.cpu().numpy()
+            assert np.abs(M[0] - px).max() <= 1e-5 and np.abs(M[1] - pi).max() <= 1e-5
+            fp, conf, dec, risk = oracle.blend_weighted(np.stack([M[0], M[1]]), [w[k] for k in names],
+                                                        [S.CONF_MULT[k] for k in names])
+            FP, CF, DC, RK = (t.cpu().numpy() for t in out)
+            np.testing.assert_array_equal(FP, fp)
+            np.testing.assert_array_equal(CF, conf)
+            np.testing.assert_array_equal(DC, dec)
+            np.testing.assert_array_equal(RK, risk)
+        occ = synth_gpu.occupancy(np.concatenate(raws))
+        assert occ["mean_events_24h"] > 3.0 and occ["frac_with_24h_history"] > 0.8, occ  # warm windows
+        assert occ["mean_events_1h"] > 0.1, occ
+    finally:
+        eng.close()
+
+
+@pytest.mark.timeout(600)
+def test_config5_chain():
+    """BASELINE configs[4]'s exact chain: 1 k micro-batches, card-state features + each card's last 10 events ->
+    XGBoost 500 x 8 (tree-split path) + IsolationForest 100 + LSTM(128) on f32 MFMA (lstm_kernel4) -> 3-model blend,
+    through fd_score_batch_device, against the oracle chain (oracle features + forests, lstm_ref's PyTorch fp32
+    forward over the oracle's card histories, scoring_ref's blend). State carried over 12 batches."""
+    import torch
+
+    import oracle
+    from fdengine import lstm as L
+    from fdengine._native import FD_SLOT_LSTM
+    from oracle import lstm_ref as R
+    from oracle import scoring_ref as S
+    from oracle.features_c import OracleFeatureState
+    T, B = 10, 1000
+    pop = synth.population(30000, 5000, seed=51)
+    tx = synth.txn_stream(pop, 12 * B, seed=52, rate_per_s=5.0)
+    xgb, ifm = _fit_models_oracle()
+    lw = L.random_weights(16, 128, 1, seed=53)
+    U, M = pop["users"], pop["merchants"]
+    names = ["xgboost_primary", "isolation_forest", "lstm_sequential"]
+    w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05, "lstm_sequential": 0.25})
+    params = FraudEngine.blend_params([w[k] for k in names], [S.CONF_MULT[k] for k in names])
+    eng = FraudEngine(0)
+    try:
+        eng.state_init(1 << 16, 1, 16, seq_len=T)
+        eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        eng.load_forest(0, xgb)
+        eng.load_forest(1, ifm)
+        eng.load_lstm(lw)
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        o = OracleFeatureState(1 << 16, 1, 16)
+        o.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+        o.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        hist = R.SequenceState(T)
+        dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f])).cuda() for f in TXN_FIELDS}
+        for b in range(12):
+            sl = slice(b * B, (b + 1) * B)
+            out = [torch.empty(B, dtype=d, device="cuda") for d in (torch.float64, torch.float64, torch.uint8,
+                                                                     torch.uint8)]
+            vec = torch.empty((B, 64), dtype=torch.float32, device="cuda")
+            mp = torch.empty((3, B), dtype=torch.float64, device="cuda")
+            eng.score_batch_device(params, [0, 1, FD_SLOT_LSTM], {f: t[sl].data_ptr() for f, t in dev.items()}, B,
+                                   *[t.data_ptr() for t in out], vec_ptr=vec.data_ptr(), model_probs_ptr=mp.data_ptr())
+            torch.cuda.synchronize()
+            part = {k: v[sl] for k, v in tx.items()}
+            rraw, rvec = o.run(part, want_raw=True)
+            V = vec.cpu().numpy()
+            _check_vectors(V, rvec)
+            Mp = mp.cpu().numpy()
+            px, _, _ = oracle.xgb_predict(xgb, V)
+            pi, _, _ = oracle.iforest_predict(ifm, V)
+            pl = R.lstm_forward(lw, hist.run(part["card_key"], rraw))
+            assert np.abs(Mp[0] - px).max() <= 1e-5 and np.abs(Mp[1] - pi).max() <= 1e-5
+            assert np.abs(Mp[2] - pl).max() <= 1e-5, np.abs(Mp[2] - pl).max()
+            fp, conf, dec, risk = oracle.blend_weighted(Mp, [w[k] for k in names], [S.CONF_MULT[k] for k in names])
+            FP, CF, DC, RK = (t.cpu().numpy() for t in out)
+            np.testing.assert_array_equal(FP, fp)
+            np.testing.assert_array_equal(CF, conf)
+            np.testing.assert_array_equal(DC, dec)
+            np.testing.assert_array_equal(RK, risk)
+    finally:
+        eng.set_stream(None)
+        eng.close()

@@ -148,43 +148,27 @@ def test_small_streams_variants_identical(world):
 
 
 @pytest.mark.timeout(200)
-def test_graph_replay_nan_tiles(world):
-    """Replayed graphs with NaN in the scored rows: an XGBoost model over 70 features scores the 64-wide vectors, so
-    features 64..69 are missing (NaN, the stored default direction) in every tile of the tree-split path. Graphs of
-    both grouping parities replay alternately, with sampled timed (direct) steps in between; each replay must still
-    see its tiles' NaN flags (they are cleared by the step's own sum kernel, not compared with a captured epoch)."""
-    import torch
-    pop, tx, _, ifm = world
-    X70 = synth.feature_matrix(4096, 70, seed=21)
-    xgb70 = xgboost_from_json_doc(synth.xgboost_doc(60, 8, 70, X70, seed=22))
-    internal = xgb70.left >= 0
-    assert (xgb70.feature[internal] >= 64).any(), "the model must split on features the vectors lack"
-    params = _params(False)
-    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f][:16000])).cuda() for f in TXN_FIELDS}
-    ref, gra = _setup(pop, xgb70, ifm, None, False), _setup(pop, xgb70, ifm, None, True)
+def test_split_path_nan_flags_per_call(world):
+    """The tree-split path's per-tile "holds a NaN" flags are set by the binning launch and cleared by the step's own
+    sum kernel (no host-side epoch, so a replayed graph cannot compare against a stale one). Scoring vectors from the
+    feature kernel are always finite (FeatureProcessor's final validation), so NaN reaches this path through
+    fd_score_matrix / predict: latency batches alternating with and without NaN (and NaN in a single tile), each
+    equal to the oracle (leaf ids exact, XGBoost `x < thr` with NaN -> default direction, sklearn NaN rows)."""
+    import oracle
+    _, _, xgb, ifm = world
+    eng = FraudEngine(0)
     try:
-        st = torch.cuda.current_stream()
-        for e in (ref, gra):
-            e.set_stream(st.cuda_stream)
-        outs = [[torch.empty(1000, dtype=t, device="cuda") for t in (torch.float64,) * 2 + (torch.uint8,) * 2]
-                for _ in range(2)]
-        mp = torch.empty((2, 1000), dtype=torch.float64, device="cuda")
-        got, want = [], []
-        for i in range(16):
-            if i == 5:
-                gra.set_option("timing_every", 3)
-                gra.set_timing(True)
-            ptrs = {f: t[i * 1000:(i + 1) * 1000].data_ptr() for f, t in dev.items()}
-            for e, dst in ((ref, want), (gra, got)):
-                fp, conf, dec, risk = outs[i & 1]
-                e.score_batch_device(params, [0, 1], ptrs, 1000, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(),
-                                     risk.data_ptr(), model_probs_ptr=mp.data_ptr())
-                dst.append([fp.clone(), dec.clone(), mp.clone()])
-        torch.cuda.synchronize()
-        for i, (g, w) in enumerate(zip(got, want)):
-            for x, y in zip(g, w):
-                assert np.array_equal(x.cpu().numpy(), y.cpu().numpy()), f"batch {i} differs"
-        assert gra.counter("graphs_replayed") >= 6, gra.counter("graphs_replayed")
+        eng.load_forest(0, xgb)
+        eng.load_forest(1, ifm)
+        for i in range(8):
+            X = synth.feature_matrix(1000, 64, seed=40 + i, nan_frac=0.05 if i % 2 == 0 else 0.0)
+            if i == 3:
+                X[700, 5] = np.nan  # one NaN in the third tile only
+            px, mx, lx = eng.predict(0, X, want_raw=True, want_leaf=True)
+            rpx, rmx, rlx = oracle.xgb_predict(xgb, X, want_leaf=True)
+            assert (lx == rlx).all() and (mx.astype(np.float32) == rmx).all(), f"XGBoost call {i}"
+            pi, di, li = eng.predict(1, X, want_raw=True, want_leaf=True)
+            rpi, rdi, rli = oracle.iforest_predict(ifm, X, want_leaf=True)
+            assert (li == rli).all() and (di == rdi).all(), f"IsolationForest call {i}"
     finally:
-        ref.close()
-        gra.close()
+        eng.close()
