@@ -605,6 +605,8 @@ class Config4(Config3):
         self.next_batch += 1
         B = self.B
         part = {f: t[b * B:(b + 1) * B] for f, t in self.dev.items()}
+        if self.world > 1 and b + 1 < self.n_batches:  # the next batch's partition + count exchange, one step ahead
+            kw["prefetch"] = ({f: t[(b + 1) * B:(b + 2) * B] for f, t in self.dev.items()}, B)
         self.out = self.scorer.step(part, B, **kw)
 
     def step_h2d(self, i):
@@ -1009,6 +1011,8 @@ def main():
                          "--history-hours of history through the feature path; cold = round 2's uniform stream "
                          "from an empty state")
     ap.add_argument("--history-hours", type=float, default=24.0)
+    ap.add_argument("--loaded-inflight", type=int, default=3,
+                    help="loaded-latency loop: micro-batches submitted and not yet returned at most")
     ap.add_argument("--loaded-iters", type=int, default=200,
                     help="steps of the loaded-latency loop: back to back like the timed region, each step's results "
                          "copied to pinned host memory, per-batch submit -> results-on-host times")
@@ -1092,46 +1096,37 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # loaded latency: the same back-to-back stream as the timed region, each step's results copied to pinned host
-    # memory behind it on the output stream; a host thread waits on each batch's completion event in order and
-    # stamps it, so a batch's latency is host submit -> its scores in host memory WHILE later batches keep the GPU
-    # busy (the operating point `value` is measured at)
+    # loaded latency: the stream at the throughput operating point with a consumer's backpressure — at most
+    # --loaded-inflight micro-batches submitted and not yet back (the host waits for batch i-D's results before it
+    # submits batch i), each step's results copied to pinned host memory behind it on the output stream. A batch's
+    # latency = its host submit -> its results in host memory, from GPU event timestamps relative to an event
+    # recorded on the idle stream when the loop's host clock starts (offset: that event's launch, a few us)
     loaded = None
     if args.loaded_iters > 0 and hasattr(wl, "fetch"):
-        import queue
-        import threading
-        q, done_at = queue.Queue(), {}
-
-        def waiter():
-            while True:
-                item = q.get()
-                if item is None:
-                    return
-                k, ev = item
-                ev.synchronize()
-                done_at[k] = time.perf_counter()
-
-        th = threading.Thread(target=waiter, daemon=True)
-        th.start()
-        sub = {}
-        a0 = time.perf_counter()
+        D = max(1, args.loaded_inflight)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        h0 = time.perf_counter()
+        evs, sub = [], []
         for i in range(args.loaded_iters):
-            sub[i] = time.perf_counter()
+            if i >= D:
+                evs[i - D].synchronize()
+            sub.append(time.perf_counter() - h0)
             wl.step(i)
             wl.fetch(i)
-            ev = torch.cuda.Event(blocking=False)
+            ev = torch.cuda.Event(enable_timing=True)
             ev.record(stream)
-            q.put((i, ev))
-        q.put(None)
-        th.join()
-        a1 = time.perf_counter()
-        ll = np.array([(done_at[i] - sub[i]) * 1e3 for i in range(args.loaded_iters)])
+            evs.append(ev)
+        torch.cuda.synchronize()
+        h1 = time.perf_counter()
+        ll = np.array([e0.elapsed_time(ev) - s_ * 1e3 for ev, s_ in zip(evs, sub)])
         loaded = {"p50_ms": round(float(np.percentile(ll, 50)), 4), "p99_ms": round(float(np.percentile(ll, 99)), 4),
-                  "max_ms": round(float(ll.max()), 4), "samples": len(ll),
-                  "throughput_txn_per_s": round(args.loaded_iters * args.batch * world / (a1 - a0), 1),
-                  "basis": "steps back to back (as the timed region) + each step's fraud_prob / decision / risk "
-                           "D2H to pinned host memory; latency = host submit -> that batch's D2H complete, stamped "
-                           "by a host thread waiting on the batches' events in order"}
+                  "max_ms": round(float(ll.max()), 4), "samples": len(ll), "inflight": D,
+                  "throughput_txn_per_s": round(args.loaded_iters * args.batch * world / (h1 - h0), 1),
+                  "basis": f"back-to-back steps with at most {D} micro-batches in flight (backpressure), each "
+                           "step's fraud_prob / decision / risk D2H to pinned host memory; latency = host submit -> "
+                           "that D2H complete (GPU event timestamps)"}
         if dist:
             t = torch.tensor([loaded["p99_ms"]], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

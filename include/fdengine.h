@@ -413,6 +413,11 @@ int fd_route_partition_device(fd_engine* eng, const fd_txn_batch* txns, int64_t 
    payment_method and is_fraud are read, fraud_score is produced by the owner) */
 int fd_route_partition_ex_device(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* extra,
                                  int64_t n, int32_t n_shards, void* d_records, int64_t* d_counts);
+/* the same on the caller's `stream` (a hipStream_t; its own scratch), leaving the engine stream and the
+   pipelined stream undisturbed: the pipelined sharded step partitions the next micro-batch and exchanges its
+   counts while the owner GPUs still score the current one (fdengine/sharding.py) */
+int fd_route_partition_stream(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* extra,
+                              int64_t n, int32_t n_shards, void* d_records, int64_t* d_counts, void* stream);
 /* owner side: received records (+ their result records, may be NULL) back to columns for the window /
    sink kernels: out's non-NULL fields (card_key, ts_ms, amount_cents, merchant, device_fp, ip_class, hour,
    weekend) and payment_method / is_fraud / fraud_score (the result's fraud_prob; NaN without results) */
@@ -423,6 +428,14 @@ int fd_route_unpack_device(fd_engine* eng, const void* d_records, const void* d_
    {f64 fraud_prob, f64 confidence, u32 seq, u8 decision, u8 risk, u16 pad} in the records' order */
 int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
                             const uint8_t* present, const void* d_records, int64_t n, void* d_results);
+/* streaming form over received records (fd_score_batch_pipelined's pipeline: features on the engine's
+   pipeline streams after the previous batch's features and after `input_ready` — the event the caller
+   recorded once the records' all-to-all had landed —, scoring, then d_results written on the engine
+   stream, where the caller queues the return all-to-all). The owner's batch i+1 features overlap batch i's
+   forests; the records must stay unchanged until the engine stream has passed the call. */
+int fd_score_records_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                               const uint8_t* present, const void* d_records, int64_t n, void* d_results,
+                               void* input_ready);
 /* out[seq] = result for each of the n returned records; conf/decision/risk may be NULL.
    fd_engine_sync reports a record whose seq is outside [0, n). */
 int fd_route_scatter_results_device(fd_engine* eng, const void* d_results, int64_t n, double* d_fraud_prob,

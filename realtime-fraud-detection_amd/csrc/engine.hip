@@ -282,7 +282,7 @@ int fd_engine_destroy(fd_engine* eng) {
   e.feat_in.release();
   fd::windows_release(e);
   fd::sink_release(e);
-  for (auto* b : {&e.route_blk, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.wpk4, &e.lstm.bias,
+  for (auto* b : {&e.route_blk, &e.route_blk_stream, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.wpk4, &e.lstm.bias,
                   &e.lstm.wout, &e.lstm.bout, &e.state.seq})
     b->release();
   if (e.aux_stream) {
@@ -982,37 +982,37 @@ int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const i
 }
 
 // fd_score_batch_pipelined's outputs: engine staging -> the caller's buffers, on the engine stream (one thread per
-// transaction; null destinations are skipped)
+// transaction; null destinations are skipped); result records (routed batches) as 8-byte words
 __global__ void __launch_bounds__(256)
 pipe_out_copy_kernel(const double* __restrict__ fp, const double* __restrict__ conf, const uint8_t* __restrict__ dec,
                      const uint8_t* __restrict__ risk, const double* __restrict__ mp, int n_mp, int64_t n,
                      double* __restrict__ o_fp, double* __restrict__ o_conf, uint8_t* __restrict__ o_dec,
                      uint8_t* __restrict__ o_risk, double* __restrict__ o_mp, const float4* __restrict__ vec,
-                     float4* __restrict__ o_vec) {
+                     float4* __restrict__ o_vec, const uint64_t* __restrict__ res, uint64_t* __restrict__ o_res) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   if (o_vec) {  // the vectors: 16 float4 per row, one float4 per thread over the whole grid
     const int64_t total = n * (FD_VECTOR_WIDTH / 4);
-    for (int64_t q = i; q < total; q += (int64_t)gridDim.x * blockDim.x) o_vec[q] = vec[q];
+    for (int64_t q = i; q < total; q += stride) o_vec[q] = vec[q];
+  }
+  if (o_res) {
+    const int64_t total = n * (int64_t)(sizeof(fd::ResultRecord) / 8);
+    for (int64_t q = i; q < total; q += stride) o_res[q] = res[q];
   }
   if (i >= n) return;
-  o_fp[i] = fp[i];
+  if (o_fp) o_fp[i] = fp[i];
   if (o_conf) o_conf[i] = conf[i];
   if (o_dec) o_dec[i] = dec[i];
   if (o_risk) o_risk[i] = risk[i];
   for (int m = 0; m < n_mp; ++m) o_mp[(size_t)m * n + i] = mp[(size_t)m * n + i];
 }
 
-int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
-                             const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
-                             int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
-                             double* d_confidence, uint8_t* d_decision, uint8_t* d_risk, void* input_ready) {
-  FD_API_BEGIN
-  FD_ENGINE_LOCK(eng);
-  Engine& e = E_quiet(eng);
-  FD_REQUIRE(params && txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
-  if (n == 0) return FD_OK;
-  FD_REQUIRE(d_fraud_prob != nullptr, FD_ERR_INVALID_ARG, "null fraud_prob output");
-  FD_REQUIRE(params->n_models >= 1 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "bad n_models");
+// One micro-batch of the pipelined stream: transaction columns (txns) or routed 48-B records (records, whose scores
+// leave as 24-B result records in d_results). Shared by fd_score_batch_pipelined and fd_score_records_pipelined.
+static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* slots, const double* const* ext_probs,
+                      const uint8_t* present, const fd_txn_batch* txns, const void* records, int64_t n,
+                      float* d_vectors, double* d_model_probs, double* d_fraud_prob, double* d_confidence,
+                      uint8_t* d_decision, uint8_t* d_risk, void* d_results, void* input_ready) {
   const bool m2 = e.pipe_mode == 2;
   for (int k = 0; k < (m2 ? 3 : 2); ++k)
     if (!e.pipe_stream[k]) FD_HIP(hipStreamCreateWithFlags(&e.pipe_stream[k], hipStreamNonBlocking));
@@ -1058,7 +1058,10 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
     e.pipe_seq[s].ensure((size_t)n * e.state.S * fd::kSeqInput * sizeof(float));
     seq = e.pipe_seq[s].as<float>();
   }
-  fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, m2 ? 0 : s & 1, before_buckets);
+  if (records)
+    fd::launch_features_records(e, records, n, vec, seq, Sf, e.pipe_lean, m2 ? 0 : s & 1, before_buckets);
+  else
+    fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, m2 ? 0 : s & 1, before_buckets);
   FD_HIP(hipEventRecord(e.pipe_feat_ev[s], Sf));
   e.pipe_feat_live[s] = true;
   if (m2) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_feat_ev[s], 0));
@@ -1066,16 +1069,19 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
   // buffers): those batches also wait for the previous batch's scoring
   if (e.pipe_done_live[prev] && !fd::ensemble_applies(e, *params, slots, present, n))
     FD_HIP(hipStreamWaitEvent(Sc, e.pipe_done_ev[prev], 0));
-  // this slot's output staging: free once batch i-nbuf's copy to its caller (on e.stream) is done
+  // this slot's output staging: free once batch i-nbuf's copy to its caller (on e.stream) is done. Routed batches
+  // always stage the four columns (the result records are packed from them when the fused kernel does not apply).
   const int n_mp = d_model_probs ? params->n_models : 0;
   const size_t n8 = (size_t)n * 8, a8 = ((size_t)n + 7) & ~(size_t)7;
-  e.pipe_out[s].ensure((2 + (size_t)n_mp) * n8 + 2 * a8);
+  const size_t rbytes = records ? (size_t)n * sizeof(fd::ResultRecord) : 0;
+  e.pipe_out[s].ensure((2 + (size_t)n_mp) * n8 + 2 * a8 + rbytes);
   char* so = e.pipe_out[s].as<char>();
   double* s_fp = reinterpret_cast<double*>(so);
-  double* s_conf = d_confidence ? reinterpret_cast<double*>(so + n8) : nullptr;
+  double* s_conf = (d_confidence || records) ? reinterpret_cast<double*>(so + n8) : nullptr;
   double* s_mp = n_mp ? reinterpret_cast<double*>(so + 2 * n8) : nullptr;
-  uint8_t* s_dec = d_decision ? reinterpret_cast<uint8_t*>(so + (2 + (size_t)n_mp) * n8) : nullptr;
-  uint8_t* s_risk = d_risk ? reinterpret_cast<uint8_t*>(so + (2 + (size_t)n_mp) * n8 + a8) : nullptr;
+  uint8_t* s_dec = (d_decision || records) ? reinterpret_cast<uint8_t*>(so + (2 + (size_t)n_mp) * n8) : nullptr;
+  uint8_t* s_risk = (d_risk || records) ? reinterpret_cast<uint8_t*>(so + (2 + (size_t)n_mp) * n8 + a8) : nullptr;
+  auto* s_res = records ? reinterpret_cast<fd::ResultRecord*>(so + (2 + (size_t)n_mp) * n8 + 2 * a8) : nullptr;
   if (e.pipe_copy_live[s]) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_copy_ev[s], 0));
   ++e.pipe_iter;
   {  // the scoring launches go on Sc: score_matrix launches on e.stream
@@ -1085,19 +1091,56 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
       ~Swap() { e.stream = saved; }
     } swap{e, e.stream};
     e.stream = Sc;
-    score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, s_mp, s_fp, s_conf, s_dec, s_risk,
-                 seq, e.state.S);
+    const auto* rec = static_cast<const fd::RouteRecord*>(records);
+    if (!score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, s_mp, s_fp, s_conf, s_dec,
+                      s_risk, seq, e.state.S, rec, s_res) &&
+        records)
+      fd::launch_result_pack(e, s_fp, s_conf, s_dec, s_risk, rec, n, s_res);
   }
   FD_HIP(hipEventRecord(e.pipe_done_ev[s], Sc));
   e.pipe_done_live[s] = true;
   FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[s], 0));
   hipLaunchKernelGGL(pipe_out_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e.stream, s_fp, s_conf,
-                     s_dec, s_risk, s_mp, n_mp, n, d_fraud_prob, d_confidence, d_decision, d_risk, d_model_probs,
-                     reinterpret_cast<const float4*>(vec), reinterpret_cast<float4*>(d_vectors));
+                     s_dec, s_risk, s_mp, n_mp, n, records ? nullptr : d_fraud_prob, d_confidence, d_decision, d_risk,
+                     d_model_probs, reinterpret_cast<const float4*>(vec), reinterpret_cast<float4*>(d_vectors),
+                     reinterpret_cast<const uint64_t*>(s_res), static_cast<uint64_t*>(d_results));
   FD_HIP(hipGetLastError());
   FD_HIP(hipEventRecord(e.pipe_copy_ev[s], e.stream));
   e.pipe_copy_live[s] = true;
   e.pipe_copy_vec[s] = d_vectors != nullptr;
+}
+
+int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                             const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
+                             int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
+                             double* d_confidence, uint8_t* d_decision, uint8_t* d_risk, void* input_ready) {
+  FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
+  Engine& e = E_quiet(eng);
+  FD_REQUIRE(params && txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  if (n == 0) return FD_OK;
+  FD_REQUIRE(d_fraud_prob != nullptr, FD_ERR_INVALID_ARG, "null fraud_prob output");
+  FD_REQUIRE(params->n_models >= 1 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "bad n_models");
+  pipe_step(e, params, slots, ext_probs, present, txns, nullptr, n, d_vectors, d_model_probs, d_fraud_prob,
+            d_confidence, d_decision, d_risk, nullptr, input_ready);
+  FD_API_END
+}
+
+int fd_score_records_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
+                               const uint8_t* present, const void* d_records, int64_t n, void* d_results,
+                               void* input_ready) {
+  FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
+  Engine& e = E_quiet(eng);
+  FD_REQUIRE(params && slots && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
+  FD_REQUIRE(params->n_models >= 1 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "bad n_models");
+  for (int m = 0; m < params->n_models; ++m)
+    FD_REQUIRE(slots[m] >= 0 || (present && !present[m]), FD_ERR_INVALID_ARG,
+               "routed scoring needs every present model in a forest slot or FD_SLOT_LSTM");
+  if (n == 0) return FD_OK;
+  FD_REQUIRE(d_records != nullptr && d_results != nullptr, FD_ERR_INVALID_ARG, "null records / results");
+  pipe_step(e, params, slots, nullptr, present, nullptr, d_records, n, nullptr, nullptr, nullptr, nullptr, nullptr,
+            nullptr, d_results, input_ready);
   FD_API_END
 }
 
@@ -1535,6 +1578,17 @@ int fd_route_partition_ex_device(fd_engine* eng, const fd_txn_batch* txns, const
   Engine& e = E(eng);
   FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
   fd::launch_route_partition(e, *txns, extra, n, n_shards, d_records, d_counts);
+  FD_API_END
+}
+
+int fd_route_partition_stream(fd_engine* eng, const fd_txn_batch* txns, const fd_window_inputs* extra, int64_t n,
+                              int32_t n_shards, void* d_records, int64_t* d_counts, void* stream) {
+  FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
+  Engine& e = E_quiet(eng);  // touches no card state: the pipelined stream stays undisturbed
+  FD_REQUIRE(txns, FD_ERR_INVALID_ARG, "null txns");
+  fd::launch_route_partition(e, *txns, extra, n, n_shards, d_records, d_counts, static_cast<hipStream_t>(stream),
+                             &e.route_blk_stream);
   FD_API_END
 }
 

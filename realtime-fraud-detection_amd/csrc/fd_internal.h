@@ -335,6 +335,7 @@ struct Engine {
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
   DeviceBuffer route_blk, route_out, route_err;  // card-hash routing scratch (route.hip)
+  DeviceBuffer route_blk_stream;                 // fd_route_partition_stream's block counts (its own stream)
   EnsemblePlan ens;                              // fused XGBoost + IsolationForest + blend (ensemble.hip)
   EnsemblePlan ens1[kMaxSlots];                  // the same kernel over one forest (forest predict), per slot
   bool route_err_live = false;
@@ -415,7 +416,9 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
                      float* d_seq = nullptr, double* d_vel5 = nullptr, hipStream_t stream = nullptr,
                      bool lean = false, int set = 0, hipEvent_t before_buckets = nullptr);
 // the same over received 48-B route records (route.hip), no unpack pass; also returns nothing else
-void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq);
+void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq,
+                             hipStream_t stream = nullptr, bool lean = false, int set = 0,
+                             hipEvent_t before_buckets = nullptr);
 void load_users_ext(Engine& e, const fd_users_ext& u);
 void load_merchants_ext(Engine& e, const fd_merchants_ext& m);
 void load_vocab(Engine& e, const uint8_t* pay_high_risk, const uint8_t* type_refund);
@@ -424,8 +427,10 @@ void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context
 void features_check(Engine& e);
 // route.hip
 unsigned shard_of_host(unsigned long long key, unsigned G);
+// stream / scratch: the launch stream and block-count scratch (default: the engine stream and route_blk)
 void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_inputs* extra, int64_t n, int G,
-                            void* d_records, int64_t* d_counts);
+                            void* d_records, int64_t* d_counts, hipStream_t stream = nullptr,
+                            DeviceBuffer* scratch = nullptr);
 void launch_route_unpack(Engine& e, const void* d_records, const void* d_results, int64_t n, const fd_txn_batch& out,
                          uint8_t* pm, uint8_t* fraud, double* score);
 void launch_result_pack(Engine& e, const double* fp, const double* conf, const uint8_t* dec, const uint8_t* risk,

@@ -1744,7 +1744,8 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
   launch_grouped(e, src, n, d_vec, d_raw, d_seq, d_vel5, stream, lean, set, before_buckets);
 }
 
-void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq) {
+void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq,
+                             hipStream_t stream, bool lean, int set, hipEvent_t before_buckets) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
   FD_REQUIRE(d_vec != nullptr && (n == 0 || d_records != nullptr), FD_ERR_INVALID_ARG, "null records / output");
@@ -1753,7 +1754,7 @@ void launch_features_records(Engine& e, const void* d_records, int64_t n, float*
   if (n == 0) return;
   TxnSrc src{};
   src.rec = static_cast<const RouteRecord*>(d_records);
-  launch_grouped(e, src, n, d_vec, nullptr, d_seq, nullptr);
+  launch_grouped(e, src, n, d_vec, nullptr, d_seq, nullptr, stream, lean, set, before_buckets);
 }
 
 void features_check(Engine& e) { check_err(e); }

@@ -203,12 +203,14 @@ unsigned shard_of_host(unsigned long long key, unsigned G) {
 }
 
 void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_inputs* extra, int64_t n, int G,
-                            void* d_records, int64_t* d_counts) {
+                            void* d_records, int64_t* d_counts, hipStream_t stream, DeviceBuffer* scratch) {
+  const hipStream_t st = stream ? stream : st;
+  DeviceBuffer& blk = scratch ? *scratch : blk;
   FD_REQUIRE(G >= 1 && G <= FD_MAX_SHARDS, FD_ERR_INVALID_ARG, "n_shards must be in [1, 64]");
   FD_REQUIRE(n >= 0 && n < (1ll << 31), FD_ERR_INVALID_ARG, "batch size out of range");
   FD_REQUIRE(d_counts != nullptr, FD_ERR_INVALID_ARG, "null counts");
   if (n == 0) {
-    FD_HIP(hipMemsetAsync(d_counts, 0, (size_t)G * sizeof(int64_t), e.stream));
+    FD_HIP(hipMemsetAsync(d_counts, 0, (size_t)G * sizeof(int64_t), st));
     return;
   }
   FD_REQUIRE(d_records != nullptr, FD_ERR_INVALID_ARG, "null records");
@@ -216,24 +218,24 @@ void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_in
                  t.weekend,
              FD_ERR_INVALID_ARG, "incomplete transaction batch");
   const int nblk = (int)((n + kRouteBlock - 1) / kRouteBlock);
-  e.route_blk.ensure((size_t)G * nblk * sizeof(int));
+  blk.ensure((size_t)G * nblk * sizeof(int));
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_ROUTE) : nullptr;
-  if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
+  if (ev) FD_HIP(hipEventRecord(ev->a, st));
   const auto* key = reinterpret_cast<const unsigned long long*>(t.card_key);
-  hipLaunchKernelGGL(route_count_kernel, dim3(nblk), dim3(kRouteBlock), 0, e.stream, key, n, (unsigned)G, nblk,
-                     e.route_blk.as<int>());
+  hipLaunchKernelGGL(route_count_kernel, dim3(nblk), dim3(kRouteBlock), 0, st, key, n, (unsigned)G, nblk,
+                     blk.as<int>());
   FD_HIP(hipGetLastError());
-  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, e.stream, e.route_blk.as<int>(),
+  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, st, blk.as<int>(),
                      (int64_t)G * nblk, (unsigned)G, nblk, reinterpret_cast<long long*>(d_counts));
   FD_HIP(hipGetLastError());
-  hipLaunchKernelGGL(route_scatter_kernel, dim3(nblk), dim3(kRouteBlock), 0, e.stream, key,
+  hipLaunchKernelGGL(route_scatter_kernel, dim3(nblk), dim3(kRouteBlock), 0, st, key,
                      reinterpret_cast<const long long*>(t.ts_ms), reinterpret_cast<const long long*>(t.amount_cents),
                      reinterpret_cast<const int*>(t.merchant), reinterpret_cast<const unsigned long long*>(t.device_fp),
                      t.ip_class, t.hour, t.weekend, extra ? extra->payment_method : nullptr,
-                     extra ? extra->is_fraud : nullptr, n, (unsigned)G, nblk, e.route_blk.as<const int>(),
+                     extra ? extra->is_fraud : nullptr, n, (unsigned)G, nblk, blk.as<const int>(),
                      static_cast<RouteRecord*>(d_records));
   FD_HIP(hipGetLastError());
-  if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
+  if (ev) FD_HIP(hipEventRecord(ev->b, st));
 }
 
 void launch_route_unpack(Engine& e, const void* d_records, const void* d_results, int64_t n, const fd_txn_batch& out,

@@ -268,6 +268,9 @@ SIGNATURES = {
     "fd_windows_observe": (C.c_int, [_vp, _i64]),
     "fd_merchant_windows_merge": (C.c_int, [_vp, _i64, _vp, C.POINTER(_i64)]),
     "fd_score_records_device": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, _vp, _vp, _i64, _vp]),
+    "fd_score_records_pipelined": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, _vp, _vp, _i64, _vp, _vp]),
+    "fd_route_partition_stream": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_window_inputs), _i64, _i32,
+                                            _vp, _vp, _vp]),
     "fd_route_scatter_results_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "fd_windows_init": (C.c_int, [_vp, C.POINTER(fd_window_params)]),
     "fd_windows_step_device": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_window_inputs), _i64, C.c_int,

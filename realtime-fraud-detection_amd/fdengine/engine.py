@@ -449,6 +449,16 @@ class FraudEngine:
         N.call("fd_route_partition_ex_device", self._h, C.byref(b), C.byref(wi), int(n), int(n_shards),
                C.c_void_p(records_ptr) if records_ptr else None, C.c_void_p(counts_ptr))
 
+    def route_partition_stream(self, txn_ptrs: dict, extra_ptrs: Optional[dict], n: int, n_shards: int,
+                               records_ptr: int, counts_ptr: int, stream_ptr: int) -> None:
+        """route_partition_ex_device launched on `stream_ptr` (a hipStream_t), beside the pipelined stream."""
+        b = N.fd_txn_batch(*[int(txn_ptrs[f]) for f in N.TXN_FIELDS])
+        wi = N.fd_window_inputs(*[int(extra_ptrs[f]) if extra_ptrs and extra_ptrs.get(f) else None
+                                  for f in ("payment_method", "is_fraud")], None)
+        N.call("fd_route_partition_stream", self._h, C.byref(b), C.byref(wi), int(n), int(n_shards),
+               C.c_void_p(records_ptr) if records_ptr else None, C.c_void_p(counts_ptr),
+               C.c_void_p(int(stream_ptr)) if stream_ptr else None)
+
     def route_unpack_device(self, records_ptr: int, results_ptr: int, n: int, out_ptrs: dict, pm_ptr: int = 0,
                             fraud_ptr: int = 0, score_ptr: int = 0) -> None:
         """Owner side: received records (+ their result records) back to device columns (out_ptrs: any of
@@ -468,6 +478,17 @@ class FraudEngine:
         N.call("fd_score_records_device", self._h, C.byref(params), _ptr(sl), _ptr(pres),
                C.c_void_p(records_ptr) if records_ptr else None, int(n),
                C.c_void_p(results_ptr) if results_ptr else None)
+
+    def score_records_pipelined(self, params: N.fd_blend_params, slots: Sequence[int], records_ptr: int, n: int,
+                                results_ptr: int, input_ready: int = 0, present: Optional[Sequence[int]] = None) -> None:
+        """Streaming form of score_records_device (fd_score_records_pipelined): the owner's features of this batch
+        overlap the previous batch's forests; input_ready: a hipEvent_t recorded once the records had landed."""
+        M = params.n_models
+        sl = np.array(list(slots) + [-1] * (N.FD_MAX_MODELS - len(slots)), np.int32)
+        pres = np.array([1] * M if present is None else list(present), np.uint8)
+        N.call("fd_score_records_pipelined", self._h, C.byref(params), _ptr(sl), _ptr(pres),
+               C.c_void_p(records_ptr) if records_ptr else None, int(n),
+               C.c_void_p(results_ptr) if results_ptr else None, C.c_void_p(input_ready) if input_ready else None)
 
     def route_scatter_results_device(self, results_ptr: int, n: int, fp_ptr: int, conf_ptr: int = 0,
                                      dec_ptr: int = 0, risk_ptr: int = 0) -> None:

@@ -7,7 +7,7 @@ shard_of(card_key, G) == r (fdengine.shard_of / fd_shard_of_host) and keeps thei
 HBM. Models (≈2 MB) and the merchant table are replicated.
 
 One micro-batch step, per rank (one process per GPU, torch.distributed: RCCL over xGMI on the GPU,
-gloo in the CPU tests):
+gloo in the CPU tests), in the serial form (`step(..., windows / sink)`, or a backend without the streaming hooks):
   1. fd_route_partition_device: group the ingested batch by owner (stable), 48-B records + counts;
   2. all_to_all of the per-owner counts (G int64), then both count vectors to the host (one sync:
      RCCL all-to-all needs host split sizes);
@@ -16,7 +16,19 @@ gloo in the CPU tests):
   5. all_to_all of the 24-B result records back (splits reversed);
   6. fd_route_scatter_results_device: results in the ingest batch's original order.
 Records from one source keep their arrival order and all_to_all concatenates sources in rank order,
-so every card sees its transactions in (step, ingest rank, ingest index) order. With one shard (world 1)
+so every card sees its transactions in (step, ingest rank, ingest index) order.
+
+Streaming form (the scoring step of a backend with `start_partition`, i.e. EngineShardBackend): the same
+exchanges, but nothing drains the device queue.
+  * the partition and the count all-to-all run on a forward stream beside the scoring; the counts land in
+    pinned host memory behind an event. Given `prefetch` (the next micro-batch), step s launches batch s+1's
+    partition and count exchange, so step s+1 finds its split sizes already on the host (the one host wait is
+    that event, which completed while the GPUs were still scoring);
+  * the records all-to-all runs on the forward stream; the owner scores through fd_score_records_pipelined
+    (its features wait for an event recorded after the records landed and overlap the previous batch's
+    forests); the result all-to-all goes on a second communicator (`group_back`), queued behind the scoring
+    on the engine stream, so a batch's returning results never hold up the next batch's records;
+  * every rank makes the same calls in the same order (prefetch in the same steps on all ranks). With one shard (world 1)
 the step is the fused hot path on the ingest batch itself (fd_score_batch_device): nothing to route.
 
 The exchange logic is backend-agnostic: `EngineShardBackend` drives libfdengine.so (the product path);
@@ -66,6 +78,57 @@ class EngineShardBackend:
         # The engine's kernels and the collectives must be ordered on ONE stream: bind the engine to the
         # stream torch (and so RCCL's all_to_all and .cpu()) uses on this device.
         eng.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ---- streaming sharded step (ShardedScorer._step_streaming)
+    def _fwd(self):
+        if getattr(self, "_x_fwd", None) is None:
+            self._x_fwd = self.torch.cuda.Stream(self.device)
+        return self._x_fwd
+
+    def fwd_ctx(self):
+        """the forward stream: partitions, count and record exchanges (torch's NCCL calls follow the current stream)"""
+        return self.torch.cuda.stream(self._fwd())
+
+    def start_partition(self, txns: dict, n: int, G: int, input_ready=None):
+        """fd_route_partition_stream on the forward stream (call inside fwd_ctx); the input tensors are marked in
+        use there, so freeing them on another stream cannot recycle them under the partition"""
+        t, x = self.torch, self._fwd()
+        if input_ready is not None:
+            x.wait_event(input_ready)
+        for v in txns.values():
+            v.record_stream(x)
+        rec = t.empty((n, REC), dtype=t.uint8, device=self.device)
+        counts = t.empty(G, dtype=t.int64, device=self.device)
+        self.eng.route_partition_stream({f: txns[f].data_ptr() for f in N.TXN_FIELDS}, None, n, G,
+                                        rec.data_ptr() if n else 0, counts.data_ptr(), x.cuda_stream)
+        return rec, counts
+
+    def counts_to_host(self, counts, recv):
+        """both count vectors to pinned host memory behind an event on the forward stream (inside fwd_ctx)"""
+        t = self.torch
+        G = counts.numel()
+        h = t.empty(2 * G, dtype=t.int64, pin_memory=True)
+        h[:G].copy_(counts, non_blocking=True)
+        h[G:].copy_(recv, non_blocking=True)
+        ev = t.cuda.Event()
+        ev.record(self._fwd())
+        return _HostCounts(h, ev, G)
+
+    def forward_ready(self):
+        """an event on the forward stream after the records landed (inside fwd_ctx)"""
+        ev = self.torch.cuda.Event()
+        ev.record(self._fwd())
+        return ev
+
+    def score_records_async(self, inbox, m: int, ready):
+        """fd_score_records_pipelined: result records written on the engine stream (torch's current stream)"""
+        t = self.torch
+        res = t.empty((m, RES), dtype=t.uint8, device=self.device)
+        if m:
+            inbox.record_stream(t.cuda.current_stream(self.device))  # reused only after the engine stream passed
+            self.eng.score_records_pipelined(self.params, self.slots, inbox.data_ptr(), m, res.data_ptr(),
+                                             ready.cuda_event, self.present)
+        return res
 
     def partition(self, txns: dict, n: int, G: int, extras: Optional[dict] = None):
         t = self.torch
@@ -176,13 +239,38 @@ class EngineShardBackend:
         return fp, conf, dec, risk
 
 
-class ShardedScorer:
-    """One rank's side of the sharded hot path. `world == 1` runs the same kernels with no collective."""
+class _HostCounts:
+    """split sizes on their way to the host (pinned buffer + event)"""
 
-    def __init__(self, backend, rank: int, world: int, group=None):
+    def __init__(self, h, ev, G):
+        self.h, self.ev, self.G = h, ev, G
+
+    def wait(self):
+        if self.ev is not None:
+            self.ev.synchronize()
+        v = [int(c) for c in self.h.tolist()]
+        return v[:self.G], v[self.G:]
+
+
+class ShardedScorer:
+    """One rank's side of the sharded hot path. `world == 1` runs the same kernels with no collective.
+    streaming (default True): use the backend's streaming hooks when it has them (module docstring); the result
+    all-to-all then runs on a second process group over the same ranks, created here (collectively)."""
+
+    def __init__(self, backend, rank: int, world: int, group=None, streaming: bool = True, force_route: bool = False):
+        """force_route: route even with one shard (partition, exchanges over a 1-rank process group, scatter) — the
+        N > 1 step's own work measured / tested on one GPU (tools/route_overhead.py)"""
         self.be, self.rank, self.world, self.group = backend, int(rank), int(world), group
         self.last_counts = None  # (send, recv) split sizes of the last step, for diagnostics
         self.last_windows = None  # (user windows, merged merchant windows) fired by the last windows step
+        self.route = self.world > 1 or bool(force_route)
+        self.streaming = bool(streaming) and self.route and hasattr(backend, "start_partition")
+        self.group_back = None
+        self._pending = None
+        if self.streaming:
+            import torch.distributed as dist
+            ranks = list(range(self.world)) if group is None else dist.get_process_group_ranks(group)
+            self.group_back = dist.new_group(ranks=ranks)
 
     def _staged(self) -> bool:
         """gloo moves host memory only: device tensors are staged through the host (several ranks sharing one
@@ -190,14 +278,15 @@ class ShardedScorer:
         import torch.distributed as dist
         return dist.get_backend(self.group) == "gloo"
 
-    def _a2a(self, out, inp, out_splits=None, in_splits=None):
+    def _a2a(self, out, inp, out_splits=None, in_splits=None, group="fwd"):
         import torch.distributed as dist
+        g = self.group_back if group == "back" else self.group
         if self._staged() and (out.is_cuda or inp.is_cuda):
             o = out.cpu()
-            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=g)
             out.copy_(o)
             return
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=g)
 
     def _allreduce_max(self, t):
         import torch.distributed as dist
@@ -206,7 +295,7 @@ class ShardedScorer:
         return int(g.cpu()[0])
 
     def step(self, txns: dict, n: int, extras: Optional[dict] = None, windows: bool = False, sink: bool = False,
-             flush: bool = False, input_ready=None, vectors=None, model_probs=None):
+             flush: bool = False, input_ready=None, vectors=None, model_probs=None, prefetch=None):
         """txns: field -> tensor (n rows) on the backend's device, in arrival order.
         input_ready: optional torch.cuda.Event recorded once `txns` were complete (a pipelined backend's features
         wait for it instead of assuming resident inputs).
@@ -216,11 +305,13 @@ class ShardedScorer:
         transactions (module docstring); the fired windows are left in self.last_windows =
         (this shard's user windows, the node's merged merchant windows); flush: end of input.
         vectors / model_probs (world 1, backends with score_batch): optional device tensors that also receive the
-        batch's scoring vectors (n x 64) / per-model probabilities (n_models x n)."""
+        batch's scoring vectors (n x 64) / per-model probabilities (n_models x n).
+        prefetch (world > 1, streaming): (next txns, next n[, next input_ready]) — the next micro-batch, whose
+        partition and count exchange this step launches ahead; every rank must pass it in the same steps."""
         import torch
         G = self.world
         aux = windows or sink
-        if G == 1:  # one shard owns every card: no partition, no exchange
+        if not self.route:  # one shard owns every card: no partition, no exchange
             self.last_counts = ([n], [n])
             if hasattr(self.be, "score_batch"):
                 kw = {k: v for k, v in (("input_ready", input_ready), ("vectors", vectors),
@@ -237,6 +328,8 @@ class ShardedScorer:
             if aux:
                 self._aggregates(self.be.unpack(rec, res, n), n, None, windows, sink, flush)
             return self.be.scatter_results(res, n)
+        if self.streaming and not aux:
+            return self._step_streaming(txns, n, input_ready, prefetch)
         rec, counts = self.be.partition(txns, n, G, extras) if aux else self.be.partition(txns, n, G)
         recv_counts = torch.empty_like(counts)
         self._a2a(recv_counts, counts)
@@ -254,6 +347,46 @@ class ShardedScorer:
                                                                         device=rec.device)
             self._aggregates(self.be.unpack(inbox, res, m), m, tmax, windows, sink, flush)
         return self.be.scatter_results(back, n, sentinel=True)
+
+    # ---------------------------------------------------------------- streaming exchange (module docstring)
+    @staticmethod
+    def _batch_key(txns, n):
+        k = txns["card_key"]
+        return (k.data_ptr() if hasattr(k, "data_ptr") else id(k), int(n))
+
+    def _launch_counts(self, txns, n, input_ready):
+        import torch
+        be = self.be
+        with be.fwd_ctx():
+            rec, counts = be.start_partition(txns, n, self.world, input_ready)
+            recv = torch.empty_like(counts)
+            self._a2a(recv, counts)
+            host = be.counts_to_host(counts, recv)
+        return {"key": self._batch_key(txns, n), "rec": rec, "host": host}
+
+    def _step_streaming(self, txns, n, input_ready, prefetch):
+        import torch
+        be = self.be
+        p = self._pending
+        self._pending = None
+        if p is None or p["key"] != self._batch_key(txns, n):
+            # no prefetch, or another batch came instead of the prefetched one: its partition and count exchange
+            # (issued on every rank alike) are dropped, this batch's are launched now
+            p = self._launch_counts(txns, n, input_ready)
+        send, recv = p["host"].wait()  # the step's one host wait: split sizes exchanged ahead
+        self.last_counts = (send, recv)
+        m = sum(recv)
+        with be.fwd_ctx():
+            inbox = torch.empty((m, REC), dtype=torch.uint8, device=p["rec"].device)
+            self._a2a(inbox, p["rec"], recv, send)
+            ready = be.forward_ready()
+        res = be.score_records_async(inbox, m, ready)
+        if prefetch is not None:
+            nt, nn = prefetch[0], prefetch[1]
+            self._pending = self._launch_counts(nt, nn, prefetch[2] if len(prefetch) > 2 else None)
+        back = torch.empty((n, RES), dtype=torch.uint8, device=res.device)
+        self._a2a(back, res, send, recv, group="back")
+        return be.scatter_results(back, n, sentinel=True)
 
     def _aggregates(self, cols: dict, m: int, tmax, windows: bool, sink: bool, flush: bool):
         import torch.distributed as dist

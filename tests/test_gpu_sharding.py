@@ -149,3 +149,66 @@ def test_emulated_shards_match_unsharded(G):
     finally:
         for e in engines + [ref]:
             e.close()
+
+
+@pytest.mark.timeout(300)
+def test_streaming_routed_step_single_rank_matches_direct():
+    """The streaming sharded step's own GPU work on one GPU (ShardedScorer(force_route=True) over a 1-rank RCCL
+    process group): fd_route_partition_stream of the next batch one step ahead on the forward stream, RCCL
+    all-to-alls of counts / records (forward group) and results (second group), fd_score_records_pipelined, the
+    scatter — each step's device outputs dropped at once — bit-identical to the direct pipelined step
+    (fd_score_batch_pipelined) on a twin engine."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from fdengine import iforest_from_sklearn, xgboost_from_json_doc
+    from fdengine.sharding import EngineShardBackend, ShardedScorer
+    pop = synth.population(30000, 500, seed=61)
+    B, steps = 50000, 6
+    tx = synth.txn_stream(pop, B * steps, seed=62, rate_per_s=20.0)
+    X = synth.feature_matrix(4000, 64, seed=63)
+    xgb = xgboost_from_json_doc(synth.xgboost_doc(120, 8, 64, X, seed=64))
+    ifm = iforest_from_sklearn(synth.isolation_forest(X.astype(np.float64), n_estimators=40))
+    params = FraudEngine.blend_params([0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
+    U, M = pop["users"], pop["merchants"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    engines = []
+    try:
+        dev = _dev(tx)
+        parts = [{f: t[i * B:(i + 1) * B] for f, t in dev.items()} for i in range(steps)]
+        torch.cuda.synchronize()
+        res = []
+        for routed in (False, True):
+            e = FraudEngine(0)
+            engines.append(e)
+            e.state_init(1 << 17, 1, 16)
+            e.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+            e.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+            e.load_forest(0, xgb)
+            e.load_forest(1, ifm)
+            sc = ShardedScorer(EngineShardBackend(e, params, [0, 1], pipelined=True), 0, 1, force_route=routed)
+            assert sc.streaming == routed
+            outs = []
+            for i in range(steps):
+                pre = (parts[i + 1], B) if i + 1 < steps and i != 3 else None  # one step without prefetch
+                out = sc.step(parts[i], B, prefetch=pre)
+                host = [torch.empty(o.shape, dtype=o.dtype, pin_memory=True) for o in out]
+                for h, o in zip(host, out):
+                    h.copy_(o, non_blocking=True)
+                outs.append(host)
+            torch.cuda.synchronize()
+            res.append(outs)
+        for a, b in zip(*res):
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x.numpy(), y.numpy())
+    finally:
+        for e in engines:
+            e.close()
+        dist.destroy_process_group()

@@ -166,3 +166,80 @@ def test_two_ranks_on_one_gpu_match_unsharded_engine(tmp_path):
         assert _rows(got[r]["merchants"], MF, (1, 0)) == _rows(merchants, MF, (1, 0))
         for k in ("hourly", "daily", "merchant"):
             np.testing.assert_array_equal(got[r]["sink"][k], q[k])
+
+
+def _stream_worker(rank, port, outdir):
+    import torch
+    import torch.distributed as dist
+
+    from fdengine import FraudEngine
+    from fdengine.sharding import EngineShardBackend, ShardedScorer, owned_mask
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    eng = None
+    try:
+        torch.cuda.set_device(0)
+        pop, streams, pms, xgb, ifm = _setup()
+        eng = _engine(pop, owned_mask(pop["users"]["key"], rank, WORLD), xgb, ifm)
+        params = FraudEngine.blend_params([0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
+        sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), rank, WORLD)
+        assert sc.streaming
+        parts = [_dev_batch(streams[rank], pms[rank], slice(s * B, (s + 1) * B))[0] for s in range(STEPS)]
+        outs = []
+        for s in range(STEPS):
+            pre = (parts[s + 1], B) if s + 1 < STEPS else None
+            out = sc.step(parts[s], B, prefetch=pre)
+            host = [torch.empty(o.shape, dtype=o.dtype, pin_memory=True) for o in out]
+            for h, o in zip(host, out):
+                h.copy_(o, non_blocking=True)
+            outs.append(host)  # the device outputs are dropped at once (allocator reuse under the streams)
+        torch.cuda.synchronize()
+        scores = np.concatenate([np.stack([h[0].numpy(), h[1].numpy(), h[2].numpy().astype(np.float64),
+                                           h[3].numpy().astype(np.float64)]) for h in outs], axis=1)
+        with open(os.path.join(outdir, f"srank{rank}.pkl"), "wb") as f:
+            pickle.dump({"scores": scores, "counts": sc.last_counts}, f)
+    finally:
+        if eng is not None:
+            eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_ranks_streaming_step_matches_oracle(tmp_path):
+    """The streaming sharded step (partition + count exchange of the next batch launched one step ahead on a
+    forward stream, records landing behind an event, fd_score_records_pipelined, results back on a second process
+    group) with two real ranks on the one GPU, against the CPU oracle chain over the global arrival order
+    (step-major, then ingest rank, then index): fraud probability, confidence, decision, risk bit-identical."""
+    import torch.multiprocessing as mp
+
+    import oracle
+    from oracle.features_c import OracleFeatureState
+    mp.spawn(_stream_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    got = [pickle.load(open(tmp_path / f"srank{r}.pkl", "rb")) for r in range(WORLD)]
+    assert all(min(g["counts"][1]) > 0 for g in got)
+    pop, streams, _, xgb, ifm = _setup()
+    U, M = pop["users"], pop["merchants"]
+    st = OracleFeatureState(4 * N_USERS + 4096, 1, 16)
+    st.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+    st.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+    exp = [[] for _ in range(WORLD)]
+    for s in range(STEPS):
+        for r in range(WORLD):
+            part = {k: v[s * B:(s + 1) * B] for k, v in streams[r].items()}
+            _, V = st.run(part, want_raw=False)
+            px, _, _ = oracle.xgb_predict(xgb, V)
+            pi, _, _ = oracle.iforest_predict(ifm, V)
+            fp, conf, dec, risk = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]),
+                                                        [0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
+            exp[r].append(np.stack([fp, conf, dec.astype(np.float64), risk.astype(np.float64)]))
+    for r in range(WORLD):
+        g, e = got[r]["scores"], np.concatenate(exp[r], axis=1)
+        # probabilities within the north-star 1e-5 (the f32 XGBoost sigmoid may differ by an ulp from the oracle's);
+        # decision / risk exact except where the oracle's value sits within 1e-6 of a threshold
+        assert np.abs(g[0] - e[0]).max() <= 1e-5 and np.abs(g[1] - e[1]).max() <= 1e-5
+        near = np.zeros(g.shape[1], bool)
+        for thr in (0.3, 0.6, 0.8, 0.95):
+            near |= np.abs(e[0] - thr) < 1e-6
+        near |= np.abs(e[1] - 0.7) < 1e-6
+        assert ((g[2] == e[2]) | near).all() and ((g[3] == e[3]) | near).all()
+        assert (g[2] == e[2]).mean() > 0.999

@@ -115,6 +115,29 @@ class OracleShardBackend:
         return tuple(self.torch.from_numpy(a) for a in out)
 
 
+class StreamingOracleBackend(OracleShardBackend):
+    """+ the streaming hooks EngineShardBackend has (forward stream, counts to the host behind an event, records
+    scored asynchronously): on the CPU they run inline, so the test checks the protocol — prefetched partitions and
+    count exchanges, the records / results exchanges on two process groups — not the streams."""
+
+    def fwd_ctx(self):
+        import contextlib
+        return contextlib.nullcontext()
+
+    def start_partition(self, txns, n, G, input_ready=None):
+        return self.partition(txns, n, G)
+
+    def counts_to_host(self, counts, recv):
+        from fdengine.sharding import _HostCounts
+        return _HostCounts(self.torch.cat([counts, recv]), None, counts.numel())
+
+    def forward_ready(self):
+        return None
+
+    def score_records_async(self, inbox, m, ready):
+        return self.score_records(inbox, m)
+
+
 class AggShardBackend(OracleShardBackend):
     """+ the owner-side keyed aggregates: WindowOracle (windows_ref) and an exact-cents sink (ExactSink), with
     the merchant windows returned as exact-moment partials in the library's fd_merchant_window layout."""
@@ -214,7 +237,7 @@ class ExactSink:
         return out
 
 
-def _worker(rank, port, outdir):
+def _worker(rank, port, outdir, mode="serial"):
     import torch
     import torch.distributed as dist
     from fdengine.sharding import ShardedScorer
@@ -223,13 +246,18 @@ def _worker(rank, port, outdir):
     try:
         pop, streams = _streams()
         xgb, ifm = _models()
-        be = OracleShardBackend(rank, WORLD, pop, xgb, ifm)
+        be = (StreamingOracleBackend if mode != "serial" else OracleShardBackend)(rank, WORLD, pop, xgb, ifm)
         sc = ShardedScorer(be, rank, WORLD)
+        assert sc.streaming == (mode != "serial")
         tx = streams[rank]
         outs = []
+        parts = [{k: torch.from_numpy(np.ascontiguousarray(v[s * B:(s + 1) * B])) for k, v in tx.items()}
+                 for s in range(STEPS)]
         for s in range(STEPS):
-            part = {k: torch.from_numpy(np.ascontiguousarray(v[s * B:(s + 1) * B])) for k, v in tx.items()}
-            fp, conf, dec, risk = sc.step(part, B)
+            part = parts[s]
+            # "prefetch": every step but the last hands over the next batch (and step 2 does not, on every rank)
+            pre = (parts[s + 1], B) if mode == "prefetch" and s + 1 < STEPS and s != 2 else None
+            fp, conf, dec, risk = sc.step(part, B, prefetch=pre)
             outs.append(np.stack([fp.numpy(), conf.numpy(), dec.numpy().astype(np.float64),
                                   risk.numpy().astype(np.float64)]))
             send, recv = sc.last_counts
@@ -249,12 +277,15 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_world2_gloo_matches_unsharded_oracle(tmp_path):
+@pytest.mark.parametrize("mode", ["serial", "streaming", "prefetch"])
+def test_world2_gloo_matches_unsharded_oracle(tmp_path, mode):
+    """serial: the exchange with a host read of the split sizes; streaming / prefetch: the streaming step (records
+    and results on two process groups), prefetch also exchanging the next batch's counts one step ahead"""
     import torch.multiprocessing as mp
 
     import oracle
     from oracle.features_c import OracleFeatureState
-    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path), mode), nprocs=WORLD, join=True)
     got = [np.load(tmp_path / f"rank{r}.npy") for r in range(WORLD)]
     scored = [int(np.load(tmp_path / f"scored{r}.npy")[0]) for r in range(WORLD)]
     assert sum(scored) == WORLD * B * STEPS and min(scored) > 0  # both owners did work

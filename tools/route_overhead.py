@@ -1,77 +1,65 @@
 #!/usr/bin/env python3
-"""The sharded step's on-GPU work without the collectives, on one GPU: the direct serial step
-(fd_score_batch_device) vs the routed one (fd_route_partition_device -> fd_score_records_device ->
-fd_route_scatter_results_device, what every rank runs around its all-to-alls at N > 1), config-4 shapes.
-Prints ms per 64k step for each (steps synchronised per step, like the bench's latency loop, and back to back)."""
+"""The sharded step's own GPU work on one GPU: the direct pipelined step (ShardedScorer at world 1 ->
+fd_score_batch_pipelined, what N = 1 runs) against the streaming routed step every rank runs at N > 1
+(ShardedScorer(force_route=True) over a 1-rank RCCL process group: fd_route_partition_stream of the next batch one
+step ahead, the count / record all-to-alls on the forward stream, fd_score_records_pipelined, the result all-to-all
+on the second group, the scatter), config-4 shapes on a warm stream (CARDS env, default 10 M; 12 h of history).
+Prints ms per 64 k step back to back for each, and the routed / direct ratio."""
 import os
+import socket
 import sys
 import time
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parent.parent
 sys.path[:0] = [str(REPO), str(REPO / "realtime-fraud-detection_amd")]
-import numpy as np
 import torch
+import torch.distributed as dist
 
 import bench
 import fdengine
-from fdengine import _native as N
-from fdengine import synth
-from fdengine.sharding import EngineShardBackend
+from fdengine import synth, synth_gpu
+from fdengine.sharding import EngineShardBackend, ShardedScorer
 
-B, CARDS, STEPS = 65536, int(os.environ.get("CARDS", 10_000_000)), 60
+B, CARDS, STEPS = 65536, int(os.environ.get("CARDS", 10_000_000)), int(os.environ.get("STEPS", 200))
 dev = torch.device("cuda", 0)
-eng = fdengine.FraudEngine(0)
-eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+s = socket.socket()
+s.bind(("127.0.0.1", 0))
+port = s.getsockname()[1]
+s.close()
+dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
 xgb, ifm = bench.fit_models(0, 500, 8, 1, 16)
-eng.load_forest(0, xgb)
-eng.load_forest(1, ifm)
 params, _, _ = bench.product_blend(["xgboost_primary", "isolation_forest"])
 merch = synth.merchants_table(5000, seed=100)
-own = synth.owned_cards(CARDS, 0, 1, seed=42)
 cap = 1
 while cap < int(CARDS * 1.6) + 65536:
     cap *= 2
-eng.state_init(cap, 1, 16)
-eng.load_users(own["key"], own["avg_amount"], own["account_age_days"], own["device_fp"])
-eng.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
-tx = synth.txn_stream_cards(CARDS, merch, (2 * STEPS + 10) * B, seed=200, card_seed=42, rate_per_s=2000.0)
-d = {f: torch.from_numpy(np.ascontiguousarray(tx[f])).to(dev) for f in N.TXN_FIELDS}
-be = EngineShardBackend(eng, params, [0, 1])
-k = [0]
+result = {}
+for routed in (False, True):
+    eng = fdengine.FraudEngine(0)
+    eng.state_init(cap, 1, 16)
+    eng.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
+    sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), 0, 1, force_route=routed)
+    w = synth_gpu.warm_workload(eng, dev, CARDS, 0, 1, STEPS + 20, B, hours=12.0, keep_batches=0)
+    eng.load_forest(0, xgb)
+    eng.load_forest(1, ifm)
+    parts = [{f: t[i * B:(i + 1) * B] for f, t in w["resident"].items()} for i in range(STEPS + 20)]
 
+    def run(a, b):
+        for i in range(a, b):
+            pre = (parts[i + 1], B) if routed and i + 1 < b else None
+            sc.step(parts[i], B, prefetch=pre)
 
-def batch():
-    b = k[0]
-    k[0] += 1
-    return {f: t[b * B:(b + 1) * B] for f, t in d.items()}
-
-
-def direct():
-    return be.score_batch(batch(), B)
-
-
-def routed():
-    rec, _ = be.partition(batch(), B, 1)
-    res = be.score_records(rec, B)
-    return be.scatter_results(res, B, sentinel=True)
-
-
-for name, fn in (("direct", direct), ("routed", routed)):
-    for _ in range(3):
-        fn()
+    run(0, 20)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(STEPS // 2):
-        fn()
+    run(20, 20 + STEPS)
     torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    lat = []
-    for _ in range(STEPS // 2):
-        a = time.perf_counter()
-        fn()
-        torch.cuda.synchronize()
-        lat.append(time.perf_counter() - a)
-    print(f"{name}: {(t1 - t0) / (STEPS // 2) * 1e3:.4f} ms/step back to back, "
-          f"{np.median(lat) * 1e3:.4f} ms synchronised (median)", flush=True)
-eng.close()
+    ms = (time.perf_counter() - t0) / STEPS * 1e3
+    result["routed" if routed else "direct"] = ms
+    print(f"{'routed streaming' if routed else 'direct pipelined'}: {ms:.4f} ms/step back to back "
+          f"({B / ms / 1e3:.1f} M txn/s)", flush=True)
+    eng.close()
+    del w, parts
+print(f"routed / direct = {result['routed'] / result['direct']:.3f}", flush=True)
+dist.destroy_process_group()
