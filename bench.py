@@ -32,6 +32,10 @@ import tempfile
 import time
 from pathlib import Path
 
+# One hardware queue per stream: the sharded step keeps the engine stream, two pipeline streams, its forward stream
+# and RCCL's streams busy at once; with HIP's default of 4 queues per process some would share a queue and a
+# blocked RCCL kernel would stall a pipeline stream behind it (set before anything initialises HIP; <= 32).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "realtime-fraud-detection_amd"))

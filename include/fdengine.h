@@ -436,6 +436,24 @@ int fd_score_records_device(fd_engine* eng, const fd_blend_params* params, const
 int fd_score_records_pipelined(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
                                const uint8_t* present, const void* d_records, int64_t n, void* d_results,
                                void* input_ready);
+/* The sharded step as one call over the engine's own RCCL communicators (csrc/comm.hip): the host loads
+   RCCL once (the process's librccl.so, by path), rank 0 makes two unique ids (fd_comm_unique_id), the host
+   broadcasts them, every rank calls fd_comm_init (collective, blocking). fd_sharded_step then runs one
+   micro-batch: its split sizes (exchanged by the previous call when it prefetched this batch, else now: the
+   step's one host wait), the records to their owners (grouped ncclSend/ncclRecv with per-peer counts, on
+   the engine's forward stream), the owner's features + scoring (fd_score_records_pipelined's pipeline, the
+   features waiting for the records), the next batch's partition and count exchange (`next`, optional:
+   prefetch), the results back (second communicator, engine stream) and into arrival order in the caller's
+   outputs, written on the engine stream. Every rank makes the same calls in the same order (the same
+   prefetch pattern). split_sizes (optional): the 2 x world send / receive counts of this batch. */
+int fd_comm_unique_id(const char* rccl_path, uint8_t* id_out /* 128 bytes */);
+int fd_comm_init(fd_engine* eng, const char* rccl_path, int32_t rank, int32_t world, const uint8_t* id_fwd,
+                 const uint8_t* id_back);
+int fd_comm_destroy(fd_engine* eng);
+int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t* slots, const uint8_t* present,
+                    const fd_txn_batch* txns, int64_t n, void* input_ready, const fd_txn_batch* next,
+                    int64_t next_n, void* next_ready, double* d_fraud_prob, double* d_confidence,
+                    uint8_t* d_decision, uint8_t* d_risk, int64_t* split_sizes);
 /* out[seq] = result for each of the n returned records; conf/decision/risk may be NULL.
    fd_engine_sync reports a record whose seq is outside [0, n). */
 int fd_route_scatter_results_device(fd_engine* eng, const void* d_results, int64_t n, double* d_fraud_prob,

@@ -296,6 +296,10 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipStreamDestroy(e.aux2_stream);
     (void)hipEventDestroy(e.join2_ev);
   }
+  try {
+    fd::comm_destroy(e);
+  } catch (...) {
+  }
   for (hipStream_t st : e.pipe_stream)
     if (st) {
       (void)hipStreamSynchronize(st);
@@ -1141,6 +1145,102 @@ int fd_score_records_pipelined(fd_engine* eng, const fd_blend_params* params, co
   FD_REQUIRE(d_records != nullptr && d_results != nullptr, FD_ERR_INVALID_ARG, "null records / results");
   pipe_step(e, params, slots, nullptr, present, nullptr, d_records, n, nullptr, nullptr, nullptr, nullptr, nullptr,
             nullptr, d_results, input_ready);
+  FD_API_END
+}
+
+// ---------------------------------------------------------------- card-hash sharded step over RCCL (comm.hip)
+int fd_comm_unique_id(const char* rccl_path, uint8_t* id_out) {
+  FD_API_BEGIN
+  FD_REQUIRE(id_out, FD_ERR_INVALID_ARG, "null id");
+  fd::comm_unique_id(rccl_path, id_out);
+  FD_API_END
+}
+
+int fd_comm_init(fd_engine* eng, const char* rccl_path, int32_t rank, int32_t world, const uint8_t* id_fwd,
+                 const uint8_t* id_back) {
+  FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
+  Engine& e = E_quiet(eng);
+  fd::comm_init(e, rccl_path, rank, world, id_fwd, id_back);
+  FD_API_END
+}
+
+int fd_comm_destroy(fd_engine* eng) {
+  FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
+  Engine& e = E_quiet(eng);
+  fd::comm_destroy(e);
+  FD_API_END
+}
+
+int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t* slots, const uint8_t* present,
+                    const fd_txn_batch* txns, int64_t n, void* input_ready, const fd_txn_batch* next, int64_t next_n,
+                    void* next_ready, double* d_fraud_prob, double* d_confidence, uint8_t* d_decision,
+                    uint8_t* d_risk, int64_t* split_sizes) {
+  FD_API_BEGIN
+  FD_ENGINE_LOCK(eng);
+  Engine& e = E_quiet(eng);
+  fd::ShardComm& c = e.comm;
+  FD_REQUIRE(c.ready, FD_ERR_NOT_LOADED, "no communicators (fd_comm_init)");
+  FD_REQUIRE(params && slots && txns && n >= 0 && (!next || next_n >= 0), FD_ERR_INVALID_ARG, "bad arguments");
+  FD_REQUIRE(params->n_models >= 1 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "bad n_models");
+  for (int m = 0; m < params->n_models; ++m)
+    FD_REQUIRE(slots[m] >= 0 || (present && !present[m]), FD_ERR_INVALID_ARG,
+               "routed scoring needs every present model in a forest slot or FD_SLOT_LSTM");
+  FD_REQUIRE(n == 0 || d_fraud_prob, FD_ERR_INVALID_ARG, "null fraud_prob output");
+  const int G = c.world;
+  // 1. this batch's split sizes: exchanged by the previous step (prefetch) or now
+  int s;
+  if (c.pending && c.pending_key == (const void*)txns->card_key && c.pending_n == n) {
+    s = c.pending_slot;
+  } else {  // no prefetch, or another batch than the prefetched one (whose exchange is dropped on every rank)
+    s = c.next_slot;
+    c.next_slot ^= 1;
+    fd::comm_launch_counts(e, *txns, n, static_cast<hipEvent_t>(input_ready), s);
+  }
+  c.pending = false;
+  FD_HIP(hipEventSynchronize(c.cnt_ev[s]));  // the step's one host wait
+  int64_t send[FD_MAX_SHARDS], recv[FD_MAX_SHARDS];
+  int64_t m = 0, sent = 0;
+  for (int p = 0; p < G; ++p) {
+    send[p] = c.h_cnt[s][p];
+    recv[p] = c.h_cnt[s][G + p];
+    FD_REQUIRE(send[p] >= 0 && recv[p] >= 0, FD_ERR_HIP, "corrupt split sizes");
+    m += recv[p];
+    sent += send[p];
+  }
+  FD_REQUIRE(sent == n, FD_ERR_HIP, "split sizes do not add up to the batch");
+  if (split_sizes)
+    for (int p = 0; p < G; ++p) {
+      split_sizes[p] = send[p];
+      split_sizes[G + p] = recv[p];
+    }
+  // 2. records to their owners (forward stream), after the owner's previous use of this inbox slot
+  if (c.inbox_live[s]) FD_HIP(hipStreamWaitEvent(c.x_fwd, c.inbox_ev[s], 0));
+  c.inbox[s].ensure((size_t)std::max<int64_t>(m, 1) * sizeof(fd::RouteRecord));
+  c.res[s].ensure((size_t)std::max<int64_t>(m, 1) * sizeof(fd::ResultRecord));
+  fd::comm_exchange(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[s].ptr, recv, sizeof(fd::RouteRecord));
+  FD_HIP(hipEventRecord(c.in_ev[s], c.x_fwd));
+  // 3. the owner's features + scoring on the pipeline (features wait for the records), results on the engine stream
+  if (m)
+    pipe_step(e, params, slots, nullptr, present, nullptr, c.inbox[s].ptr, m, nullptr, nullptr, nullptr, nullptr,
+              nullptr, nullptr, c.res[s].ptr, c.in_ev[s]);
+  FD_HIP(hipEventRecord(c.inbox_ev[s], e.stream));  // the engine stream has passed this batch's scoring
+  c.inbox_live[s] = true;
+  // 4. the next batch's partition + counts, ahead, on the forward stream
+  if (next) {
+    const int ns = c.next_slot;
+    c.next_slot ^= 1;
+    fd::comm_launch_counts(e, *next, next_n, static_cast<hipEvent_t>(next_ready), ns);
+    c.pending = true;
+    c.pending_key = next->card_key;
+    c.pending_n = next_n;
+    c.pending_slot = ns;
+  }
+  // 5. results back (reversed splits) and into arrival order, on the engine stream
+  c.back_buf.ensure((size_t)std::max<int64_t>(n, 1) * sizeof(fd::ResultRecord));
+  fd::comm_exchange(e, true, e.stream, c.res[s].ptr, recv, c.back_buf.ptr, send, sizeof(fd::ResultRecord));
+  if (n) fd::launch_result_scatter(e, c.back_buf.ptr, n, d_fraud_prob, d_confidence, d_decision, d_risk);
   FD_API_END
 }
 

@@ -275,6 +275,24 @@ struct IngestTables {
   DeviceBuffer stage_bytes, stage_offsets, stage_out;  // host-API staging
 };
 
+// the engine's own RCCL communicators and buffers for the sharded step (comm.hip, fd_sharded_step in engine.hip);
+// per-batch buffers in two slots (a step's batch and the next one, prefetched)
+struct ShardComm {
+  bool ready = false;
+  int rank = 0, world = 1;
+  void* fwd = nullptr;   // ncclComm_t: counts + records, on x_fwd
+  void* back = nullptr;  // ncclComm_t: results, on the engine stream
+  hipStream_t x_fwd = nullptr;
+  DeviceBuffer rec[2], cnt[2], inbox[2], res[2], back_buf;
+  int64_t* h_cnt[2] = {nullptr, nullptr};  // pinned: send counts [G] then receive counts [G]
+  hipEvent_t cnt_ev[2] = {}, in_ev[2] = {}, inbox_ev[2] = {};
+  bool inbox_live[2] = {};
+  bool pending = false;  // a prefetched batch's counts are in flight (slot pending_slot)
+  const void* pending_key = nullptr;
+  int64_t pending_n = 0;
+  int pending_slot = 0, next_slot = 0;
+};
+
 inline int64_t floor_div_host(int64_t a, int64_t b) {
   int64_t q = a / b;
   if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
@@ -336,6 +354,7 @@ struct Engine {
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
   DeviceBuffer route_blk, route_out, route_err;  // card-hash routing scratch (route.hip)
   DeviceBuffer route_blk_stream;                 // fd_route_partition_stream's block counts (its own stream)
+  ShardComm comm;                                // card-hash sharding over RCCL (comm.hip)
   EnsemblePlan ens;                              // fused XGBoost + IsolationForest + blend (ensemble.hip)
   EnsemblePlan ens1[kMaxSlots];                  // the same kernel over one forest (forest predict), per slot
   bool route_err_live = false;
@@ -438,6 +457,13 @@ void launch_result_pack(Engine& e, const double* fp, const double* conf, const u
 void launch_result_scatter(Engine& e, const void* d_results, int64_t n, double* fp, double* conf, uint8_t* dec,
                            uint8_t* risk);
 void route_check(Engine& e);
+// comm.hip
+void comm_unique_id(const char* rccl_path, uint8_t* out);
+void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint8_t* id_fwd, const uint8_t* id_back);
+void comm_destroy(Engine& e);
+void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot);
+void comm_exchange(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,
+                   const int64_t* recv, size_t elem);
 // lstm.hip
 void load_lstm(Engine& e, const fd_lstm_params& p);
 void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, int T, double* d_prob);

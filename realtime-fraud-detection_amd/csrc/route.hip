@@ -204,8 +204,8 @@ unsigned shard_of_host(unsigned long long key, unsigned G) {
 
 void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_inputs* extra, int64_t n, int G,
                             void* d_records, int64_t* d_counts, hipStream_t stream, DeviceBuffer* scratch) {
-  const hipStream_t st = stream ? stream : st;
-  DeviceBuffer& blk = scratch ? *scratch : blk;
+  const hipStream_t st = stream ? stream : e.stream;
+  DeviceBuffer& blk = scratch ? *scratch : e.route_blk;
   FD_REQUIRE(G >= 1 && G <= FD_MAX_SHARDS, FD_ERR_INVALID_ARG, "n_shards must be in [1, 64]");
   FD_REQUIRE(n >= 0 && n < (1ll << 31), FD_ERR_INVALID_ARG, "batch size out of range");
   FD_REQUIRE(d_counts != nullptr, FD_ERR_INVALID_ARG, "null counts");

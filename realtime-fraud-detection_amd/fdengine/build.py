@@ -20,7 +20,7 @@ LIB_DIR = PKG_ROOT / "lib"
 ORACLE_DIR = REPO_ROOT / "oracle"
 
 HIP_SOURCES = ["engine.hip", "forest.hip", "ensemble.hip", "blend.hip", "features.hip", "route.hip", "lstm.hip",
-               "windows.hip", "snapshot.hip", "ingest.hip", "sink.hip", "model_io.hip"]
+               "windows.hip", "snapshot.hip", "ingest.hip", "sink.hip", "model_io.hip", "comm.hip"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-result"]
 

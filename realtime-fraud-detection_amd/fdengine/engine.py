@@ -490,6 +490,27 @@ class FraudEngine:
                C.c_void_p(records_ptr) if records_ptr else None, int(n),
                C.c_void_p(results_ptr) if results_ptr else None, C.c_void_p(input_ready) if input_ready else None)
 
+    # ---- card-hash sharding over the engine's own RCCL communicators (fd_comm_* / fd_sharded_step)
+    @staticmethod
+    def comm_unique_id(rccl_path: str) -> bytes:
+        buf = (C.c_uint8 * 128)()
+        N.call("fd_comm_unique_id", os.fsencode(rccl_path), C.cast(buf, C.c_void_p))
+        return bytes(buf)
+
+    def comm_init(self, rccl_path: str, rank: int, world: int, id_fwd: bytes, id_back: bytes) -> None:
+        a = (C.c_uint8 * 128).from_buffer_copy(id_fwd)
+        b = (C.c_uint8 * 128).from_buffer_copy(id_back)
+        N.call("fd_comm_init", self._h, os.fsencode(rccl_path), int(rank), int(world), C.cast(a, C.c_void_p),
+               C.cast(b, C.c_void_p))
+
+    def comm_destroy(self) -> None:
+        N.call("fd_comm_destroy", self._h)
+
+    def sharded_scorer(self, params: N.fd_blend_params, slots: Sequence[int],
+                       present: Optional[Sequence[int]] = None) -> "ShardedStep":
+        """fd_sharded_step with its model arguments marshalled once"""
+        return ShardedStep(self, params, slots, present)
+
     def route_scatter_results_device(self, results_ptr: int, n: int, fp_ptr: int, conf_ptr: int = 0,
                                      dec_ptr: int = 0, risk_ptr: int = 0) -> None:
         """Ingest side: put the n returned result records back in micro-batch order."""
@@ -669,3 +690,32 @@ class PipelinedScorer:
             rc = self._fn(self.eng._h, *self._args, int(n), vec_ptr or None, model_probs_ptr or None, fp_ptr,
                           conf_ptr or None, dec_ptr or None, risk_ptr or None)
             N.check(rc, "fd_score_batch_device")
+
+
+class ShardedStep:
+    """fd_sharded_step for a fixed model set (FraudEngine.sharded_scorer): per call only the batch pointers change."""
+
+    def __init__(self, eng: FraudEngine, params: N.fd_blend_params, slots: Sequence[int],
+                 present: Optional[Sequence[int]] = None):
+        M = params.n_models
+        self.eng, self.params = eng, params
+        self._sl = np.array(list(slots) + [-1] * (N.FD_MAX_MODELS - len(slots)), np.int32)
+        self._pres = np.array([1] * M if present is None else list(present), np.uint8)
+        self._cur, self._next = N.fd_txn_batch(), N.fd_txn_batch()
+        self.split_sizes = np.zeros(2 * 64, np.int64)
+        self._fn = N.lib.fd_sharded_step
+
+    def __call__(self, txn_ptrs: dict, n: int, fp_ptr: int, conf_ptr: int, dec_ptr: int, risk_ptr: int,
+                 input_ready: int = 0, next_ptrs: Optional[dict] = None, next_n: int = 0, next_ready: int = 0) -> None:
+        for f in N.TXN_FIELDS:
+            setattr(self._cur, f, txn_ptrs[f])
+        nxt = None
+        if next_ptrs is not None:
+            for f in N.TXN_FIELDS:
+                setattr(self._next, f, next_ptrs[f])
+            nxt = C.byref(self._next)
+        rc = self._fn(self.eng._h, C.byref(self.params), self._sl.ctypes.data, self._pres.ctypes.data,
+                      C.byref(self._cur), int(n), input_ready or None, nxt, int(next_n), next_ready or None,
+                      fp_ptr or None, conf_ptr or None, dec_ptr or None, risk_ptr or None,
+                      self.split_sizes.ctypes.data)
+        N.check(rc, "fd_sharded_step")

@@ -79,6 +79,47 @@ class EngineShardBackend:
         # stream torch (and so RCCL's all_to_all and .cpu()) uses on this device.
         eng.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
+    # ---- the sharded step as one engine call over its own RCCL communicators (fd_comm_init / fd_sharded_step)
+    native = False
+
+    def init_comm(self, rank: int, world: int, group=None) -> None:
+        """Collective over `group`: rank 0 makes the two RCCL unique ids, every rank joins the engine's communicators
+        (forward: counts + records; back: results). RCCL is the process's own (torch's librccl.so)."""
+        import torch.distributed as dist
+        path = rccl_library_path()
+        ids = [None]
+        if rank == 0:
+            from .engine import FraudEngine
+            ids = [(FraudEngine.comm_unique_id(path), FraudEngine.comm_unique_id(path))]
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast_object_list(ids, src=src, group=group)
+        self.eng.comm_init(path, rank, world, ids[0][0], ids[0][1])
+        self._sharded = self.eng.sharded_scorer(self.params, self.slots, self.present)
+        self.native = True
+
+    def sharded_step(self, txns: dict, n: int, input_ready=None, prefetch=None):
+        """fd_sharded_step: outputs (fresh tensors on torch's current stream, written on the engine stream) and the
+        split sizes; prefetch = (next txns, next n[, next input_ready])"""
+        t = self.torch
+        fp = t.empty(n, dtype=t.float64, device=self.device)
+        conf = t.empty(n, dtype=t.float64, device=self.device)
+        dec = t.empty(n, dtype=t.uint8, device=self.device)
+        risk = t.empty(n, dtype=t.uint8, device=self.device)
+        nxt, nn, nready = None, 0, 0
+        if prefetch is not None:
+            nxt = {f: prefetch[0][f].data_ptr() for f in N.TXN_FIELDS}
+            nn = int(prefetch[1])
+            nready = prefetch[2].cuda_event if len(prefetch) > 2 and prefetch[2] is not None else 0
+        self._sharded({f: txns[f].data_ptr() for f in N.TXN_FIELDS}, n, fp.data_ptr(), conf.data_ptr(),
+                      dec.data_ptr(), risk.data_ptr(), input_ready.cuda_event if input_ready is not None else 0,
+                      nxt, nn, nready)
+        return (fp, conf, dec, risk), self._sharded.split_sizes
+
+    def close_comm(self) -> None:
+        if self.native:
+            self.eng.comm_destroy()
+            self.native = False
+
     # ---- streaming sharded step (ShardedScorer._step_streaming)
     def _fwd(self):
         if getattr(self, "_x_fwd", None) is None:
@@ -257,9 +298,13 @@ class ShardedScorer:
     streaming (default True): use the backend's streaming hooks when it has them (module docstring); the result
     all-to-all then runs on a second process group over the same ranks, created here (collectively)."""
 
-    def __init__(self, backend, rank: int, world: int, group=None, streaming: bool = True, force_route: bool = False):
+    def __init__(self, backend, rank: int, world: int, group=None, streaming: bool = True, force_route: bool = False,
+                 native: Optional[bool] = None):
         """force_route: route even with one shard (partition, exchanges over a 1-rank process group, scatter) — the
-        N > 1 step's own work measured / tested on one GPU (tools/route_overhead.py)"""
+        N > 1 step's own work measured / tested on one GPU (tools/route_overhead.py).
+        native: the scoring step as one engine call over the engine's own RCCL communicators (fd_sharded_step);
+        default: when the process group is RCCL ("nccl": one GPU per rank) and the backend supports it; else the
+        streaming step in Python over torch.distributed (gloo groups: ranks sharing a GPU, CPU tests)."""
         self.be, self.rank, self.world, self.group = backend, int(rank), int(world), group
         self.last_counts = None  # (send, recv) split sizes of the last step, for diagnostics
         self.last_windows = None  # (user windows, merged merchant windows) fired by the last windows step
@@ -267,10 +312,17 @@ class ShardedScorer:
         self.streaming = bool(streaming) and self.route and hasattr(backend, "start_partition")
         self.group_back = None
         self._pending = None
+        self.native = False
         if self.streaming:
             import torch.distributed as dist
-            ranks = list(range(self.world)) if group is None else dist.get_process_group_ranks(group)
-            self.group_back = dist.new_group(ranks=ranks)
+            if native is None:
+                native = hasattr(backend, "init_comm") and dist.get_backend(group) == "nccl"
+            if native:
+                backend.init_comm(self.rank, self.world, group)
+                self.native = True
+            else:
+                ranks = list(range(self.world)) if group is None else dist.get_process_group_ranks(group)
+                self.group_back = dist.new_group(ranks=ranks)
 
     def _staged(self) -> bool:
         """gloo moves host memory only: device tensors are staged through the host (several ranks sharing one
@@ -328,6 +380,10 @@ class ShardedScorer:
             if aux:
                 self._aggregates(self.be.unpack(rec, res, n), n, None, windows, sink, flush)
             return self.be.scatter_results(res, n)
+        if self.native and not aux:
+            out, split = self.be.sharded_step(txns, n, input_ready, prefetch)
+            self.last_counts = (split[:G].tolist(), split[G:2 * G].tolist())
+            return out
         if self.streaming and not aux:
             return self._step_streaming(txns, n, input_ready, prefetch)
         rec, counts = self.be.partition(txns, n, G, extras) if aux else self.be.partition(txns, n, G)
@@ -470,6 +526,17 @@ class ShardedScorer:
             raise ValueError(f"{manifest}: not an fdengine checkpoint manifest")
         base = os.path.dirname(manifest)
         return sum(self.be.restore(os.path.join(base, img), self.rank, self.world) for img in doc["images"])
+
+
+def rccl_library_path() -> str:
+    """the RCCL this process uses (torch's bundled librccl.so): the engine dlopens the same file"""
+    import os
+
+    import torch
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    if not os.path.exists(p):
+        raise RuntimeError(f"RCCL library not found at {p}")
+    return p
 
 
 def image_name(step: int, rank: int, world: int) -> str:

@@ -153,11 +153,12 @@ def test_emulated_shards_match_unsharded(G):
 
 @pytest.mark.timeout(300)
 def test_streaming_routed_step_single_rank_matches_direct():
-    """The streaming sharded step's own GPU work on one GPU (ShardedScorer(force_route=True) over a 1-rank RCCL
-    process group): fd_route_partition_stream of the next batch one step ahead on the forward stream, RCCL
-    all-to-alls of counts / records (forward group) and results (second group), fd_score_records_pipelined, the
-    scatter — each step's device outputs dropped at once — bit-identical to the direct pipelined step
-    (fd_score_batch_pipelined) on a twin engine."""
+    """The sharded step's own GPU work on one GPU (ShardedScorer(force_route=True) over a 1-rank RCCL process group),
+    in both streaming forms — native: one fd_sharded_step per batch over the engine's own RCCL communicators
+    (grouped ncclSend/ncclRecv of counts, records and results; the next batch's partition + counts one step ahead);
+    python: fd_route_partition_stream + torch.distributed all-to-alls on two groups + fd_score_records_pipelined —
+    each step's device outputs dropped at once, bit-identical to the direct pipelined step (fd_score_batch_pipelined)
+    on a twin engine."""
     import socket
 
     import torch
@@ -185,7 +186,8 @@ def test_streaming_routed_step_single_rank_matches_direct():
         parts = [{f: t[i * B:(i + 1) * B] for f, t in dev.items()} for i in range(steps)]
         torch.cuda.synchronize()
         res = []
-        for routed in (False, True):
+        for variant in ("direct", "native", "python"):
+            routed = variant != "direct"
             e = FraudEngine(0)
             engines.append(e)
             e.state_init(1 << 17, 1, 16)
@@ -193,8 +195,9 @@ def test_streaming_routed_step_single_rank_matches_direct():
             e.load_merchants(M["fraud_rate"], M["risk_multiplier"])
             e.load_forest(0, xgb)
             e.load_forest(1, ifm)
-            sc = ShardedScorer(EngineShardBackend(e, params, [0, 1], pipelined=True), 0, 1, force_route=routed)
-            assert sc.streaming == routed
+            sc = ShardedScorer(EngineShardBackend(e, params, [0, 1], pipelined=True), 0, 1, force_route=routed,
+                               native=None if variant != "python" else False)
+            assert sc.streaming == routed and sc.native == (variant == "native")
             outs = []
             for i in range(steps):
                 pre = (parts[i + 1], B) if i + 1 < steps and i != 3 else None  # one step without prefetch
@@ -204,10 +207,13 @@ def test_streaming_routed_step_single_rank_matches_direct():
                     h.copy_(o, non_blocking=True)
                 outs.append(host)
             torch.cuda.synchronize()
+            if routed:
+                assert sc.last_counts == ([B], [B])
             res.append(outs)
-        for a, b in zip(*res):
-            for x, y in zip(a, b):
-                np.testing.assert_array_equal(x.numpy(), y.numpy())
+        for other in res[1:]:
+            for a, b in zip(res[0], other):
+                for x, y in zip(a, b):
+                    np.testing.assert_array_equal(x.numpy(), y.numpy())
     finally:
         for e in engines:
             e.close()

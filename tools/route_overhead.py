@@ -35,11 +35,14 @@ cap = 1
 while cap < int(CARDS * 1.6) + 65536:
     cap *= 2
 result = {}
-for routed in (False, True):
+VARIANTS = os.environ.get("VARIANTS", "direct,native,streaming,serial").split(",")
+for name in VARIANTS:
+    routed = name != "direct"
     eng = fdengine.FraudEngine(0)
     eng.state_init(cap, 1, 16)
     eng.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
-    sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), 0, 1, force_route=routed)
+    sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), 0, 1, force_route=routed,
+                       streaming=name != "serial", native=name == "native")
     w = synth_gpu.warm_workload(eng, dev, CARDS, 0, 1, STEPS + 20, B, hours=12.0, keep_batches=0)
     eng.load_forest(0, xgb)
     eng.load_forest(1, ifm)
@@ -54,12 +57,23 @@ for routed in (False, True):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(20, 20 + STEPS)
+    t_host = time.perf_counter()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / STEPS * 1e3
-    result["routed" if routed else "direct"] = ms
-    print(f"{'routed streaming' if routed else 'direct pipelined'}: {ms:.4f} ms/step back to back "
-          f"({B / ms / 1e3:.1f} M txn/s)", flush=True)
+    result[name] = ms
+    print(f"{name}: {ms:.4f} ms/step back to back ({B / ms / 1e3:.1f} M txn/s), host submit "
+          f"{(t_host - t0) / STEPS * 1e3:.4f} ms/step", flush=True)
+    if os.environ.get("PROFILE_HOST") and routed:
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        run(0, 20)
+        pr.disable()
+        torch.cuda.synchronize()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(25)
     eng.close()
     del w, parts
-print(f"routed / direct = {result['routed'] / result['direct']:.3f}", flush=True)
+for k in result:
+    print(f"{k} / direct = {result[k] / result['direct']:.3f}", flush=True)
 dist.destroy_process_group()
