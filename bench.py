@@ -478,7 +478,7 @@ class Config5(Config3):
     name = "config5"
     with_lstm = True
     pipelined_default = False  # 1k latency batches: the per-call cost is the bound, one stream is faster
-    # engine option "graphs" measured slower here (0.103 vs 0.097 ms/step): --graphs to A/B
+    # a captured hipGraph per step measured slower here (0.103 vs 0.097 ms/step, round 2) and was removed
 
     def roofline(self, timing):
         N = self.N
@@ -976,7 +976,7 @@ def launch_ranks(n: int) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def main():
+def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -993,18 +993,12 @@ def main():
     ap.add_argument("--ring-k", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pipeline-mode", type=int, choices=[1, 2], default=1,
-                    help="fd_score_batch_pipelined option pipeline_mode (1: features + scoring per stream, 2: one "
-                         "feature stream)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="config3/4 at N=1: fd_score_batch_device per step instead of the pipelined stream")
     ap.add_argument("--small-streams", type=int, choices=[0, 1, 2], default=None,
                     help="engine option small_streams (latency batches: side streams for the LSTM / other forests)")
     ap.add_argument("--lstm-rows", type=int, choices=[0, 4, 16], default=None,
                     help="engine option lstm_rows (LSTM tile: 0 auto, 4 or 16 transactions per workgroup)")
-    ap.add_argument("--graphs", action="store_true",
-                    help="config5: fd_score_batch_device replays a captured hipGraph per step (engine option "
-                         "graphs) instead of launching every kernel")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--alone-iters", type=int, default=20,
                     help="steps run one at a time after the latency loop, every launch timed: each kernel's "
@@ -1020,11 +1014,20 @@ def main():
     ap.add_argument("--loaded-iters", type=int, default=200,
                     help="steps of the loaded-latency loop: back to back like the timed region, each step's results "
                          "copied to pinned host memory, per-batch submit -> results-on-host times")
-    args = ap.parse_args()
+    return ap
+
+
+def parse_args(argv=None):
+    args = make_parser().parse_args(argv)
     if args.batch is None:
         args.batch = 1024 if args.workload == "config5" else 65536
     if args.cards is None:
         args.cards = 100_000_000 if args.workload == "config4" else 10_000_000
+    return args
+
+
+def main():
+    args = parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -1055,11 +1058,7 @@ def main():
     eng = fdengine.FraudEngine(dev.index)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
-    eng.set_option("pipeline_mode", args.pipeline_mode)
     wl = WORKLOADS[args.workload](args, rank, dev, eng)
-    # --graphs: each fd_score_batch_device latency batch replays a captured hipGraph (one launch for the step)
-    graphs_on = bool(args.graphs)
-    eng.set_option("graphs", int(graphs_on))
     if args.lstm_rows is not None:
         eng.set_option("lstm_rows", args.lstm_rows)
     if args.small_streams is not None:
@@ -1071,6 +1070,11 @@ def main():
     except Exception as e:  # the oracle is only a checker; report, never fall back
         log(f"[rank {rank}] parity spot-check unavailable: {e!r}")
 
+    # a serving process's setup is done: move every object allocated so far out of the cyclic collector's view
+    # (a full collection over the setup's objects stalls the host for milliseconds mid-stream)
+    import gc
+    gc.collect()
+    gc.freeze()
     for i in range(args.warmup):
         wl.step(i)
     torch.cuda.synchronize()
@@ -1108,25 +1112,40 @@ def main():
     loaded = None
     if args.loaded_iters > 0 and hasattr(wl, "fetch"):
         D = max(1, args.loaded_inflight)
+        # the events exist before the loop (a HIP event is created at its first record: that allocation is the
+        # runtime's, not the stream's, and would stall the host mid-stream)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.loaded_iters)]
+        for ev in evs:
+            ev.record(stream)
         torch.cuda.synchronize()
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         h0 = time.perf_counter()
-        evs, sub = [], []
+        sub, host = [], []
+        stall_trace = os.environ.get("FD_STALL_TRACE")  # diagnostics: the host stack of a submission > N ms
+        if stall_trace:
+            import faulthandler
         for i in range(args.loaded_iters):
             if i >= D:
                 evs[i - D].synchronize()
             sub.append(time.perf_counter() - h0)
+            if stall_trace:
+                faulthandler.dump_traceback_later(float(stall_trace) / 1e3, exit=False)
             wl.step(i)
             wl.fetch(i)
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record(stream)
-            evs.append(ev)
+            evs[i].record(stream)
+            if stall_trace:
+                faulthandler.cancel_dump_traceback_later()
+            host.append(time.perf_counter() - h0 - sub[-1])
         torch.cuda.synchronize()
         h1 = time.perf_counter()
         ll = np.array([e0.elapsed_time(ev) - s_ * 1e3 for ev, s_ in zip(evs, sub)])
+        worst = np.argsort(ll)[::-1][:5]
         loaded = {"p50_ms": round(float(np.percentile(ll, 50)), 4), "p99_ms": round(float(np.percentile(ll, 99)), 4),
                   "max_ms": round(float(ll.max()), 4), "samples": len(ll), "inflight": D,
+                  "worst": [[int(j), round(float(ll[j]), 4), round(float(sub[j] * 1e3), 4)] for j in worst],
+                  "host_submit_ms_max": round(max(host) * 1e3, 4),
+                  "host_submit_ms_p50": round(float(np.percentile(host, 50)) * 1e3, 4),
                   "throughput_txn_per_s": round(args.loaded_iters * args.batch * world / (h1 - h0), 1),
                   "basis": f"back-to-back steps with at most {D} micro-batches in flight (backpressure), each "
                            "step's fraud_prob / decision / risk D2H to pinned host memory; latency = host submit -> "
@@ -1223,8 +1242,7 @@ def main():
             "kernel_timing": f"HIP events on the launch stream, 1 launch in {TIMING_EVERY} of each kernel, timed region",
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
-            "step_launch": ("one captured hipGraph per step (untimed steps; the sampled timed steps launch directly)"
-                            if graphs_on else "direct kernel launches"),
+            "step_launch": "direct kernel launches",
         }
         if wl.name in ("config3", "config4", "config5"):
             per_gpu = value / world

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FD_ABI_VERSION 14
+#define FD_ABI_VERSION 15
 
 enum fd_status {
   FD_OK = 0,
@@ -640,13 +640,9 @@ enum fd_timing_kind { FD_TIMING_ALL = -1, FD_TIMING_XGB = 0, FD_TIMING_IFOREST =
 int fd_engine_set_timing(fd_engine* eng, int enable);
 /* Engine tuning knobs (for A/B measurement; defaults are the tuned choices):
      "forest_kernel": 0 auto, 1 force the 256-thread kernel, 2 force the 1024-thread tree-split kernel
-     on the threshold layout, 3 force the 1024-thread kernel on the binned layout, 4 / 5 force the
-     512-thread pair-lane kernel on the binned layout (plain / speculative-children walk), 6 force the
-     tree-split small-batch path (auto takes it below 128 tiles of 256 transactions), 7 force the
-     binned 1024-thread kernel with its top three tree levels read from registers (A/B: slower), 8 force
-     the binned node-only-chunk kernel (auto's choice when the forest has that layout), 9 force it with
-     dynamic per-wave (tree, transaction group) work items (A/B: slower), 10 force it with more trees for
-     the older tree groups (A/B: slower)
+     on the threshold layout, 3 force the 1024-thread kernel on the binned layout, 6 force the tree-split
+     small-batch path (auto takes it below 128 tiles of 256 transactions), 8 force the binned node-only-chunk
+     kernel (auto's choice when the forest has that layout); the variants measured slower were removed
      "ensemble": 1 fused XGBoost + IsolationForest + blend kernel when applicable (default), 0 per-model kernels
      "lstm_rows": LSTM tile, 0 auto (4 transactions below 4096, else 16), 4 or 16
      "timing_every": N >= 1, fd_engine_set_timing records HIP events on one launch in N of each timing kind
@@ -654,13 +650,11 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      "small_streams": latency batches (< 32768 transactions) with the LSTM head and / or several forests: 0
      (default) all on the engine stream (no cross-queue hops; config 5 0.088 ms per 1 k step), 1 the LSTM and the
      forests after the first on one side stream (0.095), 2 on two side streams (0.095)
-     "graphs": 1 fd_score_batch_device runs latency batches (< 32768 transactions, no external probability
-     columns) as a replayed hipGraph per (size, models, outputs, stream, grouping parity): the transaction columns
-     are gathered into engine staging by one kernel, then one graph launch; the first batch of a shape runs
-     directly and captures the graph; any other engine call, a moved engine buffer or a timed (sampled) step
-     falls back to direct launches. 0 (default) direct launches. Same results bit for bit. */
+     "pipeline_lean": fd_score_batch_pipelined's bucket pass, 1 (default) the lean kernel that fits beside the
+     fused ensemble kernel, 0 the full bucket kernel */
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
-/* Engine counters (diagnostics): "graphs_captured", "graphs_replayed" (fd_score_batch_device graph option). */
+/* Engine counters (diagnostics): "pipelined_batches" (batches through fd_score_batch_pipelined /
+   fd_score_records_pipelined so far). */
 int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value);
 int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches);
 int fd_timing_reset(fd_engine* eng);

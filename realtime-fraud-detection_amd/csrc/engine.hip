@@ -71,7 +71,6 @@ static Engine& E(fd_engine* p) {
   FD_REQUIRE(p != nullptr, FD_ERR_INVALID_ARG, "null engine");
   p->e.activate();
   p->e.pipe_dirty = true;
-  ++p->e.graph_epoch;  // models, state, streams or options may change what a captured graph baked in
   return p->e;
 }
 
@@ -335,9 +334,6 @@ int fd_engine_destroy(fd_engine* eng) {
     (void)hipEventDestroy(ev.a);
     (void)hipEventDestroy(ev.b);
   }
-  for (auto& g : e.graphs) (void)hipGraphExecDestroy(g.exec);
-  e.graph_in.release();
-  if (e.graph_cap_stream) (void)hipStreamDestroy(e.graph_cap_stream);
   if (e.own_stream) (void)hipStreamDestroy(e.own_stream);
   delete eng;
   FD_API_END
@@ -394,10 +390,8 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
   Engine& e = E_quiet(eng);
   FD_REQUIRE(key && value, FD_ERR_INVALID_ARG, "null key/value");
   const std::string k(key);
-  if (k == "graphs_captured") {
-    *value = (int64_t)e.graphs_captured;
-  } else if (k == "graphs_replayed") {
-    *value = (int64_t)e.graphs_replayed;
+  if (k == "pipelined_batches") {  // fd_score_batch_pipelined / fd_score_records_pipelined batches so far
+    *value = (int64_t)e.pipe_iter_total;
   } else {
     FD_REQUIRE(false, FD_ERR_INVALID_ARG, "unknown counter: " + k);
   }
@@ -410,9 +404,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   Engine& e = E_quiet(eng);
   FD_REQUIRE(key, FD_ERR_INVALID_ARG, "null key");
   const std::string k(key);
-  if (k != "timing_every" && k != "graphs") ++e.graph_epoch;  // may change what a captured step launches
   if (k == "forest_kernel") {
-    FD_REQUIRE(value >= 0 && value <= 10, FD_ERR_INVALID_ARG, "forest_kernel must be in 0..10");
+    // 0 auto; 1 / 2 / 3 / 8 force kernel 1 / 3 / 4 / 6; 6 the tree-split path (forest.hip launch_forest)
+    FD_REQUIRE(value == 0 || value == 1 || value == 2 || value == 3 || value == 6 || value == 8, FD_ERR_INVALID_ARG,
+               "forest_kernel must be 0, 1, 2, 3, 6 or 8");
     e.forest_variant = (int)value;
   } else if (k == "ensemble") {  // 1 (default): fused forests + blend when applicable; 0: per-model kernels
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble must be 0 or 1");
@@ -423,24 +418,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "pipeline_lean") {  // fd_score_batch_pipelined's bucket pass: 1 (default) lean + deferred
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "pipeline_lean must be 0 or 1");
     e.pipe_lean = value != 0;
-  } else if (k == "pipeline_mode") {  // fd_score_batch_pipelined: 1 features + scoring of a batch on one of two
-    // streams (default); 2 every batch's features on a third stream, scoring on two
-    FD_REQUIRE(value == 1 || value == 2, FD_ERR_INVALID_ARG, "pipeline_mode must be 1 or 2");
-    if ((int)value != e.pipe_mode) {  // drain the pipeline: its buffer ring changes
-      for (hipStream_t st : e.pipe_stream)
-        if (st) FD_HIP(hipStreamSynchronize(st));
-      FD_HIP(hipStreamSynchronize(e.stream));  // the output copies of the old ring
-      for (int q = 0; q < Engine::kPipeSlots; ++q)
-        e.pipe_feat_live[q] = e.pipe_done_live[q] = e.pipe_copy_live[q] = false;
-      e.pipe_iter = 0;
-      e.pipe_mode = (int)value;
-    }
   } else if (k == "small_streams") {  // latency batches: 2 LSTM | other forests on two side streams, 1 one, 0 none
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "small_streams must be 0, 1 or 2");
     e.small_streams = (int)value;
-  } else if (k == "graphs") {  // fd_score_batch_device: latency batches replayed as captured hipGraphs
-    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "graphs must be 0 or 1");
-    e.graphs_on = value != 0;
   } else if (k == "timing_every") {  // kernel timing (fd_timing_*): HIP events on one launch in N of each kind
     FD_REQUIRE(value >= 1 && value <= 1000000, FD_ERR_INVALID_ARG, "timing_every must be >= 1");
     e.timing_every = (int)value;
@@ -835,20 +815,6 @@ int fd_score_matrix_host(fd_engine* eng, const fd_blend_params* params, const in
   FD_API_END
 }
 
-// one transaction column set gathered into the engine's fixed graph staging (8 columns of n rows)
-__global__ void __launch_bounds__(256) graph_stage_kernel(fd_txn_batch src, fd_txn_batch dst, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  reinterpret_cast<uint64_t*>(const_cast<uint64_t*>(dst.card_key))[i] = src.card_key[i];
-  reinterpret_cast<int64_t*>(const_cast<int64_t*>(dst.ts_ms))[i] = src.ts_ms[i];
-  reinterpret_cast<int64_t*>(const_cast<int64_t*>(dst.amount_cents))[i] = src.amount_cents[i];
-  reinterpret_cast<int32_t*>(const_cast<int32_t*>(dst.merchant))[i] = src.merchant[i];
-  reinterpret_cast<uint64_t*>(const_cast<uint64_t*>(dst.device_fp))[i] = src.device_fp[i];
-  const_cast<uint8_t*>(dst.ip_class)[i] = src.ip_class[i];
-  const_cast<uint8_t*>(dst.hour)[i] = src.hour[i];
-  const_cast<uint8_t*>(dst.weekend)[i] = src.weekend[i];
-}
-
 static void score_batch_body(Engine& e, const fd_blend_params& p, const int32_t* slots, const double* const* ext,
                              const uint8_t* present, const fd_txn_batch& t, int64_t n, float* d_vectors,
                              double* dMP, double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk) {
@@ -862,124 +828,16 @@ static void score_batch_body(Engine& e, const fd_blend_params& p, const int32_t*
   score_matrix(e, p, slots, ext, present, vec, n, FD_VECTOR_WIDTH, dMP, dfp, dconf, ddec, drisk, seq, e.state.S);
 }
 
-// latency batch through a captured graph; false: not applicable (the caller runs the body directly)
-static bool score_batch_graph(Engine& e, const fd_blend_params& p, const int32_t* slots, const double* const* ext,
-                              const uint8_t* present, const fd_txn_batch& t, int64_t n, float* d_vectors, double* dMP,
-                              double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk) {
-  if (!e.graphs_on || n >= (int64_t)fd::kSplitTiles * fd::kTile || !e.state.ready) return false;
-  if (p.n_models < 1 || p.n_models > FD_MAX_MODELS) return false;  // the direct path reports it
-  for (int m = 0; m < p.n_models; ++m)
-    if (ext && ext[m]) return false;  // caller columns: not baked into a graph
-  if (e.timing && (e.graph_seq++ % (unsigned long long)e.timing_every) == 0) return false;  // a timed step
-  // models / state / options changed, a buffer moved, or too many shapes: drop every captured graph
-  if (e.graphs_epoch != e.graph_epoch || e.graphs_gen != fd::g_alloc_gen || e.graphs.size() >= 16) {
-    FD_HIP(hipStreamSynchronize(e.stream));
-    for (auto& g : e.graphs) FD_HIP(hipGraphExecDestroy(g.exec));
-    e.graphs.clear();
-    e.graphs_epoch = e.graph_epoch;
-    e.graphs_gen = fd::g_alloc_gen;
-  }
-  const int par = e.state.gs[0].batch_parity;
-  std::vector<char> key;
-  auto put = [&key](const void* q, size_t b) { key.insert(key.end(), (const char*)q, (const char*)q + b); };
-  put(&n, sizeof n);
-  put(&par, sizeof par);
-  put(&p, sizeof p);
-  put(slots, sizeof(int32_t) * (size_t)p.n_models);
-  const uint8_t all = 1;
-  for (int m = 0; m < p.n_models; ++m) put(present ? present + m : &all, 1);
-  const void* ptrs[] = {d_vectors, dMP, dfp, dconf, ddec, drisk, e.stream};
-  put(ptrs, sizeof ptrs);
-  // staging columns (fixed pointers the graph reads)
-  const size_t n8 = (size_t)n * 8;
-  e.graph_in.ensure(4 * n8 + 4 * (size_t)n + 3 * (size_t)n + 64);
-  char* g = e.graph_in.as<char>();
-  fd_txn_batch st{};
-  st.card_key = reinterpret_cast<const uint64_t*>(g);
-  st.ts_ms = reinterpret_cast<const int64_t*>(g + n8);
-  st.amount_cents = reinterpret_cast<const int64_t*>(g + 2 * n8);
-  st.device_fp = reinterpret_cast<const uint64_t*>(g + 3 * n8);
-  st.merchant = reinterpret_cast<const int32_t*>(g + 4 * n8);
-  st.ip_class = reinterpret_cast<const uint8_t*>(g + 4 * n8 + 4 * (size_t)n);
-  st.hour = st.ip_class + n;
-  st.weekend = st.hour + n;
-  FD_REQUIRE(t.card_key && t.ts_ms && t.amount_cents && t.merchant && t.device_fp && t.ip_class && t.hour &&
-                 t.weekend,
-             FD_ERR_INVALID_ARG, "incomplete transaction batch");
-  const unsigned blocks = (unsigned)((n + 255) / 256);
-  for (auto& en : e.graphs)
-    if (en.key == key) {
-      hipLaunchKernelGGL(graph_stage_kernel, dim3(blocks), dim3(256), 0, e.stream, t, st, n);
-      FD_HIP(hipGetLastError());
-      FD_HIP(hipGraphLaunch(en.exec, e.stream));
-      ++e.graphs_replayed;
-      e.state.gs[0].batch_parity = par ^ 1;  // what the captured grouping launch does on the host
-      return true;
-    }
-  // no graph yet for this key: this batch runs directly (allocating every buffer the step needs), then the
-  // step for the NEXT batch of the same parity is captured over the staging columns (capture runs nothing)
-  hipLaunchKernelGGL(graph_stage_kernel, dim3(blocks), dim3(256), 0, e.stream, t, st, n);
-  FD_HIP(hipGetLastError());
-  score_batch_body(e, p, slots, ext, present, st, n, d_vectors, dMP, dfp, dconf, ddec, drisk);
-  const unsigned long long gen = fd::g_alloc_gen;  // every buffer of the step now exists
-  const int par_after = e.state.gs[0].batch_parity;
-  e.state.gs[0].batch_parity = par;  // the captured step starts from the same parity as this one
-  const bool timing = e.timing;
-  e.timing = false;
-  // captured on a private stream (the engine stream may be the null stream, which cannot be captured); the
-  // graph is then launched on the engine stream, after whatever is queued there
-  if (!e.graph_cap_stream) FD_HIP(hipStreamCreateWithFlags(&e.graph_cap_stream, hipStreamNonBlocking));
-  const hipStream_t user = e.stream;
-  hipGraph_t graph = nullptr;
-  FD_HIP(hipStreamBeginCapture(e.graph_cap_stream, hipStreamCaptureModeRelaxed));
-  e.stream = e.graph_cap_stream;
-  try {
-    score_batch_body(e, p, slots, ext, present, st, n, d_vectors, dMP, dfp, dconf, ddec, drisk);
-  } catch (...) {
-    e.stream = user;
-    (void)hipStreamEndCapture(e.graph_cap_stream, &graph);
-    if (graph) (void)hipGraphDestroy(graph);
-    e.timing = timing;
-    e.state.gs[0].batch_parity = par_after;
-    throw;
-  }
-  e.stream = user;
-  e.timing = timing;
-  FD_HIP(hipStreamEndCapture(e.graph_cap_stream, &graph));
-  e.state.gs[0].batch_parity = par_after;
-  hipGraphExec_t exec = nullptr;
-  const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-  (void)hipGraphDestroy(graph);
-  FD_HIP(ie);
-  if (gen != fd::g_alloc_gen) {  // the capture allocated (it should not): its pointers are not trusted
-    FD_HIP(hipGraphExecDestroy(exec));
-    return true;
-  }
-  if (gen != e.graphs_gen) {  // this batch's direct run moved a buffer the earlier graphs read
-    FD_HIP(hipStreamSynchronize(e.stream));
-    for (auto& g : e.graphs) FD_HIP(hipGraphExecDestroy(g.exec));
-    e.graphs.clear();
-    e.graphs_gen = gen;
-  }
-  e.graphs.push_back({std::move(key), exec});
-  ++e.graphs_captured;
-  return true;
-}
-
 int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,
                           const double* const* ext_probs, const uint8_t* present, const fd_txn_batch* txns,
                           int64_t n, float* d_vectors, double* d_model_probs, double* d_fraud_prob,
                           double* d_confidence, uint8_t* d_decision, uint8_t* d_risk) {
   FD_API_BEGIN
   FD_ENGINE_LOCK(eng);
-  Engine& e = E_quiet(eng);  // queues work on e.stream, but changes nothing a captured step depends on
-  e.pipe_dirty = true;
+  Engine& e = E(eng);
   FD_REQUIRE(params && txns && n >= 0, FD_ERR_INVALID_ARG, "bad arguments");
   if (n == 0) return FD_OK;
   FD_REQUIRE(slots != nullptr && d_fraud_prob != nullptr, FD_ERR_INVALID_ARG, "null slots/output");
-  if (score_batch_graph(e, *params, slots, ext_probs, present, *txns, n, d_vectors, d_model_probs, d_fraud_prob,
-                        d_confidence, d_decision, d_risk))
-    return FD_OK;
   score_batch_body(e, *params, slots, ext_probs, present, *txns, n, d_vectors, d_model_probs, d_fraud_prob,
                    d_confidence, d_decision, d_risk);
   FD_API_END
@@ -1017,8 +875,7 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
                       const uint8_t* present, const fd_txn_batch* txns, const void* records, int64_t n,
                       float* d_vectors, double* d_model_probs, double* d_fraud_prob, double* d_confidence,
                       uint8_t* d_decision, uint8_t* d_risk, void* d_results, void* input_ready) {
-  const bool m2 = e.pipe_mode == 2;
-  for (int k = 0; k < (m2 ? 3 : 2); ++k)
+  for (int k = 0; k < 2; ++k)
     if (!e.pipe_stream[k]) FD_HIP(hipStreamCreateWithFlags(&e.pipe_stream[k], hipStreamNonBlocking));
   if (!e.pipe_entry_ev) {
     FD_HIP(hipEventCreateWithFlags(&e.pipe_entry_ev, kStreamEventFlags));
@@ -1028,19 +885,19 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
       FD_HIP(hipEventCreateWithFlags(&e.pipe_copy_ev[k], kStreamEventFlags));
     }
   }
-  // Batch i: buffer slot s = i mod nbuf, scoring stream Sc = pipe_stream[i & 1], feature stream Sf = Sc
-  // (mode 1) or pipe_stream[2] (mode 2). Card-state order: batch i's features after batch i-1's (same queue in
-  // mode 2, an event in mode 1). Buffer s is free once batch i-nbuf's scoring is done (same queue in mode 1,
-  // an event in mode 2). Outputs: the engine stream waits for batch i's scoring.
-  const int nbuf = m2 ? 3 : 2;
+  // Batch i: buffer slot s = i mod 2, its features and its scoring on Sc = pipe_stream[i & 1] (Sf: the same
+  // stream). Card-state order: batch i's bucket pass after batch i-1's (an event). Buffer s is free once batch
+  // i-2's scoring is done (the same queue). Outputs: the engine stream waits for batch i's scoring. (Measured and
+  // dropped: one feature stream for every batch + two scoring streams, ring of three buffers — the third stream
+  // shares a hardware queue with a scoring stream: 567 vs 742 M txn/s)
+  constexpr int nbuf = 2;
   const int s = (int)(e.pipe_iter % (unsigned long long)nbuf);
-  const int prev = (s + nbuf - 1) % nbuf;
+  const int prev = s ^ 1;
   hipStream_t Sc = e.pipe_stream[e.pipe_iter & 1];
-  hipStream_t Sf = m2 ? e.pipe_stream[2] : Sc;
+  hipStream_t Sf = Sc;
   if (e.pipe_dirty) {  // work queued on e.stream by other calls (state loads, snapshots, ...) comes first
     FD_HIP(hipEventRecord(e.pipe_entry_ev, e.stream));
     FD_HIP(hipStreamWaitEvent(Sf, e.pipe_entry_ev, 0));
-    if (m2) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_entry_ev, 0));
     e.pipe_dirty = false;
   }
   if (input_ready) FD_HIP(hipStreamWaitEvent(Sf, static_cast<hipEvent_t>(input_ready), 0));
@@ -1048,8 +905,7 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   if (e.pipe_copy_live[s] && e.pipe_copy_vec[s]) FD_HIP(hipStreamWaitEvent(Sf, e.pipe_copy_ev[s], 0));
   // mode 1: the slot pass (scratch set s & 1, untouched by batch i-1) runs at once; the bucket pass waits for
   // batch i-1's card updates
-  hipEvent_t before_buckets = (!m2 && e.pipe_feat_live[prev]) ? e.pipe_feat_ev[prev] : nullptr;
-  if (m2 && e.pipe_done_live[s]) FD_HIP(hipStreamWaitEvent(Sf, e.pipe_done_ev[s], 0));
+  hipEvent_t before_buckets = e.pipe_feat_live[prev] ? e.pipe_feat_ev[prev] : nullptr;
   e.pipe_vec[s].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
   float* vec = e.pipe_vec[s].as<float>();
   float* seq = nullptr;
@@ -1063,12 +919,11 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
     seq = e.pipe_seq[s].as<float>();
   }
   if (records)
-    fd::launch_features_records(e, records, n, vec, seq, Sf, e.pipe_lean, m2 ? 0 : s & 1, before_buckets);
+    fd::launch_features_records(e, records, n, vec, seq, Sf, e.pipe_lean, s, before_buckets);
   else
-    fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, m2 ? 0 : s & 1, before_buckets);
+    fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, s, before_buckets);
   FD_HIP(hipEventRecord(e.pipe_feat_ev[s], Sf));
   e.pipe_feat_live[s] = true;
-  if (m2) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_feat_ev[s], 0));
   // scoring paths other than the fused kernel share engine scratch (per-model columns, tree-split and LSTM
   // buffers): those batches also wait for the previous batch's scoring
   if (e.pipe_done_live[prev] && !fd::ensemble_applies(e, *params, slots, present, n))
@@ -1088,6 +943,7 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   auto* s_res = records ? reinterpret_cast<fd::ResultRecord*>(so + (2 + (size_t)n_mp) * n8 + 2 * a8) : nullptr;
   if (e.pipe_copy_live[s]) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_copy_ev[s], 0));
   ++e.pipe_iter;
+  ++e.pipe_iter_total;
   {  // the scoring launches go on Sc: score_matrix launches on e.stream
     struct Swap {
       Engine& e;

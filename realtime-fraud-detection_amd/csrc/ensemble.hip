@@ -99,6 +99,9 @@ struct EnsArgs {
   uint8_t* risk;
   const RouteRecord* rec;
   ResultRecord* res;
+#ifdef FD_FOREST_PROFILE
+  int prof_slot;  // which of the kEprofSlots profile buffers this launch writes (launch count mod kEprofSlots)
+#endif
 };
 
 // Ensemble node word: j << 16 | (feature >> 1) << 10 | link << 3 | (feature & 1) << 1 | default_left. `link`
@@ -219,7 +222,9 @@ __device__ __forceinline__ int thr_pad(int g) { return g + (g >> 5); }
 #ifdef FD_FOREST_PROFILE
 // per (workgroup < 256, wave): cycles in prologue, loop top (leaf stores, DMA issue, owner add), walk + leaf
 // loads, DMA wait + barrier, epilogue (s_memtime; read by fd_debug_ens_profile)
-__device__ unsigned long long g_eprof[256 * 16 * 16];
+constexpr int kEprofSlots = 4;  // the last 4 launches (the pipelined stream: launches beside the next features)
+__device__ unsigned long long g_eprof[kEprofSlots * 256 * 16 * 16];
+static int g_eprof_next = 0;
 #define FD_ESTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #else
 #define FD_ESTAMP(var)
@@ -440,7 +445,7 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   __syncthreads();
 #ifdef FD_FOREST_PROFILE
   if (lane == 0 && blockIdx.x < 256) {
-    unsigned long long* o = g_eprof + ((size_t)blockIdx.x * 16 + wave) * 16;
+    unsigned long long* o = g_eprof + (size_t)a.prof_slot * 256 * 16 * 16 + ((size_t)blockIdx.x * 16 + wave) * 16;
     for (int k = 0; k < 7; ++k) o[6 + k] = pr_st[k] ? pr_st[k] - pr_t0 : 0;
     o[0] = pr_t1 - pr_t0;
     o[1] = pr_top;
@@ -643,9 +648,12 @@ bool plan_current(const Engine& e, const EnsemblePlan& P, int sa, int sb) {
 }  // namespace
 
 #ifdef FD_FOREST_PROFILE
+// n words from the start of the buffers: slot k's profile at word k * 256 * 16 * 16; *next_slot (if given) = the slot
+// the next launch writes (so the most recent launch wrote (next_slot + kEprofSlots - 1) % kEprofSlots)
 extern "C" __attribute__((visibility("default"))) int fd_debug_ens_profile(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eprof), sizeof(unsigned long long) * (size_t)n);
 }
+extern "C" __attribute__((visibility("default"))) int fd_debug_ens_profile_next(void) { return g_eprof_next; }
 #endif
 
 namespace {
@@ -732,6 +740,10 @@ bool run_plan(Engine& e, const EnsemblePlan& P, EnsArgs& a, int out, int timing_
   const int64_t blocks = (a.n + kTile - 1) / kTile;
   Engine::Timed* ev = e.timing ? e.next_event_pair(timing_kind) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
+#ifdef FD_FOREST_PROFILE
+  a.prof_slot = g_eprof_next;
+  g_eprof_next = (g_eprof_next + 1) % kEprofSlots;
+#endif
   void* args[] = {&a};
   FD_HIP(hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kEnsWG), args, lds, e.stream));
   if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));

@@ -44,9 +44,6 @@ void set_error(const std::string& msg);
   } while (0)
 
 // Device allocation owned by the engine; grows, never shrinks.
-// bumped by every device (re)allocation or free: a captured hipGraph bakes buffer pointers in, so graphs
-// captured before a change are dropped (engine.hip score_batch_graph)
-inline std::atomic<unsigned long long> g_alloc_gen{0};
 
 struct DeviceBuffer {
   void* ptr = nullptr;
@@ -56,13 +53,9 @@ struct DeviceBuffer {
     release();
     FD_HIP(hipMalloc(&ptr, need));
     bytes = need;
-    ++g_alloc_gen;
   }
   void release() {
-    if (ptr) {
-      (void)hipFree(ptr);
-      ++g_alloc_gen;
-    }
+    if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
     bytes = 0;
   }
@@ -315,17 +308,16 @@ struct Engine {
   hipEvent_t join2_ev = nullptr;
   DeviceBuffer seq_buf;                        // per-txn LSTM input sequences of the fused path
   DeviceBuffer feat_vec, feat_in, feat_ext;  // host-API / fused-pipeline staging for features
-  // fd_score_batch_pipelined (engine.hip): scoring of batch i on pipe_stream[i & 1]; its features on the same
-  // stream (mode 1: no cross-stream wait between a batch's features and its forests, batch i-1's features
-  // waited for by event) or on pipe_stream[2] for every batch (mode 2: the feature chain on one queue, the
-  // scoring streams wait for it); vectors / LSTM sequences in a ring of 2 (mode 1) or 3 (mode 2) buffers
-  static constexpr int kPipeSlots = 3;
-  hipStream_t pipe_stream[3] = {nullptr, nullptr, nullptr};
+  // fd_score_batch_pipelined (engine.hip): features and scoring of batch i on pipe_stream[i & 1] (no cross-stream
+  // wait between a batch's features and its forests; batch i-1's features waited for by event); vectors / LSTM
+  // sequences double-buffered by batch parity
+  static constexpr int kPipeSlots = 2;
+  hipStream_t pipe_stream[2] = {nullptr, nullptr};
   hipEvent_t pipe_entry_ev = nullptr, pipe_feat_ev[kPipeSlots] = {}, pipe_done_ev[kPipeSlots] = {};
   bool pipe_feat_live[kPipeSlots] = {}, pipe_done_live[kPipeSlots] = {};
   bool pipe_dirty = true;  // another engine call since the last pipelined one: order after `stream` first
   unsigned long long pipe_iter = 0;
-  int pipe_mode = 1;       // "pipeline_mode" option
+  unsigned long long pipe_iter_total = 0;  // counter "pipelined_batches"
   bool pipe_lean = true;   // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
   DeviceBuffer pipe_vec[kPipeSlots], pipe_seq[kPipeSlots];
   // the scoring streams write a batch's outputs into pipe_out[slot]; one copy kernel on `stream` moves them to the
@@ -335,20 +327,7 @@ struct Engine {
   hipEvent_t pipe_copy_ev[kPipeSlots] = {};
   bool pipe_copy_live[kPipeSlots] = {};
   bool pipe_copy_vec[kPipeSlots] = {};  // that copy also read the slot's vectors (the slot's next features wait)
-  // fd_score_batch_device for latency batches as a replayed hipGraph ("graphs" option, engine.hip): the inputs
-  // are gathered into fixed staging by one kernel, the rest of the step is one graph launch; a graph per
-  // (shape, models, outputs, stream, grouping parity), all dropped by any other engine call (graph_epoch)
-  bool graphs_on = false;
   int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
-  struct GraphEntry {
-    std::vector<char> key;
-    hipGraphExec_t exec;
-  };
-  std::vector<GraphEntry> graphs;
-  unsigned long long graph_epoch = 0, graphs_epoch = 0, graphs_gen = 0, graph_seq = 0;
-  DeviceBuffer graph_in;
-  hipStream_t graph_cap_stream = nullptr;
-  unsigned long long graphs_captured = 0, graphs_replayed = 0;
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns

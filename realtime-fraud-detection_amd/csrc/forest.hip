@@ -612,148 +612,7 @@ forest_kernel3(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 // word(x) <= node, the feature-row address is (node & 0xFC00) | lane, and a node's two children are
 // one 8-byte pair read: per level one ds_read_b32 (feature) and one ds_read_b64 (children).
 
-// walk4 over G independently chosen (tree, transaction group) items: per-chain tree base tb[j] and
-// feature-row lane address l4[j] (forest_kernel6's dynamic item loop).
-template <int D, int G, bool NAN_AWARE>
-__device__ __forceinline__ void walk4d(const uint32_t (&tb)[G], const uint32_t (&l4)[G], uint32_t (&slot)[G]) {
-  constexpr uint32_t NL = 1u << D;
-  uint32_t c0[G], c8[G], P[G], node[G], kl[G], kr[G], xw[G];
-#pragma unroll
-  for (int j = 0; j < G; ++j) {
-    c0[j] = 0u - tb[j];
-    c8[j] = 8u - tb[j];
-    asm volatile("" : "+v"(c0[j]), "+v"(c8[j]));
-    node[j] = lds_load<uint32_t>(tb[j] + 4u);
-    P[j] = tb[j] + 8u;
-  }
-#pragma unroll
-  for (int j = 0; j < G; ++j) {
-    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | l4[j]);
-    if (D > 1) {
-      const u32x2 k = lds_load<u32x2>(P[j]);
-      kl[j] = k.x;
-      kr[j] = k.y;
-    }
-  }
-#pragma unroll
-  for (int l = 0; l < D; ++l) {
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      bool right = xw[j] > node[j];
-      if (NAN_AWARE) {
-        if (xw[j] == 0xFFFF0000u) right = (node[j] & 1u) == 0u;
-      }
-      P[j] = (P[j] << 1) + (right ? c8[j] : c0[j]);
-      if (l + 1 < D) {
-        uint32_t a = kl[j], b = kr[j];
-        asm volatile("" : "+v"(a), "+v"(b));
-        node[j] = right ? b : a;
-        xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | l4[j]);
-        if (l + 2 < D) {
-          const u32x2 k = lds_load<u32x2>(P[j]);
-          kl[j] = k.x;
-          kr[j] = k.y;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < G; ++j) slot[j] = ((P[j] - tb[j]) >> 3) - NL;
-}
-
-// walk4 with the top three levels taken from registers: `top` holds heap slots 0-7 (the root, its two
-// children and four grandchildren) of each chain's tree, loaded from global memory one chunk ahead
-// (uniform 32-B vector loads, no LDS traffic), so levels 0-2 issue only the feature read and select
-// the next node with v_cndmask; the first children-pair read is that of the level-2 node. Per tree
-// this drops 3 of walk4's 16 LDS reads (the root word and the two top children pairs). Measured
-// SLOWER on config 2 (103.6 vs 87.6 us, tools/forest_sweep.py, interleaved): the walk is bound by
-// issue / latency, not by LDS cycles, and the register selects add VALU work. Kept as option 7 (A/B).
-template <int D, int TPG, typename LeafT, bool NAN_AWARE>
-__device__ __forceinline__ void walk4t(uint32_t buf, int gg, uint32_t lane4, const uint32_t (&top)[TPG][8],
-                                       uint32_t (&slot)[TPG]) {
-  static_assert(D >= 3, "walk4t needs three levels");
-  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
-  constexpr uint32_t NL = 1u << D;
-  uint32_t tb[TPG], c0[TPG], c8[TPG], P[TPG], node[TPG], kl[TPG], kr[TPG], xw[TPG];
-  bool r0[TPG];
-  auto go_right = [](uint32_t x, uint32_t nd) {
-    bool right = x > nd;  // bin > j  <=>  !(x < t_j)
-    if (NAN_AWARE) {
-      if (x == 0xFFFF0000u) right = (nd & 1u) == 0u;  // missing: default direction
-    }
-    return right;
-  };
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {
-    tb[j] = buf + (uint32_t)(gg * TPG + j) * TB;
-    c0[j] = 0u - tb[j];
-    c8[j] = 8u - tb[j];
-    asm volatile("" : "+v"(c0[j]), "+v"(c8[j]));
-    node[j] = top[j][1];
-    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
-  }
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {  // level 0 -> slot 2 + r0
-    r0[j] = go_right(xw[j], node[j]);
-    node[j] = r0[j] ? top[j][3] : top[j][2];
-    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
-  }
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {  // level 1 -> slot 4 + 2 r0 + r1
-    const bool r1 = go_right(xw[j], node[j]);
-    const uint32_t lo = r1 ? top[j][5] : top[j][4], hi = r1 ? top[j][7] : top[j][6];
-    node[j] = r0[j] ? hi : lo;
-    xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
-    P[j] = tb[j] + 8u * (4u + (r0[j] ? 2u : 0u) + (r1 ? 1u : 0u));  // children pair of the level-2 node
-    if (D > 3) {
-      const u32x2 k = lds_load<u32x2>(P[j]);
-      kl[j] = k.x;
-      kr[j] = k.y;
-    }
-  }
-#pragma unroll
-  for (int l = 2; l < D; ++l) {
-#pragma unroll
-    for (int j = 0; j < TPG; ++j) {
-      const bool right = go_right(xw[j], node[j]);
-      P[j] = (P[j] << 1) + (right ? c8[j] : c0[j]);
-      if (l + 1 < D) {
-        uint32_t a = kl[j], b = kr[j];
-        asm volatile("" : "+v"(a), "+v"(b));
-        node[j] = right ? b : a;
-        xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
-        if (l + 2 < D) {
-          const u32x2 k = lds_load<u32x2>(P[j]);
-          kl[j] = k.x;
-          kr[j] = k.y;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) slot[j] = ((P[j] - tb[j]) >> 3) - NL;  // leaf heap slot - 2^D
-}
-
-// heap slots 0-7 of the TPG trees a tree group walks in chunk k (global blob; global vector loads so
-// that they are counted by vmcnt only and never hold up the LDS pipeline's lgkmcnt waits). Loaded one
-// chunk ahead into VGPRs, moved to SGPRs (readfirstlane: the values are wave-uniform) when consumed.
-template <int TPG, typename LeafT, int D>
-__device__ __forceinline__ void load_top(const char* __restrict__ blob, int k, int chunk_stride, int gg,
-                                         uint32_t (&top)[TPG][8]) {
-  constexpr size_t TB = (4u + sizeof(LeafT)) << D;
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {
-    uint64_t a = (uint64_t)(blob + (size_t)k * chunk_stride + (size_t)(gg * TPG + j) * TB);
-    asm volatile("" : "+v"(a));  // a per-lane (VGPR) address: a vector load, not s_load
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const __attribute__((address_space(1))) v4u* g = (const __attribute__((address_space(1))) v4u*)a;
-    const v4u x = g[0], y = g[1];
-    top[j][0] = x.x; top[j][1] = x.y; top[j][2] = x.z; top[j][3] = x.w;
-    top[j][4] = y.x; top[j][5] = y.y; top[j][6] = y.z; top[j][7] = y.w;
-  }
-}
-
-template <int D, int CH, typename LeafT, int KIND, bool TOP>
+template <int D, int CH, typename LeafT, int KIND>
 __global__ void __launch_bounds__(kWG3)
 forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
                int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
@@ -762,7 +621,6 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
                double* __restrict__ out_raw, int32_t* __restrict__ out_leaf) {
   constexpr int TPG = CH / 4;
   constexpr int NL = 1 << D;
-  constexpr bool kTop = TOP && D >= 3;  // walk4t: top three levels from registers
   constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
@@ -785,8 +643,6 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
   FD_PROF_T(p_t0);
 
   stage_chunk_asm(blob, bufA, chunk_stride, kWG3 / 64);  // chunk 0 lands while the tile is binned
-  uint32_t topc[kTop ? TPG : 1][8], topn[kTop ? TPG : 1][8];
-  if constexpr (kTop) load_top<TPG, LeafT, D>(blob, 0, chunk_stride, gg, topn);
   // threshold tables: into LDS over bufB + lv (dead until chunk 1 / the first leaf store) if they fit
   const int n_thr = thr_off[nf];
   const bool tbl_lds = (uint32_t)n_thr * 4u <= accL - bufB;
@@ -829,17 +685,8 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
   for (int k = 0; k < n_chunks; ++k) {
     FD_PROF_T(q0);
     const uint32_t cur = (k & 1) ? bufB : bufA;
-    if constexpr (kTop) {  // chunk k's top levels (loaded during chunk k-1; complete after its dma_wait)
-#pragma unroll
-      for (int j = 0; j < TPG; ++j)
-#pragma unroll
-        for (int u = 1; u < 8; ++u) topc[j][u] = __builtin_amdgcn_readfirstlane(topn[j][u]);
-    }
     if (k + 1 < n_chunks)
       stage_chunk_asm(blob + (size_t)(k + 1) * chunk_stride, (k & 1) ? bufA : bufB, chunk_stride, kWG3 / 64);
-    if constexpr (kTop) {
-      if (k + 1 < n_chunks) load_top<TPG, LeafT, D>(blob, k + 1, chunk_stride, gg, topn);
-    }
     if (k > 0 && gg == ((k - 1) & 3)) {  // owner of chunk k-1 adds its leaf values in tree order
       const uint32_t lv = ((k - 1) & 1) ? lvB : lvA;
       LeafT acc = lds_load<LeafT>(accL + txn * sizeof(LeafT));
@@ -849,17 +696,10 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
     }
     FD_PROF_T(q1);
     uint32_t slots[TPG];
-    if constexpr (kTop) {
-      if (tile_nan)
-        walk4t<D, TPG, LeafT, true>(cur, gg, lane4, topc, slots);
-      else
-        walk4t<D, TPG, LeafT, false>(cur, gg, lane4, topc, slots);
-    } else {
-      if (tile_nan)
-        walk4<D, TPG, LeafT, true>(cur, gg, lane4, slots);
-      else
-        walk4<D, TPG, LeafT, false>(cur, gg, lane4, slots);
-    }
+    if (tile_nan)
+      walk4<D, TPG, LeafT, true>(cur, gg, lane4, slots);
+    else
+      walk4<D, TPG, LeafT, false>(cur, gg, lane4, slots);
 #ifdef FD_FOREST_PROFILE
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -904,52 +744,6 @@ forest_kernel4(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
   if (valid) write_outputs<KIND, LeafT>(acc, row, if_offset, if_denom, out_prob, out_raw);
 }
 
-// Trees of a CH-tree chunk walked by tree group g in kernel 6's skewed mode (MODE 2). The SIMD arbiter
-// issues by age, so the four tree groups (waves 4g..4g+3, launched in that order) walk equal shares in
-// 62k / 77k / 96k / 114k cycles (tools/forest_phases.py per-wave medians) and the older groups then
-// idle at the chunk barrier: the skew gives the older groups more trees.
-__host__ __device__ constexpr int skew_trees(int CH, int g) {
-  return CH == 24 ? (g == 0 ? 8 : g == 1 ? 7 : g == 2 ? 5 : 4)
-       : CH == 16 ? (g == 0 ? 5 : g == 1 ? 4 : g == 2 ? 4 : 3)
-       : CH == 32 ? (g == 0 ? 10 : g == 1 ? 9 : g == 2 ? 7 : 6)
-                  : CH / 4;
-}
-__host__ __device__ constexpr int skew_first(int CH, int g) {
-  return g == 0 ? 0 : skew_first(CH, g - 1) + skew_trees(CH, g - 1);
-}
-static_assert(skew_first(24, 4) == 24 && skew_first(16, 4) == 16 && skew_first(32, 4) == 32, "skew covers the chunk");
-
-// walk NT trees [c0, c0 + NT) of the staged node-only chunk for this lane's transaction, then store
-// their leaf values (global [tree][2^D] array) into the chunk's lv tile
-template <int D, int NT, int CH, typename LeafT>
-__device__ __forceinline__ void walk_group6(uint32_t cur, int c0, uint32_t lane4, bool tile_nan, int k,
-                                            const LeafT* __restrict__ leaves, uint32_t lv, int txn, int64_t row,
-                                            bool valid, int32_t* __restrict__ out_leaf,
-                                            const int32_t* __restrict__ leaf_ids, int n_trees) {
-  constexpr int NL = 1 << D;
-  uint32_t tb[NT], l4[NT], sl[NT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    tb[j] = cur + (uint32_t)(c0 + j) * (4u << D);
-    l4[j] = lane4;
-  }
-  if (tile_nan)
-    walk4d<D, NT, true>(tb, l4, sl);
-  else
-    walk4d<D, NT, false>(tb, l4, sl);
-  LeafT lval[NT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) lval[j] = leaves[((size_t)k * CH + c0 + j) * NL + sl[j]];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    lds_store<LeafT>(lv + ((c0 + j) * kTile + txn) * sizeof(LeafT), lval[j]);
-    if (out_leaf != nullptr && valid) {
-      const int tg = k * CH + c0 + j;
-      if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + sl[j]];
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // forest_kernel6 (depth <= 8, binned nodes): kernel 4 with node-only chunks. The staged chunk holds
 // only the CH trees' node words (1 KiB per depth-8 tree instead of 2-3 KiB with the leaves), so the
@@ -959,7 +753,7 @@ __device__ __forceinline__ void walk_group6(uint32_t cur, int c0, uint32_t lane4
 // ~35 %), so more chains per wave is the lever. After the walk each lane reads its TPG leaf values
 // from the global [tree][2^D] array (L2-resident: 0.5 MiB for 500 x depth 8) with all loads in
 // flight together; the owner pass and the tree-order sum are kernel 4's.
-template <int D, int CH, typename LeafT, int KIND, int MODE>
+template <int D, int CH, typename LeafT, int KIND>
 __global__ void __launch_bounds__(kWG3)
 forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
                int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
@@ -1023,10 +817,6 @@ forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
       lds_store<LeafT>(accL + txn * sizeof(LeafT),
                        (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0);
   }
-  typedef __attribute__((address_space(3))) uint32_t lds_u32;
-  lds_u32* const ctr = (lds_u32*)(size_t)(accL + kTile * (uint32_t)sizeof(LeafT) + 64u);  // 2 item counters
-  constexpr bool DYN = MODE == 1;
-  if (DYN && tid == 0) ctr[0] = 0u;
   dma_wait();  // chunk 0 (published by tile_any's barrier)
   const bool tile_nan =
       tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (accL - s0) + kTile * sizeof(LeafT)), kWG3 / 64);
@@ -1045,83 +835,28 @@ forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
       lds_store<LeafT>(accL + txn * sizeof(LeafT), acc);
     }
     FD_PROF_T(q1);
-    if constexpr (DYN) {
-      // dynamic items: a wave takes G (tree, transaction group) items at a time from the chunk's LDS
-      // counter until all 4 CH are taken, so waves the SIMD arbiter starves take fewer items and the
-      // end-of-chunk barrier waits less; results go to the same lv slots, the owner sum is unchanged
-      constexpr int G = 2;
-      constexpr uint32_t NI = 4u * CH;  // a multiple of G: every grab is G valid items
-      if (tid == 0) ctr[(k + 1) & 1] = 0u;  // chunk k+1's counter, last used in chunk k-1
-      const uint32_t lv = (k & 1) ? lvB : lvA;
-      for (;;) {
-        uint32_t base = 0u;
-        if (lane == 0) base = __hip_atomic_fetch_add(&ctr[k & 1], (uint32_t)G, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (base >= NI) break;
-        uint32_t tbv[G], l4[G], sl[G], cc[G], tx[G];
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-          const uint32_t it = base + (uint32_t)j;
-          cc[j] = it >> 2;
-          tx[j] = ((it & 3u) << 6) + (uint32_t)lane;
-          tbv[j] = cur + cc[j] * (4u << D);
-          l4[j] = s0 + tx[j] * 4u;
-        }
-        if (tile_nan)
-          walk4d<D, G, true>(tbv, l4, sl);
-        else
-          walk4d<D, G, false>(tbv, l4, sl);
-        LeafT lval[G];
-#pragma unroll
-        for (int j = 0; j < G; ++j) lval[j] = leaves[((size_t)k * CH + cc[j]) * NL + sl[j]];
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-          lds_store<LeafT>(lv + (cc[j] * kTile + tx[j]) * sizeof(LeafT), lval[j]);
-          const int64_t r = (int64_t)blockIdx.x * kTile + tx[j];
-          if (out_leaf != nullptr && r < n) {
-            const int tg = k * CH + (int)cc[j];
-            if (tg < n_trees) out_leaf[r * n_trees + tg] = leaf_ids[(size_t)tg * NL + sl[j]];
-          }
-        }
-      }
-    } else if constexpr (MODE == 2) {  // static, skewed tree groups (older waves walk more trees)
-      const uint32_t lv = (k & 1) ? lvB : lvA;
-#define FD_K6_GROUP(g)                                                                                      \
-  walk_group6<D, skew_trees(CH, g), CH, LeafT>(cur, skew_first(CH, g), lane4, tile_nan, k, leaves, lv, txn, row, \
-                                              valid, out_leaf, leaf_ids, n_trees)
-      if (gg == 0)
-        FD_K6_GROUP(0);
-      else if (gg == 1)
-        FD_K6_GROUP(1);
-      else if (gg == 2)
-        FD_K6_GROUP(2);
-      else
-        FD_K6_GROUP(3);
-#undef FD_K6_GROUP
-    } else {
-      uint32_t slots[TPG];
-      if (tile_nan)
-        walk4<D, TPG, LeafT, true, true>(cur, gg, lane4, slots);
-      else
-        walk4<D, TPG, LeafT, false, true>(cur, gg, lane4, slots);
+    uint32_t slots[TPG];
+    if (tile_nan)
+      walk4<D, TPG, LeafT, true, true>(cur, gg, lane4, slots);
+    else
+      walk4<D, TPG, LeafT, false, true>(cur, gg, lane4, slots);
 #ifdef FD_FOREST_PROFILE
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
-      const uint32_t lv = (k & 1) ? lvB : lvA;
-      LeafT lval[TPG];  // leaf values from global memory (L2-resident), all TPG loads in flight together
+    const uint32_t lv = (k & 1) ? lvB : lvA;
+    LeafT lval[TPG];  // leaf values from global memory (L2-resident), all TPG loads in flight together
 #pragma unroll
-      for (int j = 0; j < TPG; ++j) lval[j] = leaves[((size_t)k * CH + gg * TPG + j) * NL + slots[j]];
+    for (int j = 0; j < TPG; ++j) lval[j] = leaves[((size_t)k * CH + gg * TPG + j) * NL + slots[j]];
 #pragma unroll
-      for (int j = 0; j < TPG; ++j) {
-        const int c = gg * TPG + j;
-        lds_store<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT), lval[j]);
-        if (out_leaf != nullptr && valid) {
-          const int tg = k * CH + c;
-          if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slots[j]];
-        }
+    for (int j = 0; j < TPG; ++j) {
+      const int c = gg * TPG + j;
+      lds_store<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT), lval[j]);
+      if (out_leaf != nullptr && valid) {
+        const int tg = k * CH + c;
+        if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slots[j]];
       }
     }
-    FD_PROF_T(q2);  // DYN: walk + leaf in one phase
+    FD_PROF_T(q2);
     FD_PROF_T(q3);
     dma_wait();
     __syncthreads();  // chunk k+1 landed; lv[k&1] complete; owner of k-1 done with lv[(k-1)&1]
@@ -1148,213 +883,6 @@ forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
     for (int c = 0; c < CH; ++c) acc += lds_load<LeafT>(lv + (c * kTile + txn) * sizeof(LeafT));
   }
   if (valid) write_outputs<KIND, LeafT>(acc, row, if_offset, if_denom, out_prob, out_raw);
-}
-
-// ------------------------------------------------------------------------------------------------
-// forest_kernel5 (depth <= 8, kernel 4's binned blob): pair lanes, sums in registers.
-//
-// 512 threads (8 waves, two per SIMD) on a 256-transaction tile. Wave w holds transactions
-// 32w..32w+31 TWICE: lanes 0-31 walk the even tree of every pair (2j, 2j+1) of the staged chunk,
-// lanes 32-63 the odd tree. After a pair, v_permlane32_swap hands every lane both leaf values
-// (even in one register, odd in the other), so each half adds them in tree order to its own copy of
-// the transaction's running sum: the reference's sequential f32 / f64 sum, with no leaf values in
-// LDS, no owner pass and identical work in every wave (kernel 4 spent ~37 % of its time there).
-// Per level and chain: SPEC = false reads the chosen node after the compare (2 x ds_read_b32, 4 VALU:
-// compare, select, shift-add, and-or); SPEC = true reads both children with the feature (kernel 4's
-// ds_read_b32 + ds_read_b64, one more select). All CH / 2 pairs of a chunk are walked interleaved.
-// ds_read_b32 banks per 32-lane group, so the two halves never conflict with each other; within a
-// half the 32 transactions' feature columns are 32 consecutive words (conflict-free).
-//
-// LDS: [0, nf KiB) Xs[f][256] u32 bins | 1 KiB flags | bufA | bufB; the threshold table is staged
-// over bufB (dead until chunk 1) when it fits, else binning reads it from global memory.
-constexpr int kWG5 = 512;
-
-__host__ __device__ constexpr uint32_t lds5_base(int nf, uint32_t cs) { return (uint32_t)nf * 1024u + 2048u + 2u * cs; }
-__host__ __device__ constexpr uint32_t lds5_table(int nf, uint32_t cs, int n_thr) {
-  return (uint32_t)nf * 1024u + 2048u + cs + ((uint32_t)n_thr * 4u + 1023u) / 1024u * 1024u;
-}
-__host__ __device__ constexpr bool lds5_table_fits(int nf, uint32_t cs, int n_thr) {
-  return lds5_table(nf, cs, n_thr) <= (uint32_t)kLdsBudget;
-}
-__host__ __device__ constexpr uint32_t lds_bytes_kernel5(int nf, uint32_t cs, int n_thr) {
-  return (lds5_table_fits(nf, cs, n_thr) && lds5_table(nf, cs, n_thr) > lds5_base(nf, cs)) ? lds5_table(nf, cs, n_thr)
-                                                                                         : lds5_base(nf, cs);
-}
-
-template <int D, int NP, typename LeafT, bool NAN_AWARE, bool SPEC>
-__device__ __forceinline__ void walk5(uint32_t buf, uint32_t half, uint32_t lane4, uint32_t (&A)[NP]) {
-  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
-  uint32_t c0[NP], c4[NP], node[NP], kl[NP], kr[NP];
-#pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    const uint32_t tb = buf + (uint32_t)(2 * j) * TB + half * TB;
-    c0[j] = 0u - tb;
-    c4[j] = (SPEC ? 8u : 4u) - tb;
-    A[j] = tb + (SPEC ? 8u : 4u);  // SPEC: children pair of slot s at tb + 8 s; else slot s at tb + 4 s
-    asm volatile("" : "+v"(c0[j]), "+v"(c4[j]));
-    node[j] = lds_load<uint32_t>(tb + 4u);
-  }
-  if (SPEC) {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const u32x2 k = lds_load<u32x2>(A[j]);
-      kl[j] = k.x;
-      kr[j] = k.y;
-    }
-  }
-#pragma unroll
-  for (int l = 0; l < D; ++l) {
-    uint32_t xw[NP];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) xw[j] = lds_load<uint32_t>((node[j] & 0xFC00u) | lane4);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      bool right = xw[j] > node[j];  // bin > j  <=>  !(x < t_j)
-      if (NAN_AWARE) {
-        if (xw[j] == 0xFFFF0000u) right = (node[j] & 1u) == 0u;  // missing: default direction
-      }
-      A[j] = (A[j] << 1) + (right ? c4[j] : c0[j]);
-      if (l + 1 < D) {
-        if (SPEC) {
-          uint32_t a = kl[j], b = kr[j];
-          asm volatile("" : "+v"(a), "+v"(b));
-          node[j] = right ? b : a;
-          if (l + 2 < D) {
-            const u32x2 k = lds_load<u32x2>(A[j]);
-            kl[j] = k.x;
-            kr[j] = k.y;
-          }
-        } else {
-          node[j] = lds_load<uint32_t>(A[j]);
-        }
-      }
-    }
-  }
-}
-
-// v_permlane32_swap(v, v) is a half exchange: the first result holds v's lanes 0-31 (even-tree leaf)
-// in every lane, the second v's lanes 32-63 (odd-tree leaf)
-__device__ __forceinline__ float lane_swap_even(float v, float& odd) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  odd = __uint_as_float(r[1]);
-  return __uint_as_float(r[0]);
-}
-
-__device__ __forceinline__ double lane_swap_even(double v, double& odd) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
-  odd = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
-  return __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
-}
-
-template <int D, int CH, typename LeafT, int KIND, bool SPEC>
-__global__ void __launch_bounds__(kWG5)
-forest_kernel5(const float* __restrict__ X, int64_t n, int ld, int nf, const char* __restrict__ blob,
-               int n_chunks, int chunk_stride, const int32_t* __restrict__ leaf_ids, int n_trees,
-               const float* __restrict__ thr, const int32_t* __restrict__ thr_off, int bin_steps,
-               float base_margin, double if_offset, double if_denom, double* __restrict__ out_prob,
-               double* __restrict__ out_raw, int32_t* __restrict__ out_leaf) {
-  constexpr int NP = CH / 2;
-  constexpr int NL = 1 << D;
-  constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
-  const uint32_t s0 = (sdyn + 1023u) & ~1023u;
-  char* const lbase = smem + (s0 - sdyn);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t half = (uint32_t)(lane >> 5);
-  const int txn = (wave << 5) + (lane & 31);
-  const uint32_t lane4 = s0 + (uint32_t)txn * 4u;
-  const uint32_t flags = s0 + (uint32_t)nf * 1024u;
-  const uint32_t bufA = flags + 1024u, bufB = bufA + (uint32_t)chunk_stride;
-  const int64_t row = (int64_t)blockIdx.x * kTile + txn;
-  const bool valid = row < n;
-
-  stage_chunk_asm(blob, bufA, chunk_stride, kWG5 / 64);  // chunk 0 lands while the tile is binned
-  const int n_thr = thr_off[nf];
-  const bool tbl_lds = lds5_table_fits(nf, (uint32_t)chunk_stride, n_thr);
-  if (tbl_lds) {
-    float* tl = reinterpret_cast<float*>(lbase + (bufB - s0));
-    for (int i = tid; i < n_thr; i += kWG5) tl[i] = thr[i];
-    __syncthreads();
-  }
-  // prologue: 2 threads per transaction, each bins every other feature, 4 binary searches interleaved
-  int anynan = 0;
-  {
-    const int t = tid & 255, q = tid >> 8;
-    const int64_t r = (int64_t)blockIdx.x * kTile + t;
-    const bool ok = r < n;
-    const int ncopy = ld < nf ? ld : nf;
-    uint32_t* Xs = reinterpret_cast<uint32_t*>(lbase);
-    const float* xr = X + r * (int64_t)ld;
-    for (int f0 = q; f0 < nf; f0 += 8) {
-      float v[4];
-      int o[4], cnt[4], pos[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int f = f0 + 2 * u;
-        v[u] = (ok && f < nf) ? (f < ncopy ? xr[f] : __builtin_nanf("")) : 0.f;  // DMatrix: missing = NaN
-        o[u] = f < nf ? thr_off[f] : 0;
-        cnt[u] = f < nf ? thr_off[f + 1] - o[u] : 0;
-        pos[u] = 0;
-      }
-      for (int st = bin_steps; st > 0; st >>= 1) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int np = pos[u] + st;
-          if (np <= cnt[u]) {
-            const float tv = tbl_lds ? lds_load<float>(bufB + (uint32_t)(o[u] + np - 1) * 4u) : thr[o[u] + np - 1];
-            if (tv <= v[u]) pos[u] = np;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int f = f0 + 2 * u;
-        if (f < nf) {
-          uint32_t w = (uint32_t)pos[u] << 16;
-          if (v[u] != v[u]) {
-            w = 0xFFFF0000u;
-            anynan |= ok ? 1 : 0;
-          }
-          Xs[f * kTile + t] = ok ? w : 0u;
-        }
-      }
-    }
-  }
-  dma_wait();  // chunk 0 (published by tile_any's barrier)
-  const bool tile_nan = tile_any(anynan, reinterpret_cast<uint32_t*>(lbase + (flags - s0)), kWG5 / 64);
-
-  LeafT acc = (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) ? (LeafT)base_margin : (LeafT)0;
-  for (int k = 0; k < n_chunks; ++k) {
-    const uint32_t cur = (k & 1) ? bufB : bufA;
-    if (k + 1 < n_chunks)
-      stage_chunk_asm(blob + (size_t)(k + 1) * chunk_stride, (k & 1) ? bufA : bufB, chunk_stride, kWG5 / 64);
-    uint32_t A[NP];
-    if (tile_nan)
-      walk5<D, NP, LeafT, true, SPEC>(cur, half, lane4, A);
-    else
-      walk5<D, NP, LeafT, false, SPEC>(cur, half, lane4, A);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const uint32_t tb = cur + (uint32_t)(2 * j) * TB + half * TB;
-      // leaf heap slot P in [NL, 2NL): SPEC's A is tb + 8 P, the plain walk's tb + 4 P
-      const uint32_t slot = (SPEC ? (A[j] - tb) >> 3 : (A[j] - tb) >> 2) - NL;
-      const LeafT lv = lds_load<LeafT>(tb + NL * 4u + slot * (uint32_t)sizeof(LeafT));
-      LeafT odd;
-      const LeafT even = lane_swap_even(lv, odd);
-      acc += even;
-      acc += odd;
-      if (out_leaf != nullptr && valid) {
-        const int tg = k * CH + 2 * j + (int)half;
-        if (tg < n_trees) out_leaf[row * n_trees + tg] = leaf_ids[(size_t)tg * NL + slot];
-      }
-    }
-    dma_wait();
-    __syncthreads();  // chunk k+1 landed; every wave is done with chunk k's buffer
-  }
-  if (half == 0 && valid) write_outputs<KIND, LeafT>(acc, row, if_offset, if_denom, out_prob, out_raw);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1599,71 +1127,28 @@ KernelFn pick3(int D, int CH) {
 using KernelFn4 = void (*)(const float*, int64_t, int, int, const char*, int, int, const int32_t*, int,
                            const float*, const int32_t*, int, float, double, double, double*, double*, int32_t*);
 
-template <typename LeafT, int KIND, int CH, bool TOP>
+template <typename LeafT, int KIND, int CH>
 KernelFn4 pick4_ch(int D) {
   switch (D) {
-    case 1: return forest_kernel4<1, CH, LeafT, KIND, TOP>;
-    case 2: return forest_kernel4<2, CH, LeafT, KIND, TOP>;
-    case 3: return forest_kernel4<3, CH, LeafT, KIND, TOP>;
-    case 4: return forest_kernel4<4, CH, LeafT, KIND, TOP>;
-    case 5: return forest_kernel4<5, CH, LeafT, KIND, TOP>;
-    case 6: return forest_kernel4<6, CH, LeafT, KIND, TOP>;
-    case 7: return forest_kernel4<7, CH, LeafT, KIND, TOP>;
-    case 8: return forest_kernel4<8, CH, LeafT, KIND, TOP>;
+    case 1: return forest_kernel4<1, CH, LeafT, KIND>;
+    case 2: return forest_kernel4<2, CH, LeafT, KIND>;
+    case 3: return forest_kernel4<3, CH, LeafT, KIND>;
+    case 4: return forest_kernel4<4, CH, LeafT, KIND>;
+    case 5: return forest_kernel4<5, CH, LeafT, KIND>;
+    case 6: return forest_kernel4<6, CH, LeafT, KIND>;
+    case 7: return forest_kernel4<7, CH, LeafT, KIND>;
+    case 8: return forest_kernel4<8, CH, LeafT, KIND>;
     default: return nullptr;
   }
 }
 
-template <typename LeafT, int KIND, bool TOP>
-KernelFn4 pick4_top(int D, int CH) {
-  switch (CH) {
-    case 4: return pick4_ch<LeafT, KIND, 4, TOP>(D);
-    case 8: return pick4_ch<LeafT, KIND, 8, TOP>(D);
-    case 12: return pick4_ch<LeafT, KIND, 12, TOP>(D);
-    case 16: return pick4_ch<LeafT, KIND, 16, TOP>(D);
-    default: return nullptr;
-  }
-}
-
-// top: walk4t (top three levels from registers; option 7, A/B only) or the plain walk4 (the default)
 template <typename LeafT, int KIND>
-KernelFn4 pick4(int D, int CH, bool top) {
-  return top ? pick4_top<LeafT, KIND, true>(D, CH) : pick4_top<LeafT, KIND, false>(D, CH);
-}
-
-template <typename LeafT, int KIND, int CH>
-KernelFn4 pick5_ch(int D) {
-  switch (D) {
-    case 1: return forest_kernel5<1, CH, LeafT, KIND, false>;
-    case 2: return forest_kernel5<2, CH, LeafT, KIND, false>;
-    case 3: return forest_kernel5<3, CH, LeafT, KIND, false>;
-    case 4: return forest_kernel5<4, CH, LeafT, KIND, false>;
-    case 5: return forest_kernel5<5, CH, LeafT, KIND, false>;
-    case 6: return forest_kernel5<6, CH, LeafT, KIND, false>;
-    case 7: return forest_kernel5<7, CH, LeafT, KIND, false>;
-    case 8: return forest_kernel5<8, CH, LeafT, KIND, false>;
-    default: return nullptr;
-  }
-}
-
-// spec = true (speculative children reads) is instantiated for depth 8 only (the A/B configuration)
-template <typename LeafT, int KIND>
-KernelFn4 pick5(int D, int CH, bool spec) {
-  if (spec) {
-    if (D != 8) return nullptr;
-    switch (CH) {
-      case 4: return forest_kernel5<8, 4, LeafT, KIND, true>;
-      case 8: return forest_kernel5<8, 8, LeafT, KIND, true>;
-      case 12: return forest_kernel5<8, 12, LeafT, KIND, true>;
-      case 16: return forest_kernel5<8, 16, LeafT, KIND, true>;
-      default: return nullptr;
-    }
-  }
+KernelFn4 pick4(int D, int CH) {
   switch (CH) {
-    case 4: return pick5_ch<LeafT, KIND, 4>(D);
-    case 8: return pick5_ch<LeafT, KIND, 8>(D);
-    case 12: return pick5_ch<LeafT, KIND, 12>(D);
-    case 16: return pick5_ch<LeafT, KIND, 16>(D);
+    case 4: return pick4_ch<LeafT, KIND, 4>(D);
+    case 8: return pick4_ch<LeafT, KIND, 8>(D);
+    case 12: return pick4_ch<LeafT, KIND, 12>(D);
+    case 16: return pick4_ch<LeafT, KIND, 16>(D);
     default: return nullptr;
   }
 }
@@ -1698,38 +1183,29 @@ using KernelFn6 = void (*)(const float*, int64_t, int, int, const char*, int, in
                            const float*, const int32_t*, int, float, double, double, double*, double*, int32_t*,
                            const void*);
 
-template <typename LeafT, int KIND, int CH, int MODE>
+template <typename LeafT, int KIND, int CH>
 KernelFn6 pick6_ch(int D) {
   switch (D) {
-    case 1: return (KernelFn6)forest_kernel6<1, CH, LeafT, KIND, MODE>;
-    case 2: return (KernelFn6)forest_kernel6<2, CH, LeafT, KIND, MODE>;
-    case 3: return (KernelFn6)forest_kernel6<3, CH, LeafT, KIND, MODE>;
-    case 4: return (KernelFn6)forest_kernel6<4, CH, LeafT, KIND, MODE>;
-    case 5: return (KernelFn6)forest_kernel6<5, CH, LeafT, KIND, MODE>;
-    case 6: return (KernelFn6)forest_kernel6<6, CH, LeafT, KIND, MODE>;
-    case 7: return (KernelFn6)forest_kernel6<7, CH, LeafT, KIND, MODE>;
-    case 8: return (KernelFn6)forest_kernel6<8, CH, LeafT, KIND, MODE>;
+    case 1: return (KernelFn6)forest_kernel6<1, CH, LeafT, KIND>;
+    case 2: return (KernelFn6)forest_kernel6<2, CH, LeafT, KIND>;
+    case 3: return (KernelFn6)forest_kernel6<3, CH, LeafT, KIND>;
+    case 4: return (KernelFn6)forest_kernel6<4, CH, LeafT, KIND>;
+    case 5: return (KernelFn6)forest_kernel6<5, CH, LeafT, KIND>;
+    case 6: return (KernelFn6)forest_kernel6<6, CH, LeafT, KIND>;
+    case 7: return (KernelFn6)forest_kernel6<7, CH, LeafT, KIND>;
+    case 8: return (KernelFn6)forest_kernel6<8, CH, LeafT, KIND>;
     default: return nullptr;
   }
 }
 
-template <typename LeafT, int KIND, int MODE>
-KernelFn6 pick6_mode(int D, int CH) {
-  switch (CH) {
-    case 16: return pick6_ch<LeafT, KIND, 16, MODE>(D);
-    case 24: return pick6_ch<LeafT, KIND, 24, MODE>(D);
-    case 32: return pick6_ch<LeafT, KIND, 32, MODE>(D);
-    default: return nullptr;
-  }
-}
-
-// mode: 0 equal static tree groups (option 8), 1 dynamic (tree, transaction group) items per wave
-// (option 9), 2 skewed static tree groups (option 10)
 template <typename LeafT, int KIND>
-KernelFn6 pick6(int D, int CH, int mode) {
-  return mode == 1 ? pick6_mode<LeafT, KIND, 1>(D, CH)
-       : mode == 2 ? pick6_mode<LeafT, KIND, 2>(D, CH)
-                   : pick6_mode<LeafT, KIND, 0>(D, CH);
+KernelFn6 pick6(int D, int CH) {
+  switch (CH) {
+    case 16: return pick6_ch<LeafT, KIND, 16>(D);
+    case 24: return pick6_ch<LeafT, KIND, 24>(D);
+    case 32: return pick6_ch<LeafT, KIND, 32>(D);
+    default: return nullptr;
+  }
 }
 
 // small-batch launch: bin once, walk (tiles x chunk groups), sequential sum
@@ -1805,9 +1281,7 @@ extern "C" __attribute__((visibility("default"))) int fd_debug_forest_profile(un
 // Kernel choice (option "forest_kernel"): 0 auto = kernel 6 when the binned node-only layout exists
 // (depth <= 8, <= 65534 distinct thresholds per feature; config 2: 84.1 vs kernel 4's 88.2 us, config-3
 // IsolationForest 38.1 vs 38.7 us, tools/forest_sweep.py), else kernel 4 (binned), else kernel 3
-// (depth <= 8), else kernel 1; 8 forces kernel 6; 1/2/3 force
-// kernel 1/3/4 (7: kernel 4 with walk4t, A/B only), 4/5 force kernel 5 (plain /
-// speculative-children walk), 6 forces the tree-split
+// (depth <= 8), else kernel 1; 8 forces kernel 6; 1/2/3 force kernel 1/3/4; 6 forces the tree-split
 // small-batch path, which auto also takes below kSplitTiles tiles (FD_ERR_UNSUPPORTED when the forest
 // cannot use it).
 // Two forests of a latency batch on one stream (score_matrix, small_streams 0): one binning launch for both,
@@ -1850,7 +1324,8 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   const int64_t blocks = (n + kTile - 1) / kTile;
   FD_REQUIRE(blocks < (1ll << 31), FD_ERR_INVALID_ARG, "batch too large");
   const int v = e.forest_variant;
-  FD_REQUIRE(v >= 0 && v <= 10, FD_ERR_INVALID_ARG, "forest_kernel option must be 0..10");
+  FD_REQUIRE(v == 0 || v == 1 || v == 2 || v == 3 || v == 6 || v == 8, FD_ERR_INVALID_ARG,
+             "forest_kernel option must be 0, 1, 2, 3, 6 or 8");
   Engine::Timed* ev = nullptr;
 
   // small batches: tree-split latency path (option 6 forces it; auto below 128 tiles)
@@ -1868,27 +1343,6 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
     return;
   }
 
-  if (v == 4 || v == 5) {  // forest_kernel5 on kernel 4's binned blob
-    const uint32_t lds5 =
-        pf.binned ? lds_bytes_kernel5(pf.num_feature, (uint32_t)pf.b_chunk_stride, pf.b_n_thr) : 0u;
-    FD_REQUIRE(pf.binned && pf.depth <= 8 && pf.b_chunk % 2 == 0 && lds5 <= kLdsBudget, FD_ERR_UNSUPPORTED,
-               "forest kernel 5 needs the binned layout (depth <= 8)");
-    KernelFn4 fn = xgb ? pick5<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.b_chunk, v == 5)
-                       : pick5<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.b_chunk, v == 5);
-    FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel 5 for this depth/chunk");
-    FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds5));
-    ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
-    if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
-    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kWG5), lds5, e.stream, d_X, n, (int)ld, pf.num_feature,
-                       pf.b_blob.as<const char>(), pf.b_n_chunks, (int)pf.b_chunk_stride,
-                       pf.leaf_ids.as<const int32_t>(), pf.n_trees, pf.b_thr.as<const float>(),
-                       pf.b_thr_off.as<const int32_t>(), pf.bin_steps, pf.base_margin, pf.if_offset,
-                       pf.if_denominator, d_prob, d_raw, d_leaf);
-    FD_HIP(hipGetLastError());
-    if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
-    return;
-  }
-
   // large batches, probabilities only: the fused ensemble kernel over this one forest (its u16 merged-bin tile,
   // link-encoded nodes and LDS-staged leaves; the same f32 margin / f64 path-length sums in tree order)
   if (v == 0 && !d_raw && !d_leaf) {
@@ -1899,12 +1353,11 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
   // + 64 B: kernel 6's two item counters after the tile_any flags
   const size_t lds6 = pf.n_chunk ? lds_bytes_kernel3(pf.num_feature, pf.n_chunk_stride, pf.n_chunk, leaf_sz) + 64 : 0;
   const bool ok6 = pf.binned && pf.n_chunk > 0 && pf.depth <= 8 && lds6 <= kLdsBudget;
-  if (v >= 8)
+  if (v == 8)
     FD_REQUIRE(ok6, FD_ERR_UNSUPPORTED, "forest kernel 6 needs the binned node-only layout (depth <= 8)");
-  if ((v == 0 || v >= 8) && ok6) {
-    const int mode = v == 9 ? 1 : v == 10 ? 2 : 0;
-    KernelFn6 fn = xgb ? pick6<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.n_chunk, mode)
-                       : pick6<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.n_chunk, mode);
+  if ((v == 0 || v == 8) && ok6) {
+    KernelFn6 fn = xgb ? pick6<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.n_chunk)
+                       : pick6<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.n_chunk);
     FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel 6 for this depth/chunk");
     FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds6));
     ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;
@@ -1921,10 +1374,10 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
 
   const size_t lds4 = pf.binned ? lds_bytes_kernel4(pf.num_feature, pf.b_chunk_stride, pf.b_chunk, leaf_sz) : 0;
   const bool ok4 = pf.binned && pf.depth <= 8 && pf.b_chunk % 4 == 0 && lds4 <= kLdsBudget;
-  if (v == 3 || v == 7) FD_REQUIRE(ok4, FD_ERR_UNSUPPORTED, "forest kernel 4 needs the binned layout (depth <= 8)");
-  if ((v == 0 || v == 3 || v == 7) && ok4) {
-    KernelFn4 fn = xgb ? pick4<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.b_chunk, v == 7)
-                       : pick4<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.b_chunk, v == 7);
+  if (v == 3) FD_REQUIRE(ok4, FD_ERR_UNSUPPORTED, "forest kernel 4 needs the binned layout (depth <= 8)");
+  if ((v == 0 || v == 3) && ok4) {
+    KernelFn4 fn = xgb ? pick4<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pf.depth, pf.b_chunk)
+                       : pick4<double, FD_FOREST_SKLEARN_IFOREST>(pf.depth, pf.b_chunk);
     FD_REQUIRE(fn != nullptr, FD_ERR_UNSUPPORTED, "no forest kernel 4 for this depth/chunk");
     FD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4));
     ev = e.timing ? e.next_event_pair(xgb ? FD_TIMING_XGB : FD_TIMING_IFOREST) : nullptr;

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_error_path():
     from fdengine import _native as N
-    assert N.lib.fd_abi_version() == 14
+    assert N.lib.fd_abi_version() == 15
     # null engine -> status code + message, no exception across the ABI
     rc = N.lib.fd_engine_sync(None)
     assert rc == N.FD_ERR_INVALID_ARG

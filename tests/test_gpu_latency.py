@@ -1,8 +1,6 @@
-"""fd_score_batch_device with the "graphs" option (latency batches replayed as captured hipGraphs: inputs gathered
-into fixed staging, the rest of the step one graph launch) against the same calls on a twin engine without it:
-every batch's outputs and vectors bit-identical and the card state identical afterwards, across both grouping
-parities, two output sets, a sampled timed (un-captured) step, a batch size change, a large batch that moves the
-engine's buffers, and another engine call that invalidates the graphs.
+"""Latency batches (fd_score_batch_device, < 128 tiles: the tree-split forests, the LSTM on 4-transaction tiles):
+the engine option small_streams (side streams for the LSTM / the second forest) gives the same outputs bit for
+bit, and the split path's per-tile NaN flags are per call (a NaN batch never leaks into the next).
 Reference chain: FeatureExtractor -> FeatureProcessor -> EnsemblePredictor.predict one micro-batch at a time
 (fl/features/FeatureExtractor.java:50-87, ml/models/ensemble_predictor.py:75-148)."""
 import numpy as np
@@ -22,7 +20,7 @@ def _params(lstm):
     return FraudEngine.blend_params([w[k] for k in names], [S.CONF_MULT[k] for k in names])
 
 
-def _setup(pop, xgb, ifm, lw, graphs):
+def _setup(pop, xgb, ifm, lw):
     U, M = pop["users"], pop["merchants"]
     eng = FraudEngine(0)
     eng.state_init(1 << 17, 1, 16, seq_len=10 if lw is not None else 0)
@@ -32,7 +30,6 @@ def _setup(pop, xgb, ifm, lw, graphs):
     eng.load_forest(1, ifm)
     if lw is not None:
         eng.load_lstm(lw)
-    eng.set_option("graphs", int(graphs))
     return eng
 
 
@@ -46,71 +43,6 @@ def world():
     return pop, tx, xgb, ifm
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("lstm,side", [(False, False), (True, False), (True, True)])
-def test_graph_replay_matches_direct(world, lstm, side):
-    """side: the engines on a created stream (else torch's null stream, which the capture cannot use directly)"""
-    import torch
-    pop, tx, xgb, ifm = world
-    lw = L.random_weights(seed=5) if lstm else None
-    params = _params(lstm)
-    slots = [0, 1] + ([FD_SLOT_LSTM] if lstm else [])
-    M = len(slots)
-    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f])).cuda() for f in TXN_FIELDS}
-    # 1k latency batches, a 1001 batch, a 40k batch (the large-batch path, new buffer sizes), then 1k again
-    sizes = [1000] * 9 + [1001, 1001, 1001] + [1000] * 3 + [40000] + [1000] * 6
-    cuts = np.cumsum([0] + sizes)
-    assert cuts[-1] <= len(tx["card_key"])
-    ref, gra = _setup(pop, xgb, ifm, lw, False), _setup(pop, xgb, ifm, lw, True)
-    side_stream = torch.cuda.Stream() if side else None
-    ctx = torch.cuda.stream(side_stream) if side else torch.cuda.stream(torch.cuda.current_stream())
-    try:
-        ctx.__enter__()
-        st = torch.cuda.current_stream()
-        for e in (ref, gra):
-            e.set_stream(st.cuda_stream)
-        outs = [[torch.empty(40000, dtype=t, device="cuda") for t in (torch.float64,) * 2 + (torch.uint8,) * 2]
-                for _ in range(2)]
-        vec = torch.empty((40000, 64), dtype=torch.float32, device="cuda")
-        mp = torch.empty((M, 40000), dtype=torch.float64, device="cuda")
-        got, want = [], []
-        for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
-            n = int(b - a)
-            ptrs = {f: t[a:b].data_ptr() for f, t in dev.items()}
-            if i == 6:  # a timed stretch: one step in 2 is the sampled, un-captured launch
-                gra.set_option("timing_every", 2)
-                gra.set_timing(True)
-            if i == 10:
-                gra.set_timing(False)
-            if i == 13:  # another engine call: every captured graph is dropped
-                for e in (ref, gra):
-                    e.load_merchants(pop["merchants"]["fraud_rate"], pop["merchants"]["risk_multiplier"])
-            for e, dst in ((ref, want), (gra, got)):
-                fp, conf, dec, risk = outs[i & 1]
-                e.score_batch_device(params, slots, ptrs, n, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(),
-                                     risk.data_ptr(), vec_ptr=vec.data_ptr() if i % 2 == 0 else 0,
-                                     model_probs_ptr=mp.data_ptr())
-                r = [fp[:n].clone(), conf[:n].clone(), dec[:n].clone(), risk[:n].clone(), mp[:, :n].clone()]
-                if i % 2 == 0:
-                    r.append(vec[:n].clone())
-                dst.append(r)
-        torch.cuda.synchronize()
-        for i, (g, w) in enumerate(zip(got, want)):
-            for x, y in zip(g, w):
-                assert np.array_equal(x.cpu().numpy(), y.cpu().numpy()), f"batch {i} differs"
-        nxt = {k: v[cuts[-1]:cuts[-1] + 2048] for k, v in tx.items()}
-        assert np.array_equal(gra.features(nxt), ref.features(nxt)), "card state differs after the stream"
-        # a graph per grouping parity (the output set and vector pointer alternate with it) for each of: 1000,
-        # 1001, 1000 after load_merchants, 1000 after the 40k batch moved buffers; the other untimed steps replay
-        cap, rep = gra.counter("graphs_captured"), gra.counter("graphs_replayed")
-        assert cap >= 6 and rep >= 4, (cap, rep)
-        assert ref.counter("graphs_captured") == 0 and ref.counter("graphs_replayed") == 0
-    finally:
-        ctx.__exit__(None, None, None)
-        ref.close()
-        gra.close()
-
-
 @pytest.mark.timeout(200)
 def test_small_streams_variants_identical(world):
     """engine option small_streams (latency batches: the LSTM and the second forest on 2 / 1 / 0 side streams):
@@ -121,7 +53,7 @@ def test_small_streams_variants_identical(world):
     params = _params(True)
     slots = [0, 1, FD_SLOT_LSTM]
     dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f][:8000])).cuda() for f in TXN_FIELDS}
-    engs = [_setup(pop, xgb, ifm, lw, False) for _ in range(3)]
+    engs = [_setup(pop, xgb, ifm, lw) for _ in range(3)]
     try:
         res = []
         for v, e in enumerate(engs):
@@ -150,7 +82,7 @@ def test_small_streams_variants_identical(world):
 @pytest.mark.timeout(200)
 def test_split_path_nan_flags_per_call(world):
     """The tree-split path's per-tile "holds a NaN" flags are set by the binning launch and cleared by the step's own
-    sum kernel (no host-side epoch, so a replayed graph cannot compare against a stale one). Scoring vectors from the
+    sum kernel (no host-side epoch that one call could compare against a stale value of). Scoring vectors from the
     feature kernel are always finite (FeatureProcessor's final validation), so NaN reaches this path through
     fd_score_matrix / predict: latency batches alternating with and without NaN (and NaN in a single tile), each
     equal to the oracle (leaf ids exact, XGBoost `x < thr` with NaN -> default direction, sklearn NaN rows)."""

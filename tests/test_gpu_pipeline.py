@@ -54,7 +54,7 @@ def world():
     return pop, tx, xgb, ifm
 
 
-def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1, mode=1):
+def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1):
     import torch
     pop, tx, xgb, ifm = world
     params = _params()
@@ -67,7 +67,6 @@ def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1, mo
     torch.cuda.synchronize()
     ref, pip = _setup(pop, xgb, ifm), _setup(pop, xgb, ifm)
     pip.set_option("pipeline_lean", lean)
-    pip.set_option("pipeline_mode", mode)
     try:
         for e in (ref, pip):
             e.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -109,16 +108,15 @@ def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1, mo
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("lean,mode", [(1, 1), (0, 1), (1, 2)])
-def test_pipelined_stream_matches_serial(world, lean, mode):
-    _run(world, [0, 40000, 80000, 81000, 121000, 161000, 201000, 241000], lean=lean, mode=mode)
+@pytest.mark.parametrize("lean", [1, 0])
+def test_pipelined_stream_matches_serial(world, lean):
+    _run(world, [0, 40000, 80000, 81000, 121000, 161000, 201000, 241000], lean=lean)
 
 
 @pytest.mark.timeout(300)
-def test_pipelined_mode2_hot_cards_and_events(world):
-    """mode 2 (one feature stream, two scoring streams, three vector buffers) with hot-card buckets and inputs
-    behind input_ready events"""
-    _run(world, [0, 40000, 80000, 120000, 160000], hot=True, side_stream=True, mode=2)
+def test_pipelined_hot_cards_and_events(world):
+    """hot-card buckets with inputs behind input_ready events"""
+    _run(world, [0, 40000, 80000, 120000, 160000], hot=True, side_stream=True)
 
 
 @pytest.mark.timeout(300)

@@ -41,11 +41,12 @@ eng.load_forest(1, ifm)
 params = FraudEngine.blend_params([0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
 for _ in range(3):
     eng.score_matrix(params, [0, 1], X)
-buf = np.zeros(256 * 16 * 16, np.uint64)
+buf = np.zeros(4 * 256 * 16 * 16, np.uint64)  # the profile buffers of the last 4 launches
 _native.lib.fd_debug_ens_profile.argtypes = [C.c_void_p, C.c_int]
 assert _native.lib.fd_debug_ens_profile(buf.ctypes.data, buf.size) == 0
+newest = (_native.lib.fd_debug_ens_profile_next() + 3) % 4
 nb = min(256, (B + 255) // 256)
-p = buf.reshape(256, 16, 16)[:nb].astype(np.float64)
+p = buf.reshape(4, 256, 16, 16)[newest, :nb].astype(np.float64)
 tot = p[:, :, 5] - p[:, :, 4]
 print(f"{nb} workgroups x 16 waves; cycles per wave (median / p10 / p90):")
 for k, nm in enumerate(["prologue", "loop top", "walk+leaf", "wait+barrier"]):

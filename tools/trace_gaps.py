@@ -1,6 +1,7 @@
 """Kernel timeline of a rocprofv3 --kernel-trace run: per kernel start/end/duration/queue and the idle gap on
 the queue of the dominant kernel (usage: python tools/trace_gaps.py run_kernel_trace.csv [n] [names...])."""
 import csv
+import os
 import sys
 
 path = sys.argv[1]
@@ -9,7 +10,8 @@ names = sys.argv[3:] or ["ensemble", "feat_slot", "feat_bucket"]
 rows = list(csv.DictReader(open(path)))
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]) for r in rows)
 sel = [k for k in ks if any(x in k[2] for x in names)]
-win = sel[-(n + 20):-20] if len(sel) > n + 20 else sel
+skip = int(os.environ.get("TRACE_SKIP", "20"))  # kernels at the end left out (e.g. the bench's alone / latency loops)
+win = sel[-(n + skip):-skip] if len(sel) > n + skip else sel
 t0 = win[0][0]
 last_end = {}
 for s, e, name, q in win:
