@@ -164,6 +164,59 @@ def product_blend(names):
     return ep.blend_params(names), [ep.model_weights[n] for n in names], [E._CONF_MULT[n] for n in names]
 
 
+_HIP = None
+
+
+def hip_d2h(dst: int, src: int, nbytes: int, stream: int) -> None:
+    """hipMemcpyAsync device -> pinned host on `stream` (the process's HIP runtime: torch's libamdhip64, loaded
+    globally by fdengine)"""
+    global _HIP
+    import ctypes
+    if _HIP is None:
+        _HIP = ctypes.CDLL(None).hipMemcpyAsync
+        _HIP.restype = ctypes.c_int
+        _HIP.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    rc = _HIP(dst, src, nbytes, 2, stream)  # hipMemcpyDeviceToHost
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+
+
+class HostOutRing:
+    """k sets of a micro-batch's outputs (fraud_prob f64, confidence f64, decision u8, risk u8) in host-mapped
+    pinned memory (hipHostMalloc mapped): the engine's output kernel writes them over PCIe, so the results reach
+    host memory with the step itself — no hipMemcpyAsync per step (measured: the runtime's D2H call stalls the
+    host ~6 ms about once per 100-200 calls at this rate, FD_STALL_TRACE)"""
+
+    def __init__(self, B: int, k: int):
+        import ctypes
+        import numpy as np
+        self.hip = ctypes.CDLL(None)
+        self.hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        self.hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+        self.hip.hipHostFree.argtypes = [ctypes.c_void_p]
+        self.B, self.sets, self.host = B, [], []
+        nbytes = 18 * B + 64
+        for _ in range(k):
+            h, d = ctypes.c_void_p(), ctypes.c_void_p()
+            if self.hip.hipHostMalloc(ctypes.byref(h), nbytes, 2) != 0:  # hipHostMallocMapped
+                raise RuntimeError("hipHostMalloc failed")
+            if self.hip.hipHostGetDevicePointer(ctypes.byref(d), h, 0) != 0:
+                raise RuntimeError("hipHostGetDevicePointer failed")
+            self.host.append(h.value)
+            base = d.value
+            self.sets.append((base, base + 8 * B, base + 16 * B, base + 17 * B))
+        self.np = np
+
+    def fraud_prob(self, q: int):
+        import ctypes
+        return self.np.ctypeslib.as_array((ctypes.c_double * self.B).from_address(self.host[q]))
+
+    def close(self):
+        for h in self.host:
+            self.hip.hipHostFree(h)
+        self.host, self.sets = [], []
+
+
 def fit_models(dev_index, T, D, mode, K):
     """Models in the reference's file formats on realistic scoring vectors: a 20k-card population's stream
     through the ENGINE's own feature kernel (a scratch engine with a small table), then a random XGBoost
@@ -263,7 +316,8 @@ class Config2:
 
     def fetch(self, i):
         s = i % self.pool
-        self.host_out.copy_(self.prob[s * self.B:(s + 1) * self.B], non_blocking=True)
+        src = self.prob[s * self.B:(s + 1) * self.B]
+        hip_d2h(self.host_out.data_ptr(), src.data_ptr(), src.numel() * 8, self.torch.cuda.current_stream().cuda_stream)
 
     def parity(self):
         import oracle
@@ -397,9 +451,9 @@ class Config3:
 
     def fetch(self, i):
         fp, _, dec, risk = self.outs[self.cur]
-        self.h_fp.copy_(fp, non_blocking=True)
-        self.h_dec.copy_(dec, non_blocking=True)
-        self.h_risk.copy_(risk, non_blocking=True)
+        st = self.torch.cuda.current_stream().cuda_stream
+        for h, d in ((self.h_fp, fp), (self.h_dec, dec), (self.h_risk, risk)):
+            hip_d2h(h.data_ptr(), d.data_ptr(), d.numel() * d.element_size(), st)
 
     def parity(self):
         """The first parity_batches micro-batches (fresh state, carried across them) through the oracle chain."""
@@ -587,6 +641,7 @@ class Config4(Config3):
         self.scorer = ShardedScorer(EngineShardBackend(eng, self.params, [0, 1],
                                                        pipelined=not args.no_pipeline), rank, self.world)
         self.out = None
+        self.host_out = None
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
@@ -613,6 +668,16 @@ class Config4(Config3):
             kw["prefetch"] = ({f: t[(b + 1) * B:(b + 2) * B] for f, t in self.dev.items()}, B)
         self.out = self.scorer.step(part, B, **kw)
 
+    def step_to_host(self, i, q):
+        """one step whose outputs land in host-mapped pinned memory (HostOutRing set q): no separate D2H"""
+        if self.world > 1 and not self.scorer.native:  # out= needs one shard or the native sharded step
+            self.step(i)
+            self.fetch(i)
+            return
+        if self.host_out is None:
+            self.host_out = HostOutRing(self.B, 8)
+        self.step(i, out=self.host_out.sets[q % 8])
+
     def step_h2d(self, i):
         """One micro-batch from pinned host memory: H2D copy, the step on the copy, (fetch: D2H results)."""
         if self.next_h2d >= len(self.h2d_pool):
@@ -627,10 +692,18 @@ class Config4(Config3):
         self.out = self.scorer.step(self.stage[q], self.B, input_ready=ev)
 
     def fetch(self, i):
+        """the step's fraud_prob / decision / risk to pinned host memory, queued on the stream (hipMemcpyAsync
+        directly: torch's copy_ into pinned memory also does the caching host allocator's per-copy event
+        bookkeeping, measured to stall the host for ~6 ms about once per 100-200 copies; FD_FETCH=torch for it)"""
         fp, conf, dec, risk = self.out
-        self.h_fp.copy_(fp, non_blocking=True)
-        self.h_dec.copy_(dec, non_blocking=True)
-        self.h_risk.copy_(risk, non_blocking=True)
+        if os.environ.get("FD_FETCH") == "torch":
+            self.h_fp.copy_(fp, non_blocking=True)
+            self.h_dec.copy_(dec, non_blocking=True)
+            self.h_risk.copy_(risk, non_blocking=True)
+            return
+        st = self.torch.cuda.current_stream().cuda_stream
+        for h, d in ((self.h_fp, fp), (self.h_dec, dec), (self.h_risk, risk)):
+            hip_d2h(h.data_ptr(), d.data_ptr(), d.numel() * d.element_size(), st)
 
     def parity(self):
         """N=1: the first parity_batches micro-batches through the product path (the pipelined ShardedScorer step,
@@ -749,7 +822,9 @@ class Ingest:
         self.codec.parse_device(self.buf.data_ptr() + s * self.stride, self.off.data_ptr(), self.B, self.ptrs)
 
     def fetch(self, i):
-        self.h_status.copy_(self.cols["status"], non_blocking=True)
+        d = self.cols["status"]
+        hip_d2h(self.h_status.data_ptr(), d.data_ptr(), d.numel() * d.element_size(),
+                self.torch.cuda.current_stream().cuda_stream)
 
     def parity(self):
         from oracle import ingest_ref as R
@@ -1131,8 +1206,11 @@ def main():
             sub.append(time.perf_counter() - h0)
             if stall_trace:
                 faulthandler.dump_traceback_later(float(stall_trace) / 1e3, exit=False)
-            wl.step(i)
-            wl.fetch(i)
+            if hasattr(wl, "step_to_host"):
+                wl.step_to_host(i, i)
+            else:
+                wl.step(i)
+                wl.fetch(i)
             evs[i].record(stream)
             if stall_trace:
                 faulthandler.cancel_dump_traceback_later()
@@ -1148,8 +1226,9 @@ def main():
                   "host_submit_ms_p50": round(float(np.percentile(host, 50)) * 1e3, 4),
                   "throughput_txn_per_s": round(args.loaded_iters * args.batch * world / (h1 - h0), 1),
                   "basis": f"back-to-back steps with at most {D} micro-batches in flight (backpressure), each "
-                           "step's fraud_prob / decision / risk D2H to pinned host memory; latency = host submit -> "
-                           "that D2H complete (GPU event timestamps)"}
+                           "step's fraud_prob / confidence / decision / risk written to host-mapped pinned memory by the "
+                           "engine's output kernel (workloads without that: a D2H to pinned memory); latency = host "
+                           "submit -> results in host memory (GPU event timestamps)"}
         if dist:
             t = torch.tensor([loaded["p99_ms"]], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1158,8 +1237,11 @@ def main():
     lat = []
     for i in range(args.latency_iters):
         a = time.perf_counter()
-        wl.step(i)
-        wl.fetch(i)
+        if hasattr(wl, "step_to_host"):
+            wl.step_to_host(i, i)
+        else:
+            wl.step(i)
+            wl.fetch(i)
         stream.synchronize()
         lat.append(time.perf_counter() - a)
     lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)

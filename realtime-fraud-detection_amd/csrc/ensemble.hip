@@ -253,6 +253,9 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   unsigned long long pr_top = 0, pr_walk = 0, pr_sync = 0, pr_dma = 0, pr_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   FD_ESTAMP(pr_t0);
+#ifdef FD_FOREST_PROFILE
+  const unsigned long long pr_rt0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz, one clock for the whole GPU
+#endif
   // above the feature kernels of the next micro-batch that share the CU in the pipelined stream (priority 0):
   // this kernel is the stream's critical path, theirs is latency-bound with slack
   __builtin_amdgcn_s_setprio(2);
@@ -454,6 +457,8 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     o[13] = pr_dma;  // of pr_sync: the owner waves' wait for their chunk DMA (0 for the other waves)
     o[4] = pr_t0;
     o[5] = __builtin_amdgcn_s_memtime();
+    o[14] = pr_rt0;
+    o[15] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
   if (gg != 0 || !valid) return;

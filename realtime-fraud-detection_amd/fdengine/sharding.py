@@ -97,23 +97,18 @@ class EngineShardBackend:
         self._sharded = self.eng.sharded_scorer(self.params, self.slots, self.present)
         self.native = True
 
-    def sharded_step(self, txns: dict, n: int, input_ready=None, prefetch=None):
-        """fd_sharded_step: outputs (fresh tensors on torch's current stream, written on the engine stream) and the
-        split sizes; prefetch = (next txns, next n[, next input_ready])"""
-        t = self.torch
-        fp = t.empty(n, dtype=t.float64, device=self.device)
-        conf = t.empty(n, dtype=t.float64, device=self.device)
-        dec = t.empty(n, dtype=t.uint8, device=self.device)
-        risk = t.empty(n, dtype=t.uint8, device=self.device)
+    def sharded_step(self, txns: dict, n: int, input_ready=None, prefetch=None, out=None):
+        """fd_sharded_step: outputs (fresh tensors on torch's current stream, written on the engine stream, or the
+        caller's `out`, see _outputs) and the split sizes; prefetch = (next txns, next n[, next input_ready])"""
+        res, (fp, conf, dec, risk) = self._outputs(n, out)
         nxt, nn, nready = None, 0, 0
         if prefetch is not None:
             nxt = {f: prefetch[0][f].data_ptr() for f in N.TXN_FIELDS}
             nn = int(prefetch[1])
             nready = prefetch[2].cuda_event if len(prefetch) > 2 and prefetch[2] is not None else 0
-        self._sharded({f: txns[f].data_ptr() for f in N.TXN_FIELDS}, n, fp.data_ptr(), conf.data_ptr(),
-                      dec.data_ptr(), risk.data_ptr(), input_ready.cuda_event if input_ready is not None else 0,
-                      nxt, nn, nready)
-        return (fp, conf, dec, risk), self._sharded.split_sizes
+        self._sharded({f: txns[f].data_ptr() for f in N.TXN_FIELDS}, n, fp, conf, dec, risk,
+                      input_ready.cuda_event if input_ready is not None else 0, nxt, nn, nready)
+        return res, self._sharded.split_sizes
 
     def close_comm(self) -> None:
         if self.native:
@@ -228,32 +223,38 @@ class EngineShardBackend:
             self.eng.score_records_device(self.params, self.slots, rec.data_ptr(), m, res.data_ptr(), self.present)
         return res
 
-    def score_batch(self, txns: dict, n: int, input_ready=None, vectors=None, model_probs=None):
+    def _outputs(self, n: int, out):
+        """caller-owned outputs (tensors or raw addresses; device memory or host-mapped pinned memory, which the
+        engine's output kernel then writes over PCIe: no separate D2H) or fresh device tensors"""
+        if out is not None:
+            return tuple(out), [o if isinstance(o, int) else o.data_ptr() for o in out]
+        t = self.torch
+        o = (t.empty(n, dtype=t.float64, device=self.device), t.empty(n, dtype=t.float64, device=self.device),
+             t.empty(n, dtype=t.uint8, device=self.device), t.empty(n, dtype=t.uint8, device=self.device))
+        return o, [x.data_ptr() for x in o]
+
+    def score_batch(self, txns: dict, n: int, input_ready=None, vectors=None, model_probs=None, out=None):
         """One shard: the whole hot path on the ingest GPU in arrival order (nothing to route).
         input_ready: optional torch.cuda.Event recorded once the input tensors were complete (pipelined).
         vectors / model_probs: optional device tensors (n x 64 f32 / n_models x n f64) that also receive the
-        batch's scoring vectors / per-model probabilities."""
-        t = self.torch
-        fp = t.empty(n, dtype=t.float64, device=self.device)
-        conf = t.empty(n, dtype=t.float64, device=self.device)
-        dec = t.empty(n, dtype=t.uint8, device=self.device)
-        risk = t.empty(n, dtype=t.uint8, device=self.device)
+        batch's scoring vectors / per-model probabilities.
+        out: optional (fraud_prob f64, confidence f64, decision u8, risk u8) caller-owned buffers (see _outputs)."""
+        res, (fp, conf, dec, risk) = self._outputs(n, out)
         if n:
             ptrs = {f: txns[f].data_ptr() for f in N.TXN_FIELDS}
             if self.pipelined:
                 if self._scorer is None:
                     self._scorer = self.eng.pipelined_scorer(self.params, self.slots, self.present)
-                self._scorer(ptrs, n, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
-                             input_ready.cuda_event if input_ready is not None else 0,
+                self._scorer(ptrs, n, fp, conf, dec, risk, input_ready.cuda_event if input_ready is not None else 0,
                              vec_ptr=vectors.data_ptr() if vectors is not None else 0,
                              model_probs_ptr=model_probs.data_ptr() if model_probs is not None else 0)
             else:
-                self.eng.score_batch_device(self.params, self.slots, ptrs, n, fp.data_ptr(), conf.data_ptr(),
-                                            dec.data_ptr(), risk.data_ptr(), present=self.present,
+                self.eng.score_batch_device(self.params, self.slots, ptrs, n, fp, conf, dec, risk,
+                                            present=self.present,
                                             vec_ptr=vectors.data_ptr() if vectors is not None else 0,
                                             model_probs_ptr=model_probs.data_ptr() if model_probs is not None
                                             else 0)
-        return fp, conf, dec, risk
+        return res
 
     def snapshot(self, path: str, rank: int, world: int) -> int:
         return self.eng.state_snapshot(path, rank, world)
@@ -347,7 +348,7 @@ class ShardedScorer:
         return int(g.cpu()[0])
 
     def step(self, txns: dict, n: int, extras: Optional[dict] = None, windows: bool = False, sink: bool = False,
-             flush: bool = False, input_ready=None, vectors=None, model_probs=None, prefetch=None):
+             flush: bool = False, input_ready=None, vectors=None, model_probs=None, prefetch=None, out=None):
         """txns: field -> tensor (n rows) on the backend's device, in arrival order.
         input_ready: optional torch.cuda.Event recorded once `txns` were complete (a pipelined backend's features
         wait for it instead of assuming resident inputs).
@@ -359,7 +360,10 @@ class ShardedScorer:
         vectors / model_probs (world 1, backends with score_batch): optional device tensors that also receive the
         batch's scoring vectors (n x 64) / per-model probabilities (n_models x n).
         prefetch (world > 1, streaming): (next txns, next n[, next input_ready]) — the next micro-batch, whose
-        partition and count exchange this step launches ahead; every rank must pass it in the same steps."""
+        partition and count exchange this step launches ahead; every rank must pass it in the same steps.
+        out (world 1 with score_batch, or the native sharded step): caller-owned output buffers — tensors or raw
+        addresses, device memory or host-mapped pinned memory the engine's output kernel writes over PCIe — that
+        receive the results instead of fresh device tensors (returned as given)."""
         import torch
         G = self.world
         aux = windows or sink
@@ -367,7 +371,7 @@ class ShardedScorer:
             self.last_counts = ([n], [n])
             if hasattr(self.be, "score_batch"):
                 kw = {k: v for k, v in (("input_ready", input_ready), ("vectors", vectors),
-                                        ("model_probs", model_probs)) if v is not None}
+                                        ("model_probs", model_probs), ("out", out)) if v is not None}
                 out = self.be.score_batch(txns, n, **kw)
                 if aux:
                     cols = {f: txns[f] for f in ("card_key", "ts_ms", "amount_cents", "merchant")}
@@ -381,9 +385,11 @@ class ShardedScorer:
                 self._aggregates(self.be.unpack(rec, res, n), n, None, windows, sink, flush)
             return self.be.scatter_results(res, n)
         if self.native and not aux:
-            out, split = self.be.sharded_step(txns, n, input_ready, prefetch)
+            res, split = self.be.sharded_step(txns, n, input_ready, prefetch, out)
             self.last_counts = (split[:G].tolist(), split[G:2 * G].tolist())
-            return out
+            return res
+        if out is not None:
+            raise ValueError("out= needs one shard (score_batch) or the native sharded step")
         if self.streaming and not aux:
             return self._step_streaming(txns, n, input_ready, prefetch)
         rec, counts = self.be.partition(txns, n, G, extras) if aux else self.be.partition(txns, n, G)

@@ -292,3 +292,68 @@ def test_pipelined_outputs_dropped_each_step(world):
     finally:
         ref.close()
         pip.close()
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_outputs_into_host_mapped_memory(world):
+    """ShardedScorer at world 1 (pipelined) with out= buffers in host-mapped pinned memory (hipHostMalloc mapped):
+    the engine's output kernel writes the results over PCIe, a ring of 3 output sets reused while steps are in
+    flight; every step's results equal the serial fd_score_batch_device bit for bit."""
+    import ctypes
+
+    import torch
+
+    from fdengine.sharding import EngineShardBackend, ShardedScorer
+    pop, tx, xgb, ifm = world
+    params = _params()
+    B = 20_000
+    cuts = list(range(0, 9 * B + 1, B))
+    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f][:cuts[-1]])).cuda() for f in TXN_FIELDS}
+    torch.cuda.synchronize()
+    hip = ctypes.CDLL(None)
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+    hip.hipHostFree.argtypes = [ctypes.c_void_p]
+    host, sets = [], []
+    for _ in range(3):
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        assert hip.hipHostMalloc(ctypes.byref(h), 18 * B + 64, 2) == 0  # hipHostMallocMapped
+        assert hip.hipHostGetDevicePointer(ctypes.byref(d), h, 0) == 0
+        host.append(h.value)
+        sets.append((d.value, d.value + 8 * B, d.value + 16 * B, d.value + 17 * B))
+
+    def view(q, off, ct, k):
+        return np.ctypeslib.as_array((ct * k).from_address(host[q] + off)).copy()
+
+    ref, pip = _setup(pop, xgb, ifm), _setup(pop, xgb, ifm)
+    try:
+        sc = ShardedScorer(EngineShardBackend(pip, params, [0, 1], pipelined=True), 0, 1)
+        ref.set_stream(torch.cuda.current_stream().cuda_stream)
+        evs, got = [], []
+        for j, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+            if j >= 2:  # at most 2 in flight before a set is reused (3 sets)
+                evs[j - 2].synchronize()
+                q = (j - 2) % 3
+                got.append([view(q, 0, ctypes.c_double, B), view(q, 8 * B, ctypes.c_double, B),
+                            view(q, 16 * B, ctypes.c_uint8, B), view(q, 17 * B, ctypes.c_uint8, B)])
+            res = sc.step({f: t[a:b] for f, t in dev.items()}, b - a, out=sets[j % 3])
+            assert res == sets[j % 3]
+            ev = torch.cuda.Event()
+            ev.record()
+            evs.append(ev)
+        torch.cuda.synchronize()
+        for j in range(len(cuts) - 3, len(cuts) - 1):
+            q = j % 3
+            got.append([view(q, 0, ctypes.c_double, B), view(q, 8 * B, ctypes.c_double, B),
+                        view(q, 16 * B, ctypes.c_uint8, B), view(q, 17 * B, ctypes.c_uint8, B)])
+        for (a, b), h in zip(zip(cuts[:-1], cuts[1:]), got):
+            o_ref = _outs(b - a)
+            ref.score_batch_device(params, [0, 1], {f: t[a:b].data_ptr() for f, t in dev.items()}, b - a,
+                                   *[o.data_ptr() for o in o_ref])
+            for x, y in zip(h, o_ref):
+                np.testing.assert_array_equal(x, y.cpu().numpy())
+    finally:
+        ref.close()
+        pip.close()
+        for h in host:
+            hip.hipHostFree(h)

@@ -50,7 +50,17 @@ def summary(name, ps):
     print("  walk+leaf by tree group (median):", wk)
     st = np.concatenate([p[:, :, 6:13] for p in ps], axis=0)
     print("  prologue marks (median):", [float(np.median(st[:, :, k])) for k in range(7)])
-
+    # workgroup start / end times on the GPU-wide 100 MHz clock (s_memrealtime): how late the workgroups of a
+    # launch start (waiting for a CU) relative to its first, and the launch's span, in microseconds
+    late, span = [], []
+    for p in ps:
+        t0 = p[:, :, 14].min(axis=1)  # each workgroup's first wave start
+        t1 = p[:, :, 15].max(axis=1)
+        late.append(np.percentile(t0 - t0.min(), [50, 90, 100]) / 100.0)
+        span.append((t1.max() - t0.min()) / 100.0)
+    late = np.array(late)
+    print(f"  workgroup start after the launch's first (us, median over launches): p50 {np.median(late[:, 0]):.1f} "
+          f"p90 {np.median(late[:, 1]):.1f} max {np.median(late[:, 2]):.1f}; launch span {np.median(span):.1f} us")
 
 def main():
     cards = int(os.environ.get("CARDS", 10_000_000))
