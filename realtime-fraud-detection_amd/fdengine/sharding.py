@@ -341,6 +341,26 @@ class ShardedScorer:
             return
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=g)
 
+    def _all_gather_records(self, arr: np.ndarray) -> list:
+        """every rank's structured-array records (same dtype on all ranks), gathered as fixed-size tensors: the
+        counts first (one int64 per rank), then each rank's records as bytes padded to the largest count — no
+        pickled objects on the exchange"""
+        import torch
+        import torch.distributed as dist
+        dev = "cpu" if self._staged() else self.be.device
+        cnt = torch.tensor([len(arr)], dtype=torch.int64, device=dev)
+        counts = [torch.empty_like(cnt) for _ in range(self.world)]
+        dist.all_gather(counts, cnt, group=self.group)
+        counts = [int(c.item()) for c in counts]
+        rec = arr.dtype.itemsize
+        top = max(1, max(counts))
+        buf = np.zeros(top * rec, np.uint8)
+        buf[:len(arr) * rec] = np.frombuffer(np.ascontiguousarray(arr).tobytes(), np.uint8)
+        mine = torch.from_numpy(buf).to(dev)
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(parts, mine, group=self.group)
+        return [np.frombuffer(p.cpu().numpy().tobytes()[:c * rec], arr.dtype).copy() for p, c in zip(parts, counts)]
+
     def _allreduce_max(self, t):
         import torch.distributed as dist
         g = t.cpu() if self._staged() else t.clone()
@@ -451,18 +471,13 @@ class ShardedScorer:
         return be.scatter_results(back, n, sentinel=True)
 
     def _aggregates(self, cols: dict, m: int, tmax, windows: bool, sink: bool, flush: bool):
-        import torch.distributed as dist
         if windows:
             if tmax is not None:  # one watermark for the node: the largest event time of all ingest batches
                 gmax = self._allreduce_max(tmax)
                 if gmax != INT64_MIN:
                     self.be.windows_observe(gmax)
             uw, mw = self.be.windows_step(cols, m, flush)
-            if self.world > 1:
-                parts = [None] * self.world
-                dist.all_gather_object(parts, mw, group=self.group)
-            else:
-                parts = [mw]
+            parts = self._all_gather_records(mw) if self.world > 1 else [mw]
             from .engine import merge_merchant_windows
             self.last_windows = (uw, merge_merchant_windows(parts))
         if sink:
