@@ -1071,19 +1071,10 @@ int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t
       split_sizes[p] = send[p];
       split_sizes[G + p] = recv[p];
     }
-  // 2. records to their owners (forward stream), after the owner's previous use of this inbox slot
-  if (c.inbox_live[s]) FD_HIP(hipStreamWaitEvent(c.x_fwd, c.inbox_ev[s], 0));
-  c.inbox[s].ensure((size_t)std::max<int64_t>(m, 1) * sizeof(fd::RouteRecord));
-  c.res[s].ensure((size_t)std::max<int64_t>(m, 1) * sizeof(fd::ResultRecord));
-  fd::comm_exchange(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[s].ptr, recv, sizeof(fd::RouteRecord));
-  FD_HIP(hipEventRecord(c.in_ev[s], c.x_fwd));
-  // 3. the owner's features + scoring on the pipeline (features wait for the records), results on the engine stream
-  if (m)
-    pipe_step(e, params, slots, nullptr, present, nullptr, c.inbox[s].ptr, m, nullptr, nullptr, nullptr, nullptr,
-              nullptr, nullptr, c.res[s].ptr, c.in_ev[s]);
-  FD_HIP(hipEventRecord(c.inbox_ev[s], e.stream));  // the engine stream has passed this batch's scoring
-  c.inbox_live[s] = true;
-  // 4. the next batch's partition + counts, ahead, on the forward stream
+  // 2. the next batch's partition + counts, ahead, on the forward stream — queued BEFORE this batch's records,
+  // whose exchange waits for an inbox slot (the scoring two batches back): the counts then land while this batch
+  // is still being scored, and the next call's one host wait is already satisfied (measured on one GPU: with the
+  // counts queued after the records, the next call's features started only after this batch's forests)
   if (next) {
     const int ns = c.next_slot;
     c.next_slot ^= 1;
@@ -1093,6 +1084,18 @@ int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t
     c.pending_n = next_n;
     c.pending_slot = ns;
   }
+  // 3. records to their owners (forward stream), after the owner's previous use of this inbox slot
+  if (c.inbox_live[s]) FD_HIP(hipStreamWaitEvent(c.x_fwd, c.inbox_ev[s], 0));
+  c.inbox[s].ensure((size_t)std::max<int64_t>(m, 1) * sizeof(fd::RouteRecord));
+  c.res[s].ensure((size_t)std::max<int64_t>(m, 1) * sizeof(fd::ResultRecord));
+  fd::comm_exchange(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[s].ptr, recv, sizeof(fd::RouteRecord));
+  FD_HIP(hipEventRecord(c.in_ev[s], c.x_fwd));
+  // 4. the owner's features + scoring on the pipeline (features wait for the records), results on the engine stream
+  if (m)
+    pipe_step(e, params, slots, nullptr, present, nullptr, c.inbox[s].ptr, m, nullptr, nullptr, nullptr, nullptr,
+              nullptr, nullptr, c.res[s].ptr, c.in_ev[s]);
+  FD_HIP(hipEventRecord(c.inbox_ev[s], e.stream));  // the engine stream has passed this batch's scoring
+  c.inbox_live[s] = true;
   // 5. results back (reversed splits) and into arrival order, on the engine stream
   c.back_buf.ensure((size_t)std::max<int64_t>(n, 1) * sizeof(fd::ResultRecord));
   fd::comm_exchange(e, true, e.stream, c.res[s].ptr, recv, c.back_buf.ptr, send, sizeof(fd::ResultRecord));

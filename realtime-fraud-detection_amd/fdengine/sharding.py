@@ -458,14 +458,14 @@ class ShardedScorer:
         send, recv = p["host"].wait()  # the step's one host wait: split sizes exchanged ahead
         self.last_counts = (send, recv)
         m = sum(recv)
+        if prefetch is not None:  # the next batch's partition + counts first (as fd_sharded_step: DESIGN §7)
+            nt, nn = prefetch[0], prefetch[1]
+            self._pending = self._launch_counts(nt, nn, prefetch[2] if len(prefetch) > 2 else None)
         with be.fwd_ctx():
             inbox = torch.empty((m, REC), dtype=torch.uint8, device=p["rec"].device)
             self._a2a(inbox, p["rec"], recv, send)
             ready = be.forward_ready()
         res = be.score_records_async(inbox, m, ready)
-        if prefetch is not None:
-            nt, nn = prefetch[0], prefetch[1]
-            self._pending = self._launch_counts(nt, nn, prefetch[2] if len(prefetch) > 2 else None)
         back = torch.empty((n, RES), dtype=torch.uint8, device=res.device)
         self._a2a(back, res, send, recv, group="back")
         return be.scatter_results(back, n, sentinel=True)

@@ -75,5 +75,6 @@ for name in VARIANTS:
     eng.close()
     del w, parts
 for k in result:
-    print(f"{k} / direct = {result[k] / result['direct']:.3f}", flush=True)
+    if "direct" in result:
+        print(f"{k} / direct = {result[k] / result['direct']:.3f}", flush=True)
 dist.destroy_process_group()

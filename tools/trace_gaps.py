@@ -19,3 +19,15 @@ for s, e, name, q in win:
     gap = (s - last_end[q]) / 1000 if q in last_end else 0.0
     last_end[q] = e
     print(f"{(s - t0) / 1000:9.1f} {(e - t0) / 1000:9.1f} {(e - s) / 1000:7.1f}  qgap {gap:6.1f}  q{q} {nm}")
+
+# resources of each distinct kernel in the window (what co-residence with the fused kernel depends on)
+seen = {}
+for r in rows:
+    nm = r["Kernel_Name"].replace("void ", "").replace("fd::(anonymous namespace)::", "")[:40]
+    if nm in seen or not any(x in r["Kernel_Name"] for x in names):
+        continue
+    seen[nm] = {c: r[c] for c in r if any(t in c.lower() for t in ("lds", "vgpr", "sgpr", "workgroup", "grid",
+                                                                   "scratch", "accum"))}
+for nm, v in seen.items():
+    print(f"{nm:40s} {v}")
+
