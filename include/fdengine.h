@@ -440,11 +440,12 @@ int fd_score_records_pipelined(fd_engine* eng, const fd_blend_params* params, co
    RCCL once (the process's librccl.so, by path), rank 0 makes two unique ids (fd_comm_unique_id), the host
    broadcasts them, every rank calls fd_comm_init (collective, blocking). fd_sharded_step then runs one
    micro-batch: its split sizes (exchanged by the previous call when it prefetched this batch, else now: the
-   step's one host wait), the records to their owners (grouped ncclSend/ncclRecv with per-peer counts, on
-   the engine's forward stream), the owner's features + scoring (fd_score_records_pipelined's pipeline, the
-   features waiting for the records), the next batch's partition and count exchange (`next`, optional:
-   prefetch), the results back (second communicator, engine stream) and into arrival order in the caller's
-   outputs, written on the engine stream. Every rank makes the same calls in the same order (the same
+   step's one host wait), the next batch's partition and count exchange (`next`, optional: prefetch; queued on
+   the forward stream ahead of this batch's records, so they land while this batch is scored), the records to
+   their owners (grouped ncclSend/ncclRecv with per-peer counts, on the engine's forward stream), the owner's
+   features + scoring (fd_score_records_pipelined's pipeline, the features waiting for the records), the
+   results back (second communicator, engine stream) and into arrival order in the caller's outputs (device or
+   host-mapped memory), written on the engine stream. Every rank makes the same calls in the same order (the same
    prefetch pattern). split_sizes (optional): the 2 x world send / receive counts of this batch. */
 int fd_comm_unique_id(const char* rccl_path, uint8_t* id_out /* 128 bytes */);
 int fd_comm_init(fd_engine* eng, const char* rccl_path, int32_t rank, int32_t world, const uint8_t* id_fwd,
