@@ -652,10 +652,18 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      (default) all on the engine stream (no cross-queue hops; config 5 0.088 ms per 1 k step), 1 the LSTM and the
      forests after the first on one side stream (0.095), 2 on two side streams (0.095)
      "pipeline_lean": fd_score_batch_pipelined's bucket pass, 1 (default) the lean kernel that fits beside the
-     fused ensemble kernel, 0 the full bucket kernel */
+     fused ensemble kernel, 0 the full bucket kernel
+     "sharded_fwd_thread": fd_sharded_step with `next`, 1 (default) the next batch's forward half (partition,
+     count exchange, split-size wait, records exchange) on a worker thread of the engine's while the caller's
+     thread launches this batch's scoring and results; 0 all on the caller's thread. Every rank must use the same
+     value (it orders the forward communicator's operations); fd_engine_sync waits for the worker's job. */
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
 /* Engine counters (diagnostics): "pipelined_batches" (batches through fd_score_batch_pipelined /
-   fd_score_records_pipelined so far). */
+   fd_score_records_pipelined so far), "sharded_steps" (fd_sharded_step calls) and "sharded_host_ns_<phase>" (host
+   nanoseconds inside fd_sharded_step by phase: "wait" the split sizes, "partition" / "counts" / "count_copy" the
+   next batch's route kernels, count exchange and copy to the host, "records" the records exchange, "score" the
+   owner's pipeline launches, "back" / "scatter" the results exchange and the scatter into arrival order, "join"
+   the caller waiting for the forward worker; the worker's phases are its own thread's time). */
 int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value);
 int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches);
 int fd_timing_reset(fd_engine* eng);

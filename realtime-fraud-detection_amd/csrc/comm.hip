@@ -71,6 +71,24 @@ const RcclApi& rccl(const char* path) {
 void check(const RcclApi& R, ncclResult_t r, const char* what) {
   if (r != ncclSuccess) throw Error(FD_ERR_HIP, std::string(what) + ": " + R.error_string(r));
 }
+
+constexpr size_t kCntSeqOff = 2 * FD_MAX_SHARDS * sizeof(int64_t);  // the sequence word after the counts
+constexpr size_t kCntBytes = kCntSeqOff + 64;
+
+// the exchanged counts (send [G], receive [G]) into the slot's coherent host buffer, then its sequence word: one
+// lane per count, each store made visible system-wide before the workgroup barrier, the sequence stored last (the
+// host polls it instead of an event: a D2H copy + event wait measured ~70 us from the exchange to the host)
+__global__ void __launch_bounds__(128)
+count_publish_kernel(const int64_t* __restrict__ cnt, int n2, int64_t* h, unsigned long long* h_seq,
+                     unsigned long long seq) {
+  const int i = (int)threadIdx.x;
+  if (i < n2) {
+    __hip_atomic_store(h + i, cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+  }
+  __syncthreads();
+  if (i == 0) __hip_atomic_store(h_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 }  // namespace
 
 void comm_unique_id(const char* rccl_path, uint8_t* out) {
@@ -99,8 +117,12 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
   c.world = world;
   if (!c.x_fwd) FD_HIP(hipStreamCreateWithFlags(&c.x_fwd, hipStreamNonBlocking));
   for (int s = 0; s < 2; ++s) {
-    if (!c.h_cnt[s]) FD_HIP(hipHostMalloc(reinterpret_cast<void**>(&c.h_cnt[s]), 2 * FD_MAX_SHARDS * sizeof(int64_t)));
-    if (!c.cnt_ev[s]) FD_HIP(hipEventCreateWithFlags(&c.cnt_ev[s], hipEventDisableTiming));  // the host reads
+    if (!c.h_cnt[s]) {
+      FD_HIP(hipHostMalloc(reinterpret_cast<void**>(&c.h_cnt[s]), kCntBytes, hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(c.h_cnt[s], 0, kCntBytes);
+      c.cnt_seq[s] = 0;
+      FD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c.d_hcnt[s]), c.h_cnt[s], 0));
+    }
     if (!c.in_ev[s]) FD_HIP(hipEventCreateWithFlags(&c.in_ev[s], hipEventDisableTiming | hipEventDisableSystemFence));
     if (!c.inbox_ev[s])
       FD_HIP(hipEventCreateWithFlags(&c.inbox_ev[s], hipEventDisableTiming | hipEventDisableSystemFence));
@@ -108,11 +130,91 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
   }
   c.pending = false;
   c.next_slot = 0;
+  c.sent[0] = c.sent[1] = false;  // (the count buffers keep their sequence numbers across communicators)
+  FD_HIP(hipGetDevice(&c.device));
   c.ready = true;
+}
+
+namespace {
+// the forward worker: one job at a time (comm_post_forward), errors kept for comm_join
+void forward_worker(Engine* ep) {
+  Engine& e = *ep;
+  ShardComm& c = e.comm;
+  (void)hipSetDevice(c.device);  // the HIP device is per host thread
+  std::unique_lock<std::mutex> lk(c.fwd_mu);
+  for (;;) {
+    c.fwd_cv.wait(lk, [&] { return c.fwd_quit || c.fwd_busy; });
+    if (c.fwd_quit) return;
+    const ShardComm::FwdJob j = c.fwd_job;
+    lk.unlock();
+    int code = 0;
+    std::string msg;
+    try {
+      HostLaps L{c};
+      comm_launch_counts(e, j.t, j.n, j.ready, j.slot, L);
+      comm_wait_counts(e, j.slot, j.n, L);
+      comm_send_records(e, j.slot, L);
+    } catch (const Error& x) {
+      code = x.code;
+      msg = x.what();
+    } catch (const std::exception& x) {
+      code = FD_ERR_HIP;
+      msg = x.what();
+    }
+    lk.lock();
+    if (code == 0) c.sent[j.slot] = true;
+    c.fwd_err = code;
+    c.fwd_err_msg = msg;
+    c.fwd_busy = false;
+    c.fwd_cv.notify_all();
+  }
+}
+
+void stop_worker(ShardComm& c) {
+  if (!c.fwd_thr.joinable()) return;
+  {
+    std::lock_guard<std::mutex> lk(c.fwd_mu);
+    c.fwd_quit = true;
+  }
+  c.fwd_cv.notify_all();
+  c.fwd_thr.join();  // a job in flight finishes first (the worker only checks quit between jobs)
+  c.fwd_quit = false;
+  c.fwd_busy = false;
+}
+}  // namespace
+
+void comm_join(Engine& e) {
+  ShardComm& c = e.comm;
+  if (!c.fwd_thr.joinable()) return;
+  std::unique_lock<std::mutex> lk(c.fwd_mu);
+  c.fwd_cv.wait(lk, [&] { return !c.fwd_busy; });
+  if (c.fwd_err) {
+    const int code = c.fwd_err;
+    const std::string msg = c.fwd_err_msg;
+    c.fwd_err = 0;
+    throw Error(code, "sharded step, forward worker: " + msg);
+  }
+}
+
+void comm_post_forward(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot) {
+  ShardComm& c = e.comm;
+  if (!c.fwd_thr.joinable()) c.fwd_thr = std::thread(forward_worker, &e);
+  {
+    std::lock_guard<std::mutex> lk(c.fwd_mu);
+    FD_REQUIRE(!c.fwd_busy, FD_ERR_INVALID_ARG, "forward worker busy (join first)");
+    c.fwd_job.t = t;
+    c.fwd_job.n = n;
+    c.fwd_job.ready = ready;
+    c.fwd_job.slot = slot;
+    c.sent[slot] = false;
+    c.fwd_busy = true;
+  }
+  c.fwd_cv.notify_all();
 }
 
 void comm_destroy(Engine& e) {
   ShardComm& c = e.comm;
+  stop_worker(c);
   if (c.x_fwd) (void)hipStreamSynchronize(c.x_fwd);
   (void)hipStreamSynchronize(e.stream);
   if (c.ready) {
@@ -124,13 +226,14 @@ void comm_destroy(Engine& e) {
   for (int s = 0; s < 2; ++s) {
     for (auto* b : {&c.rec[s], &c.cnt[s], &c.inbox[s], &c.res[s]}) b->release();
     if (c.h_cnt[s]) (void)hipHostFree(c.h_cnt[s]);
-    if (c.cnt_ev[s]) (void)hipEventDestroy(c.cnt_ev[s]);
     if (c.in_ev[s]) (void)hipEventDestroy(c.in_ev[s]);
     if (c.inbox_ev[s]) (void)hipEventDestroy(c.inbox_ev[s]);
-    c.h_cnt[s] = nullptr;
-    c.cnt_ev[s] = c.in_ev[s] = c.inbox_ev[s] = nullptr;
+    c.h_cnt[s] = c.d_hcnt[s] = nullptr;
+    c.in_ev[s] = c.inbox_ev[s] = nullptr;
   }
   c.back_buf.release();
+  c.route_blk.release();
+  c.sent[0] = c.sent[1] = false;
   if (c.x_fwd) (void)hipStreamDestroy(c.x_fwd);
   c.x_fwd = nullptr;
   c.ready = false;
@@ -138,8 +241,8 @@ void comm_destroy(Engine& e) {
 }
 
 // partition `t` by owner on the forward stream, exchange the per-owner counts (send[p] to peer p, recv[p] from
-// it: one int64 each way per peer), both count vectors to pinned host memory behind cnt_ev[s]
-void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int s) {
+// it: one int64 each way per peer), both count vectors published to the slot's host buffer (count_publish_kernel)
+void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int s, HostLaps& L) {
   ShardComm& c = e.comm;
   const RcclApi& R = rccl(nullptr);
   const int G = c.world;
@@ -147,7 +250,8 @@ void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t 
   c.rec[s].ensure((size_t)std::max<int64_t>(n, 1) * sizeof(RouteRecord));
   c.cnt[s].ensure(2 * (size_t)G * sizeof(int64_t));
   int64_t* cnt = c.cnt[s].as<int64_t>();
-  launch_route_partition(e, t, nullptr, n, G, c.rec[s].ptr, cnt, c.x_fwd, &e.route_blk_stream);
+  launch_route_partition(e, t, nullptr, n, G, c.rec[s].ptr, cnt, c.x_fwd, &c.route_blk, /*timed=*/false);
+  L(1);
   const ncclComm_t f = static_cast<ncclComm_t>(c.fwd);
   check(R, R.group_start(), "ncclGroupStart");
   for (int p = 0; p < G; ++p) {
@@ -155,8 +259,59 @@ void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t 
     check(R, R.recv(cnt + G + p, 1, ncclInt64, p, f, c.x_fwd), "ncclRecv (counts)");
   }
   check(R, R.group_end(), "ncclGroupEnd (counts)");
-  FD_HIP(hipMemcpyAsync(c.h_cnt[s], cnt, 2 * (size_t)G * sizeof(int64_t), hipMemcpyDeviceToHost, c.x_fwd));
-  FD_HIP(hipEventRecord(c.cnt_ev[s], c.x_fwd));
+  L(2);
+  const unsigned long long seq = ++c.cnt_seq[s];
+  auto* dseq = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(c.d_hcnt[s]) + kCntSeqOff);
+  hipLaunchKernelGGL(count_publish_kernel, dim3(1), dim3(128), 0, c.x_fwd, cnt, 2 * G, c.d_hcnt[s], dseq, seq);
+  FD_HIP(hipGetLastError());
+  L(3);
+}
+
+// the host wait for slot s's counts, checked against the batch size n, into split[s]
+void comm_wait_counts(Engine& e, int s, int64_t n, HostLaps& L) {
+  ShardComm& c = e.comm;
+  const int G = c.world;
+  // poll the slot's sequence word; every 4096 polls ask the stream: an error ends the wait, and an idle stream
+  // with the word still behind means the publish was lost
+  const auto* hseq = reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(c.h_cnt[s]) + kCntSeqOff);
+  const unsigned long long want = c.cnt_seq[s];
+  for (unsigned spins = 1; __atomic_load_n(hseq, __ATOMIC_ACQUIRE) != want; ++spins) {
+    __builtin_ia32_pause();
+    if ((spins & 4095u) == 0) {
+      const hipError_t q = hipStreamQuery(c.x_fwd);
+      if (q == hipSuccess) {
+        FD_REQUIRE(__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == want, FD_ERR_HIP, "split sizes never arrived");
+        break;
+      }
+      FD_REQUIRE(q == hipErrorNotReady, FD_ERR_HIP, std::string("count exchange: ") + hipGetErrorString(q));
+      if (spins > (1u << 20)) std::this_thread::yield();
+    }
+  }
+  int64_t sent = 0;
+  for (int p = 0; p < 2 * G; ++p) {
+    const int64_t v = __atomic_load_n(&c.h_cnt[s][p], __ATOMIC_RELAXED);
+    FD_REQUIRE(v >= 0, FD_ERR_HIP, "corrupt split sizes");
+    c.split[s][p] = v;
+    if (p < G) sent += v;
+  }
+  FD_REQUIRE(sent == n, FD_ERR_HIP, "split sizes do not add up to the batch");
+  L(0);
+}
+
+// slot s's records to their owners on the forward stream, after the owner's previous use of that inbox slot
+void comm_send_records(Engine& e, int s, HostLaps& L) {
+  ShardComm& c = e.comm;
+  const int G = c.world;
+  const int64_t* send = c.split[s];
+  const int64_t* recv = c.split[s] + G;
+  int64_t m = 0;
+  for (int p = 0; p < G; ++p) m += recv[p];
+  if (c.inbox_live[s]) FD_HIP(hipStreamWaitEvent(c.x_fwd, c.inbox_ev[s], 0));
+  c.inbox[s].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(RouteRecord));
+  c.res[s].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(ResultRecord));
+  comm_exchange(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[s].ptr, recv, sizeof(RouteRecord));
+  FD_HIP(hipEventRecord(c.in_ev[s], c.x_fwd));
+  L(4);
 }
 
 // uneven all-to-all of `elem`-byte items: send[p] items (consecutive in sendbuf, peers in rank order) to peer p,

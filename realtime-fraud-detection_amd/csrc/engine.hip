@@ -2,6 +2,7 @@
 // Every entry point catches everything: status codes + a thread-local message cross the ABI,
 // exceptions never do (mirrors the reference's log-and-raise contract, ml/models/model_manager.py:302-307,
 // with the raise done by the Python shim).
+#include <chrono>
 #include <mutex>
 #include <cstring>
 #include <string>
@@ -261,6 +262,10 @@ int fd_engine_destroy(fd_engine* eng) {
   if (!eng) return FD_OK;
   { FD_ENGINE_LOCK(eng); }  // wait for a call in flight on another thread (destroying while in use is the caller's bug)
   Engine& e = E(eng);
+  try {
+    fd::comm_join(e);  // the sharded step's forward worker is idle from here (stopped by comm_destroy below)
+  } catch (...) {
+  }
   (void)hipStreamSynchronize(e.stream);
   for (auto& f : e.forests) {
     for (auto* b : {&f.split.bins, &f.split.nan, &f.split.leaves}) b->release();
@@ -367,7 +372,9 @@ int fd_engine_sync(fd_engine* eng) {
   FD_API_BEGIN
   FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
+  fd::comm_join(e);  // the sharded step's forward worker has queued its job
   FD_HIP(hipStreamSynchronize(e.stream));
+  if (e.comm.x_fwd) FD_HIP(hipStreamSynchronize(e.comm.x_fwd));
   for (hipStream_t st : e.pipe_stream)
     if (st) FD_HIP(hipStreamSynchronize(st));
   if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
@@ -392,6 +399,13 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
   const std::string k(key);
   if (k == "pipelined_batches") {  // fd_score_batch_pipelined / fd_score_records_pipelined batches so far
     *value = (int64_t)e.pipe_iter_total;
+  } else if (k == "sharded_steps") {  // fd_sharded_step calls so far
+    *value = (int64_t)e.comm.steps.load();
+  } else if (k.rfind("sharded_host_ns_", 0) == 0) {  // host time inside fd_sharded_step by phase
+    int i = 0;
+    while (i < fd::ShardComm::kHostPhases && k.compare(16, std::string::npos, fd::kShardHostPhase[i]) != 0) ++i;
+    FD_REQUIRE(i < fd::ShardComm::kHostPhases, FD_ERR_INVALID_ARG, "unknown counter: " + k);
+    *value = (int64_t)e.comm.host_ns[i].load();
   } else {
     FD_REQUIRE(false, FD_ERR_INVALID_ARG, "unknown counter: " + k);
   }
@@ -421,6 +435,12 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "small_streams") {  // latency batches: 2 LSTM | other forests on two side streams, 1 one, 0 none
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "small_streams must be 0, 1 or 2");
     e.small_streams = (int)value;
+  } else if (k == "sharded_fwd_thread") {  // fd_sharded_step: 1 (default) the next batch's forward half on the
+    // engine's worker thread, 0 all on the caller's thread (every rank must use the same value: it orders the
+    // forward communicator's operations)
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "sharded_fwd_thread must be 0 or 1");
+    fd::comm_join(e);
+    e.comm.fwd_thread_on = value != 0;
   } else if (k == "timing_every") {  // kernel timing (fd_timing_*): HIP events on one launch in N of each kind
     FD_REQUIRE(value >= 1 && value <= 1000000, FD_ERR_INVALID_ARG, "timing_every must be >= 1");
     e.timing_every = (int)value;
@@ -1045,61 +1065,66 @@ int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t
                "routed scoring needs every present model in a forest slot or FD_SLOT_LSTM");
   FD_REQUIRE(n == 0 || d_fraud_prob, FD_ERR_INVALID_ARG, "null fraud_prob output");
   const int G = c.world;
-  // 1. this batch's split sizes: exchanged by the previous step (prefetch) or now
+  fd::HostLaps L{c};
+  c.steps.fetch_add(1, std::memory_order_relaxed);
+  fd::comm_join(e);  // the forward worker's job (this batch's forward half, when it was prefetched)
+  L(8);
+  // 1. this batch's split sizes (and records): exchanged by the previous step (prefetch) or now
   int s;
+  bool have;
   if (c.pending && c.pending_key == (const void*)txns->card_key && c.pending_n == n) {
     s = c.pending_slot;
+    have = c.sent[s];  // the worker also queued its records
   } else {  // no prefetch, or another batch than the prefetched one (whose exchange is dropped on every rank)
     s = c.next_slot;
     c.next_slot ^= 1;
-    fd::comm_launch_counts(e, *txns, n, static_cast<hipEvent_t>(input_ready), s);
+    c.sent[s] = false;
+    fd::comm_launch_counts(e, *txns, n, static_cast<hipEvent_t>(input_ready), s, L);
+    have = false;
   }
   c.pending = false;
-  FD_HIP(hipEventSynchronize(c.cnt_ev[s]));  // the step's one host wait
-  int64_t send[FD_MAX_SHARDS], recv[FD_MAX_SHARDS];
-  int64_t m = 0, sent = 0;
-  for (int p = 0; p < G; ++p) {
-    send[p] = c.h_cnt[s][p];
-    recv[p] = c.h_cnt[s][G + p];
-    FD_REQUIRE(send[p] >= 0 && recv[p] >= 0, FD_ERR_HIP, "corrupt split sizes");
-    m += recv[p];
-    sent += send[p];
-  }
-  FD_REQUIRE(sent == n, FD_ERR_HIP, "split sizes do not add up to the batch");
+  if (!have) fd::comm_wait_counts(e, s, n, L);  // the step's one host wait (none when the worker did it)
+  const int64_t* send = c.split[s];
+  const int64_t* recv = c.split[s] + G;
   if (split_sizes)
-    for (int p = 0; p < G; ++p) {
-      split_sizes[p] = send[p];
-      split_sizes[G + p] = recv[p];
-    }
-  // 2. the next batch's partition + counts, ahead, on the forward stream — queued BEFORE this batch's records,
-  // whose exchange waits for an inbox slot (the scoring two batches back): the counts then land while this batch
-  // is still being scored, and the next call's one host wait is already satisfied (measured on one GPU: with the
-  // counts queued after the records, the next call's features started only after this batch's forests)
+    for (int p = 0; p < 2 * G; ++p) split_sizes[p] = c.split[s][p];
+  int64_t m = 0;
+  for (int p = 0; p < G; ++p) m += recv[p];
+  // 2. without the worker: the next batch's partition + counts, ahead, on the forward stream — queued BEFORE this
+  // batch's records, whose exchange waits for an inbox slot (the scoring two batches back): the counts then land
+  // while this batch is still being scored, and the next call's one host wait is already satisfied (measured on
+  // one GPU: with the counts queued after the records, the next call's features started only after this batch's
+  // forests)
+  const bool worker = c.fwd_thread_on && next != nullptr;
+  int ns = -1;
   if (next) {
-    const int ns = c.next_slot;
+    ns = c.next_slot;
     c.next_slot ^= 1;
-    fd::comm_launch_counts(e, *next, next_n, static_cast<hipEvent_t>(next_ready), ns);
+    c.sent[ns] = false;
     c.pending = true;
     c.pending_key = next->card_key;
     c.pending_n = next_n;
     c.pending_slot = ns;
+    if (!worker) fd::comm_launch_counts(e, *next, next_n, static_cast<hipEvent_t>(next_ready), ns, L);
   }
   // 3. records to their owners (forward stream), after the owner's previous use of this inbox slot
-  if (c.inbox_live[s]) FD_HIP(hipStreamWaitEvent(c.x_fwd, c.inbox_ev[s], 0));
-  c.inbox[s].ensure((size_t)std::max<int64_t>(m, 1) * sizeof(fd::RouteRecord));
-  c.res[s].ensure((size_t)std::max<int64_t>(m, 1) * sizeof(fd::ResultRecord));
-  fd::comm_exchange(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[s].ptr, recv, sizeof(fd::RouteRecord));
-  FD_HIP(hipEventRecord(c.in_ev[s], c.x_fwd));
+  if (!have) fd::comm_send_records(e, s, L);
+  // with the worker: the next batch's whole forward half (partition, counts, its host wait, records) on the worker
+  // thread from here on, while this thread launches this batch's scoring and results
+  if (worker) fd::comm_post_forward(e, *next, next_n, static_cast<hipEvent_t>(next_ready), ns);
   // 4. the owner's features + scoring on the pipeline (features wait for the records), results on the engine stream
   if (m)
     pipe_step(e, params, slots, nullptr, present, nullptr, c.inbox[s].ptr, m, nullptr, nullptr, nullptr, nullptr,
               nullptr, nullptr, c.res[s].ptr, c.in_ev[s]);
   FD_HIP(hipEventRecord(c.inbox_ev[s], e.stream));  // the engine stream has passed this batch's scoring
   c.inbox_live[s] = true;
+  L(5);
   // 5. results back (reversed splits) and into arrival order, on the engine stream
-  c.back_buf.ensure((size_t)std::max<int64_t>(n, 1) * sizeof(fd::ResultRecord));
+  c.back_buf.ensure_headroom((size_t)std::max<int64_t>(n, 1) * sizeof(fd::ResultRecord));
   fd::comm_exchange(e, true, e.stream, c.res[s].ptr, recv, c.back_buf.ptr, send, sizeof(fd::ResultRecord));
+  L(6);
   if (n) fd::launch_result_scatter(e, c.back_buf.ptr, n, d_fraud_prob, d_confidence, d_decision, d_risk);
+  L(7);
   FD_API_END
 }
 

@@ -52,8 +52,8 @@ void forest_loaded(PackedForest& pf, const fd_forest_params& p, const fd_tree_ar
 namespace {
 
 constexpr int kEnsWG = 1024;
-constexpr int kCHA = 24;  // XGBoost trees per chunk (TPG 6)
-constexpr int kCHB = 16;  // IsolationForest trees per chunk (TPG 4)
+constexpr int kCHA = 20;  // XGBoost trees per chunk (TPG 5)
+constexpr int kCHB = 12;  // IsolationForest trees per chunk (TPG 3)
 constexpr int kMaxPass = 64;
 
 // A chunk in LDS: CH node blocks of 1 KiB (walk_ens link addressing), then the CH trees' leaf values

@@ -4,10 +4,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdint>
+#include <mutex>
 #include <stdexcept>
 #include <string>
-#include <atomic>
+#include <thread>
 #include <vector>
 
 #include "fdengine.h"
@@ -53,6 +57,11 @@ struct DeviceBuffer {
     release();
     FD_HIP(hipMalloc(&ptr, need));
     bytes = need;
+  }
+  // grow by a quarter more than asked: buffers sized per batch by a count that wanders (a shard's inbox) then
+  // reallocate O(log) times instead of at every new maximum (hipFree waits for the device)
+  void ensure_headroom(size_t need) {
+    if (need > bytes) ensure(need + need / 4);
   }
   void release() {
     if (ptr) (void)hipFree(ptr);
@@ -277,13 +286,60 @@ struct ShardComm {
   void* back = nullptr;  // ncclComm_t: results, on the engine stream
   hipStream_t x_fwd = nullptr;
   DeviceBuffer rec[2], cnt[2], inbox[2], res[2], back_buf;
-  int64_t* h_cnt[2] = {nullptr, nullptr};  // pinned: send counts [G] then receive counts [G]
-  hipEvent_t cnt_ev[2] = {}, in_ev[2] = {}, inbox_ev[2] = {};
+  DeviceBuffer route_blk;                  // the partition's block counts (x_fwd)
+  // coherent host-mapped memory per slot: send counts [G], receive counts [G] (FD_MAX_SHARDS each), then a u64
+  // sequence word; count_publish_kernel writes the counts and then the sequence, the host polls the sequence
+  int64_t* h_cnt[2] = {nullptr, nullptr};
+  int64_t* d_hcnt[2] = {nullptr, nullptr};  // the same buffers' device addresses
+  unsigned long long cnt_seq[2] = {0, 0};  // the sequence the slot's latest publish writes
+  hipEvent_t in_ev[2] = {}, inbox_ev[2] = {};
   bool inbox_live[2] = {};
   bool pending = false;  // a prefetched batch's counts are in flight (slot pending_slot)
   const void* pending_key = nullptr;
   int64_t pending_n = 0;
   int pending_slot = 0, next_slot = 0;
+  // a slot whose records exchange is queued (by the forward worker): its checked split sizes, send [G] then recv [G]
+  bool sent[2] = {};
+  int64_t split[2][2 * FD_MAX_SHARDS] = {};
+  // The forward worker (engine option "sharded_fwd_thread", default on): a host thread of the engine's runs the
+  // NEXT batch's forward half — partition, count exchange, split-size wait, records exchange, all on x_fwd and the
+  // fwd communicator — while the caller's thread launches this batch's scoring, results and scatter (engine
+  // stream, back communicator). Either half is ~60 us of HIP / RCCL host calls; serial they were ~120 us per
+  // step, above the GPU's ~90. One job at a time; the caller joins it before touching the forward half again.
+  bool fwd_thread_on = true;
+  std::thread fwd_thr;
+  std::mutex fwd_mu;
+  std::condition_variable fwd_cv;
+  bool fwd_quit = false, fwd_busy = false;
+  struct FwdJob {
+    fd_txn_batch t{};
+    int64_t n = 0;
+    hipEvent_t ready = nullptr;
+    int slot = 0;
+  } fwd_job;
+  int fwd_err = 0;
+  std::string fwd_err_msg;
+  int device = 0;
+  // host time inside fd_sharded_step by phase (ns, counters "sharded_host_ns_<phase>", kShardHostPhase order;
+  // the forward worker's phases are its own thread's time)
+  static constexpr int kHostPhases = 9;
+  std::atomic<unsigned long long> steps{0}, host_ns[kHostPhases] = {};
+};
+// "wait": the split sizes; "partition", "counts", "count_copy": a batch's route kernels, count exchange and copy to
+// the host; "records": the records exchange; "score": the owner's pipeline; "back", "scatter": results; "join": the
+// caller waiting for the forward worker's job
+inline const char* const kShardHostPhase[ShardComm::kHostPhases] = {
+    "wait", "partition", "counts", "count_copy", "records", "score", "back", "scatter", "join"};
+// per-thread phase clock: lap(ph) adds the time since the previous lap to phase ph
+struct HostLaps {
+  ShardComm& c;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void operator()(int ph) {
+    const auto now = std::chrono::steady_clock::now();
+    c.host_ns[ph].fetch_add((unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count(),
+                            std::memory_order_relaxed);
+    t = now;
+  }
 };
 
 inline int64_t floor_div_host(int64_t a, int64_t b) {
@@ -428,7 +484,7 @@ unsigned shard_of_host(unsigned long long key, unsigned G);
 // stream / scratch: the launch stream and block-count scratch (default: the engine stream and route_blk)
 void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_inputs* extra, int64_t n, int G,
                             void* d_records, int64_t* d_counts, hipStream_t stream = nullptr,
-                            DeviceBuffer* scratch = nullptr);
+                            DeviceBuffer* scratch = nullptr, bool timed = true);
 void launch_route_unpack(Engine& e, const void* d_records, const void* d_results, int64_t n, const fd_txn_batch& out,
                          uint8_t* pm, uint8_t* fraud, double* score);
 void launch_result_pack(Engine& e, const double* fp, const double* conf, const uint8_t* dec, const uint8_t* risk,
@@ -440,7 +496,11 @@ void route_check(Engine& e);
 void comm_unique_id(const char* rccl_path, uint8_t* out);
 void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint8_t* id_fwd, const uint8_t* id_back);
 void comm_destroy(Engine& e);
-void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot);
+void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot, HostLaps& L);
+void comm_wait_counts(Engine& e, int slot, int64_t n, HostLaps& L);  // host wait; split[slot] checked
+void comm_send_records(Engine& e, int slot, HostLaps& L);            // records exchange behind the inbox slot
+void comm_post_forward(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot);  // to the worker
+void comm_join(Engine& e);  // wait for the worker's job; rethrows its error
 void comm_exchange(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,
                    const int64_t* recv, size_t elem);
 // lstm.hip

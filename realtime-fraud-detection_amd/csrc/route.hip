@@ -203,7 +203,8 @@ unsigned shard_of_host(unsigned long long key, unsigned G) {
 }
 
 void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_inputs* extra, int64_t n, int G,
-                            void* d_records, int64_t* d_counts, hipStream_t stream, DeviceBuffer* scratch) {
+                            void* d_records, int64_t* d_counts, hipStream_t stream, DeviceBuffer* scratch,
+                            bool timed) {
   const hipStream_t st = stream ? stream : e.stream;
   DeviceBuffer& blk = scratch ? *scratch : e.route_blk;
   FD_REQUIRE(G >= 1 && G <= FD_MAX_SHARDS, FD_ERR_INVALID_ARG, "n_shards must be in [1, 64]");
@@ -219,7 +220,7 @@ void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_in
              FD_ERR_INVALID_ARG, "incomplete transaction batch");
   const int nblk = (int)((n + kRouteBlock - 1) / kRouteBlock);
   blk.ensure((size_t)G * nblk * sizeof(int));
-  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_ROUTE) : nullptr;
+  Engine::Timed* ev = e.timing && timed ? e.next_event_pair(FD_TIMING_ROUTE) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, st));
   const auto* key = reinterpret_cast<const unsigned long long*>(t.card_key);
   hipLaunchKernelGGL(route_count_kernel, dim3(nblk), dim3(kRouteBlock), 0, st, key, n, (unsigned)G, nblk,

@@ -68,7 +68,7 @@ class FraudEngine:
         N.call("fd_engine_set_option", self._h, key.encode(), int(value))
 
     def counter(self, key: str) -> int:
-        """fd_engine_get_counter: "pipelined_batches"."""
+        """fd_engine_get_counter: "pipelined_batches", "sharded_steps", "sharded_host_ns_<phase>" (include/fdengine.h)."""
         v = N._i64()
         N.call("fd_engine_get_counter", self._h, key.encode(), C.byref(v))
         return int(v.value)

@@ -37,10 +37,14 @@ while cap < int(CARDS * 1.6) + 65536:
 result = {}
 VARIANTS = os.environ.get("VARIANTS", "direct,native,streaming,serial").split(",")
 for name in VARIANTS:
+    fwd_thread = 0 if name.endswith("_nothread") else 1  # native_nothread: fd_sharded_step all on this thread
+    name_v = name
+    name = name.removesuffix("_nothread")
     routed = name != "direct"
     eng = fdengine.FraudEngine(0)
     eng.state_init(cap, 1, 16)
     eng.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
+    eng.set_option("sharded_fwd_thread", fwd_thread)
     sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), 0, 1, force_route=routed,
                        streaming=name != "serial", native=name == "native")
     w = synth_gpu.warm_workload(eng, dev, CARDS, 0, 1, STEPS + 20, B, hours=12.0, keep_batches=0)
@@ -55,14 +59,21 @@ for name in VARIANTS:
 
     run(0, 20)
     torch.cuda.synchronize()
+    PH = ("wait", "partition", "counts", "count_copy", "records", "score", "back", "scatter", "join")
+    c0 = {ph: eng.counter("sharded_host_ns_" + ph) for ph in PH} if name == "native" else None
+    k0 = eng.counter("sharded_steps") if name == "native" else 0
     t0 = time.perf_counter()
     run(20, 20 + STEPS)
     t_host = time.perf_counter()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / STEPS * 1e3
-    result[name] = ms
-    print(f"{name}: {ms:.4f} ms/step back to back ({B / ms / 1e3:.1f} M txn/s), host submit "
+    result[name_v] = ms
+    print(f"{name_v}: {ms:.4f} ms/step back to back ({B / ms / 1e3:.1f} M txn/s), host submit "
           f"{(t_host - t0) / STEPS * 1e3:.4f} ms/step", flush=True)
+    if name == "native":  # the timed steps only
+        k = eng.counter("sharded_steps") - k0
+        print("  host us/step inside fd_sharded_step: " + ", ".join(
+            f"{ph} {(eng.counter('sharded_host_ns_' + ph) - c0[ph]) / k / 1e3:.1f}" for ph in PH), flush=True)
     if os.environ.get("PROFILE_HOST") and routed:
         import cProfile
         import pstats
