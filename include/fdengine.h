@@ -656,7 +656,11 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      "sharded_fwd_thread": fd_sharded_step with `next`, 1 (default) the next batch's forward half (partition,
      count exchange, split-size wait, records exchange) on a worker thread of the engine's while the caller's
      thread launches this batch's scoring and results; 0 all on the caller's thread. Every rank must use the same
-     value (it orders the forward communicator's operations); fd_engine_sync waits for the worker's job. */
+     value (it orders the forward communicator's operations); fd_engine_sync waits for the worker's job.
+     "stream_priority": HIP priorities of the engine's pipeline and forward streams (ROCm keeps a hardware-queue
+     pool per priority, so they stop sharing queues with the engine stream and RCCL's streams): 0 all default, 1
+     the two pipeline streams high, 2 + the forward stream low, 3 (default) + the forward stream high. Set before
+     the first pipelined call and fd_comm_init. */
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
 /* Engine counters (diagnostics): "pipelined_batches" (batches through fd_score_batch_pipelined /
    fd_score_records_pipelined so far), "sharded_steps" (fd_sharded_step calls) and "sharded_host_ns_<phase>" (host

@@ -78,13 +78,15 @@ constexpr size_t kCntBytes = kCntSeqOff + 64;
 // the exchanged counts (send [G], receive [G]) into the slot's coherent host buffer, then its sequence word: one
 // lane per count, each store made visible system-wide before the workgroup barrier, the sequence stored last (the
 // host polls it instead of an event: a D2H copy + event wait measured ~70 us from the exchange to the host)
+// The send half is zeroed behind it for the slot's next route_count (which adds its totals into it).
 __global__ void __launch_bounds__(128)
-count_publish_kernel(const int64_t* __restrict__ cnt, int n2, int64_t* h, unsigned long long* h_seq,
+count_publish_kernel(int64_t* __restrict__ cnt, int G, int64_t* h, unsigned long long* h_seq,
                      unsigned long long seq) {
   const int i = (int)threadIdx.x;
-  if (i < n2) {
+  if (i < 2 * G) {
     __hip_atomic_store(h + i, cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __threadfence_system();
+    if (i < G) cnt[i] = 0;
   }
   __syncthreads();
   if (i == 0) __hip_atomic_store(h_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -115,7 +117,7 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
   c.back = k;
   c.rank = rank;
   c.world = world;
-  if (!c.x_fwd) FD_HIP(hipStreamCreateWithFlags(&c.x_fwd, hipStreamNonBlocking));
+  if (!c.x_fwd) c.x_fwd = make_stream(e.stream_prio == 2 ? -1 : e.stream_prio == 3 ? 1 : 0);
   for (int s = 0; s < 2; ++s) {
     if (!c.h_cnt[s]) {
       FD_HIP(hipHostMalloc(reinterpret_cast<void**>(&c.h_cnt[s]), kCntBytes, hipHostMallocMapped | hipHostMallocCoherent));
@@ -123,11 +125,16 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
       c.cnt_seq[s] = 0;
       FD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c.d_hcnt[s]), c.h_cnt[s], 0));
     }
-    if (!c.in_ev[s]) FD_HIP(hipEventCreateWithFlags(&c.in_ev[s], hipEventDisableTiming | hipEventDisableSystemFence));
-    if (!c.inbox_ev[s])
-      FD_HIP(hipEventCreateWithFlags(&c.inbox_ev[s], hipEventDisableTiming | hipEventDisableSystemFence));
-    c.inbox_live[s] = false;
+    c.cnt[s].ensure(2 * FD_MAX_SHARDS * sizeof(int64_t));
+    FD_HIP(hipMemset(c.cnt[s].ptr, 0, 2 * FD_MAX_SHARDS * sizeof(int64_t)));
   }
+  for (int q = 0; q < ShardComm::kInbox; ++q) {
+    if (!c.in_ev[q]) FD_HIP(hipEventCreateWithFlags(&c.in_ev[q], hipEventDisableTiming | hipEventDisableSystemFence));
+    if (!c.inbox_ev[q])
+      FD_HIP(hipEventCreateWithFlags(&c.inbox_ev[q], hipEventDisableTiming | hipEventDisableSystemFence));
+    c.inbox_live[q] = false;
+  }
+  c.inbox_next = 0;
   c.pending = false;
   c.next_slot = 0;
   c.sent[0] = c.sent[1] = false;  // (the count buffers keep their sequence numbers across communicators)
@@ -224,12 +231,16 @@ void comm_destroy(Engine& e) {
   }
   c.fwd = c.back = nullptr;
   for (int s = 0; s < 2; ++s) {
-    for (auto* b : {&c.rec[s], &c.cnt[s], &c.inbox[s], &c.res[s]}) b->release();
+    for (auto* b : {&c.rec[s], &c.cnt[s], &c.res[s]}) b->release();
     if (c.h_cnt[s]) (void)hipHostFree(c.h_cnt[s]);
-    if (c.in_ev[s]) (void)hipEventDestroy(c.in_ev[s]);
-    if (c.inbox_ev[s]) (void)hipEventDestroy(c.inbox_ev[s]);
     c.h_cnt[s] = c.d_hcnt[s] = nullptr;
-    c.in_ev[s] = c.inbox_ev[s] = nullptr;
+  }
+  for (int q = 0; q < ShardComm::kInbox; ++q) {
+    c.inbox[q].release();
+    if (c.in_ev[q]) (void)hipEventDestroy(c.in_ev[q]);
+    if (c.inbox_ev[q]) (void)hipEventDestroy(c.inbox_ev[q]);
+    c.in_ev[q] = c.inbox_ev[q] = nullptr;
+    c.inbox_live[q] = false;
   }
   c.back_buf.release();
   c.route_blk.release();
@@ -240,30 +251,32 @@ void comm_destroy(Engine& e) {
   c.pending = false;
 }
 
-// partition `t` by owner on the forward stream, exchange the per-owner counts (send[p] to peer p, recv[p] from
-// it: one int64 each way per peer), both count vectors published to the slot's host buffer (count_publish_kernel)
+// On the forward stream: the per-owner counts of `t` (send[p] to peer p, recv[p] from it: one int64 each way per
+// peer), published to the slot's host buffer (count_publish_kernel), then the records' places (scan + scatter into
+// rec[s]; the host's wait for the counts does not include them)
 void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int s, HostLaps& L) {
   ShardComm& c = e.comm;
   const RcclApi& R = rccl(nullptr);
   const int G = c.world;
-  if (ready) FD_HIP(hipStreamWaitEvent(c.x_fwd, ready, 0));
-  c.rec[s].ensure((size_t)std::max<int64_t>(n, 1) * sizeof(RouteRecord));
-  c.cnt[s].ensure(2 * (size_t)G * sizeof(int64_t));
-  int64_t* cnt = c.cnt[s].as<int64_t>();
-  launch_route_partition(e, t, nullptr, n, G, c.rec[s].ptr, cnt, c.x_fwd, &c.route_blk, /*timed=*/false);
+  hipStream_t st = c.x_fwd;
+  if (ready) FD_HIP(hipStreamWaitEvent(st, ready, 0));
+  int64_t* cnt = c.cnt[s].as<int64_t>();  // send half zero (comm_init, then every publish)
+  launch_route_count(t, n, G, cnt, st, c.route_blk);
   L(1);
   const ncclComm_t f = static_cast<ncclComm_t>(c.fwd);
   check(R, R.group_start(), "ncclGroupStart");
   for (int p = 0; p < G; ++p) {
-    check(R, R.send(cnt + p, 1, ncclInt64, p, f, c.x_fwd), "ncclSend (counts)");
-    check(R, R.recv(cnt + G + p, 1, ncclInt64, p, f, c.x_fwd), "ncclRecv (counts)");
+    check(R, R.send(cnt + p, 1, ncclInt64, p, f, st), "ncclSend (counts)");
+    check(R, R.recv(cnt + G + p, 1, ncclInt64, p, f, st), "ncclRecv (counts)");
   }
   check(R, R.group_end(), "ncclGroupEnd (counts)");
   L(2);
   const unsigned long long seq = ++c.cnt_seq[s];
   auto* dseq = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(c.d_hcnt[s]) + kCntSeqOff);
-  hipLaunchKernelGGL(count_publish_kernel, dim3(1), dim3(128), 0, c.x_fwd, cnt, 2 * G, c.d_hcnt[s], dseq, seq);
+  hipLaunchKernelGGL(count_publish_kernel, dim3(1), dim3(128), 0, st, cnt, G, c.d_hcnt[s], dseq, seq);
   FD_HIP(hipGetLastError());
+  c.rec[s].ensure_headroom((size_t)std::max<int64_t>(n, 1) * sizeof(RouteRecord));
+  launch_route_place(t, n, G, c.rec[s].ptr, st, c.route_blk);
   L(3);
 }
 
@@ -298,7 +311,8 @@ void comm_wait_counts(Engine& e, int s, int64_t n, HostLaps& L) {
   L(0);
 }
 
-// slot s's records to their owners on the forward stream, after the owner's previous use of that inbox slot
+// slot s's records to their owners on the forward stream, into the next inbox of the ring (after the scoring
+// that last read it)
 void comm_send_records(Engine& e, int s, HostLaps& L) {
   ShardComm& c = e.comm;
   const int G = c.world;
@@ -306,11 +320,14 @@ void comm_send_records(Engine& e, int s, HostLaps& L) {
   const int64_t* recv = c.split[s] + G;
   int64_t m = 0;
   for (int p = 0; p < G; ++p) m += recv[p];
-  if (c.inbox_live[s]) FD_HIP(hipStreamWaitEvent(c.x_fwd, c.inbox_ev[s], 0));
-  c.inbox[s].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(RouteRecord));
+  const int q = c.inbox_next;
+  c.inbox_next = (q + 1) % ShardComm::kInbox;
+  c.inbox_of[s] = q;
+  if (c.inbox_live[q]) FD_HIP(hipStreamWaitEvent(c.x_fwd, c.inbox_ev[q], 0));
+  c.inbox[q].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(RouteRecord));
   c.res[s].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(ResultRecord));
-  comm_exchange(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[s].ptr, recv, sizeof(RouteRecord));
-  FD_HIP(hipEventRecord(c.in_ev[s], c.x_fwd));
+  comm_exchange(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[q].ptr, recv, sizeof(RouteRecord));
+  FD_HIP(hipEventRecord(c.in_ev[q], c.x_fwd));
   L(4);
 }
 

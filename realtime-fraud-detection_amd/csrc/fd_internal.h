@@ -285,15 +285,23 @@ struct ShardComm {
   void* fwd = nullptr;   // ncclComm_t: counts + records, on x_fwd
   void* back = nullptr;  // ncclComm_t: results, on the engine stream
   hipStream_t x_fwd = nullptr;
-  DeviceBuffer rec[2], cnt[2], inbox[2], res[2], back_buf;
+  DeviceBuffer rec[2], cnt[2], res[2], back_buf;
+  // received records: a ring of three inboxes, so a batch's records exchange waits for the scoring three batches
+  // back (long done) instead of two (still running beside the pipeline) — x_fwd is then never parked on an inbox,
+  // and the next batch's counts queued behind the records are not held up either (the process has 4 hardware
+  // queues for 4+ streams: a parked stream stalls whatever shares its queue)
+  static constexpr int kInbox = 3;
+  DeviceBuffer inbox[kInbox];
+  hipEvent_t in_ev[kInbox] = {}, inbox_ev[kInbox] = {};  // records arrived / the engine stream passed their scoring
+  bool inbox_live[kInbox] = {};
+  int inbox_next = 0;                                     // the next batch's inbox
+  int inbox_of[2] = {0, 0};                               // slot s's batch's inbox
   DeviceBuffer route_blk;                  // the partition's block counts (x_fwd)
   // coherent host-mapped memory per slot: send counts [G], receive counts [G] (FD_MAX_SHARDS each), then a u64
   // sequence word; count_publish_kernel writes the counts and then the sequence, the host polls the sequence
   int64_t* h_cnt[2] = {nullptr, nullptr};
   int64_t* d_hcnt[2] = {nullptr, nullptr};  // the same buffers' device addresses
   unsigned long long cnt_seq[2] = {0, 0};  // the sequence the slot's latest publish writes
-  hipEvent_t in_ev[2] = {}, inbox_ev[2] = {};
-  bool inbox_live[2] = {};
   bool pending = false;  // a prefetched batch's counts are in flight (slot pending_slot)
   const void* pending_key = nullptr;
   int64_t pending_n = 0;
@@ -384,6 +392,7 @@ struct Engine {
   bool pipe_copy_live[kPipeSlots] = {};
   bool pipe_copy_vec[kPipeSlots] = {};  // that copy also read the slot's vectors (the slot's next features wait)
   int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
+  int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
   DeviceBuffer scratch_probs, stage_ext;  // score_matrix per-model columns / staged external columns
@@ -479,12 +488,18 @@ void load_vocab(Engine& e, const uint8_t* pay_high_risk, const uint8_t* type_ref
 void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context& c, int64_t n, float* d_vec,
                           double* d_raw, double* d_fmap, fd_rule_scores* d_rules);
 void features_check(Engine& e);
+// engine.hip: a non-blocking stream at HIP priority level (+1 the greatest, -1 the least, 0 the default)
+hipStream_t make_stream(int level);
 // route.hip
 unsigned shard_of_host(unsigned long long key, unsigned G);
 // stream / scratch: the launch stream and block-count scratch (default: the engine stream and route_blk)
 void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_inputs* extra, int64_t n, int G,
                             void* d_records, int64_t* d_counts, hipStream_t stream = nullptr,
                             DeviceBuffer* scratch = nullptr, bool timed = true);
+// the sharded step's split form of the partition: block counts + per-shard totals added into `totals` (zero on
+// entry) first, so the count exchange can start; then the scan + record scatter (blk: the same scratch)
+void launch_route_count(const fd_txn_batch& t, int64_t n, int G, int64_t* totals, hipStream_t st, DeviceBuffer& blk);
+void launch_route_place(const fd_txn_batch& t, int64_t n, int G, void* d_records, hipStream_t st, DeviceBuffer& blk);
 void launch_route_unpack(Engine& e, const void* d_records, const void* d_results, int64_t n, const fd_txn_batch& out,
                          uint8_t* pm, uint8_t* fraud, double* score);
 void launch_result_pack(Engine& e, const double* fp, const double* conf, const uint8_t* dec, const uint8_t* risk,

@@ -48,9 +48,12 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// totals (optional, zero on entry): per-shard counts added up across blocks, so the count exchange can start
+// before the scan (the sharded step's forward half)
 __global__ void __launch_bounds__(kRouteBlock) route_count_kernel(const unsigned long long* __restrict__ key,
                                                                   int64_t n, unsigned G, int nblk,
-                                                                  int* __restrict__ blk) {
+                                                                  int* __restrict__ blk,
+                                                                  unsigned long long* __restrict__ totals) {
   __shared__ int cnt[64];
   const int64_t i = (int64_t)blockIdx.x * kRouteBlock + threadIdx.x;
   if (threadIdx.x < G) cnt[threadIdx.x] = 0;
@@ -61,7 +64,10 @@ __global__ void __launch_bounds__(kRouteBlock) route_count_kernel(const unsigned
     if (__lane_id() == 0 && m) atomicAdd(&cnt[t], __popcll(m));
   }
   __syncthreads();
-  if (threadIdx.x < G) blk[(size_t)threadIdx.x * nblk + blockIdx.x] = cnt[threadIdx.x];
+  if (threadIdx.x < G) {
+    blk[(size_t)threadIdx.x * nblk + blockIdx.x] = cnt[threadIdx.x];
+    if (totals && cnt[threadIdx.x]) atomicAdd(&totals[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+  }
 }
 
 // exclusive scan of the shard-major block counts: each of the 1024 threads scans a contiguous segment
@@ -88,7 +94,7 @@ __global__ void __launch_bounds__(1024) route_scan_kernel(int* __restrict__ blk,
     run += c;
   }
   __syncthreads();
-  if (t < (int)G) {  // per-shard totals = offset of the next shard's first block - this one's
+  if (counts && t < (int)G) {  // per-shard totals = offset of the next shard's first block - this one's
     const long long lo = blk[(size_t)t * nblk];
     const long long hi = (t + 1 < (int)G) ? (long long)blk[(size_t)(t + 1) * nblk] : part[1023];
     counts[t] = hi - lo;
@@ -224,7 +230,7 @@ void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_in
   if (ev) FD_HIP(hipEventRecord(ev->a, st));
   const auto* key = reinterpret_cast<const unsigned long long*>(t.card_key);
   hipLaunchKernelGGL(route_count_kernel, dim3(nblk), dim3(kRouteBlock), 0, st, key, n, (unsigned)G, nblk,
-                     blk.as<int>());
+                     blk.as<int>(), nullptr);
   FD_HIP(hipGetLastError());
   hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, st, blk.as<int>(),
                      (int64_t)G * nblk, (unsigned)G, nblk, reinterpret_cast<long long*>(d_counts));
@@ -237,6 +243,40 @@ void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_in
                      static_cast<RouteRecord*>(d_records));
   FD_HIP(hipGetLastError());
   if (ev) FD_HIP(hipEventRecord(ev->b, st));
+}
+
+void launch_route_count(const fd_txn_batch& t, int64_t n, int G, int64_t* totals, hipStream_t st,
+                        DeviceBuffer& blk) {
+  FD_REQUIRE(G >= 1 && G <= FD_MAX_SHARDS, FD_ERR_INVALID_ARG, "n_shards must be in [1, 64]");
+  FD_REQUIRE(n >= 0 && n < (1ll << 31), FD_ERR_INVALID_ARG, "batch size out of range");
+  if (n == 0) return;  // the totals stay zero
+  FD_REQUIRE(t.card_key, FD_ERR_INVALID_ARG, "incomplete transaction batch");
+  const int nblk = (int)((n + kRouteBlock - 1) / kRouteBlock);
+  blk.ensure((size_t)G * nblk * sizeof(int));
+  hipLaunchKernelGGL(route_count_kernel, dim3(nblk), dim3(kRouteBlock), 0, st,
+                     reinterpret_cast<const unsigned long long*>(t.card_key), n, (unsigned)G, nblk, blk.as<int>(),
+                     reinterpret_cast<unsigned long long*>(totals));
+  FD_HIP(hipGetLastError());
+}
+
+void launch_route_place(const fd_txn_batch& t, int64_t n, int G, void* d_records, hipStream_t st, DeviceBuffer& blk) {
+  if (n == 0) return;
+  FD_REQUIRE(d_records != nullptr, FD_ERR_INVALID_ARG, "null records");
+  FD_REQUIRE(t.card_key && t.ts_ms && t.amount_cents && t.merchant && t.device_fp && t.ip_class && t.hour &&
+                 t.weekend,
+             FD_ERR_INVALID_ARG, "incomplete transaction batch");
+  const int nblk = (int)((n + kRouteBlock - 1) / kRouteBlock);
+  FD_REQUIRE(blk.bytes >= (size_t)G * nblk * sizeof(int), FD_ERR_INVALID_ARG, "route_place before route_count");
+  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, st, blk.as<int>(), (int64_t)G * nblk, (unsigned)G,
+                     nblk, nullptr);
+  FD_HIP(hipGetLastError());
+  hipLaunchKernelGGL(route_scatter_kernel, dim3(nblk), dim3(kRouteBlock), 0, st,
+                     reinterpret_cast<const unsigned long long*>(t.card_key),
+                     reinterpret_cast<const long long*>(t.ts_ms), reinterpret_cast<const long long*>(t.amount_cents),
+                     reinterpret_cast<const int*>(t.merchant), reinterpret_cast<const unsigned long long*>(t.device_fp),
+                     t.ip_class, t.hour, t.weekend, nullptr, nullptr, n, (unsigned)G, nblk, blk.as<const int>(),
+                     static_cast<RouteRecord*>(d_records));
+  FD_HIP(hipGetLastError());
 }
 
 void launch_route_unpack(Engine& e, const void* d_records, const void* d_results, int64_t n, const fd_txn_batch& out,

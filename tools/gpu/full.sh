@@ -17,3 +17,6 @@ rm -rf /tmp/$T.prof
 if [ "${PHASES:-0}" = 1 ]; then
   timeout -k 10 300 python -u tools/ens_phases_pipe.py > gpurun_out/$T.ens_phases_pipe.log 2>&1 || exit $?
 fi
+if [ "${ROUTE:-0}" = 1 ]; then
+  timeout -k 10 400 python -u tools/route_overhead.py > gpurun_out/$T.route_overhead.log 2>&1 || exit $?
+fi

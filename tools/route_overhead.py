@@ -45,6 +45,8 @@ for name in VARIANTS:
     eng.state_init(cap, 1, 16)
     eng.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
     eng.set_option("sharded_fwd_thread", fwd_thread)
+    if os.environ.get("STREAM_PRIORITY"):
+        eng.set_option("stream_priority", int(os.environ["STREAM_PRIORITY"]))
     sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), 0, 1, force_route=routed,
                        streaming=name != "serial", native=name == "native")
     w = synth_gpu.warm_workload(eng, dev, CARDS, 0, 1, STEPS + 20, B, hours=12.0, keep_batches=0)
