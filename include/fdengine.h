@@ -645,6 +645,9 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      small-batch path (auto takes it below 128 tiles of 256 transactions), 8 force the binned node-only-chunk
      kernel (auto's choice when the forest has that layout); the variants measured slower were removed
      "ensemble": 1 fused XGBoost + IsolationForest + blend kernel when applicable (default), 0 per-model kernels
+     "ensemble_chunks": the fused kernel's chunk layout, 0 (default) auto: compact once the engine has RCCL
+     communicators (fd_comm_init), else wide; 1 wide (24 XGBoost / 16 IsolationForest trees per chunk, 148 KB of
+     LDS); 2 compact (20 / 12, 132 KB: room for an RCCL kernel on the same CU). Outputs are identical.
      "lstm_rows": LSTM tile, 0 auto (4 transactions below 4096, else 16), 4 or 16
      "timing_every": N >= 1, fd_engine_set_timing records HIP events on one launch in N of each timing kind
      (the others run without event records; fd_timing_read's launch count is the timed ones)

@@ -14,9 +14,10 @@
 // each thread loads 16 features of its row into registers; the merged table is staged in LDS in feature
 // ranges (passes) that fit the chunk buffers + leaf-index tiles (dead until chunk 0 is staged) and every
 // value is binned into the u16 tile (two features per 1 KiB row, 32 KiB for 64 features). Then the chunk
-// stream is XGBoost's 24-tree chunks followed by the IsolationForest's 16-tree chunks (1 KiB node block per
-// tree + the chunk's leaf values, double-buffered by LDS-DMA); per chunk each wave walks its TPG trees
-// (6 / 4) for its 64 transactions (walk_ens: 4 VALU + 2 LDS reads per node step) and stores the packed leaf
+// stream is XGBoost's 24-tree chunks followed by the IsolationForest's 16-tree chunks (the compact layout: 20 /
+// 12, see EnsCfg) (1 KiB node block per tree + the chunk's leaf values, double-buffered by LDS-DMA); per chunk
+// each wave walks its TPG trees (6 / 4; 5 / 3) for its 64 transactions (walk_ens: 4 VALU + 2 LDS reads per node
+// step) and stores the packed leaf
 // indices to the chunk's index tile; the owner tree group (0) then adds each transaction's leaf values of
 // that chunk, read from LDS, in tree order into the f32 margin (XGBoost) or the f64 path-length sum
 // (IsolationForest): both the reference's sequential sums, bit for bit. Epilogue (tree group 0, one thread
@@ -52,14 +53,22 @@ void forest_loaded(PackedForest& pf, const fd_forest_params& p, const fd_tree_ar
 namespace {
 
 constexpr int kEnsWG = 1024;
-constexpr int kCHA = 20;  // XGBoost trees per chunk (TPG 5)
-constexpr int kCHB = 12;  // IsolationForest trees per chunk (TPG 3)
 constexpr int kMaxPass = 64;
 
-// A chunk in LDS: CH node blocks of 1 KiB (walk_ens link addressing), then the CH trees' leaf values
-// [CH][2^D]; its LDS buffer is sized for depth 8: max(24 x (1 KiB + 1 KiB f32), 16 x (1 KiB + 2 KiB f64)).
-constexpr uint32_t kEnsBuf = (uint32_t)(kCHA * (1024 + 256 * 4) > kCHB * (1024 + 256 * 8) ? kCHA * (1024 + 256 * 4)
-                                                                                          : kCHB * (1024 + 256 * 8));
+// Trees per chunk, by layout: wide 24 XGBoost (TPG 6) / 16 IsolationForest (TPG 4) trees in 48 KiB chunk
+// buffers; compact 20 (TPG 5) / 12 (TPG 3) in 40 KiB, which leaves the CU the ~20 KiB of LDS an RCCL kernel
+// needs beside the scoring (the sharded step's exchanges co-run with it: with the wide layout they waited for a
+// whole scoring launch to end). A chunk in LDS: CH node blocks of 1 KiB (walk_ens link addressing), then the CH
+// trees' leaf values [CH][2^D]; its buffer is sized for depth 8: max(CHA x (1 KiB + 1 KiB f32), CHB x (1 KiB +
+// 2 KiB f64)).
+template <bool WIDE>
+struct EnsCfg {
+  static constexpr int CHA = WIDE ? 24 : 20;
+  static constexpr int CHB = WIDE ? 16 : 12;
+  static constexpr uint32_t BUF = (uint32_t)(CHA * (1024 + 256 * 4) > CHB * (1024 + 256 * 8) ? CHA * (1024 + 256 * 4)
+                                                                                             : CHB * (1024 + 256 * 8));
+};
+inline uint32_t ens_buf(bool wide) { return wide ? EnsCfg<true>::BUF : EnsCfg<false>::BUF; }
 constexpr uint32_t kEnsTile = 4u * kTile * 8u;  // leaf indices of one chunk: [tree group][txn] u64, a byte per tree
 
 // The bin tile: u16 bins, two features per 1 KiB row — feature f of transaction t at byte
@@ -69,8 +78,9 @@ __host__ __device__ constexpr uint32_t ens_xs_bytes(int nf) { return (uint32_t)(
 
 // LDS bytes of the kernel: Xs | bufA | bufB | tile0 | tile1 | accA (f32) | accB (f64) | flags + owner counter,
 // + 1 KiB alignment
-size_t ens_lds(int nf, int /*D*/) {
-  return (size_t)ens_xs_bytes(nf) + 2 * (size_t)kEnsBuf + 2 * (size_t)kEnsTile + kTile * 4 + kTile * 8 + 128 + 1024;
+size_t ens_lds(int nf, bool wide) {
+  return (size_t)ens_xs_bytes(nf) + 2 * (size_t)ens_buf(wide) + 2 * (size_t)kEnsTile + kTile * 4 + kTile * 8 + 128 +
+         1024;
 }
 
 struct EnsArgs {
@@ -230,8 +240,10 @@ static int g_eprof_next = 0;
 #define FD_ESTAMP(var)
 #endif
 
-template <int D, int OUT>
+template <int D, int OUT, bool WIDE>
 __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
+  constexpr int kCHA = EnsCfg<WIDE>::CHA, kCHB = EnsCfg<WIDE>::CHB;
+  constexpr uint32_t kEnsBuf = EnsCfg<WIDE>::BUF;
   constexpr int TPGA = kCHA / 4, TPGB = kCHB / 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t sdyn = (uint32_t)(size_t)((lds_char*)smem);
@@ -509,19 +521,24 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   }
 }
 
-template <int OUT>
+template <int OUT, bool WIDE>
 const void* pick_ensemble(int D) {
   switch (D) {
-    case 1: return (const void*)ensemble_kernel<1, OUT>;
-    case 2: return (const void*)ensemble_kernel<2, OUT>;
-    case 3: return (const void*)ensemble_kernel<3, OUT>;
-    case 4: return (const void*)ensemble_kernel<4, OUT>;
-    case 5: return (const void*)ensemble_kernel<5, OUT>;
-    case 6: return (const void*)ensemble_kernel<6, OUT>;
-    case 7: return (const void*)ensemble_kernel<7, OUT>;
-    case 8: return (const void*)ensemble_kernel<8, OUT>;
+    case 1: return (const void*)ensemble_kernel<1, OUT, WIDE>;
+    case 2: return (const void*)ensemble_kernel<2, OUT, WIDE>;
+    case 3: return (const void*)ensemble_kernel<3, OUT, WIDE>;
+    case 4: return (const void*)ensemble_kernel<4, OUT, WIDE>;
+    case 5: return (const void*)ensemble_kernel<5, OUT, WIDE>;
+    case 6: return (const void*)ensemble_kernel<6, OUT, WIDE>;
+    case 7: return (const void*)ensemble_kernel<7, OUT, WIDE>;
+    case 8: return (const void*)ensemble_kernel<8, OUT, WIDE>;
     default: return nullptr;
   }
+}
+
+const void* pick_ensemble(int out, bool wide, int D) {
+  if (wide) return out == 1 ? pick_ensemble<1, true>(D) : out == 2 ? pick_ensemble<2, true>(D) : pick_ensemble<0, true>(D);
+  return out == 1 ? pick_ensemble<1, false>(D) : out == 2 ? pick_ensemble<2, false>(D) : pick_ensemble<0, false>(D);
 }
 
 fd_tree_arrays arrays_of(const PackedForest& f) {
@@ -539,7 +556,7 @@ fd_tree_arrays arrays_of(const PackedForest& f) {
 
 // joint repack of forest A (XGBoost, slot sa) and B (IsolationForest, slot sb) into plan P; either slot may be -1
 // (a single forest: the kernel walks only the other one); false when not possible (the per-model path runs)
-bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb) {
+bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb, bool wide) {
   P.valid = false;
   const PackedForest* F[2] = {sa >= 0 ? &e.forests[sa] : nullptr, sb >= 0 ? &e.forests[sb] : nullptr};
   if (!F[0] && !F[1]) return false;
@@ -551,7 +568,7 @@ bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb) {
     D = std::max(D, f->depth);
   }
   if (D > 8) return false;
-  if (ens_lds(nf, D) > kLdsBudget) return false;
+  if (ens_lds(nf, wide) > kLdsBudget) return false;
   HostPack hp[2];
   for (int k = 0; k < 2; ++k) {
     if (!F[k]) continue;
@@ -579,7 +596,7 @@ bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb) {
     maxc = std::max(maxc, (int)merged[f].size());
   }
   const int NL = 1 << D;
-  const int CH[2] = {kCHA, kCHB};
+  const int CH[2] = {wide ? EnsCfg<true>::CHA : EnsCfg<false>::CHA, wide ? EnsCfg<true>::CHB : EnsCfg<false>::CHB};
   const size_t leaf_sz[2] = {sizeof(float), sizeof(double)};
   for (int k = 0; k < 2; ++k) {
     if (!F[k]) {
@@ -594,7 +611,7 @@ bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb) {
     // padding trees (a partial last chunk) keep zero nodes and zero leaves
     const size_t leaf_bytes = (size_t)CH[k] * NL * leaf_sz[k];
     const size_t stride = ((size_t)CH[k] * 1024 + leaf_bytes + 1023) / 1024 * 1024;
-    FD_REQUIRE(stride <= kEnsBuf, FD_ERR_UNSUPPORTED, "ensemble chunk exceeds its LDS buffer");
+    FD_REQUIRE(stride <= ens_buf(wide), FD_ERR_UNSUPPORTED, "ensemble chunk exceeds its LDS buffer");
     std::vector<char> blob((size_t)nc * stride, 0);
     for (int i = 0; i < T; ++i) {
       const char* src = h.b_blob.data() + (size_t)(i / h.b_chunk) * h.b_chunk_stride + (size_t)(i % h.b_chunk) *
@@ -636,6 +653,7 @@ bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb) {
   P.n_forests = (F[0] ? 1 : 0) + (F[1] ? 1 : 0);
   P.D = D;
   P.nf = nf;
+  P.wide = wide;
   P.kind[0] = FD_FOREST_XGB_BINARY_LOGISTIC;
   P.kind[1] = FD_FOREST_SKLEARN_IFOREST;
   P.base_margin = F[0] ? hp[0].base_margin : 0.f;
@@ -645,10 +663,14 @@ bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb) {
   return true;
 }
 
-bool plan_current(const Engine& e, const EnsemblePlan& P, int sa, int sb) {
-  return P.valid && P.slot[0] == sa && P.slot[1] == sb && P.gen[0] == (sa >= 0 ? e.forests[sa].gen : 0) &&
-         P.gen[1] == (sb >= 0 ? e.forests[sb].gen : 0);
+bool plan_current(const Engine& e, const EnsemblePlan& P, int sa, int sb, bool wide) {
+  return P.valid && P.wide == wide && P.slot[0] == sa && P.slot[1] == sb &&
+         P.gen[0] == (sa >= 0 ? e.forests[sa].gen : 0) && P.gen[1] == (sb >= 0 ? e.forests[sb].gen : 0);
 }
+
+// the chunk layout for this engine: option "ensemble_chunks" 1 wide / 2 compact, 0 (auto) compact once the engine
+// has RCCL communicators (its sharded step's exchanges co-run with the scoring), else wide
+bool want_wide(const Engine& e) { return e.ens_chunks == 1 || (e.ens_chunks == 0 && !e.comm.ready); }
 
 }  // namespace
 
@@ -692,7 +714,8 @@ bool select_pair(Engine& e, const fd_blend_params& p, const int32_t* slots, cons
     ++k;
   }
   if (q.sa < 0 || q.sb < 0) return false;
-  if (!plan_current(e, e.ens, q.sa, q.sb) && !build_plan(e, e.ens, q.sa, q.sb)) return false;
+  const bool wide = want_wide(e);
+  if (!plan_current(e, e.ens, q.sa, q.sb, wide) && !build_plan(e, e.ens, q.sa, q.sb, wide)) return false;
   return true;
 }
 }  // namespace
@@ -710,7 +733,7 @@ void plan_args(const EnsemblePlan& P, const float* dX, int64_t n, int32_t ld, bo
   a.vec4 = (ld % 4 == 0 && (reinterpret_cast<uintptr_t>(dX) & 15u) == 0) ? 1 : 0;
   // binning passes: consecutive features whose tables fit bufA + bufB + the tiles; a larger table alone,
   // searched in global memory
-  const size_t stage_floats = (2 * (size_t)kEnsBuf + 2 * (size_t)kEnsTile) / 4;  // bufA + bufB + the tiles
+  const size_t stage_floats = (2 * (size_t)ens_buf(P.wide) + 2 * (size_t)kEnsTile) / 4;  // bufA + bufB + the tiles
   int np = 0, f = 0;
   a.pass_f[0] = 0;
   while (f < P.nf) {
@@ -738,9 +761,9 @@ void plan_args(const EnsemblePlan& P, const float* dX, int64_t n, int32_t ld, bo
 
 // out: 0 blended columns, 1 route result records, 2 the single forest's probability column (a.fp)
 bool run_plan(Engine& e, const EnsemblePlan& P, EnsArgs& a, int out, int timing_kind) {
-  const void* fn = out == 1 ? pick_ensemble<1>(P.D) : out == 2 ? pick_ensemble<2>(P.D) : pick_ensemble<0>(P.D);
+  const void* fn = pick_ensemble(out, P.wide, P.D);
   if (!fn) return false;
-  const size_t lds = ens_lds(P.nf, P.D);
+  const size_t lds = ens_lds(P.nf, P.wide);
   FD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int64_t blocks = (a.n + kTile - 1) / kTile;
   Engine::Timed* ev = e.timing ? e.next_event_pair(timing_kind) : nullptr;
@@ -794,7 +817,8 @@ bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int
   const bool xgb = e.forests[slot].kind == FD_FOREST_XGB_BINARY_LOGISTIC;
   const int sa = xgb ? slot : -1, sb = xgb ? -1 : slot;
   EnsemblePlan& P = e.ens1[slot];
-  if (!plan_current(e, P, sa, sb) && !build_plan(e, P, sa, sb)) return false;
+  const bool wide = want_wide(e);
+  if (!plan_current(e, P, sa, sb, wide) && !build_plan(e, P, sa, sb, wide)) return false;
   EnsArgs a{};
   plan_args(P, dX, n, ld, e.ens_owner_fixed, a);
   a.fp = dprob;

@@ -126,6 +126,7 @@ struct PackedForest {
 // tile serves both forests; chunks of CH[k] node-only trees, leaf values [tree][2^D] per forest.
 struct EnsemblePlan {
   bool valid = false;
+  bool wide = true;  // chunk layout: 24 / 16 trees (wide) or 20 / 12 (compact: LDS room for an RCCL kernel beside)
   int slot[2] = {-1, -1};   // forest A = the XGBoost model (or the only forest), forest B = the IsolationForest
   uint64_t gen[2] = {0, 0};
   int n_forests = 0, D = 0, nf = 0;
@@ -405,6 +406,7 @@ struct Engine {
   // optional per-launch kernel timing (HIP events on the launch stream)
   int forest_variant = 0;  // "forest_kernel" option
   bool ens_owner_fixed = true;  // "ensemble_owner" option (A/B of the fused kernel's chunk-owner schedule)
+  int ens_chunks = 0;           // "ensemble_chunks": 0 auto, 1 wide, 2 compact chunk layout (ensemble.hip)
   int lstm_rows = 0;  // "lstm_rows" option: transactions per LSTM workgroup tile (0 auto, 4 or 16)
   bool ensemble_on = true;  // "ensemble" option: the fused XGBoost + IsolationForest + blend kernel (auto)
   bool timing = false;

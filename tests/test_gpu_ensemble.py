@@ -68,11 +68,17 @@ def _check(engine, xgb, ifm, X, names=("xgboost_primary", "isolation_forest"), s
         assert fp[i] == rfp and fused[2][i] == rcf
 
 
+@pytest.mark.parametrize("chunks", [1, 2])
 @pytest.mark.parametrize("strategy", [0, 1, 2])
-def test_fused_matches_per_model_and_oracle(engine, strategy):
+def test_fused_matches_per_model_and_oracle(engine, strategy, chunks):
+    """both chunk layouts (engine option ensemble_chunks: 1 wide 24 / 16 trees, 2 compact 20 / 12)"""
     xgb, ifm = _models(64, 8, seed=3)
     X = synth.feature_matrix(N, 64, seed=4, nan_frac=0.01)
-    _check(engine, xgb, ifm, X, strategy=strategy)
+    engine.set_option("ensemble_chunks", chunks)
+    try:
+        _check(engine, xgb, ifm, X, strategy=strategy)
+    finally:
+        engine.set_option("ensemble_chunks", 0)
 
 
 def test_reversed_model_order_and_depth_padding(engine):
@@ -94,17 +100,23 @@ def test_short_rows_are_missing_columns(engine):
         np.testing.assert_array_equal(a, b)
 
 
-def test_multi_pass_and_global_binning(engine):
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_multi_pass_and_global_binning(engine, chunks):
     """Raw-valued thresholds: thousands of distinct thresholds per feature, so the merged tables take several
-    LDS passes; one 2-feature model whose feature-0 table alone exceeds the LDS space (global search)."""
-    xgb, ifm = _models(64, 8, n_trees=400, max_bin=None, seed=9, ref_rows=20000)
-    X = synth.feature_matrix(N, 64, seed=10, nan_frac=0.005)
-    _check(engine, xgb, ifm, X)
-    Xr = np.random.default_rng(11).normal(size=(60000, 2)).astype(np.float32)
-    xgb2 = xgboost_from_json_doc(synth.xgboost_doc(300, 8, 2, Xr, seed=12, max_bin=None))
-    ifm2 = iforest_from_sklearn(synth.isolation_forest(Xr[:8192].astype(np.float64), n_estimators=30))
-    X2 = np.random.default_rng(13).normal(size=(N, 2)).astype(np.float32)
-    _check(engine, xgb2, ifm2, X2)
+    LDS passes (fewer staging bytes in the compact layout: more passes); one 2-feature model whose feature-0
+    table alone exceeds the LDS space (global search)."""
+    engine.set_option("ensemble_chunks", chunks)
+    try:
+        xgb, ifm = _models(64, 8, n_trees=400, max_bin=None, seed=9, ref_rows=20000)
+        X = synth.feature_matrix(N, 64, seed=10, nan_frac=0.005)
+        _check(engine, xgb, ifm, X)
+        Xr = np.random.default_rng(11).normal(size=(60000, 2)).astype(np.float32)
+        xgb2 = xgboost_from_json_doc(synth.xgboost_doc(300, 8, 2, Xr, seed=12, max_bin=None))
+        ifm2 = iforest_from_sklearn(synth.isolation_forest(Xr[:8192].astype(np.float64), n_estimators=30))
+        X2 = np.random.default_rng(13).normal(size=(N, 2)).astype(np.float32)
+        _check(engine, xgb2, ifm2, X2)
+    finally:
+        engine.set_option("ensemble_chunks", 0)
 
 
 def test_reload_invalidates_the_joint_repack(engine):
