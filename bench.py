@@ -110,13 +110,14 @@ def pmc_traffic(workload, B, kernel_symbol):
         return None
 
 
-ENSEMBLE_SYMBOL = "fd::anon::ensemble_kernel<8, 0>"
+def ensemble_symbol(out, wide):
+    return f"fd::anon::ensemble_kernel<8, {out}, {'true' if wide else 'false'}>"
 FOREST6_SYMBOL = "fd::anon::forest_kernel6<8, 24, float, 1, 0>"
 LSTM4_SYMBOL = "fd::anon::lstm_kernel4"
 INGEST_SYMBOL = "fd::anon::ingest_json_kernel"
 
 
-def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=None):
+def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=None, out=0, wide=True):
     """Roofline of a forest launch against its real bound: LDS issue of the dependent walk. With the fused
     ensemble kernel (FD_TIMING_ENSEMBLE) timed, that launch is the one reported (both forests' node steps)."""
     from fdengine import _native as N
@@ -127,13 +128,15 @@ def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=Non
         steps = B * sum(f.n_trees for f in forests) * depth
         label = "ensemble_kernel<D=8> (XGBoost 500 + IsolationForest 100 over one merged-bin tile + blend)"
         forest_bytes = sum(forest_blob_bytes(f) for f in forests)
-        symbol = ENSEMBLE_SYMBOL
+        # the instantiation that ran: output form (0 columns, 1 route result records) and chunk layout (wide
+        # unless the engine has RCCL communicators: engine option ensemble_chunks)
+        symbol = ensemble_symbol(out, wide)
     elif timing.get(N.FD_TIMING_ENSEMBLE, (0.0, 0))[1]:  # one forest through the fused kernel (config 2)
         ms, launches = timing[N.FD_TIMING_ENSEMBLE]
         steps = B * forest.n_trees * depth
         forest_bytes = forest_blob_bytes(forest)
         label = "ensemble_kernel<D=8> over one forest (probabilities only)"
-        symbol = "fd::anon::ensemble_kernel<8, 2>"
+        symbol = ensemble_symbol(2, True)
     else:
         steps = B * forest.n_trees * depth
         forest_bytes = forest_blob_bytes(forest)
@@ -499,8 +502,12 @@ class Config3:
         return out
 
     def roofline(self, timing):
+        sc = getattr(self, "scorer", None)
+        native = bool(sc is not None and sc.native)
+        routed = bool(sc is not None and sc.route)
         return forest_roofline(timing, self.N.FD_TIMING_XGB, self.xgb, 8, self.B, self.name,
-                               FOREST_KERNEL.format(d=8, t="f32", k="XGB") + " dominant", [self.xgb, self.ifm])
+                               FOREST_KERNEL.format(d=8, t="f32", k="XGB") + " dominant", [self.xgb, self.ifm],
+                               out=1 if routed else 0, wide=not native)
 
     def kernels(self, timing):
         N = self.N

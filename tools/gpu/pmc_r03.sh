@@ -12,7 +12,7 @@ PASSES=(
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
   "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
 )
-for W in 4 5; do
+for W in ${WORKLOADS:-4 5}; do
   k=0
   for p in "${PASSES[@]}"; do
     k=$((k + 1))
@@ -22,6 +22,8 @@ for W in 4 5; do
     rc=$?; echo "config$W pass $k rc=$rc"; [ $rc -ne 0 ] && exit $rc
   done
 done
-python3 tools/pmc_kernels.py config4 65536 ensemble_kernel gpurun_out/$T.pmc_config4.json /tmp/$T.c4.p* || exit $?
-python3 tools/pmc_kernels.py config5 1024 lstm_kernel4 gpurun_out/$T.pmc_config5.json /tmp/$T.c5.p* || exit $?
+for W in ${WORKLOADS:-4 5}; do
+  if [ $W = 4 ]; then python3 tools/pmc_kernels.py config4 65536 ensemble_kernel gpurun_out/$T.pmc_config4.json /tmp/$T.c4.p* || exit $?; fi
+  if [ $W = 5 ]; then python3 tools/pmc_kernels.py config5 1024 lstm_kernel4 gpurun_out/$T.pmc_config5.json /tmp/$T.c5.p* || exit $?; fi
+done
 rm -rf /tmp/$T.c4.p* /tmp/$T.c5.p*

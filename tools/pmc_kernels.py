@@ -32,10 +32,17 @@ def main(workload, batch, dominant, out, dirs):
             per = defaultdict(lambda: defaultdict(float))
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    per[(short(r["Kernel_Name"]), r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
-            for (k, _), cs in per.items():
+                    g = r.get("Grid_Size") or r.get("Grid_Size_X") or ""
+                    per[(short(r["Kernel_Name"]), g, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+            for (k, g, _), cs in per.items():
                 for c, v in cs.items():
-                    acc[k][c].append(v)
+                    acc[(k, g)][c].append(v)
+    # a kernel launched with several grid sizes (the warm-history setup's large batches beside the timed steps'
+    # 64 k ones) is reported per grid size: "name [grid G]"
+    grids = defaultdict(set)
+    for k, g in acc:
+        grids[k].add(g)
+    acc = {(k if len(grids[k]) == 1 else f"{k} [grid {g}]"): cs for (k, g), cs in acc.items()}
     kernels = {}
     for k, cs in acc.items():
         if not any(x in k for x in KEEP):
