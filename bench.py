@@ -503,8 +503,8 @@ class Config3:
 
     def roofline(self, timing):
         sc = getattr(self, "scorer", None)
-        native = bool(sc is not None and sc.native)
-        routed = bool(sc is not None and sc.route)
+        native = bool(getattr(sc, "native", False))
+        routed = bool(getattr(sc, "route", False))
         return forest_roofline(timing, self.N.FD_TIMING_XGB, self.xgb, 8, self.B, self.name,
                                FOREST_KERNEL.format(d=8, t="f32", k="XGB") + " dominant", [self.xgb, self.ifm],
                                out=1 if routed else 0, wide=not native)
