@@ -110,6 +110,49 @@ def pmc_traffic(workload, B, kernel_symbol):
         return None
 
 
+def pmc_counters(workload, B, groups, live_us):
+    """north_star's counter figures for this workload's hot kernels: from the committed rocprofv3 PMC summary
+    profiles/pmc_<workload>.json (tools/gpu/pmc_r03.sh + tools/pmc_kernels.py, same batch size only), HBM bytes per
+    launch (2*FETCH_SIZE + WRITE_SIZE), L2 hit rate (TCC_HIT / (TCC_HIT + TCC_MISS)) and MFMA busy, joined with
+    THIS run's event-timed average duration of the same launches: achieved HBM GB/s = bytes / duration.
+    groups: {label: ([kernel names in the PMC file], key of live_us)}; a kernel reported per grid size in the file
+    is taken at this batch's grid."""
+    p = REPO / "profiles" / f"pmc_{workload}.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+    except Exception:
+        return None
+    if int(d.get("batch", -1)) != B:
+        return None
+    ks = d.get("kernels", {})
+    grid = (B + 255) // 256 * 256
+    out = {}
+    for label, (names, key) in groups.items():
+        found = []
+        for nm in names:
+            k = ks.get(nm) or ks.get(f"{nm} [grid {grid}]")
+            if k is None or "hbm_bytes_per_launch" not in k:
+                break
+            found.append((nm, k))
+        else:
+            by = sum(k["hbm_bytes_per_launch"] for _, k in found)
+            us = (live_us or {}).get(key)
+            e = {"kernels": names, "hbm_bytes_per_launch": by,
+                 "achieved_GBs": round(by / (us * 1e-6) / 1e9, 2) if us else None, "live_avg_us": us,
+                 "peak_GBs": HBM_PEAK_GBS, "l2_hit_rate": {nm: k.get("l2_hit_rate") for nm, k in found}}
+            mf = {nm: k["mfma_busy"] for nm, k in found if k.get("mfma_busy")}
+            if mf:
+                e["mfma_busy"] = mf
+            out[label] = e
+    if not out:
+        return None
+    out["basis"] = (f"profiles/pmc_{workload}.json (rocprofv3 --pmc, one pass per counter group, kernels serialised "
+                    "by the collection) x this run's HIP-event durations")
+    return out
+
+
 def ensemble_symbol(out, wide):
     return f"fd::anon::ensemble_kernel<8, {out}, {'true' if wide else 'false'}>"
 FOREST6_SYMBOL = "fd::anon::forest_kernel6<8, 24, float, 1, 0>"
@@ -518,6 +561,18 @@ class Config3:
                  N.FD_TIMING_ENSEMBLE: "ensemble (XGBoost + IsolationForest + blend, fused)"}
         return {names[k]: round(ms / max(1, c) * 1e3, 3) for k, (ms, c) in timing.items() if c}
 
+    def counter_groups(self, roof):
+        """the hot kernels whose PMC figures the line carries: the feature pair and the scoring kernel"""
+        lean = getattr(self, "pipe", None)
+        if lean is None:
+            lean = bool(getattr(getattr(getattr(self, "scorer", None), "be", None), "pipelined", True))
+        bucket = "fd::anon::feat_bucket_lean_kernel<1>" if lean else "fd::anon::feat_bucket_kernel<1>"
+        g = {"features": (["fd::anon::feat_slot_kernel", bucket], "features")}
+        sym = (roof or {}).get("kernel_symbol")
+        if sym:
+            g["ensemble"] = ([sym], "ensemble (XGBoost + IsolationForest + blend, fused)")
+        return g
+
     def config(self, world):
         return {"workload": "config3: card-state features (sliding 5m/1h/24h windows, HBM-resident) -> "
                             "XGBoost 500x8 + IsolationForest 100 -> blend/decision, 64k-txn micro-batches",
@@ -554,6 +609,10 @@ class Config5(Config3):
                 "kernel": "lstm_kernel4 (v_mfma_f32_4x4x1_16b_f32, 4 transactions per workgroup)",
                 "kernel_avg_us": round(avg * 1e6, 3), "flops_per_launch": flops, "flops_per_txn": flops // self.B,
                 "note": "latency-bound 1k batch; f32 MFMA = reference fp32 precision"}
+
+    def counter_groups(self, roof):
+        return {"features": (["fd::anon::feat_slot_kernel", "fd::anon::feat_bucket_kernel<1>"], "features"),
+                "lstm_head": ([LSTM4_SYMBOL], "lstm_head")}
 
     def config(self, world):
         c = super().config(world)
@@ -1333,6 +1392,8 @@ def main():
             "parity_vs_oracle": parity,
             "step_launch": "direct kernel launches",
         }
+        if hasattr(wl, "counter_groups"):
+            line["counters"] = pmc_counters(wl.name, args.batch, wl.counter_groups(roof), line["kernel_avg_us"])
         if wl.name in ("config3", "config4", "config5"):
             per_gpu = value / world
             line["pipeline_hbm"] = {"bytes_per_txn": FUSED_BYTES_PER_TXN,
