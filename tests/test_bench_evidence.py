@@ -10,7 +10,7 @@ def test_pmc_traffic_matches_the_running_instantiation():
     assert t is not None and t > 18_000_000  # at least the algorithmic 18.6 MB per launch
     assert bench.pmc_traffic("config4", 1024, sym) is None  # another batch size
     assert bench.pmc_traffic("config4", 65536, bench.ensemble_symbol(1, False)) is None  # not measured (N > 1 form)
-    assert bench.pmc_traffic("config3", 65536, sym) is None  # no file
+    assert bench.pmc_traffic("config9", 65536, sym) is None  # no file
 
 
 def test_pmc_counters_join_live_durations():
