@@ -116,7 +116,7 @@ def pmc_counters(workload, B, groups, live_us):
     launch (2*FETCH_SIZE + WRITE_SIZE), L2 hit rate (TCC_HIT / (TCC_HIT + TCC_MISS)) and MFMA busy, joined with
     THIS run's event-timed average duration of the same launches: achieved HBM GB/s = bytes / duration.
     groups: {label: ([kernel names in the PMC file], key of live_us)}; a kernel reported per grid size in the file
-    is taken at this batch's grid."""
+    is taken at this batch's grid, else at its most frequent grid."""
     p = REPO / "profiles" / f"pmc_{workload}.json"
     if not p.exists():
         return None
@@ -133,6 +133,9 @@ def pmc_counters(workload, B, groups, live_us):
         found = []
         for nm in names:
             k = ks.get(nm) or ks.get(f"{nm} [grid {grid}]")
+            if k is None:  # per grid size, none at the batch's grid: the grid launched most often (the steps)
+                cand = [v for kn, v in ks.items() if kn.startswith(f"{nm} [grid ")]
+                k = max(cand, key=lambda v: v.get("dispatches", 0)) if cand else None
             if k is None or "hbm_bytes_per_launch" not in k:
                 break
             found.append((nm, k))

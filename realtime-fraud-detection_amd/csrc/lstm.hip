@@ -166,8 +166,11 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
                                                     const float* __restrict__ wout, const float* __restrict__ bout,
                                                     int n_out, double* __restrict__ prob) {
 #pragma clang fp contract(off)
-  // h_t and x_t in the A-operand order: (txn i, k) at lane i + 4 (k & 15), register k >> 4
-  __shared__ __attribute__((aligned(16))) float hbuf[2][64][kH / 16];       // 4 KB
+  // h_t and x_t in the A-operand order: (txn i, k) at lane i + 4 (k & 15), register k >> 4. h_t is stored
+  // register-major, [register][lane]: a lane's reads (one word per register) and the cell writes (a wave's 64
+  // lanes cover 64 consecutive words of one register row) are both bank-conflict free. (Lane-major [lane][8],
+  // read as two ds_read_b128, put a wave's 64 writes on 4 banks: PMC 74 % of LDS-active cycles in conflicts.)
+  __shared__ __attribute__((aligned(16))) float hbuf[2][kH / 16][64];       // 4 KB
   __shared__ __attribute__((aligned(16))) float xs[FD_MAX_SEQ_LEN][64];     // 4 KB
   __shared__ float hT[4][kH];
   __shared__ float zs[4][2];
@@ -192,17 +195,18 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
     for (int t = 0; t < T; ++t) {
       f32x4 acc[4] = {f32x4{bcol, bcol, bcol, bcol}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
                       f32x4{0.f, 0.f, 0.f, 0.f}};
-      const f32x4 h0 = *reinterpret_cast<const f32x4*>(&hbuf[t & 1][l][0]);
-      const f32x4 h1 = *reinterpret_cast<const f32x4*>(&hbuf[t & 1][l][4]);
+      float hv[kH / 16];
+#pragma unroll
+      for (int kk = 0; kk < kH / 16; ++kk) hv[kk] = hbuf[t & 1][kk][l];
       mfma_abid16(xs[t][l], &bw[0], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(h0[0], &bw[kI + 0], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(h0[1], &bw[kI + 16], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(h0[2], &bw[kI + 32], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(h0[3], &bw[kI + 48], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(h1[0], &bw[kI + 64], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(h1[1], &bw[kI + 80], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(h1[2], &bw[kI + 96], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(h1[3], &bw[kI + 112], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(hv[0], &bw[kI + 0], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(hv[1], &bw[kI + 16], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(hv[2], &bw[kI + 32], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(hv[3], &bw[kI + 48], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(hv[4], &bw[kI + 64], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(hv[5], &bw[kI + 80], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(hv[6], &bw[kI + 96], acc, std::make_integer_sequence<int, 16>{});
+      mfma_abid16(hv[7], &bw[kI + 112], acc, std::make_integer_sequence<int, 16>{});
       // register r = transaction r of this lane's gate column; after the transpose register j = gate j of
       // transaction q
       float g0 = (acc[0][0] + acc[1][0]) + (acc[2][0] + acc[3][0]);
@@ -213,7 +217,7 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
       const float ig = sigm(g0), fg = sigm(g1), gg = tanh_g(g2), og = sigm(g3);
       c = fg * c + ig * gg;
       h = og * tanh_g(c);
-      hbuf[(t + 1) & 1][q + 4 * (unit & 15)][unit >> 4] = h;
+      hbuf[(t + 1) & 1][unit >> 4][q + 4 * (unit & 15)] = h;
       __syncthreads();
     }
     hT[q][unit] = h;
