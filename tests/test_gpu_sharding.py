@@ -182,12 +182,13 @@ def test_streaming_routed_step_single_rank_matches_direct():
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     engines = []
+    ring = None
     try:
         dev = _dev(tx)
         parts = [{f: t[i * B:(i + 1) * B] for f, t in dev.items()} for i in range(steps)]
         torch.cuda.synchronize()
         res = []
-        for variant in ("direct", "native", "native_nothread", "python"):
+        for variant in ("direct", "native", "native_nothread", "native_hostout", "python"):
             routed = variant != "direct"
             e = FraudEngine(0)
             engines.append(e)
@@ -205,6 +206,13 @@ def test_streaming_routed_step_single_rank_matches_direct():
                 pre = (parts[i + 1], B) if i + 1 < steps and i != 3 else None  # one step without prefetch
                 if i == 1 and variant.startswith("native"):  # a prefetched batch that is not the next one: dropped
                     pre = (parts[3], B)
+                if variant == "native_hostout":  # outputs straight into host-mapped pinned memory (bench loaded loop)
+                    if ring is None:
+                        import bench
+                        ring = bench.HostOutRing(B, steps)
+                    sc.step(parts[i], B, prefetch=pre, out=ring.sets[i])
+                    outs.append(i)
+                    continue
                 out = sc.step(parts[i], B, prefetch=pre)
                 host = [torch.empty(o.shape, dtype=o.dtype, pin_memory=True) for o in out]
                 for h, o in zip(host, out):
@@ -213,6 +221,15 @@ def test_streaming_routed_step_single_rank_matches_direct():
             torch.cuda.synchronize()
             if routed:
                 assert sc.last_counts == ([B], [B])
+            if variant == "native_hostout":
+                import ctypes
+                outs = []
+                for i in range(steps):
+                    h = ring.host[i]
+                    col = lambda off, ct: np.ctypeslib.as_array((ct * B).from_address(h + off)).copy()
+                    outs.append([torch.from_numpy(col(0, ctypes.c_double)), torch.from_numpy(col(8 * B, ctypes.c_double)),
+                                 torch.from_numpy(col(16 * B, ctypes.c_uint8)),
+                                 torch.from_numpy(col(17 * B, ctypes.c_uint8))])
             res.append(outs)
         for other in res[1:]:
             for a, b in zip(res[0], other):
@@ -221,4 +238,6 @@ def test_streaming_routed_step_single_rank_matches_direct():
     finally:
         for e in engines:
             e.close()
+        if ring is not None:
+            ring.close()
         dist.destroy_process_group()
