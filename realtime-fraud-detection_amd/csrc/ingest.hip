@@ -415,7 +415,9 @@ struct Val {
   bool null = true;
 };
 
-__global__ void __launch_bounds__(256) ingest_json_kernel(const unsigned char* __restrict__ buf,
+// 4 waves per SIMD (128 VGPRs, no spills to memory): the members phase is latency-bound per lane, so occupancy
+// is the lever (142 VGPRs gave 3 waves per SIMD)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) ingest_json_kernel(const unsigned char* __restrict__ buf,
                                                           const int64_t* __restrict__ offsets, int64_t n, Tables T,
                                                           fd_ingest_out out, int stop_after) {
   __shared__ __attribute__((aligned(16))) unsigned char stage[kSlots][kStage];
