@@ -231,6 +231,7 @@ struct CardStore {
   int mode = 0;      // fd_window_mode
   int K = 1;         // ring events per card (sliding)
   int S = 0;         // LSTM history events per card (0 = off)
+  int bucket_keys = 0;  // option "bucket_keys": transactions per bucket workgroup (0 auto, features.hip)
   int64_t n_merchants = 0;
   DeviceBuffer headers, keys, ring, merchants, err, seq;  // keys: the compact key array card_slot probes
   // per-batch card grouping (feat_slot -> feat_bucket): per-txn slots, keys per bucket, [NB][C] bucket regions,

@@ -1532,11 +1532,14 @@ __global__ void __launch_bounds__(256) users_ext_load_kernel(CardHeader* H, unsi
 
 unsigned grid_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
-// buckets of a batch of n: NB = the power of two >= n / 128, so a 256-thread bucket workgroup holds ~128
-// cards: one segment per thread (a second round would double the dependent-load chain)
-unsigned buckets_for(int64_t n, int64_t cap) {
+// buckets of a batch of n: NB = the power of two >= n / T, so a 256-thread bucket workgroup holds ~T cards: one
+// segment per thread (a second round would double the dependent-load chain). T = 128 for throughput batches; a
+// latency batch (< 8192 transactions) would leave most CUs idle with 128 (8 workgroups for 1 k), so it takes 16
+// per bucket: 64 workgroups, each with a 16-key rank sort instead of 128 (engine option bucket_keys overrides)
+unsigned buckets_for(int64_t n, int64_t cap, int keys) {
+  const int64_t T = keys > 0 ? keys : (n < 8192 ? 16 : 128);
   unsigned nb = 1;
-  while ((int64_t)nb * 128 < n && nb < (unsigned)kMaxBuckets && (int64_t)nb < cap) nb <<= 1;
+  while ((int64_t)nb * T < n && nb < (unsigned)kMaxBuckets && (int64_t)nb < cap) nb <<= 1;
   return nb;
 }
 
@@ -1667,7 +1670,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   g.slot.ensure((size_t)n * 4);
   g.prep.ensure((size_t)n * sizeof(Prep));
   if (st.merchants.ptr == nullptr) st.merchants.ensure(16);
-  const unsigned nb = buckets_for(n, st.cap);
+  const unsigned nb = buckets_for(n, st.cap, st.bucket_keys);
   // bucket capacity: 4x the mean (Poisson tail beyond it is negligible for hashed cards; skewed batches spill
   // to the overflow list), a multiple of 64
   const unsigned C = (unsigned)std::max<int64_t>(512, ((4 * ((n + nb - 1) / nb)) + 63) / 64 * 64);

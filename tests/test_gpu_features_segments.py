@@ -185,3 +185,20 @@ def test_routed_records_equal_soa_path(engine):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.parametrize("keys", [0, 16, 128])
+def test_latency_batch_bucket_sizes(engine, keys):
+    """Latency batches (< 8192 transactions) group ~16 transactions per bucket workgroup by default (engine option
+    bucket_keys 0), so a 1 k batch spreads over 64 workgroups instead of 8: the same features as the oracle for the
+    default, a forced 16 and the throughput batches' 128, with a hot card holding 300 of a 1 k batch (one bucket
+    far beyond its mean: the oversized-bucket passes) and batch sizes that are not powers of two."""
+    engine.set_option("bucket_keys", keys)
+    try:
+        pop, orc = _pair(engine, 1, 16, 20000, seed=21)
+        tx = synth.txn_stream(pop, 6000, seed=22, rate_per_s=50.0)
+        rng = np.random.default_rng(23)
+        tx = _with_hot(tx, pop["users"]["key"][11], np.sort(rng.choice(1000, 300, replace=False)))
+        _run(engine, orc, tx, [0, 1000, 1700, 4000, 6000])
+    finally:
+        engine.set_option("bucket_keys", 0)
