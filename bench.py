@@ -130,19 +130,21 @@ def pmc_counters(workload, B, groups, live_us):
     grid = (B + 255) // 256 * 256
     out = {}
     for label, (names, key) in groups.items():
-        found = []
+        found, used = [], []
         for nm in names:
-            k = ks.get(nm) or ks.get(f"{nm} [grid {grid}]")
+            kn = nm if nm in ks else f"{nm} [grid {grid}]"
+            k = ks.get(kn)
             if k is None:  # per grid size, none at the batch's grid: the grid launched most often (the steps)
-                cand = [v for kn, v in ks.items() if kn.startswith(f"{nm} [grid ")]
-                k = max(cand, key=lambda v: v.get("dispatches", 0)) if cand else None
+                cand = [(x, v) for x, v in ks.items() if x.startswith(f"{nm} [grid ")]
+                kn, k = max(cand, key=lambda xv: xv[1].get("dispatches", 0)) if cand else (None, None)
             if k is None or "hbm_bytes_per_launch" not in k:
                 break
             found.append((nm, k))
+            used.append(kn)
         else:
             by = sum(k["hbm_bytes_per_launch"] for _, k in found)
             us = (live_us or {}).get(key)
-            e = {"kernels": names, "hbm_bytes_per_launch": by,
+            e = {"kernels": names, "pmc_entries": used, "hbm_bytes_per_launch": by,
                  "achieved_GBs": round(by / (us * 1e-6) / 1e9, 2) if us else None, "live_avg_us": us,
                  "peak_GBs": HBM_PEAK_GBS, "l2_hit_rate": {nm: k.get("l2_hit_rate") for nm, k in found}}
             mf = {nm: k["mfma_busy"] for nm, k in found if k.get("mfma_busy")}
