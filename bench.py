@@ -218,18 +218,60 @@ def product_blend(names):
 _HIP = None
 
 
-def hip_d2h(dst: int, src: int, nbytes: int, stream: int) -> None:
-    """hipMemcpyAsync device -> pinned host on `stream` (the process's HIP runtime: torch's libamdhip64, loaded
-    globally by fdengine)"""
+def hip_memcpy_async(dst: int, src: int, nbytes: int, kind: int, stream: int) -> None:
+    """hipMemcpyAsync on `stream` (the process's HIP runtime: torch's libamdhip64, loaded globally by fdengine);
+    kind 1 host -> device, 2 device -> host. Straight to the runtime: torch's copy_ between pinned and device memory
+    also does the caching host allocator's per-copy event bookkeeping, measured to stall the host ~6 ms about once
+    per 100-200 copies at this rate"""
     global _HIP
     import ctypes
     if _HIP is None:
         _HIP = ctypes.CDLL(None).hipMemcpyAsync
         _HIP.restype = ctypes.c_int
         _HIP.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
-    rc = _HIP(dst, src, nbytes, 2, stream)  # hipMemcpyDeviceToHost
+    rc = _HIP(dst, src, nbytes, kind, stream)
     if rc != 0:
         raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+
+
+def hip_d2h(dst: int, src: int, nbytes: int, stream: int) -> None:
+    hip_memcpy_async(dst, src, nbytes, 2, stream)
+
+
+class PackedColumns:
+    """A micro-batch's input columns packed into one buffer (256-B aligned column offsets), so a host batch
+    crosses PCIe in ONE hipMemcpyAsync: `host` pinned blocks (one per batch) and two device staging blocks with
+    per-field views."""
+
+    def __init__(self, like: dict, n_host: int, device):
+        import torch
+        from fdengine import _native as N
+        self.layout, off = [], 0
+        for f in N.TXN_FIELDS:
+            t = like[f]
+            nb = t.numel() * t.element_size()
+            self.layout.append((f, off, t.dtype, t.numel()))
+            off += (nb + 255) // 256 * 256
+        self.nbytes = off
+        self.host = []
+        for _ in range(n_host):
+            self.host.append(torch.empty(self.nbytes, dtype=torch.uint8).pin_memory())
+        self.dev = [torch.empty(self.nbytes, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.dev_views = [self.views(d) for d in self.dev]
+
+    def views(self, buf) -> dict:
+        return {f: buf[off:off + n * _itemsize(dt)].view(dt) for f, off, dt, n in self.layout}
+
+    def fill(self, q: int, cols: dict) -> None:
+        """host block q <- the columns (host tensors)"""
+        v = self.views(self.host[q])
+        for f, _, _, _ in self.layout:
+            v[f].copy_(cols[f])
+
+
+def _itemsize(dt) -> int:
+    import torch
+    return torch.empty(0, dtype=dt).element_size()
 
 
 class HostOutRing:
@@ -669,7 +711,10 @@ class Config4(Config3):
         self.params, self.weights, self.mults = product_blend(self.names)
         n_own_est = self.cards // self.world
         cap = 1
-        while cap < int(n_own_est * 1.6) + 65536:
+        # load factor ~0.75 (1.25 slots per owned card, as a power of two): the open-addressed key array stays a
+        # linear probe of a line or two, and 100 M cards with K = 64 ring events (1152 B per slot) fit one GPU's HBM
+        # (2^27 slots = 155 GB); the same factor at every N keeps the per-GPU work the same (weak scaling)
+        while cap < int(n_own_est * 1.25) + 65536:
             cap *= 2
         self.cap = cap
         eng.state_init(cap, self.mode, self.K)
@@ -678,13 +723,21 @@ class Config4(Config3):
         self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches \
             + args.loaded_iters + 1
         B = self.B
-        h2d_batches = min(args.latency_iters, 64) if args.latency_iters > 0 else 0
+        h2d_batches = args.latency_iters if args.latency_iters > 0 else 0
         self.warm_info = None
         if self.stream == "warm":
             from fdengine import synth_gpu
+            gather = None
+            if self.world > 1 and self.parity_batches:  # the node's parity batches touch cards of every owner
+                import torch.distributed as dist
+
+                def gather(k):
+                    parts = [torch.empty_like(k) for _ in range(self.world)]
+                    dist.all_gather(parts, k)
+                    return torch.cat(parts)
             w = synth_gpu.warm_workload(eng, dev, self.cards, rank, self.world, self.n_batches, B, hours=self.hours,
-                                        keep_batches=self.parity_batches if self.world == 1 else 0,
-                                        host_batches=h2d_batches, log=log)
+                                        keep_batches=self.parity_batches, host_batches=h2d_batches, log=log,
+                                        gather_keys=gather)
             self.dev = w["resident"]
             self.tx = w["head"]  # host copies of the parity batches
             self.hist_rows, self.profiles = w["history_rows"], w["profiles"]
@@ -704,7 +757,7 @@ class Config4(Config3):
             self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f][:self.n_batches * B])).to(dev)
                         for f in N.TXN_FIELDS}
             self.h2d_pool = [{f: torch.from_numpy(np.ascontiguousarray(
-                self.tx[f][(self.n_batches + q) * B:(self.n_batches + q + 1) * B])).pin_memory()
+                self.tx[f][(self.n_batches + q) * B:(self.n_batches + q + 1) * B]))
                 for f in N.TXN_FIELDS} for q in range(h2d_batches)]
             self.hist_rows = None
         # world 1: the stream of resident micro-batches goes through fd_score_batch_pipelined (batch i+1's
@@ -716,12 +769,19 @@ class Config4(Config3):
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
-        # host-resident micro-batches (pinned) for the PCIe-inclusive latency line: H2D of the 35 B/txn columns
-        # on the engine stream, then the step on the staged copy (input_ready event), then the D2H of the results;
-        # fresh batches that continue the stream after the resident ones
-        self.stage = [{f: torch.empty_like(t, device=dev) for f, t in self.h2d_pool[0].items()} for _ in range(2)] \
-            if self.h2d_pool else []
-        self.h2d_bytes = sum(t.numel() * t.element_size() for t in self.h2d_pool[0].values()) if self.h2d_pool else 0
+        # host-resident micro-batches for the PCIe-inclusive latency line, packed into one pinned block each (fresh
+        # batches continuing the stream after the resident ones): ONE H2D of the 35 B/txn columns on the engine
+        # stream, the step on the staged copy (input_ready event), results into host-mapped memory
+        self.h2d = None
+        if self.h2d_pool:
+            self.h2d = PackedColumns(self.h2d_pool[0], len(self.h2d_pool), dev)
+            for q, cols in enumerate(self.h2d_pool):
+                self.h2d.fill(q, cols)
+            self.h2d_pool = self.h2d.host
+            self.h2d_ev = [torch.cuda.Event() for _ in range(2)]
+            for ev in self.h2d_ev:  # created at their first record, before any timed loop
+                ev.record()
+        self.h2d_bytes = self.h2d.nbytes if self.h2d else 0
         self.next_batch = 0
         self.next_h2d = 0
         torch.cuda.synchronize()
@@ -750,17 +810,25 @@ class Config4(Config3):
         self.step(i, out=self.host_out.sets[q % 8])
 
     def step_h2d(self, i):
-        """One micro-batch from pinned host memory: H2D copy, the step on the copy, (fetch: D2H results)."""
+        """One micro-batch from pinned host memory: one H2D copy of the packed columns, the step on the staged copy,
+        its results into host-mapped pinned memory (the engine's output kernel; no D2H call) — or, where the step
+        cannot take host outputs (N > 1 over the Python exchange), a D2H of the results."""
         if self.next_h2d >= len(self.h2d_pool):
             raise RuntimeError("host stream exhausted")
         src = self.h2d_pool[self.next_h2d]
         self.next_h2d += 1
         q = i & 1
-        for f, t in self.stage[q].items():
-            t.copy_(src[f], non_blocking=True)
-        ev = self.torch.cuda.Event()
-        ev.record()
-        self.out = self.scorer.step(self.stage[q], self.B, input_ready=ev)
+        st = self.torch.cuda.current_stream()
+        hip_memcpy_async(self.h2d.dev[q].data_ptr(), src.data_ptr(), self.h2d.nbytes, 1, st.cuda_stream)
+        ev = self.h2d_ev[q]
+        ev.record(st)
+        if self.world > 1 and not self.scorer.native:
+            self.out = self.scorer.step(self.h2d.dev_views[q], self.B, input_ready=ev)
+            self.fetch(i)
+            return
+        if self.host_out is None:
+            self.host_out = HostOutRing(self.B, 8)
+        self.out = self.scorer.step(self.h2d.dev_views[q], self.B, input_ready=ev, out=self.host_out.sets[i % 8])
 
     def fetch(self, i):
         """the step's fraud_prob / decision / risk to pinned host memory, queued on the stream (hipMemcpyAsync
@@ -783,9 +851,7 @@ class Config4(Config3):
         independent), replayed before the batches. N>1: every rank steps the same number of batches (the exchange
         is checked by tests/test_sharding.py, gloo, and tests/test_gpu_sharding*.py)."""
         if self.world > 1:
-            for _ in range(self.parity_batches):
-                self.step(0)
-            return None
+            return self._parity_sharded()
         import oracle
         from fdengine import synth
         from oracle.features_c import OracleFeatureState
@@ -808,6 +874,7 @@ class Config4(Config3):
         vec = torch.empty((B, 64), dtype=torch.float32, device=self.dev["ts_ms"].device)
         mp = torch.empty((2, B), dtype=torch.float64, device=vec.device)
         raws = []
+        sat0 = _saturated(self.eng, self)
         for b in range(P):
             part = {f: self.tx[f][b * B:(b + 1) * B] for f in self.N.TXN_FIELDS}
             self.step(b, vectors=vec, model_probs=mp)
@@ -830,8 +897,76 @@ class Config4(Config3):
             out["decision_mismatches"] += int((self.out[2].cpu().numpy() != dec).sum())
             out["risk_mismatches"] += int((self.out[3].cpu().numpy() != risk).sum())
         from fdengine.synth_gpu import occupancy
-        self.occupancy = dict(occupancy(np.concatenate(raws)), basis=f"the {P} parity micro-batches (raw velocity "
+        allraw = np.concatenate(raws)
+        self.occupancy = dict(occupancy(allraw), basis=f"the {P} parity micro-batches (raw velocity "
                               "counts of the oracle, whose vectors equal the engine's)")
+        if sat0 is not None:  # transactions whose 24 h window held all K ring events: engine counter vs oracle
+            out["window_saturated"] = {"engine": _saturated(self.eng, self) - sat0,
+                                       "oracle": int((allraw[:, 11] >= self.K).sum())}
+        del o
+        return out
+
+    def _parity_sharded(self):
+        """N > 1: every rank scores its first parity_batches micro-batches through the product path (ShardedScorer ->
+        fd_sharded_step over RCCL, the next batch prefetched as in the timed steps); rank 0 gathers every rank's
+        batches, results, kept history rows (the owned cards any rank's parity batches touch, warm_workload
+        gather_keys) and profiles, and replays the node's stream through the oracle chain in the order the sharded
+        step defines — step-major, then ingest rank, then index (keyBy, WindowProcessor.java:44,63)."""
+        import torch.distributed as dist
+        np, torch = self.np, self.torch
+        P, B, G = self.parity_batches, self.B, self.world
+        outs = []
+        for b in range(P):
+            self.step(b)
+            outs.append([t.cpu().numpy() for t in self.out])
+        mine = {"head": self.tx, "hist": self.hist_rows, "profiles": self.profiles, "outs": outs,
+                "stream": self.stream}
+        got = [None] * G if self.rank == 0 else None
+        dist.gather_object(mine, got, dst=0)
+        if self.rank != 0:
+            return None
+        import oracle
+        from oracle.features_c import OracleFeatureState
+        o = OracleFeatureState(1 << 23, self.mode, self.K)
+        if self.stream == "warm":
+            prof = {k: np.concatenate([g["profiles"][k] for g in got]) for k in got[0]["profiles"]}
+            _, first = np.unique(prof["key"], return_index=True)
+            prof = {k: v[first] for k, v in prof.items()}
+            o.load_users(prof["key"], prof["avg_amount"], prof["account_age_days"], prof["device_fp"])
+        else:
+            from fdengine import synth
+            at = synth.card_attrs(np.concatenate([g["head"]["card_id"][:P * B] for g in got]), 42)
+            _, first = np.unique(at["key"], return_index=True)
+            at = {k: v[first] for k, v in at.items()}
+            o.load_users(at["key"], at["avg_amount"], at["account_age_days"], at["device_fp"])
+        o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
+        hist = [g["hist"] for g in got if g["hist"] is not None and len(g["hist"]["card_key"])]
+        if hist:  # disjoint card sets (each card's history lives on its owner), each in arrival order
+            o.run({f: np.concatenate([h[f] for h in hist]) for f in self.N.TXN_FIELDS}, want_raw=False)
+        out = {"batches_checked": P * G, "ranks": G, "path": "ShardedScorer -> fd_sharded_step (RCCL all-to-all)",
+               "order": "step-major, then ingest rank, then index", "stream": self.stream,
+               "max_abs_prob_diff": 0.0, "max_abs_conf_diff": 0.0, "decision_mismatches": 0, "risk_mismatches": 0,
+               "decision_mismatches_off_threshold": 0, "history_rows_replayed": int(sum(len(h["card_key"])
+                                                                                       for h in hist))}
+        for b in range(P):
+            for r in range(G):
+                part = {f: got[r]["head"][f][b * B:(b + 1) * B] for f in self.N.TXN_FIELDS}
+                _, V = o.run(part, want_raw=False)
+                px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
+                pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
+                fp, conf, dec, risk = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights,
+                                                            self.mults)
+                gfp, gconf, gdec, grisk = got[r]["outs"][b]
+                out["max_abs_prob_diff"] = max(out["max_abs_prob_diff"], float(np.abs(gfp - fp).max()))
+                out["max_abs_conf_diff"] = max(out["max_abs_conf_diff"], float(np.abs(gconf - conf).max()))
+                bad = gdec != dec
+                out["decision_mismatches"] += int(bad.sum())
+                out["risk_mismatches"] += int((grisk != risk).sum())
+                near = np.zeros(len(fp), bool)  # the f32 XGBoost sigmoid may sit an ulp from the oracle's
+                for thr in (0.6, 0.8, 0.95):
+                    near |= np.abs(fp - thr) < 1e-6
+                near |= np.abs(conf - 0.7) < 1e-6
+                out["decision_mismatches_off_threshold"] += int((bad & ~near).sum())
         del o
         return out
 
@@ -1094,6 +1229,16 @@ WORKLOADS = {"config2": Config2, "config3": Config3, "config4": Config4, "config
              "config3j": Config3J}
 
 
+def _saturated(eng, wl):
+    """the engine's cumulative window_saturated counter (sliding-window workloads; None otherwise)"""
+    if getattr(wl, "mode", 0) != 1 or not hasattr(wl, "K"):
+        return None
+    try:
+        return eng.counter("window_saturated")
+    except Exception:
+        return None
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -1136,7 +1281,9 @@ def make_parser():
     ap.add_argument("--cards", type=int, default=None,
                     help="cards resident in HBM (config4 default 100M over the node; config3 default 10M)")
     ap.add_argument("--window", choices=["sliding", "redis"], default="sliding")
-    ap.add_argument("--ring-k", type=int, default=16)
+    ap.add_argument("--ring-k", type=int, default=64,
+                    help="sliding windows: ring events per card (the bench line reports window_saturation: "
+                         "transactions whose 24 h window held all K)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -1234,6 +1381,9 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    sat0 = _saturated(eng, wl)
+    if dist:
+        dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
         wl.step(i)
@@ -1245,6 +1395,17 @@ def main():
     eng.set_timing(False)
     timing = eng.read_timing()
     elapsed = t1 - t0
+    saturation = None
+    if sat0 is not None:
+        sat = _saturated(eng, wl) - sat0
+        if dist:
+            t = torch.tensor([sat], dtype=torch.int64, device=dev if DIST_BACKEND == "nccl" else "cpu")
+            dist.all_reduce(t)
+            sat = int(t.item())
+        tot = world * args.steps * args.batch
+        saturation = {"transactions": sat, "of": tot, "frac": round(sat / tot, 8), "ring_k": wl.K,
+                      "basis": "timed steps' transactions whose 24 h window held all ring_k prior events of the card "
+                               "(engine counter window_saturated; their 24 h count / amount may be truncated at K)"}
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1322,14 +1483,14 @@ def main():
     if hasattr(wl, "step_h2d") and args.latency_iters > 0:
         for i in range(min(args.latency_iters, len(getattr(wl, "h2d_pool", [])) or args.latency_iters)):
             a = time.perf_counter()
-            wl.step_h2d(i)
-            wl.fetch(i)
+            wl.step_h2d(i)  # H2D, the step, results in host memory
             stream.synchronize()
             lat_h2d.append(time.perf_counter() - a)
+    p99_h2d = float(np.percentile(np.array(lat_h2d) * 1e3, 99)) if lat_h2d else -1.0
     if dist:  # the node's p99: the worst rank's
-        t = torch.tensor([p99], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
+        t = torch.tensor([p99, p99_h2d], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        p99 = float(t.item())
+        p99, p99_h2d = (float(v) for v in t.tolist())
 
     # the same kernels one micro-batch at a time, nothing beside them (in the pipelined stream the next batch's
     # feature kernels share the CUs with the forests): each kernel's unshared duration
@@ -1383,8 +1544,10 @@ def main():
             "p50_batch_latency_ms": round(float(np.percentile(lat_ms, 50)), 4),
             "p99_batch_latency_ms": round(p99, 4),
             "max_batch_latency_ms": round(float(lat_ms.max()), 4),
-            "p99_batch_latency_with_h2d_ms": (round(float(np.percentile(np.array(lat_h2d) * 1e3, 99)), 4)
+            "p99_batch_latency_with_h2d_ms": round(p99_h2d, 4) if lat_h2d else None,
+            "p50_batch_latency_with_h2d_ms": (round(float(np.percentile(np.array(lat_h2d) * 1e3, 50)), 4)
                                               if lat_h2d else None),
+            "latency_h2d_samples": len(lat_h2d),
             "latency_samples": len(lat),
             "latency_basis": "p50/p99/max: one micro-batch at a time (submit -> scores in host memory, then the next); "
                              "loaded_latency: at the throughput operating point",
@@ -1395,6 +1558,7 @@ def main():
             "kernel_timing": f"HIP events on the launch stream, 1 launch in {TIMING_EVERY} of each kernel, timed region",
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
+            "window_saturation": saturation,
             "step_launch": "direct kernel launches",
         }
         if hasattr(wl, "counter_groups"):

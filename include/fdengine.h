@@ -437,24 +437,33 @@ int fd_score_records_pipelined(fd_engine* eng, const fd_blend_params* params, co
                                const uint8_t* present, const void* d_records, int64_t n, void* d_results,
                                void* input_ready);
 /* The sharded step as one call over the engine's own RCCL communicators (csrc/comm.hip): the host loads
-   RCCL once (the process's librccl.so, by path), rank 0 makes two unique ids (fd_comm_unique_id), the host
-   broadcasts them, every rank calls fd_comm_init (collective, blocking). fd_sharded_step then runs one
-   micro-batch: its split sizes (exchanged by the previous call when it prefetched this batch, else now: the
+   RCCL once (the process's librccl.so, by path; any library exporting ncclGetUniqueId, ncclCommInitRank,
+   ncclCommDestroy, ncclGroupStart/End, ncclSend/Recv and ncclGetErrorString can stand in — the tests run several
+   ranks on one GPU over an in-process loopback of that API), rank 0 makes two unique ids (fd_comm_unique_id), the
+   host broadcasts them, every rank calls fd_comm_init (collective, blocking with RCCL). fd_sharded_step then runs
+   one micro-batch: its split sizes (exchanged by the previous call when it prefetched this batch, else now: the
    step's one host wait), the next batch's partition and count exchange (`next`, optional: prefetch; queued on
    the forward stream ahead of this batch's records, so they land while this batch is scored), the records to
    their owners (grouped ncclSend/ncclRecv with per-peer counts, on the engine's forward stream), the owner's
    features + scoring (fd_score_records_pipelined's pipeline, the features waiting for the records), the
    results back (second communicator, engine stream) and into arrival order in the caller's outputs (device or
-   host-mapped memory), written on the engine stream. Every rank makes the same calls in the same order (the same
-   prefetch pattern). split_sizes (optional): the 2 x world send / receive counts of this batch. */
+   host-mapped memory), written on the engine stream. The calling thread issues every communicator operation, in
+   one fixed order; every rank makes the same calls in the same order (the same prefetch pattern).
+   Batch ids (caller-chosen): `next_id` (nonzero) names the prefetched batch; the call that scores it passes the
+   same id as `batch_id`. batch_id 0 means "not the prefetched batch": a pending prefetch is dropped (its count
+   exchange completes, its records are never sent — every rank must drop alike). A nonzero batch_id that is not
+   the pending one (or with nothing pending) fails with FD_ERR_INVALID_ARG and changes nothing. The caller keeps a prefetched batch's input
+   columns alive and unchanged until the call that scores (or drops) it has returned.
+   split_sizes (optional): the 2 x world send / receive counts of this batch. */
 int fd_comm_unique_id(const char* rccl_path, uint8_t* id_out /* 128 bytes */);
 int fd_comm_init(fd_engine* eng, const char* rccl_path, int32_t rank, int32_t world, const uint8_t* id_fwd,
                  const uint8_t* id_back);
 int fd_comm_destroy(fd_engine* eng);
 int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t* slots, const uint8_t* present,
-                    const fd_txn_batch* txns, int64_t n, void* input_ready, const fd_txn_batch* next,
-                    int64_t next_n, void* next_ready, double* d_fraud_prob, double* d_confidence,
-                    uint8_t* d_decision, uint8_t* d_risk, int64_t* split_sizes);
+                    const fd_txn_batch* txns, int64_t n, uint64_t batch_id, void* input_ready,
+                    const fd_txn_batch* next, int64_t next_n, uint64_t next_id, void* next_ready,
+                    double* d_fraud_prob, double* d_confidence, uint8_t* d_decision, uint8_t* d_risk,
+                    int64_t* split_sizes);
 /* out[seq] = result for each of the n returned records; conf/decision/risk may be NULL.
    fd_engine_sync reports a record whose seq is outside [0, n). */
 int fd_route_scatter_results_device(fd_engine* eng, const void* d_results, int64_t n, double* d_fraud_prob,
@@ -656,21 +665,20 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      forests after the first on one side stream (0.095), 2 on two side streams (0.095)
      "pipeline_lean": fd_score_batch_pipelined's bucket pass, 1 (default) the lean kernel that fits beside the
      fused ensemble kernel, 0 the full bucket kernel
-     "sharded_fwd_thread": fd_sharded_step with `next`, 1 (default) the next batch's forward half (partition,
-     count exchange, split-size wait, records exchange) on a worker thread of the engine's while the caller's
-     thread launches this batch's scoring and results; 0 all on the caller's thread. Every rank must use the same
-     value (it orders the forward communicator's operations); fd_engine_sync waits for the worker's job.
+     "comm_timeout_ms": fd_sharded_step's split-size wait fails with FD_ERR_HIP after this many ms (default
+     120000): a peer that never posts its counts (a dead rank, a different call pattern) becomes an error, not a hang
      "stream_priority": HIP priorities of the engine's pipeline and forward streams (ROCm keeps a hardware-queue
      pool per priority, so they stop sharing queues with the engine stream and RCCL's streams): 0 all default, 1
      the two pipeline streams high, 2 + the forward stream low, 3 (default) + the forward stream high. Set before
      the first pipelined call and fd_comm_init. */
 int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
-/* Engine counters (diagnostics): "pipelined_batches" (batches through fd_score_batch_pipelined /
+/* Engine counters (diagnostics): "window_saturated" (sliding windows: transactions so far whose 24 h window held the
+   ring's whole capacity K of prior events — their counts may be truncated at K; synchronises the engine's streams),
+   "pipelined_batches" (batches through fd_score_batch_pipelined /
    fd_score_records_pipelined so far), "sharded_steps" (fd_sharded_step calls) and "sharded_host_ns_<phase>" (host
    nanoseconds inside fd_sharded_step by phase: "wait" the split sizes, "partition" / "counts" / "count_copy" the
    next batch's route kernels, count exchange and copy to the host, "records" the records exchange, "score" the
-   owner's pipeline launches, "back" / "scatter" the results exchange and the scatter into arrival order, "join"
-   the caller waiting for the forward worker; the worker's phases are its own thread's time). */
+   owner's pipeline launches, "back" / "scatter" the results exchange and the scatter into arrival order). */
 int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value);
 int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches);
 int fd_timing_reset(fd_engine* eng);

@@ -41,6 +41,7 @@ class OracleFeatureState:
         while cap < capacity:
             cap *= 2
         self.h = self.L.orc_state_new(cap, window_mode, ring_k)
+        self.mode, self.K = int(window_mode), int(ring_k)
 
     def __del__(self):
         if getattr(self, "h", None):

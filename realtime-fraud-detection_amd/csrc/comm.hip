@@ -7,14 +7,18 @@
 // step is one C-ABI call and no Python collective sits between the kernels.
 //
 // RCCL is the one the host process already loaded (torch's librccl.so, passed by path): dlopen on the same file
-// returns that instance, so the process keeps one RCCL and one HIP runtime. Two communicators per engine: `fwd`
-// (count and record exchanges, on the engine's forward stream) and `back` (results, on the engine stream); each
-// carries its operations in the same order on every rank.
+// returns that instance, so the process keeps one RCCL and one HIP runtime. Any library exporting the same eight
+// symbols can stand in (the tests' in-process loopback, tests/native/rccl_loopback.cpp, runs several ranks on one
+// GPU); each communicator remembers the library it came from. Two communicators per engine: `fwd` (count and
+// record exchanges, on the engine's forward stream) and `back` (results, on the engine stream). The calling
+// thread issues all of a step's operations, in the same order on every rank (fd_internal.h, ShardComm).
 #include <dlfcn.h>
+#include <time.h>
 
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -35,8 +39,7 @@ struct RcclApi {
 
 namespace {
 std::mutex g_rccl_mu;
-RcclApi g_rccl;
-std::string g_rccl_path;
+std::map<std::string, RcclApi>* g_rccl = nullptr;  // by library path; entries live for the process
 
 template <class F>
 void sym(void* h, const char* name, F& out) {
@@ -45,13 +48,11 @@ void sym(void* h, const char* name, F& out) {
 }
 
 const RcclApi& rccl(const char* path) {
-  std::lock_guard<std::mutex> lk(g_rccl_mu);
-  if (g_rccl.send) {
-    FD_REQUIRE(!path || !*path || g_rccl_path == path, FD_ERR_INVALID_ARG,
-               "RCCL already loaded from " + g_rccl_path + " (one RCCL per process)");
-    return g_rccl;
-  }
   FD_REQUIRE(path && *path, FD_ERR_INVALID_ARG, "RCCL library path required");
+  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  if (!g_rccl) g_rccl = new std::map<std::string, RcclApi>();
+  auto it = g_rccl->find(path);
+  if (it != g_rccl->end()) return it->second;
   void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
   FD_REQUIRE(h != nullptr, FD_ERR_UNSUPPORTED, std::string("dlopen RCCL failed: ") + dlerror());
   RcclApi a;
@@ -63,10 +64,10 @@ const RcclApi& rccl(const char* path) {
   sym(h, "ncclSend", a.send);
   sym(h, "ncclRecv", a.recv);
   sym(h, "ncclGetErrorString", a.error_string);
-  g_rccl = a;
-  g_rccl_path = path;
-  return g_rccl;
+  return g_rccl->emplace(path, a).first->second;
 }
+
+const RcclApi& api(const ShardComm& c) { return *static_cast<const RcclApi*>(c.api); }
 
 void check(const RcclApi& R, ncclResult_t r, const char* what) {
   if (r != ncclSuccess) throw Error(FD_ERR_HIP, std::string(what) + ": " + R.error_string(r));
@@ -113,6 +114,7 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
   ncclComm_t f = nullptr, k = nullptr;
   check(R, R.comm_init_rank(&f, world, a, rank), "ncclCommInitRank (forward)");
   check(R, R.comm_init_rank(&k, world, b, rank), "ncclCommInitRank (back)");
+  c.api = &R;
   c.fwd = f;
   c.back = k;
   c.rank = rank;
@@ -136,96 +138,18 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
   }
   c.inbox_next = 0;
   c.pending = false;
-  c.next_slot = 0;
-  c.sent[0] = c.sent[1] = false;  // (the count buffers keep their sequence numbers across communicators)
+  c.pending_id = 0;
+  c.next_slot = 0;  // (the count buffers keep their sequence numbers across communicators)
   FD_HIP(hipGetDevice(&c.device));
   c.ready = true;
 }
 
-namespace {
-// the forward worker: one job at a time (comm_post_forward), errors kept for comm_join
-void forward_worker(Engine* ep) {
-  Engine& e = *ep;
-  ShardComm& c = e.comm;
-  (void)hipSetDevice(c.device);  // the HIP device is per host thread
-  std::unique_lock<std::mutex> lk(c.fwd_mu);
-  for (;;) {
-    c.fwd_cv.wait(lk, [&] { return c.fwd_quit || c.fwd_busy; });
-    if (c.fwd_quit) return;
-    const ShardComm::FwdJob j = c.fwd_job;
-    lk.unlock();
-    int code = 0;
-    std::string msg;
-    try {
-      HostLaps L{c};
-      comm_launch_counts(e, j.t, j.n, j.ready, j.slot, L);
-      comm_wait_counts(e, j.slot, j.n, L);
-      comm_send_records(e, j.slot, L);
-    } catch (const Error& x) {
-      code = x.code;
-      msg = x.what();
-    } catch (const std::exception& x) {
-      code = FD_ERR_HIP;
-      msg = x.what();
-    }
-    lk.lock();
-    if (code == 0) c.sent[j.slot] = true;
-    c.fwd_err = code;
-    c.fwd_err_msg = msg;
-    c.fwd_busy = false;
-    c.fwd_cv.notify_all();
-  }
-}
-
-void stop_worker(ShardComm& c) {
-  if (!c.fwd_thr.joinable()) return;
-  {
-    std::lock_guard<std::mutex> lk(c.fwd_mu);
-    c.fwd_quit = true;
-  }
-  c.fwd_cv.notify_all();
-  c.fwd_thr.join();  // a job in flight finishes first (the worker only checks quit between jobs)
-  c.fwd_quit = false;
-  c.fwd_busy = false;
-}
-}  // namespace
-
-void comm_join(Engine& e) {
-  ShardComm& c = e.comm;
-  if (!c.fwd_thr.joinable()) return;
-  std::unique_lock<std::mutex> lk(c.fwd_mu);
-  c.fwd_cv.wait(lk, [&] { return !c.fwd_busy; });
-  if (c.fwd_err) {
-    const int code = c.fwd_err;
-    const std::string msg = c.fwd_err_msg;
-    c.fwd_err = 0;
-    throw Error(code, "sharded step, forward worker: " + msg);
-  }
-}
-
-void comm_post_forward(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot) {
-  ShardComm& c = e.comm;
-  if (!c.fwd_thr.joinable()) c.fwd_thr = std::thread(forward_worker, &e);
-  {
-    std::lock_guard<std::mutex> lk(c.fwd_mu);
-    FD_REQUIRE(!c.fwd_busy, FD_ERR_INVALID_ARG, "forward worker busy (join first)");
-    c.fwd_job.t = t;
-    c.fwd_job.n = n;
-    c.fwd_job.ready = ready;
-    c.fwd_job.slot = slot;
-    c.sent[slot] = false;
-    c.fwd_busy = true;
-  }
-  c.fwd_cv.notify_all();
-}
-
 void comm_destroy(Engine& e) {
   ShardComm& c = e.comm;
-  stop_worker(c);
   if (c.x_fwd) (void)hipStreamSynchronize(c.x_fwd);
   (void)hipStreamSynchronize(e.stream);
   if (c.ready) {
-    const RcclApi& R = rccl(nullptr);
+    const RcclApi& R = api(c);
     if (c.fwd) (void)R.comm_destroy(static_cast<ncclComm_t>(c.fwd));
     if (c.back) (void)R.comm_destroy(static_cast<ncclComm_t>(c.back));
   }
@@ -244,11 +168,11 @@ void comm_destroy(Engine& e) {
   }
   c.back_buf.release();
   c.route_blk.release();
-  c.sent[0] = c.sent[1] = false;
   if (c.x_fwd) (void)hipStreamDestroy(c.x_fwd);
   c.x_fwd = nullptr;
   c.ready = false;
   c.pending = false;
+  c.api = nullptr;
 }
 
 // On the forward stream: the per-owner counts of `t` (send[p] to peer p, recv[p] from it: one int64 each way per
@@ -256,7 +180,7 @@ void comm_destroy(Engine& e) {
 // rec[s]; the host's wait for the counts does not include them)
 void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int s, HostLaps& L) {
   ShardComm& c = e.comm;
-  const RcclApi& R = rccl(nullptr);
+  const RcclApi& R = api(c);
   const int G = c.world;
   hipStream_t st = c.x_fwd;
   if (ready) FD_HIP(hipStreamWaitEvent(st, ready, 0));
@@ -280,24 +204,38 @@ void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t 
   L(3);
 }
 
-// the host wait for slot s's counts, checked against the batch size n, into split[s]
+// the host wait for slot s's counts, checked against the batch size n, into split[s]: a short spin on the slot's
+// sequence word (the counts usually landed during the previous step), then a sleeping poll that also asks the
+// stream (an error ends the wait; an idle stream with the word still behind means the publish was lost) and gives
+// up after the engine's comm_timeout_ms (a peer that never posts its counts: dead rank, different call pattern)
 void comm_wait_counts(Engine& e, int s, int64_t n, HostLaps& L) {
   ShardComm& c = e.comm;
   const int G = c.world;
-  // poll the slot's sequence word; every 4096 polls ask the stream: an error ends the wait, and an idle stream
-  // with the word still behind means the publish was lost
   const auto* hseq = reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(c.h_cnt[s]) + kCntSeqOff);
   const unsigned long long want = c.cnt_seq[s];
-  for (unsigned spins = 1; __atomic_load_n(hseq, __ATOMIC_ACQUIRE) != want; ++spins) {
-    __builtin_ia32_pause();
-    if ((spins & 4095u) == 0) {
+  auto arrived = [&] { return __atomic_load_n(hseq, __ATOMIC_ACQUIRE) == want; };
+  if (!arrived()) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const auto spin_until = t0 + std::chrono::microseconds(40);
+    while (!arrived() && clk::now() < spin_until) __builtin_ia32_pause();
+    const auto deadline = t0 + std::chrono::milliseconds(c.timeout_ms);
+    long nap_ns = 2000;
+    while (!arrived()) {
       const hipError_t q = hipStreamQuery(c.x_fwd);
       if (q == hipSuccess) {
-        FD_REQUIRE(__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == want, FD_ERR_HIP, "split sizes never arrived");
+        FD_REQUIRE(arrived(), FD_ERR_HIP, "split sizes never arrived (slot " + std::to_string(s) + ", sequence " +
+                                              std::to_string(want) + ")");
         break;
       }
       FD_REQUIRE(q == hipErrorNotReady, FD_ERR_HIP, std::string("count exchange: ") + hipGetErrorString(q));
-      if (spins > (1u << 20)) std::this_thread::yield();
+      FD_REQUIRE(clk::now() < deadline, FD_ERR_HIP,
+                 "count exchange timed out after " + std::to_string(c.timeout_ms) + " ms (slot " + std::to_string(s) +
+                     ", sequence " + std::to_string(want) + ", rank " + std::to_string(c.rank) + " of " +
+                     std::to_string(G) + "): a peer did not post its counts");
+      const timespec ts{0, nap_ns};
+      nanosleep(&ts, nullptr);
+      nap_ns = std::min(nap_ns * 2, 50000L);
     }
   }
   int64_t sent = 0;
@@ -336,7 +274,7 @@ void comm_send_records(Engine& e, int s, HostLaps& L) {
 void comm_exchange(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,
                    const int64_t* recv, size_t elem) {
   ShardComm& c = e.comm;
-  const RcclApi& R = rccl(nullptr);
+  const RcclApi& R = api(c);
   const ncclComm_t k = static_cast<ncclComm_t>(back ? c.back : c.fwd);
   const char* sb = static_cast<const char*>(sendbuf);
   char* rb = static_cast<char*>(recvbuf);

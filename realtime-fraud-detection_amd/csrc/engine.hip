@@ -262,10 +262,6 @@ int fd_engine_destroy(fd_engine* eng) {
   if (!eng) return FD_OK;
   { FD_ENGINE_LOCK(eng); }  // wait for a call in flight on another thread (destroying while in use is the caller's bug)
   Engine& e = E(eng);
-  try {
-    fd::comm_join(e);  // the sharded step's forward worker is idle from here (stopped by comm_destroy below)
-  } catch (...) {
-  }
   (void)hipStreamSynchronize(e.stream);
   for (auto& f : e.forests) {
     for (auto* b : {&f.split.bins, &f.split.nan, &f.split.leaves}) b->release();
@@ -331,7 +327,8 @@ int fd_engine_destroy(fd_engine* eng) {
       t.vvals[w].release();
     }
   }
-  for (auto* b : {&e.state.headers, &e.state.keys, &e.state.ring, &e.state.merchants, &e.state.err, &e.state.bucket_scr})
+  for (auto* b : {&e.state.headers, &e.state.keys, &e.state.ring, &e.state.merchants, &e.state.err, &e.state.sat,
+                  &e.state.bucket_scr})
     b->release();
   for (auto& g : e.state.gs)
     for (auto* b : {&g.slot, &g.bucket_fill, &g.pairs, &g.ovf_cnt, &g.ovf_key, &g.ovf_b, &g.prep}) b->release();
@@ -372,7 +369,6 @@ int fd_engine_sync(fd_engine* eng) {
   FD_API_BEGIN
   FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
-  fd::comm_join(e);  // the sharded step's forward worker has queued its job
   FD_HIP(hipStreamSynchronize(e.stream));
   if (e.comm.x_fwd) FD_HIP(hipStreamSynchronize(e.comm.x_fwd));
   for (hipStream_t st : e.pipe_stream)
@@ -399,6 +395,15 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
   const std::string k(key);
   if (k == "pipelined_batches") {  // fd_score_batch_pipelined / fd_score_records_pipelined batches so far
     *value = (int64_t)e.pipe_iter_total;
+  } else if (k == "window_saturated") {  // sliding windows: transactions whose 24 h window held K prior events
+    // (its count may be truncated at the ring capacity); synchronises the engine's streams
+    FD_REQUIRE(e.state.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
+    FD_HIP(hipStreamSynchronize(e.stream));
+    for (hipStream_t st : e.pipe_stream)
+      if (st) FD_HIP(hipStreamSynchronize(st));
+    unsigned long long v = 0;
+    FD_HIP(hipMemcpy(&v, e.state.sat.ptr, 8, hipMemcpyDeviceToHost));
+    *value = (int64_t)v;
   } else if (k == "sharded_steps") {  // fd_sharded_step calls so far
     *value = (int64_t)e.comm.steps.load();
   } else if (k.rfind("sharded_host_ns_", 0) == 0) {  // host time inside fd_sharded_step by phase
@@ -439,12 +444,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "small_streams") {  // latency batches: 2 LSTM | other forests on two side streams, 1 one, 0 none
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "small_streams must be 0, 1 or 2");
     e.small_streams = (int)value;
-  } else if (k == "sharded_fwd_thread") {  // fd_sharded_step: 1 (default) the next batch's forward half on the
-    // engine's worker thread, 0 all on the caller's thread (every rank must use the same value: it orders the
-    // forward communicator's operations)
-    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "sharded_fwd_thread must be 0 or 1");
-    fd::comm_join(e);
-    e.comm.fwd_thread_on = value != 0;
+  } else if (k == "comm_timeout_ms") {  // fd_sharded_step: the split-size wait gives up (FD_ERR_HIP) after this
+    FD_REQUIRE(value >= 1, FD_ERR_INVALID_ARG, "comm_timeout_ms must be >= 1");
+    e.comm.timeout_ms = value;
   } else if (k == "stream_priority") {  // HIP stream priorities (ROCm keeps a hardware-queue pool per priority):
     // 0 all default; 1 the two pipeline streams high; 2 + the sharded step's forward stream low; 3 (default) + it
     // high. Set before the first pipelined call / fd_comm_init (the streams are created then). With every stream
@@ -1082,68 +1084,66 @@ int fd_comm_destroy(fd_engine* eng) {
 }
 
 int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t* slots, const uint8_t* present,
-                    const fd_txn_batch* txns, int64_t n, void* input_ready, const fd_txn_batch* next, int64_t next_n,
-                    void* next_ready, double* d_fraud_prob, double* d_confidence, uint8_t* d_decision,
-                    uint8_t* d_risk, int64_t* split_sizes) {
+                    const fd_txn_batch* txns, int64_t n, uint64_t batch_id, void* input_ready,
+                    const fd_txn_batch* next, int64_t next_n, uint64_t next_id, void* next_ready,
+                    double* d_fraud_prob, double* d_confidence, uint8_t* d_decision, uint8_t* d_risk,
+                    int64_t* split_sizes) {
   FD_API_BEGIN
   FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);
   fd::ShardComm& c = e.comm;
   FD_REQUIRE(c.ready, FD_ERR_NOT_LOADED, "no communicators (fd_comm_init)");
   FD_REQUIRE(params && slots && txns && n >= 0 && (!next || next_n >= 0), FD_ERR_INVALID_ARG, "bad arguments");
+  FD_REQUIRE(!next || next_id != 0, FD_ERR_INVALID_ARG, "a prefetched batch needs a nonzero next_id");
   FD_REQUIRE(params->n_models >= 1 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "bad n_models");
   for (int m = 0; m < params->n_models; ++m)
     FD_REQUIRE(slots[m] >= 0 || (present && !present[m]), FD_ERR_INVALID_ARG,
                "routed scoring needs every present model in a forest slot or FD_SLOT_LSTM");
   FD_REQUIRE(n == 0 || d_fraud_prob, FD_ERR_INVALID_ARG, "null fraud_prob output");
+  // the prefetched batch is named by its id: batch_id 0 drops a pending prefetch (on every rank alike: its count
+  // exchange completes, its records are never sent); any other id must be the pending one
+  const bool use_pending = batch_id != 0;
+  if (use_pending)
+    FD_REQUIRE(c.pending && batch_id == c.pending_id && n == c.pending_n, FD_ERR_INVALID_ARG,
+               "batch " + std::to_string(batch_id) + " (n " + std::to_string(n) + ") is not the prefetched batch " +
+                   std::to_string(c.pending_id) + " (n " + std::to_string(c.pending_n) +
+                   "): pass its id, or 0 to drop the prefetch");
   const int G = c.world;
   fd::HostLaps L{c};
   c.steps.fetch_add(1, std::memory_order_relaxed);
-  fd::comm_join(e);  // the forward worker's job (this batch's forward half, when it was prefetched)
-  L(8);
-  // 1. this batch's split sizes (and records): exchanged by the previous step (prefetch) or now
+  // Every communicator operation below is issued by this thread in one fixed order on every rank:
+  //   [counts of this batch, when not prefetched] -> counts of `next` -> records of this batch (x_fwd, fwd comm)
+  //   -> results of this batch (engine stream, back comm)
+  // 1. this batch's split sizes: exchanged by the previous call (prefetch) or now
   int s;
-  bool have;
-  if (c.pending && c.pending_key == (const void*)txns->card_key && c.pending_n == n) {
+  if (use_pending) {
     s = c.pending_slot;
-    have = c.sent[s];  // the worker also queued its records
-  } else {  // no prefetch, or another batch than the prefetched one (whose exchange is dropped on every rank)
+  } else {
     s = c.next_slot;
     c.next_slot ^= 1;
-    c.sent[s] = false;
     fd::comm_launch_counts(e, *txns, n, static_cast<hipEvent_t>(input_ready), s, L);
-    have = false;
   }
   c.pending = false;
-  if (!have) fd::comm_wait_counts(e, s, n, L);  // the step's one host wait (none when the worker did it)
+  fd::comm_wait_counts(e, s, n, L);  // the step's one host wait (a prefetched batch's counts landed a step ago)
   const int64_t* send = c.split[s];
   const int64_t* recv = c.split[s] + G;
   if (split_sizes)
     for (int p = 0; p < 2 * G; ++p) split_sizes[p] = c.split[s][p];
   int64_t m = 0;
   for (int p = 0; p < G; ++p) m += recv[p];
-  // 2. without the worker: the next batch's partition + counts, ahead, on the forward stream — queued BEFORE this
-  // batch's records, whose exchange waits for an inbox slot (the scoring two batches back): the counts then land
-  // while this batch is still being scored, and the next call's one host wait is already satisfied (measured on
-  // one GPU: with the counts queued after the records, the next call's features started only after this batch's
-  // forests)
-  const bool worker = c.fwd_thread_on && next != nullptr;
-  int ns = -1;
+  // 2. the next batch's partition + counts, on the forward stream ahead of this batch's records (whose exchange may
+  // wait for an inbox slot): the counts land while this batch is scored, and the next call's wait is satisfied
   if (next) {
-    ns = c.next_slot;
+    const int ns = c.next_slot;
     c.next_slot ^= 1;
-    c.sent[ns] = false;
+    fd::comm_launch_counts(e, *next, next_n, static_cast<hipEvent_t>(next_ready), ns, L);
     c.pending = true;
-    c.pending_key = next->card_key;
+    c.pending_id = next_id;
     c.pending_n = next_n;
     c.pending_slot = ns;
-    if (!worker) fd::comm_launch_counts(e, *next, next_n, static_cast<hipEvent_t>(next_ready), ns, L);
   }
   // 3. records to their owners (forward stream), after the owner's previous use of this inbox slot
-  if (!have) fd::comm_send_records(e, s, L);
-  // with the worker: the next batch's whole forward half (partition, counts, its host wait, records) on the worker
-  // thread from here on, while this thread launches this batch's scoring and results
-  if (worker) fd::comm_post_forward(e, *next, next_n, static_cast<hipEvent_t>(next_ready), ns);
+  fd::comm_send_records(e, s, L);
   // 4. the owner's features + scoring on the pipeline (features wait for the records), results on the engine stream
   const int q = c.inbox_of[s];
   if (m)

@@ -234,6 +234,7 @@ struct CardStore {
   int bucket_keys = 0;  // option "bucket_keys": transactions per bucket workgroup (0 auto, features.hip)
   int64_t n_merchants = 0;
   DeviceBuffer headers, keys, ring, merchants, err, seq;  // keys: the compact key array card_slot probes
+  DeviceBuffer sat;  // u64: transactions whose 24 h window held K prior events (counter "window_saturated")
   // per-batch card grouping (feat_slot -> feat_bucket): per-txn slots, keys per bucket, [NB][C] bucket regions,
   // overflow counters by batch parity + the overflow list (key, bucket), prep records. Two sets: the pipelined
   // stream alternates them, so batch i+1's slot kernel runs while batch i's bucket kernel still reads its set.
@@ -284,6 +285,7 @@ struct IngestTables {
 struct ShardComm {
   bool ready = false;
   int rank = 0, world = 1;
+  const void* api = nullptr;  // the RcclApi (comm.hip) of the library fd_comm_init was given
   void* fwd = nullptr;   // ncclComm_t: counts + records, on x_fwd
   void* back = nullptr;  // ncclComm_t: results, on the engine stream
   hipStream_t x_fwd = nullptr;
@@ -304,42 +306,28 @@ struct ShardComm {
   int64_t* h_cnt[2] = {nullptr, nullptr};
   int64_t* d_hcnt[2] = {nullptr, nullptr};  // the same buffers' device addresses
   unsigned long long cnt_seq[2] = {0, 0};  // the sequence the slot's latest publish writes
-  bool pending = false;  // a prefetched batch's counts are in flight (slot pending_slot)
-  const void* pending_key = nullptr;
+  // the prefetched batch (fd_sharded_step's `next`): its caller-given id, size and count slot; its counts are in
+  // flight on x_fwd. A later call names it by that id (never by its address: torch's allocator recycles them).
+  bool pending = false;
+  unsigned long long pending_id = 0;
   int64_t pending_n = 0;
   int pending_slot = 0, next_slot = 0;
-  // a slot whose records exchange is queued (by the forward worker): its checked split sizes, send [G] then recv [G]
-  bool sent[2] = {};
-  int64_t split[2][2 * FD_MAX_SHARDS] = {};
-  // The forward worker (engine option "sharded_fwd_thread", default on): a host thread of the engine's runs the
-  // NEXT batch's forward half — partition, count exchange, split-size wait, records exchange, all on x_fwd and the
-  // fwd communicator — while the caller's thread launches this batch's scoring, results and scatter (engine
-  // stream, back communicator). Either half is ~60 us of HIP / RCCL host calls; serial they were ~120 us per
-  // step, above the GPU's ~90. One job at a time; the caller joins it before touching the forward half again.
-  bool fwd_thread_on = true;
-  std::thread fwd_thr;
-  std::mutex fwd_mu;
-  std::condition_variable fwd_cv;
-  bool fwd_quit = false, fwd_busy = false;
-  struct FwdJob {
-    fd_txn_batch t{};
-    int64_t n = 0;
-    hipEvent_t ready = nullptr;
-    int slot = 0;
-  } fwd_job;
-  int fwd_err = 0;
-  std::string fwd_err_msg;
+  int64_t split[2][2 * FD_MAX_SHARDS] = {};  // a slot's checked split sizes, send [G] then recv [G]
+  // Every communicator operation of a step is issued by the calling thread, in one fixed order on every rank
+  // (counts of batch i+1, records of batch i on x_fwd; results of batch i on the engine stream): RCCL kernels block
+  // on their peers, and ops of two communicators issued from two threads could reach a shared hardware queue in
+  // opposite orders on two ranks. (Round 3 ran the next batch's forward half on a worker thread; it measured no
+  // faster - 0.0932 vs 0.0943 ms per step, profiles/r03/route_overhead_stream_priority_p1.log - and had that hazard.)
+  int64_t timeout_ms = 120000;  // option "comm_timeout_ms": the split-size wait gives up (FD_ERR_HIP) after this
   int device = 0;
-  // host time inside fd_sharded_step by phase (ns, counters "sharded_host_ns_<phase>", kShardHostPhase order;
-  // the forward worker's phases are its own thread's time)
-  static constexpr int kHostPhases = 9;
+  // host time inside fd_sharded_step by phase (ns, counters "sharded_host_ns_<phase>", kShardHostPhase order)
+  static constexpr int kHostPhases = 8;
   std::atomic<unsigned long long> steps{0}, host_ns[kHostPhases] = {};
 };
 // "wait": the split sizes; "partition", "counts", "count_copy": a batch's route kernels, count exchange and copy to
-// the host; "records": the records exchange; "score": the owner's pipeline; "back", "scatter": results; "join": the
-// caller waiting for the forward worker's job
+// the host; "records": the records exchange; "score": the owner's pipeline; "back", "scatter": results
 inline const char* const kShardHostPhase[ShardComm::kHostPhases] = {
-    "wait", "partition", "counts", "count_copy", "records", "score", "back", "scatter", "join"};
+    "wait", "partition", "counts", "count_copy", "records", "score", "back", "scatter"};
 // per-thread phase clock: lap(ph) adds the time since the previous lap to phase ph
 struct HostLaps {
   ShardComm& c;
@@ -517,8 +505,6 @@ void comm_destroy(Engine& e);
 void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot, HostLaps& L);
 void comm_wait_counts(Engine& e, int slot, int64_t n, HostLaps& L);  // host wait; split[slot] checked
 void comm_send_records(Engine& e, int slot, HostLaps& L);            // records exchange behind the inbox slot
-void comm_post_forward(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot);  // to the worker
-void comm_join(Engine& e);  // wait for the worker's job; rethrows its error
 void comm_exchange(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,
                    const int64_t* recv, size_t elem);
 // lstm.hip

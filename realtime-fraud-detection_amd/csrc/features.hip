@@ -407,9 +407,14 @@ struct Outputs {
   float* seq;     // [n][S][16] LSTM input sequences or null
   float* seq_ring;  // [cap][S][16] per-card LSTM history (S > 0)
   int S;
+  // sliding mode: transactions whose 24 h window held the ring's whole capacity K of prior events (the count may
+  // be truncated there: the reference's counters are unbounded, RedisTransactionSink.java:93-105); null otherwise
+  unsigned long long* sat;
+  int K;
 };
 
 __device__ __forceinline__ void emit(const Outputs& o, int64_t i, const double* r, long long s5, float o1, float dv0) {
+  if (o.sat && r[11] >= (double)o.K) atomicAdd(o.sat, 1ull);  // rare: the card's last K events all within 24 h
   if (o.raw) {
     double2* ro = reinterpret_cast<double2*>(o.raw + (size_t)i * FD_RAW_FEATURES);
 #pragma unroll
@@ -1566,6 +1571,7 @@ void state_init(Engine& e, const fd_state_params& p) {
   // allocates for the new capacity)
   st.uext.release();
   st.err.ensure(16);
+  st.sat.ensure(8);
   for (auto& g : st.gs) {
     g.bucket_fill.ensure(kMaxBuckets * sizeof(unsigned));
     g.ovf_cnt.ensure(2 * sizeof(unsigned));
@@ -1581,6 +1587,7 @@ void state_clear(Engine& e) {
   FD_HIP(hipMemsetAsync(st.keys.ptr, 0, (size_t)st.cap * sizeof(unsigned long long), e.stream));
   if (st.uext.ptr) FD_HIP(hipMemsetAsync(st.uext.ptr, 0, (size_t)st.cap * sizeof(UserExt), e.stream));
   FD_HIP(hipMemsetAsync(st.err.ptr, 0, 16, e.stream));
+  FD_HIP(hipMemsetAsync(st.sat.ptr, 0, 8, e.stream));
   for (auto& g : st.gs) {
     FD_HIP(hipMemsetAsync(g.bucket_fill.ptr, 0, kMaxBuckets * sizeof(unsigned), e.stream));
     FD_HIP(hipMemsetAsync(g.ovf_cnt.ptr, 0, 2 * sizeof(unsigned), e.stream));
@@ -1703,7 +1710,8 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.K = st.K;
   a.n = n;
   a.prep = g.prep.as<const Prep>();
-  a.out = Outputs{d_vec, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S};
+  a.out = Outputs{d_vec, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S,
+                  st.mode == FD_WINDOW_SLIDING ? st.sat.as<unsigned long long>() : nullptr, st.K};
   a.fill = g.bucket_fill.as<unsigned>();
   a.pairs = g.pairs.as<const unsigned long long>();
   a.C = C;

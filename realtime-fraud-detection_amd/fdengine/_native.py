@@ -272,8 +272,9 @@ SIGNATURES = {
     "fd_comm_unique_id": (C.c_int, [C.c_char_p, _vp]),
     "fd_comm_init": (C.c_int, [_vp, C.c_char_p, _i32, _i32, _vp, _vp]),
     "fd_comm_destroy": (C.c_int, [_vp]),
-    "fd_sharded_step": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, _vp, C.POINTER(fd_txn_batch), _i64, _vp,
-                                  C.POINTER(fd_txn_batch), _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fd_sharded_step": (C.c_int, [_vp, C.POINTER(fd_blend_params), _vp, _vp, C.POINTER(fd_txn_batch), _i64,
+                                  C.c_uint64, _vp, C.POINTER(fd_txn_batch), _i64, C.c_uint64, _vp, _vp, _vp, _vp, _vp,
+                                  _vp]),
     "fd_route_partition_stream": (C.c_int, [_vp, C.POINTER(fd_txn_batch), C.POINTER(fd_window_inputs), _i64, _i32,
                                             _vp, _vp, _vp]),
     "fd_route_scatter_results_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),

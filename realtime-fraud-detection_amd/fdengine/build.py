@@ -122,9 +122,32 @@ def build_oracle(force: bool = False, verbose: bool = True) -> Path:
     return out
 
 
+TEST_NATIVE = REPO_ROOT / "tests" / "native"
+
+
+def build_test_libs(force: bool = False, verbose: bool = True) -> Path:
+    """Test infrastructure: tests/native/rccl_loopback.cpp -> tests/native/build/librccl_loopback.so, the in-process
+    loopback of the eight RCCL entry points the sharded step calls (several ranks on one GPU in the GPU tests)."""
+    src = TEST_NATIVE / "rccl_loopback.cpp"
+    bdir = TEST_NATIVE / "build"
+    bdir.mkdir(exist_ok=True)
+    out = bdir / "librccl_loopback.so"
+    if not force and not _stale(out, [src]):
+        return out
+    tmp = out.with_suffix(".so.tmp")
+    cmd = [_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", str(src), "-o", str(tmp)]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    tmp.replace(out)
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = True) -> None:
     build_engine(force=force, verbose=verbose)
     build_oracle(force=force, verbose=verbose)
+    if (TEST_NATIVE / "rccl_loopback.cpp").exists():
+        build_test_libs(force=force, verbose=verbose)
 
 
 if __name__ == "__main__":

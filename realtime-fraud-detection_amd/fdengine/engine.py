@@ -693,7 +693,9 @@ class PipelinedScorer:
 
 
 class ShardedStep:
-    """fd_sharded_step for a fixed model set (FraudEngine.sharded_scorer): per call only the batch pointers change."""
+    """fd_sharded_step for a fixed model set (FraudEngine.sharded_scorer): per call only the batch pointers change.
+    batch_id / next_id: the C-ABI's prefetch ids (include/fdengine.h): next_id (nonzero) names the prefetched batch,
+    the call that scores it passes it as batch_id; 0 = not the prefetched batch."""
 
     def __init__(self, eng: FraudEngine, params: N.fd_blend_params, slots: Sequence[int],
                  present: Optional[Sequence[int]] = None):
@@ -706,7 +708,8 @@ class ShardedStep:
         self._fn = N.lib.fd_sharded_step
 
     def __call__(self, txn_ptrs: dict, n: int, fp_ptr: int, conf_ptr: int, dec_ptr: int, risk_ptr: int,
-                 input_ready: int = 0, next_ptrs: Optional[dict] = None, next_n: int = 0, next_ready: int = 0) -> None:
+                 input_ready: int = 0, next_ptrs: Optional[dict] = None, next_n: int = 0, next_ready: int = 0,
+                 batch_id: int = 0, next_id: int = 0) -> None:
         for f in N.TXN_FIELDS:
             setattr(self._cur, f, txn_ptrs[f])
         nxt = None
@@ -715,7 +718,7 @@ class ShardedStep:
                 setattr(self._next, f, next_ptrs[f])
             nxt = C.byref(self._next)
         rc = self._fn(self.eng._h, C.byref(self.params), self._sl.ctypes.data, self._pres.ctypes.data,
-                      C.byref(self._cur), int(n), input_ready or None, nxt, int(next_n), next_ready or None,
-                      fp_ptr or None, conf_ptr or None, dec_ptr or None, risk_ptr or None,
+                      C.byref(self._cur), int(n), int(batch_id), input_ready or None, nxt, int(next_n), int(next_id),
+                      next_ready or None, fp_ptr or None, conf_ptr or None, dec_ptr or None, risk_ptr or None,
                       self.split_sizes.ctypes.data)
         N.check(rc, "fd_sharded_step")

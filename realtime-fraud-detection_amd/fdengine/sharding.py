@@ -82,32 +82,47 @@ class EngineShardBackend:
     # ---- the sharded step as one engine call over its own RCCL communicators (fd_comm_init / fd_sharded_step)
     native = False
 
-    def init_comm(self, rank: int, world: int, group=None) -> None:
+    def init_comm(self, rank: int, world: int, group=None, rccl_path: Optional[str] = None, ids=None) -> None:
         """Collective over `group`: rank 0 makes the two RCCL unique ids, every rank joins the engine's communicators
-        (forward: counts + records; back: results). RCCL is the process's own (torch's librccl.so)."""
-        import torch.distributed as dist
-        path = rccl_library_path()
-        ids = [None]
-        if rank == 0:
-            from .engine import FraudEngine
-            ids = [(FraudEngine.comm_unique_id(path), FraudEngine.comm_unique_id(path))]
-        src = dist.get_global_rank(group, 0) if group is not None else 0
-        dist.broadcast_object_list(ids, src=src, group=group)
-        self.eng.comm_init(path, rank, world, ids[0][0], ids[0][1])
+        (forward: counts + records; back: results). RCCL is the process's own (torch's librccl.so) unless
+        `rccl_path` names another library with the same API; `ids` (the two unique ids, made by the caller) skips
+        the broadcast over `group` (ranks that are threads of one process: the loopback tests)."""
+        path = rccl_path or rccl_library_path()
+        if ids is None:
+            import torch.distributed as dist
+            box = [None]
+            if rank == 0:
+                from .engine import FraudEngine
+                box = [(FraudEngine.comm_unique_id(path), FraudEngine.comm_unique_id(path))]
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast_object_list(box, src=src, group=group)
+            ids = box[0]
+        self.eng.comm_init(path, rank, world, ids[0], ids[1])
         self._sharded = self.eng.sharded_scorer(self.params, self.slots, self.present)
+        self._prefetched = None  # (id, the prefetch tuple): kept alive until the call that scores or drops it
+        self._next_id = 0
         self.native = True
 
     def sharded_step(self, txns: dict, n: int, input_ready=None, prefetch=None, out=None):
         """fd_sharded_step: outputs (fresh tensors on torch's current stream, written on the engine stream, or the
-        caller's `out`, see _outputs) and the split sizes; prefetch = (next txns, next n[, next input_ready])"""
+        caller's `out`, see _outputs) and the split sizes; prefetch = (next txns, next n[, next input_ready]).
+        The prefetched batch is named to the engine by an id: this call passes the pending id only when `txns` is
+        the very mapping (or the very tensors) given as the last prefetch, never by comparing addresses; the
+        prefetch's tensors are referenced here until the call that consumes or drops them has returned."""
         res, (fp, conf, dec, risk) = self._outputs(n, out)
-        nxt, nn, nready = None, 0, 0
+        pend = self._prefetched
+        bid = pend[0] if pend is not None and int(pend[1][1]) == int(n) and _same_batch(pend[1][0], txns) else 0
+        nxt, nn, nready, nid = None, 0, 0, 0
         if prefetch is not None:
             nxt = {f: prefetch[0][f].data_ptr() for f in N.TXN_FIELDS}
             nn = int(prefetch[1])
             nready = prefetch[2].cuda_event if len(prefetch) > 2 and prefetch[2] is not None else 0
+            self._next_id += 1
+            nid = self._next_id
         self._sharded({f: txns[f].data_ptr() for f in N.TXN_FIELDS}, n, fp, conf, dec, risk,
-                      input_ready.cuda_event if input_ready is not None else 0, nxt, nn, nready)
+                      input_ready.cuda_event if input_ready is not None else 0, nxt, nn, nready,
+                      batch_id=bid, next_id=nid)
+        self._prefetched = (nid, prefetch) if prefetch is not None else None
         return res, self._sharded.split_sizes
 
     def close_comm(self) -> None:
@@ -281,6 +296,11 @@ class EngineShardBackend:
         return fp, conf, dec, risk
 
 
+def _same_batch(a, b) -> bool:
+    """the same input batch object: the same mapping, or the same tensor objects in every field"""
+    return a is b or all(a[f] is b[f] for f in N.TXN_FIELDS)
+
+
 class _HostCounts:
     """split sizes on their way to the host (pinned buffer + event)"""
 
@@ -300,12 +320,14 @@ class ShardedScorer:
     all-to-all then runs on a second process group over the same ranks, created here (collectively)."""
 
     def __init__(self, backend, rank: int, world: int, group=None, streaming: bool = True, force_route: bool = False,
-                 native: Optional[bool] = None):
+                 native: Optional[bool] = None, comm=None):
         """force_route: route even with one shard (partition, exchanges over a 1-rank process group, scatter) — the
         N > 1 step's own work measured / tested on one GPU (tools/route_overhead.py).
         native: the scoring step as one engine call over the engine's own RCCL communicators (fd_sharded_step);
         default: when the process group is RCCL ("nccl": one GPU per rank) and the backend supports it; else the
-        streaming step in Python over torch.distributed (gloo groups: ranks sharing a GPU, CPU tests)."""
+        streaming step in Python over torch.distributed (gloo groups: ranks sharing a GPU, CPU tests).
+        comm: (library path, (id_fwd, id_back)) for the native step's communicators instead of torch's RCCL and a
+        broadcast over `group` — ranks that are threads of one process (the loopback tests; no process group)."""
         self.be, self.rank, self.world, self.group = backend, int(rank), int(world), group
         self.last_counts = None  # (send, recv) split sizes of the last step, for diagnostics
         self.last_windows = None  # (user windows, merged merchant windows) fired by the last windows step
@@ -317,9 +339,12 @@ class ShardedScorer:
         if self.streaming:
             import torch.distributed as dist
             if native is None:
-                native = hasattr(backend, "init_comm") and dist.get_backend(group) == "nccl"
+                native = comm is not None or (hasattr(backend, "init_comm") and dist.get_backend(group) == "nccl")
             if native:
-                backend.init_comm(self.rank, self.world, group)
+                if comm is not None:
+                    backend.init_comm(self.rank, self.world, group, rccl_path=comm[0], ids=comm[1])
+                else:
+                    backend.init_comm(self.rank, self.world, group)
                 self.native = True
             else:
                 ranks = list(range(self.world)) if group is None else dist.get_process_group_ranks(group)

@@ -206,7 +206,7 @@ T_HISTORY_MS = 1_757_030_400_000  # 2025-09-05 00:00 UTC: where the synthetic hi
 
 def warm_workload(eng, device, n_cards: int, rank: int, world: int, n_batches: int, batch: int, hours: float = 24.0,
                   keep_batches: int = 2, host_batches: int = 0, n_merchants: int = 5000, seed: int = 42,
-                  t_history_ms: int = T_HISTORY_MS, log=None) -> dict:
+                  t_history_ms: int = T_HISTORY_MS, log=None, gather_keys=None) -> dict:
     """The warm-state workload of BASELINE config 4 (and its GPU test) on one rank of `world`:
 
     1. the population of n_cards (synth.card_attrs, hash-derived from the card id) — this rank's owned cards are
@@ -219,6 +219,9 @@ def warm_workload(eng, device, n_cards: int, rank: int, world: int, n_batches: i
     4. host copies of the first keep_batches resident batches, the history rows of the cards they touch and those
        cards' profiles (an oracle replays exactly that: per-card state is independent), and host_batches more
        micro-batches after the resident ones (host memory only: the PCIe-inclusive latency line).
+    gather_keys (world > 1): a collective mapping this rank's kept card keys (int64 device tensor) to every rank's
+    (concatenated): the history rows kept are then those of the OWNED cards any rank's kept batches touch — the
+    rows an oracle of the whole node needs (a card's history lives on its owner only).
     -> dict of the above plus counts and timings."""
     import time
 
@@ -251,9 +254,11 @@ def warm_workload(eng, device, n_cards: int, rank: int, world: int, n_batches: i
     extra = []
     for _ in range(host_batches):
         b = gen.next(batch)
-        extra.append({f: v.cpu().pin_memory() for f, v in ((f, b[f]) for f in TXN_FIELDS)})
+        extra.append({f: b[f].cpu() for f in TXN_FIELDS})
     kr = min(total, keep_batches * batch)
     keep_keys = resident["card_key"][:kr] if kr else None
+    if keep_keys is not None and gather_keys is not None:
+        keep_keys = gather_keys(keep_keys.contiguous())
     t = time.time()
     hist = warm_history(eng, pop_own, n_merchants, seed=900 + rank, t_start_ms=t_history_ms, t_end_ms=T0,
                         keep_keys=keep_keys)

@@ -153,7 +153,10 @@ def test_config4_full_size_warm_pipelined():
     (RedisService.java:178-207), then three 64 k micro-batches submitted back to back through ShardedScorer at
     world 1 over EngineShardBackend(pipelined=True) -> fd_score_batch_pipelined (batch i+1's features overlap
     batch i's forests). Vectors, model probabilities, fraud probability, decision and risk against the oracle chain,
-    which replays the history rows of exactly the cards those batches touch."""
+    which replays the history rows of exactly the cards those batches touch. K = 64 ring events per card (the bench's
+    headline) in 2^27 slots (load factor ~0.78 after the history's unknown-user cards): the engine's
+    window_saturated counter over the three batches equals the oracle's count of transactions whose 24 h window
+    held all K prior events."""
     import torch
 
     import oracle
@@ -161,7 +164,7 @@ def test_config4_full_size_warm_pipelined():
     from fdengine.sharding import EngineShardBackend, ShardedScorer
     from oracle import scoring_ref as S
     from oracle.features_c import OracleFeatureState
-    cards, B, K, P = 100_000_000, 65536, 16, 3
+    cards, B, K, P = 100_000_000, 65536, 64, 3
     merch = synth.merchants_table(5000, seed=100)
     xgb, ifm = _fit_models_oracle()
     names = ["xgboost_primary", "isolation_forest"]
@@ -169,7 +172,7 @@ def test_config4_full_size_warm_pipelined():
     params = FraudEngine.blend_params([w[k] for k in names], [S.CONF_MULT[k] for k in names])
     eng = FraudEngine(0)
     try:
-        eng.state_init(1 << 28, 1, K)
+        eng.state_init(1 << 27, 1, K)
         eng.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
         sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), 0, 1)  # binds torch's stream
         dev = torch.device("cuda", 0)
@@ -180,6 +183,7 @@ def test_config4_full_size_warm_pipelined():
         assert eng.state_info()["cards"] >= cards
         res = wk["resident"]
         got = []
+        sat0 = eng.counter("window_saturated")
         for b in range(P):  # back to back: no sync between the pipelined steps
             vec = torch.empty((B, 64), dtype=torch.float32, device=dev)
             mp = torch.empty((2, B), dtype=torch.float64, device=dev)
@@ -209,6 +213,8 @@ def test_config4_full_size_warm_pipelined():
             np.testing.assert_array_equal(CF, conf)
             np.testing.assert_array_equal(DC, dec)
             np.testing.assert_array_equal(RK, risk)
+        sat = eng.counter("window_saturated") - sat0
+        assert sat == int((np.concatenate(raws)[:, 11] >= K).sum())
         occ = synth_gpu.occupancy(np.concatenate(raws))
         assert occ["mean_events_24h"] > 3.0 and occ["frac_with_24h_history"] > 0.8, occ  # warm windows
         assert occ["mean_events_1h"] > 0.1, occ

@@ -49,11 +49,18 @@ def _pair(engine, mode, K, n_users, seed=1, seq_len=0):
 
 
 def _run(engine, orc, tx, cuts):
+    """batch by batch against the oracle; sliding mode: the engine's window_saturated counter advances by the
+    oracle's count of transactions whose 24 h window held all K prior events"""
+    sat = engine.counter("window_saturated") if orc.mode == 1 else None
     for a, b in zip(cuts[:-1], cuts[1:]):
         part = {k: v[a:b] for k, v in tx.items()}
         vec, raw = engine.features(part, want_raw=True)
         rraw, rvec = orc.run(part)
         _check(vec, raw, rvec, rraw)
+        if sat is not None:
+            now = engine.counter("window_saturated")
+            assert now - sat == int((rraw[:, 11] >= orc.K).sum())
+            sat = now
 
 
 def _with_hot(tx, hot_key, idx):

@@ -1,0 +1,238 @@
+"""GPU: the native N >= 2 sharded step (fd_sharded_step, csrc/comm.hip + engine.hip) executed with 2 and 4 ranks on
+the test box's one GPU, checked against the CPU oracle chain over the global arrival order.
+
+RCCL refuses two ranks on one device, so the ranks here are threads of one process, each driving its own engine
+(its cards' state, loaded with only the users it owns) through ShardedScorer's native path — the code `bench.py
+--gpus N` runs on a node — with the engine's communicators opened on tests/native/build/librccl_loopback.so: the
+eight RCCL entry points the step calls, pairing each ncclSend with its ncclRecv in issue order as a device copy
+(test infrastructure; tests/native/rccl_loopback.cpp). Everything else is the product path: partition + count
+kernels, count exchange, the publish kernel and the host's split-size wait, the prefetch of the next batch one step
+ahead (named by id), the records exchange into the three-inbox ring, the owner's pipelined features + fused
+ensemble writing result records, the results exchange and the scatter into arrival order.
+
+Covered: uneven batch sizes per rank, an empty batch on one rank, a hot card holding 40 % of one batch (skewed owner
+counts), a step without prefetch, a prefetched batch that is not the next one (dropped by id 0 on every rank), a
+wrong nonzero batch id (FD_ERR_INVALID_ARG, nothing issued, the step then runs normally). Oracle order: step-major,
+then ingest rank, then index — the order every card sees its transactions in (WindowProcessor.java:44,63 keyBy).
+Reference: fraud probability / confidence within the north-star 1e-5 (the f32 XGBoost sigmoid may sit an ulp from
+the oracle's), decision / risk exact except within 1e-6 of a threshold."""
+import os
+import threading
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LOOPBACK = Path(__file__).resolve().parent / "native" / "build" / "librccl_loopback.so"
+N_USERS, N_MERCH, STEPS = 3000, 80, 6
+
+
+def _setup(world):
+    from fdengine import iforest_from_sklearn, synth, xgboost_from_json_doc
+    pop = synth.population(N_USERS, N_MERCH, seed=171)
+    sizes = [[3000 - 250 * r for r in range(world)] for _ in range(STEPS)]
+    sizes[2][world - 1] = 0  # an empty batch on the last rank
+    streams = []
+    for r in range(world):
+        tot = sum(s[r] for s in sizes)
+        streams.append(synth.txn_stream(pop, max(tot, 1), seed=172 + r, rate_per_s=2.0))
+    # a hot card: 40 % of rank 0's step-1 batch
+    off = sizes[0][0]
+    hot = np.random.default_rng(5).random(sizes[1][0]) < 0.4
+    streams[0]["card_key"][off:off + sizes[1][0]][hot] = pop["users"]["key"][7]
+    X = synth.feature_matrix(3000, 64, seed=173)
+    xgb = xgboost_from_json_doc(synth.xgboost_doc(80, 8, 64, X, seed=174, p_leaf=0.1))
+    ifm = iforest_from_sklearn(synth.isolation_forest(X.astype(np.float64), n_estimators=30))
+    return pop, streams, sizes, xgb, ifm
+
+
+def _batches(streams, sizes, r):
+    """rank r's per-step slices (start offsets are the cumulative sizes)"""
+    out, off = [], 0
+    for s in range(STEPS):
+        n = sizes[s][r]
+        out.append({k: v[off:off + n] for k, v in streams[r].items()})
+        off += n
+    return out
+
+
+def _engine(pop, owned, xgb, ifm):
+    from fdengine import FraudEngine
+    U, M = pop["users"], pop["merchants"]
+    e = FraudEngine(0)
+    e.state_init(4 * N_USERS + 4096, 1, 16)
+    e.load_users(U["key"][owned], U["avg_amount"][owned], U["account_age_days"][owned], U["device_fp"][owned])
+    e.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+    e.load_forest(0, xgb)
+    e.load_forest(1, ifm)
+    return e
+
+
+def _prefetch_plan(s, parts):
+    """step s's prefetch: the next batch, except step 1 prefetches batch 3 (not the next one: step 2 drops it) and
+    step 3 prefetches nothing"""
+    if s == 1:
+        return parts[3]
+    if s == 3 or s + 1 >= STEPS:
+        return None
+    return parts[s + 1]
+
+
+def _run_ranks(world):
+    import torch
+
+    from fdengine import FraudEngine, NativeError
+    from fdengine._native import TXN_FIELDS
+    from fdengine.sharding import ShardedScorer, EngineShardBackend, owned_mask
+    pop, streams, sizes, xgb, ifm = _setup(world)
+    path = str(LOOPBACK)
+    ids = (FraudEngine.comm_unique_id(path), FraudEngine.comm_unique_id(path))
+    engines = [_engine(pop, owned_mask(pop["users"]["key"], r, world), xgb, ifm) for r in range(world)]
+    dev = [[{f: torch.from_numpy(np.ascontiguousarray(b[f])).cuda() for f in TXN_FIELDS}
+            for b in _batches(streams, sizes, r)] for r in range(world)]
+    torch.cuda.synchronize()
+    params = FraudEngine.blend_params([0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
+    results = [None] * world
+    errors = [None] * world
+    wrong_id = [None] * world
+
+    def rank_main(r):
+        try:
+            torch.cuda.set_device(0)
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                be = EngineShardBackend(engines[r], params, [0, 1], pipelined=True)
+                sc = ShardedScorer(be, r, world, native=True, comm=(path, ids))
+                assert sc.native and sc.streaming
+                outs, counts = [], []
+                for s in range(STEPS):
+                    n = sizes[s][r]
+                    nxt = _prefetch_plan(s, dev[r])
+                    pre = (nxt, len(nxt["card_key"])) if nxt is not None else None
+                    if s == 5:  # a wrong nonzero id for the prefetched batch: refused before any exchange
+                        fp = torch.empty(n, dtype=torch.float64, device="cuda")
+                        try:
+                            be._sharded({f: dev[r][s][f].data_ptr() for f in TXN_FIELDS}, n, fp.data_ptr(), 0, 0, 0,
+                                        batch_id=999)
+                        except NativeError as ex:
+                            wrong_id[r] = str(ex)
+                    out = sc.step(dev[r][s], n, prefetch=pre)
+                    counts.append(sc.last_counts)
+                    host = [torch.empty(o.shape, dtype=o.dtype, pin_memory=True) for o in out]
+                    for h, o in zip(host, out):
+                        h.copy_(o, non_blocking=True)
+                    outs.append(host)  # device outputs dropped at once (allocator reuse under the streams)
+                st.synchronize()
+                engines[r].sync()
+            results[r] = (np.concatenate([np.stack([h[0].numpy(), h[1].numpy(), h[2].numpy().astype(np.float64),
+                                                    h[3].numpy().astype(np.float64)]) for h in outs], axis=1),
+                          counts)
+            be.close_comm()
+        except BaseException as ex:  # reported by the main thread
+            errors[r] = ex
+
+    try:
+        threads = [threading.Thread(target=rank_main, args=(r,), daemon=True) for r in range(world)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=240)
+        if any(t.is_alive() for t in threads):
+            engines = []  # a hung rank still uses its engine: leave them to process teardown
+            raise AssertionError("a rank thread hung")
+        for r, ex in enumerate(errors):
+            if ex is not None:
+                raise AssertionError(f"rank {r} failed: {ex!r}") from ex
+    finally:
+        for e in engines:
+            e.close()
+    return pop, streams, sizes, xgb, ifm, results, wrong_id
+
+
+def _oracle(pop, streams, sizes, xgb, ifm, world):
+    import oracle
+    from oracle.features_c import OracleFeatureState
+    U, M = pop["users"], pop["merchants"]
+    st = OracleFeatureState(4 * N_USERS + 4096, 1, 16)
+    st.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+    st.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+    per = [_batches(streams, sizes, r) for r in range(world)]
+    exp = [[] for _ in range(world)]
+    for s in range(STEPS):
+        for r in range(world):
+            part = per[r][s]
+            if sizes[s][r] == 0:
+                continue
+            _, V = st.run(part, want_raw=False)
+            px, _, _ = oracle.xgb_predict(xgb, V)
+            pi, _, _ = oracle.iforest_predict(ifm, V)
+            fp, conf, dec, risk = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]),
+                                                        [0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
+            exp[r].append(np.stack([fp, conf, dec.astype(np.float64), risk.astype(np.float64)]))
+    return [np.concatenate(e, axis=1) for e in exp]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4])
+def test_native_sharded_step_loopback_matches_oracle(world):
+    from fdengine import shard_of
+    assert LOOPBACK.exists(), "tests/native/build/librccl_loopback.so missing (fdengine/build.py build_test_libs)"
+    pop, streams, sizes, xgb, ifm, results, wrong_id = _run_ranks(world)
+    for r in range(world):
+        assert wrong_id[r] is not None and "not the prefetched batch" in wrong_id[r], wrong_id[r]
+    # split sizes: every rank's send counts are its batch's owner histogram; receive = the peers' sends to it
+    per = [_batches(streams, sizes, r) for r in range(world)]
+    for s in range(STEPS):
+        sends = []
+        for r in range(world):
+            own = shard_of(per[r][s]["card_key"], world)
+            sends.append(np.bincount(own, minlength=world)[:world])
+            assert results[r][1][s][0] == sends[r].tolist()
+        for r in range(world):
+            assert results[r][1][s][1] == [int(sends[p][r]) for p in range(world)]
+    exp = _oracle(pop, streams, sizes, xgb, ifm, world)
+    for r in range(world):
+        g, e = results[r][0], exp[r]
+        assert g.shape == e.shape
+        assert np.abs(g[0] - e[0]).max() <= 1e-5 and np.abs(g[1] - e[1]).max() <= 1e-5
+        near = np.zeros(g.shape[1], bool)
+        for thr in (0.3, 0.6, 0.8, 0.95):
+            near |= np.abs(e[0] - thr) < 1e-6
+        near |= np.abs(e[1] - 0.7) < 1e-6
+        assert ((g[2] == e[2]) | near).all() and ((g[3] == e[3]) | near).all()
+        assert (g[2] == e[2]).mean() > 0.999
+
+
+@pytest.mark.timeout(120)
+def test_missing_peer_is_an_error_not_a_hang():
+    """Rank 1 never steps: rank 0's count exchange cannot complete; the loopback gives up after its timeout and the
+    engine reports the failed group as an error (the product's own guard is the engine option comm_timeout_ms on
+    the split-size wait)."""
+    import torch
+
+    from fdengine import FraudEngine, NativeError
+    from fdengine._native import TXN_FIELDS
+    from fdengine.sharding import EngineShardBackend, ShardedScorer
+    pop, streams, sizes, xgb, ifm = _setup(2)
+    path = str(LOOPBACK)
+    ids = (FraudEngine.comm_unique_id(path), FraudEngine.comm_unique_id(path))
+    e = _engine(pop, np.ones(N_USERS, bool), xgb, ifm)
+    old = os.environ.get("LOOPBACK_TIMEOUT_S")
+    os.environ["LOOPBACK_TIMEOUT_S"] = "2"
+    try:
+        e.set_option("comm_timeout_ms", 3000)
+        b = _batches(streams, sizes, 0)[0]
+        d = {f: torch.from_numpy(np.ascontiguousarray(b[f])).cuda() for f in TXN_FIELDS}
+        sc = ShardedScorer(EngineShardBackend(e, FraudEngine.blend_params([0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5]),
+                                              [0, 1], pipelined=True), 0, 2, native=True, comm=(path, ids))
+        with pytest.raises(NativeError) as ei:
+            sc.step(d, len(d["card_key"]))
+        assert "ncclGroupEnd" in str(ei.value)
+    finally:
+        if old is None:
+            os.environ.pop("LOOPBACK_TIMEOUT_S", None)
+        else:
+            os.environ["LOOPBACK_TIMEOUT_S"] = old
+        e.close()

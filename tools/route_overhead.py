@@ -37,14 +37,11 @@ while cap < int(CARDS * 1.6) + 65536:
 result = {}
 VARIANTS = os.environ.get("VARIANTS", "direct,native,streaming,serial").split(",")
 for name in VARIANTS:
-    fwd_thread = 0 if name.endswith("_nothread") else 1  # native_nothread: fd_sharded_step all on this thread
     name_v = name
-    name = name.removesuffix("_nothread")
     routed = name != "direct"
     eng = fdengine.FraudEngine(0)
     eng.state_init(cap, 1, 16)
     eng.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
-    eng.set_option("sharded_fwd_thread", fwd_thread)
     if os.environ.get("STREAM_PRIORITY"):
         eng.set_option("stream_priority", int(os.environ["STREAM_PRIORITY"]))
     sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), 0, 1, force_route=routed,
@@ -61,7 +58,7 @@ for name in VARIANTS:
 
     run(0, 20)
     torch.cuda.synchronize()
-    PH = ("wait", "partition", "counts", "count_copy", "records", "score", "back", "scatter", "join")
+    PH = ("wait", "partition", "counts", "count_copy", "records", "score", "back", "scatter")
     c0 = {ph: eng.counter("sharded_host_ns_" + ph) for ph in PH} if name == "native" else None
     k0 = eng.counter("sharded_steps") if name == "native" else 0
     t0 = time.perf_counter()
