@@ -93,11 +93,11 @@ def forest_blob_bytes(forest) -> int:
 FOREST_KERNEL = "forest_kernel6<D={d},{t},{k}> (binned node-only chunks)"
 
 
-def pmc_traffic(workload, B, kernel_symbol):
+def pmc_traffic(workload, B, kernel_symbol, root=None):
     """HBM bytes per launch of `kernel_symbol` (its demangled name as rocprofv3 reports it) from the committed
     rocprofv3 PMC summary profiles/pmc_<workload>.json; None unless that file measured this kernel at this batch
     size (a summary of another kernel, e.g. an older build's, is never reported as this one's traffic)."""
-    p = REPO / "profiles" / f"pmc_{workload}.json"
+    p = Path(root or REPO / "profiles") / f"pmc_{workload}.json"
     if not p.exists():
         return None
     try:
@@ -110,14 +110,15 @@ def pmc_traffic(workload, B, kernel_symbol):
         return None
 
 
-def pmc_counters(workload, B, groups, live_us):
+def pmc_counters(workload, B, groups, live_us, root=None):
     """north_star's counter figures for this workload's hot kernels: from the committed rocprofv3 PMC summary
     profiles/pmc_<workload>.json (tools/gpu/pmc_r03.sh + tools/pmc_kernels.py, same batch size only), HBM bytes per
     launch (2*FETCH_SIZE + WRITE_SIZE), L2 hit rate (TCC_HIT / (TCC_HIT + TCC_MISS)) and MFMA busy, joined with
     THIS run's event-timed average duration of the same launches: achieved HBM GB/s = bytes / duration.
     groups: {label: ([kernel names in the PMC file], key of live_us)}; a kernel reported per grid size in the file
-    is taken at this batch's grid, else at its most frequent grid."""
-    p = REPO / "profiles" / f"pmc_{workload}.json"
+    is taken at this batch's grid only — a group whose kernels were not measured at this grid is omitted (another
+    launch's counters are never reported as this one's)."""
+    p = Path(root or REPO / "profiles") / f"pmc_{workload}.json"
     if not p.exists():
         return None
     try:
@@ -134,9 +135,6 @@ def pmc_counters(workload, B, groups, live_us):
         for nm in names:
             kn = nm if nm in ks else f"{nm} [grid {grid}]"
             k = ks.get(kn)
-            if k is None:  # per grid size, none at the batch's grid: the grid launched most often (the steps)
-                cand = [(x, v) for x, v in ks.items() if x.startswith(f"{nm} [grid ")]
-                kn, k = max(cand, key=lambda xv: xv[1].get("dispatches", 0)) if cand else (None, None)
             if k is None or "hbm_bytes_per_launch" not in k:
                 break
             found.append((nm, k))
@@ -158,8 +156,8 @@ def pmc_counters(workload, B, groups, live_us):
     return out
 
 
-def ensemble_symbol(out, wide):
-    return f"fd::anon::ensemble_kernel<8, {out}, {'true' if wide else 'false'}>"
+def ensemble_symbol(out, wide, top=False):
+    return f"fd::anon::ensemble_kernel<8, {out}, {'true' if wide else 'false'}, {'true' if top else 'false'}>"
 FOREST6_SYMBOL = "fd::anon::forest_kernel6<8, 24, float, 1, 0>"
 LSTM4_SYMBOL = "fd::anon::lstm_kernel4"
 INGEST_SYMBOL = "fd::anon::ingest_json_kernel"
@@ -498,7 +496,7 @@ class Config3:
         eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
         eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
         self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches \
-            + args.loaded_iters + 1
+            + args.loaded_iters + args.timing_steps + 1
         self.tx = synth.txn_stream(self.pop, self.n_batches * self.B, seed=200 + rank)
         self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
         self.elem = {f: self.tx[f].dtype.itemsize for f in N.TXN_FIELDS}
@@ -721,7 +719,7 @@ class Config4(Config3):
         eng.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
         self.parity_batches = args.parity_batches
         self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches \
-            + args.loaded_iters + 1
+            + args.loaded_iters + args.timing_steps + 1
         B = self.B
         h2d_batches = args.latency_iters if args.latency_iters > 0 else 0
         self.warm_info = None
@@ -1297,6 +1295,9 @@ def make_parser():
                     help="steps run one at a time after the latency loop, every launch timed: each kernel's "
                          "duration with nothing beside it (roofline.alone)")
     ap.add_argument("--parity-batches", type=int, default=2)
+    ap.add_argument("--timing-steps", type=int, default=160,
+                    help="back-to-back steps after the timed region, kernel timing still sampled (kernel averages over "
+                         ">= 20 launches even for short --steps)")
     ap.add_argument("--stream", choices=["warm", "cold"], default="warm",
                     help="config4: warm = SURVEY §8(d) stream (Gamma(2,2)+1 txn/card/day, Poisson arrivals) after "
                          "--history-hours of history through the feature path; cold = round 2's uniform stream "
@@ -1392,6 +1393,13 @@ def main():
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
+    # more of the same back-to-back steps, still sampled 1 in TIMING_EVERY, so the kernel averages rest on >= 20
+    # launches of each kernel even when --steps is short (outside the timed region: `value` is unaffected)
+    for i in range(args.timing_steps):
+        wl.step(args.steps + i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
     eng.set_timing(False)
     timing = eng.read_timing()
     elapsed = t1 - t0
@@ -1555,7 +1563,8 @@ def main():
             "roofline": roof,
             "kernel_avg_us": wl.kernels(timing),
             "kernel_avg_us_alone": wl.kernels(timing_alone) if timing_alone else None,
-            "kernel_timing": f"HIP events on the launch stream, 1 launch in {TIMING_EVERY} of each kernel, timed region",
+            "kernel_timing": f"HIP events on the launch stream, 1 launch in {TIMING_EVERY} of each kernel, over the timed "
+                             f"region and {args.timing_steps} more back-to-back steps after it",
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
             "window_saturation": saturation,

@@ -201,9 +201,10 @@ def txn_stream(pop: dict, n: int, seed: int = 7, t0_ms: int = 1_757_030_400_000,
 
 
 def isolation_forest(X_train: np.ndarray, n_estimators: int = 100, contamination: float = 0.05,
-                     random_state: int = 42):
+                     random_state: int = 42, max_samples="auto"):
     from sklearn.ensemble import IsolationForest
-    m = IsolationForest(contamination=contamination, n_estimators=n_estimators, random_state=random_state)
+    m = IsolationForest(contamination=contamination, n_estimators=n_estimators, random_state=random_state,
+                        max_samples=max_samples)
     m.fit(X_train)
     return m
 

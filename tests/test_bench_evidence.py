@@ -1,26 +1,58 @@
 """The bench line's counter evidence is tied to committed PMC files of the kernels that run:
 the roofline's `traffic` and the `counters` object come from profiles/pmc_<workload>.json only when that file
-measured the same kernel instantiation at the same batch size."""
+measured the same kernel instantiation at the same batch size and grid (another launch's counters are
+never reported as this one's). Checked on a synthetic summary in the format tools/pmc_kernels.py writes."""
+import json
+
 import bench
 
 
-def test_pmc_traffic_matches_the_running_instantiation():
-    sym = bench.ensemble_symbol(0, True)  # N = 1: column outputs, wide chunk layout
-    t = bench.pmc_traffic("config4", 65536, sym)
-    assert t is not None and t > 18_000_000  # at least the algorithmic 18.6 MB per launch
-    assert bench.pmc_traffic("config4", 1024, sym) is None  # another batch size
-    assert bench.pmc_traffic("config4", 65536, bench.ensemble_symbol(1, False)) is None  # not measured (N > 1 form)
-    assert bench.pmc_traffic("config9", 65536, sym) is None  # no file
+def _summary(tmp_path, workload="config4", batch=65536):
+    ens = bench.ensemble_symbol(0, True, False)
+    doc = {"batch": batch, "kernels": {
+        ens: {"hbm_bytes_per_launch": 29_700_000, "l2_hit_rate": 0.92, "dispatches": 40},
+        "fd::anon::feat_slot_kernel [grid 65536]": {"hbm_bytes_per_launch": 18_400_000, "l2_hit_rate": 0.69,
+                                                    "dispatches": 40},
+        "fd::anon::feat_slot_kernel [grid 1048576]": {"hbm_bytes_per_launch": 300_000_000, "l2_hit_rate": 0.5,
+                                                      "dispatches": 400},
+        "fd::anon::feat_bucket_lean_kernel<1> [grid 65536]": {"hbm_bytes_per_launch": 53_200_000,
+                                                              "l2_hit_rate": 0.81, "dispatches": 40},
+        "fd::anon::feat_bucket_kernel<1> [grid 1048576]": {"hbm_bytes_per_launch": 500_000_000, "dispatches": 400},
+        bench.LSTM4_SYMBOL: {"hbm_bytes_per_launch": 3_100_000, "mfma_busy": 0.5, "dispatches": 40}}}
+    (tmp_path / f"pmc_{workload}.json").write_text(json.dumps(doc))
+    return ens
 
 
-def test_pmc_counters_join_live_durations():
+def test_pmc_traffic_matches_the_running_instantiation(tmp_path):
+    ens = _summary(tmp_path)
+    assert bench.pmc_traffic("config4", 65536, ens, root=tmp_path) == 29_700_000
+    assert bench.pmc_traffic("config4", 1024, ens, root=tmp_path) is None  # another batch size
+    assert bench.pmc_traffic("config4", 65536, bench.ensemble_symbol(0, True, True), root=tmp_path) is None
+    assert bench.pmc_traffic("config4", 65536, bench.ensemble_symbol(1, False), root=tmp_path) is None
+    assert bench.pmc_traffic("config9", 65536, ens, root=tmp_path) is None  # no file
+
+
+def test_pmc_counters_join_live_durations_at_the_run_grid_only(tmp_path):
+    ens = _summary(tmp_path)
     groups = {"features": (["fd::anon::feat_slot_kernel", "fd::anon::feat_bucket_lean_kernel<1>"], "features"),
-              "ensemble": ([bench.ensemble_symbol(0, True)], "ens")}
-    c = bench.pmc_counters("config4", 65536, groups, {"features": 70.0, "ens": 90.0})
+              "ensemble": ([ens], "ens"),
+              # measured only at another grid (the history's large launches): omitted, not substituted
+              "full_bucket": (["fd::anon::feat_bucket_kernel<1>"], "features")}
+    c = bench.pmc_counters("config4", 65536, groups, {"features": 70.0, "ens": 90.0}, root=tmp_path)
     f, e = c["features"], c["ensemble"]
-    # the 64 k step launch of the slot kernel, not the warm-history setup's large ones
-    assert 1e6 < f["hbm_bytes_per_launch"] < 2e8 and set(f["l2_hit_rate"]) == set(groups["features"][0])
-    assert abs(e["achieved_GBs"] - e["hbm_bytes_per_launch"] / 90e-6 / 1e9) < 0.01
-    c5 = bench.pmc_counters("config5", 1024, {"lstm": ([bench.LSTM4_SYMBOL], "lstm_head")}, {"lstm_head": 22.0})
-    assert 0.0 < c5["lstm"]["mfma_busy"][bench.LSTM4_SYMBOL] <= 1.0
-    assert bench.pmc_counters("config4", 4096, groups, {}) is None
+    assert f["hbm_bytes_per_launch"] == 18_400_000 + 53_200_000
+    assert f["pmc_entries"] == ["fd::anon::feat_slot_kernel [grid 65536]",
+                                "fd::anon::feat_bucket_lean_kernel<1> [grid 65536]"]
+    assert abs(e["achieved_GBs"] - 29_700_000 / 90e-6 / 1e9) < 0.01
+    assert "full_bucket" not in c
+    c5 = bench.pmc_counters("config4", 65536, {"lstm": ([bench.LSTM4_SYMBOL], "lstm_head")}, {"lstm_head": 22.0},
+                            root=tmp_path)
+    assert c5["lstm"]["mfma_busy"][bench.LSTM4_SYMBOL] == 0.5
+    assert bench.pmc_counters("config4", 4096, groups, {}, root=tmp_path) is None
+
+
+def test_committed_summaries_parse():
+    """the committed profiles/pmc_*.json are in the format the lookup reads"""
+    for p in sorted((bench.REPO / "profiles").glob("pmc_*.json")):
+        d = json.loads(p.read_text())
+        assert int(d["batch"]) > 0 and isinstance(d["kernels"], dict), p
