@@ -99,13 +99,16 @@ static fd::PackedForest& slot_of(Engine& e, int slot) {
 static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slots, const double* const* ext,
                          const uint8_t* present, const float* dX, int64_t n, int32_t ld, double* dMP,
                          double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk, const float* d_seq = nullptr,
-                         int T = 0, const fd::RouteRecord* records = nullptr, fd::ResultRecord* results = nullptr) {
+                         int T = 0, const fd::RouteRecord* records = nullptr, fd::ResultRecord* results = nullptr,
+                         bool compact = false) {
   FD_REQUIRE(p.n_models > 0 && p.n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "n_models out of range");
   FD_REQUIRE(slots != nullptr && (dfp != nullptr || results != nullptr), FD_ERR_INVALID_ARG, "null slots/output");
   if (n == 0) return false;
   // one XGBoost + one IsolationForest, large batch: both forests and the blend in one kernel
-  if (fd::launch_ensemble(e, p, slots, present, dX, n, ld, dMP, dfp, dconf, ddec, drisk, records, results))
+  if (fd::launch_ensemble(e, p, slots, present, dX, n, ld, dMP, dfp, dconf, ddec, drisk, records, results, compact))
     return results != nullptr;
+  // compact vectors are written only when the fused kernel applies (pipe_step): any other path is a bug
+  FD_REQUIRE(!compact, FD_ERR_UNSUPPORTED, "internal: compact vectors without the fused ensemble kernel");
   FD_REQUIRE(dfp != nullptr, FD_ERR_INVALID_ARG, "null output");
   const int M = p.n_models;
   if (!dMP) {
@@ -951,6 +954,9 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   // mode 1: the slot pass (scratch set s & 1, untouched by batch i-1) runs at once; the bucket pass waits for
   // batch i-1's card updates
   hipEvent_t before_buckets = e.pipe_feat_live[prev] ? e.pipe_feat_ev[prev] : nullptr;
+  // the fused kernel alone reads the vectors and nobody asked for them: the compact form (96 instead of 256 B per
+  // transaction written here and read by the ensemble kernel, fd_internal.h kCompactSlot)
+  const bool compact = d_vectors == nullptr && fd::ensemble_applies(e, *params, slots, present, n);
   e.pipe_vec[s].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
   float* vec = e.pipe_vec[s].as<float>();
   float* seq = nullptr;
@@ -964,14 +970,14 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
     seq = e.pipe_seq[s].as<float>();
   }
   if (records)
-    fd::launch_features_records(e, records, n, vec, seq, Sf, e.pipe_lean, s, before_buckets);
+    fd::launch_features_records(e, records, n, vec, seq, Sf, e.pipe_lean, s, before_buckets, compact);
   else
-    fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, s, before_buckets);
+    fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, s, before_buckets, compact);
   FD_HIP(hipEventRecord(e.pipe_feat_ev[s], Sf));
   e.pipe_feat_live[s] = true;
   // scoring paths other than the fused kernel share engine scratch (per-model columns, tree-split and LSTM
   // buffers): those batches also wait for the previous batch's scoring
-  if (e.pipe_done_live[prev] && !fd::ensemble_applies(e, *params, slots, present, n))
+  if (e.pipe_done_live[prev] && !compact && !fd::ensemble_applies(e, *params, slots, present, n))
     FD_HIP(hipStreamWaitEvent(Sc, e.pipe_done_ev[prev], 0));
   // this slot's output staging: free once batch i-nbuf's copy to its caller (on e.stream) is done. Routed batches
   // always stage the four columns (the result records are packed from them when the fused kernel does not apply).
@@ -998,7 +1004,7 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
     e.stream = Sc;
     const auto* rec = static_cast<const fd::RouteRecord*>(records);
     if (!score_matrix(e, *params, slots, ext_probs, present, vec, n, FD_VECTOR_WIDTH, s_mp, s_fp, s_conf, s_dec,
-                      s_risk, seq, e.state.S, rec, s_res) &&
+                      s_risk, seq, e.state.S, rec, s_res, compact) &&
         records)
       fd::launch_result_pack(e, s_fp, s_conf, s_dec, s_risk, rec, n, s_res);
   }

@@ -90,6 +90,7 @@ struct EnsArgs {
   const float* thr;
   int thr_off[kMaxFeatures + 1];  // per-feature table offsets into thr (kernel arguments: scalar loads)
   int vec4;                       // rows 16-B aligned (ld % 4 == 0, aligned X): float4 row loads
+  int compact;                    // X rows are the compact vector (kCompactWidth floats), expanded here
   int owner_fixed;                // chunk owner: tree group 0 (the oldest waves: highest issue priority), else rotating
   int n_pass;
   int pass_f[kMaxPass + 1];
@@ -342,6 +343,16 @@ static int g_eprof_next = 0;
 #define FD_ESTAMP(var)
 #endif
 
+// slots [16 Q, 16 Q + 16) of the 64-wide vector from its compact form (fd_internal.h compact_src)
+template <int Q>
+__device__ __forceinline__ void expand_compact(const float (&c)[kCompactWidth], float (&v)[16]) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int src = compact_src(16 * Q + k);  // a constant after unrolling
+    v[k] = src >= 0 ? c[src >= 0 ? src : 0] : (src == -2 ? 0.5f : 0.f);
+  }
+}
+
 template <int D, int OUT, bool WIDE, bool STOP>
 __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   constexpr int kCHA = EnsCfg<WIDE>::CHA, kCHB = EnsCfg<WIDE>::CHB;
@@ -381,7 +392,24 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     // (1) raw values: thread (q, txn) loads features [16 q, 16 q + 16) of its row in one go (all loads in
     // flight together) and keeps them in registers until they are binned
     float v[16];
-    if (valid) {
+    if (valid && a.compact) {  // the pipeline's compact row (6 x 16 B), expanded to this thread's 16 slots
+      const float4* x4 = reinterpret_cast<const float4*>(a.X + row * (int64_t)kCompactWidth);
+      float c[kCompactWidth];
+#pragma unroll
+      for (int k = 0; k < kCompactWidth / 4; ++k) {
+        const float4 t = x4[k];
+        c[4 * k] = t.x;
+        c[4 * k + 1] = t.y;
+        c[4 * k + 2] = t.z;
+        c[4 * k + 3] = t.w;
+      }
+      switch (q) {  // wave-uniform
+        case 0: expand_compact<0>(c, v); break;
+        case 1: expand_compact<1>(c, v); break;
+        case 2: expand_compact<2>(c, v); break;
+        default: expand_compact<3>(c, v); break;
+      }
+    } else if (valid) {
       const float* xr = a.X + row * (int64_t)a.ld;
       const int ncopy = a.ld < a.nf ? a.ld : a.nf;
       if (a.vec4 && fq + 16 <= ncopy) {
@@ -907,12 +935,13 @@ bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots,
 
 bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
                      const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
-                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results) {
+                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results, bool compact) {
   Pair q;
   if (!select_pair(e, p, slots, present, n, q)) return false;
   const int pa = q.pa, pb = q.pb, ma = q.ma, mb = q.mb;
   EnsArgs a{};
-  plan_args(e.ens, dX, n, ld, e.ens_owner_fixed, a);
+  plan_args(e.ens, dX, n, compact ? kCompactWidth : ld, e.ens_owner_fixed, a);
+  a.compact = compact ? 1 : 0;
   a.pos[0] = pa;
   a.pos[1] = pb;
   a.mcol[0] = ma;

@@ -21,6 +21,21 @@ namespace fd {
 constexpr int kMaxSlots = 8;      // forest slots per engine
 constexpr int kTile = 256;        // transactions per workgroup in the forest kernel (one per thread)
 constexpr int kMaxFeatures = 64;  // model columns held in LDS ([feature][kTile] f32 = 64 KiB max)
+// The compact scoring vector of the fused pipeline (features.hip write_vector -> ensemble.hip prologue): of the 64
+// slots of the engine's vector (FeatureProcessor's 41 definitions + derived features + pad, _prepare_features) only
+// these 22 vary per transaction; slots 12, 24, 25, 33, 34 are always 0.5 (defaults with no bridged source) and the
+// rest 0. The pipelined stream writes 24 floats (96 B: the 22 + 2 pad) per transaction instead of 64 (256 B) when
+// nothing else reads the vectors, and the ensemble kernel expands them.
+constexpr int kCompactWidth = 24;
+constexpr int kCompactSlots = 22;
+constexpr int kCompactSlot[kCompactSlots] = {0, 1, 5, 6, 7, 14, 15, 16, 17, 19, 21, 23,
+                                             26, 27, 31, 32, 41, 42, 43, 44, 45, 46};
+// the slot's place in the compact row, -2 for the constant 0.5, -1 for the constant 0
+__host__ __device__ constexpr int compact_src(int f) {
+  for (int k = 0; k < kCompactSlots; ++k)
+    if (kCompactSlot[k] == f) return k;
+  return (f == 12 || f == 24 || f == 25 || f == 33 || f == 34) ? -2 : -1;
+}
 constexpr int kMaxDepth = 10;     // deepest tree the repacker accepts
 constexpr size_t kLdsBudget = 160 * 1024;  // LDS per CU (one workgroup per CU at 64k batches)
 constexpr int kMaxBins = 65534;   // distinct thresholds per feature in the binned layout
@@ -467,13 +482,14 @@ void state_clear(Engine& e);
 int64_t state_count(Engine& e);
 void load_users(Engine& e, const fd_users& u);
 void load_merchants(Engine& e, const fd_merchants& m);
+// compact: d_vec rows are the fused pipeline's compact form (kCompactWidth floats), not the 64-wide vector
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw,
                      float* d_seq = nullptr, double* d_vel5 = nullptr, hipStream_t stream = nullptr,
-                     bool lean = false, int set = 0, hipEvent_t before_buckets = nullptr);
+                     bool lean = false, int set = 0, hipEvent_t before_buckets = nullptr, bool compact = false);
 // the same over received 48-B route records (route.hip), no unpack pass; also returns nothing else
 void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq,
                              hipStream_t stream = nullptr, bool lean = false, int set = 0,
-                             hipEvent_t before_buckets = nullptr);
+                             hipEvent_t before_buckets = nullptr, bool compact = false);
 void load_users_ext(Engine& e, const fd_users_ext& u);
 void load_merchants_ext(Engine& e, const fd_merchants_ext& m);
 void load_vocab(Engine& e, const uint8_t* pay_high_risk, const uint8_t* type_refund);
@@ -528,9 +544,10 @@ bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots,
 // one forest's probabilities through the fused kernel (large batches, no raw / leaf outputs); false: not applicable
 bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int32_t ld, double* dprob,
                             hipStream_t stream);
+// compact: dX rows are the compact vector (kCompactWidth floats, ld ignored; the plan's features <= 64)
 bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
                      const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
-                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results);
+                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results, bool compact = false);
 void forest_loaded(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);
 // blend.hip
 void launch_blend(Engine& e, const fd_blend_params& p, int64_t n, const double* const* d_probs,

@@ -299,7 +299,7 @@ __global__ void __launch_bounds__(kST) feat_slot_kernel(CardHeader* H, unsigned 
 // bridged raw features -> scoring vector: FeatureProcessor.process_features (41 definitions, derived
 // features appended when present) + _prepare_features (pad to 64, clip +-10), then the f32 cast the
 // models apply. Mirrors oracle/oracle_features.c orc_vector_from_raw.
-__device__ void write_vector(const double* r, float o1, float dv0, float* __restrict__ out) {
+__device__ void write_vector(const double* r, float o1, float dv0, float* __restrict__ out, bool compact) {
 #pragma clang fp contract(off)
   const double amount = pmax(r[0], 0.0);
   const double hour = pmin(pmax(r[2], 0.0), 23.0);
@@ -355,6 +355,14 @@ __device__ void write_vector(const double* r, float o1, float dv0, float* __rest
     }
   }
   float4* o4 = reinterpret_cast<float4*>(out);
+  if (compact) {  // the 22 slots that vary (fd_internal.h kCompactSlot) + 2 pad: 6 x 16 B
+    float c[kCompactWidth];
+#pragma unroll
+    for (int k = 0; k < kCompactWidth; ++k) c[k] = k < kCompactSlots ? o[kCompactSlot[k < kCompactSlots ? k : 0]] : 0.f;
+#pragma unroll
+    for (int q = 0; q < kCompactWidth / 4; ++q) o4[q] = make_float4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < FD_VECTOR_WIDTH / 4; ++q) o4[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
 }
@@ -411,6 +419,7 @@ struct Outputs {
   // be truncated there: the reference's counters are unbounded, RedisTransactionSink.java:93-105); null otherwise
   unsigned long long* sat;
   int K;
+  bool compact;  // vec rows are the compact form (kCompactWidth floats: the fused pipeline's ensemble reads them)
 };
 
 __device__ __forceinline__ void emit(const Outputs& o, int64_t i, const double* r, long long s5, float o1, float dv0) {
@@ -420,7 +429,7 @@ __device__ __forceinline__ void emit(const Outputs& o, int64_t i, const double* 
 #pragma unroll
     for (int c = 0; c < FD_RAW_FEATURES / 2; ++c) ro[c] = make_double2(r[2 * c], r[2 * c + 1]);
   }
-  write_vector(r, o1, dv0, o.vec + (size_t)i * FD_VECTOR_WIDTH);
+  write_vector(r, o1, dv0, o.vec + (size_t)i * (o.compact ? kCompactWidth : FD_VECTOR_WIDTH), o.compact);
   if (o.vel5) o.vel5[i] = (double)s5 / 100.0;
 }
 
@@ -1669,7 +1678,7 @@ namespace {
 // card updates, pipelined stream) while the slot pass runs ahead
 void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, double* d_raw, float* d_seq,
                     double* d_vel5, hipStream_t stream = nullptr, bool lean = false, int set = 0,
-                    hipEvent_t before_buckets = nullptr) {
+                    hipEvent_t before_buckets = nullptr, bool compact = false) {
   CardStore& st = e.state;
   CardStore::GroupScratch& g = st.gs[set];
   const hipStream_t s = stream ? stream : e.stream;
@@ -1711,7 +1720,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.n = n;
   a.prep = g.prep.as<const Prep>();
   a.out = Outputs{d_vec, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S,
-                  st.mode == FD_WINDOW_SLIDING ? st.sat.as<unsigned long long>() : nullptr, st.K};
+                  st.mode == FD_WINDOW_SLIDING ? st.sat.as<unsigned long long>() : nullptr, st.K, compact};
   a.fill = g.bucket_fill.as<unsigned>();
   a.pairs = g.pairs.as<const unsigned long long>();
   a.C = C;
@@ -1739,7 +1748,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
 }  // namespace
 
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw, float* d_seq,
-                     double* d_vel5, hipStream_t stream, bool lean, int set, hipEvent_t before_buckets) {
+                     double* d_vel5, hipStream_t stream, bool lean, int set, hipEvent_t before_buckets, bool compact) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
   FD_REQUIRE(d_vec != nullptr, FD_ERR_INVALID_ARG, "null vector output");
@@ -1752,11 +1761,11 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
   TxnSrc src{reinterpret_cast<const unsigned long long*>(t.card_key), reinterpret_cast<const long long*>(t.ts_ms),
              reinterpret_cast<const long long*>(t.amount_cents), reinterpret_cast<const int*>(t.merchant),
              reinterpret_cast<const unsigned long long*>(t.device_fp), t.ip_class, t.hour, t.weekend, nullptr};
-  launch_grouped(e, src, n, d_vec, d_raw, d_seq, d_vel5, stream, lean, set, before_buckets);
+  launch_grouped(e, src, n, d_vec, d_raw, d_seq, d_vel5, stream, lean, set, before_buckets, compact);
 }
 
 void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq,
-                             hipStream_t stream, bool lean, int set, hipEvent_t before_buckets) {
+                             hipStream_t stream, bool lean, int set, hipEvent_t before_buckets, bool compact) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
   FD_REQUIRE(d_vec != nullptr && (n == 0 || d_records != nullptr), FD_ERR_INVALID_ARG, "null records / output");
@@ -1765,7 +1774,7 @@ void launch_features_records(Engine& e, const void* d_records, int64_t n, float*
   if (n == 0) return;
   TxnSrc src{};
   src.rec = static_cast<const RouteRecord*>(d_records);
-  launch_grouped(e, src, n, d_vec, nullptr, d_seq, nullptr, stream, lean, set, before_buckets);
+  launch_grouped(e, src, n, d_vec, nullptr, d_seq, nullptr, stream, lean, set, before_buckets, compact);
 }
 
 void features_check(Engine& e) { check_err(e); }
