@@ -792,9 +792,15 @@ class Config4(Config3):
             raise RuntimeError("stream exhausted: raise n_batches")
         self.next_batch += 1
         B = self.B
-        part = {f: t[b * B:(b + 1) * B] for f, t in self.dev.items()}
+        # the batch the previous step prefetched is passed as the very same mapping (ShardedScorer names a prefetch
+        # to the engine by identity, not by address)
+        nb = getattr(self, "_next_part", None)
+        part = nb[1] if nb is not None and nb[0] == b else {f: t[b * B:(b + 1) * B] for f, t in self.dev.items()}
+        self._next_part = None
         if self.world > 1 and b + 1 < self.n_batches:  # the next batch's partition + count exchange, one step ahead
-            kw["prefetch"] = ({f: t[(b + 1) * B:(b + 2) * B] for f, t in self.dev.items()}, B)
+            nxt = {f: t[(b + 1) * B:(b + 2) * B] for f, t in self.dev.items()}
+            kw["prefetch"] = (nxt, B)
+            self._next_part = (b + 1, nxt)
         self.out = self.scorer.step(part, B, **kw)
 
     def step_to_host(self, i, q):

@@ -456,11 +456,6 @@ class ShardedScorer:
         return self.be.scatter_results(back, n, sentinel=True)
 
     # ---------------------------------------------------------------- streaming exchange (module docstring)
-    @staticmethod
-    def _batch_key(txns, n):
-        k = txns["card_key"]
-        return (k.data_ptr() if hasattr(k, "data_ptr") else id(k), int(n))
-
     def _launch_counts(self, txns, n, input_ready):
         import torch
         be = self.be
@@ -469,14 +464,16 @@ class ShardedScorer:
             recv = torch.empty_like(counts)
             self._a2a(recv, counts)
             host = be.counts_to_host(counts, recv)
-        return {"key": self._batch_key(txns, n), "rec": rec, "host": host}
+        # the batch itself (referenced: its tensors cannot be recycled while the prefetch is pending), matched by
+        # identity — never by address, which torch's allocator reuses
+        return {"txns": txns, "n": int(n), "rec": rec, "host": host}
 
     def _step_streaming(self, txns, n, input_ready, prefetch):
         import torch
         be = self.be
         p = self._pending
         self._pending = None
-        if p is None or p["key"] != self._batch_key(txns, n):
+        if p is None or p["n"] != int(n) or not _same_batch(p["txns"], txns):
             # no prefetch, or another batch came instead of the prefetched one: its partition and count exchange
             # (issued on every rank alike) are dropped, this batch's are launched now
             p = self._launch_counts(txns, n, input_ready)
