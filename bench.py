@@ -163,7 +163,12 @@ LSTM4_SYMBOL = "fd::anon::lstm_kernel4"
 INGEST_SYMBOL = "fd::anon::ingest_json_kernel"
 
 
-def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=None, out=0, wide=True):
+# the engine's default for option "ensemble_scalar_top" (engine.hip / fd_internal.h Engine::ens_scalar_top): the
+# instantiation the bench's launches use, for the PMC lookup by symbol
+ENS_SCALAR_TOP = False
+
+
+def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=None, out=0, wide=True, vec_bytes=256):
     """Roofline of a forest launch against its real bound: LDS issue of the dependent walk. With the fused
     ensemble kernel (FD_TIMING_ENSEMBLE) timed, that launch is the one reported (both forests' node steps)."""
     from fdengine import _native as N
@@ -176,13 +181,13 @@ def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=Non
         forest_bytes = sum(forest_blob_bytes(f) for f in forests)
         # the instantiation that ran: output form (0 columns, 1 route result records) and chunk layout (wide
         # unless the engine has RCCL communicators: engine option ensemble_chunks)
-        symbol = ensemble_symbol(out, wide)
+        symbol = ensemble_symbol(out, wide, ENS_SCALAR_TOP)
     elif timing.get(N.FD_TIMING_ENSEMBLE, (0.0, 0))[1]:  # one forest through the fused kernel (config 2)
         ms, launches = timing[N.FD_TIMING_ENSEMBLE]
         steps = B * forest.n_trees * depth
         forest_bytes = forest_blob_bytes(forest)
         label = "ensemble_kernel<D=8> over one forest (probabilities only)"
-        symbol = ensemble_symbol(2, True)
+        symbol = ensemble_symbol(2, True, ENS_SCALAR_TOP)
     else:
         steps = B * forest.n_trees * depth
         forest_bytes = forest_blob_bytes(forest)
@@ -196,8 +201,10 @@ def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=Non
             "kernel_samples": launches, "node_steps_per_launch": steps,
             "peak_basis": "per node-step 1 ds_read_b32 + 1 ds_read_b64 per lane = 4 LDS-array cycles per 64 "
                           "node-steps: 16/clk/CU x 256 CUs x 2.4 GHz",
-            "hbm_view": {"algorithmic_bytes_per_launch": B * (64 * 4 + 8) + model_bytes,
-                         "achieved_GBs": round((B * (64 * 4 + 8) + model_bytes) / avg / 1e9, 3), "peak_GBs": HBM_PEAK_GBS}}
+            "hbm_view": {"algorithmic_bytes_per_launch": B * (vec_bytes + 8) + model_bytes,
+                         "vector_bytes_per_txn": vec_bytes,
+                         "achieved_GBs": round((B * (vec_bytes + 8) + model_bytes) / avg / 1e9, 3),
+                         "peak_GBs": HBM_PEAK_GBS}}
 
 
 def product_blend(names):
@@ -593,9 +600,12 @@ class Config3:
         sc = getattr(self, "scorer", None)
         native = bool(getattr(sc, "native", False))
         routed = bool(getattr(sc, "route", False))
+        be = getattr(sc, "be", None)
+        pipelined = bool(getattr(be, "pipelined", getattr(self, "pipe", False)))
+        # the pipelined stream hands the fused kernel the compact 24-float vector (96 B) unless vectors are requested
         return forest_roofline(timing, self.N.FD_TIMING_XGB, self.xgb, 8, self.B, self.name,
                                FOREST_KERNEL.format(d=8, t="f32", k="XGB") + " dominant", [self.xgb, self.ifm],
-                               out=1 if routed else 0, wide=not native)
+                               out=1 if routed else 0, wide=not native, vec_bytes=96 if pipelined else 256)
 
     def kernels(self, timing):
         N = self.N
