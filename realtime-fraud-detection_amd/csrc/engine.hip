@@ -7,6 +7,7 @@
 #include <cstring>
 #include <string>
 
+#include "blend_row.h"
 #include "fd_internal.h"
 #include "ingest_parse.h"
 
@@ -161,7 +162,9 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     FD_HIP(hipStreamWaitEvent(e.aux2_stream, e.fork_ev, 0));
   }
   if (use1) fork_aux();
-  // two forests, one stream: one binning launch for both (fd::launch_forest_pair)
+  // two forests, one stream: one binning launch for both (fd::launch_forest_pair); when every other present model
+  // is the LSTM head (already queued above), both walks in one launch and both sums + the blend in another
+  // (fd::launch_forest_pair_blend: 3 launches instead of 6)
   bool paired = false;
   if (small && ss == 0 && n_forests == 2) {
     int fm[2], k = 0;
@@ -172,6 +175,22 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     if (pa.loaded && pb.loaded) {
       double* ca = dMP + (size_t)fm[0] * n;
       double* cb = dMP + (size_t)fm[1] * n;
+      bool others_lstm = true;
+      for (int m = 0; m < M; ++m)
+        if (!(present && !present[m]) && m != fm[0] && m != fm[1] && slots[m] != FD_SLOT_LSTM) others_lstm = false;
+      if (others_lstm && e.latency_fused) {
+        const double* pc[FD_MAX_MODELS] = {};
+        int q = 0, pos_a = -1, pos_b = -1;
+        for (int m = 0; m < M; ++m) {
+          if (present && !present[m]) continue;
+          if (m == fm[0]) pos_a = q;
+          if (m == fm[1]) pos_b = q;
+          pc[q++] = m == fm[0] ? ca : m == fm[1] ? cb : cols[m];
+        }
+        if (fd::launch_forest_pair_blend(e, pa, pb, dX, n, ld, fd::blend_consts(p, present), pc, pos_a, pos_b, dfp,
+                                         dconf, ddec, drisk))
+          return false;
+      }
       paired = fd::launch_forest_pair(e, pa, pb, dX, n, ld, ca, cb);
       if (paired) {
         cols[fm[0]] = ca;
@@ -444,6 +463,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "ensemble_scalar_top") {  // fused kernel: 1 the walk's top three levels from scalar loads
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_scalar_top must be 0 or 1");
     e.ens_scalar_top = value != 0;
+  } else if (k == "latency_fused") {  // latency batches: 1 (default) both forests' walks in one launch and their
+    // sums + the blend in another (fd::launch_forest_pair_blend); 0 the per-forest walk + sum launches + blend
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "latency_fused must be 0 or 1");
+    e.latency_fused = value != 0;
   } else if (k == "pipeline_lean") {  // fd_score_batch_pipelined's bucket pass: 1 (default) lean + deferred
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "pipeline_lean must be 0 or 1");
     e.pipe_lean = value != 0;

@@ -397,6 +397,7 @@ struct Engine {
   bool pipe_copy_live[kPipeSlots] = {};
   bool pipe_copy_vec[kPipeSlots] = {};  // that copy also read the slot's vectors (the slot's next features wait)
   int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
+  bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
   int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
@@ -455,6 +456,14 @@ bool launch_forest_pair(Engine& e, const PackedForest& pa, const PackedForest& p
                         int32_t ld, double* d_prob_a, double* d_prob_b);
 void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t n, int32_t ld,
                    double* d_prob, double* d_raw, int32_t* d_leaf, hipStream_t stream = nullptr);
+// a latency batch's XGBoost + IsolationForest and the blend: bin (one launch), both walks (one launch), both
+// sequential sums + blend_row over every present model (one launch); cols = the present models' probability columns
+// in present order (the two forests' are written, the others read), pos1 / pos2 = p1's / p2's place in it.
+// false: not applicable (not one of each kind on the split path at depth 8); nothing launched.
+struct BlendConsts;
+bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedForest& p2, const float* d_X, int64_t n,
+                              int32_t ld, const BlendConsts& bc, const double* const* cols, int pos1, int pos2,
+                              double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk);
 // windows.hip
 void windows_init(Engine& e, const fd_window_params& p);
 void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, int64_t n, bool flush,

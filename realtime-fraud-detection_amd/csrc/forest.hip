@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstring>
 
+#include "blend_row.h"
 #include "fd_internal.h"
 #include "walk_common.h"
 
@@ -962,11 +963,11 @@ __device__ __forceinline__ void stage_rows_asm(const char* __restrict__ src, siz
 }
 
 template <int D, int CH, typename LeafT>
-__global__ void __launch_bounds__(kWG3)
-split_walk_kernel(const uint32_t* __restrict__ bins, int64_t n, int64_t n_pad, int nf,
-                  const uint32_t* __restrict__ tile_nan, const char* __restrict__ blob, int n_chunks,
-                  int chunk_stride, int chunks_per_group, const int32_t* __restrict__ leaf_ids, int n_trees,
-                  LeafT* __restrict__ leaves, int32_t* __restrict__ out_leaf) {
+__device__ __forceinline__ void split_walk_body(const uint32_t* __restrict__ bins, int64_t n, int64_t n_pad, int nf,
+                                                const uint32_t* __restrict__ tile_nan, const char* __restrict__ blob,
+                                                int n_chunks, int chunk_stride, int chunks_per_group,
+                                                const int32_t* __restrict__ leaf_ids, int n_trees,
+                                                LeafT* __restrict__ leaves, int32_t* __restrict__ out_leaf, int gy) {
   constexpr int TPG = CH / 4;
   constexpr int NL = 1 << D;
   constexpr uint32_t TB = (4u + (uint32_t)sizeof(LeafT)) << D;
@@ -980,7 +981,7 @@ split_walk_kernel(const uint32_t* __restrict__ bins, int64_t n, int64_t n_pad, i
   const uint32_t bufA = s0 + (uint32_t)nf * 1024u, bufB = bufA + (uint32_t)chunk_stride;
   const int tile = blockIdx.x;
   const int64_t row = (int64_t)tile * kTile + txn;
-  const int k0 = blockIdx.y * chunks_per_group;
+  const int k0 = gy * chunks_per_group;
   const int k1 = min(n_chunks, k0 + chunks_per_group);
   if (k0 >= k1) return;  // uniform per workgroup
   stage_rows_asm(reinterpret_cast<const char*>(bins + (size_t)tile * kTile), (size_t)n_pad * 4u, s0, nf, kWG3 / 64);
@@ -1012,9 +1013,146 @@ split_walk_kernel(const uint32_t* __restrict__ bins, int64_t n, int64_t n_pad, i
   }
 }
 
+template <int D, int CH, typename LeafT>
+__global__ void __launch_bounds__(kWG3)
+split_walk_kernel(const uint32_t* __restrict__ bins, int64_t n, int64_t n_pad, int nf,
+                  const uint32_t* __restrict__ tile_nan, const char* __restrict__ blob, int n_chunks,
+                  int chunk_stride, int chunks_per_group, const int32_t* __restrict__ leaf_ids, int n_trees,
+                  LeafT* __restrict__ leaves, int32_t* __restrict__ out_leaf) {
+  split_walk_body<D, CH, LeafT>(bins, n, n_pad, nf, tile_nan, blob, n_chunks, chunk_stride, chunks_per_group, leaf_ids,
+                                n_trees, leaves, out_leaf, (int)blockIdx.y);
+}
+
+constexpr int kSumRows = 8;  // transactions per workgroup of the sum kernels (below)
+
+// one forest's side of the latency pair (split_walk_pair_kernel / split_sum_pair_blend_kernel)
+struct SplitWalkArgs {
+  const uint32_t* bins;
+  const uint32_t* tile_nan;
+  const char* blob;
+  int n_chunks, chunk_stride, cpg, groups;
+  const int32_t* leaf_ids;
+  int n_trees;
+  void* leaves;
+};
+
+// Both forests of a latency batch walked in ONE launch (grid.y = XGBoost's chunk groups, then the
+// IsolationForest's): the launch and the queue gap between two walks saved, and the two walks' workgroups share the
+// CUs instead of running one after the other
+template <int DX, int CHX, int DI, int CHI>
+__global__ void __launch_bounds__(kWG3) split_walk_pair_kernel(int64_t n, int64_t n_pad, int nf, SplitWalkArgs x,
+                                                               SplitWalkArgs f) {
+  const int gy = (int)blockIdx.y;
+  if (gy < x.groups)
+    split_walk_body<DX, CHX, float>(x.bins, n, n_pad, nf, x.tile_nan, x.blob, x.n_chunks, x.chunk_stride, x.cpg,
+                                    x.leaf_ids, x.n_trees, static_cast<float*>(x.leaves), nullptr, gy);
+  else
+    split_walk_body<DI, CHI, double>(f.bins, n, n_pad, nf, f.tile_nan, f.blob, f.n_chunks, f.chunk_stride, f.cpg,
+                                     f.leaf_ids, f.n_trees, static_cast<double*>(f.leaves), nullptr, gy - x.groups);
+}
+
+// The latency pair's epilogue in ONE launch: per transaction the XGBoost margin (base + f32 leaves in tree order)
+// and the IsolationForest path-length sum (f64, tree order) — split_sum_kernel's sequential sums, bit for bit —
+// their probabilities (into the model-probability columns), then blend_row over every present model (the others'
+// columns, e.g. the LSTM head's, read from memory) -> fraud probability, confidence, decision, risk. Replaces two
+// sum launches and the blend launch.
+struct PairBlendArgs {
+  BlendConsts blend;
+  Cols cols;      // present models' columns (present order); the two forests' entries are written here
+  int pos_x, pos_f;  // present-order positions of the XGBoost / IsolationForest
+  float base_margin;
+  double if_offset, if_denom;
+  double *fp, *conf;
+  uint8_t *dec, *risk;
+};
+
+template <int R>
+__device__ __forceinline__ void stream_leaves(const char* __restrict__ leaves, int esz, int64_t n, int n_trees,
+                                              int64_t r0, int rows, char* __restrict__ blk, int t0, int tc) {
+  // [tc][R] block of leaf values (esz bytes each) into LDS: independent loads, 16 in flight per thread
+  const int total = tc * R;
+  for (int base = 0; base < total; base += 256 * 16) {
+    unsigned long long v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = base + u * 256 + (int)threadIdx.x;
+      const int t = i / R, r = i - t * R;
+      v[u] = 0ull;
+      if (i < total && r < rows) {
+        const char* src = leaves + ((size_t)(t0 + t) * n + r0 + r) * esz;
+        v[u] = esz == 8 ? *reinterpret_cast<const unsigned long long*>(src) : *reinterpret_cast<const unsigned*>(src);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = base + u * 256 + (int)threadIdx.x;
+      if (i < total) {
+        if (esz == 8)
+          reinterpret_cast<unsigned long long*>(blk)[i] = v[u];
+        else
+          reinterpret_cast<unsigned*>(blk)[i] = (unsigned)v[u];
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+split_sum_pair_blend_kernel(const float* __restrict__ lx, int tx, const double* __restrict__ lf, int tf, int64_t n,
+                            PairBlendArgs a, uint32_t* __restrict__ nan_x, uint32_t* __restrict__ nan_f) {
+  constexpr int R = kSumRows;
+  constexpr int kTc = 65536 / (R * 8);  // trees per LDS block (64 KiB of f64; f32 blocks use half)
+  __shared__ double blk[kTc * R];
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int rows = (int)min<int64_t>(R, n - r0);
+  float accx = a.base_margin;
+  for (int t0 = 0; t0 < tx; t0 += kTc) {
+    const int tc = min(kTc, tx - t0);
+    stream_leaves<R>(reinterpret_cast<const char*>(lx), 4, n, tx, r0, rows, reinterpret_cast<char*>(blk), t0, tc);
+    __syncthreads();
+    if (tid < rows) {
+      const float* b = reinterpret_cast<const float*>(blk);
+      for (int t = 0; t < tc; ++t) accx += b[t * R + tid];
+    }
+    __syncthreads();
+  }
+  double accf = 0.0;
+  for (int t0 = 0; t0 < tf; t0 += kTc) {
+    const int tc = min(kTc, tf - t0);
+    stream_leaves<R>(reinterpret_cast<const char*>(lf), 8, n, tf, r0, rows, reinterpret_cast<char*>(blk), t0, tc);
+    __syncthreads();
+    if (tid < rows)
+      for (int t = 0; t < tc; ++t) accf += blk[t * R + tid];
+    __syncthreads();
+  }
+  if (tid == 0 && r0 % kTile == 0) {  // every walk of the tile is done (stream order): clear the NaN flags
+    nan_x[r0 / kTile] = 0u;
+    nan_f[r0 / kTile] = 0u;
+  }
+  if (tid >= rows) return;
+  const int64_t row = r0 + tid;
+  double px, pf;
+  write_outputs<FD_FOREST_XGB_BINARY_LOGISTIC, float>(accx, row, 0.0, 0.0, const_cast<double*>(a.cols.p[a.pos_x]),
+                                                      nullptr);
+  write_outputs<FD_FOREST_SKLEARN_IFOREST, double>(accf, row, a.if_offset, a.if_denom,
+                                                   const_cast<double*>(a.cols.p[a.pos_f]), nullptr);
+  px = a.cols.p[a.pos_x][row];
+  pf = a.cols.p[a.pos_f][row];
+  double raw[FD_MAX_MODELS];
+#pragma unroll
+  for (int m = 0; m < FD_MAX_MODELS; ++m)
+    raw[m] = m >= a.blend.n_models ? 0.0 : (m == a.pos_x ? px : (m == a.pos_f ? pf : a.cols.p[m][row]));
+  double fp, conf;
+  uint8_t dec, risk;
+  blend_row(a.blend, raw, fp, conf, dec, risk);
+  a.fp[row] = fp;
+  if (a.conf) a.conf[row] = conf;
+  if (a.dec) a.dec[row] = dec;
+  if (a.risk) a.risk[row] = risk;
+}
+
 // 8 transactions per workgroup (128 workgroups for a 1 k batch): all 256 threads stream a [trees][8] block of
 // leaf values into LDS (independent 32-B row loads), then 8 threads add them in tree order (the sequential sum)
-constexpr int kSumRows = 8;
 
 template <int KIND, typename LeafT>
 __global__ void __launch_bounds__(256)
@@ -1311,6 +1449,101 @@ bool launch_forest_pair(Engine& e, const PackedForest& pa, const PackedForest& p
     split_walk_sum<float, FD_FOREST_XGB_BINARY_LOGISTIC>(pb, n, d_prob_b, nullptr, nullptr, tiles, st);
   else
     split_walk_sum<double, FD_FOREST_SKLEARN_IFOREST>(pb, n, d_prob_b, nullptr, nullptr, tiles, st);
+  if (ev) FD_HIP(hipEventRecord(ev->b, st));
+  return true;
+}
+
+namespace {
+template <int CHX>
+const void* pick_walk_pair_i(int chi) {
+  switch (chi) {
+    case 4: return (const void*)split_walk_pair_kernel<8, CHX, 8, 4>;
+    case 8: return (const void*)split_walk_pair_kernel<8, CHX, 8, 8>;
+    case 12: return (const void*)split_walk_pair_kernel<8, CHX, 8, 12>;
+    case 16: return (const void*)split_walk_pair_kernel<8, CHX, 8, 16>;
+    default: return nullptr;
+  }
+}
+const void* pick_walk_pair(int chx, int chi) {
+  switch (chx) {
+    case 4: return pick_walk_pair_i<4>(chi);
+    case 8: return pick_walk_pair_i<8>(chi);
+    case 12: return pick_walk_pair_i<12>(chi);
+    case 16: return pick_walk_pair_i<16>(chi);
+    default: return nullptr;
+  }
+}
+
+// chunk groups of one forest's walk over `tiles` tiles: enough workgroups to cover the CUs (as split_walk_sum)
+void walk_groups(const PackedForest& pf, int64_t tiles, int& cpg, int& groups) {
+  const int want = (int)std::max<int64_t>(1, (256 + tiles - 1) / tiles);
+  cpg = std::max(1, (pf.b_n_chunks + want - 1) / want);
+  groups = (pf.b_n_chunks + cpg - 1) / cpg;
+}
+}  // namespace
+
+bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedForest& p2, const float* d_X, int64_t n,
+                              int32_t ld, const BlendConsts& bc, const double* const* cols, int pos1, int pos2,
+                              double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk) {
+  if (n == 0 || &p1 == &p2 || !split_path(e, p1, n) || !split_path(e, p2, n)) return false;
+  const bool x1 = p1.kind == FD_FOREST_XGB_BINARY_LOGISTIC, x2 = p2.kind == FD_FOREST_XGB_BINARY_LOGISTIC;
+  if (x1 == x2) return false;  // one XGBoost and one IsolationForest
+  const PackedForest& X = x1 ? p1 : p2;
+  const PackedForest& F = x1 ? p2 : p1;
+  if (X.depth != 8 || F.depth != 8 || X.num_feature != F.num_feature) return false;
+  const void* walk = pick_walk_pair(X.b_chunk, F.b_chunk);
+  if (!walk) return false;
+  const int nf = X.num_feature;
+  const size_t lds = (size_t)nf * 1024 + 2 * std::max(X.b_chunk_stride, F.b_chunk_stride) + 1024;
+  if (lds > kLdsBudget) return false;
+  FD_REQUIRE(d_X && dfp && cols && ld > 0, FD_ERR_INVALID_ARG, "null buffer or bad ld");
+  const int64_t tiles = (n + kTile - 1) / kTile, n_pad = tiles * kTile;
+  const hipStream_t st = e.stream;
+  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_XGB) : nullptr;  // the pair's three launches
+  if (ev) FD_HIP(hipEventRecord(ev->a, st));
+  const SplitBinArgs a = split_prepare<float>(X, n, tiles, st);
+  const SplitBinArgs b = split_prepare<double>(F, n, tiles, st);
+  hipLaunchKernelGGL(split_bin_pair_kernel, dim3((unsigned)(tiles * kTile / kSplitBin), (unsigned)(a.nf + b.nf)),
+                     dim3(kSplitBin), 0, st, d_X, n, n_pad, (int)ld, a, b);
+  FD_HIP(hipGetLastError());
+  SplitWalkArgs wx{}, wf{};
+  wx.bins = a.bins;
+  wx.tile_nan = a.tile_nan;
+  wx.blob = X.b_blob.as<const char>();
+  wx.n_chunks = X.b_n_chunks;
+  wx.chunk_stride = (int)X.b_chunk_stride;
+  walk_groups(X, tiles, wx.cpg, wx.groups);
+  wx.leaf_ids = X.leaf_ids.as<const int32_t>();
+  wx.n_trees = X.n_trees;
+  wx.leaves = X.split.leaves.ptr;
+  wf.bins = b.bins;
+  wf.tile_nan = b.tile_nan;
+  wf.blob = F.b_blob.as<const char>();
+  wf.n_chunks = F.b_n_chunks;
+  wf.chunk_stride = (int)F.b_chunk_stride;
+  walk_groups(F, tiles, wf.cpg, wf.groups);
+  wf.leaf_ids = F.leaf_ids.as<const int32_t>();
+  wf.n_trees = F.n_trees;
+  wf.leaves = F.split.leaves.ptr;
+  FD_HIP(hipFuncSetAttribute(walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  void* wargs[] = {&n, const_cast<int64_t*>(&n_pad), const_cast<int*>(&nf), &wx, &wf};
+  FD_HIP(hipLaunchKernel(walk, dim3((unsigned)tiles, (unsigned)(wx.groups + wf.groups)), dim3(kWG3), wargs, lds, st));
+  PairBlendArgs pa{};
+  pa.blend = bc;
+  for (int m = 0; m < bc.n_models; ++m) pa.cols.p[m] = cols[m];
+  pa.pos_x = x1 ? pos1 : pos2;
+  pa.pos_f = x1 ? pos2 : pos1;
+  pa.base_margin = X.base_margin;
+  pa.if_offset = F.if_offset;
+  pa.if_denom = F.if_denominator;
+  pa.fp = dfp;
+  pa.conf = dconf;
+  pa.dec = ddec;
+  pa.risk = drisk;
+  hipLaunchKernelGGL(split_sum_pair_blend_kernel, dim3((unsigned)((n + kSumRows - 1) / kSumRows)), dim3(256), 0, st,
+                     X.split.leaves.as<const float>(), X.n_trees, F.split.leaves.as<const double>(), F.n_trees, n, pa,
+                     a.tile_nan, b.tile_nan);
+  FD_HIP(hipGetLastError());
   if (ev) FD_HIP(hipEventRecord(ev->b, st));
   return true;
 }

@@ -45,19 +45,21 @@ def world():
 
 @pytest.mark.timeout(200)
 def test_small_streams_variants_identical(world):
-    """engine option small_streams (latency batches: the LSTM and the second forest on 2 / 1 / 0 side streams):
-    the same outputs bit for bit, batch after batch"""
+    """engine option small_streams (latency batches: the LSTM and the second forest on 2 / 1 / 0 side streams) and,
+    on one stream, latency_fused (1: both walks in one launch, both sums + the blend in another; 0: per-forest walk
+    and sum launches + the blend kernel): the same outputs bit for bit, batch after batch"""
     import torch
     pop, tx, xgb, ifm = world
     lw = L.random_weights(seed=6)
     params = _params(True)
     slots = [0, 1, FD_SLOT_LSTM]
     dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f][:8000])).cuda() for f in TXN_FIELDS}
-    engs = [_setup(pop, xgb, ifm, lw) for _ in range(3)]
+    engs = [_setup(pop, xgb, ifm, lw) for _ in range(4)]
     try:
         res = []
         for v, e in enumerate(engs):
-            e.set_option("small_streams", v)
+            e.set_option("small_streams", v if v < 3 else 0)
+            e.set_option("latency_fused", 0 if v == 3 else 1)
             e.set_stream(torch.cuda.current_stream().cuda_stream)
             out = []
             for a in range(0, 8000, 1000):
@@ -70,10 +72,10 @@ def test_small_streams_variants_identical(world):
                 out.append([fp, conf, dec, risk, mp])
             res.append(out)
         torch.cuda.synchronize()
-        for v in (1, 2):
+        for v in (1, 2, 3):
             for b, (x, y) in enumerate(zip(res[v], res[0])):
                 for s, t in zip(x, y):
-                    assert np.array_equal(s.cpu().numpy(), t.cpu().numpy()), f"small_streams {v} batch {b}"
+                    assert np.array_equal(s.cpu().numpy(), t.cpu().numpy()), f"variant {v} batch {b}"
     finally:
         for e in engs:
             e.close()
@@ -102,5 +104,37 @@ def test_split_path_nan_flags_per_call(world):
             pi, di, li = eng.predict(1, X, want_raw=True, want_leaf=True)
             rpi, rdi, rli = oracle.iforest_predict(ifm, X, want_leaf=True)
             assert (li == rli).all() and (di == rdi).all(), f"IsolationForest call {i}"
+    finally:
+        eng.close()
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("strategy", [0, 1, 2])
+def test_latency_fused_pair_matches_per_forest_path(world, strategy):
+    """XGBoost + IsolationForest on 1 k matrices with NaNs (fd_score_matrix, the latency split path): the fused pair
+    (latency_fused 1) equals the per-forest launches + blend kernel (0) bit for bit — model probabilities, fraud
+    probability, confidence, decision, risk — for every blend strategy, and the model probabilities equal the oracle
+    within 1e-5 (leaf sums exact)."""
+    import oracle
+    _, _, xgb, ifm = world
+    from oracle import scoring_ref as S
+    names = ["xgboost_primary", "isolation_forest"]
+    w = S.normalized_weights({"xgboost_primary": 0.4, "isolation_forest": 0.05})
+    params = FraudEngine.blend_params([w[k] for k in names], [S.CONF_MULT[k] for k in names], strategy=strategy)
+    eng = FraudEngine(0)
+    try:
+        eng.load_forest(0, xgb)
+        eng.load_forest(1, ifm)
+        for i in range(4):
+            X = synth.feature_matrix(1000 + 37 * i, 64, seed=60 + i, nan_frac=0.02 if i % 2 == 0 else 0.0)
+            eng.set_option("latency_fused", 1)
+            a = eng.score_matrix(params, [0, 1], X)
+            eng.set_option("latency_fused", 0)
+            b = eng.score_matrix(params, [0, 1], X)
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
+            px, _, _ = oracle.xgb_predict(xgb, X)
+            pi, _, _ = oracle.iforest_predict(ifm, X)
+            assert np.abs(a[0][0] - px).max() <= 1e-5 and np.abs(a[0][1] - pi).max() <= 1e-12
     finally:
         eng.close()
