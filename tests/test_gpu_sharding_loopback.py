@@ -83,7 +83,8 @@ def _prefetch_plan(s, parts):
 def _run_ranks(world):
     import torch
 
-    from fdengine import FraudEngine, NativeError
+    from fdengine import FraudEngine
+    from fdengine._native import NativeError
     from fdengine._native import TXN_FIELDS
     from fdengine.sharding import ShardedScorer, EngineShardBackend, owned_mask
     pop, streams, sizes, xgb, ifm = _setup(world)
@@ -177,7 +178,7 @@ def _oracle(pop, streams, sizes, xgb, ifm, world):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world", [2, 4])
 def test_native_sharded_step_loopback_matches_oracle(world):
-    from fdengine import shard_of
+    from fdengine.engine import shard_of
     assert LOOPBACK.exists(), "tests/native/build/librccl_loopback.so missing (fdengine/build.py build_test_libs)"
     pop, streams, sizes, xgb, ifm, results, wrong_id = _run_ranks(world)
     for r in range(world):
@@ -212,7 +213,8 @@ def test_missing_peer_is_an_error_not_a_hang():
     the split-size wait)."""
     import torch
 
-    from fdengine import FraudEngine, NativeError
+    from fdengine import FraudEngine
+    from fdengine._native import NativeError
     from fdengine._native import TXN_FIELDS
     from fdengine.sharding import EngineShardBackend, ShardedScorer
     pop, streams, sizes, xgb, ifm = _setup(2)
