@@ -172,8 +172,9 @@ __device__ __forceinline__ void walk_ens(uint32_t buf, int t0, uint32_t lane4, u
 // each lane selects its level-1 / level-2 node with v_cndmask on its own comparisons. That drops the root read
 // and the level-0 and level-1 children-pair reads (one ds_read_b32 + two ds_read_b64 of a walk's 16 LDS reads,
 // 1.3 of its 4.9 KB of LDS data per wave) for a few VALU selects, on a walk bound by LDS issue.
+typedef uint32_t u32x8t __attribute__((ext_vector_type(8)));
 template <int D, int TPG, int TM, bool NAN_AWARE>
-__device__ __forceinline__ void walk_ens_top(uint32_t buf, int t0, uint32_t lane4, const uint32_t (&top)[TM][8],
+__device__ __forceinline__ void walk_ens_top(uint32_t buf, int t0, uint32_t lane4, const u32x8t (&top)[TM],
                                              uint32_t (&leaf)[TPG]) {
   static_assert(D >= 3 && TPG <= TM, "scalar top levels need depth >= 3");
   uint32_t tb[TPG], node[TPG], kl[TPG], kr[TPG], xw[TPG];
@@ -237,7 +238,7 @@ __device__ __forceinline__ void walk_ens_top(uint32_t buf, int t0, uint32_t lane
 
 template <int D, int TPG, int TM>
 __device__ __forceinline__ unsigned long long walk_pack_top(uint32_t cur, int gg, uint32_t lane4, bool tile_nan,
-                                                            const uint32_t (&top)[TM][8]) {
+                                                            const u32x8t (&top)[TM]) {
   uint32_t leaf[TPG];
   if (tile_nan)
     walk_ens_top<D, TPG, TM, true>(cur, gg * TPG, lane4, top, leaf);
@@ -252,21 +253,24 @@ __device__ __forceinline__ unsigned long long walk_pack_top(uint32_t cur, int gg
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// heap slots 0-7 of this wave's trees of chunk h (tree group gg) from the chunk in global memory: scalar loads
-// (the constant address space: the blobs do not change during the launch)
+// heap slots 0-7 of this wave's trees of chunk h (tree group gg) from the chunk in global memory, by scalar loads
+// issued in inline asm: the compiler would otherwise sink these invariant loads to their first use inside the walk
+// and wait there with lgkmcnt(0), which also drains every LDS read in flight (scalar loads share that counter and
+// return out of order). The caller issues them after a chunk's walk and completes them with top_wait() before the
+// chunk barrier, where the wave waits anyway.
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 template <int TM>
 __device__ __forceinline__ void load_top(const EnsArgs& a, int h, int nA, int gg, int tpga, int tpgb,
-                                         uint32_t (&top)[TM][8]) {
+                                         u32x8 (&top)[TM]) {
   const int fb = h >= nA ? 1 : 0;
   const int tpg = fb ? tpgb : tpga;
-  typedef const __attribute__((address_space(4))) uint32_t* cptr;
-  const cptr base = (cptr)(size_t)(a.nodes[fb] + (size_t)(fb ? h - nA : h) * (size_t)a.stride[fb]) +
-                    (size_t)(gg * tpg) * 256u;
+  const char* base = a.nodes[fb] + (size_t)(fb ? h - nA : h) * (size_t)a.stride[fb] + (size_t)(gg * tpg) * 1024u;
 #pragma unroll
-  for (int j = 0; j < TM; ++j)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) top[j][k] = j < tpg ? base[(size_t)j * 256u + k] : 0u;
+  for (int j = 0; j < TM; ++j) {
+    if (j < tpg) asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(top[j]) : "s"(base), "i"(j * 1024));
+  }
 }
+__device__ __forceinline__ void top_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Walk this wave's TPG trees of the chunk at `cur` (trees gg*TPG ...) for its 64 transactions; the leaf
 // indices (< 2^D <= 256) packed a byte per tree, in tree order, stored as one u64 per (tree group, txn).
@@ -540,9 +544,10 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   // tile[g&1]; the owners complete their DMA; the barrier publishes chunk g+1 and tile[g&1].
   FD_ESTAMP(pr_t1);
   constexpr bool kTop = STOP && D >= 3;
-  uint32_t top[kTop ? TPGA : 1][8];
+  u32x8 top[kTop ? TPGA : 1];
   if constexpr (kTop) {
     if (G > 0) load_top(a, 0, nA, gg, TPGA, TPGB, top);
+    top_wait();
   }
   for (int g = 0; g < G; ++g) {
     FD_ESTAMP(q0);
@@ -573,12 +578,13 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     if constexpr (kTop) {
       w = g < nA ? walk_pack_top<D, TPGA, TPGA>(cur, gg, lane4, tile_nan, top)
                  : walk_pack_top<D, TPGB, TPGA>(cur, gg, lane4, tile_nan, top);
-      if (g + 1 < G) load_top(a, g + 1, nA, gg, TPGA, TPGB, top);  // the next chunk's, under this chunk's barrier
+      if (g + 1 < G) load_top(a, g + 1, nA, gg, TPGA, TPGB, top);  // the next chunk's, landing during the barrier
     } else {
       w = g < nA ? walk_pack<D, TPGA>(cur, gg, lane4, tile_nan) : walk_pack<D, TPGB>(cur, gg, lane4, tile_nan);
     }
     lds_store<unsigned long long>(tw + (uint32_t)(gg * kTile + txn) * 8u, w);
     FD_ESTAMP(q2);
+    if constexpr (kTop) top_wait();  // the next chunk's top words (and this wave's LDS ops) before the barrier
     if (owner) dma_wait();
 #ifdef FD_FOREST_PROFILE
     const unsigned long long q2d = __builtin_amdgcn_s_memtime();

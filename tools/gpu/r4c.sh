@@ -1,0 +1,12 @@
+# round 4: config 4 (K = 64, compact vectors) bench + rocprof stats, config 5 bench, the native step at world 1
+cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+T=${1:-r4c}
+timeout -k 10 300 python -u bench.py > gpurun_out/$T.bench.log 2>&1 || exit $?
+grep '^{' gpurun_out/$T.bench.log > gpurun_out/$T.bench.json
+timeout -k 10 200 python -u bench.py --workload config5 > gpurun_out/$T.config5.log 2>&1 || exit $?
+grep '^{' gpurun_out/$T.config5.log > gpurun_out/$T.config5.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/$T.prof -o run -- \
+  python bench.py --no-cpu-baseline > gpurun_out/$T.prof.log 2>&1 || exit $?
+f=$(find /tmp/$T.prof -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/$T.kernel_stats.csv
+rm -rf /tmp/$T.prof
+VARIANTS=direct,native timeout -k 10 300 python -u tools/route_overhead.py > gpurun_out/$T.route_overhead.log 2>&1
