@@ -10,3 +10,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/$
 f=$(find /tmp/$T.prof -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/$T.kernel_stats.csv
 rm -rf /tmp/$T.prof
 VARIANTS=direct,native timeout -k 10 300 python -u tools/route_overhead.py > gpurun_out/$T.route_overhead.log 2>&1
+# the bench's N-rank control flow (two ranks sharing the GPU, gloo-staged exchange: not a measurement), incl. the
+# N > 1 parity gather + oracle replay
+FD_BENCH_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 2 --cards 4000000 --steps 20 --warmup 5 \
+  --latency-iters 20 --loaded-iters 20 --alone-iters 5 --timing-steps 20 --history-hours 6 --cpu-seconds 1 \
+  > gpurun_out/$T.gloo2.log 2>&1
