@@ -166,7 +166,7 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
   // is the LSTM head (already queued above), both walks in one launch and both sums + the blend in another
   // (fd::launch_forest_pair_blend: 3 launches instead of 6)
   bool paired = false;
-  if (small && ss == 0 && n_forests == 2) {
+  if (small && n_forests == 2 && (ss == 0 || (e.latency_fused && !use2))) {
     int fm[2], k = 0;
     for (int m = 0; m < M && k < 2; ++m)
       if (!(present && !present[m]) && slots[m] >= 0 && slots[m] != FD_SLOT_LSTM) fm[k++] = m;
@@ -187,14 +187,22 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
           if (m == fm[1]) pos_b = q;
           pc[q++] = m == fm[0] ? ca : m == fm[1] ? cb : cols[m];
         }
+        // the LSTM head on the side stream (small_streams 1): the blend launch waits for it
+        hipEvent_t lstm_done = nullptr;
+        if (aux_forked) {
+          FD_HIP(hipEventRecord(e.join_ev, e.aux_stream));
+          lstm_done = e.join_ev;
+        }
         if (fd::launch_forest_pair_blend(e, pa, pb, dX, n, ld, fd::blend_consts(p, present), pc, pos_a, pos_b, dfp,
-                                         dconf, ddec, drisk))
+                                         dconf, ddec, drisk, lstm_done))
           return false;
       }
-      paired = fd::launch_forest_pair(e, pa, pb, dX, n, ld, ca, cb);
-      if (paired) {
-        cols[fm[0]] = ca;
-        cols[fm[1]] = cb;
+      if (ss == 0) {  // (with side streams the per-forest launches below)
+        paired = fd::launch_forest_pair(e, pa, pb, dX, n, ld, ca, cb);
+        if (paired) {
+          cols[fm[0]] = ca;
+          cols[fm[1]] = cb;
+        }
       }
     }
   }

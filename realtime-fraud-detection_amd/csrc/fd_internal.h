@@ -463,7 +463,8 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
 struct BlendConsts;
 bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedForest& p2, const float* d_X, int64_t n,
                               int32_t ld, const BlendConsts& bc, const double* const* cols, int pos1, int pos2,
-                              double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk);
+                              double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk,
+                              hipEvent_t before_blend = nullptr);
 // windows.hip
 void windows_init(Engine& e, const fd_window_params& p);
 void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, int64_t n, bool flush,

@@ -1484,7 +1484,7 @@ void walk_groups(const PackedForest& pf, int64_t tiles, int& cpg, int& groups) {
 
 bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedForest& p2, const float* d_X, int64_t n,
                               int32_t ld, const BlendConsts& bc, const double* const* cols, int pos1, int pos2,
-                              double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk) {
+                              double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk, hipEvent_t before_blend) {
   if (n == 0 || &p1 == &p2 || !split_path(e, p1, n) || !split_path(e, p2, n)) return false;
   const bool x1 = p1.kind == FD_FOREST_XGB_BINARY_LOGISTIC, x2 = p2.kind == FD_FOREST_XGB_BINARY_LOGISTIC;
   if (x1 == x2) return false;  // one XGBoost and one IsolationForest
@@ -1540,6 +1540,7 @@ bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedFor
   pa.conf = dconf;
   pa.dec = ddec;
   pa.risk = drisk;
+  if (before_blend) FD_HIP(hipStreamWaitEvent(st, before_blend, 0));  // e.g. the LSTM head on a side stream
   hipLaunchKernelGGL(split_sum_pair_blend_kernel, dim3((unsigned)((n + kSumRows - 1) / kSumRows)), dim3(256), 0, st,
                      X.split.leaves.as<const float>(), X.n_trees, F.split.leaves.as<const double>(), F.n_trees, n, pa,
                      a.tile_nan, b.tile_nan);
