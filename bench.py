@@ -156,16 +156,11 @@ def pmc_counters(workload, B, groups, live_us, root=None):
     return out
 
 
-def ensemble_symbol(out, wide, top=False):
-    return f"fd::anon::ensemble_kernel<8, {out}, {'true' if wide else 'false'}, {'true' if top else 'false'}>"
+def ensemble_symbol(out, wide):
+    return f"fd::anon::ensemble_kernel<8, {out}, {'true' if wide else 'false'}>"
 FOREST6_SYMBOL = "fd::anon::forest_kernel6<8, 24, float, 1, 0>"
 LSTM4_SYMBOL = "fd::anon::lstm_kernel4"
 INGEST_SYMBOL = "fd::anon::ingest_json_kernel"
-
-
-# the engine's default for option "ensemble_scalar_top" (engine.hip / fd_internal.h Engine::ens_scalar_top): the
-# instantiation the bench's launches use, for the PMC lookup by symbol
-ENS_SCALAR_TOP = False
 
 
 def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=None, out=0, wide=True, vec_bytes=256):
@@ -181,13 +176,13 @@ def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=Non
         forest_bytes = sum(forest_blob_bytes(f) for f in forests)
         # the instantiation that ran: output form (0 columns, 1 route result records) and chunk layout (wide
         # unless the engine has RCCL communicators: engine option ensemble_chunks)
-        symbol = ensemble_symbol(out, wide, ENS_SCALAR_TOP)
+        symbol = ensemble_symbol(out, wide)
     elif timing.get(N.FD_TIMING_ENSEMBLE, (0.0, 0))[1]:  # one forest through the fused kernel (config 2)
         ms, launches = timing[N.FD_TIMING_ENSEMBLE]
         steps = B * forest.n_trees * depth
         forest_bytes = forest_blob_bytes(forest)
         label = "ensemble_kernel<D=8> over one forest (probabilities only)"
-        symbol = ensemble_symbol(2, True, ENS_SCALAR_TOP)
+        symbol = ensemble_symbol(2, True)
     else:
         steps = B * forest.n_trees * depth
         forest_bytes = forest_blob_bytes(forest)

@@ -468,9 +468,6 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     // communicators, else wide), 1 wide (24 / 16 trees), 2 compact (20 / 12: LDS room for an RCCL kernel beside)
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "ensemble_chunks must be 0, 1 or 2");
     e.ens_chunks = (int)value;
-  } else if (k == "ensemble_scalar_top") {  // fused kernel: 1 the walk's top three levels from scalar loads
-    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_scalar_top must be 0 or 1");
-    e.ens_scalar_top = value != 0;
   } else if (k == "latency_fused") {  // latency batches: 1 (default) both forests' walks in one launch and their
     // sums + the blend in another (fd::launch_forest_pair_blend); 0 the per-forest walk + sum launches + blend
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "latency_fused must be 0 or 1");

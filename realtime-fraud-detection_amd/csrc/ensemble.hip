@@ -166,112 +166,6 @@ __device__ __forceinline__ void walk_ens(uint32_t buf, int t0, uint32_t lane4, u
   }
 }
 
-// The same walk with the top three levels' node words in scalar registers (option "ensemble_scalar_top", D >= 3):
-// a tree's root, its two children and four grandchildren (heap slots 1-7) are the same for every lane, so they
-// come from one s_load_dwordx8 of the tree's block in global memory (L2 / scalar cache; loaded a chunk ahead) and
-// each lane selects its level-1 / level-2 node with v_cndmask on its own comparisons. That drops the root read
-// and the level-0 and level-1 children-pair reads (one ds_read_b32 + two ds_read_b64 of a walk's 16 LDS reads,
-// 1.3 of its 4.9 KB of LDS data per wave) for a few VALU selects, on a walk bound by LDS issue.
-typedef uint32_t u32x8t __attribute__((ext_vector_type(8)));
-template <int D, int TPG, int TM, bool NAN_AWARE>
-__device__ __forceinline__ void walk_ens_top(uint32_t buf, int t0, uint32_t lane4, const u32x8t (&top)[TM],
-                                             uint32_t (&leaf)[TPG]) {
-  static_assert(D >= 3 && TPG <= TM, "scalar top levels need depth >= 3");
-  uint32_t tb[TPG], node[TPG], kl[TPG], kr[TPG], xw[TPG];
-  bool r0[TPG];
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {
-    tb[j] = buf + (uint32_t)(t0 + j) * 1024u;
-    asm volatile("" : "+v"(tb[j]));
-    node[j] = top[j][1];
-    xw[j] = lds_load<uint16_t>((node[j] & 0xFC02u) | lane4);
-  }
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {  // level 0: the root
-    bool right = xw[j] > (node[j] >> 16);
-    if (NAN_AWARE) {
-      if (xw[j] == 0xFFFFu) right = (node[j] & 1u) == 0u;
-    }
-    r0[j] = right;
-    node[j] = right ? top[j][3] : top[j][2];
-    xw[j] = lds_load<uint16_t>((node[j] & 0xFC02u) | lane4);
-  }
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {  // level 1: heap slot 2 + r0; its children are slots 4 + 2 r0 + r1
-    bool right = xw[j] > (node[j] >> 16);
-    if (NAN_AWARE) {
-      if (xw[j] == 0xFFFFu) right = (node[j] & 1u) == 0u;
-    }
-    const uint32_t lo = right ? top[j][5] : top[j][4], hi = right ? top[j][7] : top[j][6];
-    node[j] = r0[j] ? hi : lo;
-    xw[j] = lds_load<uint16_t>((node[j] & 0xFC02u) | lane4);
-    if (D > 3) {
-      const u32x2 k = lds_load<u32x2>((node[j] & kLinkMask) | tb[j]);
-      kl[j] = k.x;
-      kr[j] = k.y;
-    }
-  }
-#pragma unroll
-  for (int l = 2; l < D; ++l) {  // levels 2 .. D-1: as walk_ens
-#pragma unroll
-    for (int j = 0; j < TPG; ++j) {
-      bool right = xw[j] > (node[j] >> 16);
-      if (NAN_AWARE) {
-        if (xw[j] == 0xFFFFu) right = (node[j] & 1u) == 0u;
-      }
-      if (l + 1 < D) {
-        uint32_t a = kl[j], b = kr[j];
-        asm volatile("" : "+v"(a), "+v"(b));
-        node[j] = right ? b : a;
-        xw[j] = lds_load<uint16_t>((node[j] & 0xFC02u) | lane4);
-        if (l + 2 < D) {
-          const u32x2 k = lds_load<u32x2>((node[j] & kLinkMask) | tb[j]);
-          kl[j] = k.x;
-          kr[j] = k.y;
-        }
-      } else {
-        leaf[j] = ((node[j] & kLinkMask) >> 2) + (right ? 1u : 0u);
-      }
-    }
-  }
-}
-
-template <int D, int TPG, int TM>
-__device__ __forceinline__ unsigned long long walk_pack_top(uint32_t cur, int gg, uint32_t lane4, bool tile_nan,
-                                                            const u32x8t (&top)[TM]) {
-  uint32_t leaf[TPG];
-  if (tile_nan)
-    walk_ens_top<D, TPG, TM, true>(cur, gg * TPG, lane4, top, leaf);
-  else
-    walk_ens_top<D, TPG, TM, false>(cur, gg * TPG, lane4, top, leaf);
-  uint32_t lo = 0, hi = 0;
-#pragma unroll
-  for (int j = 0; j < TPG; ++j) {
-    if (j < 4) lo |= leaf[j] << (8 * j);
-    else hi |= leaf[j] << (8 * (j - 4));
-  }
-  return ((unsigned long long)hi << 32) | lo;
-}
-
-// heap slots 0-7 of this wave's trees of chunk h (tree group gg) from the chunk in global memory, by scalar loads
-// issued in inline asm: the compiler would otherwise sink these invariant loads to their first use inside the walk
-// and wait there with lgkmcnt(0), which also drains every LDS read in flight (scalar loads share that counter and
-// return out of order). The caller issues them after a chunk's walk and completes them with top_wait() before the
-// chunk barrier, where the wave waits anyway.
-typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
-template <int TM>
-__device__ __forceinline__ void load_top(const EnsArgs& a, int h, int nA, int gg, int tpga, int tpgb,
-                                         u32x8 (&top)[TM]) {
-  const int fb = h >= nA ? 1 : 0;
-  const int tpg = fb ? tpgb : tpga;
-  const char* base = a.nodes[fb] + (size_t)(fb ? h - nA : h) * (size_t)a.stride[fb] + (size_t)(gg * tpg) * 1024u;
-#pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    if (j < tpg) asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(top[j]) : "s"(base), "i"(j * 1024));
-  }
-}
-__device__ __forceinline__ void top_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
 // Walk this wave's TPG trees of the chunk at `cur` (trees gg*TPG ...) for its 64 transactions; the leaf
 // indices (< 2^D <= 256) packed a byte per tree, in tree order, stored as one u64 per (tree group, txn).
 // (Measured: byte-per-tree stores of a [txn][16] tile cost ~5 us more per 64k batch; skewing the split
@@ -357,7 +251,7 @@ __device__ __forceinline__ void expand_compact(const float (&c)[kCompactWidth], 
   }
 }
 
-template <int D, int OUT, bool WIDE, bool STOP>
+template <int D, int OUT, bool WIDE>
 __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   constexpr int kCHA = EnsCfg<WIDE>::CHA, kCHB = EnsCfg<WIDE>::CHB;
   constexpr uint32_t kEnsBuf = EnsCfg<WIDE>::BUF;
@@ -543,12 +437,6 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   // then stages chunk g+1 into it; every wave walks chunk g and stores its packed leaf indices to
   // tile[g&1]; the owners complete their DMA; the barrier publishes chunk g+1 and tile[g&1].
   FD_ESTAMP(pr_t1);
-  constexpr bool kTop = STOP && D >= 3;
-  u32x8 top[kTop ? TPGA : 1];
-  if constexpr (kTop) {
-    if (G > 0) load_top(a, 0, nA, gg, TPGA, TPGB, top);
-    top_wait();
-  }
   for (int g = 0; g < G; ++g) {
     FD_ESTAMP(q0);
     const bool owner = gg == (a.owner_fixed ? 0 : ((g - 1) & 3));
@@ -574,17 +462,10 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     }
     const uint32_t cur = (g & 1) ? bufB : bufA, tw = (g & 1) ? tile1 : tile0;
     FD_ESTAMP(q1);
-    unsigned long long w;
-    if constexpr (kTop) {
-      w = g < nA ? walk_pack_top<D, TPGA, TPGA>(cur, gg, lane4, tile_nan, top)
-                 : walk_pack_top<D, TPGB, TPGA>(cur, gg, lane4, tile_nan, top);
-      if (g + 1 < G) load_top(a, g + 1, nA, gg, TPGA, TPGB, top);  // the next chunk's, landing during the barrier
-    } else {
-      w = g < nA ? walk_pack<D, TPGA>(cur, gg, lane4, tile_nan) : walk_pack<D, TPGB>(cur, gg, lane4, tile_nan);
-    }
+    const unsigned long long w =
+        g < nA ? walk_pack<D, TPGA>(cur, gg, lane4, tile_nan) : walk_pack<D, TPGB>(cur, gg, lane4, tile_nan);
     lds_store<unsigned long long>(tw + (uint32_t)(gg * kTile + txn) * 8u, w);
     FD_ESTAMP(q2);
-    if constexpr (kTop) top_wait();  // the next chunk's top words (and this wave's LDS ops) before the barrier
     if (owner) dma_wait();
 #ifdef FD_FOREST_PROFILE
     const unsigned long long q2d = __builtin_amdgcn_s_memtime();
@@ -668,32 +549,24 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   }
 }
 
-template <int OUT, bool WIDE, bool STOP>
+template <int OUT, bool WIDE>
 const void* pick_ensemble(int D) {
   switch (D) {
-    case 1: return (const void*)ensemble_kernel<1, OUT, WIDE, false>;
-    case 2: return (const void*)ensemble_kernel<2, OUT, WIDE, false>;
-    case 3: return (const void*)ensemble_kernel<3, OUT, WIDE, STOP>;
-    case 4: return (const void*)ensemble_kernel<4, OUT, WIDE, STOP>;
-    case 5: return (const void*)ensemble_kernel<5, OUT, WIDE, STOP>;
-    case 6: return (const void*)ensemble_kernel<6, OUT, WIDE, STOP>;
-    case 7: return (const void*)ensemble_kernel<7, OUT, WIDE, STOP>;
-    case 8: return (const void*)ensemble_kernel<8, OUT, WIDE, STOP>;
+    case 1: return (const void*)ensemble_kernel<1, OUT, WIDE>;
+    case 2: return (const void*)ensemble_kernel<2, OUT, WIDE>;
+    case 3: return (const void*)ensemble_kernel<3, OUT, WIDE>;
+    case 4: return (const void*)ensemble_kernel<4, OUT, WIDE>;
+    case 5: return (const void*)ensemble_kernel<5, OUT, WIDE>;
+    case 6: return (const void*)ensemble_kernel<6, OUT, WIDE>;
+    case 7: return (const void*)ensemble_kernel<7, OUT, WIDE>;
+    case 8: return (const void*)ensemble_kernel<8, OUT, WIDE>;
     default: return nullptr;
   }
 }
 
-template <bool STOP>
-const void* pick_ensemble_t(int out, bool wide, int D) {
-  if (wide)
-    return out == 1 ? pick_ensemble<1, true, STOP>(D) : out == 2 ? pick_ensemble<2, true, STOP>(D)
-                                                                 : pick_ensemble<0, true, STOP>(D);
-  return out == 1 ? pick_ensemble<1, false, STOP>(D) : out == 2 ? pick_ensemble<2, false, STOP>(D)
-                                                                : pick_ensemble<0, false, STOP>(D);
-}
-
-const void* pick_ensemble(int out, bool wide, int D, bool stop) {
-  return stop ? pick_ensemble_t<true>(out, wide, D) : pick_ensemble_t<false>(out, wide, D);
+const void* pick_ensemble(int out, bool wide, int D) {
+  if (wide) return out == 1 ? pick_ensemble<1, true>(D) : out == 2 ? pick_ensemble<2, true>(D) : pick_ensemble<0, true>(D);
+  return out == 1 ? pick_ensemble<1, false>(D) : out == 2 ? pick_ensemble<2, false>(D) : pick_ensemble<0, false>(D);
 }
 
 fd_tree_arrays arrays_of(const PackedForest& f) {
@@ -916,7 +789,7 @@ void plan_args(const EnsemblePlan& P, const float* dX, int64_t n, int32_t ld, bo
 
 // out: 0 blended columns, 1 route result records, 2 the single forest's probability column (a.fp)
 bool run_plan(Engine& e, const EnsemblePlan& P, EnsArgs& a, int out, int timing_kind) {
-  const void* fn = pick_ensemble(out, P.wide, P.D, e.ens_scalar_top);
+  const void* fn = pick_ensemble(out, P.wide, P.D);
   if (!fn) return false;
   const size_t lds = ens_lds(P.nf, P.wide);
   FD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -412,7 +412,6 @@ struct Engine {
   int forest_variant = 0;  // "forest_kernel" option
   bool ens_owner_fixed = true;  // "ensemble_owner" option (A/B of the fused kernel's chunk-owner schedule)
   int ens_chunks = 0;           // "ensemble_chunks": 0 auto, 1 wide, 2 compact chunk layout (ensemble.hip)
-  bool ens_scalar_top = false;  // "ensemble_scalar_top": the walk's top three levels from scalar loads (ensemble.hip)
   int lstm_rows = 0;  // "lstm_rows" option: transactions per LSTM workgroup tile (0 auto, 4 or 16)
   bool ensemble_on = true;  // "ensemble" option: the fused XGBoost + IsolationForest + blend kernel (auto)
   bool timing = false;

@@ -8,7 +8,7 @@ import bench
 
 
 def _summary(tmp_path, workload="config4", batch=65536):
-    ens = bench.ensemble_symbol(0, True, False)
+    ens = bench.ensemble_symbol(0, True)
     doc = {"batch": batch, "kernels": {
         ens: {"hbm_bytes_per_launch": 29_700_000, "l2_hit_rate": 0.92, "dispatches": 40},
         "fd::anon::feat_slot_kernel [grid 65536]": {"hbm_bytes_per_launch": 18_400_000, "l2_hit_rate": 0.69,
@@ -27,7 +27,7 @@ def test_pmc_traffic_matches_the_running_instantiation(tmp_path):
     ens = _summary(tmp_path)
     assert bench.pmc_traffic("config4", 65536, ens, root=tmp_path) == 29_700_000
     assert bench.pmc_traffic("config4", 1024, ens, root=tmp_path) is None  # another batch size
-    assert bench.pmc_traffic("config4", 65536, bench.ensemble_symbol(0, True, True), root=tmp_path) is None
+    assert bench.pmc_traffic("config4", 65536, bench.ensemble_symbol(0, False), root=tmp_path) is None
     assert bench.pmc_traffic("config4", 65536, bench.ensemble_symbol(1, False), root=tmp_path) is None
     assert bench.pmc_traffic("config9", 65536, ens, root=tmp_path) is None  # no file
 

@@ -68,47 +68,33 @@ def _check(engine, xgb, ifm, X, names=("xgboost_primary", "isolation_forest"), s
         assert fp[i] == rfp and fused[2][i] == rcf
 
 
-@pytest.mark.parametrize("top", [0, 1])
 @pytest.mark.parametrize("chunks", [1, 2])
 @pytest.mark.parametrize("strategy", [0, 1, 2])
-def test_fused_matches_per_model_and_oracle(engine, strategy, chunks, top):
-    """both chunk layouts (engine option ensemble_chunks: 1 wide 24 / 16 trees, 2 compact 20 / 12), the walk's top
-    three levels from LDS or from scalar loads (ensemble_scalar_top)"""
+def test_fused_matches_per_model_and_oracle(engine, strategy, chunks):
+    """both chunk layouts (engine option ensemble_chunks: 1 wide 24 / 16 trees, 2 compact 20 / 12)"""
     xgb, ifm = _models(64, 8, seed=3)
     X = synth.feature_matrix(N, 64, seed=4, nan_frac=0.01)
     engine.set_option("ensemble_chunks", chunks)
-    engine.set_option("ensemble_scalar_top", top)
     try:
         _check(engine, xgb, ifm, X, strategy=strategy)
     finally:
         engine.set_option("ensemble_chunks", 0)
-        engine.set_option("ensemble_scalar_top", 0)
 
 
-@pytest.mark.parametrize("top", [0, 1])
-def test_reversed_model_order_and_depth_padding(engine, top):
+def test_reversed_model_order_and_depth_padding(engine):
     xgb, ifm = _models(40, 6, n_trees=90, seed=5)  # XGBoost depth 6 padded to the IsolationForest's 8
     X = synth.feature_matrix(N + 123, 40, seed=6)
-    engine.set_option("ensemble_scalar_top", top)
-    try:
-        _check(engine, xgb, ifm, X, names=("isolation_forest", "xgboost_primary"))
-    finally:
-        engine.set_option("ensemble_scalar_top", 0)
+    _check(engine, xgb, ifm, X, names=("isolation_forest", "xgboost_primary"))
 
 
-@pytest.mark.parametrize("top", [0, 1])
-def test_shallow_forests(engine, top):
-    """depth 3 (the scalar walk's smallest: all split levels but the last from scalar registers) and depth 2"""
+def test_shallow_forests(engine):
+    """depth 3 and depth 2 forests (IsolationForest max_samples 8 / 4) through the fused kernel"""
     for d, s in ((3, 31), (2, 33)):
         Xr = synth.feature_matrix(4096, 24, seed=s)
         xgb = xgboost_from_json_doc(synth.xgboost_doc(70, d, 24, Xr, seed=s + 1, base_score=0.4))
         ifm = iforest_from_sklearn(synth.isolation_forest(Xr.astype(np.float64), n_estimators=20, max_samples=2 ** d))
         X = synth.feature_matrix(N, 24, seed=s + 2, nan_frac=0.01)
-        engine.set_option("ensemble_scalar_top", top)
-        try:
-            _check(engine, xgb, ifm, X)
-        finally:
-            engine.set_option("ensemble_scalar_top", 0)
+        _check(engine, xgb, ifm, X)
 
 
 def test_short_rows_are_missing_columns(engine):
