@@ -1301,6 +1301,8 @@ def make_parser():
                     help="engine option small_streams (latency batches: side streams for the LSTM / other forests)")
     ap.add_argument("--lstm-rows", type=int, choices=[0, 4, 16], default=None,
                     help="engine option lstm_rows (LSTM tile: 0 auto, 4 or 16 transactions per workgroup)")
+    ap.add_argument("--engine-option", action="append", default=[], metavar="KEY=VALUE",
+                    help="fd_engine_set_option before the workload's setup (A/B runs; the product defaults otherwise)")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--alone-iters", type=int, default=20,
                     help="steps run one at a time after the latency loop, every launch timed: each kernel's "
@@ -1361,6 +1363,9 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     eng = fdengine.FraudEngine(dev.index)
+    for kv in args.engine_option:
+        k, v = kv.split("=")
+        eng.set_option(k.strip(), int(v))
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
     wl = WORKLOADS[args.workload](args, rank, dev, eng)
@@ -1580,6 +1585,7 @@ def main():
             "parity_vs_oracle": parity,
             "window_saturation": saturation,
             "step_launch": "direct kernel launches",
+            "engine_options": dict(kv.split("=") for kv in args.engine_option) or None,
         }
         if hasattr(wl, "counter_groups"):
             line["counters"] = pmc_counters(wl.name, args.batch, wl.counter_groups(roof), line["kernel_avg_us"])

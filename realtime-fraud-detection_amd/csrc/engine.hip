@@ -468,6 +468,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     // communicators, else wide), 1 wide (24 / 16 trees), 2 compact (20 / 12: LDS room for an RCCL kernel beside)
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "ensemble_chunks must be 0, 1 or 2");
     e.ens_chunks = (int)value;
+  } else if (k == "compact_vectors") {  // pipelined stream: 1 (default) the fused kernel's batches carry the
+    // compact 24-float vector when nobody asked for the vectors; 0 always the 64-wide one (outputs identical)
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "compact_vectors must be 0 or 1");
+    e.compact_vectors = value != 0;
   } else if (k == "latency_fused") {  // latency batches: 1 (default) both forests' walks in one launch and their
     // sums + the blend in another (fd::launch_forest_pair_blend); 0 the per-forest walk + sum launches + blend
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "latency_fused must be 0 or 1");
@@ -984,7 +988,7 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   hipEvent_t before_buckets = e.pipe_feat_live[prev] ? e.pipe_feat_ev[prev] : nullptr;
   // the fused kernel alone reads the vectors and nobody asked for them: the compact form (96 instead of 256 B per
   // transaction written here and read by the ensemble kernel, fd_internal.h kCompactSlot)
-  const bool compact = d_vectors == nullptr && fd::ensemble_applies(e, *params, slots, present, n);
+  const bool compact = e.compact_vectors && d_vectors == nullptr && fd::ensemble_applies(e, *params, slots, present, n);
   e.pipe_vec[s].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
   float* vec = e.pipe_vec[s].as<float>();
   float* seq = nullptr;

@@ -90,7 +90,8 @@ struct EnsArgs {
   const float* thr;
   int thr_off[kMaxFeatures + 1];  // per-feature table offsets into thr (kernel arguments: scalar loads)
   int vec4;                       // rows 16-B aligned (ld % 4 == 0, aligned X): float4 row loads
-  int compact;                    // X rows are the compact vector (kCompactWidth floats), expanded here
+  int compact;                    // X rows are the compact vector (kCompactWidth floats), binned here
+  uint16_t cbin[kMaxFeatures];    // compact mode: the bins of the constant slots (0 or 0.5), per plan
   int owner_fixed;                // chunk owner: tree group 0 (the oldest waves: highest issue priority), else rotating
   int n_pass;
   int pass_f[kMaxPass + 1];
@@ -241,13 +242,98 @@ static int g_eprof_next = 0;
 #define FD_ESTAMP(var)
 #endif
 
-// slots [16 Q, 16 Q + 16) of the 64-wide vector from its compact form (fd_internal.h compact_src)
-template <int Q>
-__device__ __forceinline__ void expand_compact(const float (&c)[kCompactWidth], float (&v)[16]) {
+// bin = #{t <= v} by binary lifting, as bin_of, for L values in lockstep: branch-free (clamped index + select), so
+// the L reads of a step issue back to back; tables staged in LDS at tl (element g at thr_pad(g)) or, glob, in global
+template <int L>
+__device__ __forceinline__ void search_lockstep(const float (&vv)[L], const int (&o)[L], const int (&cnt)[L],
+                                                int (&pos)[L], int steps, bool glob, uint32_t tl, int o0,
+                                                const float* __restrict__ thr) {
+  if (!glob) {
+    for (int st = steps; st > 0; st >>= 1) {
+      float t[L];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int src = compact_src(16 * Q + k);  // a constant after unrolling
-    v[k] = src >= 0 ? c[src >= 0 ? src : 0] : (src == -2 ? 0.5f : 0.f);
+      for (int k = 0; k < L; ++k) {
+        const int np = pos[k] + st;
+        const int idx = np <= cnt[k] ? np - 1 : 0;
+        t[k] = lds_load<float>(tl + (uint32_t)thr_pad(o[k] - o0 + idx) * 4u);
+      }
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+        const int np = pos[k] + st;
+        pos[k] = (np <= cnt[k] && t[k] <= vv[k]) ? np : pos[k];
+      }
+    }
+  } else {
+    for (int st = steps; st > 0; st >>= 1) {
+      float t[L];
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+        const int np = pos[k] + st;
+        t[k] = thr[o[k] + (np <= cnt[k] ? np - 1 : 0)];
+      }
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+        const int np = pos[k] + st;
+        pos[k] = (np <= cnt[k] && t[k] <= vv[k]) ? np : pos[k];
+      }
+    }
+  }
+}
+
+// Compact rows (the pipeline): the 42 constant slots' bins are the plan's (a.cbin), written without a search —
+// thread Q of a transaction writes the bin-tile dwords (feature pairs) Q, Q + 4, ... — and the 22 varying slots are
+// dealt round-robin to the four threads of the transaction (compact slots Q, Q + 4, ...: 6, 6, 5, 5 searches instead
+// of up to 16 per thread over the 64-wide row)
+template <int Q>
+__device__ __forceinline__ void bin_compact_constants(const EnsArgs& a, uint16_t* Xs, int txn) {
+  uint32_t* X32 = reinterpret_cast<uint32_t*>(Xs);
+#pragma unroll
+  for (int j = Q; j < kMaxFeatures / 2; j += 4) {
+    const int f = 2 * j;
+    const bool c0 = compact_src(f) < 0 && f < a.nf, c1 = compact_src(f + 1) < 0 && f + 1 < a.nf;
+    if (c0 && c1)
+      X32[j * 256 + txn] = (uint32_t)a.cbin[f] | ((uint32_t)a.cbin[f + 1] << 16);
+    else if (c0)
+      Xs[j * 512 + txn * 2] = a.cbin[f];
+    else if (c1)
+      Xs[j * 512 + txn * 2 + 1] = a.cbin[f + 1];
+  }
+}
+
+template <int Q, int L>
+__device__ __forceinline__ void bin_compact_pass(const EnsArgs& a, const float (&c)[kCompactWidth], uint16_t* Xs,
+                                                 int txn, int f0, int f1, bool glob, uint32_t tl, int o0,
+                                                 int& anynan) {
+  constexpr int NV = (kCompactSlots - Q + 3) / 4;  // compact slots Q, Q + 4, ... below kCompactSlots
+#pragma unroll
+  for (int g0 = 0; g0 < NV; g0 += L) {
+    float vv[L];
+    int o[L], cnt[L], pos[L];
+    bool act[L];
+    int steps = 0;
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      const int i = g0 + k;
+      const int ci = Q + 4 * (i < NV ? i : 0);
+      const int f = kCompactSlot[ci];
+      act[k] = i < NV && f >= f0 && f < f1 && f < a.nf;
+      vv[k] = act[k] ? c[ci] : 0.f;
+      o[k] = act[k] ? a.thr_off[f] : o0;
+      cnt[k] = act[k] ? a.thr_off[f + 1] - o[k] : 0;
+      pos[k] = 0;
+      steps = max(steps, lift_steps(cnt[k]));
+    }
+    search_lockstep<L>(vv, o, cnt, pos, steps, glob, tl, o0, a.thr);
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      const int i = g0 + k;
+      const int f = kCompactSlot[Q + 4 * (i < NV ? i : 0)];
+      if (act[k]) {
+        const bool nan = vv[k] != vv[k];
+        anynan |= nan ? 1 : 0;
+        Xs[(f >> 1) * 512 + txn * 2 + (f & 1)] = nan ? (uint16_t)0xFFFFu : (uint16_t)pos[k];
+      }
+    }
   }
 }
 
@@ -290,9 +376,9 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     // (1) raw values: thread (q, txn) loads features [16 q, 16 q + 16) of its row in one go (all loads in
     // flight together) and keeps them in registers until they are binned
     float v[16];
-    if (valid && a.compact) {  // the pipeline's compact row (6 x 16 B), expanded to this thread's 16 slots
+    float c[kCompactWidth];  // compact mode: the whole compact row (each of the 4 threads bins its share of it)
+    if (valid && a.compact) {  // the pipeline's compact row (6 x 16 B); the constant slots' bins straight away
       const float4* x4 = reinterpret_cast<const float4*>(a.X + row * (int64_t)kCompactWidth);
-      float c[kCompactWidth];
 #pragma unroll
       for (int k = 0; k < kCompactWidth / 4; ++k) {
         const float4 t = x4[k];
@@ -302,10 +388,10 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
         c[4 * k + 3] = t.w;
       }
       switch (q) {  // wave-uniform
-        case 0: expand_compact<0>(c, v); break;
-        case 1: expand_compact<1>(c, v); break;
-        case 2: expand_compact<2>(c, v); break;
-        default: expand_compact<3>(c, v); break;
+        case 0: bin_compact_constants<0>(a, Xs, txn); break;
+        case 1: bin_compact_constants<1>(a, Xs, txn); break;
+        case 2: bin_compact_constants<2>(a, Xs, txn); break;
+        default: bin_compact_constants<3>(a, Xs, txn); break;
       }
     } else if (valid) {
       const float* xr = a.X + row * (int64_t)a.ld;
@@ -354,7 +440,14 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
 #ifdef FD_FOREST_PROFILE
       if (p < 3) pr_st[1 + 2 * p] = __builtin_amdgcn_s_memtime();
 #endif
-      if (valid) {
+      if (valid && a.compact) {
+        switch (q) {
+          case 0: bin_compact_pass<0, kLock>(a, c, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
+          case 1: bin_compact_pass<1, kLock>(a, c, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
+          case 2: bin_compact_pass<2, kLock>(a, c, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
+          default: bin_compact_pass<3, kLock>(a, c, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
+        }
+      } else if (valid) {
 #pragma unroll
         for (int kk = 0; kk < 16; kk += kLock) {
           const int fb = fq + kk;
@@ -673,6 +766,14 @@ bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb, bool wide) {
   P.thr.ensure(std::max<size_t>(4, thr.size() * sizeof(float)));
   if (!thr.empty()) FD_HIP(hipMemcpy(P.thr.ptr, thr.data(), thr.size() * sizeof(float), hipMemcpyHostToDevice));
   P.h_thr_off = off;
+  // the bins of the compact vector's constant slots (0 or 0.5): #{t <= value} in the feature's merged table
+  P.h_cbin.assign(kMaxFeatures, 0);
+  for (int f = 0; f < nf && f < kMaxFeatures; ++f) {
+    const int src = compact_src(f);
+    if (src >= 0) continue;
+    const float val = src == -2 ? 0.5f : 0.0f;
+    P.h_cbin[f] = (uint16_t)(std::upper_bound(merged[f].begin(), merged[f].end(), val) - merged[f].begin());
+  }
   P.max_feature_thr = maxc;
   P.slot[0] = sa;
   P.slot[1] = sb;
@@ -758,6 +859,7 @@ void plan_args(const EnsemblePlan& P, const float* dX, int64_t n, int32_t ld, bo
   FD_REQUIRE(P.nf <= kMaxFeatures, FD_ERR_UNSUPPORTED, "ensemble: more than 64 features");
   for (int f = 0; f <= P.nf; ++f) a.thr_off[f] = P.h_thr_off[f];
   a.owner_fixed = owner_fixed ? 1 : 0;
+  for (int f = 0; f < kMaxFeatures; ++f) a.cbin[f] = f < (int)P.h_cbin.size() ? P.h_cbin[f] : 0;
   a.vec4 = (ld % 4 == 0 && (reinterpret_cast<uintptr_t>(dX) & 15u) == 0) ? 1 : 0;
   // binning passes: consecutive features whose tables fit bufA + bufB + the tiles; a larger table alone,
   // searched in global memory

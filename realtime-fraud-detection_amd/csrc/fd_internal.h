@@ -151,6 +151,7 @@ struct EnsemblePlan {
   double if_offset = 0.0, if_denominator = 0.0;
   DeviceBuffer nodes[2], thr;  // per forest: chunk blobs (node blocks + leaf values); merged threshold tables
   std::vector<int32_t> h_thr_off;  // merged table offsets (host copy: binning pass plan)
+  std::vector<uint16_t> h_cbin;    // bins of the compact vector's constant slots (ensemble.hip)
   int max_feature_thr = 0;
 };
 
@@ -398,6 +399,7 @@ struct Engine {
   bool pipe_copy_vec[kPipeSlots] = {};  // that copy also read the slot's vectors (the slot's next features wait)
   int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
+  bool compact_vectors = true;  // "compact_vectors": the pipelined stream's compact scoring vectors (engine.hip)
   int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;

@@ -1,17 +1,17 @@
-# round 4: config 4 (K = 64, compact vectors) bench + rocprof stats, config 5 bench, the native step at world 1
+# round 4: parity of the compact-binning prologue, then config 4 (K = 64) with / without compact vectors, config 5
+# with / without the fused latency pair
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${1:-r4c}
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_pipeline.py tests/test_gpu_sharding_loopback.py tests/test_gpu_latency.py tests/test_gpu_ensemble.py \
+  tests/test_gpu_configs.py > gpurun_out/$T.pytest.log 2>&1; rc=$?; tail -3 gpurun_out/$T.pytest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u bench.py > gpurun_out/$T.bench.log 2>&1 || exit $?
 grep '^{' gpurun_out/$T.bench.log > gpurun_out/$T.bench.json
+timeout -k 10 300 python -u bench.py --engine-option compact_vectors=0 --no-cpu-baseline > gpurun_out/$T.bench_c0.log 2>&1 || exit $?
+grep '^{' gpurun_out/$T.bench_c0.log > gpurun_out/$T.bench_c0.json
 timeout -k 10 200 python -u bench.py --workload config5 > gpurun_out/$T.config5.log 2>&1 || exit $?
 grep '^{' gpurun_out/$T.config5.log > gpurun_out/$T.config5.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/$T.prof -o run -- \
-  python bench.py --no-cpu-baseline > gpurun_out/$T.prof.log 2>&1 || exit $?
-f=$(find /tmp/$T.prof -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/$T.kernel_stats.csv
-rm -rf /tmp/$T.prof
-VARIANTS=direct,native timeout -k 10 300 python -u tools/route_overhead.py > gpurun_out/$T.route_overhead.log 2>&1
-# the bench's N-rank control flow (two ranks sharing the GPU, gloo-staged exchange: not a measurement), incl. the
-# N > 1 parity gather + oracle replay
-FD_BENCH_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 2 --cards 4000000 --steps 20 --warmup 5 \
-  --latency-iters 20 --loaded-iters 20 --alone-iters 5 --timing-steps 20 --history-hours 6 --cpu-seconds 1 \
-  > gpurun_out/$T.gloo2.log 2>&1
+timeout -k 10 200 python -u bench.py --workload config5 --engine-option latency_fused=0 --no-cpu-baseline > gpurun_out/$T.config5_f0.log 2>&1 || exit $?
+grep '^{' gpurun_out/$T.config5_f0.log > gpurun_out/$T.config5_f0.json
+timeout -k 10 200 python -u bench.py --workload config5 --small-streams 1 --no-cpu-baseline > gpurun_out/$T.config5_s1.log 2>&1 || exit $?
+grep '^{' gpurun_out/$T.config5_s1.log > gpurun_out/$T.config5_s1.json
