@@ -95,7 +95,24 @@ struct Reader {
   const unsigned char* st;
   int shift;
   __device__ __forceinline__ int operator[](int i) const { return st[shift + i]; }
+  // message bytes i .. i+3 (little-endian) from two dword reads and one v_alignbyte (i >= 0; the stage slot is
+  // padded so the second dword of the last byte stays inside it)
+  __device__ __forceinline__ unsigned word(int i) const {
+    const int p = shift + i;
+    const unsigned* w = reinterpret_cast<const unsigned*>(st) + (p >> 2);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (unsigned)(p & 3));
+  }
 };
+
+// SWAR byte masks over one dword (bit 7 of each byte): the lowest flagged byte of the borrow form is exact
+__device__ __forceinline__ unsigned first_zero_mask(unsigned x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
+__device__ __forceinline__ unsigned exact_zero_mask(unsigned x) {  // every byte exact (no borrow)
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+// bytes that end a raw string run: '"', '\\' or a control character
+__device__ __forceinline__ unsigned string_stop_mask(unsigned w) {
+  return first_zero_mask(w ^ 0x22222222u) | first_zero_mask(w ^ 0x5C5C5C5Cu) | ((w - 0x20202020u) & ~w & 0x80808080u);
+}
 
 __device__ __forceinline__ bool is_ws(int c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 
@@ -106,24 +123,32 @@ __device__ __forceinline__ int hexval(int c) {
   return -1;
 }
 
-// streaming view of one decoded JSON string: FNV-1a, UTF-16 length (Java String.length()), the first 8
-// decoded bytes, and the "bot" / "crawler" substring matchers (FeatureExtractor.java:447-451)
+// streaming view of one decoded JSON string: FNV-1a, the first 8 decoded bytes and the byte count; with UA
+// also the UTF-16 length (Java String.length()) and the "bot" / "crawler" substring matchers
+// (FeatureExtractor.java:447-451) — only the user-agent fallback decoder needs those, every other member scans
+// with the lean form
+template <bool UA>
 struct StrStats {
   uint64_t fnv = kFnvBasis;
   uint64_t head = 0;  // first 8 decoded bytes, little-endian
-  uint64_t roll = 0;  // last 8 decoded bytes
+  uint64_t roll = 0;  // UA: last 8 decoded bytes
   int nbytes = 0;
-  int units = 0;
-  bool bot = false, crawler = false;
+  int units = 0;  // UA
+  bool bot = false, crawler = false;  // UA
   bool escaped = false;
   __device__ __forceinline__ void byte(unsigned c) {  // branchless: selects, no divergent branches per byte
     fnv = fnv_step(fnv, (unsigned char)c);
     const uint64_t sh = (uint64_t)c << (8 * (nbytes & 7));
     head |= (nbytes < 8) ? sh : 0ull;
     ++nbytes;
-    roll = (roll << 8) | c;
-    bot = bot | ((roll & 0xFFFFFFull) == 0x626F74ull);                     // "bot"
-    crawler = crawler | ((roll & 0xFFFFFFFFFFFFFFull) == 0x637261776C6572ull);  // "crawler"
+    if constexpr (UA) {
+      roll = (roll << 8) | c;
+      bot = bot | ((roll & 0xFFFFFFull) == 0x626F74ull);                     // "bot"
+      crawler = crawler | ((roll & 0xFFFFFFFFFFFFFFull) == 0x637261776C6572ull);  // "crawler"
+    }
+  }
+  __device__ __forceinline__ void add_units(int n) {
+    if constexpr (UA) units += n;
   }
   __device__ __forceinline__ void utf8(unsigned cp) {
     if (cp < 0x80) {
@@ -145,17 +170,31 @@ struct StrStats {
 };
 
 // decode the string whose opening quote is at s[pos]; returns the index after the closing quote, -1 if malformed
-__device__ __forceinline__ int scan_string(const Reader& s, int pos, int end, StrStats& st) {
+template <class S>
+__device__ __forceinline__ int scan_string(const Reader& s, int pos, int end, S& st) {
   int i = pos + 1;
   while (i < end) {
-    // the raw run: one tight loop, no per-byte branches besides the loop exit
-    int c = s[i];
-    while (c >= 0x20 && c != '"' && c != '\\') {
-      st.byte((unsigned)c);
-      // UTF-16 units of raw UTF-8: one per lead byte, two for a 4-byte sequence
-      st.units += (int)((c & 0xC0) != 0x80) + (int)(c >= 0xF0);
-      ++i;
-      c = i < end ? s[min(i, end - 1)] : -1;
+    // the raw run, four bytes per LDS access: the first stop byte ('"', '\\', control) from the SWAR masks, the
+    // bytes before it fed to the stats (predicated, no per-byte branches)
+    int c;
+    for (;;) {
+      const unsigned w = s.word(i);
+      const unsigned stop = string_stop_mask(w);
+      const int nb = min(stop ? (__builtin_ctz(stop) >> 3) : 4, end - i);
+  #pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < nb) {
+          const unsigned b = (w >> (8 * k)) & 0xFFu;
+          st.byte(b);
+          // UTF-16 units of raw UTF-8: one per lead byte, two for a 4-byte sequence
+          st.add_units((int)((b & 0xC0u) != 0x80u) + (int)(b >= 0xF0u));
+        }
+      }
+      i += nb;
+      if (nb < 4) {
+        c = i < end ? (int)((w >> (8 * nb)) & 0xFFu) : -1;
+        break;
+      }
     }
     if (c == '"') return i + 1;
     if (c != '\\') return -1;  // unescaped control character, or the end
@@ -182,7 +221,7 @@ __device__ __forceinline__ int scan_string(const Reader& s, int pos, int end, St
           v = v * 16 + h;
         }
         i += 4;
-        st.units += 1;
+        st.add_units(1);
         if (v >= 0xD800 && v <= 0xDBFF && i + 6 <= end && s[i] == '\\' && s[i + 1] == 'u') {
           int lo = 0;
           bool ok = true;
@@ -193,7 +232,7 @@ __device__ __forceinline__ int scan_string(const Reader& s, int pos, int end, St
           }
           if (ok && lo >= 0xDC00 && lo <= 0xDFFF) {
             i += 6;
-            st.units += 1;
+            st.add_units(1);
             st.utf8(0x10000u + (((unsigned)v - 0xD800u) << 10) + ((unsigned)lo - 0xDC00u));
             continue;
           }
@@ -204,10 +243,90 @@ __device__ __forceinline__ int scan_string(const Reader& s, int pos, int end, St
       }
       default: return -1;
     }
-    st.units += 1;
+    st.add_units(1);
     st.byte(cp);
   }
   return -1;
+}
+
+// a run of decimal digits from s[i] (at least i < end), four bytes per LDS access: per-byte digit test on the
+// dword (t = byte ^ '0' is a digit iff its high nibble is 0 and its low nibble + 6 stays below 16), the digits
+// before the first other byte fed to `digit` in order; returns the index after the run
+template <class F>
+__device__ __forceinline__ int digit_run(const Reader& s, int i, int end, F&& digit) {
+  for (;;) {
+    const unsigned t = s.word(i) ^ 0x30303030u;
+    const unsigned other = (t & 0xF0F0F0F0u) | (((t & 0x0F0F0F0Fu) + 0x06060606u) & 0x10101010u);
+    const int nb = min(other ? (__builtin_ctz(other) >> 3) : 4, end - i);
+  #pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < nb) digit((int)((t >> (8 * k)) & 0xFu));
+    i += nb;
+    if (nb < 4) return i;
+  }
+}
+
+// scan_number (ingest_parse.h, the RFC 8259 grammar and the same Decimal) with the integer and fraction digit runs
+// read a dword at a time; the exponent (rare) byte by byte
+__device__ __forceinline__ int scan_number_w(const Reader& s, int pos, int end, Decimal& d) {
+  d = Decimal{};
+  int i = pos;
+  if (i < end && s[i] == '-') {
+    d.neg = true;
+    ++i;
+  }
+  if (i >= end) return -1;
+  int nd = 0;  // significant digits taken
+  const int c0 = s[i];
+  if (c0 == '0') {
+    ++i;
+  } else if (c0 >= '1' && c0 <= '9') {
+    i = digit_run(s, i, end, [&](int g) {
+      if (nd < 19) {
+        d.w = d.w * 10 + (uint64_t)g;
+        ++nd;
+      } else {
+        d.many = d.many || g != 0;  // a dropped non-zero digit: the value is truncated
+        ++d.q;
+      }
+    });
+  } else {
+    return -1;
+  }
+  if (i < end && s[i] == '.') {
+    d.frac_or_exp = true;
+    ++i;
+    if (i >= end || s[i] < '0' || s[i] > '9') return -1;
+    i = digit_run(s, i, end, [&](int g) {
+      if (nd == 0 && g == 0) {
+        --d.q;  // leading zero of the fraction: not significant
+      } else if (nd < 19) {
+        d.w = d.w * 10 + (uint64_t)g;
+        ++nd;
+        --d.q;
+      } else {
+        d.many = d.many || g != 0;
+      }
+    });
+  }
+  if (i < end && (s[i] == 'e' || s[i] == 'E')) {
+    d.frac_or_exp = true;
+    ++i;
+    bool eneg = false;
+    if (i < end && (s[i] == '+' || s[i] == '-')) {
+      eneg = s[i] == '-';
+      ++i;
+    }
+    if (i >= end || s[i] < '0' || s[i] > '9') return -1;
+    int64_t e = 0;
+    while (i < end && s[i] >= '0' && s[i] <= '9') {
+      if (e < 100000) e = e * 10 + (s[i] - '0');
+      ++i;
+    }
+    d.q += eneg ? -e : e;
+  }
+  if (d.w == 0) d.many = false;  // zero (any digits): exact
+  return i;
 }
 
 __device__ __forceinline__ bool lit_at(const Reader& s, int i, int end, const char* w, int n);
@@ -272,7 +391,7 @@ __device__ __forceinline__ int skip_value(const Reader& s, int pos, int end) {
         value_done = true;
       } else {
         Decimal d;
-        i = scan_number(s, i, end, d);
+        i = scan_number_w(s, i, end, d);
         if (i < 0) return -1;
         value_done = true;
       }
@@ -325,6 +444,28 @@ __device__ __forceinline__ double nan_d() { return __builtin_nan(""); }
 // returned (conversion happens at the caller's single decimal -> binary64 site); has[t] = 0 absent/null, 1 set.
 __device__ __forceinline__ int scan_latlon(const Reader& s, int pos, int end, Decimal& d0, Decimal& d1, int& has0,
                                            int& has1) {
+  // fast path: the simulator's shape {"lat": x, "lon": y} (numbers or numeric strings, one space after ':' and
+  // ','), recognised by dword compares; any other shape -> the general walk below from the start
+  if (pos + 8 <= end && s.word(pos) == 0x616C227Bu && s.word(pos + 4) == 0x203A2274u) {  // {"la  t":_
+    int i = pos + 8;
+    for (int t = 0; t < 2; ++t) {  // one number-scan site for both coordinates
+      const bool q = s[i] == '"';
+      Decimal tmp;
+      int e = scan_number_w(s, q ? i + 1 : i, end, tmp);
+      if (e >= 0 && q) e = (e < end && s[e] == '"') ? e + 1 : -1;
+      if (e < 0) break;
+      if (t == 0) {
+        d0 = tmp;
+        if (!(e + 9 <= end && s.word(e) == 0x6C22202Cu && s.word(e + 4) == 0x3A226E6Fu && s[e + 8] == ' ')) break;
+        i = e + 9;  // ,_"l  on":  _
+      } else {
+        d1 = tmp;
+        if (e >= end || s[e] != '}') break;
+        has0 = has1 = 1;
+        return e + 1;
+      }
+    }
+  }
   has0 = has1 = 0;
   if (lit_at(s, pos, end, "null", 4)) return pos + 4;
   if (s[pos] != '{') return -1;
@@ -351,18 +492,12 @@ __device__ __forceinline__ int scan_latlon(const Reader& s, int pos, int end, De
         if (t == 0) has0 = 0; else has1 = 0;
         i += 4;
       } else {
-        int a = i, b = end;
+        // a numeric string: the number must end at the closing quote (its characters are never '"' or '\\')
         const bool quoted = s[i] == '"';
-        if (quoted) {
-          b = a + 1;
-          while (b < end && s[b] != '"' && s[b] != '\\') ++b;
-          if (b >= end || s[b] != '"') return -1;
-          ++a;
-        }
         Decimal tmp;
-        const int e = scan_number(s, a, b, tmp);
-        if (e < 0 || (quoted && e != b)) return -1;
-        i = quoted ? b + 1 : e;
+        const int e = scan_number_w(s, quoted ? i + 1 : i, end, tmp);
+        if (e < 0 || (quoted && (e >= end || s[e] != '"'))) return -1;
+        i = quoted ? e + 1 : e;
         if (t == 0) {
           d0 = tmp;
           has0 = 1;
@@ -420,7 +555,7 @@ struct Val {
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) ingest_json_kernel(const unsigned char* __restrict__ buf,
                                                           const int64_t* __restrict__ offsets, int64_t n, Tables T,
                                                           fd_ingest_out out, int stop_after) {
-  __shared__ __attribute__((aligned(16))) unsigned char stage[kSlots][kStage];
+  __shared__ __attribute__((aligned(16))) unsigned char stage[kSlots][kStage + 16];  // + the word reads' tail
   __shared__ int colon[kSlots][kMaxMembers];
   __shared__ int nmem[kSlots], ncomma[kSlots], shift_s[kSlots], len_s[kSlots];
   __shared__ unsigned status_s[kSlots];
@@ -640,14 +775,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
       my_status |= FD_INGEST_MALFORMED;
       continue;
     }
+    // the key's opening quote: the last unescaped '"' before kc, four bytes per LDS access
     int ko = kc - 1;
-    for (;; --ko) {
-      if (ko < 0) break;
-      if (s[ko] == '"') {
-        int r = 0;
-        for (int q = ko - 1; q >= 0 && s[q] == '\\'; --q) ++r;
-        if (!(r & 1)) break;
+    while (ko >= 0) {
+      const int lo = max(ko - 3, 0);
+      const unsigned z = exact_zero_mask(s.word(lo) ^ 0x22222222u) & (0xFFFFFFFFu >> (8 * (3 - (ko - lo))));
+      if (!z) {
+        ko = lo - 1;
+        continue;
       }
+      const int q = lo + ((31 - __builtin_clz(z)) >> 3);
+      int r = 0;
+      for (int b = q - 1; b >= 0 && s[b] == '\\'; --b) ++r;
+      ko = q;
+      if (!(r & 1)) break;
+      --ko;
     }
     int pre = ko - 1;
     while (pre >= 0 && is_ws(s[pre])) --pre;
@@ -655,7 +797,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
       my_status |= FD_INGEST_MALFORMED;
       continue;
     }
-    StrStats key;
+    StrStats<false> key;
     if (scan_string(s, ko, L, key) != kc + 1) {
       my_status |= FD_INGEST_MALFORMED;
       continue;
@@ -668,12 +810,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
       continue;
     }
     int e = -1;
-    if (f < 0) {  // unknown property: validated, then ignored (@JsonIgnoreProperties(ignoreUnknown = true))
-      e = skip_value(s, v, L);
-      while (e >= 0 && e < L && is_ws(s[e])) ++e;
-      if (e < 0 || e >= L || (s[e] != ',' && s[e] != '}')) my_status |= FD_INGEST_MALFORMED;
-      continue;
-    }
     if (f == F_UA && s[v] == '"') {  // the message's longest string: scanned by the whole wave below
       if (r == 0) {
         ua_pend0 = true;
@@ -686,12 +822,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
       }
       continue;
     }
-    // ---- one token scan per member: string / literal / number / location object
+    // ---- one token scan per member: string / literal / number / location object. An unknown property
+    //      (f < 0: validated, then ignored — @JsonIgnoreProperties(ignoreUnknown = true)) shares the scalar
+    //      scans; only an object / array value takes the generic skip_value walk.
     Val val;
     val.null = false;
     const int ch = s[v];
-    int kind = -1;  // 0 null, 1 string, 2 number, 3 true, 4 false, 5 location
-    StrStats st;
+    int kind = -1;  // 0 null, 1 string, 2 number, 3 true, 4 false, 5 location, 6 skipped structure
+    StrStats<false> st;
     Decimal dec0, dec1;
     int has0 = 0, has1 = 0;
     int num_a = -1, num_b = L;
@@ -718,13 +856,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
     } else if (ch == '-' || (ch >= '0' && ch <= '9')) {
       kind = 2;
       num_a = v;
+    } else if (f < 0 && (ch == '{' || ch == '[')) {
+      e = skip_value(s, v, L);
+      kind = 6;
     }
     if (e < 0 && kind != 2) {
       my_status |= FD_INGEST_MALFORMED;
       continue;
     }
     if (num_a >= 0 && e >= -1) {  // the single number scan
-      const int ne = scan_number(s, num_a, num_b, dec0);
+      const int ne = scan_number_w(s, num_a, num_b, dec0);
       if (kind == 2) e = ne;
       else if (ne != num_b) e = -1;
       has0 = e >= 0 ? 1 : 0;
@@ -735,12 +876,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
     }
     if (kind == 0) val.null = true;
     // literal text of a scalar bound to a String property (Jackson's scalar -> String coercion)
-    if ((kind == 2 || kind == 3 || kind == 4) && f != F_AMOUNT && f != F_SCORE && f != F_HOUR && f != F_WEEKEND &&
-        f != F_FRAUD) {
-      for (int q = v; q < e; ++q) {
-        st.byte((unsigned)s[q]);
-        ++st.units;
-      }
+    if ((kind == 2 || kind == 3 || kind == 4) && f >= 0 && f != F_AMOUNT && f != F_SCORE && f != F_HOUR &&
+        f != F_WEEKEND && f != F_FRAUD) {
+      for (int q = v; q < e; ++q) st.byte((unsigned)s[q]);
       kind = 1;
     }
     bool bad = false;
@@ -754,8 +892,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
                             (st.nbytes >= 3 && (st.head & 0xFFFFFFull) == 0x2E3031ull) ||       // "10."
                             (st.nbytes >= 7 && (st.head & 0xFFFFFFFFFFFFFFull) == 0x2E36312E323731ull);  // "172.16."
           val.u = priv ? 1 : 2;
-        } else if (f == F_UA) {
-          val.u = (st.bot || st.crawler || st.units < 20) ? 1 : 0;
+        } else if (f == F_UA) {  // literal text only (strings are deferred): ASCII, no "bot" / "crawler"
+          val.u = st.nbytes < 20 ? 1 : 0;
         } else if (f == F_MERCHANT_ID) {
           val.u = (uint64_t)(int64_t)table_find(T.merchants, h, -1);
         } else if (f == F_PAY || f == F_TTYPE || f == F_CTYPE) {
@@ -862,6 +1000,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
       my_status |= FD_INGEST_MALFORMED;
       continue;
     }
+    if (f < 0) continue;  // an ignored property, validated
     if (r == 0) {
       my_field0 = f;
       my_colon0 = c;
@@ -961,7 +1100,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
     int e = r == 0 ? ua_e0 : ua_e1;
     unsigned flag = r == 0 ? ua_f0 : ua_f1;
     if (r == 0 ? ua_serial0 : ua_serial1) {
-      StrStats st;
+      StrStats<true> st;
       e = scan_string(s, v, L, st);
       flag = (st.bot || st.crawler || st.units < 20) ? 1u : 0u;
     }

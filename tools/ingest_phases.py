@@ -1,4 +1,5 @@
-"""Per-phase timing of the ingest kernel (option "ingest_stop_after"): stage / + structure / + members / full."""
+"""Per-phase timing of the ingest kernel (option "ingest_stop_after"): stage / + structure / + members / full.
+Arguments: the stop_after values to run (default 1 2 3 0)."""
 import sys
 import time
 sys.path[:0] = [".", "realtime-fraud-detection_amd"]
@@ -17,7 +18,7 @@ buf, off = pack(msgs)
 dbuf, doff = torch.from_numpy(buf.copy()).cuda(), torch.from_numpy(off).cuda()
 cols, ptrs = device_columns(B)
 eng.set_stream(torch.cuda.current_stream().cuda_stream)
-for stop in (1, 2, 3, 0):
+for stop in [int(a) for a in sys.argv[1:]] or [1, 2, 3, 0]:
     eng.set_option("ingest_stop_after", stop)
     for _ in range(3):
         codec.parse_device(dbuf.data_ptr(), doff.data_ptr(), B, ptrs)
