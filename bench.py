@@ -717,7 +717,7 @@ class Config4(Config3):
         # load factor ~0.75 (1.25 slots per owned card, as a power of two): the open-addressed key array stays a
         # linear probe of a line or two, and 100 M cards with K = 64 ring events (1152 B per slot) fit one GPU's HBM
         # (2^27 slots = 155 GB); the same factor at every N keeps the per-GPU work the same (weak scaling)
-        while cap < int(n_own_est * 1.25) + 65536:
+        while cap < int(n_own_est * args.slots_per_card) + 65536:
             cap *= 2
         self.cap = cap
         eng.state_init(cap, self.mode, self.K)
@@ -983,7 +983,7 @@ class Config4(Config3):
         return {"workload": "config4: card-hash-sharded keyed state (fmix64 owner) + RCCL all-to-all routing "
                             "(48-B txn records out, 24-B results back) -> features + XGBoost 500x8 + "
                             "IsolationForest 100 + blend on the owner, 64k-txn micro-batch per GPU per step",
-                "cards": self.cards, "cards_per_gpu": self.n_owned, "window_mode": "sliding" if self.mode else
+                "cards": self.cards, "cards_per_gpu": self.n_owned, "card_slots": self.cap, "window_mode": "sliding" if self.mode else
                 "redis_compat", "ring_k": self.K, "trees": self.T, "depth": self.D, "features": 64,
                 "batch_per_gpu": self.B, "global_batch": self.B * world,
                 "stream": self.stream, "warm_state": self.warm_info,
@@ -1290,6 +1290,9 @@ def make_parser():
     ap.add_argument("--cards", type=int, default=None,
                     help="cards resident in HBM (config4 default 100M over the node; config3 default 10M)")
     ap.add_argument("--window", choices=["sliding", "redis"], default="sliding")
+    ap.add_argument("--slots-per-card", type=float, default=1.25,
+                    help="config 4: card-table slots per owned card before rounding up to a power of two (1.25: "
+                         "2^27 slots at 100 M cards, load ~0.75)")
     ap.add_argument("--ring-k", type=int, default=64,
                     help="sliding windows: ring events per card (the bench line reports window_saturation: "
                          "transactions whose 24 h window held all K)")
