@@ -357,7 +357,7 @@ int fd_engine_destroy(fd_engine* eng) {
       t.vvals[w].release();
     }
   }
-  for (auto* b : {&e.state.headers, &e.state.keys, &e.state.ring, &e.state.merchants, &e.state.err, &e.state.sat,
+  for (auto* b : {&e.state.pages, &e.state.keys, &e.state.merchants, &e.state.err, &e.state.sat,
                   &e.state.bucket_scr})
     b->release();
   for (auto& g : e.state.gs)

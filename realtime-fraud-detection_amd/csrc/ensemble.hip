@@ -301,7 +301,7 @@ __device__ __forceinline__ void bin_compact_constants(const EnsArgs& a, uint16_t
 }
 
 template <int Q, int L>
-__device__ __forceinline__ void bin_compact_pass(const EnsArgs& a, const float (&c)[kCompactWidth], uint16_t* Xs,
+__device__ __forceinline__ void bin_compact_pass(const EnsArgs& a, const float (&v)[16], uint16_t* Xs,
                                                  int txn, int f0, int f1, bool glob, uint32_t tl, int o0,
                                                  int& anynan) {
   constexpr int NV = (kCompactSlots - Q + 3) / 4;  // compact slots Q, Q + 4, ... below kCompactSlots
@@ -317,7 +317,7 @@ __device__ __forceinline__ void bin_compact_pass(const EnsArgs& a, const float (
       const int ci = Q + 4 * (i < NV ? i : 0);
       const int f = kCompactSlot[ci];
       act[k] = i < NV && f >= f0 && f < f1 && f < a.nf;
-      vv[k] = act[k] ? c[ci] : 0.f;
+      vv[k] = act[k] ? v[i < NV ? i : 0] : 0.f;  // v[i]: compact slot Q + 4 i of the row
       o[k] = act[k] ? a.thr_off[f] : o0;
       cnt[k] = act[k] ? a.thr_off[f + 1] - o[k] : 0;
       pos[k] = 0;
@@ -375,18 +375,15 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     const int fq = q * 16;
     // (1) raw values: thread (q, txn) loads features [16 q, 16 q + 16) of its row in one go (all loads in
     // flight together) and keeps them in registers until they are binned
+    // compact mode: thread q's share of the pipeline's compact row, slots q, q + 4, ... (6, 6, 5, 5 of the 22) in
+    // v[0..5] — the same registers as the full row's 16 (one value array live through the passes, not two: 54
+    // VGPRs, the bucket kernel's wave fits beside the ensemble's four per SIMD); the constant slots' bins straight
+    // away
     float v[16];
-    float c[kCompactWidth];  // compact mode: the whole compact row (each of the 4 threads bins its share of it)
-    if (valid && a.compact) {  // the pipeline's compact row (6 x 16 B); the constant slots' bins straight away
-      const float4* x4 = reinterpret_cast<const float4*>(a.X + row * (int64_t)kCompactWidth);
+    if (valid && a.compact) {
+      const float* xr = a.X + row * (int64_t)kCompactWidth;
 #pragma unroll
-      for (int k = 0; k < kCompactWidth / 4; ++k) {
-        const float4 t = x4[k];
-        c[4 * k] = t.x;
-        c[4 * k + 1] = t.y;
-        c[4 * k + 2] = t.z;
-        c[4 * k + 3] = t.w;
-      }
+      for (int i = 0; i < 6; ++i) v[i] = q + 4 * i < kCompactSlots ? xr[q + 4 * i] : 0.f;
       switch (q) {  // wave-uniform
         case 0: bin_compact_constants<0>(a, Xs, txn); break;
         case 1: bin_compact_constants<1>(a, Xs, txn); break;
@@ -442,10 +439,10 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
 #endif
       if (valid && a.compact) {
         switch (q) {
-          case 0: bin_compact_pass<0, kLock>(a, c, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
-          case 1: bin_compact_pass<1, kLock>(a, c, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
-          case 2: bin_compact_pass<2, kLock>(a, c, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
-          default: bin_compact_pass<3, kLock>(a, c, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
+          case 0: bin_compact_pass<0, kLock>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
+          case 1: bin_compact_pass<1, kLock>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
+          case 2: bin_compact_pass<2, kLock>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
+          default: bin_compact_pass<3, kLock>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
         }
       } else if (valid) {
 #pragma unroll

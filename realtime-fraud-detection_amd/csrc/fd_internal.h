@@ -206,6 +206,27 @@ struct __attribute__((aligned(128))) CardHeader {
 static_assert(sizeof(CardHeader) == 128, "CardHeader must be one 128-B line");
 constexpr int kCardHeaderBytes = (int)sizeof(CardHeader);
 
+// one event of a card's ring (sliding windows): time and cents
+struct __attribute__((aligned(16))) RingEvent {
+  long long ts;
+  long long cents;
+};
+
+// The card table's state pages: slot s owns bytes [s * stride, (s + 1) * stride) of one allocation — its
+// 128-B header, then (sliding mode) its K ring events of 16 B. A transaction's state (header and the ring
+// entries it evicts / appends) lies in one contiguous page: one address translation per card instead of one
+// per array (round 4; before, headers and rings were two arrays of their own).
+struct CardPages {
+  char* base;
+  long long stride;  // bytes per slot: 128 + 16 K (sliding), 128 (redis_compat)
+  __host__ __device__ __forceinline__ CardHeader* hdr(long long s) const {
+    return reinterpret_cast<CardHeader*>(base + s * stride);
+  }
+  __host__ __device__ __forceinline__ RingEvent* ring(long long s) const {
+    return reinterpret_cast<RingEvent*>(base + s * stride + kCardHeaderBytes);
+  }
+};
+
 #ifdef __HIP_DEVICE_COMPILE__
 #define FD_CARD_SLOT_QUAL __device__ __forceinline__
 #else
@@ -218,7 +239,7 @@ constexpr int kCardHeaderBytes = (int)sizeof(CardHeader);
 // dependent load round instead of one per slot. A key seen as 0 is claimed by CAS, whose result also corrects a
 // stale read (another CU's insert): it returns the key that is there. An insert mirrors the key into the slot's
 // header (snapshots and occupancy read it there). Returns the slot, -1 when the table is full.
-FD_CARD_SLOT_QUAL long long card_slot(unsigned long long* keys, CardHeader* hdr, long long mask, unsigned long long key) {
+FD_CARD_SLOT_QUAL long long card_slot(unsigned long long* keys, CardPages pg, long long mask, unsigned long long key) {
   if (key == 0ull) key = 1ull;  // 0 marks an empty slot
   unsigned long long m = key;
   m ^= m >> 33;
@@ -245,7 +266,7 @@ FD_CARD_SLOT_QUAL long long card_slot(unsigned long long* keys, CardHeader* hdr,
         if (k == 0ull) {
           const unsigned long long old = atomicCAS(&keys[g + j], 0ull, key);
           if (old == 0ull) {
-            hdr[g + j].key = key;
+            pg.hdr(g + j)->key = key;
             return g + j;
           }
           if (old == key) return g + j;
@@ -262,7 +283,7 @@ FD_CARD_SLOT_QUAL long long card_slot(unsigned long long* keys, CardHeader* hdr,
     if (k == 0ull) {
       const unsigned long long old = atomicCAS(&keys[h], 0ull, key);
       if (old == 0ull) {
-        hdr[h].key = key;
+        pg.hdr(h)->key = key;
         return h;
       }
       if (old == key) return h;
@@ -281,7 +302,10 @@ struct CardStore {
   int S = 0;         // LSTM history events per card (0 = off)
   int bucket_keys = 0;  // option "bucket_keys": transactions per bucket workgroup (0 auto, features.hip)
   int64_t n_merchants = 0;
-  DeviceBuffer headers, keys, ring, merchants, err, seq;  // keys: the compact key array card_slot probes
+  DeviceBuffer pages, keys, merchants, err, seq;  // pages: CardPages (header + ring per slot); keys: the compact
+                                                  // key array card_slot probes
+  long long page_bytes = kCardHeaderBytes;
+  CardPages view() const { return CardPages{static_cast<char*>(pages.ptr), page_bytes}; }
   DeviceBuffer sat;  // u64: transactions whose 24 h window held K prior events (counter "window_saturated")
   // per-batch card grouping (feat_slot -> feat_bucket): per-txn slots, keys per bucket, [NB][C] bucket regions,
   // overflow counters by batch parity + the overflow list (key, bucket), prep records. Two sets: the pipelined

@@ -60,11 +60,6 @@ __device__ unsigned long long g_fprof[4096 * 8];
 #define FD_FSTAMP(k)
 #endif
 
-struct __attribute__((aligned(16))) RingEvent {
-  long long ts;
-  long long cents;
-};
-
 struct Merchant {
   double fraud_rate;  // NaN = null
   double mult;
@@ -80,21 +75,22 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long k) {
 }
 
 
-__global__ void __launch_bounds__(256) users_load_kernel(CardHeader* H, unsigned long long* K, long long mask, int64_t n,
+__global__ void __launch_bounds__(256) users_load_kernel(CardPages P, unsigned long long* K, long long mask, int64_t n,
                                                          const unsigned long long* key, const double* avg,
                                                          const int* age, const unsigned long long* dfp,
                                                          unsigned* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const long long s = card_slot(K, H, mask, key[i]);
+  const long long s = card_slot(K, P, mask, key[i]);
   if (s < 0) {
     atomicOr(err, 1u);
     return;
   }
-  H[s].avg = avg[i];
-  H[s].age = age[i];
-  H[s].flags |= 1u;
-  for (int f = 0; f < 3; ++f) H[s].fp[f] = dfp[i * 3 + f];
+  CardHeader* h = P.hdr(s);
+  h->avg = avg[i];
+  h->age = age[i];
+  h->flags |= 1u;
+  for (int f = 0; f < 3; ++f) h->fp[f] = dfp[i * 3 + f];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -246,7 +242,7 @@ __device__ __forceinline__ Prep load_prep(const Prep* __restrict__ src) {
 // (block, bucket) reserving the block's run, then each key at its rank in the run. A bucket that outgrows its
 // capacity C spills the rest to an overflow list (bucket id + key) its bucket kernel scans. No count / scan /
 // scatter passes: the bucket kernel's inputs are complete when this kernel ends.
-__global__ void __launch_bounds__(kST) feat_slot_kernel(CardHeader* H, unsigned long long* K, long long mask, int64_t n, TxnSrc src,
+__global__ void __launch_bounds__(kST) feat_slot_kernel(CardPages P, unsigned long long* K, long long mask, int64_t n, TxnSrc src,
                                                         const Merchant* __restrict__ merchants, int nm,
                                                         unsigned nbm, unsigned C, unsigned* __restrict__ slot,
                                                         Prep* __restrict__ prep, unsigned* __restrict__ fill,
@@ -264,7 +260,7 @@ __global__ void __launch_bounds__(kST) feat_slot_kernel(CardHeader* H, unsigned 
   bool have = false;
   if (i < n) {
     const Txn t = src.get(i);  // in flight with the probe
-    const long long s = card_slot(K, H, mask, src.get_key(i));
+    const long long s = card_slot(K, P, mask, src.get_key(i));
     store_prep(prep + i, make_prep(t, merchants, nm));
     if (s < 0) {
       atomicOr(err, 1u);
@@ -638,8 +634,7 @@ __device__ __forceinline__ void seq_step(const Outputs& o, unsigned s, unsigned&
 }
 
 struct BucketArgs {
-  CardHeader* H;
-  RingEvent* ring;
+  CardPages P;  // header + ring per card slot
   int K;
   int64_t n;
   const Prep* prep;  // [n] in arrival order (feat_slot_kernel)
@@ -655,12 +650,12 @@ struct BucketArgs {
 
 template <int MODE>
 __device__ void process_short(const BucketArgs& a, unsigned s, const unsigned long long* keys, int len) {
-  CardHeader* h = a.H + s;
+  CardHeader* h = a.P.hdr(s);
   CardRegs c;
   Profile p;
   Prep t = load_prep(a.prep + (unsigned)keys[0]);  // in flight with the header
   load_card(h, c, p);
-  RingEvent* rg = a.ring + (size_t)s * a.K;
+  RingEvent* rg = a.P.ring(s);
   for (int q = 0; q < len; ++q) {
     const int64_t i = (int64_t)(unsigned)keys[q];
     if (q > 0) t = load_prep(a.prep + i);
@@ -710,8 +705,8 @@ __device__ void block_scan_max(int* v) {  // inclusive, kBT entries
 template <int MODE>
 __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned long long* keys, int L, LongLds& sm) {
   const int tid = threadIdx.x, K = a.K, S = a.out.S;
-  CardHeader* h = a.H + s;
-  RingEvent* rg = a.ring + (size_t)s * K;
+  CardHeader* h = a.P.hdr(s);
+  RingEvent* rg = a.P.ring(s);
   if (tid == 0) {
     sm.hdr = *h;
     sm.carry_c = sm.hdr.rc_cnt;
@@ -1183,12 +1178,20 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
   }
 }
 
-__global__ void __launch_bounds__(256) count_cards_kernel(const CardHeader* H, int64_t cap,
-                                                          unsigned long long* out) {
+__global__ void __launch_bounds__(256) count_cards_kernel(CardPages P, int64_t cap, unsigned long long* out) {
   unsigned long long c = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x)
-    c += (H[i].key != 0ull);
+    c += (P.hdr(i)->key != 0ull);
   atomicAdd(out, c);
+}
+
+// zero every slot's header (the rings need no clearing: a header with ring_n 0 holds no events); 16 B per thread
+__global__ void __launch_bounds__(256) clear_headers_kernel(CardPages P, int64_t cap) {
+  const int64_t words = cap * (kCardHeaderBytes / 16);
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < words; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = t / (kCardHeaderBytes / 16);
+    reinterpret_cast<uint4*>(P.hdr(s))[t - s * (kCardHeaderBytes / 16)] = make_uint4(0u, 0u, 0u, 0u);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1259,7 +1262,7 @@ __device__ __forceinline__ bool operating_at(const MerchExt& me, int h) {
 
 __device__ __forceinline__ double to_rad(double d) { return d * 0.017453292519943295; }  // Math.toRadians
 
-__global__ void __launch_bounds__(256) feat_ext_kernel(const CardHeader* __restrict__ H,
+__global__ void __launch_bounds__(256) feat_ext_kernel(CardPages P,
                                                        const UserExt* __restrict__ uext,
                                                        const Merchant* __restrict__ merchants,
                                                        const MerchExt* __restrict__ mext, int nm, int n_mext,
@@ -1274,7 +1277,7 @@ __global__ void __launch_bounds__(256) feat_ext_kernel(const CardHeader* __restr
   const double* r = raw + (size_t)i * FD_RAW_FEATURES;
   const unsigned s = slot[i];
   const bool has_slot = s != 0xffffffffu;
-  const CardHeader h = has_slot ? H[s] : CardHeader{};
+  const CardHeader h = has_slot ? *P.hdr(s) : CardHeader{};
   const bool has_user = has_slot && (h.flags & 1u) != 0u;
   UserExt ue{};
   if (has_user && uext != nullptr) ue = uext[s];
@@ -1529,12 +1532,12 @@ __global__ void __launch_bounds__(256) feat_ext_kernel(const CardHeader* __restr
   rules[i] = out;
 }
 
-__global__ void __launch_bounds__(256) users_ext_load_kernel(CardHeader* H, unsigned long long* K, UserExt* U, long long mask, int64_t n,
+__global__ void __launch_bounds__(256) users_ext_load_kernel(CardPages P, unsigned long long* K, UserExt* U, long long mask, int64_t n,
                                                              const unsigned long long* key, const UserExt* src,
                                                              unsigned* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const long long s = card_slot(K, H, mask, key[i]);
+  const long long s = card_slot(K, P, mask, key[i]);
   if (s < 0) {
     atomicOr(err, 1u);
     return;
@@ -1571,9 +1574,10 @@ void state_init(Engine& e, const fd_state_params& p) {
   st.cap = cap;
   st.mode = p.window_mode;
   st.K = p.window_mode == FD_WINDOW_SLIDING ? p.ring_k : 1;
-  st.headers.ensure((size_t)cap * sizeof(CardHeader));
+  st.page_bytes = kCardHeaderBytes + (st.mode == FD_WINDOW_SLIDING ? (long long)st.K * (long long)sizeof(RingEvent) : 0);
+  if (st.pages.bytes < (size_t)cap * st.page_bytes) st.pages.release();  // free before the keys grow (peak HBM)
   st.keys.ensure((size_t)cap * sizeof(unsigned long long));
-  st.ring.ensure((size_t)cap * st.K * sizeof(RingEvent));
+  st.pages.ensure((size_t)cap * st.page_bytes);
   st.S = p.seq_len;
   if (st.S) st.seq.ensure((size_t)cap * st.S * kSeqInput * sizeof(float));
   // extended user profiles are per slot: a re-initialised table starts without them (fd_state_load_users_ext
@@ -1592,7 +1596,8 @@ void state_init(Engine& e, const fd_state_params& p) {
 void state_clear(Engine& e) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
-  FD_HIP(hipMemsetAsync(st.headers.ptr, 0, (size_t)st.cap * sizeof(CardHeader), e.stream));
+  hipLaunchKernelGGL(clear_headers_kernel, dim3(4096), dim3(256), 0, e.stream, st.view(), (int64_t)st.cap);
+  FD_HIP(hipGetLastError());
   FD_HIP(hipMemsetAsync(st.keys.ptr, 0, (size_t)st.cap * sizeof(unsigned long long), e.stream));
   if (st.uext.ptr) FD_HIP(hipMemsetAsync(st.uext.ptr, 0, (size_t)st.cap * sizeof(UserExt), e.stream));
   FD_HIP(hipMemsetAsync(st.err.ptr, 0, 16, e.stream));
@@ -1616,7 +1621,7 @@ int64_t state_count(Engine& e) {
   DeviceBuffer tmp;
   tmp.ensure(8);
   FD_HIP(hipMemsetAsync(tmp.ptr, 0, 8, e.stream));
-  hipLaunchKernelGGL(count_cards_kernel, dim3(1024), dim3(256), 0, e.stream, st.headers.as<const CardHeader>(),
+  hipLaunchKernelGGL(count_cards_kernel, dim3(1024), dim3(256), 0, e.stream, st.view(),
                      st.cap, tmp.as<unsigned long long>());
   FD_HIP(hipGetLastError());
   unsigned long long c = 0;
@@ -1651,7 +1656,7 @@ void load_users(Engine& e, const fd_users& u) {
   FD_HIP(hipMemcpyAsync(a.ptr, u.avg_amount, u.n * 8, hipMemcpyHostToDevice, e.stream));
   FD_HIP(hipMemcpyAsync(g.ptr, u.account_age_days, u.n * 4, hipMemcpyHostToDevice, e.stream));
   FD_HIP(hipMemcpyAsync(f.ptr, u.device_fp, u.n * 24, hipMemcpyHostToDevice, e.stream));
-  hipLaunchKernelGGL(users_load_kernel, dim3(grid_for(u.n)), dim3(256), 0, e.stream, st.headers.as<CardHeader>(),
+  hipLaunchKernelGGL(users_load_kernel, dim3(grid_for(u.n)), dim3(256), 0, e.stream, st.view(),
                      st.keys.as<unsigned long long>(),
                      (long long)(st.cap - 1), u.n, k.as<const unsigned long long>(), a.as<const double>(),
                      g.as<const int>(), f.as<const unsigned long long>(), st.err.as<unsigned>());
@@ -1698,7 +1703,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, s));
   hipLaunchKernelGGL(feat_slot_kernel, dim3((unsigned)((n + kST - 1) / kST)), dim3(kST), 2 * nb * sizeof(unsigned),
-                     s, st.headers.as<CardHeader>(), st.keys.as<unsigned long long>(), (long long)(st.cap - 1), n, src,
+                     s, st.view(), st.keys.as<unsigned long long>(), (long long)(st.cap - 1), n, src,
                      st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, C, g.slot.as<unsigned>(),
                      g.prep.as<Prep>(), g.bucket_fill.as<unsigned>(), g.pairs.as<unsigned long long>(),
                      g.ovf_cnt.as<unsigned>() + par, g.ovf_key.as<unsigned long long>(), g.ovf_b.as<unsigned>(),
@@ -1714,8 +1719,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
     attrs = true;
   }
   BucketArgs a{};
-  a.H = st.headers.as<CardHeader>();
-  a.ring = st.ring.as<RingEvent>();
+  a.P = st.view();
   a.K = st.K;
   a.n = n;
   a.prep = g.prep.as<const Prep>();
@@ -1808,7 +1812,7 @@ void load_users_ext(Engine& e, const fd_users_ext& u) {
   d.ensure(h.size() * sizeof(UserExt));
   FD_HIP(hipMemcpyAsync(k.ptr, u.key, u.n * 8, hipMemcpyHostToDevice, e.stream));
   FD_HIP(hipMemcpyAsync(d.ptr, h.data(), h.size() * sizeof(UserExt), hipMemcpyHostToDevice, e.stream));
-  hipLaunchKernelGGL(users_ext_load_kernel, dim3(grid_for(u.n)), dim3(256), 0, e.stream, st.headers.as<CardHeader>(),
+  hipLaunchKernelGGL(users_ext_load_kernel, dim3(grid_for(u.n)), dim3(256), 0, e.stream, st.view(),
                      st.keys.as<unsigned long long>(),
                      st.uext.as<UserExt>(), (long long)(st.cap - 1), u.n, k.as<const unsigned long long>(),
                      d.as<const UserExt>(), st.err.as<unsigned>());
@@ -1869,7 +1873,7 @@ void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context
            reinterpret_cast<const unsigned long long*>(t.device_fp), t.ip_class, t.hour, t.weekend, nullptr};
   CtxArgs ca{c.geo_lat, c.geo_lon, c.merchant_lat, c.merchant_lon, c.payment_method, c.transaction_type,
              c.card_type, c.user_agent_flag, c.fraud_score};
-  hipLaunchKernelGGL(feat_ext_kernel, dim3(grid_for(n)), dim3(256), 0, e.stream, st.headers.as<const CardHeader>(),
+  hipLaunchKernelGGL(feat_ext_kernel, dim3(grid_for(n)), dim3(256), 0, e.stream, st.view(),
                      st.uext.ptr ? st.uext.as<const UserExt>() : nullptr,
                      st.merchants.as<const Merchant>(), st.mext.ptr ? st.mext.as<const MerchExt>() : nullptr,
                      (int)st.n_merchants, (int)st.n_mext, n, a, ca,

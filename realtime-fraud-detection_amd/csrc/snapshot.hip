@@ -80,17 +80,18 @@ RecMap rec_map(int K, int S, bool uext) {
   return m;
 }
 
-struct Planes {  // the per-slot state arrays as 16-B words
-  uint4* headers;
-  uint4* ring;
+struct Planes {  // the per-slot state as 16-B words: the card pages (header, then ring), LSTM history, extended profile
+  uint4* pages;
+  long long page_words;
+  bool ring;  // the pages hold the K ring events (sliding mode); redis_compat records carry zero ring words
   uint4* seq;
   uint4* uext;
 };
 
-// the word of `slot`'s state that record word w maps to
+// the word of `slot`'s state that record word w maps to (null: a ring word of a page without a ring)
 __device__ __forceinline__ uint4* plane_word(const Planes& P, const RecMap& m, long long slot, int w) {
-  if (w < m.w_ring) return P.headers + slot * kHeaderWords + w;
-  if (w < m.w_seq) return P.ring + slot * m.K + (w - m.w_ring);
+  if (w < m.w_ring) return P.pages + slot * P.page_words + w;
+  if (w < m.w_seq) return P.ring ? P.pages + slot * P.page_words + w : nullptr;  // header words, then ring words
   if (w < m.w_uext) return P.seq + slot * (m.S * 4) + (w - m.w_seq);
   return P.uext + slot * kUextWords + (w - m.w_uext);
 }
@@ -113,11 +114,11 @@ __device__ __forceinline__ bool owned(unsigned long long key, unsigned shard, un
 
 // features.hip find_or_insert over a strided key array
 
-__global__ void __launch_bounds__(256) snap_flag_kernel(const uint4* __restrict__ headers, long long lo, long long n,
-                                                        unsigned char* __restrict__ flags) {
+__global__ void __launch_bounds__(256) snap_flag_kernel(const uint4* __restrict__ pages, long long page_words,
+                                                        long long lo, long long n, unsigned char* __restrict__ flags) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint4 h = headers[(lo + i) * kHeaderWords];
+  const uint4 h = pages[(lo + i) * page_words];
   flags[i] = (h.x | h.y) != 0u;
 }
 
@@ -127,10 +128,11 @@ __global__ void __launch_bounds__(256) snap_gather_kernel(Planes P, RecMap m, co
   if (t >= n_words) return;
   const long long r = t / m.words;
   const int w = (int)(t - r * m.words);
-  out[t] = *plane_word(P, m, (long long)slots[r], w);
+  const uint4* src = plane_word(P, m, (long long)slots[r], w);
+  out[t] = src ? *src : make_uint4(0u, 0u, 0u, 0u);
 }
 
-__global__ void __launch_bounds__(256) restore_slot_kernel(unsigned long long* keys, CardHeader* headers, long long mask,
+__global__ void __launch_bounds__(256) restore_slot_kernel(unsigned long long* keys, CardPages pages, long long mask,
                                                            const uint4* __restrict__ recs, int words, long long n,
                                                            unsigned shard, unsigned G, long long* __restrict__ slots,
                                                            unsigned long long* restored, unsigned* err) {
@@ -140,7 +142,7 @@ __global__ void __launch_bounds__(256) restore_slot_kernel(unsigned long long* k
   const unsigned long long key = ((unsigned long long)h.y << 32) | h.x;
   long long s = -1;
   if (owned(key, shard, G)) {
-    s = card_slot(keys, headers, mask, key);
+    s = card_slot(keys, pages, mask, key);
     if (s < 0)
       atomicOr(err, 1u);
     else
@@ -157,12 +159,13 @@ __global__ void __launch_bounds__(256) restore_scatter_kernel(Planes P, RecMap m
   const int w = (int)(t - r * m.words);
   const long long s = slots[r];
   if (s < 0) return;
-  *plane_word(P, m, s, w) = recs[t];
+  uint4* dst = plane_word(P, m, s, w);
+  if (dst) *dst = recs[t];
 }
 
 // window events (windows.hip WinEvent: ts @0, cents @8, card key @16, slot @24): filter by owner, re-slot
 // through the card table, append to the log
-__global__ void __launch_bounds__(256) restore_events_kernel(unsigned long long* keys, CardHeader* headers, long long mask,
+__global__ void __launch_bounds__(256) restore_events_kernel(unsigned long long* keys, CardPages pages, long long mask,
                                                              const unsigned char* __restrict__ in, long long n,
                                                              unsigned shard, unsigned G, unsigned char* __restrict__ log,
                                                              unsigned long long* count, unsigned* err) {
@@ -171,7 +174,7 @@ __global__ void __launch_bounds__(256) restore_events_kernel(unsigned long long*
   const unsigned char* ev = in + i * kWinEventBytes;
   const unsigned long long key = *reinterpret_cast<const unsigned long long*>(ev + 16);
   if (!owned(key, shard, G)) return;
-  const long long s = card_slot(keys, headers, mask, key);
+  const long long s = card_slot(keys, pages, mask, key);
   if (s < 0) {
     atomicOr(err, 1u);
     return;
@@ -268,7 +271,7 @@ void verify_image(FILE* f, const SnapHeader& hd, size_t rec_bytes) {
 }
 
 Planes planes_of(CardStore& st) {
-  return Planes{st.headers.as<uint4>(), st.ring.as<uint4>(),
+  return Planes{st.pages.as<uint4>(), st.page_bytes / 16, st.mode == FD_WINDOW_SLIDING,
                 st.seq.ptr ? st.seq.as<uint4>() : nullptr, st.uext.ptr ? st.uext.as<uint4>() : nullptr};
 }
 
@@ -343,8 +346,8 @@ void state_snapshot(Engine& e, const char* path, int shard, int n_shards, int64_
   int64_t n_cards = 0;
   for (int64_t lo = 0; lo < st.cap; lo += chunk) {
     const int64_t n = std::min<int64_t>(chunk, st.cap - lo);
-    hipLaunchKernelGGL(snap_flag_kernel, dim3(blocks(n)), dim3(256), 0, e.stream, st.headers.as<const uint4>(),
-                       (long long)lo, (long long)n, flags.as<unsigned char>());
+    hipLaunchKernelGGL(snap_flag_kernel, dim3(blocks(n)), dim3(256), 0, e.stream, st.pages.as<const uint4>(),
+                       st.page_bytes / 16, (long long)lo, (long long)n, flags.as<unsigned char>());
     FD_HIP(hipGetLastError());
     FD_HIP(rocprim::select(tmpbuf.ptr, tb, rocprim::counting_iterator<unsigned>((unsigned)lo),
                            flags.as<unsigned char>(), sel.as<unsigned>(), nsel.as<unsigned>(), (size_t)n, e.stream));
@@ -463,7 +466,7 @@ void state_restore(Engine& e, const char* path, int shard, int n_shards, int fla
     read_all(in.f, pin.p, (size_t)n * rec_bytes, &h_cards);
     FD_HIP(hipMemcpyAsync(recs.ptr, pin.p, (size_t)n * rec_bytes, hipMemcpyHostToDevice, e.stream));
     hipLaunchKernelGGL(restore_slot_kernel, dim3(blocks(n)), dim3(256), 0, e.stream,
-                       st.keys.as<unsigned long long>(), st.headers.as<CardHeader>(), (long long)(st.cap - 1),
+                       st.keys.as<unsigned long long>(), st.view(), (long long)(st.cap - 1),
                        recs.as<const uint4>(), m.words, (long long)n, (unsigned)shard, (unsigned)n_shards,
                        slots.as<long long>(), d_restored, d_err);
     FD_HIP(hipGetLastError());
@@ -531,7 +534,7 @@ void state_restore(Engine& e, const char* path, int shard, int n_shards, int fla
         read_all(in.f, pin.p, (size_t)n * kWinEventBytes, &hh);
         FD_HIP(hipMemcpyAsync(recs.ptr, pin.p, (size_t)n * kWinEventBytes, hipMemcpyHostToDevice, e.stream));
         hipLaunchKernelGGL(restore_events_kernel, dim3(blocks(n)), dim3(256), 0, e.stream,
-                           st.keys.as<unsigned long long>(), st.headers.as<CardHeader>(), (long long)(st.cap - 1),
+                           st.keys.as<unsigned long long>(), st.view(), (long long)(st.cap - 1),
                            recs.as<const unsigned char>(), (long long)n, (unsigned)shard, (unsigned)n_shards,
                            log.as<unsigned char>(), d_count, d_err);
         FD_HIP(hipGetLastError());

@@ -62,7 +62,7 @@ __device__ __forceinline__ long long floor_div(long long a, long long b) {
   return q;
 }
 
-__global__ void __launch_bounds__(256) win_append_kernel(unsigned long long* card_keys, CardHeader* headers,
+__global__ void __launch_bounds__(256) win_append_kernel(unsigned long long* card_keys, CardPages pages,
                                                          long long mask, int64_t n, const unsigned long long* key,
                                                          const long long* ts, const long long* cents,
                                                          const int* merchant, const unsigned char* pm,
@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(256) win_append_kernel(unsigned long long* car
                                                          unsigned long long* min_ts, unsigned* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const long long s = card_slot(card_keys, headers, mask, key[i]);
+  const long long s = card_slot(card_keys, pages, mask, key[i]);
   if (s < 0) {
     atomicOr(err, 1u);
     return;
@@ -416,7 +416,7 @@ void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, 
     WinEvent* ul = w.ulog[w.ucur].as<WinEvent>() + w.ucount;
     WinEvent* ml = w.mlog[w.mcur].as<WinEvent>() + w.mcount;
     hipLaunchKernelGGL(win_append_kernel, dim3(g256(n)), dim3(256), 0, e.stream,
-                       st.keys.as<unsigned long long>(), st.headers.as<CardHeader>(), (long long)(st.cap - 1), n,
+                       st.keys.as<unsigned long long>(), st.view(), (long long)(st.cap - 1), n,
                        reinterpret_cast<const unsigned long long*>(t.card_key),
                        reinterpret_cast<const long long*>(t.ts_ms), reinterpret_cast<const long long*>(t.amount_cents),
                        reinterpret_cast<const int*>(t.merchant), in.payment_method, in.is_fraud, in.fraud_score, ul,
