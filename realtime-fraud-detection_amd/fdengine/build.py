@@ -22,7 +22,26 @@ ORACLE_DIR = REPO_ROOT / "oracle"
 HIP_SOURCES = ["engine.hip", "forest.hip", "ensemble.hip", "blend.hip", "features.hip", "route.hip", "lstm.hip",
                "windows.hip", "snapshot.hip", "ingest.hip", "sink.hip", "model_io.hip", "comm.hip"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wno-unused-result"]
+               "-Wno-unused-result", "-Rpass-analysis=kernel-resource-usage"]
+RESOURCES = LIB_DIR / "kernel_resources.json"  # per kernel: VGPRs, AGPRs, scratch, occupancy (the compiler's remarks)
+
+
+def parse_resource_remarks(text: str) -> dict:
+    """hipcc's kernel-resource-usage remarks -> {mangled kernel name: {"vgpr", "agpr", "sgpr", "scratch", "occupancy",
+    "lds"}} (tests/test_kernel_budget.py holds the hot kernels to their register budgets)."""
+    import re
+    out, cur = {}, None
+    keys = {"VGPRs": "vgpr", "AGPRs": "agpr", "TotalSGPRs": "sgpr", "ScratchSize [bytes/lane]": "scratch",
+            "Occupancy [waves/SIMD]": "occupancy", "LDS Size [bytes/block]": "lds"}
+    for line in text.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([A-Za-z][A-Za-z /\[\]]*?): (\d+) \[-Rpass-analysis", line)
+        if m and cur is not None and m.group(1) in keys:
+            cur[keys[m.group(1)]] = int(m.group(2))
+    return out
 
 
 def _hipcc() -> str:
@@ -83,6 +102,8 @@ def build_engine(force: bool = False, verbose: bool = True, profile: bool = Fals
             if r.returncode != 0:
                 raise RuntimeError(f"hipcc failed on {src.name}:\n{r.stderr[-6000:]}")
             tmp.replace(o)
+            import json
+            o.with_suffix(".res.json").write_text(json.dumps(parse_resource_remarks(r.stderr), indent=0))
             stamp.write_text(dig)
         return o
 
@@ -101,6 +122,14 @@ def build_engine(force: bool = False, verbose: bool = True, profile: bool = Fals
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     tmp.replace(out)
+    if not profile:
+        import json
+        res = {}
+        for o in objs:
+            rj = o.with_suffix(".res.json")
+            if rj.exists():
+                res.update(json.loads(rj.read_text()))
+        RESOURCES.write_text(json.dumps(res, indent=0, sort_keys=True))
     return out
 
 
