@@ -513,7 +513,8 @@ class Config3:
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         # after the parity batches (which need the vectors): the pipelined stream, outputs alternating two sets
-        self.pipe, self.parity_done, self.cur = self.pipelined_default and not args.no_pipeline, False, 0
+        self.pipe, self.parity_done, self.cur = ((self.pipelined_default or args.pipeline) and not args.no_pipeline,
+                                                 False, 0)
         self.outs = [[self.fp, self.conf, self.dec, self.risk],
                      [torch.empty_like(t) for t in (self.fp, self.conf, self.dec, self.risk)]]
         self.scorer = eng.pipelined_scorer(self.params, self.slots)
@@ -1298,6 +1299,9 @@ def make_parser():
                          "transactions whose 24 h window held all K)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="config5: the pipelined stream (batch i+1's features beside batch i's scoring) instead of "
+                         "fd_score_batch_device per step")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="config3/4 at N=1: fd_score_batch_device per step instead of the pipelined stream")
     ap.add_argument("--small-streams", type=int, choices=[0, 1, 2], default=None,

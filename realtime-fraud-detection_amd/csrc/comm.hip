@@ -177,30 +177,51 @@ void comm_destroy(Engine& e) {
 
 // On the forward stream: the per-owner counts of `t` (send[p] to peer p, recv[p] from it: one int64 each way per
 // peer), published to the slot's host buffer (count_publish_kernel), then the records' places (scan + scatter into
-// rec[s]; the host's wait for the counts does not include them)
-void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int s, HostLaps& L) {
+// rec[s]; the host's wait for the counts does not include them). Three parts, so the count exchange can also ride
+// in the records exchange's group (comm_forward_group): the count kernel, the exchange's sends / receives (inside a
+// group the caller opened), the publish + places.
+namespace {
+void counts_pre(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int s) {
+  ShardComm& c = e.comm;
+  hipStream_t st = c.x_fwd;
+  if (ready) FD_HIP(hipStreamWaitEvent(st, ready, 0));
+  launch_route_count(t, n, c.world, c.cnt[s].as<int64_t>(), st, c.route_blk);  // send half zero (comm_init)
+}
+
+void counts_ops(Engine& e, int s) {
   ShardComm& c = e.comm;
   const RcclApi& R = api(c);
   const int G = c.world;
-  hipStream_t st = c.x_fwd;
-  if (ready) FD_HIP(hipStreamWaitEvent(st, ready, 0));
-  int64_t* cnt = c.cnt[s].as<int64_t>();  // send half zero (comm_init, then every publish)
-  launch_route_count(t, n, G, cnt, st, c.route_blk);
-  L(1);
+  int64_t* cnt = c.cnt[s].as<int64_t>();
   const ncclComm_t f = static_cast<ncclComm_t>(c.fwd);
-  check(R, R.group_start(), "ncclGroupStart");
   for (int p = 0; p < G; ++p) {
-    check(R, R.send(cnt + p, 1, ncclInt64, p, f, st), "ncclSend (counts)");
-    check(R, R.recv(cnt + G + p, 1, ncclInt64, p, f, st), "ncclRecv (counts)");
+    check(R, R.send(cnt + p, 1, ncclInt64, p, f, c.x_fwd), "ncclSend (counts)");
+    check(R, R.recv(cnt + G + p, 1, ncclInt64, p, f, c.x_fwd), "ncclRecv (counts)");
   }
-  check(R, R.group_end(), "ncclGroupEnd (counts)");
-  L(2);
+}
+
+void counts_post(Engine& e, const fd_txn_batch& t, int64_t n, int s) {
+  ShardComm& c = e.comm;
+  hipStream_t st = c.x_fwd;
   const unsigned long long seq = ++c.cnt_seq[s];
   auto* dseq = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(c.d_hcnt[s]) + kCntSeqOff);
-  hipLaunchKernelGGL(count_publish_kernel, dim3(1), dim3(128), 0, st, cnt, G, c.d_hcnt[s], dseq, seq);
+  hipLaunchKernelGGL(count_publish_kernel, dim3(1), dim3(128), 0, st, c.cnt[s].as<int64_t>(), c.world, c.d_hcnt[s],
+                     dseq, seq);
   FD_HIP(hipGetLastError());
   c.rec[s].ensure_headroom((size_t)std::max<int64_t>(n, 1) * sizeof(RouteRecord));
-  launch_route_place(t, n, G, c.rec[s].ptr, st, c.route_blk);
+  launch_route_place(t, n, c.world, c.rec[s].ptr, st, c.route_blk);
+}
+}  // namespace
+
+void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int s, HostLaps& L) {
+  const RcclApi& R = api(e.comm);
+  counts_pre(e, t, n, ready, s);
+  L(1);
+  check(R, R.group_start(), "ncclGroupStart");
+  counts_ops(e, s);
+  check(R, R.group_end(), "ncclGroupEnd (counts)");
+  L(2);
+  counts_post(e, t, n, s);
   L(3);
 }
 
@@ -249,43 +270,62 @@ void comm_wait_counts(Engine& e, int s, int64_t n, HostLaps& L) {
   L(0);
 }
 
+void exchange_ops(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,
+                  const int64_t* recv, size_t elem);
+
 // slot s's records to their owners on the forward stream, into the next inbox of the ring (after the scoring
-// that last read it)
-void comm_send_records(Engine& e, int s, HostLaps& L) {
+// that last read it); with `next`, the next batch's count exchange in the same group (one RCCL launch for both:
+// per peer pair the records' send / receive precede the counts' on every rank), then its publish + places
+void comm_forward_group(Engine& e, int s, const fd_txn_batch* next, int64_t next_n, hipEvent_t next_ready, int ns,
+                        HostLaps& L) {
   ShardComm& c = e.comm;
+  const RcclApi& R = api(c);
   const int G = c.world;
   const int64_t* send = c.split[s];
   const int64_t* recv = c.split[s] + G;
   int64_t m = 0;
   for (int p = 0; p < G; ++p) m += recv[p];
+  if (next) counts_pre(e, *next, next_n, next_ready, ns);
+  L(1);
   const int q = c.inbox_next;
   c.inbox_next = (q + 1) % ShardComm::kInbox;
   c.inbox_of[s] = q;
   if (c.inbox_live[q]) FD_HIP(hipStreamWaitEvent(c.x_fwd, c.inbox_ev[q], 0));
   c.inbox[q].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(RouteRecord));
   c.res[s].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(ResultRecord));
-  comm_exchange(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[q].ptr, recv, sizeof(RouteRecord));
+  check(R, R.group_start(), "ncclGroupStart");
+  exchange_ops(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[q].ptr, recv, sizeof(RouteRecord));
+  if (next) counts_ops(e, ns);
+  check(R, R.group_end(), "ncclGroupEnd (records + counts)");
   FD_HIP(hipEventRecord(c.in_ev[q], c.x_fwd));
   L(4);
+  if (next) counts_post(e, *next, next_n, ns);
+  L(3);
 }
 
 // uneven all-to-all of `elem`-byte items: send[p] items (consecutive in sendbuf, peers in rank order) to peer p,
 // recv[p] items from peer p into recvbuf (peers in rank order) — the concatenation order the unsharded order needs
-void comm_exchange(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,
-                   const int64_t* recv, size_t elem) {
+void exchange_ops(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,
+                  const int64_t* recv, size_t elem) {
   ShardComm& c = e.comm;
   const RcclApi& R = api(c);
   const ncclComm_t k = static_cast<ncclComm_t>(back ? c.back : c.fwd);
   const char* sb = static_cast<const char*>(sendbuf);
   char* rb = static_cast<char*>(recvbuf);
   size_t os = 0, orr = 0;
-  check(R, R.group_start(), "ncclGroupStart");
   for (int p = 0; p < c.world; ++p) {
     if (send[p] > 0) check(R, R.send(sb + os * elem, (size_t)send[p] * elem, ncclUint8, p, k, st), "ncclSend");
     if (recv[p] > 0) check(R, R.recv(rb + orr * elem, (size_t)recv[p] * elem, ncclUint8, p, k, st), "ncclRecv");
     os += (size_t)send[p];
     orr += (size_t)recv[p];
   }
+}
+
+void comm_exchange(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,
+                   const int64_t* recv, size_t elem) {
+  const RcclApi& R = api(e.comm);
+  check(R, R.group_start(), "ncclGroupStart");
+  exchange_ops(e, back, st, sendbuf, send, recvbuf, recv, elem);
   check(R, R.group_end(), "ncclGroupEnd");
 }
 

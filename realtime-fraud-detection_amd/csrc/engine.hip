@@ -1153,8 +1153,8 @@ int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t
   fd::HostLaps L{c};
   c.steps.fetch_add(1, std::memory_order_relaxed);
   // Every communicator operation below is issued by this thread in one fixed order on every rank:
-  //   [counts of this batch, when not prefetched] -> counts of `next` -> records of this batch (x_fwd, fwd comm)
-  //   -> results of this batch (engine stream, back comm)
+  //   [counts of this batch, when not prefetched] -> {records of this batch + counts of `next`: one group}
+  //   (x_fwd, fwd comm) -> results of this batch (engine stream, back comm)
   // 1. this batch's split sizes: exchanged by the previous call (prefetch) or now
   int s;
   if (use_pending) {
@@ -1172,20 +1172,20 @@ int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t
     for (int p = 0; p < 2 * G; ++p) split_sizes[p] = c.split[s][p];
   int64_t m = 0;
   for (int p = 0; p < G; ++p) m += recv[p];
-  // 2. the next batch's partition + counts, on the forward stream ahead of this batch's records (whose exchange may
-  // wait for an inbox slot): the counts land while this batch is scored, and the next call's wait is satisfied
+  // 2. this batch's records to their owners and the next batch's counts, one group on the forward stream (after the
+  // owner's previous use of the inbox slot): the counts land while this batch is scored, and the next call's wait
+  // is satisfied
+  int ns = -1;
   if (next) {
-    const int ns = c.next_slot;
+    ns = c.next_slot;
     c.next_slot ^= 1;
-    fd::comm_launch_counts(e, *next, next_n, static_cast<hipEvent_t>(next_ready), ns, L);
     c.pending = true;
     c.pending_id = next_id;
     c.pending_n = next_n;
     c.pending_slot = ns;
   }
-  // 3. records to their owners (forward stream), after the owner's previous use of this inbox slot
-  fd::comm_send_records(e, s, L);
-  // 4. the owner's features + scoring on the pipeline (features wait for the records), results on the engine stream
+  fd::comm_forward_group(e, s, next, next_n, static_cast<hipEvent_t>(next_ready), ns, L);
+  // 3. the owner's features + scoring on the pipeline (features wait for the records), results on the engine stream
   const int q = c.inbox_of[s];
   if (m)
     pipe_step(e, params, slots, nullptr, present, nullptr, c.inbox[q].ptr, m, nullptr, nullptr, nullptr, nullptr,
@@ -1193,7 +1193,7 @@ int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t
   FD_HIP(hipEventRecord(c.inbox_ev[q], e.stream));  // the engine stream has passed this batch's scoring
   c.inbox_live[q] = true;
   L(5);
-  // 5. results back (reversed splits) and into arrival order, on the engine stream
+  // 4. results back (reversed splits) and into arrival order, on the engine stream
   c.back_buf.ensure_headroom((size_t)std::max<int64_t>(n, 1) * sizeof(fd::ResultRecord));
   fd::comm_exchange(e, true, e.stream, c.res[s].ptr, recv, c.back_buf.ptr, send, sizeof(fd::ResultRecord));
   L(6);

@@ -588,7 +588,9 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
 void comm_destroy(Engine& e);
 void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot, HostLaps& L);
 void comm_wait_counts(Engine& e, int slot, int64_t n, HostLaps& L);  // host wait; split[slot] checked
-void comm_send_records(Engine& e, int slot, HostLaps& L);            // records exchange behind the inbox slot
+// records exchange of `slot` behind its inbox slot, + the next batch's count exchange in the same group
+void comm_forward_group(Engine& e, int slot, const fd_txn_batch* next, int64_t next_n, hipEvent_t next_ready,
+                        int next_slot, HostLaps& L);
 void comm_exchange(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,
                    const int64_t* recv, size_t elem);
 // lstm.hip
