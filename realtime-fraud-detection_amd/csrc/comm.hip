@@ -75,23 +75,6 @@ void check(const RcclApi& R, ncclResult_t r, const char* what) {
 
 constexpr size_t kCntSeqOff = 2 * FD_MAX_SHARDS * sizeof(int64_t);  // the sequence word after the counts
 constexpr size_t kCntBytes = kCntSeqOff + 64;
-
-// the exchanged counts (send [G], receive [G]) into the slot's coherent host buffer, then its sequence word: one
-// lane per count, each store made visible system-wide before the workgroup barrier, the sequence stored last (the
-// host polls it instead of an event: a D2H copy + event wait measured ~70 us from the exchange to the host)
-// The send half is zeroed behind it for the slot's next route_count (which adds its totals into it).
-__global__ void __launch_bounds__(128)
-count_publish_kernel(int64_t* __restrict__ cnt, int G, int64_t* h, unsigned long long* h_seq,
-                     unsigned long long seq) {
-  const int i = (int)threadIdx.x;
-  if (i < 2 * G) {
-    __hip_atomic_store(h + i, cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __threadfence_system();
-    if (i < G) cnt[i] = 0;
-  }
-  __syncthreads();
-  if (i == 0) __hip_atomic_store(h_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 }  // namespace
 
 void comm_unique_id(const char* rccl_path, uint8_t* out) {
@@ -176,8 +159,10 @@ void comm_destroy(Engine& e) {
 }
 
 // On the forward stream: the per-owner counts of `t` (send[p] to peer p, recv[p] from it: one int64 each way per
-// peer), published to the slot's host buffer (count_publish_kernel), then the records' places (scan + scatter into
-// rec[s]; the host's wait for the counts does not include them). Three parts, so the count exchange can also ride
+// peer), published to the slot's coherent host buffer by the first thing the places' scan kernel does (one lane per
+// count, each store visible system-wide before the barrier, the sequence word last: the host polls it instead of an
+// event — a D2H copy + event wait measured ~70 us from the exchange to the host), then the records' places (scan +
+// scatter into rec[s]). Three parts, so the count exchange can also ride
 // in the records exchange's group (comm_forward_group): the count kernel, the exchange's sends / receives (inside a
 // group the caller opened), the publish + places.
 namespace {
@@ -205,11 +190,9 @@ void counts_post(Engine& e, const fd_txn_batch& t, int64_t n, int s) {
   hipStream_t st = c.x_fwd;
   const unsigned long long seq = ++c.cnt_seq[s];
   auto* dseq = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(c.d_hcnt[s]) + kCntSeqOff);
-  hipLaunchKernelGGL(count_publish_kernel, dim3(1), dim3(128), 0, st, c.cnt[s].as<int64_t>(), c.world, c.d_hcnt[s],
-                     dseq, seq);
-  FD_HIP(hipGetLastError());
   c.rec[s].ensure_headroom((size_t)std::max<int64_t>(n, 1) * sizeof(RouteRecord));
-  launch_route_place(t, n, c.world, c.rec[s].ptr, st, c.route_blk);
+  const CountPublish pub{c.cnt[s].as<int64_t>(), c.world, c.d_hcnt[s], dseq, seq};
+  launch_route_place(t, n, c.world, c.rec[s].ptr, st, c.route_blk, &pub);  // its scan kernel publishes first
 }
 }  // namespace
 

@@ -574,7 +574,17 @@ void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_in
 // the sharded step's split form of the partition: block counts + per-shard totals added into `totals` (zero on
 // entry) first, so the count exchange can start; then the scan + record scatter (blk: the same scratch)
 void launch_route_count(const fd_txn_batch& t, int64_t n, int G, int64_t* totals, hipStream_t st, DeviceBuffer& blk);
-void launch_route_place(const fd_txn_batch& t, int64_t n, int G, void* d_records, hipStream_t st, DeviceBuffer& blk);
+// the sharded step's split sizes to the host (comm.hip): cnt[0, 2G) -> host-mapped h, the send half zeroed for the
+// next count, then the sequence word h_seq = seq (release); run by the scan kernel of launch_route_place
+struct CountPublish {
+  int64_t* cnt;
+  int G;
+  int64_t* h;
+  unsigned long long* h_seq;
+  unsigned long long seq;
+};
+void launch_route_place(const fd_txn_batch& t, int64_t n, int G, void* d_records, hipStream_t st, DeviceBuffer& blk,
+                        const CountPublish* pub = nullptr);
 void launch_route_unpack(Engine& e, const void* d_records, const void* d_results, int64_t n, const fd_txn_batch& out,
                          uint8_t* pm, uint8_t* fraud, double* score);
 void launch_result_pack(Engine& e, const double* fp, const double* conf, const uint8_t* dec, const uint8_t* risk,

@@ -72,9 +72,18 @@ __global__ void __launch_bounds__(kRouteBlock) route_count_kernel(const unsigned
 
 // exclusive scan of the shard-major block counts: each of the 1024 threads scans a contiguous segment
 __global__ void __launch_bounds__(1024) route_scan_kernel(int* __restrict__ blk, int64_t total, unsigned G,
-                                                          int nblk, long long* __restrict__ counts) {
+                                                          int nblk, long long* __restrict__ counts, CountPublish pub) {
   __shared__ long long part[1024];
   const int t = threadIdx.x;
+  if (pub.cnt) {  // the sharded step's split sizes first (the host is waiting for them), then the scan
+    if (t < 2 * pub.G) {
+      __hip_atomic_store(pub.h + t, pub.cnt[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+      if (t < pub.G) pub.cnt[t] = 0;
+    }
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(pub.h_seq, pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   const int64_t seg = (total + 1023) / 1024;
   const int64_t a = t * seg, b = (a + seg < total) ? a + seg : total;
   long long s = 0;
@@ -233,7 +242,7 @@ void launch_route_partition(Engine& e, const fd_txn_batch& t, const fd_window_in
                      blk.as<int>(), nullptr);
   FD_HIP(hipGetLastError());
   hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, st, blk.as<int>(),
-                     (int64_t)G * nblk, (unsigned)G, nblk, reinterpret_cast<long long*>(d_counts));
+                     (int64_t)G * nblk, (unsigned)G, nblk, reinterpret_cast<long long*>(d_counts), CountPublish{});
   FD_HIP(hipGetLastError());
   hipLaunchKernelGGL(route_scatter_kernel, dim3(nblk), dim3(kRouteBlock), 0, st, key,
                      reinterpret_cast<const long long*>(t.ts_ms), reinterpret_cast<const long long*>(t.amount_cents),
@@ -259,8 +268,16 @@ void launch_route_count(const fd_txn_batch& t, int64_t n, int G, int64_t* totals
   FD_HIP(hipGetLastError());
 }
 
-void launch_route_place(const fd_txn_batch& t, int64_t n, int G, void* d_records, hipStream_t st, DeviceBuffer& blk) {
-  if (n == 0) return;
+void launch_route_place(const fd_txn_batch& t, int64_t n, int G, void* d_records, hipStream_t st, DeviceBuffer& blk,
+                        const CountPublish* pub) {
+  const CountPublish P = pub ? *pub : CountPublish{};
+  if (n == 0) {  // nothing to place; the publish alone
+    if (pub) {
+      hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, st, nullptr, (int64_t)0, (unsigned)G, 0, nullptr, P);
+      FD_HIP(hipGetLastError());
+    }
+    return;
+  }
   FD_REQUIRE(d_records != nullptr, FD_ERR_INVALID_ARG, "null records");
   FD_REQUIRE(t.card_key && t.ts_ms && t.amount_cents && t.merchant && t.device_fp && t.ip_class && t.hour &&
                  t.weekend,
@@ -268,7 +285,7 @@ void launch_route_place(const fd_txn_batch& t, int64_t n, int G, void* d_records
   const int nblk = (int)((n + kRouteBlock - 1) / kRouteBlock);
   FD_REQUIRE(blk.bytes >= (size_t)G * nblk * sizeof(int), FD_ERR_INVALID_ARG, "route_place before route_count");
   hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, st, blk.as<int>(), (int64_t)G * nblk, (unsigned)G,
-                     nblk, nullptr);
+                     nblk, nullptr, P);
   FD_HIP(hipGetLastError());
   hipLaunchKernelGGL(route_scatter_kernel, dim3(nblk), dim3(kRouteBlock), 0, st,
                      reinterpret_cast<const unsigned long long*>(t.card_key),
