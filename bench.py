@@ -1145,7 +1145,20 @@ class Config3J(Config3):
         eng.state_init(cap, self.mode, self.K)
         eng.load_users(self.ukeys, self.uavg, self.uage, self.ufp)
         eng.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
-        self.codec = IngestCodec(eng, self.merchant_ids, synth.SIM_PAYMENT_METHODS, synth.SIM_TXN_TYPES,
+        # pipelined (default): the codec runs on an engine of its own with its own stream, so batch i+1's parse
+        # overlaps batch i's scoring on the pipelined stream; two column sets, handed over by events (the scoring
+        # waits for its parse; a set's next parse waits for the scoring that read it)
+        self.pipe, self.parity_done, self.cur = not args.no_pipeline, False, 0
+        self.extra_engines = []
+        codec_eng = eng
+        if self.pipe:
+            import fdengine
+            self.ceng = fdengine.FraudEngine(dev.index)
+            self.cstream = torch.cuda.Stream(device=dev)
+            self.ceng.set_stream(self.cstream.cuda_stream)
+            self.extra_engines = [self.ceng]
+            codec_eng = self.ceng
+        self.codec = IngestCodec(codec_eng, self.merchant_ids, synth.SIM_PAYMENT_METHODS, synth.SIM_TXN_TYPES,
                                  synth.SIM_CARD_TYPES)
         self.pool = max(1, min(args.pool, 4))
         self.msgs, bufs, offs = [], [], []
@@ -1157,7 +1170,11 @@ class Config3J(Config3):
             bufs.append(torch.from_numpy(b.copy()).to(dev))
             offs.append(torch.from_numpy(o).to(dev))
         self.bufs, self.offs = bufs, offs
-        self.cols, self.cptrs = device_columns(self.B, dev.index)
+        self.csets = [device_columns(self.B, dev.index) for _ in range(2 if self.pipe else 1)]
+        self.cols, self.cptrs = self.csets[0]
+        self.ready = [torch.cuda.Event() for _ in range(2)]
+        self.freed, self.freed_live = [torch.cuda.Event() for _ in range(2)], [False, False]
+        self.dev_stream = torch.cuda.current_stream(dev)
         B = self.B
         self.fp = torch.empty(B, dtype=torch.float64, device=dev)
         self.conf = torch.empty(B, dtype=torch.float64, device=dev)
@@ -1168,18 +1185,39 @@ class Config3J(Config3):
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
-        self.outs, self.cur = [[self.fp, self.conf, self.dec, self.risk]], 0  # Config3.fetch (serial steps here)
+        self.outs = [[self.fp, self.conf, self.dec, self.risk],
+                     [torch.empty_like(t) for t in (self.fp, self.conf, self.dec, self.risk)]]  # Config3.fetch
+        self.scorer = eng.pipelined_scorer(self.params, self.slots)
         self.nbytes = [int(o[-1].item()) for o in offs]
         log(f"[rank {rank}] config3j setup {time.time() - t:.1f}s: {self.cards} cards, capacity {cap}, "
             f"{self.pool} JSON batches resident ({self.nbytes[0] / B:.0f} B/message)")
 
     def step(self, i):
         s = i % self.pool
-        self.codec.parse_device(self.bufs[s].data_ptr(), self.offs[s].data_ptr(), self.B, self.cptrs)
-        txn = {f: self.cptrs[f] for f in self.N.TXN_FIELDS}
-        self.eng.score_batch_device(self.params, self.slots, txn, self.B, self.fp.data_ptr(),
-                                    self.conf.data_ptr(), self.dec.data_ptr(), self.risk.data_ptr(),
-                                    vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
+        if not (self.pipe and self.parity_done):  # one stream, vectors kept (the parity batch reads them)
+            if self.pipe:
+                self.cstream.wait_stream(self.dev_stream)
+            self.codec.parse_device(self.bufs[s].data_ptr(), self.offs[s].data_ptr(), self.B, self.cptrs)
+            if self.pipe:
+                self.dev_stream.wait_stream(self.cstream)
+            txn = {f: self.cptrs[f] for f in self.N.TXN_FIELDS}
+            self.cur = 0
+            self.eng.score_batch_device(self.params, self.slots, txn, self.B, self.fp.data_ptr(),
+                                        self.conf.data_ptr(), self.dec.data_ptr(), self.risk.data_ptr(),
+                                        vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
+            return
+        k = i & 1
+        _, cptrs = self.csets[k]
+        if self.freed_live[k]:
+            self.cstream.wait_event(self.freed[k])
+        self.codec.parse_device(self.bufs[s].data_ptr(), self.offs[s].data_ptr(), self.B, cptrs)
+        self.ready[k].record(self.cstream)
+        self.cur = k
+        fp, conf, dec, risk = self.outs[k]
+        self.scorer({f: cptrs[f] for f in self.N.TXN_FIELDS}, self.B, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(),
+                    risk.data_ptr(), input_ready=self.ready[k].cuda_event)
+        self.freed[k].record(self.dev_stream)  # the engine stream: past this batch's scoring (its output copy)
+        self.freed_live[k] = True
 
     def parity(self):
         """Batch 0 (fresh state): oracle ingest -> oracle features -> forests -> blend, first 8192 rows."""
@@ -1203,6 +1241,7 @@ class Config3J(Config3):
         px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
         pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
         fp, _, dec, _ = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults)
+        self.parity_done = True
         return {"rows_checked": k, "vector_mismatched_elements": int((V != rvec).sum()),
                 "max_abs_prob_diff": float(np.abs(self.fp[:k].cpu().numpy() - fp).max()),
                 "decision_mismatches": int((self.dec[:k].cpu().numpy() != dec).sum())}
@@ -1237,6 +1276,20 @@ class Config3J(Config3):
 
 WORKLOADS = {"config2": Config2, "config3": Config3, "config4": Config4, "config5": Config5, "ingest": Ingest,
              "config3j": Config3J}
+
+
+def _engines(eng, wl):
+    """the scoring engine and any engine the workload runs beside it (config 3j's codec engine)"""
+    return [eng] + list(getattr(wl, "extra_engines", []))
+
+
+def _read_timing(eng, wl):
+    out = {}
+    for e in _engines(eng, wl):
+        for k, (ms, c) in e.read_timing().items():
+            a, b = out.get(k, (0.0, 0))
+            out[k] = (a + ms, b + c)
+    return out
 
 
 def _saturated(eng, wl):
@@ -1397,11 +1450,12 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    eng.read_timing()
+    _read_timing(eng, wl)
     # kernel durations: HIP events on the launch stream, on one launch in TIMING_EVERY of each kernel (an event
     # record costs stream time; timing every launch would charge ~10 us per step of instrumentation to `value`)
-    eng.set_option("timing_every", TIMING_EVERY)
-    eng.set_timing(True)
+    for e in _engines(eng, wl):
+        e.set_option("timing_every", TIMING_EVERY)
+        e.set_timing(True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -1423,8 +1477,9 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    eng.set_timing(False)
-    timing = eng.read_timing()
+    for e in _engines(eng, wl):
+        e.set_timing(False)
+    timing = _read_timing(eng, wl)
     elapsed = t1 - t0
     saturation = None
     if sat0 is not None:
@@ -1527,13 +1582,15 @@ def main():
     # feature kernels share the CUs with the forests): each kernel's unshared duration
     timing_alone = None
     if args.alone_iters > 0:
-        eng.set_option("timing_every", 1)
-        eng.set_timing(True)
+        for e in _engines(eng, wl):
+            e.set_option("timing_every", 1)
+            e.set_timing(True)
         for i in range(args.alone_iters):
             wl.step(i)
-            stream.synchronize()
-        eng.set_timing(False)
-        timing_alone = eng.read_timing()
+            torch.cuda.synchronize()
+        for e in _engines(eng, wl):
+            e.set_timing(False)
+        timing_alone = _read_timing(eng, wl)
 
     value = world * args.steps * args.batch / elapsed
     cpu = None

@@ -9,7 +9,7 @@
 // (fl/features/FeatureExtractor.java:300-325 device / IP / user agent, :434-451 isPrivateIP /
 // analyzeSuspiciousUserAgent, :366-381 payment / type / card). Declared semantics: DESIGN.md "Ingest".
 //
-// One wavefront per message, four per workgroup:
+// One wavefront per message (two messages per wave in the member phase), two waves per workgroup:
 //   stage      : 16-B coalesced loads of the message into LDS (<= 4 KiB; longer -> FD_INGEST_TOO_LONG)
 //   structure  : lane i owns bytes [64i, 64i+64): unescaped-quote parity -> wave prefix XOR (ballot) gives
 //                the in-string state at every segment start; bracket depth deltas -> wave prefix sum; the
@@ -29,7 +29,9 @@
 namespace fd {
 namespace {
 
-constexpr int kWaves = 4;
+// two waves per workgroup (4 messages, ~19 KB of LDS): a workgroup fits beside the fused ensemble kernel's
+// compact-layout workgroup (132 KB) on one CU, so a codec running on its own stream overlaps the scoring (config 3j)
+constexpr int kWaves = 2;
 constexpr int kSlots = 2 * kWaves;  // messages per workgroup
 constexpr int kMaxMsg = 4080;      // bytes per message: 64 lanes x 64-byte segments minus the 16-B alignment shift
 constexpr int kMaxMembers = 64;    // top-level members per message (one per lane; more -> malformed)
@@ -552,7 +554,7 @@ struct Val {
 
 // 4 waves per SIMD (128 VGPRs, no spills to memory): the members phase is latency-bound per lane, so occupancy
 // is the lever (142 VGPRs gave 3 waves per SIMD)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) ingest_json_kernel(const unsigned char* __restrict__ buf,
+__global__ void __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4))) ingest_json_kernel(const unsigned char* __restrict__ buf,
                                                           const int64_t* __restrict__ offsets, int64_t n, Tables T,
                                                           fd_ingest_out out, int stop_after) {
   __shared__ __attribute__((aligned(16))) unsigned char stage[kSlots][kStage + 16];  // + the word reads' tail
@@ -611,44 +613,70 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
     const int seg_words = max(1, (shift + L + 255) / 256);
     const unsigned* seg = reinterpret_cast<const unsigned*>(&stage[ms][lane * 4 * seg_words]);
     const int q0 = lane * 4 * seg_words - shift;
-    // pass 1: trailing backslash run (escape carry into the next lane), first / last non-whitespace byte, quote
-    // parity assuming an even carry, and the byte after the segment's leading backslash run
-    int run = 0, nvalid = 0, first_nw = L, last_nw = -1, par = 0, lead = 0, after_lead = -1;
-    bool leading = true;
+    // pass 1, the only per-byte pass: the segment's bytes classified into bit masks (bit k = segment byte k; only
+    // bytes of the message): quotes, backslashes, opening / closing brackets, colons, commas, non-whitespace
+    // message bytes of the segment: k in [klo, khi)
+    const int klo = max(0, -q0), khi = min(4 * seg_words, L - q0);
+    const unsigned long long vm =
+        khi > klo ? ((khi - klo == 64 ? ~0ull : ((1ull << (khi - klo)) - 1ull)) << klo) : 0ull;
+    unsigned long long qm = 0, bm = 0, om = 0, cm = 0, km = 0, mm = 0;
+    int first_nw = L, last_nw = -1;
   #pragma unroll 2
     for (int j = 0; j < seg_words; ++j) {
       const unsigned w = seg[j];
+      unsigned nq = 0, nb = 0, no = 0, nc = 0, nk = 0, nm4 = 0, nn = 0;
   #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        const int k = 4 * j + b, p = q0 + k;
         const int c = (int)((w >> (8 * b)) & 0xFFu);
-        if ((unsigned)p < (unsigned)L) {
-          ++nvalid;
-          if (c == '"' && !(run & 1)) par ^= 1;
-          if (leading) {
-            if (c == '\\') {
-              ++lead;
-            } else {
-              leading = false;
-              after_lead = c;
-            }
-          }
-          run = (c == '\\') ? run + 1 : 0;
-          if (!is_ws(c)) {
-            first_nw = min(first_nw, p);
-            last_nw = p;
-          }
-        }
+        const bool v = (unsigned)(q0 + 4 * j + b) < (unsigned)L;
+        const int c20 = c | 0x20;  // '[' -> '{', ']' -> '}'
+        nq |= (v && c == '"' ? 1u : 0u) << b;
+        nb |= (v && c == '\\' ? 1u : 0u) << b;
+        no |= (v && c20 == '{' ? 1u : 0u) << b;
+        nc |= (v && c20 == '}' ? 1u : 0u) << b;
+        nk |= (v && c == ':' ? 1u : 0u) << b;
+        nm4 |= (v && c == ',' ? 1u : 0u) << b;
+        nn |= (v && !is_ws(c) ? 1u : 0u) << b;
       }
+      const int sh = 4 * j;
+      if (nn) {
+        first_nw = min(first_nw, q0 + sh + (__ffs((int)nn) - 1));
+        last_nw = q0 + sh + (31 - __clz((int)nn));
+      }
+      qm |= (unsigned long long)nq << sh;
+      bm |= (unsigned long long)nb << sh;
+      om |= (unsigned long long)no << sh;
+      cm |= (unsigned long long)nc << sh;
+      km |= (unsigned long long)nk << sh;
+      mm |= (unsigned long long)nm4 << sh;
+    }
+    // escape carry into the next lane: the backslash run ending at the segment's last message byte
+    int run = 0;
+    if (vm) {
+      const int top = 63 - __clzll(vm);
+      const unsigned long long below = (top == 63) ? ~0ull : ((2ull << top) - 1ull);
+      const unsigned long long nonbs = vm & ~bm & below;
+      run = nonbs ? top - (63 - __clzll(nonbs)) : __popcll(vm);
     }
     int bs0 = __shfl_up(run, 1);
     if (lane == 0) bs0 = 0;
-    if (__ballot(nvalid > 0 && run == nvalid) != 0ull) {  // a segment of only backslashes: exact carry from LDS
+    if (__ballot(vm != 0ull && bm == vm) != 0ull) {  // a segment of only backslashes: exact carry from LDS
       int b2 = 0;
       for (int p = q0 - 1; p >= 0 && q0 < L && s[p] == '\\'; --p) ++b2;
       bs0 = b2;
     }
-    if ((bs0 & 1) && after_lead == '"') par ^= 1;  // the carry escapes the first quote after the leading run
+    // escaped bytes (after an odd backslash run, the carry included): only lanes with a backslash or an odd carry
+    unsigned long long esc = 0;
+    if (bm != 0ull || (bs0 & 1)) {
+      int r = bs0;
+      for (unsigned long long x = vm; x; x &= x - 1) {
+        const int k = __ffsll((long long)x) - 1;
+        if (r & 1) esc |= 1ull << k;
+        r = ((bm >> k) & 1ull) ? r + 1 : 0;
+      }
+    }
+    const unsigned long long uq = qm & ~esc;  // string delimiters
+    const int par = __popcll(uq) & 1;
     for (int d = 32; d >= 1; d >>= 1) {
       first_nw = min(first_nw, __shfl_xor(first_nw, d));
       last_nw = max(last_nw, __shfl_xor(last_nw, d));
@@ -657,29 +685,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const int in0 = __popcll(pb & lt) & 1;
     const int total_par = __popcll(pb) & 1;
-    // pass 2: bracket depth deltas outside strings -> wave prefix sum
-    int in = in0, delta = 0, mind = 0, bs = bs0;
-  #pragma unroll 2
-    for (int j = 0; j < seg_words; ++j) {
-      const unsigned w = seg[j];
-  #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int p = q0 + 4 * j + b;
-        const int c = (int)((w >> (8 * b)) & 0xFFu);
-        if ((unsigned)p < (unsigned)L) {
-          if (c == '"' && !(bs & 1)) {
-            in ^= 1;
-          } else if (!in) {
-            if (c == '{' || c == '[') ++delta;
-            if (c == '}' || c == ']') {
-              --delta;
-              mind = min(mind, delta);
-            }
-          }
-          bs = (c == '\\') ? bs + 1 : 0;
-        }
-      }
-    }
+    // inside a string: the inclusive prefix XOR of the delimiters, flipped by the state at the segment start
+    unsigned long long instr = uq;
+    instr ^= instr << 1;
+    instr ^= instr << 2;
+    instr ^= instr << 4;
+    instr ^= instr << 8;
+    instr ^= instr << 16;
+    instr ^= instr << 32;
+    if (in0) instr = ~instr;
+    const unsigned long long oo = om & ~instr, oc = cm & ~instr;  // brackets outside strings
+    // pass 2: the bracket depth delta -> wave prefix sum
+    const int delta = __popcll(oo) - __popcll(oc);
     int depth0 = delta;  // inclusive prefix sum over lanes
     for (int d = 1; d < 64; d <<= 1) {
       const int v = __shfl_up(depth0, d);
@@ -687,36 +704,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) i
     }
     const int total_depth = __shfl(depth0, 63);
     depth0 -= delta;
-    bool bad = (depth0 + mind < 0);
-    // pass 3: depth-1 colons (members), depth-1 commas and the first return to depth 0
-    in = in0;
-    bs = bs0;
+    // pass 3, over the structural bytes outside strings only: depth-1 colons (members), depth-1 commas, the first
+    // return to depth 0, and a depth below 0 anywhere (malformed)
+    bool bad = false;
     int depth = depth0, zero_at = L;
-  #pragma unroll 2
-    for (int j = 0; j < seg_words; ++j) {
-      const unsigned w = seg[j];
-  #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int p = q0 + 4 * j + b;
-        const int c = (int)((w >> (8 * b)) & 0xFFu);
-        if ((unsigned)p < (unsigned)L) {
-          if (c == '"' && !(bs & 1)) {
-            in ^= 1;
-          } else if (!in) {
-            if (c == ':' && depth == 1) {
-              const int slot = atomicAdd(&nmem[ms], 1);
-              if (slot < kMaxMembers) colon[ms][slot] = p;
-            } else if (c == ',' && depth == 1) {
-              atomicAdd(&ncomma[ms], 1);
-            } else if (c == '{' || c == '[') {
-              ++depth;
-            } else if (c == '}' || c == ']') {
-              --depth;
-              if (depth == 0) zero_at = min(zero_at, p);
-            }
-          }
-          bs = (c == '\\') ? bs + 1 : 0;
+    for (unsigned long long x = (oo | oc | km | mm) & ~instr; x; x &= x - 1) {
+      const int k = __ffsll((long long)x) - 1;
+      const unsigned long long bit = 1ull << k;
+      const int p = q0 + k;
+      if (km & bit) {
+        if (depth == 1) {
+          const int slot = atomicAdd(&nmem[ms], 1);
+          if (slot < kMaxMembers) colon[ms][slot] = p;
         }
+      } else if (mm & bit) {
+        if (depth == 1) atomicAdd(&ncomma[ms], 1);
+      } else if (oo & bit) {
+        ++depth;
+      } else {
+        --depth;
+        bad = bad || depth < 0;
+        if (depth == 0) zero_at = min(zero_at, p);
       }
     }
     for (int d = 32; d >= 1; d >>= 1) zero_at = min(zero_at, __shfl_xor(zero_at, d));
@@ -1255,7 +1263,7 @@ void launch_ingest(Engine& e, const uint8_t* d_bytes, const int64_t* d_offsets, 
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_INGEST) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, e.stream));
   const int64_t blocks = (n + kSlots - 1) / kSlots;
-  hipLaunchKernelGGL(ingest_json_kernel, dim3((unsigned)blocks), dim3(256), 0, e.stream, d_bytes, d_offsets, n, T, out,
+  hipLaunchKernelGGL(ingest_json_kernel, dim3((unsigned)blocks), dim3(64 * kWaves), 0, e.stream, d_bytes, d_offsets, n, T, out,
                      t.stop_after);
   FD_HIP(hipGetLastError());
   if (ev) FD_HIP(hipEventRecord(ev->b, e.stream));
