@@ -332,6 +332,63 @@ __device__ __forceinline__ int scan_number_w(const Reader& s, int pos, int end, 
 }
 
 __device__ __forceinline__ bool lit_at(const Reader& s, int i, int end, const char* w, int n);
+// parse_iso_instant (ingest_parse.h, same grammar and result) with the fixed 19-byte prefix read as five dwords and
+// the fraction as a digit run: "YYYY-MM-DDTHH:MM:SS[.f{1,9}][Z|(+|-)HH:MM]" occupying exactly s[pos..end)
+__device__ __forceinline__ bool parse_iso_w(const Reader& s, int pos, int end, int64_t* ms) {
+  if (pos + 19 > end) return false;
+  unsigned w[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) w[q] = s.word(pos + 4 * q);
+  auto B = [&](int i) { return (int)((w[i >> 2] >> (8 * (i & 3))) & 0xFFu); };
+  bool ok = B(4) == '-' && B(7) == '-' && B(10) == 'T' && B(13) == ':' && B(16) == ':';
+  auto num = [&](int i, int nd) {  // nd digits from byte i (ok cleared on a non-digit)
+    int v = 0;
+#pragma unroll
+    for (int k = 0; k < nd; ++k) {
+      const int g = B(i + k) - '0';
+      ok = ok && (unsigned)g <= 9u;
+      v = v * 10 + g;
+    }
+    return v;
+  };
+  const int Y = num(0, 4), M = num(5, 2), D = num(8, 2), h = num(11, 2), mi = num(14, 2), sec = num(17, 2);
+  if (!ok) return false;
+  if (M < 1 || M > 12 || D < 1 || h > 23 || mi > 59 || sec > 59) return false;
+  const bool leap = (Y % 4 == 0 && Y % 100 != 0) || Y % 400 == 0;
+  const int mdays = 28 + (int)((0xeefbb3u >> (2 * (M - 1))) & 3u) + ((M == 2 && leap) ? 1 : 0);
+  if (D > mdays) return false;
+  int i = pos + 19;
+  int frac_ms = 0;
+  if (i < end && s[i] == '.') {
+    ++i;
+    int nd = 0;
+    if (i < end && s[i] >= '0' && s[i] <= '9')
+      i = digit_run(s, i, end, [&](int g) {
+        if (nd < 3) frac_ms = frac_ms * 10 + g;
+        ++nd;
+      });
+    if (nd == 0 || nd > 9) return false;
+    for (int k = nd; k < 3; ++k) frac_ms *= 10;
+  }
+  int off_min = 0;
+  if (i < end && (s[i] == 'Z' || s[i] == 'z')) {
+    ++i;
+  } else if (i < end && (s[i] == '+' || s[i] == '-')) {
+    int oh, om;
+    const bool neg = s[i] == '-';
+    if (!digits_at(s, i + 1, 2, end, &oh) || i + 6 > end || s[i + 3] != ':' || !digits_at(s, i + 4, 2, end, &om) ||
+        oh > 18 || om > 59)
+      return false;
+    off_min = (neg ? -1 : 1) * (oh * 60 + om);
+    i += 6;
+  }
+  if (i != end) return false;
+  const int64_t days = days_from_civil(Y, (unsigned)M, (unsigned)D);
+  const int64_t secs = days * 86400 + h * 3600 + mi * 60 + sec - (int64_t)off_min * 60;
+  *ms = secs * 1000 + frac_ms;
+  return true;
+}
+
 
 // the end of the string whose opening quote is at s[pos] (escapes validated, nothing decoded); -1 if malformed
 __device__ __forceinline__ int skip_string(const Reader& s, int pos, int end) {
@@ -565,7 +622,21 @@ __global__ void __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_e
 
   const int wv = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  // ---- staging and structure: wave w indexes messages 2w and 2w+1 of the block's 8, one after the other
+  // ---- staging: wave w stages messages 2w and 2w+1 of the block's, the first 1 KiB of both loaded before either
+  //      is stored (both loads in flight), the rest (messages > 1 KiB) after; one barrier
+  const int64_t total_bytes = offsets[n];
+  int64_t a0h[2];
+  int spanh[2];
+  auto load16 = [&](int64_t g) {
+    if (g + 16 <= total_bytes) return *reinterpret_cast<const uint4*>(buf + g);
+    unsigned wq[4] = {0u, 0u, 0u, 0u};  // the buffer's last partial chunk, byte by byte (no read past its end)
+  #pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (g + q < total_bytes) wq[q >> 2] |= (unsigned)buf[g + q] << (8 * (q & 3));
+    return make_uint4(wq[0], wq[1], wq[2], wq[3]);
+  };
+  uint4 first[2];
+  #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int ms = 2 * wv + h;
     const int64_t m = (int64_t)blockIdx.x * kSlots + ms;
@@ -575,7 +646,6 @@ __global__ void __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_e
       off = offsets[m];
       len = offsets[m + 1] - off;
     }
-    const int64_t total_bytes = offsets[n];
     if (lane == 0) {
       nmem[ms] = 0;
       ncomma[ms] = 0;
@@ -583,27 +653,31 @@ __global__ void __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_e
     }
     if (lane < F_COUNT) win[ms][lane] = -1;
     const bool go = live && len >= 0 && len <= kMaxMsg;
-    const int L = go ? (int)len : 0;
-    // ---- stage (aligned 16-B loads; the tail beyond the input buffer byte by byte)
-    const int64_t a0 = off & ~15ll;
-    const int shift = (int)(off - a0);
-    const int span = shift + L;
-    for (int k = lane; k * 16 < span; k += 64) {
-      const int64_t g = a0 + 16ll * k;
-      uint4 v;
-      if (g + 16 <= total_bytes) {
-        v = *reinterpret_cast<const uint4*>(buf + g);
-      } else {  // the buffer's last partial chunk, byte by byte (no read past its end)
-        unsigned wq[4] = {0u, 0u, 0u, 0u};
+    a0h[h] = off & ~15ll;
+    spanh[h] = (int)(off - a0h[h]) + (go ? (int)len : 0);
+    if (lane * 16 < spanh[h]) first[h] = load16(a0h[h] + 16ll * lane);
+  }
   #pragma unroll
-        for (int q = 0; q < 16; ++q)
-          if (g + q < total_bytes) wq[q >> 2] |= (unsigned)buf[g + q] << (8 * (q & 3));
-        v = make_uint4(wq[0], wq[1], wq[2], wq[3]);
-      }
-      *reinterpret_cast<uint4*>(&stage[ms][16 * k]) = v;
+  for (int h = 0; h < 2; ++h) {
+    const int ms = 2 * wv + h;
+    if (lane * 16 < spanh[h]) *reinterpret_cast<uint4*>(&stage[ms][16 * lane]) = first[h];
+    for (int k = lane + 64; k * 16 < spanh[h]; k += 64)
+      *reinterpret_cast<uint4*>(&stage[ms][16 * k]) = load16(a0h[h] + 16ll * k);
+  }
+  __syncthreads();
+  // ---- structure: the wave's two messages one after the other
+  for (int h = 0; h < 2 && stop_after != 1; ++h) {
+    const int ms = 2 * wv + h;
+    const int64_t m = (int64_t)blockIdx.x * kSlots + ms;
+    const bool live = m < n;
+    int64_t off = 0, len = 0;
+    if (live) {
+      off = offsets[m];
+      len = offsets[m + 1] - off;
     }
-    __syncthreads();
-    if (stop_after == 1) continue;
+    const bool go = live && len >= 0 && len <= kMaxMsg;
+    const int L = go ? (int)len : 0;
+    const int shift = (int)(off & 15ll);
     const Reader s{&stage[ms][0], shift};
 
     // ---- structure, from registers: lane i owns stage bytes [64i, 64i + 64) (16-B aligned) = message bytes
@@ -935,7 +1009,7 @@ __global__ void __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_e
       case F_TIMESTAMP: {
         if (kind == 0) break;
         int64_t ms;
-        if (kind != 1 || st.escaped || !parse_iso_instant(s, v + 1, e - 1, &ms)) {
+        if (kind != 1 || st.escaped || !parse_iso_w(s, v + 1, e - 1, &ms)) {
           bad = true;
           break;
         }

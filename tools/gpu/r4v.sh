@@ -6,7 +6,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_ingest.py -m gpu -x -q --ti
 tail -1 gpurun_out/$T.pytest.log
 timeout -k 10 300 python -u tools/ingest_phases.py > gpurun_out/$T.phases.log 2>&1 || exit 1
 grep stop_after gpurun_out/$T.phases.log
-timeout -k 10 300 python -u tools/ingest_variants.py base loc_null > gpurun_out/$T.variants.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/ingest_variants.py base loc_null ts_nofrac > gpurun_out/$T.variants.log 2>&1 || exit 1
 grep us gpurun_out/$T.variants.log
 timeout -k 10 300 python -u bench.py --workload config3j --no-cpu-baseline > gpurun_out/$T.c3j.log 2>&1 || { tail -20 gpurun_out/$T.c3j.log; exit 1; }
 grep '^{' gpurun_out/$T.c3j.log > gpurun_out/$T.c3j.json
