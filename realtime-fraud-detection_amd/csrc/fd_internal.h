@@ -43,6 +43,23 @@ constexpr int kSplitTiles = 128;  // below this many 256-txn tiles the forest ru
 constexpr int kSeqInput = 16;     // LSTM per-event input width (the bridged raw features)
 constexpr int kLstmHidden = 128;  // lstm_sequential hidden_units (ml/utils/config.py:152-156)
 
+#ifdef FD_FOREST_PROFILE
+// Latency-path timeline (profiling build only; tools/c5_phases.py): per (kernel id, linear workgroup < 1024)
+// {start, mark 1, mark 2, end} of thread 0 in the GPU-wide 100 MHz clock. Each translation unit keeps its own buffer
+// (FD_TL_BUF) and exports it (fd_debug_tl_<unit>); the last launch of each kernel id wins.
+constexpr int kTlKernels = 8;
+#define FD_TL_BUF(name) __device__ unsigned long long name[fd::kTlKernels * 1024 * 4]
+#define FD_TL(buf, kid, k)                                                                            \
+  do {                                                                                                \
+    const unsigned tl_b = blockIdx.x + blockIdx.y * gridDim.x;                                        \
+    if (threadIdx.x == 0 && tl_b < 1024u) buf[((kid) * 1024 + tl_b) * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define FD_TL(buf, kid, k) \
+  do {                     \
+  } while (0)
+#endif
+
 struct Error : std::runtime_error {
   int code;
   Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}

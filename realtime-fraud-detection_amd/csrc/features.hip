@@ -52,6 +52,7 @@ constexpr size_t kBucketLds = (size_t)kChunkCap * 8 + (size_t)(kMaxBins + 1) * 4
 // Phase stamps of the bucket kernel (profiling build only): per workgroup b < 4096 {start, keys loaded,
 // sorted, short segments done (workgroup barrier), end} plus each wave's own end of the short loop.
 __device__ unsigned long long g_fprof[4096 * 8];
+FD_TL_BUF(g_tl_feat);
 #define FD_FSTAMP(k)                                                                              \
   do {                                                                                            \
     if (threadIdx.x == 0 && blockIdx.x < 4096) g_fprof[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
@@ -252,6 +253,7 @@ __global__ void __launch_bounds__(kST) feat_slot_kernel(CardPages P, unsigned lo
                                                         unsigned* __restrict__ ovf_b, unsigned* err) {
   extern __shared__ unsigned hist[];  // [nbm + 1] block counts | [nbm + 1] reserved run starts
   unsigned* run = hist + nbm + 1;
+  FD_TL(g_tl_feat, 0, 0);
   for (unsigned b = threadIdx.x; b <= nbm; b += kST) hist[b] = 0u;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kST + threadIdx.x;
@@ -287,6 +289,7 @@ __global__ void __launch_bounds__(kST) feat_slot_kernel(CardPages P, unsigned lo
       ovf_b[j] = b;
     }
   }
+  FD_TL(g_tl_feat, 0, 3);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -646,6 +649,7 @@ struct BucketArgs {
   int par;
   const unsigned long long* ovf_key;  // overflow list: key, bucket
   const unsigned* ovf_b;
+  unsigned spec;                      // latency batches: region entries read before the fill count (<= kBT, <= C)
 };
 
 template <int MODE>
@@ -1029,12 +1033,16 @@ __device__ void bucket_body(const BucketArgs& a, const int b, unsigned long long
                             int& n_long, int& chunk_m) {
   unsigned* bins = reinterpret_cast<unsigned*>(skeys + kChunkCap);
   FD_FSTAMP(0);
-  const unsigned m = a.fill[b];  // region (min(m, C)) + overflow entries (m - C) of this bucket
   const unsigned long long* src = a.pairs + (size_t)b * a.C;
+  // latency batches: the region's first `spec` entries are read in the same round trip as the fill count (stale
+  // entries past it are dropped below), not after it
+  const unsigned long long early = threadIdx.x < a.spec ? src[threadIdx.x] : 0ull;
+  const unsigned m = a.fill[b];  // region (min(m, C)) + overflow entries (m - C) of this bucket
   const unsigned in_region = m < a.C ? m : a.C;
   const unsigned n_ovf = m > a.C ? a.ovf_cnt[a.par] : 0u;  // the whole list is scanned for this bucket's entries
   if (m <= (unsigned)kChunkCap) {
-    for (unsigned q = threadIdx.x; q < in_region; q += kBT) skeys[q] = src[q];
+    if (threadIdx.x < a.spec && threadIdx.x < in_region) skeys[threadIdx.x] = early;
+    for (unsigned q = threadIdx.x + a.spec; q < in_region; q += kBT) skeys[q] = src[q];
     if (n_ovf) {
       if (threadIdx.x == 0) chunk_m = (int)in_region;
       __syncthreads();
@@ -1121,7 +1129,9 @@ __global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
   __shared__ LongLds sm;
   __shared__ int long_list[kChunkCap / (kSegLong + 1) + 1];
   __shared__ int n_long, chunk_m;
+  FD_TL(g_tl_feat, 1, 0);
   bucket_body<MODE>(a, blockIdx.x, skeys, sm, long_list, n_long, chunk_m);
+  FD_TL(g_tl_feat, 1, 3);
 }
 
 // The bucket kernel's LDS working set, in global memory (one per bucket) for the lean kernel's slow path
@@ -1732,6 +1742,8 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.par = par;
   a.ovf_key = g.ovf_key.as<const unsigned long long>();
   a.ovf_b = g.ovf_b.as<const unsigned>();
+  // early region reads (latency batches): 4x the mean bucket fill covers the Poisson tail, at most one per thread
+  a.spec = n < 8192 ? (unsigned)std::min<int64_t>({(int64_t)kBT, (int64_t)C, 4 * ((n + nb - 1) / nb)}) : 0u;
   const size_t lds = kBucketLds;
   if (lean) {
     st.bucket_scr.ensure((size_t)nb * sizeof(BucketScratch));
@@ -1885,6 +1897,9 @@ void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context
 #ifdef FD_FOREST_PROFILE
 extern "C" __attribute__((visibility("default"))) int fd_debug_feat_profile(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprof), sizeof(unsigned long long) * (size_t)n);
+}
+extern "C" __attribute__((visibility("default"))) int fd_debug_tl_feat(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tl_feat), sizeof(g_tl_feat));
 }
 #endif
 

@@ -415,6 +415,7 @@ constexpr int kWG3 = 1024;
 // Phase-cycle instrumentation (s_memtime), built only into the profiling variant of the library:
 // per wave of the first 256 workgroups {prologue, walk, leaf store, owner sum, barrier, total}.
 __device__ unsigned long long g_prof[256 * 16 * 8];
+FD_TL_BUF(g_tl_forest);
 #define FD_PROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define FD_PROF_ADD(acc, a, b) acc += (b) - (a)
 #else
@@ -938,11 +939,13 @@ struct SplitBinArgs {
 // both forests of a latency batch binned in one launch: grid.y = nf_a + nf_b
 __global__ void __launch_bounds__(kSplitBin)
 split_bin_pair_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, SplitBinArgs a, SplitBinArgs b) {
+  FD_TL(g_tl_forest, 3, 0);
   const int y = (int)blockIdx.y;
   if (y < a.nf)
     split_bin_body(X, n, n_pad, ld, y, a.thr, a.thr_off, a.bins, a.tile_nan);
   else
     split_bin_body(X, n, n_pad, ld, y - a.nf, b.thr, b.thr_off, b.bins, b.tile_nan);
+  FD_TL(g_tl_forest, 3, 3);
 }
 
 // Stage `rows` rows of 1 KiB (row r at src + r * row_stride) into LDS at dst + r * 1024 by LDS-DMA.
@@ -1042,6 +1045,7 @@ struct SplitWalkArgs {
 template <int DX, int CHX, int DI, int CHI>
 __global__ void __launch_bounds__(kWG3) split_walk_pair_kernel(int64_t n, int64_t n_pad, int nf, SplitWalkArgs x,
                                                                SplitWalkArgs f) {
+  FD_TL(g_tl_forest, 4, 0);
   const int gy = (int)blockIdx.y;
   if (gy < x.groups)
     split_walk_body<DX, CHX, float>(x.bins, n, n_pad, nf, x.tile_nan, x.blob, x.n_chunks, x.chunk_stride, x.cpg,
@@ -1049,6 +1053,7 @@ __global__ void __launch_bounds__(kWG3) split_walk_pair_kernel(int64_t n, int64_
   else
     split_walk_body<DI, CHI, double>(f.bins, n, n_pad, nf, f.tile_nan, f.blob, f.n_chunks, f.chunk_stride, f.cpg,
                                      f.leaf_ids, f.n_trees, static_cast<double*>(f.leaves), nullptr, gy - x.groups);
+  FD_TL(g_tl_forest, 4, 3);
 }
 
 // The latency pair's epilogue in ONE launch: per transaction the XGBoost margin (base + f32 leaves in tree order)
@@ -1066,82 +1071,146 @@ struct PairBlendArgs {
   uint8_t *dec, *risk;
 };
 
-template <int R>
-__device__ __forceinline__ void stream_leaves(const char* __restrict__ leaves, int esz, int64_t n, int n_trees,
-                                              int64_t r0, int rows, char* __restrict__ blk, int t0, int tc) {
-  // [tc][R] block of leaf values (esz bytes each) into LDS: independent loads, 16 in flight per thread
-  const int total = tc * R;
-  for (int base = 0; base < total; base += 256 * 16) {
-    unsigned long long v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int i = base + u * 256 + (int)threadIdx.x;
-      const int t = i / R, r = i - t * R;
-      v[u] = 0ull;
-      if (i < total && r < rows) {
-        const char* src = leaves + ((size_t)(t0 + t) * n + r0 + r) * esz;
-        v[u] = esz == 8 ? *reinterpret_cast<const unsigned long long*>(src) : *reinterpret_cast<const unsigned*>(src);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int i = base + u * 256 + (int)threadIdx.x;
-      if (i < total) {
-        if (esz == 8)
-          reinterpret_cast<unsigned long long*>(blk)[i] = v[u];
-        else
-          reinterpret_cast<unsigned*>(blk)[i] = (unsigned)v[u];
-      }
-    }
-  }
-}
+constexpr int kPairRows = 4;    // transactions per workgroup of the pair epilogue (256 workgroups for a 1 k batch)
+static_assert(kPairRows == 4, "the pair epilogue stages a tree's rows as one 16-B (f32) / 32-B (f64) load");
+constexpr int kPairTcX = 2048;  // XGBoost trees per LDS block (f32: 32 KiB)
+constexpr int kPairTcF = 1024;  // IsolationForest trees per LDS block (f64: 32 KiB)
+constexpr int kPairLoads = 4;   // trees (16 / 32-B leaf loads) in flight per thread per staging round
 
+// One dependent global round trip for the whole epilogue: the other models' columns (e.g. the LSTM head's) and
+// both forests' [trees][rows] leaf blocks are loaded together (a tree's 4 rows per 16 / 32-B load), then one wave adds
+// the f32 margins and another wave the f64 path lengths, each in tree order (the sequential sums, bit for bit),
+// and the probabilities go straight into blend_row (not written and read back).
 __global__ void __launch_bounds__(256)
 split_sum_pair_blend_kernel(const float* __restrict__ lx, int tx, const double* __restrict__ lf, int tf, int64_t n,
                             PairBlendArgs a, uint32_t* __restrict__ nan_x, uint32_t* __restrict__ nan_f) {
-  constexpr int R = kSumRows;
-  constexpr int kTc = 65536 / (R * 8);  // trees per LDS block (64 KiB of f64; f32 blocks use half)
-  __shared__ double blk[kTc * R];
+  constexpr int R = kPairRows;
+  // row-major blocks (a row's trees contiguous: the sums read 4 / 2 leaves per ds_read_b128); the row strides are
+  // 16 mod 64 banks, so the staging stores of a wave ((tree, row) = (i / 4, i % 4)) hit distinct banks
+  constexpr int kSX = kPairTcX + 16, kSF = kPairTcF + 16;
+  __shared__ __attribute__((aligned(16))) float bx[R * kSX];
+  __shared__ __attribute__((aligned(16))) double bfl[R * kSF];
+  __shared__ double fsum[R];
+  FD_TL(g_tl_forest, 5, 0);
   const int tid = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * R;
+  // XCD-aware rows: workgroups b and b + 8 run on the same XCD (round-robin dispatch), so give each XCD a
+  // contiguous run of row blocks — the 128-B lines of a tree's leaves are then fetched into one L2, not eight
+  const unsigned G = gridDim.x, xq = G / 8u, xr = G % 8u, x = blockIdx.x % 8u, k = blockIdx.x / 8u;
+  const unsigned lb = (x < xr ? x * (xq + 1u) : xr * (xq + 1u) + (x - xr) * xq) + k;
+  const int64_t r0 = (int64_t)lb * R;
   const int rows = (int)min<int64_t>(R, n - r0);
+  const bool xrow = tid < rows;                  // wave 0: the XGBoost margin and the blend of row tid
+  const bool frow = tid >= 64 && tid < 64 + rows;  // wave 1: the IsolationForest sum of row tid - 64
+  double other[FD_MAX_MODELS];
+#pragma unroll
+  for (int m = 0; m < FD_MAX_MODELS; ++m)
+    other[m] = (xrow && m < a.blend.n_models && m != a.pos_x && m != a.pos_f) ? a.cols.p[m][r0 + tid] : 0.0;
   float accx = a.base_margin;
-  for (int t0 = 0; t0 < tx; t0 += kTc) {
-    const int tc = min(kTc, tx - t0);
-    stream_leaves<R>(reinterpret_cast<const char*>(lx), 4, n, tx, r0, rows, reinterpret_cast<char*>(blk), t0, tc);
-    __syncthreads();
-    if (tid < rows) {
-      const float* b = reinterpret_cast<const float*>(blk);
-      for (int t = 0; t < tc; ++t) accx += b[t * R + tid];
+  double accf = 0.0;
+  for (int t0x = 0, t0f = 0; t0x < tx || t0f < tf; t0x += kPairTcX, t0f += kPairTcF) {
+    const int tcx = max(0, min(kPairTcX, tx - t0x)), tcf = max(0, min(kPairTcF, tf - t0f));
+    // one tree's R leaves per item (16 B of f32 / 32 B of f64 when the rows are aligned and complete)
+    const int items = tcx + tcf;
+    const bool vec = rows == R && (n % R) == 0;
+    for (int base = 0; base < items; base += 256 * kPairLoads) {
+      uint4 v[kPairLoads][2];
+#pragma unroll
+      for (int u = 0; u < kPairLoads; ++u) {
+        const int i = base + u * 256 + tid;
+        v[u][0] = v[u][1] = make_uint4(0u, 0u, 0u, 0u);
+        if (i < tcx) {
+          const float* src = lx + (size_t)(t0x + i) * n + r0;
+          if (vec) {
+            v[u][0] = *reinterpret_cast<const uint4*>(src);
+          } else {
+            unsigned w[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) w[r] = r < rows ? __float_as_uint(src[r]) : 0u;
+            v[u][0] = make_uint4(w[0], w[1], w[2], w[3]);
+          }
+        } else if (i < items) {
+          const double* src = lf + (size_t)(t0f + i - tcx) * n + r0;
+          if (vec) {
+            v[u][0] = reinterpret_cast<const uint4*>(src)[0];
+            v[u][1] = reinterpret_cast<const uint4*>(src)[1];
+          } else {
+            unsigned long long w[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) w[r] = r < rows ? (unsigned long long)__double_as_longlong(src[r]) : 0ull;
+            v[u][0] = make_uint4((unsigned)w[0], (unsigned)(w[0] >> 32), (unsigned)w[1], (unsigned)(w[1] >> 32));
+            v[u][1] = make_uint4((unsigned)w[2], (unsigned)(w[2] >> 32), (unsigned)w[3], (unsigned)(w[3] >> 32));
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kPairLoads; ++u) {
+        const int i = base + u * 256 + tid;
+        if (i < tcx) {
+          bx[0 * kSX + i] = __uint_as_float(v[u][0].x);
+          bx[1 * kSX + i] = __uint_as_float(v[u][0].y);
+          bx[2 * kSX + i] = __uint_as_float(v[u][0].z);
+          bx[3 * kSX + i] = __uint_as_float(v[u][0].w);
+        } else if (i < items) {
+          const int t = i - tcx;
+          bfl[0 * kSF + t] = __longlong_as_double((long long)(((unsigned long long)v[u][0].y << 32) | v[u][0].x));
+          bfl[1 * kSF + t] = __longlong_as_double((long long)(((unsigned long long)v[u][0].w << 32) | v[u][0].z));
+          bfl[2 * kSF + t] = __longlong_as_double((long long)(((unsigned long long)v[u][1].y << 32) | v[u][1].x));
+          bfl[3 * kSF + t] = __longlong_as_double((long long)(((unsigned long long)v[u][1].w << 32) | v[u][1].z));
+        }
+      }
     }
     __syncthreads();
-  }
-  double accf = 0.0;
-  for (int t0 = 0; t0 < tf; t0 += kTc) {
-    const int tc = min(kTc, tf - t0);
-    stream_leaves<R>(reinterpret_cast<const char*>(lf), 8, n, tf, r0, rows, reinterpret_cast<char*>(blk), t0, tc);
+    if (t0x == 0) FD_TL(g_tl_forest, 5, 1);
+    if (xrow) {  // tree order: 64 leaves per batch of 16 ds_read_b128
+      const float4* q = reinterpret_cast<const float4*>(&bx[tid * kSX]);
+      int t = 0;
+      for (; t + 64 <= tcx; t += 64) {
+        float4 w[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) w[u] = q[t / 4 + u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          accx += w[u].x;
+          accx += w[u].y;
+          accx += w[u].z;
+          accx += w[u].w;
+        }
+      }
+      for (; t < tcx; ++t) accx += bx[tid * kSX + t];
+    } else if (frow) {
+      const int r = tid - 64;
+      const double2* q = reinterpret_cast<const double2*>(&bfl[r * kSF]);
+      int t = 0;
+      for (; t + 32 <= tcf; t += 32) {
+        double2 w[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) w[u] = q[t / 2 + u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          accf += w[u].x;
+          accf += w[u].y;
+        }
+      }
+      for (; t < tcf; ++t) accf += bfl[r * kSF + t];
+    }
     __syncthreads();
-    if (tid < rows)
-      for (int t = 0; t < tc; ++t) accf += blk[t * R + tid];
-    __syncthreads();
+    if (t0x == 0) FD_TL(g_tl_forest, 5, 2);
   }
+  if (frow) fsum[tid - 64] = accf;
   if (tid == 0 && r0 % kTile == 0) {  // every walk of the tile is done (stream order): clear the NaN flags
     nan_x[r0 / kTile] = 0u;
     nan_f[r0 / kTile] = 0u;
   }
-  if (tid >= rows) return;
+  __syncthreads();
+  if (!xrow) return;
   const int64_t row = r0 + tid;
-  double px, pf;
-  write_outputs<FD_FOREST_XGB_BINARY_LOGISTIC, float>(accx, row, 0.0, 0.0, const_cast<double*>(a.cols.p[a.pos_x]),
-                                                      nullptr);
-  write_outputs<FD_FOREST_SKLEARN_IFOREST, double>(accf, row, a.if_offset, a.if_denom,
-                                                   const_cast<double*>(a.cols.p[a.pos_f]), nullptr);
-  px = a.cols.p[a.pos_x][row];
-  pf = a.cols.p[a.pos_f][row];
+  const double px = forest_prob<FD_FOREST_XGB_BINARY_LOGISTIC, float>(accx, 0.0, 0.0);
+  const double pf = forest_prob<FD_FOREST_SKLEARN_IFOREST, double>(fsum[tid], a.if_offset, a.if_denom);
+  const_cast<double*>(a.cols.p[a.pos_x])[row] = px;
+  const_cast<double*>(a.cols.p[a.pos_f])[row] = pf;
   double raw[FD_MAX_MODELS];
 #pragma unroll
-  for (int m = 0; m < FD_MAX_MODELS; ++m)
-    raw[m] = m >= a.blend.n_models ? 0.0 : (m == a.pos_x ? px : (m == a.pos_f ? pf : a.cols.p[m][row]));
+  for (int m = 0; m < FD_MAX_MODELS; ++m) raw[m] = m == a.pos_x ? px : (m == a.pos_f ? pf : other[m]);
   double fp, conf;
   uint8_t dec, risk;
   blend_row(a.blend, raw, fp, conf, dec, risk);
@@ -1149,6 +1218,7 @@ split_sum_pair_blend_kernel(const float* __restrict__ lx, int tx, const double* 
   if (a.conf) a.conf[row] = conf;
   if (a.dec) a.dec[row] = dec;
   if (a.risk) a.risk[row] = risk;
+  FD_TL(g_tl_forest, 5, 3);
 }
 
 // 8 transactions per workgroup (128 workgroups for a 1 k batch): all 256 threads stream a [trees][8] block of
@@ -1414,6 +1484,9 @@ bool split_path(const Engine& e, const PackedForest& pf, int64_t n) {
 extern "C" __attribute__((visibility("default"))) int fd_debug_forest_profile(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * (size_t)n);
 }
+extern "C" __attribute__((visibility("default"))) int fd_debug_tl_forest(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(fd::g_tl_forest), sizeof(fd::g_tl_forest));
+}
 #endif
 
 // Kernel choice (option "forest_kernel"): 0 auto = kernel 6 when the binned node-only layout exists
@@ -1541,7 +1614,7 @@ bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedFor
   pa.dec = ddec;
   pa.risk = drisk;
   if (before_blend) FD_HIP(hipStreamWaitEvent(st, before_blend, 0));  // e.g. the LSTM head on a side stream
-  hipLaunchKernelGGL(split_sum_pair_blend_kernel, dim3((unsigned)((n + kSumRows - 1) / kSumRows)), dim3(256), 0, st,
+  hipLaunchKernelGGL(split_sum_pair_blend_kernel, dim3((unsigned)((n + kPairRows - 1) / kPairRows)), dim3(256), 0, st,
                      X.split.leaves.as<const float>(), X.n_trees, F.split.leaves.as<const double>(), F.n_trees, n, pa,
                      a.tile_nan, b.tile_nan);
   FD_HIP(hipGetLastError());

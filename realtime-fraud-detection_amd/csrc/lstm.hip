@@ -37,6 +37,9 @@
 #include "fd_internal.h"
 
 namespace fd {
+#ifdef FD_FOREST_PROFILE
+FD_TL_BUF(g_tl_lstm);
+#endif
 namespace {
 
 constexpr int kH = kLstmHidden;  // 128
@@ -174,6 +177,7 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
   __shared__ __attribute__((aligned(16))) float xs[FD_MAX_SEQ_LEN][64];     // 4 KB
   __shared__ float hT[4][kH];
   __shared__ float zs[4][2];
+  FD_TL(g_tl_lstm, 2, 0);
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
   // B operands: lane l holds W[(l >> 4) * 128 + 16 w + (l & 15)][k] for k = 0..143 (W_ih, then W_hh)
@@ -182,6 +186,10 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
   for (int k = 0; k < kKT; ++k) bw[k] = wpk4[((size_t)w * kKT + k) * 64 + l];
   const int q = l >> 4, unit = 16 * w + (l & 15);
   const float bcol = bias[q * kH + unit];
+  // dense head: wave w computes output ho of transaction hr, lane l the products of units l and l + 64
+  const int hr = w & 3, ho = w >> 2;
+  const float wo0 = ho < n_out ? wout[ho * kH + l] : 0.f, wo1 = ho < n_out ? wout[ho * kH + 64 + l] : 0.f;
+  const float bo = ho < n_out ? bout[ho] : 0.f;
   const int64_t ntiles = (n + 3) / 4;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t row0 = tile * 4;
@@ -192,6 +200,7 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
     (&hbuf[0][0][0])[tid] = 0.f;  // 512 threads = 4 x 128
     float c = 0.f, h = 0.f;
     __syncthreads();
+    if (tile == blockIdx.x) FD_TL(g_tl_lstm, 2, 1);
     for (int t = 0; t < T; ++t) {
       f32x4 acc[4] = {f32x4{bcol, bcol, bcol, bcol}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
                       f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -220,13 +229,14 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
       hbuf[(t + 1) & 1][unit >> 4][q + 4 * (unit & 15)] = h;
       __syncthreads();
     }
+    if (tile == blockIdx.x) FD_TL(g_tl_lstm, 2, 2);
     hT[q][unit] = h;
     __syncthreads();
-    if (tid < 4 * n_out) {  // dense head over h_T, fixed k order
-      const int r = tid / n_out, o = tid - r * n_out;
-      float z = bout[o];
-      for (int k = 0; k < kH; ++k) z = z + wout[o * kH + k] * hT[r][k];
-      zs[r][o] = z;
+    if (ho < n_out) {  // dense head over h_T: a wave's 64 two-product partials, then a butterfly sum
+      float z = wo0 * hT[hr][l] + wo1 * hT[hr][l + 64];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) z += __shfl_xor(z, off);
+      if (l == 0) zs[hr][ho] = bo + z;
     }
     __syncthreads();
     if (tid < 4 && row0 + tid < n) {
@@ -242,6 +252,7 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
     }
     __syncthreads();  // xs / hbuf / hT / zs are rewritten by the next tile
   }
+  FD_TL(g_tl_lstm, 2, 3);
 }
 
 }  // namespace
@@ -325,3 +336,9 @@ void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, i
 }
 
 }  // namespace fd
+
+#ifdef FD_FOREST_PROFILE
+extern "C" __attribute__((visibility("default"))) int fd_debug_tl_lstm(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(fd::g_tl_lstm), sizeof(fd::g_tl_lstm));
+}
+#endif

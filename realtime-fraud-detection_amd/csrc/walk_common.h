@@ -76,22 +76,25 @@ __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" :
 // XGBoost common::Sigmoid (src/common/math.h) in f32 / sklearn score -> decision -> the
 // reference's 1/(1+exp(s)) in f64.
 template <int KIND, typename LeafT>
-__device__ __forceinline__ void write_outputs(LeafT acc, int64_t row, double if_offset, double if_denom,
-                                              double* out_prob, double* out_raw) {
+__device__ __forceinline__ double forest_prob(LeafT acc, double if_offset, double if_denom) {
   if (KIND == FD_FOREST_XGB_BINARY_LOGISTIC) {
     const float m = (float)acc;
     const float xm = fminf(-m, 88.7f);
     const float denom = expf(xm) + 1.0f + 1e-16f;
-    out_prob[row] = (double)(1.0f / denom);
-    if (out_raw) out_raw[row] = (double)m;
+    return (double)(1.0f / denom);
   } else {
     const double d = (double)acc;
     const double q = (if_denom != 0.0) ? d / if_denom : 1.0;
     const double score = pow(2.0, -q);
     const double decision = -score - if_offset;
-    out_prob[row] = 1.0 / (1.0 + exp(decision));
-    if (out_raw) out_raw[row] = d;
+    return 1.0 / (1.0 + exp(decision));
   }
+}
+template <int KIND, typename LeafT>
+__device__ __forceinline__ void write_outputs(LeafT acc, int64_t row, double if_offset, double if_denom,
+                                              double* out_prob, double* out_raw) {
+  out_prob[row] = forest_prob<KIND, LeafT>(acc, if_offset, if_denom);
+  if (out_raw) out_raw[row] = KIND == FD_FOREST_XGB_BINARY_LOGISTIC ? (double)(float)acc : (double)acc;
 }
 
 
