@@ -101,7 +101,7 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
                          const uint8_t* present, const float* dX, int64_t n, int32_t ld, double* dMP,
                          double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk, const float* d_seq = nullptr,
                          int T = 0, const fd::RouteRecord* records = nullptr, fd::ResultRecord* results = nullptr,
-                         bool compact = false) {
+                         bool compact = false, const unsigned long long* d_seq_desc = nullptr) {
   FD_REQUIRE(p.n_models > 0 && p.n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "n_models out of range");
   FD_REQUIRE(slots != nullptr && (dfp != nullptr || results != nullptr), FD_ERR_INVALID_ARG, "null slots/output");
   if (n == 0) return false;
@@ -144,10 +144,10 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
                "the LSTM head needs card-history sequences (fd_score_batch_device with seq_len > 0)");
     double* col = dMP + (size_t)m * n;
     if (ss == 0) {
-      fd::launch_lstm(e, e.stream, d_seq, n, T, col);
+      fd::launch_lstm(e, e.stream, d_seq, n, T, col, d_seq_desc);
     } else {
       fork_aux();
-      fd::launch_lstm(e, e.aux_stream, d_seq, n, T, col);
+      fd::launch_lstm(e, e.aux_stream, d_seq, n, T, col, d_seq_desc);
     }
     cols[m] = col;
   }
@@ -312,7 +312,7 @@ int fd_engine_destroy(fd_engine* eng) {
   e.feat_in.release();
   fd::windows_release(e);
   fd::sink_release(e);
-  for (auto* b : {&e.route_blk, &e.route_blk_stream, &e.route_out, &e.route_err, &e.seq_buf, &e.lstm.wpk, &e.lstm.wpk4, &e.lstm.bias,
+  for (auto* b : {&e.route_blk, &e.route_blk_stream, &e.route_out, &e.route_err, &e.seq_buf, &e.seq_desc, &e.lstm.wpk, &e.lstm.wpk4, &e.lstm.bias,
                   &e.lstm.wout, &e.lstm.bout, &e.state.seq})
     b->release();
   if (e.aux_stream) {
@@ -501,10 +501,17 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(value == 0 || (value >= 8 && value <= 512 && (value & (value - 1)) == 0), FD_ERR_INVALID_ARG,
                "bucket_keys must be 0 or a power of two in 8..512");
     e.state.bucket_keys = (int)value;
+  } else if (k == "bucket_spread") {  // feature bucket pass, >= 8 k transactions: 1 (default) card segments
+    // round-robin over the 4 waves
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "bucket_spread must be 0 or 1");
+    e.state.bucket_spread = value != 0;
   } else if (k == "timing_every") {  // kernel timing (fd_timing_*): HIP events on one launch in N of each kind
     FD_REQUIRE(value >= 1 && value <= 1000000, FD_ERR_INVALID_ARG, "timing_every must be >= 1");
     e.timing_every = (int)value;
     for (auto& q : e.timing_seq) q = 0;  // the next launch of every kind is a timed one
+  } else if (k == "seq_ring_lstm") {  // latency batches: 1 (default) the LSTM reads card histories from the ring
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "seq_ring_lstm must be 0 or 1");
+    e.seq_ring_lstm = value != 0;
   } else if (k == "lstm_rows") {  // LSTM tile: 0 auto (4 below 4096 transactions, else 16), 4 or 16
     FD_REQUIRE(value == 0 || value == 4 || value == 16, FD_ERR_INVALID_ARG, "lstm_rows must be 0, 4 or 16");
     e.lstm_rows = (int)value;
@@ -904,8 +911,17 @@ static void score_batch_body(Engine& e, const fd_blend_params& p, const int32_t*
     vec = e.feat_vec.as<float>();
   }
   float* seq = lstm_seq_buffer(e, p, slots, present, n);
-  fd::launch_features(e, t, n, vec, nullptr, seq);
-  score_matrix(e, p, slots, ext, present, vec, n, FD_VECTOR_WIDTH, dMP, dfp, dconf, ddec, drisk, seq, e.state.S);
+  // latency batches: the LSTM (4-row kernel) reads each card's last transaction's sequence from the history ring,
+  // which nothing rewrites before it runs (the next batch's features follow on this stream); the feature kernel
+  // writes only the other rows
+  unsigned long long* desc = nullptr;
+  if (seq && e.seq_ring_lstm && n < 4096 && (e.lstm_rows == 0 || e.lstm_rows == 4)) {
+    e.seq_desc.ensure((size_t)n * sizeof(unsigned long long));
+    desc = e.seq_desc.as<unsigned long long>();
+  }
+  fd::launch_features(e, t, n, vec, nullptr, seq, nullptr, nullptr, false, 0, nullptr, false, desc);
+  score_matrix(e, p, slots, ext, present, vec, n, FD_VECTOR_WIDTH, dMP, dfp, dconf, ddec, drisk, seq, e.state.S,
+               nullptr, nullptr, false, desc);
 }
 
 int fd_score_batch_device(fd_engine* eng, const fd_blend_params* params, const int32_t* slots,

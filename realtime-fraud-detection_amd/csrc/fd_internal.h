@@ -41,6 +41,7 @@ constexpr size_t kLdsBudget = 160 * 1024;  // LDS per CU (one workgroup per CU a
 constexpr int kMaxBins = 65534;   // distinct thresholds per feature in the binned layout
 constexpr int kSplitTiles = 128;  // below this many 256-txn tiles the forest runs the tree-split path
 constexpr int kSeqInput = 16;     // LSTM per-event input width (the bridged raw features)
+constexpr unsigned long long kSeqMaterialized = 1ull << 63;  // sequence descriptor: row i of the sequence buffer
 constexpr int kLstmHidden = 128;  // lstm_sequential hidden_units (ml/utils/config.py:152-156)
 
 #ifdef FD_FOREST_PROFILE
@@ -318,6 +319,7 @@ struct CardStore {
   int K = 1;         // ring events per card (sliding)
   int S = 0;         // LSTM history events per card (0 = off)
   int bucket_keys = 0;  // option "bucket_keys": transactions per bucket workgroup (0 auto, features.hip)
+  bool bucket_spread = true;  // option "bucket_spread": a bucket's card segments dealt over all 4 waves
   int64_t n_merchants = 0;
   DeviceBuffer pages, keys, merchants, err, seq;  // pages: CardPages (header + ring per slot); keys: the compact
                                                   // key array card_slot probes
@@ -450,6 +452,7 @@ struct Engine {
   hipStream_t aux2_stream = nullptr;           // small batches: the second forest, concurrent with the first
   hipEvent_t join2_ev = nullptr;
   DeviceBuffer seq_buf;                        // per-txn LSTM input sequences of the fused path
+  DeviceBuffer seq_desc;                       // latency path: per-txn sequence descriptors (kSeqMaterialized)
   DeviceBuffer feat_vec, feat_in, feat_ext;  // host-API / fused-pipeline staging for features
   // fd_score_batch_pipelined (engine.hip): features and scoring of batch i on pipe_stream[i & 1] (no cross-stream
   // wait between a batch's features and its forests; batch i-1's features waited for by event); vectors / LSTM
@@ -472,6 +475,7 @@ struct Engine {
   bool pipe_copy_vec[kPipeSlots] = {};  // that copy also read the slot's vectors (the slot's next features wait)
   int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
+  bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
   bool compact_vectors = true;  // "compact_vectors": the pipelined stream's compact scoring vectors (engine.hip)
   int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)
   // host-API staging
@@ -569,7 +573,8 @@ void load_merchants(Engine& e, const fd_merchants& m);
 // compact: d_vec rows are the fused pipeline's compact form (kCompactWidth floats), not the 64-wide vector
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw,
                      float* d_seq = nullptr, double* d_vel5 = nullptr, hipStream_t stream = nullptr,
-                     bool lean = false, int set = 0, hipEvent_t before_buckets = nullptr, bool compact = false);
+                     bool lean = false, int set = 0, hipEvent_t before_buckets = nullptr, bool compact = false,
+                     unsigned long long* d_seq_desc = nullptr);
 // the same over received 48-B route records (route.hip), no unpack pass; also returns nothing else
 void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq,
                              hipStream_t stream = nullptr, bool lean = false, int set = 0,
@@ -622,7 +627,10 @@ void comm_exchange(Engine& e, bool back, hipStream_t st, const void* sendbuf, co
                    const int64_t* recv, size_t elem);
 // lstm.hip
 void load_lstm(Engine& e, const fd_lstm_params& p);
-void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, int T, double* d_prob);
+// d_desc (latency path): per transaction its sequence's place — the card's history ring or row i of d_seq
+// (features.hip seq_step); null: every row of d_seq
+void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, int T, double* d_prob,
+                 const unsigned long long* d_desc = nullptr);
 // model_io.hip: the unchanged XGBoost 2.0.3 JSON model file, flattened (fdengine/forest.py semantics)
 struct XgbModel {
   int num_feature = 0;

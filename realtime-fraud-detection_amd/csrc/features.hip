@@ -414,6 +414,10 @@ struct Outputs {
   float* seq;     // [n][S][16] LSTM input sequences or null
   float* seq_ring;  // [cap][S][16] per-card LSTM history (S > 0)
   int S;
+  // latency path (fd_score_batch_device, < 4 k transactions): per transaction where the LSTM kernel reads its
+  // sequence — the card's ring (slot | head << 32 | count << 40; the card's last transaction of the batch, whose
+  // sequence is the ring as this launch leaves it) or, kSeqMaterialized, row i of seq. Null: every row into seq.
+  unsigned long long* seq_desc;
   // sliding mode: transactions whose 24 h window held the ring's whole capacity K of prior events (the count may
   // be truncated there: the reference's counters are unbounded, RedisTransactionSink.java:93-105); null otherwise
   unsigned long long* sat;
@@ -608,8 +612,10 @@ __device__ __forceinline__ void velocity_step(CardRegs& c, RingEvent* __restrict
   }
 }
 
-// LSTM head input: this event appended to the card's history, the last S events emitted
-__device__ __forceinline__ void seq_step(const Outputs& o, unsigned s, unsigned& flags, int64_t i, const double* r) {
+// LSTM head input: this event appended to the card's history, the last S events emitted (or, for the card's last
+// transaction of the batch on the latency path, its place in the ring: the LSTM kernel reads them there)
+__device__ __forceinline__ void seq_step(const Outputs& o, unsigned s, unsigned& flags, int64_t i, const double* r,
+                                         bool last) {
   const int S = o.S;
   int seq_n = (int)((flags >> 8) & 0xffu), seq_head = (int)((flags >> 16) & 0xffu);
   float* sr = o.seq_ring + (size_t)s * S * kSeqInput;
@@ -618,7 +624,14 @@ __device__ __forceinline__ void seq_step(const Outputs& o, unsigned s, unsigned&
   for (int c = 0; c < kSeqInput; ++c) slot_ev[c] = seq_input(r[c]);
   seq_head = (seq_head + 1 == S) ? 0 : seq_head + 1;
   if (seq_n < S) ++seq_n;
-  if (o.seq) {  // oldest -> newest, left-padded with zero events (Keras pad_sequences 'pre')
+  if (o.seq_desc) {
+    if (last) {
+      o.seq_desc[i] = (unsigned long long)s | ((unsigned long long)seq_head << 32) | ((unsigned long long)seq_n << 40);
+    } else {
+      o.seq_desc[i] = kSeqMaterialized;
+    }
+  }
+  if (o.seq && !(o.seq_desc && last)) {  // oldest -> newest, left-padded with zero events (Keras pad_sequences 'pre')
     float* so = o.seq + (size_t)i * S * kSeqInput;
     const int pad = S - seq_n;
     for (int q = 0; q < S; ++q) {
@@ -650,7 +663,17 @@ struct BucketArgs {
   const unsigned long long* ovf_key;  // overflow list: key, bucket
   const unsigned* ovf_b;
   unsigned spec;                      // latency batches: region entries read before the fill count (<= kBT, <= C)
+  bool spread;                        // card segments dealt round-robin over the 4 waves (engine option bucket_spread)
 };
+
+// The thread that takes bucket position pos (mod kBT): with `spread`, consecutive positions go to different waves, so
+// a bucket's m < kBT cards are worked by all four SIMDs instead of the first m / 64 waves (the card loop is
+// latency- and f64-issue-bound per wave)
+static_assert(kBT == 256, "spread_pos deals positions over 4 waves of 64");
+__device__ __forceinline__ int first_pos(bool spread) {
+  const int t = (int)threadIdx.x;
+  return spread ? (((t & 63) << 2) | (t >> 6)) : t;
+}
 
 template <int MODE>
 __device__ void process_short(const BucketArgs& a, unsigned s, const unsigned long long* keys, int len) {
@@ -669,7 +692,7 @@ __device__ void process_short(const BucketArgs& a, unsigned s, const unsigned lo
     velocity_step<MODE>(c, rg, a.K, t.ts, t.cents, cw, sw);
     velocity_raw(cw, sw, r);
     emit(a.out, i, r, sw[0], t.o1, t.dv0);
-    if (a.out.S) seq_step(a.out, s, c.flags, i, r);
+    if (a.out.S) seq_step(a.out, s, c.flags, i, r, q == len - 1);
   }
   store_card(h, c);
 }
@@ -816,6 +839,7 @@ __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned lon
         const float4* src = reinterpret_cast<const float4*>(&sm.seqb[(j + 1 + q) * kSeqInput]);
         for (int c = 0; c < kSeqInput / 4; ++c) dst[c] = q < pad ? make_float4(0.f, 0.f, 0.f, 0.f) : src[c];
       }
+      if (a.out.seq_desc) a.out.seq_desc[i] = kSeqMaterialized;
     }
     // carries for the next tile (values read before the barrier, written after it)
     long long nts = 0, nc = 0;
@@ -1001,7 +1025,7 @@ __device__ void process_sorted(const BucketArgs& a, unsigned long long* skeys, i
     bitonic_sort(skeys, N);
   }
   FD_FSTAMP(2);
-  for (int pos = threadIdx.x; pos < m; pos += kBT) {
+  for (int pos = first_pos(a.spread); pos < m; pos += kBT) {
     const unsigned s = (unsigned)(skeys[pos] >> 32);
     if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;  // not the first txn of its card
     int len = 1;
@@ -1175,7 +1199,7 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
     bucket_body<MODE>(a, b, w.keys, w.sm, w.long_list, w.n_long, w.chunk_m);
     return;
   }
-  for (int pos = threadIdx.x; pos < (int)m; pos += kBT) {
+  for (int pos = first_pos(a.spread); pos < (int)m; pos += kBT) {
     const unsigned s = (unsigned)(skeys[pos] >> 32);
     if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;
     int len = 1;
@@ -1693,7 +1717,8 @@ namespace {
 // card updates, pipelined stream) while the slot pass runs ahead
 void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, double* d_raw, float* d_seq,
                     double* d_vel5, hipStream_t stream = nullptr, bool lean = false, int set = 0,
-                    hipEvent_t before_buckets = nullptr, bool compact = false) {
+                    hipEvent_t before_buckets = nullptr, bool compact = false,
+                    unsigned long long* d_seq_desc = nullptr) {
   CardStore& st = e.state;
   CardStore::GroupScratch& g = st.gs[set];
   const hipStream_t s = stream ? stream : e.stream;
@@ -1733,7 +1758,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.K = st.K;
   a.n = n;
   a.prep = g.prep.as<const Prep>();
-  a.out = Outputs{d_vec, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S,
+  a.out = Outputs{d_vec, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S, d_seq_desc,
                   st.mode == FD_WINDOW_SLIDING ? st.sat.as<unsigned long long>() : nullptr, st.K, compact};
   a.fill = g.bucket_fill.as<unsigned>();
   a.pairs = g.pairs.as<const unsigned long long>();
@@ -1743,6 +1768,9 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.ovf_key = g.ovf_key.as<const unsigned long long>();
   a.ovf_b = g.ovf_b.as<const unsigned>();
   // early region reads (latency batches): 4x the mean bucket fill covers the Poisson tail, at most one per thread
+  // spread measured: config 4 (64 k, ~128 keys per bucket: 2 full waves -> 4 half waves) 0.0967 -> 0.0942 ms per
+  // step; config 5 (1 k, 16 keys: 1 wave -> 4 waves of 4 lanes) the card loop 2x slower (profiles/r04/config5)
+  a.spread = st.bucket_spread && n >= 8192;
   a.spec = n < 8192 ? (unsigned)std::min<int64_t>({(int64_t)kBT, (int64_t)C, 4 * ((n + nb - 1) / nb)}) : 0u;
   const size_t lds = kBucketLds;
   if (lean) {
@@ -1764,7 +1792,8 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
 }  // namespace
 
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw, float* d_seq,
-                     double* d_vel5, hipStream_t stream, bool lean, int set, hipEvent_t before_buckets, bool compact) {
+                     double* d_vel5, hipStream_t stream, bool lean, int set, hipEvent_t before_buckets, bool compact,
+                     unsigned long long* d_seq_desc) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
   FD_REQUIRE(d_vec != nullptr, FD_ERR_INVALID_ARG, "null vector output");
@@ -1777,7 +1806,8 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
   TxnSrc src{reinterpret_cast<const unsigned long long*>(t.card_key), reinterpret_cast<const long long*>(t.ts_ms),
              reinterpret_cast<const long long*>(t.amount_cents), reinterpret_cast<const int*>(t.merchant),
              reinterpret_cast<const unsigned long long*>(t.device_fp), t.ip_class, t.hour, t.weekend, nullptr};
-  launch_grouped(e, src, n, d_vec, d_raw, d_seq, d_vel5, stream, lean, set, before_buckets, compact);
+  FD_REQUIRE(d_seq_desc == nullptr || d_seq != nullptr, FD_ERR_INVALID_ARG, "sequence descriptors need the buffer");
+  launch_grouped(e, src, n, d_vec, d_raw, d_seq, d_vel5, stream, lean, set, before_buckets, compact, d_seq_desc);
 }
 
 void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq,

@@ -167,7 +167,9 @@ __device__ __forceinline__ void mfma_abid16(float a, const float* b, f32x4* acc,
 __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ seq, int64_t n, int T,
                                                     const float* __restrict__ wpk4, const float* __restrict__ bias,
                                                     const float* __restrict__ wout, const float* __restrict__ bout,
-                                                    int n_out, double* __restrict__ prob) {
+                                                    int n_out, double* __restrict__ prob,
+                                                    const unsigned long long* __restrict__ desc,
+                                                    const float* __restrict__ ring) {
 #pragma clang fp contract(off)
   // h_t and x_t in the A-operand order: (txn i, k) at lane i + 4 (k & 15), register k >> 4. h_t is stored
   // register-major, [register][lane]: a lane's reads (one word per register) and the cell writes (a wave's 64
@@ -180,6 +182,18 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
   FD_TL(g_tl_lstm, 2, 0);
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
+  const int per = T * kI;  // sequence elements per transaction (<= 256: two staging elements per thread)
+  const int64_t ntiles = (n + 3) / 4;
+  // latency path: the first tile's sequence descriptors are loaded before the weights (vector loads retire in
+  // order, so the ring gather below waits for these alone, and its own loads overlap the weights')
+  unsigned long long dsc[2] = {0ull, 0ull};
+  if (desc != nullptr && blockIdx.x < ntiles) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int idx = tid + 512 * j, r = idx / per;
+      if (idx < 4 * per && (int64_t)blockIdx.x * 4 + r < n) dsc[j] = desc[(int64_t)blockIdx.x * 4 + r];
+    }
+  }
   // B operands: lane l holds W[(l >> 4) * 128 + 16 w + (l & 15)][k] for k = 0..143 (W_ih, then W_hh)
   float bw[kKT];
 #pragma unroll
@@ -190,12 +204,28 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
   const int hr = w & 3, ho = w >> 2;
   const float wo0 = ho < n_out ? wout[ho * kH + l] : 0.f, wo1 = ho < n_out ? wout[ho * kH + 64 + l] : 0.f;
   const float bo = ho < n_out ? bout[ho] : 0.f;
-  const int64_t ntiles = (n + 3) / 4;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t row0 = tile * 4;
-    for (int idx = tid; idx < 4 * T * kI; idx += 512) {
-      const int r = idx / (T * kI), rem = idx - r * (T * kI), t = rem / kI, k = rem - t * kI;
-      xs[t][r + 4 * k] = (row0 + r < n) ? seq[(size_t)(row0 + r) * T * kI + rem] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int idx = tid + 512 * j;
+      if (idx >= 4 * per) break;
+      const int r = idx / per, rem = idx - r * per, t = rem / kI, k = rem - t * kI;
+      float v = 0.f;
+      if (row0 + r < n) {
+        const unsigned long long d = desc == nullptr ? kSeqMaterialized : (tile == blockIdx.x ? dsc[j] : desc[row0 + r]);
+        if (d & kSeqMaterialized) {
+          v = seq[(size_t)(row0 + r) * per + rem];
+        } else {  // the card's ring: oldest -> newest, left-padded with zero events (features.hip seq_step)
+          const int head = (int)((d >> 32) & 0xffu), sn = (int)((d >> 40) & 0xffu), pad = T - sn;
+          if (t >= pad) {
+            int src = head - sn + (t - pad);
+            if (src < 0) src += T;
+            v = ring[((size_t)(unsigned)d * T + src) * kI + k];
+          }
+        }
+      }
+      xs[t][r + 4 * k] = v;
     }
     (&hbuf[0][0][0])[tid] = 0.f;  // 512 threads = 4 x 128
     float c = 0.f, h = 0.f;
@@ -311,7 +341,8 @@ void load_lstm(Engine& e, const fd_lstm_params& p) {
   m.loaded = true;
 }
 
-void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, int T, double* d_prob) {
+void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, int T, double* d_prob,
+                 const unsigned long long* d_desc) {
   const LstmModel& m = e.lstm;
   FD_REQUIRE(m.loaded, FD_ERR_NOT_LOADED, "Model lstm_sequential not loaded");
   FD_REQUIRE(T >= 1 && T <= FD_MAX_SEQ_LEN, FD_ERR_INVALID_ARG, "sequence length must be in [1, 16]");
@@ -321,11 +352,14 @@ void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, i
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_LSTM) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, stream));
   const int rows = e.lstm_rows ? e.lstm_rows : (n < 4096 ? 4 : 16);
+  FD_REQUIRE(d_desc == nullptr || (rows == 4 && e.state.S == T && e.state.seq.ptr), FD_ERR_INVALID_ARG,
+             "internal: sequence descriptors need the 4-row LSTM kernel and the engine's history ring");
   if (rows == 4) {  // one 512-thread workgroup per CU (bw[] holds 144 VGPRs), looping over 4-row tiles
     const int64_t tiles = (n + 3) / 4;
     hipLaunchKernelGGL(lstm_kernel4, dim3((unsigned)std::min<int64_t>(tiles, 256)), dim3(512), 0, stream, d_seq, n,
                        T, m.wpk4.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),
-                       m.bout.as<const float>(), m.n_out, d_prob);
+                       m.bout.as<const float>(), m.n_out, d_prob, d_desc,
+                       d_desc ? e.state.seq.as<const float>() : nullptr);
   } else {
     hipLaunchKernelGGL(lstm_kernel, dim3((unsigned)((n + kRows - 1) / kRows)), dim3(512), 0, stream, d_seq, n, T,
                        m.wpk.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),

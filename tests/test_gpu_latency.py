@@ -1,6 +1,6 @@
 """Latency batches (fd_score_batch_device, < 128 tiles: the tree-split forests, the LSTM on 4-transaction tiles):
-the engine option small_streams (side streams for the LSTM / the second forest) gives the same outputs bit for
-bit, and the split path's per-tile NaN flags are per call (a NaN batch never leaks into the next).
+the engine options small_streams (side streams for the LSTM / the second forest) and seq_ring_lstm give the same
+outputs bit for bit, and the split path's per-tile NaN flags are per call (a NaN batch never leaks into the next).
 Reference chain: FeatureExtractor -> FeatureProcessor -> EnsemblePredictor.predict one micro-batch at a time
 (fl/features/FeatureExtractor.java:50-87, ml/models/ensemble_predictor.py:75-148)."""
 import numpy as np
@@ -138,3 +138,46 @@ def test_latency_fused_pair_matches_per_forest_path(world, strategy):
             assert np.abs(a[0][0] - px).max() <= 1e-5 and np.abs(a[0][1] - pi).max() <= 1e-12
     finally:
         eng.close()
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("users", [50, 3000])
+def test_lstm_ring_sequences_identical(world, users):
+    """Latency batches read each card's last transaction's LSTM sequence from the card's history ring (engine
+    option seq_ring_lstm 1, descriptors from the feature kernel) instead of a materialised copy (0): the same model
+    probabilities and outputs bit for bit, batch after batch — including cards repeated inside a batch (their earlier
+    transactions' sequences materialised), hot cards on the cooperative path (50 users: ~20 transactions per card per
+    batch), short histories (left padding) and ragged batch sizes."""
+    import torch
+    _, _, xgb, ifm = world
+    pop = synth.population(users, 500, seed=70 + users)
+    tx = synth.txn_stream(pop, 6000, seed=71, rate_per_s=50.0)
+    lw = L.random_weights(seed=7)
+    params = _params(True)
+    slots = [0, 1, FD_SLOT_LSTM]
+    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f])).cuda() for f in TXN_FIELDS}
+    engs = [_setup(pop, xgb, ifm, lw) for _ in range(2)]
+    sizes = [1, 1000, 997, 1000, 1024, 1978]
+    try:
+        res = []
+        for v, e in enumerate(engs):
+            e.set_option("seq_ring_lstm", v)
+            e.set_stream(torch.cuda.current_stream().cuda_stream)
+            out, a = [], 0
+            for B in sizes:
+                fp, conf = (torch.empty(B, dtype=torch.float64, device="cuda") for _ in range(2))
+                dec, risk = (torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(2))
+                mp = torch.empty((3, B), dtype=torch.float64, device="cuda")
+                e.score_batch_device(params, slots, {f: t[a:a + B].data_ptr() for f, t in dev.items()}, B,
+                                     fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
+                                     model_probs_ptr=mp.data_ptr())
+                out.append([fp, conf, dec, risk, mp])
+                a += B
+            res.append(out)
+        torch.cuda.synchronize()
+        for b, (x, y) in enumerate(zip(res[1], res[0])):
+            for s, t in zip(x, y):
+                assert np.array_equal(s.cpu().numpy(), t.cpu().numpy()), f"batch {b}"
+    finally:
+        for e in engs:
+            e.close()
