@@ -1156,6 +1156,9 @@ class Config3J(Config3):
             self.ceng = fdengine.FraudEngine(dev.index)
             self.cstream = torch.cuda.Stream(device=dev)
             self.ceng.set_stream(self.cstream.cuda_stream)
+            for kv in args.engine_option:  # --engine-option applies to the codec engine too
+                k, v = kv.split("=")
+                self.ceng.set_option(k.strip(), int(v))
             self.extra_engines = [self.ceng]
             codec_eng = self.ceng
         self.codec = IngestCodec(codec_eng, self.merchant_ids, synth.SIM_PAYMENT_METHODS, synth.SIM_TXN_TYPES,
@@ -1170,10 +1173,14 @@ class Config3J(Config3):
             bufs.append(torch.from_numpy(b.copy()).to(dev))
             offs.append(torch.from_numpy(o).to(dev))
         self.bufs, self.offs = bufs, offs
-        self.csets = [device_columns(self.B, dev.index) for _ in range(2 if self.pipe else 1)]
+        # three column sets: batch i+3's parse reuses batch i's set after its scoring — the parse of i+1 (whose
+        # VALU-bound workgroups fill the CUs' registers, so batch i's feature kernels mostly run after it) and batch
+        # i's scoring then never stall the codec stream (with two sets it idled ~90 us per batch)
+        self.nsets = 3 if self.pipe else 1
+        self.csets = [device_columns(self.B, dev.index) for _ in range(self.nsets)]
         self.cols, self.cptrs = self.csets[0]
-        self.ready = [torch.cuda.Event() for _ in range(2)]
-        self.freed, self.freed_live = [torch.cuda.Event() for _ in range(2)], [False, False]
+        self.ready = [torch.cuda.Event() for _ in range(self.nsets)]
+        self.freed, self.freed_live = [torch.cuda.Event() for _ in range(self.nsets)], [False] * self.nsets
         self.dev_stream = torch.cuda.current_stream(dev)
         B = self.B
         self.fp = torch.empty(B, dtype=torch.float64, device=dev)
@@ -1185,8 +1192,9 @@ class Config3J(Config3):
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
-        self.outs = [[self.fp, self.conf, self.dec, self.risk],
-                     [torch.empty_like(t) for t in (self.fp, self.conf, self.dec, self.risk)]]  # Config3.fetch
+        self.outs = [[self.fp, self.conf, self.dec, self.risk]] + [
+            [torch.empty_like(t) for t in (self.fp, self.conf, self.dec, self.risk)]
+            for _ in range(max(2, self.nsets) - 1)]  # Config3.fetch
         self.scorer = eng.pipelined_scorer(self.params, self.slots)
         self.nbytes = [int(o[-1].item()) for o in offs]
         log(f"[rank {rank}] config3j setup {time.time() - t:.1f}s: {self.cards} cards, capacity {cap}, "
@@ -1206,7 +1214,7 @@ class Config3J(Config3):
                                         self.conf.data_ptr(), self.dec.data_ptr(), self.risk.data_ptr(),
                                         vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
             return
-        k = i & 1
+        k = i % self.nsets
         _, cptrs = self.csets[k]
         if self.freed_live[k]:
             self.cstream.wait_event(self.freed[k])
