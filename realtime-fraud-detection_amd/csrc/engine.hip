@@ -464,6 +464,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "ensemble_owner") {  // fused kernel: 0 owner tree group rotates per chunk; 1 always group 0
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_owner must be 0 or 1");
     e.ens_owner_fixed = value != 0;
+  } else if (k == "ensemble_prio") {  // fused kernel: 1 its waves issue above the co-running feature kernels'
+    // (s_setprio 2); 0 (default) the same priority (config 4: 0.0929 vs 0.0908-0.0918 ms, profiles/r04/prio)
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_prio must be 0 or 1");
+    e.ens_prio = value != 0;
   } else if (k == "ensemble_chunks") {  // fused kernel's chunk layout: 0 auto (compact once the engine has RCCL
     // communicators, else wide), 1 wide (24 / 16 trees), 2 compact (20 / 12: LDS room for an RCCL kernel beside)
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "ensemble_chunks must be 0, 1 or 2");
@@ -501,6 +505,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(value == 0 || (value >= 8 && value <= 512 && (value & (value - 1)) == 0), FD_ERR_INVALID_ARG,
                "bucket_keys must be 0 or a power of two in 8..512");
     e.state.bucket_keys = (int)value;
+  } else if (k == "feature_prio") {  // pipelined stream: 1 the feature kernels' waves issue at priority 2
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "feature_prio must be 0 or 1");
+    e.state.feat_prio = value != 0;
   } else if (k == "bucket_spread") {  // feature bucket pass, >= 8 k transactions: 1 (default) card segments
     // round-robin over the 4 waves
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "bucket_spread must be 0 or 1");

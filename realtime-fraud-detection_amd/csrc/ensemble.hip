@@ -93,6 +93,7 @@ struct EnsArgs {
   int compact;                    // X rows are the compact vector (kCompactWidth floats), binned here
   uint16_t cbin[kMaxFeatures];    // compact mode: the bins of the constant slots (0 or 0.5), per plan
   int owner_fixed;                // chunk owner: tree group 0 (the oldest waves: highest issue priority), else rotating
+  int prio;                       // issue priority 2 above the co-running feature kernels (engine option ensemble_prio)
   int n_pass;
   int pass_f[kMaxPass + 1];
   unsigned long long pass_global;  // bit p: pass p bins from global memory (its table does not fit LDS)
@@ -367,7 +368,7 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
 #endif
   // above the feature kernels of the next micro-batch that share the CU in the pipelined stream (priority 0):
   // this kernel is the stream's critical path, theirs is latency-bound with slack
-  __builtin_amdgcn_s_setprio(2);
+  if (a.prio) __builtin_amdgcn_s_setprio(2);
   int anynan = 0;
   {
     uint16_t* Xs = reinterpret_cast<uint16_t*>(lbase);
@@ -920,6 +921,7 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
   EnsArgs a{};
   plan_args(e.ens, dX, n, compact ? kCompactWidth : ld, e.ens_owner_fixed, a);
   a.compact = compact ? 1 : 0;
+  a.prio = e.ens_prio ? 1 : 0;
   a.pos[0] = pa;
   a.pos[1] = pb;
   a.mcol[0] = ma;
@@ -949,6 +951,7 @@ bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int
   if (!plan_current(e, P, sa, sb, wide) && !build_plan(e, P, sa, sb, wide)) return false;
   EnsArgs a{};
   plan_args(P, dX, n, ld, e.ens_owner_fixed, a);
+  a.prio = e.ens_prio ? 1 : 0;
   a.fp = dprob;
   const hipStream_t saved = e.stream;
   if (stream) e.stream = stream;

@@ -320,6 +320,7 @@ struct CardStore {
   int S = 0;         // LSTM history events per card (0 = off)
   int bucket_keys = 0;  // option "bucket_keys": transactions per bucket workgroup (0 auto, features.hip)
   bool bucket_spread = true;  // option "bucket_spread": a bucket's card segments dealt over all 4 waves
+  bool feat_prio = false;  // option "feature_prio": the pipelined stream's feature kernels issue at priority 2
   int64_t n_merchants = 0;
   DeviceBuffer pages, keys, merchants, err, seq;  // pages: CardPages (header + ring per slot); keys: the compact
                                                   // key array card_slot probes
@@ -475,7 +476,8 @@ struct Engine {
   bool pipe_copy_vec[kPipeSlots] = {};  // that copy also read the slot's vectors (the slot's next features wait)
   int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
-  bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
+  bool seq_ring_lstm = true;
+  bool ens_prio = false;  // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels)  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
   bool compact_vectors = true;  // "compact_vectors": the pipelined stream's compact scoring vectors (engine.hip)
   int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)
   // host-API staging

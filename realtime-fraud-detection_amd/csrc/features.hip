@@ -664,6 +664,7 @@ struct BucketArgs {
   const unsigned* ovf_b;
   unsigned spec;                      // latency batches: region entries read before the fill count (<= kBT, <= C)
   bool spread;                        // card segments dealt round-robin over the 4 waves (engine option bucket_spread)
+  bool prio;                          // issue priority 2 (engine option feature_prio, pipelined stream)
 };
 
 // The thread that takes bucket position pos (mod kBT): with `spread`, consecutive positions go to different waves, so
@@ -1177,6 +1178,7 @@ template <int MODE>
 __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, BucketScratch* scratch) {
   __shared__ __attribute__((aligned(16))) unsigned long long skeys[kLeanCap];
   __shared__ int any_long;
+  if (a.prio) __builtin_amdgcn_s_setprio(2);
   const int b = blockIdx.x;
   const unsigned m = a.fill[b];
   if (threadIdx.x == 0) any_long = 0;
@@ -1771,6 +1773,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   // spread measured: config 4 (64 k, ~128 keys per bucket: 2 full waves -> 4 half waves) 0.0967 -> 0.0942 ms per
   // step; config 5 (1 k, 16 keys: 1 wave -> 4 waves of 4 lanes) the card loop 2x slower (profiles/r04/config5)
   a.spread = st.bucket_spread && n >= 8192;
+  a.prio = lean && st.feat_prio;
   a.spec = n < 8192 ? (unsigned)std::min<int64_t>({(int64_t)kBT, (int64_t)C, 4 * ((n + nb - 1) / nb)}) : 0u;
   const size_t lds = kBucketLds;
   if (lean) {
