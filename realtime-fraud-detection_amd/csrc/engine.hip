@@ -29,6 +29,7 @@ Engine::Timed* Engine::next_event_pair(int kind) {
   }
   Timed* t = &events[events_used++];
   t->kind = kind;
+  t->split = false;
   return t;
 }
 
@@ -335,8 +336,13 @@ int fd_engine_destroy(fd_engine* eng) {
       (void)hipStreamSynchronize(st);
       (void)hipStreamDestroy(st);
     }
+  if (e.pipe_slot_stream) {
+    (void)hipStreamSynchronize(e.pipe_slot_stream);
+    (void)hipStreamDestroy(e.pipe_slot_stream);
+  }
   if (e.pipe_entry_ev) (void)hipEventDestroy(e.pipe_entry_ev);
   for (int k = 0; k < Engine::kPipeSlots; ++k) {
+    if (e.pipe_slot_ev[k]) (void)hipEventDestroy(e.pipe_slot_ev[k]);
     if (e.pipe_feat_ev[k]) (void)hipEventDestroy(e.pipe_feat_ev[k]);
     if (e.pipe_done_ev[k]) (void)hipEventDestroy(e.pipe_done_ev[k]);
     if (e.pipe_copy_ev[k]) (void)hipEventDestroy(e.pipe_copy_ev[k]);
@@ -365,6 +371,8 @@ int fd_engine_destroy(fd_engine* eng) {
   for (auto& ev : e.events) {
     (void)hipEventDestroy(ev.a);
     (void)hipEventDestroy(ev.b);
+    if (ev.c) (void)hipEventDestroy(ev.c);
+    if (ev.d) (void)hipEventDestroy(ev.d);
   }
   if (e.own_stream) (void)hipStreamDestroy(e.own_stream);
   delete eng;
@@ -403,6 +411,7 @@ int fd_engine_sync(fd_engine* eng) {
   if (e.comm.x_fwd) FD_HIP(hipStreamSynchronize(e.comm.x_fwd));
   for (hipStream_t st : e.pipe_stream)
     if (st) FD_HIP(hipStreamSynchronize(st));
+  if (e.pipe_slot_stream) FD_HIP(hipStreamSynchronize(e.pipe_slot_stream));
   if (e.aux_stream) FD_HIP(hipStreamSynchronize(e.aux_stream));
   if (e.aux2_stream) FD_HIP(hipStreamSynchronize(e.aux2_stream));
   fd::route_check(e);
@@ -505,6 +514,13 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(value == 0 || (value >= 8 && value <= 512 && (value & (value - 1)) == 0), FD_ERR_INVALID_ARG,
                "bucket_keys must be 0 or a power of two in 8..512");
     e.state.bucket_keys = (int)value;
+  } else if (k == "slot_stream") {  // fd_score_batch_pipelined: batch i's slot pass on a stream of its own (1 high
+    // priority, 2 low; 0 on pipe_stream[i & 1] behind batch i-2's fused kernel; -1 auto by the card table's size),
+    // set before the first pipelined call
+    FD_REQUIRE(value >= -1 && value <= 2, FD_ERR_INVALID_ARG, "slot_stream must be -1, 0, 1 or 2");
+    FD_REQUIRE(!e.pipe_slot_stream || (int)value == e.pipe_slot_mode, FD_ERR_INVALID_ARG,
+               "slot_stream: set before the first pipelined call");
+    e.pipe_slot_mode = (int)value;
   } else if (k == "feature_prio") {  // pipelined stream: 1 the feature kernels' waves issue at priority 2
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "feature_prio must be 0 or 1");
     e.state.feat_prio = value != 0;
@@ -546,6 +562,11 @@ int fd_timing_read(fd_engine* eng, int kind, double* total_ms, int64_t* launches
     float ms = 0.f;
     FD_HIP(hipEventElapsedTime(&ms, e.events[i].a, e.events[i].b));
     tot += ms;
+    if (e.events[i].split) {
+      FD_HIP(hipEventSynchronize(e.events[i].d));
+      FD_HIP(hipEventElapsedTime(&ms, e.events[i].c, e.events[i].d));
+      tot += ms;
+    }
     ++cnt;
   }
   if (total_ms) *total_ms = tot;
@@ -557,7 +578,10 @@ int fd_timing_reset(fd_engine* eng) {
   FD_API_BEGIN
   FD_ENGINE_LOCK(eng);
   Engine& e = E_quiet(eng);
-  for (size_t i = 0; i < e.events_used; ++i) FD_HIP(hipEventSynchronize(e.events[i].b));  // pairs on 2+ streams
+  for (size_t i = 0; i < e.events_used; ++i) {  // pairs on 2+ streams
+    FD_HIP(hipEventSynchronize(e.events[i].b));
+    if (e.events[i].split) FD_HIP(hipEventSynchronize(e.events[i].d));
+  }
   e.events_used = 0;
   FD_API_END
 }
@@ -980,6 +1004,13 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
                       uint8_t* d_decision, uint8_t* d_risk, void* d_results, void* input_ready) {
   for (int k = 0; k < 2; ++k)
     if (!e.pipe_stream[k]) e.pipe_stream[k] = fd::make_stream(e.stream_prio >= 1 ? 1 : 0);
+  if (e.pipe_slot_mode < 0)  // auto: where the feature chain outlasts the fused kernel (random card traffic over a
+    // large table), not where an earlier slot pass only adds contention beside it
+    e.pipe_slot_mode = (e.state.ready && e.state.cap >= (1ll << 26)) ? 2 : 0;
+  if (e.pipe_slot_mode && !e.pipe_slot_stream) {
+    e.pipe_slot_stream = fd::make_stream(e.pipe_slot_mode == 1 ? 1 : -1);
+    for (int k = 0; k < Engine::kPipeSlots; ++k) FD_HIP(hipEventCreateWithFlags(&e.pipe_slot_ev[k], kStreamEventFlags));
+  }
   if (!e.pipe_entry_ev) {
     FD_HIP(hipEventCreateWithFlags(&e.pipe_entry_ev, kStreamEventFlags));
     for (int k = 0; k < Engine::kPipeSlots; ++k) {
@@ -998,12 +1029,19 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   const int prev = s ^ 1;
   hipStream_t Sc = e.pipe_stream[e.pipe_iter & 1];
   hipStream_t Sf = Sc;
+  // option slot_stream: the slot pass on Ss, after what it reads (the entry order, the inputs) and batch i-2's
+  // bucket pass (scratch set s: its fill counts and keys are consumed and reset there); feat_slot_kernel only
+  // finds / inserts card keys, which the bucket passes of earlier batches never change
+  hipStream_t Ss = e.pipe_slot_stream;
   if (e.pipe_dirty) {  // work queued on e.stream by other calls (state loads, snapshots, ...) comes first
     FD_HIP(hipEventRecord(e.pipe_entry_ev, e.stream));
     FD_HIP(hipStreamWaitEvent(Sf, e.pipe_entry_ev, 0));
+    if (Ss) FD_HIP(hipStreamWaitEvent(Ss, e.pipe_entry_ev, 0));
     e.pipe_dirty = false;
   }
   if (input_ready) FD_HIP(hipStreamWaitEvent(Sf, static_cast<hipEvent_t>(input_ready), 0));
+  if (Ss && input_ready) FD_HIP(hipStreamWaitEvent(Ss, static_cast<hipEvent_t>(input_ready), 0));
+  if (Ss && e.pipe_feat_live[s]) FD_HIP(hipStreamWaitEvent(Ss, e.pipe_feat_ev[s], 0));
   // the slot's vectors are rewritten below: after batch i-nbuf's output copy if that one read them
   if (e.pipe_copy_live[s] && e.pipe_copy_vec[s]) FD_HIP(hipStreamWaitEvent(Sf, e.pipe_copy_ev[s], 0));
   // mode 1: the slot pass (scratch set s & 1, untouched by batch i-1) runs at once; the bucket pass waits for
@@ -1024,10 +1062,18 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
     e.pipe_seq[s].ensure((size_t)n * e.state.S * fd::kSeqInput * sizeof(float));
     seq = e.pipe_seq[s].as<float>();
   }
-  if (records)
-    fd::launch_features_records(e, records, n, vec, seq, Sf, e.pipe_lean, s, before_buckets, compact);
-  else
-    fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, s, before_buckets, compact);
+  {
+    struct SlotPass {  // launch_grouped reads these for this call only
+      Engine& e;
+      ~SlotPass() { e.slot_pass_stream = nullptr, e.slot_pass_ev = nullptr; }
+    } slot_pass{e};
+    e.slot_pass_stream = Ss;
+    e.slot_pass_ev = Ss ? e.pipe_slot_ev[s] : nullptr;
+    if (records)
+      fd::launch_features_records(e, records, n, vec, seq, Sf, e.pipe_lean, s, before_buckets, compact);
+    else
+      fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, s, before_buckets, compact);
+  }
   FD_HIP(hipEventRecord(e.pipe_feat_ev[s], Sf));
   e.pipe_feat_live[s] = true;
   // scoring paths other than the fused kernel share engine scratch (per-model columns, tree-split and LSTM

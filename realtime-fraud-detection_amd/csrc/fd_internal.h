@@ -463,6 +463,16 @@ struct Engine {
   hipEvent_t pipe_entry_ev = nullptr, pipe_feat_ev[kPipeSlots] = {}, pipe_done_ev[kPipeSlots] = {};
   bool pipe_feat_live[kPipeSlots] = {}, pipe_done_live[kPipeSlots] = {};
   bool pipe_dirty = true;  // another engine call since the last pipelined one: order after `stream` first
+  // option "slot_stream" (0 off, 1 high-priority stream, 2 low): batch i's slot pass on a stream of its own, so it
+  // does not queue behind batch i-2's fused kernel on pipe_stream[i & 1]; its bucket pass waits for it by event.
+  // -1 (default) auto: 2 when the card table has >= 2^26 slots, else 0. Config 4 (2^27 slots): 0.0915 -> 0.0897 ms
+  // per step at 2 (1: 0.0906); config 3 (10 M cards): 0.0876 -> 0.0948
+  int pipe_slot_mode = -1;
+  hipStream_t pipe_slot_stream = nullptr;
+  hipEvent_t pipe_slot_ev[kPipeSlots] = {};
+  // launch_grouped's slot pass goes to this stream (then an event the bucket pass's stream waits for) while set
+  hipStream_t slot_pass_stream = nullptr;
+  hipEvent_t slot_pass_ev = nullptr;
   unsigned long long pipe_iter = 0;
   unsigned long long pipe_iter_total = 0;  // counter "pipelined_batches"
   bool pipe_lean = true;   // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
@@ -501,6 +511,10 @@ struct Engine {
   struct Timed {
     hipEvent_t a, b;
     int kind;
+    // a launch split over two streams (the pipelined slot pass on its own stream, then the bucket pass): its
+    // second part is c..d, the launch's time the sum of both (the wait between them excluded)
+    hipEvent_t c = nullptr, d = nullptr;
+    bool split = false;
   };
   std::vector<Timed> events;  // pool
   size_t events_used = 0;

@@ -1737,16 +1737,31 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   g.ovf_b.ensure((size_t)n * 4);
   const int par = g.batch_parity;
   g.batch_parity ^= 1;
+  // the slot pass on the engine's slot stream when the pipelined step set one (option slot_stream), else on s
+  const hipStream_t ss = e.slot_pass_stream ? e.slot_pass_stream : s;
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
-  if (ev) FD_HIP(hipEventRecord(ev->a, s));
+  if (ev) FD_HIP(hipEventRecord(ev->a, ss));
   hipLaunchKernelGGL(feat_slot_kernel, dim3((unsigned)((n + kST - 1) / kST)), dim3(kST), 2 * nb * sizeof(unsigned),
-                     s, st.view(), st.keys.as<unsigned long long>(), (long long)(st.cap - 1), n, src,
+                     ss, st.view(), st.keys.as<unsigned long long>(), (long long)(st.cap - 1), n, src,
                      st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, C, g.slot.as<unsigned>(),
                      g.prep.as<Prep>(), g.bucket_fill.as<unsigned>(), g.pairs.as<unsigned long long>(),
                      g.ovf_cnt.as<unsigned>() + par, g.ovf_key.as<unsigned long long>(), g.ovf_b.as<unsigned>(),
                      st.err.as<unsigned>());
   FD_HIP(hipGetLastError());
+  if (ss != s) {
+    FD_HIP(hipEventRecord(e.slot_pass_ev, ss));
+    FD_HIP(hipStreamWaitEvent(s, e.slot_pass_ev, 0));
+  }
   if (before_buckets) FD_HIP(hipStreamWaitEvent(s, before_buckets, 0));
+  if (ev && ss != s) {  // timed in two parts: the slot pass on ss, the bucket pass from here on s
+    if (!ev->c) {
+      FD_HIP(hipEventCreateWithFlags(&ev->c, hipEventDisableSystemFence));
+      FD_HIP(hipEventCreateWithFlags(&ev->d, hipEventDisableSystemFence));
+    }
+    FD_HIP(hipEventRecord(ev->b, ss));
+    FD_HIP(hipEventRecord(ev->c, s));
+    ev->split = true;
+  }
   static bool attrs = false;
   if (!attrs) {  // > 48 KiB of dynamic LDS
     FD_HIP(hipFuncSetAttribute((const void*)feat_bucket_kernel<FD_WINDOW_SLIDING>,
@@ -1789,7 +1804,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
     hipLaunchKernelGGL(feat_bucket_kernel<FD_WINDOW_REDIS_COMPAT>, dim3(nb), dim3(kBT), lds, s, a);
   }
   FD_HIP(hipGetLastError());
-  if (ev) FD_HIP(hipEventRecord(ev->b, s));
+  if (ev) FD_HIP(hipEventRecord(ev->split ? ev->d : ev->b, s));
 }
 
 }  // namespace

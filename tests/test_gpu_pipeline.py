@@ -56,7 +56,7 @@ def world():
     return pop, tx, xgb, ifm
 
 
-def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1):
+def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1, slot_stream=0):
     import torch
     pop, tx, xgb, ifm = world
     params = _params()
@@ -69,6 +69,7 @@ def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1):
     torch.cuda.synchronize()
     ref, pip = _setup(pop, xgb, ifm), _setup(pop, xgb, ifm)
     pip.set_option("pipeline_lean", lean)
+    pip.set_option("slot_stream", slot_stream)
     try:
         for e in (ref, pip):
             e.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -110,15 +111,17 @@ def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("lean", [1, 0])
-def test_pipelined_stream_matches_serial(world, lean):
-    _run(world, [0, 40000, 80000, 81000, 121000, 161000, 201000, 241000], lean=lean)
+@pytest.mark.parametrize("lean,slot_stream", [(1, 0), (0, 0), (1, 1), (1, 2)])
+def test_pipelined_stream_matches_serial(world, lean, slot_stream):
+    """slot_stream 1 / 2: every batch's slot pass on the engine's slot stream (high / low priority)"""
+    _run(world, [0, 40000, 80000, 81000, 121000, 161000, 201000, 241000], lean=lean, slot_stream=slot_stream)
 
 
 @pytest.mark.timeout(300)
-def test_pipelined_hot_cards_and_events(world):
+@pytest.mark.parametrize("slot_stream", [0, 1])
+def test_pipelined_hot_cards_and_events(world, slot_stream):
     """hot-card buckets with inputs behind input_ready events"""
-    _run(world, [0, 40000, 80000, 120000, 160000], hot=True, side_stream=True)
+    _run(world, [0, 40000, 80000, 120000, 160000], hot=True, side_stream=True, slot_stream=slot_stream)
 
 
 @pytest.mark.timeout(300)
@@ -128,8 +131,9 @@ def test_pipelined_hot_cards_deferred_buckets(world):
 
 
 @pytest.mark.timeout(300)
-def test_pipelined_with_interleaved_calls(world):
-    _run(world, [0, 40000, 80000, 120000], interleave=True)
+@pytest.mark.parametrize("slot_stream", [0, 1])
+def test_pipelined_with_interleaved_calls(world, slot_stream):
+    _run(world, [0, 40000, 80000, 120000], interleave=True, slot_stream=slot_stream)
 
 
 @pytest.mark.timeout(300)
