@@ -58,10 +58,11 @@ def _batches(streams, sizes, r):
     return out
 
 
-def _engine(pop, owned, xgb, ifm):
+def _engine(pop, owned, xgb, ifm, slot_stream=-1):
     from fdengine import FraudEngine
     U, M = pop["users"], pop["merchants"]
     e = FraudEngine(0)
+    e.set_option("slot_stream", slot_stream)  # -1 auto: off at this table size; 2 as config 4 runs it
     e.state_init(4 * N_USERS + 4096, 1, 16)
     e.load_users(U["key"][owned], U["avg_amount"][owned], U["account_age_days"][owned], U["device_fp"][owned])
     e.load_merchants(M["fraud_rate"], M["risk_multiplier"])
@@ -80,7 +81,7 @@ def _prefetch_plan(s, parts):
     return parts[s + 1]
 
 
-def _run_ranks(world):
+def _run_ranks(world, slot_stream=-1):
     import torch
 
     from fdengine import FraudEngine
@@ -90,7 +91,7 @@ def _run_ranks(world):
     pop, streams, sizes, xgb, ifm = _setup(world)
     path = str(LOOPBACK)
     ids = (FraudEngine.comm_unique_id(path), FraudEngine.comm_unique_id(path))
-    engines = [_engine(pop, owned_mask(pop["users"]["key"], r, world), xgb, ifm) for r in range(world)]
+    engines = [_engine(pop, owned_mask(pop["users"]["key"], r, world), xgb, ifm, slot_stream) for r in range(world)]
     dev = [[{f: torch.from_numpy(np.ascontiguousarray(b[f])).cuda() for f in TXN_FIELDS}
             for b in _batches(streams, sizes, r)] for r in range(world)]
     torch.cuda.synchronize()
@@ -176,11 +177,12 @@ def _oracle(pop, streams, sizes, xgb, ifm, world):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world", [2, 4])
-def test_native_sharded_step_loopback_matches_oracle(world):
+@pytest.mark.parametrize("world,slot_stream", [(2, -1), (4, -1), (2, 2), (4, 2)])
+def test_native_sharded_step_loopback_matches_oracle(world, slot_stream):
+    """slot_stream 2: the owner pipeline's slot pass on its own stream, as the config-4 card table runs it"""
     from fdengine.engine import shard_of
     assert LOOPBACK.exists(), "tests/native/build/librccl_loopback.so missing (fdengine/build.py build_test_libs)"
-    pop, streams, sizes, xgb, ifm, results, wrong_id = _run_ranks(world)
+    pop, streams, sizes, xgb, ifm, results, wrong_id = _run_ranks(world, slot_stream)
     for r in range(world):
         assert wrong_id[r] is not None and "not the prefetched batch" in wrong_id[r], wrong_id[r]
     # split sizes: every rank's send counts are its batch's owner histogram; receive = the peers' sends to it
