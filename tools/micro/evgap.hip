@@ -1,5 +1,5 @@
 // Stream-gap microbenchmark (tools/micro/evgap.hip): the time from one kernel's end to the next kernel's start on
-// the same stream, with nothing between them, a hipEventRecord, a hipStreamWaitEvent on an event that completed
+// the same stream, with nothing between them, a hipEventRecord (with / without the system-scope fence), a hipStreamWaitEvent on an event that completed
 // long before, or stream memory operations (hipStreamWriteValue32 / hipStreamWaitValue32 already satisfied).
 // Kernel A spins ~40 us on the GPU's 100 MHz clock and stamps its end; kernel B stamps its start (one thread each,
 // vector stores). Build: hipcc --offload-arch=gfx950 -O2 tools/micro/evgap.hip -o tools/micro/evgap
@@ -39,20 +39,22 @@ int main() {
   hipStream_t s, o;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&o, hipStreamNonBlocking));
-  hipEvent_t ev, done;
+  hipEvent_t ev, evnf, done;
   CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  CK(hipEventCreateWithFlags(&evnf, hipEventDisableTiming | hipEventDisableSystemFence));
   CK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
   CK(hipEventRecord(done, o));  // completes at once: "a wait on an event that completed long before"
   CK(hipStreamSynchronize(o));
   const char* names[] = {"nothing", "hipEventRecord", "hipStreamWaitEvent (done)", "hipStreamWriteValue32",
-                         "hipStreamWaitValue32 (satisfied)"};
-  for (int variant = 0; variant < 5; ++variant) {
+                         "hipStreamWaitValue32 (satisfied)", "hipEventRecord (no system fence)"};
+  for (int variant = 0; variant < 6; ++variant) {
     for (int r = 0; r < reps; ++r) {
       hipLaunchKernelGGL(spin_end, dim3(1), dim3(64), 0, s, d, r, 4000ull);  // 40 us
       if (variant == 1) CK(hipEventRecord(ev, s));
       if (variant == 2) CK(hipStreamWaitEvent(s, done, 0));
       if (variant == 3) CK(hipStreamWriteValue32(s, flag, (uint32_t)r + 1, 0));
       if (variant == 4) CK(hipStreamWaitValue32(s, flag + 4, 0, hipStreamWaitValueGte, 0xffffffffu));
+      if (variant == 5) CK(hipEventRecord(evnf, s));
       hipLaunchKernelGGL(stamp_start, dim3(1), dim3(64), 0, s, d, r);
     }
     CK(hipStreamSynchronize(s));
