@@ -514,6 +514,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(value == 0 || (value >= 8 && value <= 512 && (value & (value - 1)) == 0), FD_ERR_INVALID_ARG,
                "bucket_keys must be 0 or a power of two in 8..512");
     e.state.bucket_keys = (int)value;
+  } else if (k == "slot_gather") {  // batches of <= 4096 transactions outside the pipelined stream: card slots found
+    // inside the bucket kernel, no slot launch (1, default) / the slot kernel first (0)
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "slot_gather must be 0 or 1");
+    e.state.slot_gather = value != 0;
   } else if (k == "slot_stream") {  // fd_score_batch_pipelined: batch i's slot pass on a stream of its own (1 high
     // priority, 2 low; 0 on pipe_stream[i & 1] behind batch i-2's fused kernel; -1 auto by the card table's size),
     // set before the first pipelined call

@@ -320,6 +320,9 @@ struct CardStore {
   int S = 0;         // LSTM history events per card (0 = off)
   int bucket_keys = 0;  // option "bucket_keys": transactions per bucket workgroup (0 auto, features.hip)
   bool bucket_spread = true;  // option "bucket_spread": a bucket's card segments dealt over all 4 waves
+  // option "slot_gather": batches of <= 4096 transactions outside the pipelined stream find their card slots inside
+  // the bucket kernel (each bucket workgroup takes the keys that hash to it), no slot launch (features.hip)
+  bool slot_gather = true;
   bool feat_prio = false;  // option "feature_prio": the pipelined stream's feature kernels issue at priority 2
   int64_t n_merchants = 0;
   DeviceBuffer pages, keys, merchants, err, seq;  // pages: CardPages (header + ring per slot); keys: the compact

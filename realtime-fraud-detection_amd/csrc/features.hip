@@ -667,6 +667,27 @@ struct BucketArgs {
   bool prio;                          // issue priority 2 (engine option feature_prio, pipelined stream)
 };
 
+// gather (latency batches, n <= kChunkCap, engine option slot_gather; feat_bucket_gather_kernel): no slot launch;
+// bucket b takes the transactions whose key hashes to it (gather_bucket), finds / inserts their card slots, writes
+// their prep records and slots, then runs the same sorted card pass. Its own argument block, so the other bucket
+// kernels' arguments (and registers) do not grow.
+struct GatherArgs {
+  unsigned nbm;
+  TxnSrc src;
+  unsigned long long* keys;
+  long long mask;
+  const Merchant* merchants;
+  int nm;
+  Prep* prep_w;
+  unsigned* slot;
+  unsigned* err;
+};
+
+// a card's bucket in gather mode: every transaction of a card in one bucket, buckets filled evenly
+__device__ __forceinline__ unsigned gather_bucket(unsigned long long key, unsigned nbm) {
+  return (unsigned)(mix64(key ^ 0x9E3779B97F4A7C15ull) >> 32) & nbm;
+}
+
 // The thread that takes bucket position pos (mod kBT): with `spread`, consecutive positions go to different waves, so
 // a bucket's m < kBT cards are worked by all four SIMDs instead of the first m / 64 waves (the card loop is
 // latency- and f64-issue-bound per wave)
@@ -1053,11 +1074,64 @@ __device__ void process_sorted(const BucketArgs& a, unsigned long long* skeys, i
   }
 }
 
-template <int MODE>
+template <int MODE, bool GATHER = false>
 __device__ void bucket_body(const BucketArgs& a, const int b, unsigned long long* skeys, LongLds& sm, int* long_list,
-                            int& n_long, int& chunk_m) {
+                            int& n_long, int& chunk_m, const GatherArgs* ga = nullptr) {
   unsigned* bins = reinterpret_cast<unsigned*>(skeys + kChunkCap);
   FD_FSTAMP(0);
+  if (GATHER) {  // n <= kChunkCap: this bucket's keys always fit the LDS pass
+    if (threadIdx.x == 0) chunk_m = 0;
+    __syncthreads();
+    const GatherArgs& g = *ga;
+    // phase 1: every key of the batch in flight at once (kChunkCap / kBT per thread), this bucket's indices listed
+    constexpr int kPer = kChunkCap / kBT;
+    unsigned long long kk[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int64_t i = threadIdx.x + (int64_t)r * kBT;
+      kk[r] = i < a.n ? g.src.get_key(i) : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int64_t i = threadIdx.x + (int64_t)r * kBT;
+      if (i < a.n && gather_bucket(kk[r], g.nbm) == (unsigned)b) skeys[atomicAdd(&chunk_m, 1)] = (unsigned long long)i;
+    }
+    if (threadIdx.x == 0) n_long = 0;  // phase 2's "a probe failed" flag (process_sorted resets it)
+    __syncthreads();
+    // phase 2: one listed transaction per thread: card slot (find-or-insert), prep record, its (slot, index) key in
+    // the list position it came from
+    const int m = chunk_m;
+    for (int j = threadIdx.x; j < m; j += kBT) {
+      const unsigned i = (unsigned)skeys[j];
+      const Txn t = g.src.get(i);  // in flight with the probe
+      const long long s = card_slot(g.keys, a.P, g.mask, g.src.get_key(i));
+      store_prep(g.prep_w + i, make_prep(t, g.merchants, g.nm));
+      if (s < 0) {  // table full: the batch fails (err), the key leaves the list below
+        atomicOr(g.err, 1u);
+        g.slot[i] = 0xffffffffu;
+        skeys[j] = ~0ull;
+        n_long = 1;
+        continue;
+      }
+      g.slot[i] = (unsigned)s;
+      skeys[j] = ((unsigned long long)s << 32) | (unsigned long long)i;
+    }
+    __threadfence_block();  // the prep records above are read back by other threads of this workgroup
+    __syncthreads();
+    if (n_long) {  // rare: compact the failed probes out (one thread; then every thread sees the new count)
+      if (threadIdx.x == 0) {
+        int w = 0;
+        for (int j = 0; j < m; ++j)
+          if (skeys[j] != ~0ull) skeys[w++] = skeys[j];
+        chunk_m = w;
+      }
+      __syncthreads();
+    }
+    process_sorted<MODE>(a, skeys, chunk_m, sm, long_list, &n_long);
+    __syncthreads();
+    if (threadIdx.x == 0 && b == 0) a.ovf_cnt[a.par ^ 1] = 0u;  // as below: the next batch's overflow list
+    return;
+  }
   const unsigned long long* src = a.pairs + (size_t)b * a.C;
   // latency batches: the region's first `spec` entries are read in the same round trip as the fill count (stale
   // entries past it are dropped below), not after it
@@ -1156,6 +1230,18 @@ __global__ void __launch_bounds__(kBT) feat_bucket_kernel(BucketArgs a) {
   __shared__ int n_long, chunk_m;
   FD_TL(g_tl_feat, 1, 0);
   bucket_body<MODE>(a, blockIdx.x, skeys, sm, long_list, n_long, chunk_m);
+  FD_TL(g_tl_feat, 1, 3);
+}
+
+// The same with the slot pass folded in (BucketArgs::gather; a kernel of its own so the others keep their registers)
+template <int MODE>
+__global__ void __launch_bounds__(kBT) feat_bucket_gather_kernel(BucketArgs a, GatherArgs g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long skeys[];
+  __shared__ LongLds sm;
+  __shared__ int long_list[kChunkCap / (kSegLong + 1) + 1];
+  __shared__ int n_long, chunk_m;
+  FD_TL(g_tl_feat, 1, 0);
+  bucket_body<MODE, true>(a, blockIdx.x, skeys, sm, long_list, n_long, chunk_m, &g);
   FD_TL(g_tl_feat, 1, 3);
 }
 
@@ -1739,9 +1825,11 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   g.batch_parity ^= 1;
   // the slot pass on the engine's slot stream when the pipelined step set one (option slot_stream), else on s
   const hipStream_t ss = e.slot_pass_stream ? e.slot_pass_stream : s;
+  // latency batches: the slot pass inside the bucket kernel (no slot launch; its probes in the card loop's launch)
+  const bool gather = st.slot_gather && !lean && n <= (int64_t)kChunkCap && ss == s;
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, ss));
-  hipLaunchKernelGGL(feat_slot_kernel, dim3((unsigned)((n + kST - 1) / kST)), dim3(kST), 2 * nb * sizeof(unsigned),
+  if (!gather) hipLaunchKernelGGL(feat_slot_kernel, dim3((unsigned)((n + kST - 1) / kST)), dim3(kST), 2 * nb * sizeof(unsigned),
                      ss, st.view(), st.keys.as<unsigned long long>(), (long long)(st.cap - 1), n, src,
                      st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, C, g.slot.as<unsigned>(),
                      g.prep.as<Prep>(), g.bucket_fill.as<unsigned>(), g.pairs.as<unsigned long long>(),
@@ -1768,6 +1856,10 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLds));
     FD_HIP(hipFuncSetAttribute((const void*)feat_bucket_kernel<FD_WINDOW_REDIS_COMPAT>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLds));
+    FD_HIP(hipFuncSetAttribute((const void*)feat_bucket_gather_kernel<FD_WINDOW_SLIDING>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLds));
+    FD_HIP(hipFuncSetAttribute((const void*)feat_bucket_gather_kernel<FD_WINDOW_REDIS_COMPAT>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLds));
     attrs = true;
   }
   BucketArgs a{};
@@ -1790,6 +1882,18 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.spread = st.bucket_spread && n >= 8192;
   a.prio = lean && st.feat_prio;
   a.spec = n < 8192 ? (unsigned)std::min<int64_t>({(int64_t)kBT, (int64_t)C, 4 * ((n + nb - 1) / nb)}) : 0u;
+  GatherArgs ga{};
+  if (gather) {
+    ga.nbm = nb - 1;
+    ga.src = src;
+    ga.keys = st.keys.as<unsigned long long>();
+    ga.mask = (long long)(st.cap - 1);
+    ga.merchants = st.merchants.as<const Merchant>();
+    ga.nm = (int)st.n_merchants;
+    ga.prep_w = g.prep.as<Prep>();
+    ga.slot = g.slot.as<unsigned>();
+    ga.err = st.err.as<unsigned>();
+  }
   const size_t lds = kBucketLds;
   if (lean) {
     st.bucket_scr.ensure((size_t)nb * sizeof(BucketScratch));
@@ -1798,6 +1902,11 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
       hipLaunchKernelGGL(feat_bucket_lean_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), 0, s, a, scr);
     else
       hipLaunchKernelGGL(feat_bucket_lean_kernel<FD_WINDOW_REDIS_COMPAT>, dim3(nb), dim3(kBT), 0, s, a, scr);
+  } else if (gather) {
+    if (st.mode == FD_WINDOW_SLIDING)
+      hipLaunchKernelGGL(feat_bucket_gather_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), lds, s, a, ga);
+    else
+      hipLaunchKernelGGL(feat_bucket_gather_kernel<FD_WINDOW_REDIS_COMPAT>, dim3(nb), dim3(kBT), lds, s, a, ga);
   } else if (st.mode == FD_WINDOW_SLIDING) {
     hipLaunchKernelGGL(feat_bucket_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), lds, s, a);
   } else {

@@ -181,3 +181,48 @@ def test_lstm_ring_sequences_identical(world, users):
     finally:
         for e in engs:
             e.close()
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("users", [50, 3000])
+def test_slot_gather_identical(world, users):
+    """Batches of <= 4096 transactions find their card slots inside the bucket kernel (engine option slot_gather 1:
+    each bucket workgroup takes the keys that hash to it, no slot launch) instead of the slot kernel first (0): the
+    same outputs bit for bit, batch after batch, and the same card state after them (the next batch's vectors) —
+    hot cards (50 users: ~80 transactions per card per 4 k batch), new cards inserted inside the bucket kernel,
+    a batch of 1, the 4096 limit and one past it."""
+    import torch
+    _, _, xgb, ifm = world
+    pop = synth.population(users, 500, seed=90 + users)
+    tx = synth.txn_stream(pop, 16000, seed=91, rate_per_s=50.0)
+    lw = L.random_weights(seed=7)
+    params = _params(True)
+    slots = [0, 1, FD_SLOT_LSTM]
+    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f])).cuda() for f in TXN_FIELDS}
+    engs = [_setup(pop, xgb, ifm, lw) for _ in range(2)]
+    sizes = [1, 1000, 997, 4096, 4097, 1024]
+    try:
+        res = []
+        for v, e in enumerate(engs):
+            e.set_option("slot_gather", v)
+            e.set_stream(torch.cuda.current_stream().cuda_stream)
+            out, a = [], 0
+            for B in sizes:
+                fp, conf = (torch.empty(B, dtype=torch.float64, device="cuda") for _ in range(2))
+                dec, risk = (torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(2))
+                mp = torch.empty((3, B), dtype=torch.float64, device="cuda")
+                e.score_batch_device(params, slots, {f: t[a:a + B].data_ptr() for f, t in dev.items()}, B,
+                                     fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
+                                     model_probs_ptr=mp.data_ptr())
+                out.append([fp, conf, dec, risk, mp])
+                a += B
+            res.append(out)
+        torch.cuda.synchronize()
+        for b, (x, y) in enumerate(zip(res[1], res[0])):
+            for s, t in zip(x, y):
+                assert np.array_equal(s.cpu().numpy(), t.cpu().numpy()), f"batch {b}"
+        nxt = {k: v[sum(sizes):sum(sizes) + 2000] for k, v in tx.items()}
+        np.testing.assert_array_equal(engs[1].features(nxt), engs[0].features(nxt))
+    finally:
+        for e in engs:
+            e.close()
