@@ -471,6 +471,7 @@ class Config3:
         from fdengine import _native as N
         from fdengine import synth
         self.np, self.torch, self.N = np, torch, N
+        self.args = args
         self.B, self.T, self.D = args.batch, args.trees, args.depth
         self.cards, self.mode, self.K = args.cards, (1 if args.window == "sliding" else 0), args.ring_k
         self.eng = eng
@@ -662,8 +663,11 @@ class Config5(Config3):
                 "note": "latency-bound 1k batch; f32 MFMA = reference fp32 precision"}
 
     def counter_groups(self, roof):
-        return {"features": (["fd::anon::feat_slot_kernel", "fd::anon::feat_bucket_kernel<1>"], "features"),
-                "lstm_head": ([LSTM4_SYMBOL], "lstm_head")}
+        # batches of <= 4096 transactions: the slot pass runs inside the bucket launch (engine option slot_gather)
+        gather = self.B <= 4096 and "slot_gather=0" not in [kv.replace(" ", "") for kv in self.args.engine_option]
+        feats = (["fd::anon::feat_bucket_gather_kernel<1>"] if gather
+                 else ["fd::anon::feat_slot_kernel", "fd::anon::feat_bucket_kernel<1>"])
+        return {"features": (feats, "features"), "lstm_head": ([LSTM4_SYMBOL], "lstm_head")}
 
     def config(self, world):
         c = super().config(world)

@@ -15,7 +15,8 @@ import re
 import sys
 from collections import defaultdict
 
-KEEP = ("ensemble_kernel", "feat_slot_kernel", "feat_bucket_lean_kernel", "feat_bucket_kernel", "lstm_kernel4",
+KEEP = ("ensemble_kernel", "feat_slot_kernel", "feat_bucket_lean_kernel", "feat_bucket_kernel", "feat_bucket_gather_kernel",
+        "lstm_kernel4",
         "lstm_kernel", "split_walk_kernel", "split_sum_kernel", "split_bin_pair_kernel", "pipe_out_copy_kernel",
         "split_walk_pair_kernel", "split_sum_pair_blend_kernel",
         "ingest_json_kernel", "forest_kernel6", "blend_kernel", "route_")
