@@ -509,8 +509,8 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(!e.pipe_stream[0] && !e.comm.x_fwd, FD_ERR_INVALID_ARG,
                "stream_priority: set before the first pipelined call and fd_comm_init");
     e.stream_prio = (int)value;
-  } else if (k == "bucket_keys") {  // feature bucket pass: transactions per bucket workgroup, 0 auto (16 below
-    // 8192 transactions, else 128), else a power of two in 8..512
+  } else if (k == "bucket_keys") {  // feature bucket pass: transactions per bucket workgroup, 0 auto (8 up to
+    // 2048 transactions, 16 below 8192, else 128), else a power of two in 8..512
     FD_REQUIRE(value == 0 || (value >= 8 && value <= 512 && (value & (value - 1)) == 0), FD_ERR_INVALID_ARG,
                "bucket_keys must be 0 or a power of two in 8..512");
     e.state.bucket_keys = (int)value;
