@@ -42,7 +42,7 @@ def test_ensemble_and_lean_bucket_share_a_simd(res):
 
 @pytest.mark.parametrize("parts", [("ensemble_kernelILi8E",), ("feat_slot_kernel",), ("feat_bucket_lean_kernel",),
                                    ("split_walk_pair_kernel",), ("split_sum_pair_blend_kernel",),
-                                   ("lstm_kernel4",)])
+                                   ("lstm_kernel4",), ("feat_bucket_gather_kernel",)])
 def test_hot_kernels_do_not_spill(res, parts):
     for name, v in _find(res, *parts).items():
         assert v["scratch"] == 0, f"{name} spills {v['scratch']} B/lane"
