@@ -218,6 +218,44 @@ def product_blend(names):
 _HIP = None
 
 
+def _parity_record(batches, path, rows_per_batch):
+    """the parity_vs_oracle record: the timed path's batches (no vectors requested) and the vectors-requested twin"""
+    def leg():
+        return {"rows": 0, "max_abs_prob_diff": 0.0, "max_abs_conf_diff": 0.0, "prob_exact_rows": 0,
+                "decision_mismatches": 0, "risk_mismatches": 0, "decision_mismatches_off_threshold": 0}
+    twin = dict(leg(), vector_mismatched_elements=0, vector_max_ulp=0, max_abs_model_prob_diff=0.0)
+    return {"batches_checked": batches, "rows_per_batch": rows_per_batch, "path": path, "timed_path": leg(),
+            "twin": twin, "bar": "fraud_prob / confidence within 1e-5 (north star), decision / risk exact (off a "
+                                 "decision threshold by more than 1e-6)"}
+
+
+def _parity_compare(rec, got, ref):
+    """fraud_prob, confidence, decision, risk of one batch against the oracle chain's"""
+    import numpy as np
+    gfp, gconf, gdec, grisk = got
+    fp, conf, dec, risk = ref
+    rec["rows"] += len(fp)
+    rec["max_abs_prob_diff"] = max(rec["max_abs_prob_diff"], float(np.abs(gfp - fp).max()) if len(fp) else 0.0)
+    rec["max_abs_conf_diff"] = max(rec["max_abs_conf_diff"], float(np.abs(gconf - conf).max()) if len(fp) else 0.0)
+    rec["prob_exact_rows"] += int((gfp == fp).sum())
+    bad = gdec != dec
+    rec["decision_mismatches"] += int(bad.sum())
+    rec["risk_mismatches"] += int((grisk != risk).sum())
+    near = np.abs(conf - 0.7) < 1e-6  # an f32 sigmoid an ulp from the oracle's may cross a threshold
+    for thr in (0.6, 0.8, 0.95):
+        near |= np.abs(fp - thr) < 1e-6
+    rec["decision_mismatches_off_threshold"] += int((bad & ~near).sum())
+
+
+def _parity_vectors(rec, V, rvec):
+    import numpy as np
+    diff = V != rvec
+    rec["vector_mismatched_elements"] += int(diff.sum())
+    if diff.any():
+        ulp = np.abs(V.view(np.int32)[diff].astype(np.int64) - rvec.view(np.int32)[diff].astype(np.int64))
+        rec["vector_max_ulp"] = max(rec["vector_max_ulp"], int(ulp.max()))
+
+
 def hip_memcpy_async(dst: int, src: int, nbytes: int, kind: int, stream: int) -> None:
     """hipMemcpyAsync on `stream` (the process's HIP runtime: torch's libamdhip64, loaded globally by fdengine);
     kind 1 host -> device, 2 device -> host. Straight to the runtime: torch's copy_ between pinned and device memory
@@ -498,7 +536,7 @@ class Config3:
         U, M = self.pop["users"], self.pop["merchants"]
         eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
         eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
-        self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches \
+        self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches + 1 \
             + args.loaded_iters + args.timing_steps + 1
         self.tx = synth.txn_stream(self.pop, self.n_batches * self.B, seed=200 + rank)
         self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
@@ -513,9 +551,8 @@ class Config3:
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
-        # after the parity batches (which need the vectors): the pipelined stream, outputs alternating two sets
-        self.pipe, self.parity_done, self.cur = ((self.pipelined_default or args.pipeline) and not args.no_pipeline,
-                                                 False, 0)
+        # the pipelined stream (parity batches included: they run the timed path), outputs alternating two sets
+        self.pipe, self.cur = (self.pipelined_default or args.pipeline) and not args.no_pipeline, 0
         self.outs = [[self.fp, self.conf, self.dec, self.risk],
                      [torch.empty_like(t) for t in (self.fp, self.conf, self.dec, self.risk)]]
         self.scorer = eng.pipelined_scorer(self.params, self.slots)
@@ -530,19 +567,25 @@ class Config3:
             self._base = {f: (t.data_ptr(), self.B * self.elem[f]) for f, t in self.dev.items()}
         return {f: p + b * w for f, (p, w) in self._base.items()}
 
-    def step(self, i):
+    def step(self, i, vectors=False):
+        """One micro-batch through the product path the timed region runs: the pipelined stream (config 3; the fused
+        kernel reads the compact 24-float vectors) or fd_score_batch_device per step (config 5). vectors: also ask
+        for the scoring vectors and per-model probabilities (the parity twin batch; the non-compact variant)."""
         b = self.next_batch
         if b >= self.n_batches:
             raise RuntimeError("stream exhausted: raise n_batches")
         self.next_batch += 1
-        if self.pipe and self.parity_done:
+        vp = self.vec.data_ptr() if vectors else 0
+        mp = self.mp.data_ptr() if vectors else 0
+        if self.pipe:
             self.cur = b & 1
             fp, conf, dec, risk = self.outs[self.cur]
-            self.scorer(self._ptrs(b), self.B, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr())
+            self.scorer(self._ptrs(b), self.B, fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
+                        vec_ptr=vp, model_probs_ptr=mp)
             return
         self.cur = 0
         self.serial(self._ptrs(b), self.B, self.fp.data_ptr(), self.conf.data_ptr(), self.dec.data_ptr(),
-                    self.risk.data_ptr(), vec_ptr=self.vec.data_ptr(), model_probs_ptr=self.mp.data_ptr())
+                    self.risk.data_ptr(), vec_ptr=vp, model_probs_ptr=mp)
 
     def fetch(self, i):
         fp, _, dec, risk = self.outs[self.cur]
@@ -551,11 +594,14 @@ class Config3:
             hip_d2h(h.data_ptr(), d.data_ptr(), d.numel() * d.element_size(), st)
 
     def parity(self):
-        """The first parity_batches micro-batches (fresh state, carried across them) through the oracle chain."""
-        try:
-            return self._parity()
-        finally:
-            self.parity_done = True
+        """The first parity_batches micro-batches (fresh state, carried across them) through the timed path — no
+        vectors requested, so the pipelined stream's fused kernel reads the compact 24-float vectors — against the
+        oracle chain, which computes its own vectors; then one twin batch with the vectors and per-model
+        probabilities requested (the non-compact variant), whose vectors are compared too."""
+        return self._parity()
+
+    def outputs(self):
+        return self.outs[self.cur] if self.pipe else (self.fp, self.conf, self.dec, self.risk)
 
     def _parity(self):
         import oracle
@@ -569,27 +615,33 @@ class Config3:
         if self.with_lstm:
             from oracle import lstm_ref
             hist = lstm_ref.SequenceState(self.seq_len)
-        out = {"batches_checked": self.parity_batches, "vector_mismatched_elements": 0, "max_abs_prob_diff": 0.0,
-               "decision_mismatches": 0}
-        for b in range(self.parity_batches):
+        P = self.parity_batches
+        c0 = self.eng.counter("pipelined_compact_batches") if self.pipe else None
+        out = _parity_record(P, "pipelined stream, fused kernel from compact vectors" if self.pipe else
+                             "fd_score_batch_device (latency path)", self.B)
+        for b in range(P + 1):
+            twin = b == P  # the vectors-requested twin batch
             part = {f: self.tx[f][b * self.B:(b + 1) * self.B] for f in self.N.TXN_FIELDS}
-            self.step(b)
+            self.step(b, vectors=twin)
             self.torch.cuda.synchronize()
             rraw, rvec = o.run(part, want_raw=self.with_lstm)
-            V = self.vec.cpu().numpy()
-            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
-            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
-            cols = [px.astype(np.float64), pi]
+            cols = [oracle.xgb_predict(self.xgb, rvec, nthreads=cpu_threads())[0].astype(np.float64),
+                    oracle.iforest_predict(self.ifm, rvec, nthreads=cpu_threads())[0]]
             if self.with_lstm:
                 from oracle import lstm_ref
-                pl = lstm_ref.lstm_forward(self.lw, hist.run(part["card_key"], rraw))
-                cols.append(pl)
-                out["lstm_max_abs_prob_diff"] = max(out.get("lstm_max_abs_prob_diff", 0.0),
-                                                    float(np.abs(self.mp[2].cpu().numpy() - pl).max()))
-            fp, _, dec, _ = oracle.blend_weighted(np.stack(cols), self.weights, self.mults)
-            out["vector_mismatched_elements"] += int((V != rvec).sum())
-            out["max_abs_prob_diff"] = max(out["max_abs_prob_diff"], float(np.abs(self.fp.cpu().numpy() - fp).max()))
-            out["decision_mismatches"] += int((self.dec.cpu().numpy() != dec).sum())
+                cols.append(lstm_ref.lstm_forward(self.lw, hist.run(part["card_key"], rraw)))
+            ref = oracle.blend_weighted(np.stack(cols), self.weights, self.mults)
+            got = [t.cpu().numpy() for t in self.outputs()]
+            _parity_compare(out["twin" if twin else "timed_path"], got, ref)
+            if twin:
+                V = self.vec.cpu().numpy()
+                _parity_vectors(out["twin"], V, rvec)
+                Mp = self.mp.cpu().numpy()
+                for m, col in enumerate(cols):
+                    out["twin"]["max_abs_model_prob_diff"] = max(out["twin"]["max_abs_model_prob_diff"],
+                                                                 float(np.abs(Mp[m] - col).max()))
+        if c0 is not None:
+            out["timed_path"]["compact_batches"] = self.eng.counter("pipelined_compact_batches") - c0
         del o
         return out
 
@@ -728,7 +780,8 @@ class Config4(Config3):
         eng.state_init(cap, self.mode, self.K)
         eng.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
         self.parity_batches = args.parity_batches
-        self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches \
+        # + 1: the parity twin batch (vectors requested)
+        self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches + 1 \
             + args.loaded_iters + args.timing_steps + 1
         B = self.B
         h2d_batches = args.latency_iters if args.latency_iters > 0 else 0
@@ -744,7 +797,7 @@ class Config4(Config3):
                     dist.all_gather(parts, k)
                     return torch.cat(parts)
             w = synth_gpu.warm_workload(eng, dev, self.cards, rank, self.world, self.n_batches, B, hours=self.hours,
-                                        keep_batches=self.parity_batches, host_batches=h2d_batches, log=log,
+                                        keep_batches=self.parity_batches + 1, host_batches=h2d_batches, log=log,
                                         gather_keys=gather)
             self.dev = w["resident"]
             self.tx = w["head"]  # host copies of the parity batches
@@ -774,6 +827,17 @@ class Config4(Config3):
                                                        pipelined=not args.no_pipeline), rank, self.world)
         self.out = None
         self.host_out = None
+        # the resident micro-batches as column views, made once (a serving loop hands the scorer batches it already
+        # holds; slicing nine columns per step is harness cost, ~10-20 us of Python)
+        self.parts = [{f: t[b * B:(b + 1) * B] for f, t in self.dev.items()} for b in range(self.n_batches)]
+        # caller-owned outputs, two sets alternating by batch (ShardedScorer.step out=: the engine's output copy
+        # writes them in stream order, so batch i+2 reuses batch i's set after it); the Python exchange (gloo
+        # rehearsal) allocates its own
+        self.out_sets = None
+        if self.world == 1 or self.scorer.native:
+            self.out_sets = [tuple(torch.empty(B, dtype=d, device=dev) for d in (torch.float64, torch.float64,
+                                                                                  torch.uint8, torch.uint8))
+                             for _ in range(2)]
         self.h_fp = torch.empty(B, dtype=torch.float64, pin_memory=True)
         self.h_dec = torch.empty(B, dtype=torch.uint8, pin_memory=True)
         self.h_risk = torch.empty(B, dtype=torch.uint8, pin_memory=True)
@@ -804,13 +868,11 @@ class Config4(Config3):
         B = self.B
         # the batch the previous step prefetched is passed as the very same mapping (ShardedScorer names a prefetch
         # to the engine by identity, not by address)
-        nb = getattr(self, "_next_part", None)
-        part = nb[1] if nb is not None and nb[0] == b else {f: t[b * B:(b + 1) * B] for f, t in self.dev.items()}
-        self._next_part = None
+        part = self.parts[b]  # views made once at setup (the same mapping object when it was the prefetch)
         if self.world > 1 and b + 1 < self.n_batches:  # the next batch's partition + count exchange, one step ahead
-            nxt = {f: t[(b + 1) * B:(b + 2) * B] for f, t in self.dev.items()}
-            kw["prefetch"] = (nxt, B)
-            self._next_part = (b + 1, nxt)
+            kw["prefetch"] = (self.parts[b + 1], B)
+        if "out" not in kw and self.out_sets is not None:
+            kw["out"] = self.out_sets[b & 1]
         self.out = self.scorer.step(part, B, **kw)
 
     def step_to_host(self, i, q):
@@ -875,41 +937,44 @@ class Config4(Config3):
         if self.stream == "warm":
             at = self.profiles
         else:
-            at = synth.card_attrs(self.tx["card_id"][:P * B], 42)  # the profiles of the cards these batches touch
+            at = synth.card_attrs(self.tx["card_id"][:(P + 1) * B], 42)  # the profiles of the cards these batches touch
             _, first = np.unique(at["key"], return_index=True)
             at = {k: v[first] for k, v in at.items()}
         o.load_users(at["key"], at["avg_amount"], at["account_age_days"], at["device_fp"])
         o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
         if self.hist_rows is not None and len(self.hist_rows["card_key"]):
             o.run(self.hist_rows, want_raw=False)
-        out = {"batches_checked": P, "path": "ShardedScorer world 1 -> fd_score_batch_pipelined", "stream": self.stream,
-               "vector_mismatched_elements": 0, "vector_max_ulp": 0, "max_abs_model_prob_diff": 0.0,
-               "max_abs_prob_diff": 0.0, "decision_mismatches": 0, "risk_mismatches": 0}
+        out = _parity_record(P, "ShardedScorer world 1 -> fd_score_batch_pipelined, no vectors requested: the fused "
+                             "ensemble kernel from the compact 24-float vectors (the timed variant); twin: one more "
+                             "batch with vectors + model probabilities requested (64-wide vectors)", B)
+        out["stream"] = self.stream
         vec = torch.empty((B, 64), dtype=torch.float32, device=self.dev["ts_ms"].device)
         mp = torch.empty((2, B), dtype=torch.float64, device=vec.device)
         raws = []
         sat0 = _saturated(self.eng, self)
-        for b in range(P):
+        c0 = self.eng.counter("pipelined_compact_batches")
+        s0 = self.eng.counter("pipelined_slot_stream_batches")
+        for b in range(P + 1):
+            twin = b == P
             part = {f: self.tx[f][b * B:(b + 1) * B] for f in self.N.TXN_FIELDS}
-            self.step(b, vectors=vec, model_probs=mp)
+            if twin:
+                self.step(b, vectors=vec, model_probs=mp)
+            else:
+                self.step(b)
             torch.cuda.synchronize()
             raw, rvec = o.run(part, want_raw=True)
             raws.append(raw)
-            V = vec.cpu().numpy()
-            diff = V != rvec
-            out["vector_mismatched_elements"] += int(diff.sum())
-            if diff.any():
-                ulp = np.abs(V.view(np.int32)[diff].astype(np.int64) - rvec.view(np.int32)[diff].astype(np.int64))
-                out["vector_max_ulp"] = max(out["vector_max_ulp"], int(ulp.max()))
-            px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
-            pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
-            M = mp.cpu().numpy()
-            out["max_abs_model_prob_diff"] = max(out["max_abs_model_prob_diff"], float(np.abs(M[0] - px).max()),
-                                                 float(np.abs(M[1] - pi).max()))
-            fp, _, dec, risk = oracle.blend_weighted(np.stack([M[0], M[1]]), self.weights, self.mults)
-            out["max_abs_prob_diff"] = max(out["max_abs_prob_diff"], float(np.abs(self.out[0].cpu().numpy() - fp).max()))
-            out["decision_mismatches"] += int((self.out[2].cpu().numpy() != dec).sum())
-            out["risk_mismatches"] += int((self.out[3].cpu().numpy() != risk).sum())
+            px, _, _ = oracle.xgb_predict(self.xgb, rvec, nthreads=cpu_threads())
+            pi, _, _ = oracle.iforest_predict(self.ifm, rvec, nthreads=cpu_threads())
+            ref = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults)
+            leg = out["twin" if twin else "timed_path"]
+            _parity_compare(leg, [t.cpu().numpy() for t in self.out], ref)
+            if twin:
+                _parity_vectors(leg, vec.cpu().numpy(), rvec)
+                M = mp.cpu().numpy()
+                leg["max_abs_model_prob_diff"] = max(float(np.abs(M[0] - px).max()), float(np.abs(M[1] - pi).max()))
+        out["timed_path"]["compact_batches"] = self.eng.counter("pipelined_compact_batches") - c0
+        out["timed_path"]["slot_stream_batches"] = self.eng.counter("pipelined_slot_stream_batches") - s0
         from fdengine.synth_gpu import occupancy
         allraw = np.concatenate(raws)
         self.occupancy = dict(occupancy(allraw), basis=f"the {P} parity micro-batches (raw velocity "
@@ -1152,7 +1217,7 @@ class Config3J(Config3):
         # pipelined (default): the codec runs on an engine of its own with its own stream, so batch i+1's parse
         # overlaps batch i's scoring on the pipelined stream; two column sets, handed over by events (the scoring
         # waits for its parse; a set's next parse waits for the scoring that read it)
-        self.pipe, self.parity_done, self.cur = not args.no_pipeline, False, 0
+        self.pipe, self.parity_done, self.cur = not args.no_pipeline, True, 0
         self.extra_engines = []
         codec_eng = eng
         if self.pipe:
@@ -1206,7 +1271,7 @@ class Config3J(Config3):
 
     def step(self, i):
         s = i % self.pool
-        if not (self.pipe and self.parity_done):  # one stream, vectors kept (the parity batch reads them)
+        if not self.pipe:  # one stream, vectors kept
             if self.pipe:
                 self.cstream.wait_stream(self.dev_stream)
             self.codec.parse_device(self.bufs[s].data_ptr(), self.offs[s].data_ptr(), self.B, self.cptrs)
@@ -1232,7 +1297,9 @@ class Config3J(Config3):
         self.freed_live[k] = True
 
     def parity(self):
-        """Batch 0 (fresh state): oracle ingest -> oracle features -> forests -> blend, first 8192 rows."""
+        """Batch 0 (fresh state) through the timed path (codec stream -> pipelined scoring from compact vectors; with
+        --no-pipeline one stream, vectors kept and compared too) against oracle ingest -> oracle features -> forests
+        -> blend on the oracle's own vectors, first 8192 rows."""
         import oracle
         from fdengine import synth
         from oracle import ingest_ref as R
@@ -1242,6 +1309,8 @@ class Config3J(Config3):
         o = OracleFeatureState(self.cap, self.mode, self.K)
         o.load_users(self.ukeys, self.uavg, self.uage, self.ufp)
         o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
+        self.parity_done = True  # the pipelined stream from the first batch on (the timed path)
+        c0 = self.eng.counter("pipelined_compact_batches")
         self.step(0)
         self.torch.cuda.synchronize()
         cols = R.parse_batch(self.msgs[0][:k], {m: i for i, m in enumerate(self.merchant_ids)},
@@ -1249,14 +1318,19 @@ class Config3J(Config3):
                                                                          synth.SIM_TXN_TYPES, synth.SIM_CARD_TYPES)])
         _, rvec = o.run({f: cols[f] for f in self.N.TXN_FIELDS}, want_raw=False)
         del o
-        V = self.vec[:k].cpu().numpy()
-        px, _, _ = oracle.xgb_predict(self.xgb, V, nthreads=cpu_threads())
-        pi, _, _ = oracle.iforest_predict(self.ifm, V, nthreads=cpu_threads())
-        fp, _, dec, _ = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]), self.weights, self.mults)
-        self.parity_done = True
-        return {"rows_checked": k, "vector_mismatched_elements": int((V != rvec).sum()),
-                "max_abs_prob_diff": float(np.abs(self.fp[:k].cpu().numpy() - fp).max()),
-                "decision_mismatches": int((self.dec[:k].cpu().numpy() != dec).sum())}
+        px, _, _ = oracle.xgb_predict(self.xgb, rvec, nthreads=cpu_threads())
+        pi, _, _ = oracle.iforest_predict(self.ifm, rvec, nthreads=cpu_threads())
+        ref = [np.ascontiguousarray(a) for a in oracle.blend_weighted(np.stack([px.astype(np.float64), pi]),
+                                                                       self.weights, self.mults)]
+        got = [t[:k].cpu().numpy() for t in self.outs[self.cur]]
+        out = _parity_record(1, "codec stream -> pipelined stream, fused kernel from compact vectors" if self.pipe
+                             else "codec -> fd_score_batch_device", k)
+        _parity_compare(out["timed_path"], got, ref)
+        out["timed_path"]["compact_batches"] = self.eng.counter("pipelined_compact_batches") - c0
+        if not self.pipe:
+            _parity_vectors(out["timed_path"], self.vec[:k].cpu().numpy(), rvec)
+        del out["twin"]
+        return out
 
     def kernels(self, timing):
         out = super().kernels(timing)
@@ -1302,6 +1376,32 @@ def _read_timing(eng, wl):
             a, b = out.get(k, (0.0, 0))
             out[k] = (a + ms, b + c)
     return out
+
+
+def _host_counters(eng):
+    """the engine's cumulative host-side counters for the pipelined / sharded step (None where unsupported)"""
+    out = {}
+    for k in ("pipelined_batches", "pipelined_host_ns", "sharded_steps"):
+        try:
+            out[k] = eng.counter(k)
+        except Exception:
+            out[k] = None
+    return out
+
+
+def _host_breakdown(h0, h1, submit_s, steps):
+    """host submit time per step split into the native step call (HIP launches, event records / waits inside
+    fd_score_batch_pipelined) and everything above it (bench loop, ShardedScorer, ctypes)"""
+    if h0.get("pipelined_host_ns") is None or h1.get("pipelined_host_ns") is None:
+        return None
+    calls = h1["pipelined_batches"] - h0["pipelined_batches"]
+    if calls <= 0:
+        return None
+    native = (h1["pipelined_host_ns"] - h0["pipelined_host_ns"]) / 1e3 / steps
+    total = submit_s * 1e6 / steps
+    return {"native_us_per_step": round(native, 2), "above_native_us_per_step": round(total - native, 2),
+            "pipelined_calls": calls, "basis": "engine counter pipelined_host_ns (steady_clock around "
+                                               "fd_score_batch_pipelined's body) over the timed region"}
 
 
 def _saturated(eng, wl):
@@ -1463,17 +1563,12 @@ def main():
     if dist:
         dist.barrier()
     _read_timing(eng, wl)
-    # kernel durations: HIP events on the launch stream, on one launch in TIMING_EVERY of each kernel (an event
-    # record costs stream time; timing every launch would charge ~10 us per step of instrumentation to `value`)
-    for e in _engines(eng, wl):
-        e.set_option("timing_every", TIMING_EVERY)
-        e.set_timing(True)
+    sat0 = _saturated(eng, wl)
+    host0 = _host_counters(eng)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    sat0 = _saturated(eng, wl)
-    if dist:
-        dist.barrier()
+    # the timed region: exactly --steps back-to-back steps, no instrumentation inside (kernel timing is off)
     t0 = time.perf_counter()
     for i in range(args.steps):
         wl.step(i)
@@ -1482,8 +1577,13 @@ def main():
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
-    # more of the same back-to-back steps, still sampled 1 in TIMING_EVERY, so the kernel averages rest on >= 20
-    # launches of each kernel even when --steps is short (outside the timed region: `value` is unaffected)
+    host1 = _host_counters(eng)
+    # kernel durations: HIP events on the launch stream, on one launch in TIMING_EVERY of each kernel (an event
+    # record costs stream time), over more of the same back-to-back steps AFTER the timed region, so the kernel
+    # averages rest on >= 20 launches of each kernel and `value` carries no instrumentation
+    for e in _engines(eng, wl):
+        e.set_option("timing_every", TIMING_EVERY)
+        e.set_timing(True)
     for i in range(args.timing_steps):
         wl.step(args.steps + i)
     torch.cuda.synchronize()
@@ -1633,6 +1733,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
             "host_submit_ms_per_step": round((t_sub - t0) / args.steps * 1e3, 5),
+            "host_submit_breakdown": _host_breakdown(host0, host1, t_sub - t0, args.steps),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -1655,8 +1756,8 @@ def main():
             "roofline": roof,
             "kernel_avg_us": wl.kernels(timing),
             "kernel_avg_us_alone": wl.kernels(timing_alone) if timing_alone else None,
-            "kernel_timing": f"HIP events on the launch stream, 1 launch in {TIMING_EVERY} of each kernel, over the timed "
-                             f"region and {args.timing_steps} more back-to-back steps after it",
+            "kernel_timing": f"HIP events on the launch stream, 1 launch in {TIMING_EVERY} of each kernel, over "
+                             f"{args.timing_steps} back-to-back steps after the timed region (none inside it)",
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
             "window_saturation": saturation,

@@ -438,13 +438,14 @@ int fd_score_records_pipelined(fd_engine* eng, const fd_blend_params* params, co
                                void* input_ready);
 /* The sharded step as one call over the engine's own RCCL communicators (csrc/comm.hip): the host loads
    RCCL once (the process's librccl.so, by path; any library exporting ncclGetUniqueId, ncclCommInitRank,
-   ncclCommDestroy, ncclGroupStart/End, ncclSend/Recv and ncclGetErrorString can stand in — the tests run several
+   ncclCommDestroy, ncclCommAbort, ncclGroupStart/End, ncclSend/Recv and ncclGetErrorString can stand in — the tests run several
    ranks on one GPU over an in-process loopback of that API), rank 0 makes two unique ids (fd_comm_unique_id), the
    host broadcasts them, every rank calls fd_comm_init (collective, blocking with RCCL). fd_sharded_step then runs
    one micro-batch: its split sizes (exchanged by the previous call when it prefetched this batch, else now: the
-   step's one host wait), the next batch's partition and count exchange (`next`, optional: prefetch; queued on
-   the forward stream ahead of this batch's records, so they land while this batch is scored), the records to
-   their owners (grouped ncclSend/ncclRecv with per-peer counts, on the engine's forward stream), the owner's
+   step's one host wait), then, on the engine's forward stream behind the wait for this batch's inbox slot, ONE
+   RCCL group holding this batch's records to their owners (ncclSend/ncclRecv with per-peer counts) and — with
+   `next` (optional: prefetch) — the next batch's count exchange, its count kernel queued before the group and its
+   publish + places after it (so the next counts land while this batch is scored), then the owner's
    features + scoring (fd_score_records_pipelined's pipeline, the features waiting for the records), the
    results back (second communicator, engine stream) and into arrival order in the caller's outputs (device or
    host-mapped memory), written on the engine stream. The calling thread issues every communicator operation, in
@@ -454,7 +455,12 @@ int fd_score_records_pipelined(fd_engine* eng, const fd_blend_params* params, co
    exchange completes, its records are never sent — every rank must drop alike). A nonzero batch_id that is not
    the pending one (or with nothing pending) fails with FD_ERR_INVALID_ARG and changes nothing. The caller keeps a prefetched batch's input
    columns alive and unchanged until the call that scores (or drops) it has returned.
-   split_sizes (optional): the 2 x world send / receive counts of this batch. */
+   split_sizes (optional): the 2 x world send / receive counts of this batch.
+   Failure: the split-size wait gives up after the engine option comm_timeout_ms (a peer that never posts its counts)
+   or on a stream error; it first aborts both communicators (ncclCommAbort: RCCL's kernels blocked on the peer exit),
+   then fails with FD_ERR_HIP. Later fd_sharded_step calls fail with the abort's reason; fd_engine_sync,
+   fd_comm_destroy and fd_engine_destroy wait on the streams at most comm_timeout_ms each; fd_comm_destroy then
+   fd_comm_init makes new communicators. */
 int fd_comm_unique_id(const char* rccl_path, uint8_t* id_out /* 128 bytes */);
 int fd_comm_init(fd_engine* eng, const char* rccl_path, int32_t rank, int32_t world, const uint8_t* id_fwd,
                  const uint8_t* id_back);
@@ -675,7 +681,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
 /* Engine counters (diagnostics): "window_saturated" (sliding windows: transactions so far whose 24 h window held the
    ring's whole capacity K of prior events — their counts may be truncated at K; synchronises the engine's streams),
    "pipelined_batches" (batches through fd_score_batch_pipelined /
-   fd_score_records_pipelined so far), "sharded_steps" (fd_sharded_step calls) and "sharded_host_ns_<phase>" (host
+   fd_score_records_pipelined so far), "pipelined_compact_batches" (of those, scored by the fused ensemble kernel from
+   the compact 24-float vectors: no vectors requested), "pipelined_slot_stream_batches" (of those, with the slot pass on
+   its own stream), "pipelined_host_ns" (host nanoseconds inside fd_score_batch_pipelined), "sharded_steps" (fd_sharded_step calls) and "sharded_host_ns_<phase>" (host
    nanoseconds inside fd_sharded_step by phase: "wait" the split sizes, "partition" / "counts" / "count_copy" the
    next batch's route kernels, count exchange and copy to the host, "records" the records exchange, "score" the
    owner's pipeline launches, "back" / "scatter" the results exchange and the scatter into arrival order). */

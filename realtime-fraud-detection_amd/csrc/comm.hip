@@ -7,7 +7,7 @@
 // step is one C-ABI call and no Python collective sits between the kernels.
 //
 // RCCL is the one the host process already loaded (torch's librccl.so, passed by path): dlopen on the same file
-// returns that instance, so the process keeps one RCCL and one HIP runtime. Any library exporting the same eight
+// returns that instance, so the process keeps one RCCL and one HIP runtime. Any library exporting the same nine
 // symbols can stand in (the tests' in-process loopback, tests/native/rccl_loopback.cpp, runs several ranks on one
 // GPU); each communicator remembers the library it came from. Two communicators per engine: `fwd` (count and
 // record exchanges, on the engine's forward stream) and `back` (results, on the engine stream). The calling
@@ -30,6 +30,7 @@ struct RcclApi {
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclSend) send = nullptr;
@@ -59,6 +60,7 @@ const RcclApi& rccl(const char* path) {
   sym(h, "ncclGetUniqueId", a.get_unique_id);
   sym(h, "ncclCommInitRank", a.comm_init_rank);
   sym(h, "ncclCommDestroy", a.comm_destroy);
+  sym(h, "ncclCommAbort", a.comm_abort);
   sym(h, "ncclGroupStart", a.group_start);
   sym(h, "ncclGroupEnd", a.group_end);
   sym(h, "ncclSend", a.send);
@@ -127,16 +129,53 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
   c.ready = true;
 }
 
+void comm_abort(Engine& e, const std::string& reason) {
+  ShardComm& c = e.comm;
+  if (!c.ready || c.aborted) return;
+  const RcclApi& R = api(c);
+  // RCCL kernels still queued or running on x_fwd / the engine stream wait for peers that will not come: abort
+  // exits them, so the streams drain instead of the hang moving into the next sync or the teardown
+  if (c.fwd) (void)R.comm_abort(static_cast<ncclComm_t>(c.fwd));
+  if (c.back) (void)R.comm_abort(static_cast<ncclComm_t>(c.back));
+  c.fwd = c.back = nullptr;
+  c.aborted = true;
+  c.abort_reason = reason;
+  c.pending = false;
+}
+
+bool comm_sync_stream(Engine& e, hipStream_t st) {
+  if (!st) return true;
+  if (!e.comm.aborted) {
+    FD_HIP(hipStreamSynchronize(st));
+    return true;
+  }
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(e.comm.timeout_ms);
+  for (;;) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q != hipErrorNotReady) return true;  // done, or an error the stream already reported
+    if (std::chrono::steady_clock::now() >= deadline) return false;
+    const timespec ts{0, 200000};
+    nanosleep(&ts, nullptr);
+  }
+}
+
 void comm_destroy(Engine& e) {
   ShardComm& c = e.comm;
-  if (c.x_fwd) (void)hipStreamSynchronize(c.x_fwd);
-  (void)hipStreamSynchronize(e.stream);
-  if (c.ready) {
+  // after an abort the forward stream is waited for at most comm_timeout_ms; one that never drains is leaked
+  // (its buffers too) rather than destroyed under a live operation
+  const bool drained = comm_sync_stream(e, c.x_fwd);
+  (void)comm_sync_stream(e, e.stream);
+  if (c.ready && !c.aborted) {
     const RcclApi& R = api(c);
     if (c.fwd) (void)R.comm_destroy(static_cast<ncclComm_t>(c.fwd));
     if (c.back) (void)R.comm_destroy(static_cast<ncclComm_t>(c.back));
   }
   c.fwd = c.back = nullptr;
+  if (!drained) {
+    c.x_fwd = nullptr;
+    for (int s = 0; s < 2; ++s) c.rec[s].ptr = c.cnt[s].ptr = c.res[s].ptr = nullptr, c.h_cnt[s] = nullptr;
+    for (int q = 0; q < ShardComm::kInbox; ++q) c.inbox[q].ptr = nullptr;
+  }
   for (int s = 0; s < 2; ++s) {
     for (auto* b : {&c.rec[s], &c.cnt[s], &c.res[s]}) b->release();
     if (c.h_cnt[s]) (void)hipHostFree(c.h_cnt[s]);
@@ -154,6 +193,8 @@ void comm_destroy(Engine& e) {
   if (c.x_fwd) (void)hipStreamDestroy(c.x_fwd);
   c.x_fwd = nullptr;
   c.ready = false;
+  c.aborted = false;
+  c.abort_reason.clear();
   c.pending = false;
   c.api = nullptr;
 }
@@ -225,18 +266,24 @@ void comm_wait_counts(Engine& e, int s, int64_t n, HostLaps& L) {
     while (!arrived() && clk::now() < spin_until) __builtin_ia32_pause();
     const auto deadline = t0 + std::chrono::milliseconds(c.timeout_ms);
     long nap_ns = 2000;
+    // every failure below aborts the communicators first: the count exchange (and whatever RCCL queued behind it)
+    // would otherwise keep waiting on the device for the missing peer, and the next sync or the teardown would hang
+    auto fail = [&](const std::string& why) {
+      comm_abort(e, why);
+      throw Error(FD_ERR_HIP, why);
+    };
     while (!arrived()) {
       const hipError_t q = hipStreamQuery(c.x_fwd);
       if (q == hipSuccess) {
-        FD_REQUIRE(arrived(), FD_ERR_HIP, "split sizes never arrived (slot " + std::to_string(s) + ", sequence " +
-                                              std::to_string(want) + ")");
+        if (!arrived())
+          fail("split sizes never arrived (slot " + std::to_string(s) + ", sequence " + std::to_string(want) + ")");
         break;
       }
-      FD_REQUIRE(q == hipErrorNotReady, FD_ERR_HIP, std::string("count exchange: ") + hipGetErrorString(q));
-      FD_REQUIRE(clk::now() < deadline, FD_ERR_HIP,
-                 "count exchange timed out after " + std::to_string(c.timeout_ms) + " ms (slot " + std::to_string(s) +
-                     ", sequence " + std::to_string(want) + ", rank " + std::to_string(c.rank) + " of " +
-                     std::to_string(G) + "): a peer did not post its counts");
+      if (q != hipErrorNotReady) fail(std::string("count exchange: ") + hipGetErrorString(q));
+      if (clk::now() >= deadline)
+        fail("count exchange timed out after " + std::to_string(c.timeout_ms) + " ms (slot " + std::to_string(s) +
+             ", sequence " + std::to_string(want) + ", rank " + std::to_string(c.rank) + " of " + std::to_string(G) +
+             "): a peer did not post its counts; communicators aborted");
       const timespec ts{0, nap_ns};
       nanosleep(&ts, nullptr);
       nap_ns = std::min(nap_ns * 2, 50000L);

@@ -293,6 +293,14 @@ int fd_engine_destroy(fd_engine* eng) {
   if (!eng) return FD_OK;
   { FD_ENGINE_LOCK(eng); }  // wait for a call in flight on another thread (destroying while in use is the caller's bug)
   Engine& e = E(eng);
+  if (e.comm.aborted) {  // an aborted exchange: every stream gets a bounded wait; one that never drains leaks the engine
+    bool ok = fd::comm_sync_stream(e, e.comm.x_fwd);
+    ok = fd::comm_sync_stream(e, e.stream) && ok;
+    for (hipStream_t st : e.pipe_stream) ok = fd::comm_sync_stream(e, st) && ok;
+    ok = fd::comm_sync_stream(e, e.pipe_slot_stream) && ok;
+    FD_REQUIRE(ok, FD_ERR_HIP, "engine leaked: streams still busy " + std::to_string(e.comm.timeout_ms) +
+                                   " ms after the communicators were aborted (" + e.comm.abort_reason + ")");
+  }
   (void)hipStreamSynchronize(e.stream);
   for (auto& f : e.forests) {
     for (auto* b : {&f.split.bins, &f.split.nan, &f.split.leaves}) b->release();
@@ -407,6 +415,13 @@ int fd_engine_sync(fd_engine* eng) {
   FD_API_BEGIN
   FD_ENGINE_LOCK(eng);
   Engine& e = E(eng);
+  if (e.comm.aborted) {  // streams behind an aborted exchange: bounded waits, then the abort's reason
+    bool ok = fd::comm_sync_stream(e, e.comm.x_fwd);
+    ok = fd::comm_sync_stream(e, e.stream) && ok;
+    for (hipStream_t st : e.pipe_stream) ok = fd::comm_sync_stream(e, st) && ok;
+    FD_REQUIRE(ok, FD_ERR_HIP, "streams still busy " + std::to_string(e.comm.timeout_ms) +
+                                   " ms after the communicators were aborted (" + e.comm.abort_reason + ")");
+  }
   FD_HIP(hipStreamSynchronize(e.stream));
   if (e.comm.x_fwd) FD_HIP(hipStreamSynchronize(e.comm.x_fwd));
   for (hipStream_t st : e.pipe_stream)
@@ -434,6 +449,14 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
   const std::string k(key);
   if (k == "pipelined_batches") {  // fd_score_batch_pipelined / fd_score_records_pipelined batches so far
     *value = (int64_t)e.pipe_iter_total;
+  } else if (k == "pipelined_compact_batches") {  // of those: scored by the fused kernel from the compact 24-float
+    // vectors (no vectors requested), the variant the config-3/4 bench times
+    *value = (int64_t)e.pipe_compact_total;
+  } else if (k == "pipelined_host_ns") {  // host nanoseconds inside fd_score_batch_pipelined (HIP launches, event
+    // records and waits of the pipelined step)
+    *value = (int64_t)e.pipe_host_ns;
+  } else if (k == "pipelined_slot_stream_batches") {  // of those: the slot pass on its own stream (slot_stream)
+    *value = (int64_t)e.pipe_slot_stream_total;
   } else if (k == "window_saturated") {  // sliding windows: transactions whose 24 h window held K prior events
     // (its count may be truncated at the ring capacity); synchronises the engine's streams
     FD_REQUIRE(e.state.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
@@ -953,6 +976,9 @@ static void score_batch_body(Engine& e, const fd_blend_params& p, const int32_t*
   if (seq && e.seq_ring_lstm && n < 4096 && (e.lstm_rows == 0 || e.lstm_rows == 4)) {
     e.seq_desc.ensure((size_t)n * sizeof(unsigned long long));
     desc = e.seq_desc.as<unsigned long long>();
+    // a transaction whose card probe fails (table full) gets no descriptor from the feature kernel: the gather
+    // kernel writes kSeqMaterialized for it; the slot-kernel path starts from all-materialized (bit 63 set)
+    if (!e.state.slot_gather) FD_HIP(hipMemsetAsync(desc, 0xff, (size_t)n * sizeof(unsigned long long), e.stream));
   }
   fd::launch_features(e, t, n, vec, nullptr, seq, nullptr, nullptr, false, 0, nullptr, false, desc);
   score_matrix(e, p, slots, ext, present, vec, n, FD_VECTOR_WIDTH, dMP, dfp, dconf, ddec, drisk, seq, e.state.S,
@@ -1100,6 +1126,8 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   if (e.pipe_copy_live[s]) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_copy_ev[s], 0));
   ++e.pipe_iter;
   ++e.pipe_iter_total;
+  e.pipe_compact_total += compact;
+  e.pipe_slot_stream_total += Ss != nullptr;
   {  // the scoring launches go on Sc: score_matrix launches on e.stream
     struct Swap {
       Engine& e;
@@ -1137,8 +1165,11 @@ int fd_score_batch_pipelined(fd_engine* eng, const fd_blend_params* params, cons
   if (n == 0) return FD_OK;
   FD_REQUIRE(d_fraud_prob != nullptr, FD_ERR_INVALID_ARG, "null fraud_prob output");
   FD_REQUIRE(params->n_models >= 1 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "bad n_models");
+  const auto t0 = std::chrono::steady_clock::now();
   pipe_step(e, params, slots, ext_probs, present, txns, nullptr, n, d_vectors, d_model_probs, d_fraud_prob,
             d_confidence, d_decision, d_risk, nullptr, input_ready);
+  e.pipe_host_ns += (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now() - t0).count();
   FD_API_END
 }
 
@@ -1207,6 +1238,7 @@ int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t
   Engine& e = E_quiet(eng);
   fd::ShardComm& c = e.comm;
   FD_REQUIRE(c.ready, FD_ERR_NOT_LOADED, "no communicators (fd_comm_init)");
+  FD_REQUIRE(!c.aborted, FD_ERR_HIP, "communicators aborted (" + c.abort_reason + "): fd_comm_destroy, then fd_comm_init");
   FD_REQUIRE(params && slots && txns && n >= 0 && (!next || next_n >= 0), FD_ERR_INVALID_ARG, "bad arguments");
   FD_REQUIRE(!next || next_id != 0, FD_ERR_INVALID_ARG, "a prefetched batch needs a nonzero next_id");
   FD_REQUIRE(params->n_models >= 1 && params->n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "bad n_models");

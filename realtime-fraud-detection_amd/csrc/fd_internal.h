@@ -379,6 +379,11 @@ struct IngestTables {
 // per-batch buffers in two slots (a step's batch and the next one, prefetched)
 struct ShardComm {
   bool ready = false;
+  // a step that timed out or failed on the device aborts both communicators (ncclCommAbort: RCCL's blocked
+  // kernels exit) before it throws, so no stream is left parked on a peer; afterwards the engine refuses sharded
+  // steps, and its syncs / fd_comm_destroy wait on the forward stream only up to comm_timeout_ms
+  bool aborted = false;
+  std::string abort_reason;
   int rank = 0, world = 1;
   const void* api = nullptr;  // the RcclApi (comm.hip) of the library fd_comm_init was given
   void* fwd = nullptr;   // ncclComm_t: counts + records, on x_fwd
@@ -478,6 +483,9 @@ struct Engine {
   hipEvent_t slot_pass_ev = nullptr;
   unsigned long long pipe_iter = 0;
   unsigned long long pipe_iter_total = 0;  // counter "pipelined_batches"
+  unsigned long long pipe_compact_total = 0;  // counter "pipelined_compact_batches": batches scored from compact vectors
+  unsigned long long pipe_host_ns = 0;  // counter "pipelined_host_ns": host time inside fd_score_batch_pipelined
+  unsigned long long pipe_slot_stream_total = 0;  // counter "pipelined_slot_stream_batches": slot pass on its own stream
   bool pipe_lean = true;   // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
   DeviceBuffer pipe_vec[kPipeSlots], pipe_seq[kPipeSlots];
   // the scoring streams write a batch's outputs into pipe_out[slot]; one copy kernel on `stream` moves them to the
@@ -489,8 +497,8 @@ struct Engine {
   bool pipe_copy_vec[kPipeSlots] = {};  // that copy also read the slot's vectors (the slot's next features wait)
   int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
-  bool seq_ring_lstm = true;
-  bool ens_prio = false;  // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels)  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
+  bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
+  bool ens_prio = false;  // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels)
   bool compact_vectors = true;  // "compact_vectors": the pipelined stream's compact scoring vectors (engine.hip)
   int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)
   // host-API staging
@@ -637,6 +645,10 @@ void route_check(Engine& e);
 void comm_unique_id(const char* rccl_path, uint8_t* out);
 void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint8_t* id_fwd, const uint8_t* id_back);
 void comm_destroy(Engine& e);
+// ncclCommAbort both communicators (idempotent); reason is kept for the errors of later calls
+void comm_abort(Engine& e, const std::string& reason);
+// hipStreamSynchronize, or for an aborted engine a poll bounded by comm_timeout_ms (false: still busy)
+bool comm_sync_stream(Engine& e, hipStream_t st);
 void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, int slot, HostLaps& L);
 void comm_wait_counts(Engine& e, int slot, int64_t n, HostLaps& L);  // host wait; split[slot] checked
 // records exchange of `slot` behind its inbox slot, + the next batch's count exchange in the same group

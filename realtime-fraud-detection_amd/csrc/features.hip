@@ -1109,6 +1109,9 @@ __device__ void bucket_body(const BucketArgs& a, const int b, unsigned long long
       if (s < 0) {  // table full: the batch fails (err), the key leaves the list below
         atomicOr(g.err, 1u);
         g.slot[i] = 0xffffffffu;
+        // no card, so no ring: the LSTM (which runs before the error is reported) reads row i of the sequence
+        // buffer instead of a stale descriptor's slot
+        if (a.out.seq_desc) a.out.seq_desc[i] = kSeqMaterialized;
         skeys[j] = ~0ull;
         n_long = 1;
         continue;

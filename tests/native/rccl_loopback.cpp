@@ -1,8 +1,8 @@
 // TEST INFRASTRUCTURE ONLY — never loaded by the product path.
 //
-// An in-process loopback of the eight RCCL entry points the engine's sharded step uses (csrc/comm.hip dlopens its
-// RCCL by path and calls only these): ncclGetUniqueId, ncclCommInitRank, ncclCommDestroy, ncclGroupStart,
-// ncclGroupEnd, ncclSend, ncclRecv, ncclGetErrorString. It lets one process run several ranks — one engine and one
+// An in-process loopback of the nine RCCL entry points the engine's sharded step uses (csrc/comm.hip dlopens its
+// RCCL by path and calls only these): ncclGetUniqueId, ncclCommInitRank, ncclCommDestroy, ncclCommAbort,
+// ncclGroupStart, ncclGroupEnd, ncclSend, ncclRecv, ncclGetErrorString. It lets one process run several ranks — one engine and one
 // host thread per rank, all on the test box's one GPU — through the very fd_sharded_step the driver runs across
 // GPUs, so the N >= 2 step is executed and checked against the oracle without a multi-GPU node
 // (tests/test_gpu_sharding_loopback.py). RCCL itself refuses two ranks on one device.
@@ -15,6 +15,12 @@
 // host thread until every op of the group is matched (the peers are other threads), so every stream wait is on an
 // event recorded earlier: nothing here can deadlock a hardware queue. A group left unmatched for LOOPBACK_TIMEOUT_S
 // seconds (default 60) fails with ncclInvalidUsage and a message on stderr — the test fails instead of hanging.
+//
+// LOOPBACK_STALL=1 (read per group) models RCCL's device-side blocking instead: the group returns ncclSuccess at once
+// and each op's stream is parked behind a host function that waits until its communicator is aborted
+// (ncclCommAbort) — or LOOPBACK_TIMEOUT_S passes, so nothing can park a stream for good. No op is ever matched: the
+// peers are taken to be dead. The engine's own comm_timeout_ms must then notice, abort and report
+// (tests/test_gpu_sharding_loopback.py::test_count_timeout_aborts_the_communicators).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -97,6 +103,7 @@ double timeout_s() {
 struct ncclComm {
   unsigned long long group = 0;
   int rank = 0, nranks = 0;
+  bool aborted = false;  // (under g_mu) ncclCommAbort: parked streams of this communicator go on
 };
 
 namespace {
@@ -125,7 +132,30 @@ void match(Op* s, Op* r) {
   s->done = r->done = d;
 }
 
+bool stall_mode() {
+  const char* v = std::getenv("LOOPBACK_STALL");
+  return v && *v == '1';
+}
+
+// the stream side of a stalled op: a host function holding its stream until the communicator is aborted
+void stall_fn(void* arg) {
+  auto* comm = static_cast<ncclComm*>(arg);
+  std::unique_lock<std::mutex> lk(g_mu);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s());
+  if (!g_cv.wait_until(lk, deadline, [&] { return comm->aborted; }))
+    std::fprintf(stderr, "rccl_loopback: stalled op released by LOOPBACK_TIMEOUT_S, never aborted\n");
+}
+
 ncclResult_t flush(std::vector<Pending>& ops) {
+  if (stall_mode()) {
+    for (const Pending& p : ops)
+      if (hipLaunchHostFunc(p.stream, stall_fn, p.comm) != hipSuccess) {
+        ops.clear();
+        return ncclUnhandledCudaError;
+      }
+    ops.clear();
+    return ncclSuccess;
+  }
   std::vector<std::unique_ptr<Op>> mine;
   mine.reserve(ops.size());
   for (const Pending& p : ops) {
@@ -241,6 +271,16 @@ ncclResult_t ncclCommDestroy(ncclComm_t comm) {
     if (it != g_groups->end() && --it->second.refs == 0) g_groups->erase(it);
   }
   delete comm;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommAbort(ncclComm_t comm) {
+  if (!comm) return ncclInvalidArgument;
+  std::lock_guard<std::mutex> lk(g_mu);
+  comm->aborted = true;  // the object stays allocated: a parked host function may still read it
+  auto it = g_groups->find(comm->group);
+  if (it != g_groups->end() && --it->second.refs == 0) g_groups->erase(it);
+  g_cv.notify_all();
   return ncclSuccess;
 }
 

@@ -152,8 +152,11 @@ def test_config4_full_size_warm_pipelined():
     simulator.py:229,302) run through the feature path so the 5 min / 1 h / 24 h windows hold events
     (RedisService.java:178-207), then three 64 k micro-batches submitted back to back through ShardedScorer at
     world 1 over EngineShardBackend(pipelined=True) -> fd_score_batch_pipelined (batch i+1's features overlap
-    batch i's forests). Vectors, model probabilities, fraud probability, decision and risk against the oracle chain,
-    which replays the history rows of exactly the cards those batches touch. K = 64 ring events per card (the bench's
+    batch i's forests). The first two batches request no vectors — the exact variant the bench times: compact 24-float
+    vectors into the fused ensemble kernel, slot pass on its own stream (engine counters prove both) — and their
+    fraud probability, confidence, decision and risk are checked against the oracle chain on the oracle's own vectors;
+    the third requests vectors and model probabilities (64-wide variant), checked element by element. The oracle
+    replays the history rows of exactly the cards those batches touch. K = 64 ring events per card (the bench's
     headline) in 2^27 slots (load factor ~0.78 after the history's unknown-user cards): the engine's
     window_saturated counter over the three batches equals the oracle's count of transactions whose 24 h window
     held all K prior events."""
@@ -184,12 +187,20 @@ def test_config4_full_size_warm_pipelined():
         res = wk["resident"]
         got = []
         sat0 = eng.counter("window_saturated")
+        c0 = eng.counter("pipelined_compact_batches")
+        s0 = eng.counter("pipelined_slot_stream_batches")
         for b in range(P):  # back to back: no sync between the pipelined steps
+            if b < P - 1:  # the variant the bench times: no vectors requested -> compact vectors, fused kernel
+                out = sc.step({f: t[b * B:(b + 1) * B] for f, t in res.items()}, B)
+                got.append((None, None, out))
+                continue
             vec = torch.empty((B, 64), dtype=torch.float32, device=dev)
             mp = torch.empty((2, B), dtype=torch.float64, device=dev)
             out = sc.step({f: t[b * B:(b + 1) * B] for f, t in res.items()}, B, vectors=vec, model_probs=mp)
             got.append((vec, mp, out))
         torch.cuda.synchronize()
+        assert eng.counter("pipelined_compact_batches") - c0 == P - 1
+        assert eng.counter("pipelined_slot_stream_batches") - s0 == P  # 2^27 slots: the slot pass on its own stream
         o = OracleFeatureState(1 << 22, 1, K)
         pr = wk["profiles"]
         o.load_users(pr["key"], pr["avg_amount"], pr["account_age_days"], pr["device_fp"])
@@ -200,6 +211,20 @@ def test_config4_full_size_warm_pipelined():
             part = {f: v[b * B:(b + 1) * B] for f, v in wk["head"].items()}
             raw, rvec = o.run(part, want_raw=True)
             raws.append(raw)
+            FP, CF, DC, RK = (t.cpu().numpy() for t in out)
+            if vec is None:
+                # compact leg: the oracle chain on its OWN vectors (the engine's are never materialised); bar: the
+                # north star's 1e-5 on probabilities, decisions / risk exact off a threshold
+                px, _, _ = oracle.xgb_predict(xgb, rvec)
+                pi, _, _ = oracle.iforest_predict(ifm, rvec)
+                fp, conf, dec, risk = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]),
+                                                            [w[k] for k in names], [S.CONF_MULT[k] for k in names])
+                assert np.abs(FP - fp).max() <= 1e-5 and np.abs(CF - conf).max() <= 1e-5
+                near = np.abs(conf - 0.7) < 1e-6
+                for thr in (0.3, 0.6, 0.8, 0.95):
+                    near |= np.abs(fp - thr) < 1e-6
+                assert not ((DC != dec) & ~near).any() and not ((RK != risk) & ~near).any()
+                continue
             V = vec.cpu().numpy()
             _check_vectors(V, rvec)
             px, _, _ = oracle.xgb_predict(xgb, V)
@@ -208,7 +233,6 @@ def test_config4_full_size_warm_pipelined():
             assert np.abs(M[0] - px).max() <= 1e-5 and np.abs(M[1] - pi).max() <= 1e-5
             fp, conf, dec, risk = oracle.blend_weighted(np.stack([M[0], M[1]]), [w[k] for k in names],
                                                         [S.CONF_MULT[k] for k in names])
-            FP, CF, DC, RK = (t.cpu().numpy() for t in out)
             np.testing.assert_array_equal(FP, fp)
             np.testing.assert_array_equal(CF, conf)
             np.testing.assert_array_equal(DC, dec)
@@ -227,7 +251,9 @@ def test_config5_chain():
     """BASELINE configs[4]'s exact chain: 1 k micro-batches, card-state features + each card's last 10 events ->
     XGBoost 500 x 8 (tree-split path) + IsolationForest 100 + LSTM(128) on f32 MFMA (lstm_kernel4) -> 3-model blend,
     through fd_score_batch_device, against the oracle chain (oracle features + forests, lstm_ref's PyTorch fp32
-    forward over the oracle's card histories, scoring_ref's blend). State carried over 12 batches."""
+    forward over the oracle's card histories, scoring_ref's blend). State carried over 12 batches; the even ones request
+    no vectors / model probabilities (the bench's timed variant) and are checked on their outputs against the oracle
+    chain over its own vectors, the odd ones element by element."""
     import torch
 
     import oracle
@@ -265,11 +291,26 @@ def test_config5_chain():
                                                                      torch.uint8)]
             vec = torch.empty((B, 64), dtype=torch.float32, device="cuda")
             mp = torch.empty((3, B), dtype=torch.float64, device="cuda")
+            timed = b % 2 == 0  # the bench's timed variant: no vectors / model probabilities requested
             eng.score_batch_device(params, [0, 1, FD_SLOT_LSTM], {f: t[sl].data_ptr() for f, t in dev.items()}, B,
-                                   *[t.data_ptr() for t in out], vec_ptr=vec.data_ptr(), model_probs_ptr=mp.data_ptr())
+                                   *[t.data_ptr() for t in out], vec_ptr=0 if timed else vec.data_ptr(),
+                                   model_probs_ptr=0 if timed else mp.data_ptr())
             torch.cuda.synchronize()
             part = {k: v[sl] for k, v in tx.items()}
             rraw, rvec = o.run(part, want_raw=True)
+            if timed:  # the oracle chain on its own vectors and histories; LSTM f32 MFMA vs torch fp32 within 1e-5
+                px, _, _ = oracle.xgb_predict(xgb, rvec)
+                pi, _, _ = oracle.iforest_predict(ifm, rvec)
+                pl = R.lstm_forward(lw, hist.run(part["card_key"], rraw))
+                fp, conf, dec, risk = oracle.blend_weighted(np.stack([px.astype(np.float64), pi, pl]),
+                                                            [w[k] for k in names], [S.CONF_MULT[k] for k in names])
+                FP, CF, DC, RK = (t.cpu().numpy() for t in out)
+                assert np.abs(FP - fp).max() <= 1e-5 and np.abs(CF - conf).max() <= 1e-5
+                near = np.abs(conf - 0.7) < 1e-5
+                for thr in (0.3, 0.6, 0.8, 0.95):
+                    near |= np.abs(fp - thr) < 1e-5
+                assert not ((DC != dec) & ~near).any() and not ((RK != risk) & ~near).any()
+                continue
             V = vec.cpu().numpy()
             _check_vectors(V, rvec)
             Mp = mp.cpu().numpy()

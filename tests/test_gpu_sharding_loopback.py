@@ -240,3 +240,55 @@ def test_missing_peer_is_an_error_not_a_hang():
         else:
             os.environ["LOOPBACK_TIMEOUT_S"] = old
         e.close()
+
+
+@pytest.mark.timeout(120)
+def test_count_timeout_aborts_the_communicators():
+    """The engine's own guard: the loopback's groups return success but park their streams (LOOPBACK_STALL,
+    as RCCL's kernels block on a dead peer). The split-size wait gives up after comm_timeout_ms, aborts both
+    communicators (ncclCommAbort releases the parked streams) and raises; later steps are refused with the reason, and
+    sync / close return promptly instead of hanging on the stuck exchange."""
+    import time
+
+    import torch
+
+    from fdengine import FraudEngine
+    from fdengine._native import NativeError
+    from fdengine._native import TXN_FIELDS
+    from fdengine.sharding import EngineShardBackend, ShardedScorer
+    pop, streams, sizes, xgb, ifm = _setup(2)
+    path = str(LOOPBACK)
+    ids = (FraudEngine.comm_unique_id(path), FraudEngine.comm_unique_id(path))
+    e = _engine(pop, np.ones(N_USERS, bool), xgb, ifm)
+    saved = {k: os.environ.get(k) for k in ("LOOPBACK_STALL", "LOOPBACK_TIMEOUT_S")}
+    os.environ["LOOPBACK_STALL"] = "1"
+    os.environ["LOOPBACK_TIMEOUT_S"] = "30"  # safety only: the abort must release the streams long before
+    closed = False
+    try:
+        e.set_option("comm_timeout_ms", 1500)
+        b = _batches(streams, sizes, 0)[0]
+        d = {f: torch.from_numpy(np.ascontiguousarray(b[f])).cuda() for f in TXN_FIELDS}
+        torch.cuda.synchronize()
+        sc = ShardedScorer(EngineShardBackend(e, FraudEngine.blend_params([0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5]),
+                                              [0, 1], pipelined=True), 0, 2, native=True, comm=(path, ids))
+        t0 = time.monotonic()
+        with pytest.raises(NativeError) as ei:
+            sc.step(d, len(d["card_key"]))
+        assert "timed out" in str(ei.value) and "aborted" in str(ei.value), str(ei.value)
+        assert time.monotonic() - t0 < 15
+        with pytest.raises(NativeError) as ei2:  # the aborted communicators refuse further steps, with the reason
+            sc.step(d, len(d["card_key"]))
+        assert "communicators aborted" in str(ei2.value)
+        t1 = time.monotonic()
+        e.sync()  # the parked streams were released by the abort: no hang here
+        e.close()
+        closed = True
+        assert time.monotonic() - t1 < 10
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        if not closed:
+            e.close()
