@@ -218,6 +218,10 @@ def product_blend(names):
 _HIP = None
 
 
+def _diag_blocks() -> int:
+    return int(os.environ.get("FD_BENCH_BLOCKS", "0") or 0)
+
+
 def _parity_record(batches, path, rows_per_batch):
     """the parity_vs_oracle record: the timed path's batches (no vectors requested) and the vectors-requested twin"""
     def leg():
@@ -537,7 +541,7 @@ class Config3:
         eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
         eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
         self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches + 1 \
-            + args.loaded_iters + args.timing_steps + 1
+            + args.loaded_iters + args.timing_steps + 1 + _diag_blocks() * args.steps
         self.tx = synth.txn_stream(self.pop, self.n_batches * self.B, seed=200 + rank)
         self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
         self.elem = {f: self.tx[f].dtype.itemsize for f in N.TXN_FIELDS}
@@ -782,7 +786,7 @@ class Config4(Config3):
         self.parity_batches = args.parity_batches
         # + 1: the parity twin batch (vectors requested)
         self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches + 1 \
-            + args.loaded_iters + args.timing_steps + 1
+            + args.loaded_iters + args.timing_steps + 1 + _diag_blocks() * args.steps
         B = self.B
         h2d_batches = args.latency_iters if args.latency_iters > 0 else 0
         self.warm_info = None
@@ -1557,6 +1561,37 @@ def main():
     import gc
     gc.collect()
     gc.freeze()
+    # latency first (one micro-batch at a time, then the same from pinned host memory): besides p50 / p99, these
+    # ~400 steps bring the GPU out of the idle the parity check's CPU phase left it in. Measured (FD_BENCH_BLOCKS,
+    # profiles/r05/warm_blocks): right after an idle phase back-to-back steps run ~0.101 ms and reach the steady
+    # ~0.091 only after ~150 of them (clock / power ramp), so a short --steps region straight after the parity check
+    # timed the ramp, not the pipeline
+    lat = []
+    for i in range(args.latency_iters):
+        a = time.perf_counter()
+        if hasattr(wl, "step_to_host"):
+            wl.step_to_host(i, i)
+        else:
+            wl.step(i)
+            wl.fetch(i)
+        stream.synchronize()
+        lat.append(time.perf_counter() - a)
+    lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
+    p99 = float(np.percentile(lat_ms, 99))
+    # the same with the input columns crossing PCIe from pinned host memory first (workloads that support it)
+    lat_h2d = []
+    if hasattr(wl, "step_h2d") and args.latency_iters > 0:
+        for i in range(min(args.latency_iters, len(getattr(wl, "h2d_pool", [])) or args.latency_iters)):
+            a = time.perf_counter()
+            wl.step_h2d(i)  # H2D, the step, results in host memory
+            stream.synchronize()
+            lat_h2d.append(time.perf_counter() - a)
+    p99_h2d = float(np.percentile(np.array(lat_h2d) * 1e3, 99)) if lat_h2d else -1.0
+    if dist:  # the node's p99: the worst rank's
+        t = torch.tensor([p99, p99_h2d], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        p99, p99_h2d = (float(v) for v in t.tolist())
+
     for i in range(args.warmup):
         wl.step(i)
     torch.cuda.synchronize()
@@ -1578,6 +1613,16 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     host1 = _host_counters(eng)
+    # diagnostics (FD_BENCH_BLOCKS=N): N more blocks of --steps steps after the timed region, each bracketed by a
+    # synchronize, their ms per step in the line (is a short region's rate a first-block effect or its fill / drain?)
+    blocks = []
+    for _ in range(_diag_blocks()):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for i in range(args.steps):
+            wl.step(i)
+        torch.cuda.synchronize()
+        blocks.append(round((time.perf_counter() - a) / args.steps * 1e3, 5))
     # kernel durations: HIP events on the launch stream, on one launch in TIMING_EVERY of each kernel (an event
     # record costs stream time), over more of the same back-to-back steps AFTER the timed region, so the kernel
     # averages rest on >= 20 launches of each kernel and `value` carries no instrumentation
@@ -1664,32 +1709,6 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             loaded["p99_ms"] = float(t.item())
 
-    lat = []
-    for i in range(args.latency_iters):
-        a = time.perf_counter()
-        if hasattr(wl, "step_to_host"):
-            wl.step_to_host(i, i)
-        else:
-            wl.step(i)
-            wl.fetch(i)
-        stream.synchronize()
-        lat.append(time.perf_counter() - a)
-    lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
-    p99 = float(np.percentile(lat_ms, 99))
-    # the same with the input columns crossing PCIe from pinned host memory first (workloads that support it)
-    lat_h2d = []
-    if hasattr(wl, "step_h2d") and args.latency_iters > 0:
-        for i in range(min(args.latency_iters, len(getattr(wl, "h2d_pool", [])) or args.latency_iters)):
-            a = time.perf_counter()
-            wl.step_h2d(i)  # H2D, the step, results in host memory
-            stream.synchronize()
-            lat_h2d.append(time.perf_counter() - a)
-    p99_h2d = float(np.percentile(np.array(lat_h2d) * 1e3, 99)) if lat_h2d else -1.0
-    if dist:  # the node's p99: the worst rank's
-        t = torch.tensor([p99, p99_h2d], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        p99, p99_h2d = (float(v) for v in t.tolist())
-
     # the same kernels one micro-batch at a time, nothing beside them (in the pipelined stream the next batch's
     # feature kernels share the CUs with the forests): each kernel's unshared duration
     timing_alone = None
@@ -1764,6 +1783,8 @@ def main():
             "step_launch": "direct kernel launches",
             "engine_options": dict(kv.split("=") for kv in args.engine_option) or None,
         }
+        if blocks:
+            line["diag_blocks_ms_per_step"] = blocks
         if hasattr(wl, "counter_groups"):
             line["counters"] = pmc_counters(wl.name, args.batch, wl.counter_groups(roof), line["kernel_avg_us"])
         if wl.name in ("config3", "config4", "config5"):
