@@ -222,6 +222,11 @@ def _diag_blocks() -> int:
     return int(os.environ.get("FD_BENCH_BLOCKS", "0") or 0)
 
 
+def _diag_offset() -> int:
+    """FD_BENCH_BATCH_OFFSET=N (diagnostics): skip N resident micro-batches after the parity check"""
+    return int(os.environ.get("FD_BENCH_BATCH_OFFSET", "0") or 0)
+
+
 def _parity_record(batches, path, rows_per_batch):
     """the parity_vs_oracle record: the timed path's batches (no vectors requested) and the vectors-requested twin"""
     def leg():
@@ -541,7 +546,7 @@ class Config3:
         eng.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
         eng.load_merchants(M["fraud_rate"], M["risk_multiplier"])
         self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches + 1 \
-            + args.loaded_iters + args.timing_steps + 1 + _diag_blocks() * args.steps
+            + args.loaded_iters + args.timing_steps + 1 + _diag_blocks() * args.steps + _diag_offset()
         self.tx = synth.txn_stream(self.pop, self.n_batches * self.B, seed=200 + rank)
         self.dev = {f: torch.from_numpy(np.ascontiguousarray(self.tx[f])).to(dev) for f in N.TXN_FIELDS}
         self.elem = {f: self.tx[f].dtype.itemsize for f in N.TXN_FIELDS}
@@ -786,7 +791,7 @@ class Config4(Config3):
         self.parity_batches = args.parity_batches
         # + 1: the parity twin batch (vectors requested)
         self.n_batches = args.warmup + args.steps + args.latency_iters + args.alone_iters + args.parity_batches + 1 \
-            + args.loaded_iters + args.timing_steps + 1 + _diag_blocks() * args.steps
+            + args.loaded_iters + args.timing_steps + 1 + _diag_blocks() * args.steps + _diag_offset()
         B = self.B
         h2d_batches = args.latency_iters if args.latency_iters > 0 else 0
         self.warm_info = None
@@ -1556,41 +1561,43 @@ def main():
     except Exception as e:  # the oracle is only a checker; report, never fall back
         log(f"[rank {rank}] parity spot-check unavailable: {e!r}")
 
+    if _diag_offset() and hasattr(wl, "next_batch"):
+        wl.next_batch += _diag_offset()
     # a serving process's setup is done: move every object allocated so far out of the cyclic collector's view
     # (a full collection over the setup's objects stalls the host for milliseconds mid-stream)
     import gc
     gc.collect()
     gc.freeze()
-    # latency first (one micro-batch at a time, then the same from pinned host memory): besides p50 / p99, these
-    # ~400 steps bring the GPU out of the idle the parity check's CPU phase left it in. Measured (FD_BENCH_BLOCKS,
-    # profiles/r05/warm_blocks): right after an idle phase back-to-back steps run ~0.101 ms and reach the steady
-    # ~0.091 only after ~150 of them (clock / power ramp), so a short --steps region straight after the parity check
-    # timed the ramp, not the pipeline
-    lat = []
-    for i in range(args.latency_iters):
-        a = time.perf_counter()
-        if hasattr(wl, "step_to_host"):
-            wl.step_to_host(i, i)
-        else:
-            wl.step(i)
-            wl.fetch(i)
-        stream.synchronize()
-        lat.append(time.perf_counter() - a)
-    lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
-    p99 = float(np.percentile(lat_ms, 99))
-    # the same with the input columns crossing PCIe from pinned host memory first (workloads that support it)
-    lat_h2d = []
-    if hasattr(wl, "step_h2d") and args.latency_iters > 0:
-        for i in range(min(args.latency_iters, len(getattr(wl, "h2d_pool", [])) or args.latency_iters)):
+    # p50 / p99: one micro-batch at a time, then the same from pinned host memory (run after the throughput region:
+    # run before it they left the pipelined steps ~7 % slower for hundreds of steps, profiles/r05/warm_blocks)
+    def latency_loops():
+        lat = []
+        for i in range(args.latency_iters):
             a = time.perf_counter()
-            wl.step_h2d(i)  # H2D, the step, results in host memory
+            if hasattr(wl, "step_to_host"):
+                wl.step_to_host(i, i)
+            else:
+                wl.step(i)
+                wl.fetch(i)
             stream.synchronize()
-            lat_h2d.append(time.perf_counter() - a)
-    p99_h2d = float(np.percentile(np.array(lat_h2d) * 1e3, 99)) if lat_h2d else -1.0
-    if dist:  # the node's p99: the worst rank's
-        t = torch.tensor([p99, p99_h2d], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        p99, p99_h2d = (float(v) for v in t.tolist())
+            lat.append(time.perf_counter() - a)
+        lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
+        p99 = float(np.percentile(lat_ms, 99))
+        # the same with the input columns crossing PCIe from pinned host memory first (workloads that support it)
+        lat_h2d = []
+        if hasattr(wl, "step_h2d") and args.latency_iters > 0:
+            for i in range(min(args.latency_iters, len(getattr(wl, "h2d_pool", [])) or args.latency_iters)):
+                a = time.perf_counter()
+                wl.step_h2d(i)  # H2D, the step, results in host memory
+                stream.synchronize()
+                lat_h2d.append(time.perf_counter() - a)
+        p99_h2d = float(np.percentile(np.array(lat_h2d) * 1e3, 99)) if lat_h2d else -1.0
+        if dist:  # the node's p99: the worst rank's
+            t = torch.tensor([p99, p99_h2d], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            p99, p99_h2d = (float(v) for v in t.tolist())
+        return lat, lat_ms, p99, lat_h2d, p99_h2d
+
 
     for i in range(args.warmup):
         wl.step(i)
@@ -1708,6 +1715,8 @@ def main():
             t = torch.tensor([loaded["p99_ms"]], dtype=torch.float64, device=dev if DIST_BACKEND == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             loaded["p99_ms"] = float(t.item())
+
+    lat, lat_ms, p99, lat_h2d, p99_h2d = latency_loops()
 
     # the same kernels one micro-batch at a time, nothing beside them (in the pipelined stream the next batch's
     # feature kernels share the CUs with the forests): each kernel's unshared duration
