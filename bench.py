@@ -222,6 +222,21 @@ def _diag_blocks() -> int:
     return int(os.environ.get("FD_BENCH_BLOCKS", "0") or 0)
 
 
+def _dump_fprof(tag) -> None:
+    """FD_BENCH_DUMP_FPROF=prefix with the profiling library (FDENGINE_LIB=.../libfdengine_prof.so): the feature
+    kernels' per-workgroup phase stamps of the last launch, saved as prefix.<tag>.npy (tools/lean_phases.py)"""
+    pre = os.environ.get("FD_BENCH_DUMP_FPROF")
+    if not pre:
+        return
+    import ctypes
+    import numpy as np
+    from fdengine import _native
+    buf = np.zeros(4096 * 8, np.uint64)
+    _native.lib.fd_debug_feat_profile.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    if _native.lib.fd_debug_feat_profile(buf.ctypes.data, buf.size) == 0:
+        np.save(f"{pre}.{tag}.npy", buf)
+
+
 def _diag_offset() -> int:
     """FD_BENCH_BATCH_OFFSET=N (diagnostics): skip N resident micro-batches after the parity check"""
     return int(os.environ.get("FD_BENCH_BATCH_OFFSET", "0") or 0)
@@ -1620,6 +1635,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     host1 = _host_counters(eng)
+    _dump_fprof(0)
     # diagnostics (FD_BENCH_BLOCKS=N): N more blocks of --steps steps after the timed region, each bracketed by a
     # synchronize, their ms per step in the line (is a short region's rate a first-block effect or its fill / drain?)
     blocks = []
@@ -1630,6 +1646,7 @@ def main():
             wl.step(i)
         torch.cuda.synchronize()
         blocks.append(round((time.perf_counter() - a) / args.steps * 1e3, 5))
+        _dump_fprof(len(blocks))
     # kernel durations: HIP events on the launch stream, on one launch in TIMING_EVERY of each kernel (an event
     # record costs stream time), over more of the same back-to-back steps AFTER the timed region, so the kernel
     # averages rest on >= 20 launches of each kernel and `value` carries no instrumentation

@@ -665,6 +665,7 @@ struct BucketArgs {
   unsigned spec;                      // latency batches: region entries read before the fill count (<= kBT, <= C)
   bool spread;                        // card segments dealt round-robin over the 4 waves (engine option bucket_spread)
   bool prio;                          // issue priority 2 (engine option feature_prio, pipelined stream)
+  bool split_sort;                    // lean kernel: rank_sort_split for <= kBT keys (engine option split_sort)
 };
 
 // gather (latency batches, n <= kChunkCap, engine option slot_gather; feat_bucket_gather_kernel): no slot launch;
@@ -1030,6 +1031,34 @@ __device__ void rank_sort(unsigned long long* k, int m) {
   __syncthreads();
 }
 
+// The same ranks for m <= kBT keys with every thread working: key j's rank is summed over P = kBT / m' parts of the
+// key list (m' = m rounded up to a power of two >= 64), each thread scanning one part for one key, the partial ranks
+// added into rk[] (zeroed by the caller before the barrier that published the keys). The full form gives each of
+// the first m threads all m compares and leaves the other waves idle — with m ~ 128 on the pipelined stream half its
+// VALU issue, spent beside the fused ensemble kernel's waves on the same SIMDs.
+__device__ void rank_sort_split(unsigned long long* k, int m, int* rk) {
+  int mp = 64;
+  while (mp < m) mp <<= 1;
+  const int P = kBT / mp;
+  const int j = (int)threadIdx.x & (mp - 1), p = (int)threadIdx.x / mp;
+  const int L = (((m + P - 1) / P) + 1) & ~1;  // even: the part starts on a 16-B pair
+  const int lo = min(m, p * L), hi = min(m, lo + L);
+  const unsigned long long mine = j < m ? k[j] : 0ull;
+  const unsigned long long own = (int)threadIdx.x < m ? k[threadIdx.x] : 0ull;
+  const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(k);
+  int r = 0;
+#pragma unroll 4
+  for (int q = lo; q + 1 < hi; q += 2) {
+    const ulonglong2 v = k2[q >> 1];
+    r += (int)(v.x < mine) + (int)(v.y < mine);
+  }
+  if ((hi - lo) & 1) r += (int)(k[hi - 1] < mine);
+  if (j < m && r) atomicAdd(&rk[j], r);
+  __syncthreads();
+  if ((int)threadIdx.x < m) k[rk[threadIdx.x]] = own;
+  __syncthreads();
+}
+
 // m keys (slot << 32 | arrival index) already in LDS skeys[0, m): sort, then process every segment
 template <int MODE>
 __device__ void process_sorted(const BucketArgs& a, unsigned long long* skeys, int m, LongLds& sm, int* long_list,
@@ -1266,8 +1295,10 @@ constexpr int kLeanCap = 512;
 template <int MODE>
 __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, BucketScratch* scratch) {
   __shared__ __attribute__((aligned(16))) unsigned long long skeys[kLeanCap];
+  __shared__ int rk[kBT];
   __shared__ int any_long;
   if (a.prio) __builtin_amdgcn_s_setprio(2);
+  FD_FSTAMP(0);
   const int b = blockIdx.x;
   const unsigned m = a.fill[b];
   if (threadIdx.x == 0) any_long = 0;
@@ -1275,8 +1306,13 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
   if (!slow) {
     const unsigned long long* src = a.pairs + (size_t)b * a.C;
     for (unsigned q = threadIdx.x; q < m; q += kBT) skeys[q] = src[q];
+    rk[threadIdx.x] = 0;
     __syncthreads();
-    if (m > 1) rank_sort(skeys, (int)m);
+    FD_FSTAMP(1);
+    if (m > 1) {
+      if (m <= (unsigned)kBT && a.split_sort) rank_sort_split(skeys, (int)m, rk);
+      else rank_sort(skeys, (int)m);
+    }
     for (int pos = threadIdx.x; pos < (int)m; pos += kBT) {
       const unsigned s = (unsigned)(skeys[pos] >> 32);
       if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;
@@ -1284,6 +1320,7 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
     }
     __syncthreads();
     slow = any_long != 0;
+    FD_FSTAMP(2);
   }
   if (slow) {
     BucketScratch& w = scratch[b];
@@ -1297,6 +1334,11 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
     while (pos + len < (int)m && (unsigned)(skeys[pos + len] >> 32) == s) ++len;
     process_short<MODE>(a, s, skeys + pos, len);
   }
+#ifdef FD_FOREST_PROFILE
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)
+    g_fprof[blockIdx.x * 8 + 4 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();
+#endif
+  FD_FSTAMP(3);
   if (threadIdx.x == 0) {  // the next batch's counters (it runs after this launch on the stream)
     a.fill[b] = 0u;
     if (b == 0) a.ovf_cnt[a.par ^ 1] = 0u;
@@ -1885,6 +1927,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   // step; config 5 (1 k, 16 keys: 1 wave -> 4 waves of 4 lanes) the card loop 2x slower (profiles/r04/config5)
   a.spread = st.bucket_spread && n >= 8192;
   a.prio = lean && st.feat_prio;
+  a.split_sort = st.split_sort;
   a.spec = n < 8192 ? (unsigned)std::min<int64_t>({(int64_t)kBT, (int64_t)C, 4 * ((n + nb - 1) / nb)}) : 0u;
   GatherArgs ga{};
   if (gather) {

@@ -1,5 +1,5 @@
-"""GPU: the native N >= 2 sharded step (fd_sharded_step, csrc/comm.hip + engine.hip) executed with 2 and 4 ranks on
-the test box's one GPU, checked against the CPU oracle chain over the global arrival order.
+"""GPU: the native N >= 2 sharded step (fd_sharded_step, csrc/comm.hip + engine.hip) executed with 2, 4 and 8 ranks
+(8: the node size BASELINE configs[3] names) on the test box's one GPU, checked against the CPU oracle chain over the global arrival order.
 
 RCCL refuses two ranks on one device, so the ranks here are threads of one process, each driving its own engine
 (its cards' state, loaded with only the users it owns) through ShardedScorer's native path — the code `bench.py
@@ -177,7 +177,7 @@ def _oracle(pop, streams, sizes, xgb, ifm, world):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world,slot_stream", [(2, -1), (4, -1), (2, 2), (4, 2)])
+@pytest.mark.parametrize("world,slot_stream", [(2, -1), (4, -1), (8, -1), (2, 2), (4, 2), (8, 2)])
 def test_native_sharded_step_loopback_matches_oracle(world, slot_stream):
     """slot_stream 2: the owner pipeline's slot pass on its own stream, as the config-4 card table runs it"""
     from fdengine.engine import shard_of
