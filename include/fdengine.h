@@ -671,8 +671,9 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      forests after the first on one side stream (0.095), 2 on two side streams (0.095)
      "pipeline_lean": fd_score_batch_pipelined's bucket pass, 1 (default) the lean kernel that fits beside the
      fused ensemble kernel, 0 the full bucket kernel
-     "split_sort": the lean bucket kernel's key sort for <= 256 keys, 1 (default) every thread ranks one key over
-     a part of the list (partial ranks summed in LDS), 0 the first m threads each rank one key over the whole list
+     "lean_group": how the lean bucket kernel groups a bucket's keys by card (outputs identical): 2 (default) an
+     LDS hash table of card slots (no sort), 1 a rank sort split over all threads, 0 the first m threads each rank
+     one key over the whole list
      (further options — "slot_stream", "slot_gather", "bucket_spread", "feature_prio", "ensemble_prio",
      "compact_vectors", "latency_fused", "seq_ring_lstm", "bucket_keys" — are listed with their measurements in
      DESIGN.md §3)

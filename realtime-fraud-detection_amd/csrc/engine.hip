@@ -537,10 +537,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(value == 0 || (value >= 8 && value <= 512 && (value & (value - 1)) == 0), FD_ERR_INVALID_ARG,
                "bucket_keys must be 0 or a power of two in 8..512");
     e.state.bucket_keys = (int)value;
-  } else if (k == "split_sort") {  // pipelined stream: 1 (default) the lean bucket kernel ranks <= 256 keys with all
-    // 256 threads (partial ranks over key-list parts), 0 the first m threads each rank one key over the whole list
-    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "split_sort must be 0 or 1");
-    e.state.split_sort = value != 0;
+  } else if (k == "lean_group") {  // pipelined stream: the lean bucket kernel's grouping of a bucket's keys by card,
+    // 0 rank sort (first m threads, whole list each), 1 rank sort split over all threads, 2 (default) LDS hash table
+    FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "lean_group must be 0, 1 or 2");
+    e.state.lean_group = (int)value;
   } else if (k == "slot_gather") {  // batches of <= 4096 transactions outside the pipelined stream: card slots found
     // inside the bucket kernel, no slot launch (1, default) / the slot kernel first (0)
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "slot_gather must be 0 or 1");

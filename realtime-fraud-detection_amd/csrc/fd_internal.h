@@ -323,8 +323,9 @@ struct CardStore {
   // option "slot_gather": batches of <= 4096 transactions outside the pipelined stream find their card slots inside
   // the bucket kernel (each bucket workgroup takes the keys that hash to it), no slot launch (features.hip)
   bool slot_gather = true;
-  // option "split_sort": the lean bucket kernel ranks <= 256 keys with every thread (rank_sort_split)
-  bool split_sort = true;
+  // option "lean_group": how the lean bucket kernel groups a bucket's keys by card — 0 rank sort, 1 rank sort split
+  // over every thread (rank_sort_split), 2 (default) LDS hash table (no sort)
+  int lean_group = 2;
   bool feat_prio = false;  // option "feature_prio": the pipelined stream's feature kernels issue at priority 2
   int64_t n_merchants = 0;
   DeviceBuffer pages, keys, merchants, err, seq;  // pages: CardPages (header + ring per slot); keys: the compact

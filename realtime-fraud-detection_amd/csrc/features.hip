@@ -665,7 +665,7 @@ struct BucketArgs {
   unsigned spec;                      // latency batches: region entries read before the fill count (<= kBT, <= C)
   bool spread;                        // card segments dealt round-robin over the 4 waves (engine option bucket_spread)
   bool prio;                          // issue priority 2 (engine option feature_prio, pipelined stream)
-  bool split_sort;                    // lean kernel: rank_sort_split for <= kBT keys (engine option split_sort)
+  int lean_group;                     // lean kernel grouping: 0 rank sort, 1 split rank sort, 2 hash (option lean_group)
 };
 
 // gather (latency batches, n <= kChunkCap, engine option slot_gather; feat_bucket_gather_kernel): no slot launch;
@@ -698,8 +698,8 @@ __device__ __forceinline__ int first_pos(bool spread) {
   return spread ? (((t & 63) << 2) | (t >> 6)) : t;
 }
 
-template <int MODE>
-__device__ void process_short(const BucketArgs& a, unsigned s, const unsigned long long* keys, int len) {
+template <int MODE, typename KeyT = unsigned long long>
+__device__ void process_short(const BucketArgs& a, unsigned s, const KeyT* keys, int len) {
   CardHeader* h = a.P.hdr(s);
   CardRegs c;
   Profile p;
@@ -1291,32 +1291,67 @@ struct BucketScratch {
 // segment short — is sorted and walked in LDS; any other bucket (a hot card) takes the full bucket kernel's
 // code with its working set in a per-bucket global scratch block (L1/L2-resident; same results, no launch
 // that would have to wait for a whole CU).
-constexpr int kLeanCap = 512;
+constexpr int kLeanCap = 256;  // a bucket of ~128 keys on average; a larger one takes the slow path
+// Lean grouping (engine option lean_group, default 2): the bucket's keys need only be grouped by card, each card's
+// transactions in arrival order — not sorted. Each key's card slot goes into a 256-entry LDS hash table (atomic CAS
+// insert, then an atomic count per card); a card of one transaction (nearly all at 64 k over 100 M cards) is
+// processed at once, a card of several by the thread whose key inserted it, which gathers and orders that card's
+// arrival indices. Two LDS atomics per key instead of the sort's ~m / 2 16-B LDS reads, which queue behind the
+// fused ensemble kernel's LDS traffic on the same CU (lean phases, profiles/r05/lean_phases).
+constexpr int kHashCap = 256;
+constexpr unsigned kHashEmpty = 0xffffffffu;
+constexpr int kLeadBit = 1 << 30;  // rk[pos]: the table entry of the key at pos, | kLeadBit where it inserted the card
+static_assert(kHashCap == kBT, "one table entry per thread at initialisation");
+
 template <int MODE>
 __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, BucketScratch* scratch) {
+  // 6 KiB: beside a running ensemble_kernel workgroup (148 of the CU's 160 KiB) with room to spare
   __shared__ __attribute__((aligned(16))) unsigned long long skeys[kLeanCap];
-  __shared__ int rk[kBT];
-  __shared__ int any_long;
+  __shared__ int rk[kBT];  // split sort: partial ranks; hash grouping: each position's table entry (+ kLeadBit)
+  __shared__ unsigned hslot[kHashCap], hcnt[kHashCap];
+  __shared__ unsigned pool[kHashCap];  // the arrival indices of several-transaction cards, in order
+  __shared__ int any_long, pool_n;
   if (a.prio) __builtin_amdgcn_s_setprio(2);
   FD_FSTAMP(0);
   const int b = blockIdx.x;
+  const int t = (int)threadIdx.x;
   const unsigned m = a.fill[b];
-  if (threadIdx.x == 0) any_long = 0;
+  if (t == 0) any_long = 0, pool_n = 0;
   bool slow = m > (unsigned)kLeanCap || m > a.C;
+  const bool hashed = a.lean_group == 2;
   if (!slow) {
     const unsigned long long* src = a.pairs + (size_t)b * a.C;
     for (unsigned q = threadIdx.x; q < m; q += kBT) skeys[q] = src[q];
-    rk[threadIdx.x] = 0;
+    rk[t] = 0;
+    if (hashed) {
+      hslot[t] = kHashEmpty;
+      hcnt[t] = 0u;
+    }
     __syncthreads();
     FD_FSTAMP(1);
-    if (m > 1) {
-      if (m <= (unsigned)kBT && a.split_sort) rank_sort_split(skeys, (int)m, rk);
-      else rank_sort(skeys, (int)m);
-    }
-    for (int pos = threadIdx.x; pos < (int)m; pos += kBT) {
-      const unsigned s = (unsigned)(skeys[pos] >> 32);
-      if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;
-      if (pos + kSegLong < (int)m && (unsigned)(skeys[pos + kSegLong] >> 32) == s) any_long = 1;
+    if (hashed) {
+      if (t < (int)m) {
+        const unsigned s = (unsigned)(skeys[t] >> 32);
+        unsigned h = (unsigned)(mix64(s) >> 32) & (kHashCap - 1);
+        unsigned old;
+        for (;;) {
+          old = atomicCAS(&hslot[h], kHashEmpty, s);
+          if (old == kHashEmpty || old == s) break;
+          h = (h + 1) & (kHashCap - 1);
+        }
+        rk[t] = (int)h | (old == kHashEmpty ? kLeadBit : 0);
+        if (atomicAdd(&hcnt[h], 1u) >= (unsigned)kSegLong) any_long = 1;  // a card past kSegLong transactions
+      }
+    } else {
+      if (m > 1) {
+        if (a.lean_group == 1) rank_sort_split(skeys, (int)m, rk);
+        else rank_sort(skeys, (int)m);
+      }
+      for (int pos = t; pos < (int)m; pos += kBT) {
+        const unsigned s = (unsigned)(skeys[pos] >> 32);
+        if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;
+        if (pos + kSegLong < (int)m && (unsigned)(skeys[pos + kSegLong] >> 32) == s) any_long = 1;
+      }
     }
     __syncthreads();
     slow = any_long != 0;
@@ -1327,19 +1362,49 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
     bucket_body<MODE>(a, b, w.keys, w.sm, w.long_list, w.n_long, w.chunk_m);
     return;
   }
-  for (int pos = first_pos(a.spread); pos < (int)m; pos += kBT) {
-    const unsigned s = (unsigned)(skeys[pos] >> 32);
-    if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;
-    int len = 1;
-    while (pos + len < (int)m && (unsigned)(skeys[pos + len] >> 32) == s) ++len;
-    process_short<MODE>(a, s, skeys + pos, len);
+  if (hashed) {
+    for (int pos = first_pos(a.spread); pos < (int)m; pos += kBT) {
+      const unsigned long long k = skeys[pos];
+      const unsigned s = (unsigned)(k >> 32);
+      const int e = rk[pos];
+      const unsigned c = hcnt[e & (kHashCap - 1)];
+      if (c == 1u) {
+        process_short<MODE>(a, s, skeys + pos, 1);
+        continue;
+      }
+      if (!(e & kLeadBit)) continue;  // the thread whose key inserted the card processes all of its transactions
+      const int base = atomicAdd(&pool_n, (int)c);
+      int w = 0;
+      for (int q = 0; q < (int)m; ++q) {
+        const unsigned long long x = skeys[q];
+        if ((unsigned)(x >> 32) == s) pool[base + w++] = (unsigned)x;
+      }
+      for (int x = 1; x < w; ++x) {  // arrival order
+        const unsigned v = pool[base + x];
+        int y = x - 1;
+        while (y >= 0 && pool[base + y] > v) {
+          pool[base + y + 1] = pool[base + y];
+          --y;
+        }
+        pool[base + y + 1] = v;
+      }
+      process_short<MODE>(a, s, pool + base, w);
+    }
+  } else {
+    for (int pos = first_pos(a.spread); pos < (int)m; pos += kBT) {
+      const unsigned s = (unsigned)(skeys[pos] >> 32);
+      if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;
+      int len = 1;
+      while (pos + len < (int)m && (unsigned)(skeys[pos + len] >> 32) == s) ++len;
+      process_short<MODE>(a, s, skeys + pos, len);
+    }
   }
 #ifdef FD_FOREST_PROFILE
   if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)
     g_fprof[blockIdx.x * 8 + 4 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();
 #endif
   FD_FSTAMP(3);
-  if (threadIdx.x == 0) {  // the next batch's counters (it runs after this launch on the stream)
+  if (t == 0) {  // the next batch's counters (it runs after this launch on the stream)
     a.fill[b] = 0u;
     if (b == 0) a.ovf_cnt[a.par ^ 1] = 0u;
   }
@@ -1927,7 +1992,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   // step; config 5 (1 k, 16 keys: 1 wave -> 4 waves of 4 lanes) the card loop 2x slower (profiles/r04/config5)
   a.spread = st.bucket_spread && n >= 8192;
   a.prio = lean && st.feat_prio;
-  a.split_sort = st.split_sort;
+  a.lean_group = st.lean_group;
   a.spec = n < 8192 ? (unsigned)std::min<int64_t>({(int64_t)kBT, (int64_t)C, 4 * ((n + nb - 1) / nb)}) : 0u;
   GatherArgs ga{};
   if (gather) {
