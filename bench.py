@@ -157,7 +157,7 @@ def pmc_counters(workload, B, groups, live_us, root=None):
 
 
 def ensemble_symbol(out, wide):
-    return f"fd::anon::ensemble_kernel<8, {out}, {'true' if wide else 'false'}>"
+    return f"fd::anon::ensemble_kernel<8, {out}, {'true' if wide else 'false'}, true>"
 FOREST6_SYMBOL = "fd::anon::forest_kernel6<8, 24, float, 1, 0>"
 LSTM4_SYMBOL = "fd::anon::lstm_kernel4"
 INGEST_SYMBOL = "fd::anon::ingest_json_kernel"
@@ -235,6 +235,10 @@ def _dump_fprof(tag) -> None:
     _native.lib.fd_debug_feat_profile.argtypes = [ctypes.c_void_p, ctypes.c_int]
     if _native.lib.fd_debug_feat_profile(buf.ctypes.data, buf.size) == 0:
         np.save(f"{pre}.{tag}.npy", buf)
+    buf2 = np.zeros(4096 * 4, np.uint64)
+    _native.lib.fd_debug_feat_profile2.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    if _native.lib.fd_debug_feat_profile2(buf2.ctypes.data, buf2.size) == 0:
+        np.save(f"{pre}.{tag}.c.npy", buf2)
 
 
 def _diag_offset() -> int:

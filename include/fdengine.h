@@ -671,6 +671,8 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      forests after the first on one side stream (0.095), 2 on two side streams (0.095)
      "pipeline_lean": fd_score_batch_pipelined's bucket pass, 1 (default) the lean kernel that fits beside the
      fused ensemble kernel, 0 the full bucket kernel
+     "ensemble_int_lut": the fused kernel's compact rows, 1 (default) the eight small-integer slots binned by one
+     lookup in a per-plan table of the bins of 0..31, 0 searched like the others (outputs identical)
      "lean_group": how the lean bucket kernel groups a bucket's keys by card (outputs identical): 2 (default) an
      LDS hash table of card slots (no sort), 1 a rank sort split over all threads, 0 the first m threads each rank
      one key over the whole list

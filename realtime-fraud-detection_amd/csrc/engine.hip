@@ -537,6 +537,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(value == 0 || (value >= 8 && value <= 512 && (value & (value - 1)) == 0), FD_ERR_INVALID_ARG,
                "bucket_keys must be 0 or a power of two in 8..512");
     e.state.bucket_keys = (int)value;
+  } else if (k == "ensemble_int_lut") {  // the fused kernel's compact rows: 1 (default) the eight small-integer slots
+    // (hour, day of week, weekend, counts, account age, new device) binned by a per-plan table lookup, 0 searched
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_int_lut must be 0 or 1");
+    e.ens_int_lut = value != 0;
   } else if (k == "lean_group") {  // pipelined stream: the lean bucket kernel's grouping of a bucket's keys by card,
     // 0 rank sort (first m threads, whole list each), 1 rank sort split over all threads, 2 (default) LDS hash table
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "lean_group must be 0, 1 or 2");

@@ -92,6 +92,7 @@ struct EnsArgs {
   int vec4;                       // rows 16-B aligned (ld % 4 == 0, aligned X): float4 row loads
   int compact;                    // X rows are the compact vector (kCompactWidth floats), binned here
   uint16_t cbin[kMaxFeatures];    // compact mode: the bins of the constant slots (0 or 0.5), per plan
+  alignas(4) uint16_t lut[8 * 32];  // compact mode: [kIntSlots][kLutN] bins of the small-integer slots' values 0..31
   int owner_fixed;                // chunk owner: tree group 0 (the oldest waves: highest issue priority), else rotating
   int prio;                       // issue priority 2 above the co-running feature kernels (engine option ensemble_prio)
   int n_pass;
@@ -301,24 +302,87 @@ __device__ __forceinline__ void bin_compact_constants(const EnsArgs& a, uint16_t
   }
 }
 
-template <int Q, int L>
+// The compact slots whose values are always small integers — hour, day of week, weekend, the 1 h / 24 h / 5 min
+// counts and the account age (each clip10 of an integer), the new-device flag (features.hip write_vector) — are
+// binned by one lookup in a per-plan table of the bins of 0..31 (staged in LDS), not searched: each thread keeps 3-4
+// searches of its 5-6 (one lockstep group instead of two). A value outside 0..31 or not integral (never, from the
+// engine's own feature kernel) takes its own search, so the bins stay #{t <= v} for any input.
+constexpr int kIntSlots = 8;
+constexpr int kIntCompact[kIntSlots] = {2, 3, 4, 5, 6, 9, 12, 15};  // compact indices (features 5 6 7 14 15 19 26 32)
+constexpr int kLutN = 32;
+static_assert(kIntSlots * kLutN == 8 * 32, "EnsArgs::lut");
+__host__ __device__ constexpr int int_slot(int ci) {
+  for (int k = 0; k < kIntSlots; ++k)
+    if (kIntCompact[k] == ci) return k;
+  return -1;
+}
+// thread Q's compact indices Q + 4 i: the LUT row of each small-integer one (-1: searched), and the searched i's
+constexpr int kIntOf[4][6] = {{-1, 2, -1, 6, -1, -1}, {-1, 3, 5, -1, -1, -1}, {0, 4, -1, -1, -1, -1},
+                              {1, -1, -1, 7, -1, -1}};
+constexpr int kNSearched[4] = {4, 4, 3, 3};
+constexpr int kSearched[4][4] = {{0, 2, 4, 5}, {0, 3, 4, 5}, {2, 3, 4, 0}, {1, 2, 4, 0}};
+constexpr bool int_tables_agree() {
+  for (int q = 0; q < 4; ++q) {
+    int ns = 0;
+    for (int i = 0; i < 6; ++i) {
+      const int ci = q + 4 * i;
+      const int want = ci < kCompactSlots ? int_slot(ci) : -1;
+      if (kIntOf[q][i] != want) return false;
+      if (ci < kCompactSlots && want < 0) {
+        if (ns >= 4 || kSearched[q][ns] != i) return false;
+        ++ns;
+      }
+    }
+    if (ns != kNSearched[q]) return false;
+  }
+  return true;
+}
+static_assert(int_tables_agree(), "kIntOf / kSearched must follow kIntCompact and kCompactSlot");
+
+template <int Q, int L, bool LUT>
 __device__ __forceinline__ void bin_compact_pass(const EnsArgs& a, const float (&v)[16], uint16_t* Xs,
                                                  int txn, int f0, int f1, bool glob, uint32_t tl, int o0,
-                                                 int& anynan) {
+                                                 int& anynan, uint32_t lut) {
   constexpr int NV = (kCompactSlots - Q + 3) / 4;  // compact slots Q, Q + 4, ... below kCompactSlots
+  constexpr int NS = LUT ? kNSearched[Q] : NV;
+  // the small-integer slots: one LDS lookup each
 #pragma unroll
-  for (int g0 = 0; g0 < NV; g0 += L) {
+  for (int i = 0; i < NV; ++i) {
+    const int ks = LUT ? kIntOf[Q][i] : -1;
+    if (ks < 0) continue;
+    const int f = kCompactSlot[Q + 4 * i];
+    if (!(f >= f0 && f < f1 && f < a.nf)) continue;  // wave-uniform
+    const float x = v[i];
+    uint16_t bin;
+    if (x != x) {
+      anynan = 1;
+      bin = (uint16_t)0xFFFFu;
+    } else if (x >= 0.f && x < (float)kLutN && x == truncf(x)) {
+      bin = lds_load<uint16_t>(lut + (uint32_t)(ks * kLutN + (int)x) * 2u);
+    } else {  // #{t <= x} over the feature's merged table in global memory: binary lifting with a fixed trip count
+      // (tables hold < 2^16 thresholds), straight-line code, so this loop over i stays unrolled and v[] in registers
+      const int o = a.thr_off[f], cnt = a.thr_off[f + 1] - o;
+      int pos = 0;
+#pragma unroll
+      for (int st = 1 << 15; st > 0; st >>= 1)
+        if (pos + st <= cnt && a.thr[o + pos + st - 1] <= x) pos += st;
+      bin = (uint16_t)pos;
+    }
+    Xs[(f >> 1) * 512 + txn * 2 + (f & 1)] = bin;
+  }
+  // the others: binary lifting in lockstep groups of L
+#pragma unroll
+  for (int g0 = 0; g0 < NS; g0 += L) {
     float vv[L];
     int o[L], cnt[L], pos[L];
     bool act[L];
     int steps = 0;
 #pragma unroll
     for (int k = 0; k < L; ++k) {
-      const int i = g0 + k;
-      const int ci = Q + 4 * (i < NV ? i : 0);
-      const int f = kCompactSlot[ci];
-      act[k] = i < NV && f >= f0 && f < f1 && f < a.nf;
-      vv[k] = act[k] ? v[i < NV ? i : 0] : 0.f;  // v[i]: compact slot Q + 4 i of the row
+      const int i = LUT ? kSearched[Q][g0 + k < NS ? g0 + k : 0] : (g0 + k < NS ? g0 + k : 0);
+      const int f = kCompactSlot[Q + 4 * i];
+      act[k] = g0 + k < NS && f >= f0 && f < f1 && f < a.nf;
+      vv[k] = act[k] ? v[i] : 0.f;  // v[i]: compact slot Q + 4 i of the row
       o[k] = act[k] ? a.thr_off[f] : o0;
       cnt[k] = act[k] ? a.thr_off[f + 1] - o[k] : 0;
       pos[k] = 0;
@@ -327,8 +391,8 @@ __device__ __forceinline__ void bin_compact_pass(const EnsArgs& a, const float (
     search_lockstep<L>(vv, o, cnt, pos, steps, glob, tl, o0, a.thr);
 #pragma unroll
     for (int k = 0; k < L; ++k) {
-      const int i = g0 + k;
-      const int f = kCompactSlot[Q + 4 * (i < NV ? i : 0)];
+      const int i = LUT ? kSearched[Q][g0 + k < NS ? g0 + k : 0] : (g0 + k < NS ? g0 + k : 0);
+      const int f = kCompactSlot[Q + 4 * i];
       if (act[k]) {
         const bool nan = vv[k] != vv[k];
         anynan |= nan ? 1 : 0;
@@ -338,7 +402,7 @@ __device__ __forceinline__ void bin_compact_pass(const EnsArgs& a, const float (
   }
 }
 
-template <int D, int OUT, bool WIDE>
+template <int D, int OUT, bool WIDE, bool LUT = true>
 __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   constexpr int kCHA = EnsCfg<WIDE>::CHA, kCHB = EnsCfg<WIDE>::CHB;
   constexpr uint32_t kEnsBuf = EnsCfg<WIDE>::BUF;
@@ -412,6 +476,10 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
 #ifdef FD_FOREST_PROFILE
     pr_st[0] = __builtin_amdgcn_s_memtime();
 #endif
+    // compact mode: the small-integer slots' bin table into the accumulator area (unused until the chunk loop)
+    // (published by the first pass's staging barrier: no barrier of its own)
+    if (LUT && a.compact && tid < kIntSlots * kLutN / 2)
+      lds_store<uint32_t>(accA + (uint32_t)tid * 4u, reinterpret_cast<const uint32_t*>(a.lut)[tid]);
     // (2) per pass: stage its tables, then bin this thread's features of the pass kLock at a time (independent
     // searches in lockstep, so kLock LDS reads are in flight per step) into the u16 tile
     constexpr int kLock = 4;  // 8 measured slower (bank conflicts of the diverging searches, not latency)
@@ -434,16 +502,25 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
         }
         for (; i < cnt; i += kEnsWG) tp[thr_pad(i)] = a.thr[o0 + i];
         __syncthreads();
+      } else if (LUT && a.compact && p == 0) {
+        __syncthreads();  // the small-integer table
       }
 #ifdef FD_FOREST_PROFILE
       if (p < 3) pr_st[1 + 2 * p] = __builtin_amdgcn_s_memtime();
 #endif
-      if (valid && a.compact) {
+      if (LUT && valid && a.compact) {
         switch (q) {
-          case 0: bin_compact_pass<0, kLock>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
-          case 1: bin_compact_pass<1, kLock>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
-          case 2: bin_compact_pass<2, kLock>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
-          default: bin_compact_pass<3, kLock>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan); break;
+          case 0: bin_compact_pass<0, kLock, true>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan, accA); break;
+          case 1: bin_compact_pass<1, kLock, true>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan, accA); break;
+          case 2: bin_compact_pass<2, kLock, true>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan, accA); break;
+          default: bin_compact_pass<3, kLock, true>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan, accA); break;
+        }
+      } else if (valid && a.compact) {
+        switch (q) {
+          case 0: bin_compact_pass<0, kLock, false>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan, accA); break;
+          case 1: bin_compact_pass<1, kLock, false>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan, accA); break;
+          case 2: bin_compact_pass<2, kLock, false>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan, accA); break;
+          default: bin_compact_pass<3, kLock, false>(a, v, Xs, txn, f0, f1, glob, tl, o0, anynan, accA); break;
         }
       } else if (valid) {
 #pragma unroll
@@ -655,7 +732,12 @@ const void* pick_ensemble(int D) {
   }
 }
 
-const void* pick_ensemble(int out, bool wide, int D) {
+const void* pick_ensemble(int out, bool wide, int D, bool lut) {
+  // engine option ensemble_int_lut 0 (A/B): the pipeline's instantiations without the small-integer table
+  if (!lut && D == 8 && out == 0)
+    return wide ? (const void*)ensemble_kernel<8, 0, true, false> : (const void*)ensemble_kernel<8, 0, false, false>;
+  if (!lut && D == 8 && out == 1)
+    return wide ? (const void*)ensemble_kernel<8, 1, true, false> : (const void*)ensemble_kernel<8, 1, false, false>;
   if (wide) return out == 1 ? pick_ensemble<1, true>(D) : out == 2 ? pick_ensemble<2, true>(D) : pick_ensemble<0, true>(D);
   return out == 1 ? pick_ensemble<1, false>(D) : out == 2 ? pick_ensemble<2, false>(D) : pick_ensemble<0, false>(D);
 }
@@ -772,6 +854,17 @@ bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb, bool wide) {
     const float val = src == -2 ? 0.5f : 0.0f;
     P.h_cbin[f] = (uint16_t)(std::upper_bound(merged[f].begin(), merged[f].end(), val) - merged[f].begin());
   }
+  {  // the small-integer compact slots: bins of the values 0 .. kLutN - 1
+    std::vector<uint16_t> lut((size_t)kIntSlots * kLutN, 0);
+    for (int k = 0; k < kIntSlots; ++k) {
+      const int f = kCompactSlot[kIntCompact[k]];
+      if (f >= nf) continue;
+      for (int x = 0; x < kLutN; ++x)
+        lut[(size_t)k * kLutN + x] =
+            (uint16_t)(std::upper_bound(merged[f].begin(), merged[f].end(), (float)x) - merged[f].begin());
+    }
+    P.h_lut = lut;
+  }
   P.max_feature_thr = maxc;
   P.slot[0] = sa;
   P.slot[1] = sb;
@@ -858,6 +951,7 @@ void plan_args(const EnsemblePlan& P, const float* dX, int64_t n, int32_t ld, bo
   for (int f = 0; f <= P.nf; ++f) a.thr_off[f] = P.h_thr_off[f];
   a.owner_fixed = owner_fixed ? 1 : 0;
   for (int f = 0; f < kMaxFeatures; ++f) a.cbin[f] = f < (int)P.h_cbin.size() ? P.h_cbin[f] : 0;
+  for (size_t k = 0; k < P.h_lut.size() && k < sizeof(a.lut) / sizeof(a.lut[0]); ++k) a.lut[k] = P.h_lut[k];
   a.vec4 = (ld % 4 == 0 && (reinterpret_cast<uintptr_t>(dX) & 15u) == 0) ? 1 : 0;
   // binning passes: consecutive features whose tables fit bufA + bufB + the tiles; a larger table alone,
   // searched in global memory
@@ -889,7 +983,7 @@ void plan_args(const EnsemblePlan& P, const float* dX, int64_t n, int32_t ld, bo
 
 // out: 0 blended columns, 1 route result records, 2 the single forest's probability column (a.fp)
 bool run_plan(Engine& e, const EnsemblePlan& P, EnsArgs& a, int out, int timing_kind) {
-  const void* fn = pick_ensemble(out, P.wide, P.D);
+  const void* fn = pick_ensemble(out, P.wide, P.D, e.ens_int_lut);
   if (!fn) return false;
   const size_t lds = ens_lds(P.nf, P.wide);
   FD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

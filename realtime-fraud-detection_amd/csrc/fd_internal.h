@@ -170,6 +170,7 @@ struct EnsemblePlan {
   DeviceBuffer nodes[2], thr;  // per forest: chunk blobs (node blocks + leaf values); merged threshold tables
   std::vector<int32_t> h_thr_off;  // merged table offsets (host copy: binning pass plan)
   std::vector<uint16_t> h_cbin;    // bins of the compact vector's constant slots (ensemble.hip)
+  std::vector<uint16_t> h_lut;     // bins of the small-integer compact slots' values 0..31 (ensemble.hip kIntCompact)
   int max_feature_thr = 0;
 };
 
@@ -502,6 +503,7 @@ struct Engine {
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
   bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
   bool ens_prio = false;  // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels)
+  bool ens_int_lut = true;  // "ensemble_int_lut": compact rows' small-integer slots binned by table lookup
   bool compact_vectors = true;  // "compact_vectors": the pipelined stream's compact scoring vectors (engine.hip)
   int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)
   // host-API staging

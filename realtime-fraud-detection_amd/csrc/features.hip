@@ -52,6 +52,11 @@ constexpr size_t kBucketLds = (size_t)kChunkCap * 8 + (size_t)(kMaxBins + 1) * 4
 // Phase stamps of the bucket kernel (profiling build only): per workgroup b < 4096 {start, keys loaded,
 // sorted, short segments done (workgroup barrier), end} plus each wave's own end of the short loop.
 __device__ unsigned long long g_fprof[4096 * 8];
+__device__ unsigned long long g_fprof2[4096 * 4];  // thread 0's first card: header + prep in, ring done, emitted
+#define FD_CSTAMP(k)                                                                                   \
+  do {                                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_fprof2[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 FD_TL_BUF(g_tl_feat);
 #define FD_FSTAMP(k)                                                                              \
   do {                                                                                            \
@@ -59,6 +64,7 @@ FD_TL_BUF(g_tl_feat);
   } while (0)
 #else
 #define FD_FSTAMP(k)
+#define FD_CSTAMP(k)
 #endif
 
 struct Merchant {
@@ -711,11 +717,14 @@ __device__ void process_short(const BucketArgs& a, unsigned s, const KeyT* keys,
     if (q > 0) t = load_prep(a.prep + i);
     double r[FD_RAW_FEATURES];
     base_raw(t, p, r);
+    if (q == 0) FD_CSTAMP(0);
     long long cw[3], sw[3];
     velocity_step<MODE>(c, rg, a.K, t.ts, t.cents, cw, sw);
+    if (q == 0) FD_CSTAMP(1);
     velocity_raw(cw, sw, r);
     emit(a.out, i, r, sw[0], t.o1, t.dv0);
     if (a.out.S) seq_step(a.out, s, c.flags, i, r, q == len - 1);
+    if (q == 0) FD_CSTAMP(2);
   }
   store_card(h, c);
 }
@@ -2164,6 +2173,14 @@ void launch_features_full(Engine& e, const fd_txn_batch& t, const fd_txn_context
 }
 
 #ifdef FD_FOREST_PROFILE
+extern "C" __attribute__((visibility("default"))) int fd_debug_feat_profile2(unsigned long long* out, int n) {
+#ifdef FD_FOREST_PROFILE
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprof2), sizeof(unsigned long long) * (size_t)n);
+#else
+  (void)out, (void)n;
+  return -1;
+#endif
+}
 extern "C" __attribute__((visibility("default"))) int fd_debug_feat_profile(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprof), sizeof(unsigned long long) * (size_t)n);
 }

@@ -24,8 +24,18 @@ def main(paths, nb=512):
         print(f"  per-wave card loop median {np.median(w):8.0f}  p90 {np.percentile(w, 90):8.0f}  max {w.max():8.0f}")
         tot = p[:, 4:8].max(axis=1) - p[:, 0]
         print(f"  workgroup total  median {np.median(tot):8.0f}  p90 {np.percentile(tot, 90):8.0f}")
+        cpath = path.replace(".npy", ".c.npy")
+        try:
+            c = np.load(cpath).reshape(4096, 4)[:nb].astype(np.float64)[ok]
+        except OSError:
+            continue
+        good = (c[:, 0] > p[:, 2]) & (c[:, 2] >= c[:, 1]) & (c[:, 1] >= c[:, 0])
+        c, q = c[good], p[good]
+        for nm, d in (("card: header+prep in", c[:, 0] - q[:, 2]), ("card: velocity/ring", c[:, 1] - c[:, 0]),
+                      ("card: emit (vector)", c[:, 2] - c[:, 1]), ("card: rest to end", q[:, 3] - c[:, 2])):
+            print(f"  {nm:22s} median {np.median(d):8.0f}  p90 {np.percentile(d, 90):8.0f}")
 
 
 if __name__ == "__main__":
-    args = [a for a in sys.argv[1:] if a.endswith(".npy")]
+    args = [a for a in sys.argv[1:] if a.endswith(".npy") and not a.endswith(".c.npy")]
     main(args)
