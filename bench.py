@@ -1759,7 +1759,10 @@ def main():
         cpu = wl.cpu_baseline(args.cpu_seconds)
 
     if rank == 0:
-        roof = wl.roofline(timing)
+        try:
+            roof = wl.roofline(timing)
+        except ZeroDivisionError:  # no kernel timing samples (--timing-steps 0)
+            roof = None
         if isinstance(roof, dict) and roof.get("unit") == "node-steps/s":  # the dominant kernel per pipeline step
             tp = roof["node_steps_per_launch"] / (elapsed / args.steps)
             roof["throughput_basis"] = {"achieved": round(tp, 1), "frac": round(tp / roof["peak"], 6),

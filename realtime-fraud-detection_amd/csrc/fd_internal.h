@@ -7,6 +7,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstddef>
 #include <cstdint>
 #include <mutex>
 #include <stdexcept>
@@ -201,28 +202,33 @@ struct LstmModel {
   DeviceBuffer wpk, wpk4, bias, wout, bout;  // wpk: 16-row kernel's B operands; wpk4: the 4-row kernel's
 };
 
-// One card's keyed state header (features.hip): 128 B = one L2 line, so a transaction's state read and
-// write-back touch one line. Line 0 is what every mode reads (key, profile, ring cursor, window counts,
-// device fingerprints); line 1 the sliding-window sums / oldest times and the redis_compat session.
+// One card's keyed state header (features.hip): 128 B = one L2 line, so a transaction's state read touches one
+// line. Bytes 0-63 hold everything a transaction rewrites (last time, ring cursor, window counts / sums / oldest
+// times, the redis_compat session, the LSTM history cursor in flags), bytes 64-127 what only an insert or a profile
+// load writes (key, profile, device fingerprints): a transaction's write-back dirties half the line (round 5; the
+// oldest times are stored as 32-bit offsets below last_ts to fit — exact, a window spans < 2^32 ms).
 struct __attribute__((aligned(128))) CardHeader {
-  unsigned long long key;          // 0 = empty slot
   long long last_ts;               // time of the card's last event (sliding: last appended; redis: last write)
-  double avg;                      // profile: avg_transaction_amount (NaN = null)
-  int age;                         // profile: account_age_days
-  unsigned flags;                  // bit 0 user profile; bit 1 redis session live; bits 8-15 LSTM events held;
-                                   // bits 16-23 LSTM history write position
   unsigned char ring_n, ring_head; // sliding: events held (<= K), next write position
   unsigned char unsorted;          // sliding: appends left before the ring is time-sorted again (0 = sorted)
   unsigned char pad0;
   unsigned char wc[3], pad1;       // sliding: events of the ring's newest suffix inside the 5m / 1h / 24h window
-  unsigned long long fp[3];        // profile: device fingerprints (0 = none)
-  long long ws[3];                 // sliding: window sums (cents)
-  long long wo[3];                 // sliding: time of the oldest in-window event (valid when wc > 0)
-  long long rc_sum;                // redis_compat: session amount (cents)
+  unsigned flags;                  // bit 0 user profile; bit 1 redis session live; bits 8-15 LSTM events held;
+                                   // bits 16-23 LSTM history write position
   int rc_cnt;                      // redis_compat: session count
-  int pad2;
+  long long ws[3];                 // sliding: window sums (cents); redis_compat: ws[0] is the session amount
+  unsigned wod[3];                 // sliding: last_ts - time of the oldest in-window event (valid when wc > 0)
+  unsigned pad2;
+  unsigned long long key;          // 0 = empty slot
+  double avg;                      // profile: avg_transaction_amount (NaN = null)
+  int age;                         // profile: account_age_days
+  int pad3;
+  unsigned long long fp[3];        // profile: device fingerprints (0 = none)
+  long long pad4[2];
 };
 static_assert(sizeof(CardHeader) == 128, "CardHeader must be one 128-B line");
+static_assert(offsetof(CardHeader, key) == 64 && offsetof(CardHeader, wod) + sizeof(unsigned) * 3 <= 64,
+              "the mutable fields in bytes 0-63, the key at 64 (snapshot.hip reads it there)");
 constexpr int kCardHeaderBytes = (int)sizeof(CardHeader);
 
 // one event of a card's ring (sliding windows): time and cents

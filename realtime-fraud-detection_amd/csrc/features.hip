@@ -461,48 +461,54 @@ __device__ __forceinline__ long long ll2(unsigned lo, unsigned hi) {
 
 __device__ __forceinline__ void load_card(const CardHeader* __restrict__ h, CardRegs& c, Profile& p) {
   const uint4* q = reinterpret_cast<const uint4*>(h);
-  uint4 w[8];
+  uint4 w[7];  // bytes 0-111 (the last 16 are padding)
 #pragma unroll
-  for (int k = 0; k < 8; ++k) w[k] = q[k];
+  for (int k = 0; k < 7; ++k) w[k] = q[k];
   // field offsets: see CardHeader (fd_internal.h)
-  c.last_ts = ll2(w[0].z, w[0].w);
-  p.avg = __longlong_as_double(ll2(w[1].x, w[1].y));
-  p.age = (int)w[1].z;
-  c.flags = w[1].w;
-  c.rn = (int)(w[2].x & 0xffu);
-  c.rh = (int)((w[2].x >> 8) & 0xffu);
-  c.us = (int)((w[2].x >> 16) & 0xffu);
-  c.wc[0] = (int)(w[2].y & 0xffu);
-  c.wc[1] = (int)((w[2].y >> 8) & 0xffu);
-  c.wc[2] = (int)((w[2].y >> 16) & 0xffu);
-  p.fp[0] = (unsigned long long)ll2(w[2].z, w[2].w);
-  p.fp[1] = (unsigned long long)ll2(w[3].x, w[3].y);
-  p.fp[2] = (unsigned long long)ll2(w[3].z, w[3].w);
-  c.ws[0] = ll2(w[4].x, w[4].y);
-  c.ws[1] = ll2(w[4].z, w[4].w);
-  c.ws[2] = ll2(w[5].x, w[5].y);
-  c.wo[0] = ll2(w[5].z, w[5].w);
-  c.wo[1] = ll2(w[6].x, w[6].y);
-  c.wo[2] = ll2(w[6].z, w[6].w);
-  c.rc_sum = ll2(w[7].x, w[7].y);
-  c.rc_cnt = (int)w[7].z;
+  c.last_ts = ll2(w[0].x, w[0].y);
+  c.rn = (int)(w[0].z & 0xffu);
+  c.rh = (int)((w[0].z >> 8) & 0xffu);
+  c.us = (int)((w[0].z >> 16) & 0xffu);
+  c.wc[0] = (int)(w[0].w & 0xffu);
+  c.wc[1] = (int)((w[0].w >> 8) & 0xffu);
+  c.wc[2] = (int)((w[0].w >> 16) & 0xffu);
+  c.flags = w[1].x;
+  c.rc_cnt = (int)w[1].y;
+  c.ws[0] = ll2(w[1].z, w[1].w);
+  c.rc_sum = c.ws[0];  // redis_compat keeps its session amount in ws[0]
+  c.ws[1] = ll2(w[2].x, w[2].y);
+  c.ws[2] = ll2(w[2].z, w[2].w);
+  const unsigned wod[3] = {w[3].x, w[3].y, w[3].z};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) c.wo[k] = c.wc[k] > 0 ? c.last_ts - (long long)wod[k] : 0;
+  p.avg = __longlong_as_double(ll2(w[4].z, w[4].w));
+  p.age = (int)w[5].x;
+  p.fp[0] = (unsigned long long)ll2(w[5].z, w[5].w);
+  p.fp[1] = (unsigned long long)ll2(w[6].x, w[6].y);
+  p.fp[2] = (unsigned long long)ll2(w[6].z, w[6].w);
   p.has_user = (c.flags & 1u) != 0u;
 }
 
-// write back the mutable fields (line 0: last_ts, flags, ring cursor + window counts; line 1 whole)
+// write back the mutable fields: bytes 0-63 of the header, as four 16-B stores (the key / profile half is never
+// rewritten here). An in-window oldest time is at most a window (< 2^32 ms) below the last event: a 32-bit offset.
+template <int MODE>
 __device__ __forceinline__ void store_card(CardHeader* h, const CardRegs& c) {
-  h->last_ts = c.last_ts;
-  h->flags = c.flags;
-  unsigned long long cur = (unsigned long long)(unsigned)c.rn | ((unsigned long long)(unsigned)c.rh << 8) |
-                           ((unsigned long long)(unsigned)c.us << 16) | ((unsigned long long)(unsigned)c.wc[0] << 32) |
-                           ((unsigned long long)(unsigned)c.wc[1] << 40) | ((unsigned long long)(unsigned)c.wc[2] << 48);
-  *reinterpret_cast<unsigned long long*>(&h->ring_n) = cur;
-  const long long l1[8] = {c.ws[0], c.ws[1], c.ws[2], c.wo[0], c.wo[1], c.wo[2], c.rc_sum, (long long)(unsigned)c.rc_cnt};
-  uint4* q = reinterpret_cast<uint4*>(h->ws);
+  const unsigned long long cur = (unsigned long long)(unsigned)c.rn | ((unsigned long long)(unsigned)c.rh << 8) |
+                                 ((unsigned long long)(unsigned)c.us << 16) |
+                                 ((unsigned long long)(unsigned)c.wc[0] << 32) |
+                                 ((unsigned long long)(unsigned)c.wc[1] << 40) |
+                                 ((unsigned long long)(unsigned)c.wc[2] << 48);
+  const unsigned long long lt = (unsigned long long)c.last_ts;
+  const unsigned long long s0 = (unsigned long long)(MODE == FD_WINDOW_REDIS_COMPAT ? c.rc_sum : c.ws[0]);
+  const unsigned long long s1 = (unsigned long long)c.ws[1], s2 = (unsigned long long)c.ws[2];
+  unsigned wod[3];
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    q[k] = make_uint4((unsigned)l1[2 * k], (unsigned)((unsigned long long)l1[2 * k] >> 32), (unsigned)l1[2 * k + 1],
-                      (unsigned)((unsigned long long)l1[2 * k + 1] >> 32));
+  for (int k = 0; k < 3; ++k) wod[k] = c.wc[k] > 0 ? (unsigned)(c.last_ts - c.wo[k]) : 0u;
+  uint4* q = reinterpret_cast<uint4*>(h);
+  q[0] = make_uint4((unsigned)lt, (unsigned)(lt >> 32), (unsigned)cur, (unsigned)(cur >> 32));
+  q[1] = make_uint4(c.flags, (unsigned)c.rc_cnt, (unsigned)s0, (unsigned)(s0 >> 32));
+  q[2] = make_uint4((unsigned)s1, (unsigned)(s1 >> 32), (unsigned)s2, (unsigned)(s2 >> 32));
+  q[3] = make_uint4(wod[0], wod[1], wod[2], 0u);
 }
 
 // windows as of time t from the (time-sorted) ring: the newest events with ts > t - W
@@ -726,7 +732,7 @@ __device__ void process_short(const BucketArgs& a, unsigned s, const KeyT* keys,
     if (a.out.S) seq_step(a.out, s, c.flags, i, r, q == len - 1);
     if (q == 0) FD_CSTAMP(2);
   }
-  store_card(h, c);
+  store_card<MODE>(h, c);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -769,7 +775,7 @@ __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned lon
   if (tid == 0) {
     sm.hdr = *h;
     sm.carry_c = sm.hdr.rc_cnt;
-    sm.carry_s = sm.hdr.rc_sum;
+    sm.carry_s = sm.hdr.ws[0];  // redis_compat: the session amount
     sm.hist_n = MODE == FD_WINDOW_SLIDING ? sm.hdr.ring_n : 0;
     sm.us = sm.hdr.unsorted;
     sm.seq_n = (int)((sm.hdr.flags >> 8) & 0xffu);
@@ -940,9 +946,9 @@ __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned lon
     for (int w = 0; w < 3; ++w) {
       c.wc[w] = sm.hdr.wc[w];
       c.ws[w] = sm.hdr.ws[w];
-      c.wo[w] = sm.hdr.wo[w];
+      c.wo[w] = sm.hdr.wc[w] > 0 ? sm.hdr.last_ts - (long long)sm.hdr.wod[w] : 0;
     }
-    c.rc_sum = sm.hdr.rc_sum;
+    c.rc_sum = sm.hdr.ws[0];
     c.rc_cnt = sm.hdr.rc_cnt;
     if (MODE == FD_WINDOW_REDIS_COMPAT) {
       c.rc_cnt = (int)sm.carry_c;
@@ -972,7 +978,7 @@ __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned lon
           if (c.wc[w] == 0) c.wo[w] = 0;
       }
     }
-    store_card(h, c);
+    store_card<MODE>(h, c);
   }
   __syncthreads();
 }

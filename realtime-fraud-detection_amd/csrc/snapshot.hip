@@ -28,7 +28,9 @@
 namespace fd {
 namespace {
 
-constexpr int kHeaderWords = kCardHeaderBytes / 16;  // CardHeader (fd_internal.h): key @0
+constexpr int kHeaderWords = kCardHeaderBytes / 16;  // CardHeader (fd_internal.h)
+constexpr int kHeaderKeyWord = (int)(offsetof(CardHeader, key) / 16);  // the 16-B word holding the key (low half)
+static_assert(offsetof(CardHeader, key) % 16 == 0, "the key opens its 16-B word");
 constexpr int kUextWords = 3;      // 48-B UserExt
 constexpr size_t kMerchantBytes = 16, kMerchExtBytes = 16, kWinEventBytes = 40, kVocabBytes = 512;
 constexpr int64_t kChunkSlots = 1 << 18;
@@ -50,7 +52,8 @@ struct __attribute__((packed)) SnapHeader {  // 256 B, little-endian
 };
 static_assert(sizeof(SnapHeader) == 256, "SnapHeader must be 256 B");
 constexpr char kMagic[8] = {'F', 'D', 'S', 'N', 'A', 'P', 0, 1};
-constexpr uint32_t kVersion = 2;  // 2: 128-B card header with the fingerprints folded in (1: 64-B + fps plane)
+constexpr uint32_t kVersion = 3;  // 3: the mutable fields in the header's first 64 B, the key at byte 64 (round 5);
+                                  // 2: 128-B card header with the fingerprints folded in; 1: 64-B + fps plane
 
 struct Fnv {
   uint64_t h = 0xcbf29ce484222325ull;
@@ -118,7 +121,7 @@ __global__ void __launch_bounds__(256) snap_flag_kernel(const uint4* __restrict_
                                                         long long lo, long long n, unsigned char* __restrict__ flags) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint4 h = pages[(lo + i) * page_words];
+  const uint4 h = pages[(lo + i) * page_words + kHeaderKeyWord];  // the header's key
   flags[i] = (h.x | h.y) != 0u;
 }
 
@@ -138,7 +141,7 @@ __global__ void __launch_bounds__(256) restore_slot_kernel(unsigned long long* k
                                                            unsigned long long* restored, unsigned* err) {
   const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
-  const uint4 h = recs[r * words];
+  const uint4 h = recs[r * words + kHeaderKeyWord];
   const unsigned long long key = ((unsigned long long)h.y << 32) | h.x;
   long long s = -1;
   if (owned(key, shard, G)) {
