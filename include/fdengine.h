@@ -673,6 +673,9 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      fused ensemble kernel, 0 the full bucket kernel
      "ensemble_int_lut": the fused kernel's compact rows, 1 (default) the eight small-integer slots binned by one
      lookup in a per-plan table of the bins of 0..31, 0 searched like the others (outputs identical)
+     "ensemble_bin_global": the fused kernel's compact rows, 1 every varying slot binned by a search of its merged
+     threshold table in global memory (L2-resident; no staging pass, chunk 0's DMA issued at the kernel's start),
+     0 (default) the tables staged in LDS first (outputs identical)
      "lean_group": how the lean bucket kernel groups a bucket's keys by card (outputs identical): 2 (default) an
      LDS hash table of card slots (no sort), 1 a rank sort split over all threads, 0 the first m threads each rank
      one key over the whole list

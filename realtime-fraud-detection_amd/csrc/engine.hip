@@ -541,6 +541,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     // (hour, day of week, weekend, counts, account age, new device) binned by a per-plan table lookup, 0 searched
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_int_lut must be 0 or 1");
     e.ens_int_lut = value != 0;
+  } else if (k == "ensemble_bin_global") {  // the fused kernel's compact rows: 1 binned by searches of the merged
+    // tables where they lie (L2), chunk 0's DMA issued at once; 0 the tables staged in LDS first
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_bin_global must be 0 or 1");
+    e.ens_bin_global = value != 0;
   } else if (k == "lean_group") {  // pipelined stream: the lean bucket kernel's grouping of a bucket's keys by card,
     // 0 rank sort (first m threads, whole list each), 1 rank sort split over all threads, 2 (default) LDS hash table
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "lean_group must be 0, 1 or 2");

@@ -93,11 +93,14 @@ struct EnsArgs {
   int compact;                    // X rows are the compact vector (kCompactWidth floats), binned here
   uint16_t cbin[kMaxFeatures];    // compact mode: the bins of the constant slots (0 or 0.5), per plan
   alignas(4) uint16_t lut[8 * 32];  // compact mode: [kIntSlots][kLutN] bins of the small-integer slots' values 0..31
+
   int owner_fixed;                // chunk owner: tree group 0 (the oldest waves: highest issue priority), else rotating
   int prio;                       // issue priority 2 above the co-running feature kernels (engine option ensemble_prio)
   int n_pass;
   int pass_f[kMaxPass + 1];
   unsigned long long pass_global;  // bit p: pass p bins from global memory (its table does not fit LDS)
+  const char* img;                 // the passes' padded table images (thr_pad layout), 1 KiB pieces
+  int img_off[kMaxPass + 1];       // pass p's image: bytes [img_off[p], img_off[p + 1]) of img
   const char* nodes[2];
   int n_chunks[2];
   int stride[2];
@@ -211,12 +214,14 @@ __device__ __forceinline__ void owner_sum(uint32_t buf, uint32_t tile, uint32_t 
   lds_store<LeafT>(acc + (uint32_t)txn * (uint32_t)sizeof(LeafT), s);
 }
 
-// LDS-DMA of one chunk by the four waves of one tree group (part = transaction group): 1 KiB pieces dealt
-// round-robin; completed by dma_wait() in the issuing waves before the chunk barrier
-__device__ __forceinline__ void stage_chunk_part(const char* __restrict__ src, uint32_t dst, int stride, int part) {
+// LDS-DMA of `bytes` (a multiple of 1 KiB) by nparts waves (this one: part), 1 KiB pieces dealt round-robin;
+// completed by dma_wait() in the issuing waves (measured: the piece order rotated by workgroup, so that the CUs
+// staging the same tables and chunks at once spread over the L2 channels, changed nothing)
+__device__ __forceinline__ void stage_pieces(const char* __restrict__ src, uint32_t dst, int bytes, int nparts,
+                                             int part) {
   const int lane = threadIdx.x & 63;
-  const int pieces = stride >> 10;
-  for (int p = part; p < pieces; p += 4) {
+  const int pieces = bytes >> 10;
+  for (int p = part; p < pieces; p += nparts) {
     const char* g = src + (p << 10) + lane * 16;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane(dst + ((uint32_t)p << 10));
     asm volatile(
@@ -231,7 +236,7 @@ __device__ __forceinline__ void stage_chunk_part(const char* __restrict__ src, u
 
 // Staged threshold tables hold element g at word g + g / 32: the binary search's power-of-two strides would
 // otherwise put every lane of a step on one LDS bank (up to 32-way conflicts); one pad word per 32 spreads them.
-__device__ __forceinline__ int thr_pad(int g) { return g + (g >> 5); }
+__host__ __device__ __forceinline__ int thr_pad(int g) { return g + (g >> 5); }
 
 #ifdef FD_FOREST_PROFILE
 // per (workgroup < 256, wave): cycles in prologue, loop top (leaf stores, DMA issue, owner add), walk + leaf
@@ -434,6 +439,7 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
   // this kernel is the stream's critical path, theirs is latency-bound with slack
   if (a.prio) __builtin_amdgcn_s_setprio(2);
   int anynan = 0;
+  const bool early0 = G > 0 && a.n_pass == 1 && (a.pass_global & 1ull) != 0;
   {
     uint16_t* Xs = reinterpret_cast<uint16_t*>(lbase);
     const int q = __builtin_amdgcn_readfirstlane(tid >> 8);  // wave-uniform: the four threads sharing `txn`
@@ -473,6 +479,11 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
         for (int k = 0; k < 16; ++k) v[k] = fq + k < ncopy ? xr[fq + k] : __builtin_nanf("");  // missing: NaN
       }
     }
+    // pass 0's table image goes out by LDS-DMA now, beside the row loads (it lands while they are in flight); every
+    // search in global memory instead (engine option ensemble_bin_global): nothing staged, so chunk 0's DMA goes out
+    if (a.n_pass > 0 && !(a.pass_global & 1ull))
+      stage_pieces(a.img + a.img_off[0], bufA, a.img_off[1] - a.img_off[0], kEnsWG / 64, wave);
+    if (early0) stage_chunk_asm(nA > 0 ? a.nodes[0] : a.nodes[1], bufA, nA > 0 ? a.stride[0] : a.stride[1], kEnsWG / 64);
 #ifdef FD_FOREST_PROFILE
     pr_st[0] = __builtin_amdgcn_s_memtime();
 #endif
@@ -488,19 +499,10 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
       const bool glob = (a.pass_global >> p) & 1ull;
       const int o0 = a.thr_off[f0];
       const uint32_t tl = bufA;  // this pass's tables: bufA + bufB + the tiles (free until chunk 0 is staged)
-      if (!glob) {
-        float* tp = reinterpret_cast<float*>(lbase + (bufA - s0));
-        const int cnt = a.thr_off[f1] - o0;
-        int i = tid;  // element g at word g + g / 32 (thr_pad)
-        for (; i + 3 * kEnsWG < cnt; i += 4 * kEnsWG) {
-          const float t0 = a.thr[o0 + i], t1 = a.thr[o0 + i + kEnsWG], t2 = a.thr[o0 + i + 2 * kEnsWG],
-                      t3 = a.thr[o0 + i + 3 * kEnsWG];
-          tp[thr_pad(i)] = t0;
-          tp[thr_pad(i + kEnsWG)] = t1;
-          tp[thr_pad(i + 2 * kEnsWG)] = t2;
-          tp[thr_pad(i + 3 * kEnsWG)] = t3;
-        }
-        for (; i < cnt; i += kEnsWG) tp[thr_pad(i)] = a.thr[o0 + i];
+      if (!glob) {  // the pass's image (element g at word g + g / 32, thr_pad) in LDS: DMA, then publish
+        if (p > 0)
+          stage_pieces(a.img + a.img_off[p], bufA, a.img_off[p + 1] - a.img_off[p], kEnsWG / 64, wave);
+        dma_wait();
         __syncthreads();
       } else if (LUT && a.compact && p == 0) {
         __syncthreads();  // the small-integer table
@@ -590,8 +592,8 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
 #endif
     }
   }
-  if (G > 0)  // chunk 0 (the tables are dead): forest A's first, or B's when A is absent
-    stage_chunk_asm(nA > 0 ? a.nodes[0] : a.nodes[1], bufA, nA > 0 ? a.stride[0] : a.stride[1], kEnsWG / 64);
+  if (G > 0 && !early0)  // chunk 0 (the tables are dead): forest A's first, or B's when A is absent
+    stage_pieces(nA > 0 ? a.nodes[0] : a.nodes[1], bufA, nA > 0 ? a.stride[0] : a.stride[1], kEnsWG / 64, wave);
   if (gg == 0) {
     lds_store<float>(accA + txn * 4, a.base_margin);
     lds_store<double>(accB + txn * 8, 0.0);
@@ -624,8 +626,8 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
       }
       if (g + 1 < G) {
         const int h = g + 1, fb = h >= nA ? 1 : 0;
-        stage_chunk_part(a.nodes[fb] + (size_t)(fb ? h - nA : h) * a.stride[fb], (g & 1) ? bufA : bufB, a.stride[fb],
-                         wave & 3);
+        stage_pieces(a.nodes[fb] + (size_t)(fb ? h - nA : h) * a.stride[fb], (g & 1) ? bufA : bufB, a.stride[fb], 4,
+                  wave & 3);
       }
     }
     const uint32_t cur = (g & 1) ? bufB : bufA, tw = (g & 1) ? tile1 : tile0;
@@ -755,6 +757,37 @@ fd_tree_arrays arrays_of(const PackedForest& f) {
   return t;
 }
 
+// Binning passes over the tables (thr, off): consecutive features whose padded tables fit the staging area (bufA +
+// bufB + the tiles), a larger table alone, searched in global memory; each staged pass's image (element g of the
+// pass at word thr_pad(g), 1 KiB pieces) appended to img
+void plan_passes(const std::vector<float>& thr, const std::vector<int32_t>& off, int nf, bool wide, EnsPassSet& ps,
+                 std::vector<float>& img) {
+  const size_t stage_floats = (2 * (size_t)ens_buf(wide) + 2 * (size_t)kEnsTile) / 4;
+  ps = EnsPassSet{};
+  ps.f.push_back(0);
+  ps.img_off.push_back((int)(img.size() * 4));
+  int f = 0;
+  while (f < nf) {
+    int g = f;
+    while (g < nf && (size_t)(off[g + 1] - off[f]) + (size_t)(off[g + 1] - off[f]) / 32 + 1 <= stage_floats) ++g;
+    const int np = (int)ps.f.size() - 1;
+    FD_REQUIRE(np < kMaxPass, FD_ERR_UNSUPPORTED, "ensemble binning plan too long");
+    if (g == f) {  // one feature's table exceeds the LDS space
+      ps.glob |= 1ull << np;
+      g = f + 1;
+    } else {
+      const int cnt = off[g] - off[f];
+      const size_t words = cnt > 0 ? (size_t)thr_pad(cnt - 1) + 1 : 0;
+      const size_t base = img.size();
+      img.resize(base + (words + 255) / 256 * 256, 0.f);
+      for (int i = 0; i < cnt; ++i) img[base + (size_t)thr_pad(i)] = thr[(size_t)off[f] + i];
+    }
+    ps.f.push_back(g);
+    ps.img_off.push_back((int)(img.size() * 4));
+    f = g;
+  }
+}
+
 // joint repack of forest A (XGBoost, slot sa) and B (IsolationForest, slot sb) into plan P; either slot may be -1
 // (a single forest: the kernel walks only the other one); false when not possible (the per-model path runs)
 bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb, bool wide) {
@@ -865,6 +898,12 @@ bool build_plan(Engine& e, EnsemblePlan& P, int sa, int sb, bool wide) {
     }
     P.h_lut = lut;
   }
+  {  // the binning passes and their table images
+    std::vector<float> img;
+    plan_passes(thr, off, nf, wide, P.passes, img);
+    P.img.ensure(std::max<size_t>(1024, img.size() * sizeof(float)));
+    if (!img.empty()) FD_HIP(hipMemcpy(P.img.ptr, img.data(), img.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   P.max_feature_thr = maxc;
   P.slot[0] = sa;
   P.slot[1] = sb;
@@ -953,24 +992,14 @@ void plan_args(const EnsemblePlan& P, const float* dX, int64_t n, int32_t ld, bo
   for (int f = 0; f < kMaxFeatures; ++f) a.cbin[f] = f < (int)P.h_cbin.size() ? P.h_cbin[f] : 0;
   for (size_t k = 0; k < P.h_lut.size() && k < sizeof(a.lut) / sizeof(a.lut[0]); ++k) a.lut[k] = P.h_lut[k];
   a.vec4 = (ld % 4 == 0 && (reinterpret_cast<uintptr_t>(dX) & 15u) == 0) ? 1 : 0;
-  // binning passes: consecutive features whose tables fit bufA + bufB + the tiles; a larger table alone,
-  // searched in global memory
-  const size_t stage_floats = (2 * (size_t)ens_buf(P.wide) + 2 * (size_t)kEnsTile) / 4;  // bufA + bufB + the tiles
-  int np = 0, f = 0;
-  a.pass_f[0] = 0;
-  while (f < P.nf) {
-    const int32_t* o = P.h_thr_off.data();
-    int g = f;
-    while (g < P.nf && (size_t)(o[g + 1] - o[f]) + (size_t)(o[g + 1] - o[f]) / 32 + 1 <= stage_floats) ++g;  // thr_pad
-    if (g == f) {  // one feature's table exceeds the LDS space
-      a.pass_global |= 1ull << np;
-      g = f + 1;
-    }
-    FD_REQUIRE(np < kMaxPass, FD_ERR_UNSUPPORTED, "ensemble binning plan too long");
-    a.pass_f[++np] = g;
-    f = g;
+  const EnsPassSet& ps = P.passes;  // plan_passes
+  a.n_pass = (int)ps.f.size() - 1;
+  for (int p = 0; p <= a.n_pass; ++p) {
+    a.pass_f[p] = ps.f[p];
+    a.img_off[p] = ps.img_off[p];
   }
-  a.n_pass = np;
+  a.pass_global = ps.glob;
+  a.img = P.img.as<const char>();
   for (int q = 0; q < 2; ++q) {
     a.nodes[q] = P.nodes[q].as<const char>();
     a.n_chunks[q] = P.n_chunks[q];
@@ -1015,6 +1044,12 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
   EnsArgs a{};
   plan_args(e.ens, dX, n, compact ? kCompactWidth : ld, e.ens_owner_fixed, a);
   a.compact = compact ? 1 : 0;
+  if (compact && e.ens_bin_global) {  // one pass, every table searched where it lies (L2), nothing staged
+    a.n_pass = 1;
+    a.pass_f[0] = 0;
+    a.pass_f[1] = e.ens.nf;
+    a.pass_global = 1ull;
+  }
   a.prio = e.ens_prio ? 1 : 0;
   a.pos[0] = pa;
   a.pos[1] = pb;

@@ -158,6 +158,13 @@ struct PackedForest {
 // The fused ensemble kernel's joint repack of one XGBoost and/or one IsolationForest (ensemble.hip): both
 // padded to one depth D, node words rewritten against the MERGED per-feature threshold tables, so one bin
 // tile serves both forests; chunks of CH[k] node-only trees, leaf values [tree][2^D] per forest.
+// binning passes of one row form (ensemble.hip): pass p covers features [f[p], f[p + 1]); bit p of glob: searched in
+// global memory (a table larger than the staging area); img_off[p] .. img_off[p + 1]: pass p's padded LDS image
+struct EnsPassSet {
+  std::vector<int> f, img_off;
+  unsigned long long glob = 0;
+};
+
 struct EnsemblePlan {
   bool valid = false;
   bool wide = true;  // chunk layout: 24 / 16 trees (wide) or 20 / 12 (compact: LDS room for an RCCL kernel beside)
@@ -172,6 +179,8 @@ struct EnsemblePlan {
   std::vector<int32_t> h_thr_off;  // merged table offsets (host copy: binning pass plan)
   std::vector<uint16_t> h_cbin;    // bins of the compact vector's constant slots (ensemble.hip)
   std::vector<uint16_t> h_lut;     // bins of the small-integer compact slots' values 0..31 (ensemble.hip kIntCompact)
+  DeviceBuffer img;    // every staged binning pass's padded table image (ensemble.hip plan_passes), LDS-DMA source
+  EnsPassSet passes;
   int max_feature_thr = 0;
 };
 
@@ -509,6 +518,7 @@ struct Engine {
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
   bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
   bool ens_prio = false;  // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels)
+  bool ens_bin_global = false;  // "ensemble_bin_global": compact rows binned by searches in global memory (no staging)
   bool ens_int_lut = true;  // "ensemble_int_lut": compact rows' small-integer slots binned by table lookup
   bool compact_vectors = true;  // "compact_vectors": the pipelined stream's compact scoring vectors (engine.hip)
   int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)

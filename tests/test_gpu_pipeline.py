@@ -56,7 +56,7 @@ def world():
     return pop, tx, xgb, ifm
 
 
-def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1, slot_stream=0):
+def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1, slot_stream=0, opts=()):
     import torch
     pop, tx, xgb, ifm = world
     params = _params()
@@ -70,6 +70,8 @@ def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1, sl
     ref, pip = _setup(pop, xgb, ifm), _setup(pop, xgb, ifm)
     pip.set_option("pipeline_lean", lean)
     pip.set_option("slot_stream", slot_stream)
+    for k, v in opts:
+        pip.set_option(k, v)
     try:
         for e in (ref, pip):
             e.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -115,6 +117,17 @@ def _run(world, cuts, interleave=False, side_stream=False, hot=False, lean=1, sl
 def test_pipelined_stream_matches_serial(world, lean, slot_stream):
     """slot_stream 1 / 2: every batch's slot pass on the engine's slot stream (high / low priority)"""
     _run(world, [0, 40000, 80000, 81000, 121000, 161000, 201000, 241000], lean=lean, slot_stream=slot_stream)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("opts", [(("ensemble_bin_global", 1),), (("ensemble_int_lut", 0),),
+                                  (("ensemble_int_lut", 0), ("ensemble_bin_global", 1)), (("lean_group", 0),),
+                                  (("lean_group", 1),)], ids=["bin_global", "no_int_lut", "no_lut_bin_global",
+                                                              "lean_group0", "lean_group1"])
+def test_pipelined_engine_options(world, opts):
+    """the compact path's A/B options (binning of the fused kernel's rows, the lean kernel's card grouping): the
+    pipelined stream's outputs and end state equal the serial full-vector path's under every one"""
+    _run(world, [0, 40000, 80000, 81000, 121000], hot=True, opts=opts)
 
 
 @pytest.mark.timeout(300)

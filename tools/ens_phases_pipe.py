@@ -71,6 +71,10 @@ def main():
     dev = torch.device("cuda", 0)
     eng = fdengine.FraudEngine(0)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    for kv in os.environ.get("OPTS", "").split(","):  # engine options, e.g. OPTS=ensemble_bin_global=1
+        if kv:
+            k, v = kv.split("=")
+            eng.set_option(k.strip(), int(v))
     wl = bench.WORKLOADS["config4"](args, 0, dev, eng)
     for i in range(args.warmup):
         wl.step(i)
