@@ -88,11 +88,12 @@ def test_reversed_model_order_and_depth_padding(engine):
 
 
 def test_shallow_forests(engine):
-    """depth 3 and depth 2 forests (IsolationForest max_samples 8 / 4) through the fused kernel"""
-    for d, s in ((3, 31), (2, 33)):
+    """depth 3 and depth 2 forests (IsolationForest max_samples 8 / 4) through the fused kernel; one chunk of each
+    forest only (17 + 5 trees) included"""
+    for d, s, nx, ni in ((3, 31, 70, 20), (2, 33, 70, 20), (3, 35, 17, 5)):
         Xr = synth.feature_matrix(4096, 24, seed=s)
-        xgb = xgboost_from_json_doc(synth.xgboost_doc(70, d, 24, Xr, seed=s + 1, base_score=0.4))
-        ifm = iforest_from_sklearn(synth.isolation_forest(Xr.astype(np.float64), n_estimators=20, max_samples=2 ** d))
+        xgb = xgboost_from_json_doc(synth.xgboost_doc(nx, d, 24, Xr, seed=s + 1, base_score=0.4))
+        ifm = iforest_from_sklearn(synth.isolation_forest(Xr.astype(np.float64), n_estimators=ni, max_samples=2 ** d))
         X = synth.feature_matrix(N, 24, seed=s + 2, nan_frac=0.01)
         _check(engine, xgb, ifm, X)
 
@@ -197,3 +198,13 @@ def _k6(engine, slot, X):
         return engine.predict(slot, X)
     finally:
         engine.set_option("ensemble", 1)
+
+
+@pytest.mark.parametrize("n_trees", [1, 10, 30])
+def test_single_forest_few_chunks(engine, n_trees):
+    """one forest of one or two chunks through the fused kernel: probabilities bit-identical to forest kernel 6"""
+    Xr = synth.feature_matrix(4096, 32, seed=41)
+    xgb = xgboost_from_json_doc(synth.xgboost_doc(n_trees, 8, 32, Xr, seed=42, base_score=0.2))
+    engine.load_forest(3, xgb)
+    X = synth.feature_matrix(N, 32, seed=43, nan_frac=0.01)
+    np.testing.assert_array_equal(engine.predict(3, X), _k6(engine, 3, X))
