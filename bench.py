@@ -45,6 +45,10 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA peak (MI355X_MICROARCH.md "
 # Forest walk: per node-step one ds_read_b32 (feature bin) + one ds_read_b64 (children pair) per lane; per
 # 64-lane wave-instruction 2 + 2 LDS-array cycles (MI355X_MICROARCH.md §LDS) = 16 node-steps/clk/CU.
 LDS_NODE_STEPS_PEAK = 256 * 2.4e9 * 16  # 9.83e12 node-steps/s
+# The same read pair chased the way the walk chases it (each step's addresses from the previous step's data, random
+# 1 KiB rows, conflict-free columns, 16 waves x 8 chains per CU): measured 4.19e9 node-steps in 0.867 ms on every CU
+# (tools/micro/lds_width.hip, profiles/r05/lds_width/) — ~4 LDS cycles per wave-read, not the table's 2
+LDS_NODE_STEPS_ATTAINABLE = 4.19e9 / 0.867e-3  # 4.83e12 node-steps/s
 FUSED_BYTES_PER_TXN = 238  # txn 36 + card header R/W 96 + profiles 64 + outputs 10 + ring append 32
 TIMING_EVERY = 8  # kernel-timing sample period (engine option "timing_every")
 
@@ -196,6 +200,11 @@ def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=Non
             "kernel_samples": launches, "node_steps_per_launch": steps,
             "peak_basis": "per node-step 1 ds_read_b32 + 1 ds_read_b64 per lane = 4 LDS-array cycles per 64 "
                           "node-steps: 16/clk/CU x 256 CUs x 2.4 GHz",
+            "attainable": {"peak": round(LDS_NODE_STEPS_ATTAINABLE, 1),
+                           "frac": round(achieved / LDS_NODE_STEPS_ATTAINABLE, 6),
+                           "basis": "the walk's dependent ds_read_u16 + ds_read_b64 pair chased on every CU (16 waves "
+                                    "x 8 chains, random rows, conflict-free banks; tools/micro/lds_width.hip, "
+                                    "profiles/r05/lds_width): 4.19e9 node-steps in 0.867 ms"},
             "hbm_view": {"algorithmic_bytes_per_launch": B * (vec_bytes + 8) + model_bytes,
                          "vector_bytes_per_txn": vec_bytes,
                          "achieved_GBs": round((B * (vec_bytes + 8) + model_bytes) / avg / 1e9, 3),
