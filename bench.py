@@ -606,7 +606,7 @@ class Config3:
 
     def step(self, i, vectors=False):
         """One micro-batch through the product path the timed region runs: the pipelined stream (config 3; the fused
-        kernel reads the compact 24-float vectors) or fd_score_batch_device per step (config 5). vectors: also ask
+        kernel reads the compact 64-B rows) or fd_score_batch_device per step (config 5). vectors: also ask
         for the scoring vectors and per-model probabilities (the parity twin batch; the non-compact variant)."""
         b = self.next_batch
         if b >= self.n_batches:
@@ -632,7 +632,7 @@ class Config3:
 
     def parity(self):
         """The first parity_batches micro-batches (fresh state, carried across them) through the timed path — no
-        vectors requested, so the pipelined stream's fused kernel reads the compact 24-float vectors — against the
+        vectors requested, so the pipelined stream's fused kernel reads the compact 64-B rows — against the
         oracle chain, which computes its own vectors; then one twin batch with the vectors and per-model
         probabilities requested (the non-compact variant), whose vectors are compared too."""
         return self._parity()
@@ -688,10 +688,10 @@ class Config3:
         routed = bool(getattr(sc, "route", False))
         be = getattr(sc, "be", None)
         pipelined = bool(getattr(be, "pipelined", getattr(self, "pipe", False)))
-        # the pipelined stream hands the fused kernel the compact 24-float vector (96 B) unless vectors are requested
+        # the pipelined stream hands the fused kernel the compact 64-B row (14 f32 + 8 byte slots) unless vectors are requested
         return forest_roofline(timing, self.N.FD_TIMING_XGB, self.xgb, 8, self.B, self.name,
                                FOREST_KERNEL.format(d=8, t="f32", k="XGB") + " dominant", [self.xgb, self.ifm],
-                               out=1 if routed else 0, wide=not native, vec_bytes=96 if pipelined else 256)
+                               out=1 if routed else 0, wide=not native, vec_bytes=64 if pipelined else 256)
 
     def kernels(self, timing):
         N = self.N
@@ -982,7 +982,7 @@ class Config4(Config3):
         if self.hist_rows is not None and len(self.hist_rows["card_key"]):
             o.run(self.hist_rows, want_raw=False)
         out = _parity_record(P, "ShardedScorer world 1 -> fd_score_batch_pipelined, no vectors requested: the fused "
-                             "ensemble kernel from the compact 24-float vectors (the timed variant); twin: one more "
+                             "ensemble kernel from the compact 64-B rows (the timed variant); twin: one more "
                              "batch with vectors + model probabilities requested (64-wide vectors)", B)
         out["stream"] = self.stream
         vec = torch.empty((B, 64), dtype=torch.float32, device=self.dev["ts_ms"].device)

@@ -693,7 +693,7 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
    ring's whole capacity K of prior events — their counts may be truncated at K; synchronises the engine's streams),
    "pipelined_batches" (batches through fd_score_batch_pipelined /
    fd_score_records_pipelined so far), "pipelined_compact_batches" (of those, scored by the fused ensemble kernel from
-   the compact 24-float vectors: no vectors requested), "pipelined_slot_stream_batches" (of those, with the slot pass on
+   the compact 64-B rows: no vectors requested), "pipelined_slot_stream_batches" (of those, with the slot pass on
    its own stream), "pipelined_host_ns" (host nanoseconds inside fd_score_batch_pipelined), "sharded_steps" (fd_sharded_step calls) and "sharded_host_ns_<phase>" (host
    nanoseconds inside fd_sharded_step by phase: "wait" the split sizes, "partition" / "counts" / "count_copy" the
    next batch's route kernels, count exchange and copy to the host, "records" the records exchange, "score" the

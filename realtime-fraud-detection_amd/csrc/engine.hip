@@ -1089,7 +1089,7 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   // mode 1: the slot pass (scratch set s & 1, untouched by batch i-1) runs at once; the bucket pass waits for
   // batch i-1's card updates
   hipEvent_t before_buckets = e.pipe_feat_live[prev] ? e.pipe_feat_ev[prev] : nullptr;
-  // the fused kernel alone reads the vectors and nobody asked for them: the compact form (96 instead of 256 B per
+  // the fused kernel alone reads the vectors and nobody asked for them: the compact form (64 instead of 256 B per
   // transaction written here and read by the ensemble kernel, fd_internal.h kCompactSlot)
   const bool compact = e.compact_vectors && d_vectors == nullptr && fd::ensemble_applies(e, *params, slots, present, n);
   e.pipe_vec[s].ensure((size_t)n * FD_VECTOR_WIDTH * 4);

@@ -312,15 +312,8 @@ __device__ __forceinline__ void bin_compact_constants(const EnsArgs& a, uint16_t
 // binned by one lookup in a per-plan table of the bins of 0..31 (staged in LDS), not searched: each thread keeps 3-4
 // searches of its 5-6 (one lockstep group instead of two). A value outside 0..31 or not integral (never, from the
 // engine's own feature kernel) takes its own search, so the bins stay #{t <= v} for any input.
-constexpr int kIntSlots = 8;
-constexpr int kIntCompact[kIntSlots] = {2, 3, 4, 5, 6, 9, 12, 15};  // compact indices (features 5 6 7 14 15 19 26 32)
-constexpr int kLutN = 32;
+constexpr int kLutN = 32;  // (kIntSlots, kIntCompact, int_slot: fd_internal.h, the compact row's byte slots)
 static_assert(kIntSlots * kLutN == 8 * 32, "EnsArgs::lut");
-__host__ __device__ constexpr int int_slot(int ci) {
-  for (int k = 0; k < kIntSlots; ++k)
-    if (kIntCompact[k] == ci) return k;
-  return -1;
-}
 // thread Q's compact indices Q + 4 i: the LUT row of each small-integer one (-1: searched), and the searched i's
 constexpr int kIntOf[4][6] = {{-1, 2, -1, 6, -1, -1}, {-1, 3, 5, -1, -1, -1}, {0, 4, -1, -1, -1, -1},
                               {1, -1, -1, 7, -1, -1}};
@@ -343,6 +336,24 @@ constexpr bool int_tables_agree() {
   return true;
 }
 static_assert(int_tables_agree(), "kIntOf / kSearched must follow kIntCompact and kCompactSlot");
+
+// thread Q's share of a compact row (fd_internal.h: 14 f32 words, then 8 byte slots): compact slots Q, Q + 4, ...
+// into v[0..5], the byte slots as the f32 of their integer (exactly the value the feature kernel computed)
+template <int Q>
+__device__ __forceinline__ void load_compact(const float* __restrict__ xr, float (&v)[16]) {
+  const unsigned long long ib = *reinterpret_cast<const unsigned long long*>(xr + 14);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int ci = Q + 4 * i;
+    if (ci >= kCompactSlots) {
+      v[i] = 0.f;
+    } else if (int_slot(ci) >= 0) {
+      v[i] = (float)(unsigned)((ib >> (8 * int_slot(ci))) & 0xFFull);
+    } else {
+      v[i] = xr[compact_word(ci)];
+    }
+  }
+}
 
 template <int Q, int L, bool LUT>
 __device__ __forceinline__ void bin_compact_pass(const EnsArgs& a, const float (&v)[16], uint16_t* Xs,
@@ -453,13 +464,11 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     float v[16];
     if (valid && a.compact) {
       const float* xr = a.X + row * (int64_t)kCompactWidth;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) v[i] = q + 4 * i < kCompactSlots ? xr[q + 4 * i] : 0.f;
       switch (q) {  // wave-uniform
-        case 0: bin_compact_constants<0>(a, Xs, txn); break;
-        case 1: bin_compact_constants<1>(a, Xs, txn); break;
-        case 2: bin_compact_constants<2>(a, Xs, txn); break;
-        default: bin_compact_constants<3>(a, Xs, txn); break;
+        case 0: load_compact<0>(xr, v); bin_compact_constants<0>(a, Xs, txn); break;
+        case 1: load_compact<1>(xr, v); bin_compact_constants<1>(a, Xs, txn); break;
+        case 2: load_compact<2>(xr, v); bin_compact_constants<2>(a, Xs, txn); break;
+        default: load_compact<3>(xr, v); bin_compact_constants<3>(a, Xs, txn); break;
       }
     } else if (valid) {
       const float* xr = a.X + row * (int64_t)a.ld;

@@ -25,12 +25,31 @@ constexpr int kMaxFeatures = 64;  // model columns held in LDS ([feature][kTile]
 // The compact scoring vector of the fused pipeline (features.hip write_vector -> ensemble.hip prologue): of the 64
 // slots of the engine's vector (FeatureProcessor's 41 definitions + derived features + pad, _prepare_features) only
 // these 22 vary per transaction; slots 12, 24, 25, 33, 34 are always 0.5 (defaults with no bridged source) and the
-// rest 0. The pipelined stream writes 24 floats (96 B: the 22 + 2 pad) per transaction instead of 64 (256 B) when
-// nothing else reads the vectors, and the ensemble kernel expands them.
-constexpr int kCompactWidth = 24;
+// rest 0. The pipelined stream writes a 64-B row per transaction instead of 64 floats (256 B) when nothing else reads
+// the vectors, and the ensemble kernel expands it: the 14 slots with arbitrary values as f32 in words
+// 0..13 (compact-index order), the 8 that are always small integers — hour, day of week, weekend, the 1 h / 24 h /
+// 5 min counts, the account age (each clip10 of an integer), the new-device flag — as bytes 56..63.
+constexpr int kCompactWidth = 16;  // row stride in 4-B words
 constexpr int kCompactSlots = 22;
 constexpr int kCompactSlot[kCompactSlots] = {0, 1, 5, 6, 7, 14, 15, 16, 17, 19, 21, 23,
                                              26, 27, 31, 32, 41, 42, 43, 44, 45, 46};
+constexpr int kIntSlots = 8;
+constexpr int kIntCompact[kIntSlots] = {2, 3, 4, 5, 6, 9, 12, 15};  // compact indices (features 5 6 7 14 15 19 26 32)
+// the byte (0..7) of a small-integer compact slot, -1 for the others
+__host__ __device__ constexpr int int_slot(int ci) {
+  for (int k = 0; k < kIntSlots; ++k)
+    if (kIntCompact[k] == ci) return k;
+  return -1;
+}
+// the f32 word (0..13) of a compact slot with arbitrary values, -1 for the small-integer ones
+__host__ __device__ constexpr int compact_word(int ci) {
+  if (int_slot(ci) >= 0) return -1;
+  int w = 0;
+  for (int k = 0; k < ci; ++k) w += int_slot(k) < 0 ? 1 : 0;
+  return w;
+}
+static_assert(compact_word(kCompactSlots - 1) == kCompactSlots - kIntSlots - 1 && kCompactSlots - kIntSlots <= 14,
+              "14 f32 words, then the 8 bytes");
 // the slot's place in the compact row, -2 for the constant 0.5, -1 for the constant 0
 __host__ __device__ constexpr int compact_src(int f) {
   for (int k = 0; k < kCompactSlots; ++k)

@@ -360,10 +360,19 @@ __device__ void write_vector(const double* r, float o1, float dv0, float* __rest
     }
   }
   float4* o4 = reinterpret_cast<float4*>(out);
-  if (compact) {  // the 22 slots that vary (fd_internal.h kCompactSlot) + 2 pad: 6 x 16 B
+  if (compact) {  // the 22 slots that vary (fd_internal.h kCompactSlot): 14 f32 words + 8 byte slots, 4 x 16 B
     float c[kCompactWidth];
+    unsigned ib[2] = {0u, 0u};
 #pragma unroll
-    for (int k = 0; k < kCompactWidth; ++k) c[k] = k < kCompactSlots ? o[kCompactSlot[k < kCompactSlots ? k : 0]] : 0.f;
+    for (int ci = 0; ci < kCompactSlots; ++ci) {
+      const float x = o[kCompactSlot[ci]];
+      if (int_slot(ci) >= 0)  // an integer in 0..23 (see kIntCompact): exact as a byte (v_cvt_pk_u8_f32)
+        ib[int_slot(ci) >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(x, int_slot(ci) & 3, ib[int_slot(ci) >> 2]);
+      else
+        c[compact_word(ci)] = x;
+    }
+    c[14] = __uint_as_float(ib[0]);
+    c[15] = __uint_as_float(ib[1]);
 #pragma unroll
     for (int q = 0; q < kCompactWidth / 4; ++q) o4[q] = make_float4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
     return;

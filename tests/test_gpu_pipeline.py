@@ -2,7 +2,7 @@
 feature stream overlap batch i's forests) against fd_score_batch_device on a twin engine with the same state:
 every batch's outputs bit-identical, the card state after the stream identical (the next batch's vectors), with
 other engine calls interleaved and with inputs that arrive on a side stream behind an `input_ready` event. The
-pipelined batches that go through the fused ensemble kernel without a vectors output use the compact 24-float vector
+pipelined batches that go through the fused ensemble kernel without a vectors output use the compact 64-B row
 (fd_internal.h kCompactSlot); the reference engine writes and reads the full 64-wide one: same bits.
 Reference chain: FeatureExtractor -> RedisTransactionSink -> FeatureProcessor -> EnsemblePredictor.predict
 (fl/features/FeatureExtractor.java:50-87, ml/models/ensemble_predictor.py:75-148), one micro-batch at a time."""
