@@ -23,6 +23,7 @@ times, and the CPU baseline: the oracle C restatement of the whole chain on a co
 (100k simulator transactions), at 1 core and at the host threads available (rank 0, N=1 only).
 """
 import argparse
+import gc
 import json
 import os
 import socket
@@ -1501,6 +1502,11 @@ def make_parser():
                          "transactions whose 24 h window held all K)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--secondary", default=None,
+                    help="config 4 at N = 1: other BASELINE configurations run after the line's own measurements, each "
+                         "as a child process (its own engine, 200 steps), their results embedded as "
+                         "secondary_workloads (comma list; default config5,config2,config3; 'none' or "
+                         "FD_BENCH_SECONDARY=0 to skip)")
     ap.add_argument("--pipeline", action="store_true",
                     help="config5: the pipelined stream (batch i+1's features beside batch i's scoring) instead of "
                          "fd_score_batch_device per step")
@@ -1593,7 +1599,6 @@ def main():
         wl.next_batch += _diag_offset()
     # a serving process's setup is done: move every object allocated so far out of the cyclic collector's view
     # (a full collection over the setup's objects stalls the host for milliseconds mid-stream)
-    import gc
     gc.collect()
     gc.freeze()
     # p50 / p99: one micro-batch at a time, then the same from pinned host memory (run after the throughput region:
@@ -1836,10 +1841,72 @@ def main():
                                     "peak_GBs": HBM_PEAK_GBS,
                                     "frac": round(per_gpu * FUSED_BYTES_PER_TXN / 1e9 / HBM_PEAK_GBS, 6),
                                     "basis": "SURVEY §8(d) fused-pipeline algorithmic bytes x txn/s per GPU"}
+        secondary = _secondary_list(args, world, wl.name)
+        if secondary:
+            # the line's own measurements are complete: free this process's GPU state (the config-4 card table is
+            # ~160 GB of the card's 288) before the children allocate theirs
+            wl = None
+            eng.close()
+            gc.unfreeze()
+            gc.collect()
+            torch.cuda.empty_cache()
+            line["secondary_workloads"] = _run_secondaries(secondary)
         print(json.dumps(line), flush=True)
     eng.close()
     if dist:
         dist.destroy_process_group()
+
+
+SECONDARY_DEFAULT = ("config5", "config2", "config3")  # BASELINE configs[4], [1], [2]
+
+
+def _secondary_list(args, world, name):
+    if world != 1 or name != "config4" or os.environ.get("FD_BENCH_SECONDARY", "1") == "0":
+        return []
+    if args.secondary is None:
+        return list(SECONDARY_DEFAULT)
+    if args.secondary.strip().lower() in ("", "none"):
+        return []
+    return [w.strip() for w in args.secondary.split(",") if w.strip() in WORKLOADS and w.strip() != "config4"]
+
+
+def _run_secondaries(names):
+    """Each secondary workload as `python bench.py --workload W --steps 200 --warmup 20 --no-cpu-baseline` in a child
+    process (started after this process freed its GPU state; never an exec), its JSON line parsed and summarised:
+    the other BASELINE configurations measured by the same command the driver runs."""
+    out = {}
+    for w in names:
+        cmd = [sys.executable, str(Path(__file__).resolve()), "--workload", w, "--steps", "200", "--warmup", "20",
+               "--no-cpu-baseline", "--secondary", "none"]
+        a = time.perf_counter()
+        try:
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+            rows = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode != 0 or not rows:
+                out[w] = {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-600:]}
+                continue
+            d = json.loads(rows[-1])
+        except Exception as e:  # a failed secondary is reported, never fatal to the line
+            out[w] = {"error": repr(e)}
+            continue
+        roof = d.get("roofline") or {}
+        par = d.get("parity_vs_oracle") or {}
+        out[w] = {
+            "workload": (d.get("config") or {}).get("workload"),
+            "metric": d.get("metric"), "value": d.get("value"), "unit": d.get("unit"),
+            "ms_per_step": d.get("ms_per_step"), "steps": d.get("steps"), "warmup": d.get("warmup"),
+            "p50_batch_latency_ms": d.get("p50_batch_latency_ms"), "p99_batch_latency_ms": d.get("p99_batch_latency_ms"),
+            "p99_batch_latency_with_h2d_ms": d.get("p99_batch_latency_with_h2d_ms"),
+            "dtype": d.get("dtype"),
+            "roofline": {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "kernel", "kernel_avg_us")
+                         if k in roof} or None,
+            "kernel_avg_us": d.get("kernel_avg_us"),
+            "parity_vs_oracle": {k: v for k, v in par.items() if not isinstance(v, (list, dict))} or None,
+            "parity_legs": {k: {q: u for q, u in v.items() if not isinstance(u, (list, dict))}
+                            for k, v in par.items() if isinstance(v, dict)} or None,
+            "wall_s": round(time.perf_counter() - a, 1),
+        }
+    return out
 
 
 if __name__ == "__main__":

@@ -56,3 +56,21 @@ def test_committed_summaries_parse():
     for p in sorted((bench.REPO / "profiles").glob("pmc_*.json")):
         d = json.loads(p.read_text())
         assert int(d["batch"]) > 0 and isinstance(d["kernels"], dict), p
+
+
+def test_secondary_workloads_only_for_the_config4_line(monkeypatch):
+    """The default line (config 4, N = 1) runs the other BASELINE configurations as child processes after its own
+    measurements; N > 1, other workloads, the children themselves ('none') and FD_BENCH_SECONDARY=0 run none."""
+    class A:
+        secondary = None
+    monkeypatch.delenv("FD_BENCH_SECONDARY", raising=False)
+    assert bench._secondary_list(A, 1, "config4") == list(bench.SECONDARY_DEFAULT)
+    assert bench._secondary_list(A, 2, "config4") == []
+    assert bench._secondary_list(A, 1, "config5") == []
+    A.secondary = "none"
+    assert bench._secondary_list(A, 1, "config4") == []
+    A.secondary = "config5, ingest,bogus,config4"
+    assert bench._secondary_list(A, 1, "config4") == ["config5", "ingest"]
+    A.secondary = None
+    monkeypatch.setenv("FD_BENCH_SECONDARY", "0")
+    assert bench._secondary_list(A, 1, "config4") == []
