@@ -36,7 +36,7 @@ for wl in ${WORKLOADS:-}; do
   grep '^{' "$OUT/$TAG.bench_$wl.log" > "$OUT/$TAG.$wl.bench.json" || true
 done
 if [ "${PROFILE:-1}" = "1" ]; then
-  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$TAG.prof" -o run -- \
+  FD_BENCH_SECONDARY=0 run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$TAG.prof" -o run -- \
       python "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline --latency-iters 10; rc=$?
   fatal $rc && exit $rc
 fi
