@@ -1419,7 +1419,7 @@ def _read_timing(eng, wl):
 def _host_counters(eng):
     """the engine's cumulative host-side counters for the pipelined / sharded step (None where unsupported)"""
     out = {}
-    for k in ("pipelined_batches", "pipelined_host_ns", "sharded_steps"):
+    for k in ("pipelined_batches", "pipelined_host_ns", "sharded_steps", "rccl_ops"):
         try:
             out[k] = eng.counter(k)
         except Exception:
@@ -1437,9 +1437,12 @@ def _host_breakdown(h0, h1, submit_s, steps):
         return None
     native = (h1["pipelined_host_ns"] - h0["pipelined_host_ns"]) / 1e3 / steps
     total = submit_s * 1e6 / steps
-    return {"native_us_per_step": round(native, 2), "above_native_us_per_step": round(total - native, 2),
-            "pipelined_calls": calls, "basis": "engine counter pipelined_host_ns (steady_clock around "
-                                               "fd_score_batch_pipelined's body) over the timed region"}
+    out = {"native_us_per_step": round(native, 2), "above_native_us_per_step": round(total - native, 2),
+           "pipelined_calls": calls, "basis": "engine counter pipelined_host_ns (steady_clock around "
+                                              "fd_score_batch_pipelined's body) over the timed region"}
+    if h0.get("rccl_ops") is not None and h1.get("rccl_ops") is not None and h1["rccl_ops"] > h0["rccl_ops"]:
+        out["rccl_ops_per_step"] = round((h1["rccl_ops"] - h0["rccl_ops"]) / steps, 2)  # N > 1: sends / recvs / gathers
+    return out
 
 
 def _saturated(eng, wl):

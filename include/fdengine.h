@@ -438,14 +438,17 @@ int fd_score_records_pipelined(fd_engine* eng, const fd_blend_params* params, co
                                void* input_ready);
 /* The sharded step as one call over the engine's own RCCL communicators (csrc/comm.hip): the host loads
    RCCL once (the process's librccl.so, by path; any library exporting ncclGetUniqueId, ncclCommInitRank,
-   ncclCommDestroy, ncclCommAbort, ncclGroupStart/End, ncclSend/Recv and ncclGetErrorString can stand in — the tests run several
+   ncclCommDestroy, ncclCommAbort, ncclGroupStart/End, ncclSend/Recv, ncclAllGather and ncclGetErrorString can stand in — the tests run several
    ranks on one GPU over an in-process loopback of that API), rank 0 makes two unique ids (fd_comm_unique_id), the
    host broadcasts them, every rank calls fd_comm_init (collective, blocking with RCCL). fd_sharded_step then runs
    one micro-batch: its split sizes (exchanged by the previous call when it prefetched this batch, else now: the
    step's one host wait), then, on the engine's forward stream behind the wait for this batch's inbox slot, ONE
    RCCL group holding this batch's records to their owners (ncclSend/ncclRecv with per-peer counts) and — with
-   `next` (optional: prefetch) — the next batch's count exchange, its count kernel queued before the group and its
-   publish + places after it (so the next counts land while this batch is scored), then the owner's
+   `next` (optional: prefetch) — the next batch's count exchange (from 4 ranks one ncclAllGather of every rank's
+   per-peer send counts right after the group, below that 2 x world point-to-point operations inside it: engine
+   option count_exchange), its
+   count kernel queued before the group and its publish + places after it (so the next counts land while this
+   batch is scored), then the owner's
    features + scoring (fd_score_records_pipelined's pipeline, the features waiting for the records), the
    results back (second communicator, engine stream) and into arrival order in the caller's outputs (device or
    host-mapped memory), written on the engine stream. The calling thread issues every communicator operation, in
@@ -684,6 +687,9 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      DESIGN.md §3)
      "comm_timeout_ms": fd_sharded_step's split-size wait fails with FD_ERR_HIP after this many ms (default
      120000): a peer that never posts its counts (a dead rank, a different call pattern) becomes an error, not a hang
+     "count_exchange": fd_sharded_step's per-peer counts as 1 one ncclAllGather per batch, 0 2 x world
+     ncclSend/ncclRecv in the records group, -1 (default) the all-gather from 4 ranks (every rank the same; not while
+     a prefetched batch is pending)
      "stream_priority": HIP priorities of the engine's pipeline and forward streams (ROCm keeps a hardware-queue
      pool per priority, so they stop sharing queues with the engine stream and RCCL's streams): 0 all default, 1
      the two pipeline streams high, 2 + the forward stream low, 3 (default) + the forward stream high. Set before
@@ -694,7 +700,8 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value);
    "pipelined_batches" (batches through fd_score_batch_pipelined /
    fd_score_records_pipelined so far), "pipelined_compact_batches" (of those, scored by the fused ensemble kernel from
    the compact 64-B rows: no vectors requested), "pipelined_slot_stream_batches" (of those, with the slot pass on
-   its own stream), "pipelined_host_ns" (host nanoseconds inside fd_score_batch_pipelined), "sharded_steps" (fd_sharded_step calls) and "sharded_host_ns_<phase>" (host
+   its own stream), "pipelined_host_ns" (host nanoseconds inside fd_score_batch_pipelined), "sharded_steps" (fd_sharded_step calls), "rccl_ops" (RCCL operations the exchanges issued: sends, receives,
+   all-gathers) and "sharded_host_ns_<phase>" (host
    nanoseconds inside fd_sharded_step by phase: "wait" the split sizes, "partition" / "counts" / "count_copy" the
    next batch's route kernels, count exchange and copy to the host, "records" the records exchange, "score" the
    owner's pipeline launches, "back" / "scatter" the results exchange and the scatter into arrival order). */

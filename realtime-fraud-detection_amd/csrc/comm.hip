@@ -7,7 +7,7 @@
 // step is one C-ABI call and no Python collective sits between the kernels.
 //
 // RCCL is the one the host process already loaded (torch's librccl.so, passed by path): dlopen on the same file
-// returns that instance, so the process keeps one RCCL and one HIP runtime. Any library exporting the same nine
+// returns that instance, so the process keeps one RCCL and one HIP runtime. Any library exporting the same ten
 // symbols can stand in (the tests' in-process loopback, tests/native/rccl_loopback.cpp, runs several ranks on one
 // GPU); each communicator remembers the library it came from. Two communicators per engine: `fwd` (count and
 // record exchanges, on the engine's forward stream) and `back` (results, on the engine stream). The calling
@@ -35,6 +35,7 @@ struct RcclApi {
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
 };
 
@@ -65,6 +66,7 @@ const RcclApi& rccl(const char* path) {
   sym(h, "ncclGroupEnd", a.group_end);
   sym(h, "ncclSend", a.send);
   sym(h, "ncclRecv", a.recv);
+  sym(h, "ncclAllGather", a.all_gather);
   sym(h, "ncclGetErrorString", a.error_string);
   return g_rccl->emplace(path, a).first->second;
 }
@@ -104,6 +106,7 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
   c.back = k;
   c.rank = rank;
   c.world = world;
+  c.count_gather = c.count_mode == 1 || (c.count_mode < 0 && world >= 4);
   if (!c.x_fwd) c.x_fwd = make_stream(e.stream_prio == 2 ? -1 : e.stream_prio == 3 ? 1 : 0);
   for (int s = 0; s < 2; ++s) {
     if (!c.h_cnt[s]) {
@@ -112,8 +115,10 @@ void comm_init(Engine& e, const char* rccl_path, int rank, int world, const uint
       c.cnt_seq[s] = 0;
       FD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c.d_hcnt[s]), c.h_cnt[s], 0));
     }
-    c.cnt[s].ensure(2 * FD_MAX_SHARDS * sizeof(int64_t));
-    FD_HIP(hipMemset(c.cnt[s].ptr, 0, 2 * FD_MAX_SHARDS * sizeof(int64_t)));
+    // send [G], then the receive half: [G] (point-to-point counts) or the G x G all-gathered matrix
+    const size_t cb = (size_t)(FD_MAX_SHARDS + FD_MAX_SHARDS * FD_MAX_SHARDS) * sizeof(int64_t);
+    c.cnt[s].ensure(cb);
+    FD_HIP(hipMemset(c.cnt[s].ptr, 0, cb));
   }
   for (int q = 0; q < ShardComm::kInbox; ++q) {
     if (!c.in_ev[q]) FD_HIP(hipEventCreateWithFlags(&c.in_ev[q], hipEventDisableTiming | hipEventDisableSystemFence));
@@ -214,6 +219,7 @@ void counts_pre(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t ready, i
   launch_route_count(t, n, c.world, c.cnt[s].as<int64_t>(), st, c.route_blk);  // send half zero (comm_init)
 }
 
+// the point-to-point form (option count_exchange 0): inside the caller's group
 void counts_ops(Engine& e, int s) {
   ShardComm& c = e.comm;
   const RcclApi& R = api(c);
@@ -224,6 +230,18 @@ void counts_ops(Engine& e, int s) {
     check(R, R.send(cnt + p, 1, ncclInt64, p, f, c.x_fwd), "ncclSend (counts)");
     check(R, R.recv(cnt + G + p, 1, ncclInt64, p, f, c.x_fwd), "ncclRecv (counts)");
   }
+  c.ops.fetch_add(2 * (unsigned long long)G, std::memory_order_relaxed);
+}
+
+// the all-gather form (default): every rank's send vector to every rank, one collective outside any group (the same
+// place in the call sequence on every rank: after the records group, or alone)
+void counts_gather(Engine& e, int s) {
+  ShardComm& c = e.comm;
+  const RcclApi& R = api(c);
+  int64_t* cnt = c.cnt[s].as<int64_t>();
+  check(R, R.all_gather(cnt, cnt + c.world, (size_t)c.world, ncclInt64, static_cast<ncclComm_t>(c.fwd), c.x_fwd),
+        "ncclAllGather (counts)");
+  c.ops.fetch_add(1, std::memory_order_relaxed);
 }
 
 void counts_post(Engine& e, const fd_txn_batch& t, int64_t n, int s) {
@@ -232,7 +250,7 @@ void counts_post(Engine& e, const fd_txn_batch& t, int64_t n, int s) {
   const unsigned long long seq = ++c.cnt_seq[s];
   auto* dseq = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(c.d_hcnt[s]) + kCntSeqOff);
   c.rec[s].ensure_headroom((size_t)std::max<int64_t>(n, 1) * sizeof(RouteRecord));
-  const CountPublish pub{c.cnt[s].as<int64_t>(), c.world, c.d_hcnt[s], dseq, seq};
+  const CountPublish pub{c.cnt[s].as<int64_t>(), c.world, c.count_gather ? c.rank : -1, c.d_hcnt[s], dseq, seq};
   launch_route_place(t, n, c.world, c.rec[s].ptr, st, c.route_blk, &pub);  // its scan kernel publishes first
 }
 }  // namespace
@@ -241,9 +259,13 @@ void comm_launch_counts(Engine& e, const fd_txn_batch& t, int64_t n, hipEvent_t 
   const RcclApi& R = api(e.comm);
   counts_pre(e, t, n, ready, s);
   L(1);
-  check(R, R.group_start(), "ncclGroupStart");
-  counts_ops(e, s);
-  check(R, R.group_end(), "ncclGroupEnd (counts)");
+  if (e.comm.count_gather) {
+    counts_gather(e, s);
+  } else {
+    check(R, R.group_start(), "ncclGroupStart");
+    counts_ops(e, s);
+    check(R, R.group_end(), "ncclGroupEnd (counts)");
+  }
   L(2);
   counts_post(e, t, n, s);
   L(3);
@@ -325,9 +347,10 @@ void comm_forward_group(Engine& e, int s, const fd_txn_batch* next, int64_t next
   c.res[s].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(ResultRecord));
   check(R, R.group_start(), "ncclGroupStart");
   exchange_ops(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[q].ptr, recv, sizeof(RouteRecord));
-  if (next) counts_ops(e, ns);
+  if (next && !c.count_gather) counts_ops(e, ns);
   check(R, R.group_end(), "ncclGroupEnd (records + counts)");
   FD_HIP(hipEventRecord(c.in_ev[q], c.x_fwd));
+  if (next && c.count_gather) counts_gather(e, ns);
   L(4);
   if (next) counts_post(e, *next, next_n, ns);
   L(3);
@@ -343,12 +366,15 @@ void exchange_ops(Engine& e, bool back, hipStream_t st, const void* sendbuf, con
   const char* sb = static_cast<const char*>(sendbuf);
   char* rb = static_cast<char*>(recvbuf);
   size_t os = 0, orr = 0;
+  unsigned long long n_ops = 0;
   for (int p = 0; p < c.world; ++p) {
     if (send[p] > 0) check(R, R.send(sb + os * elem, (size_t)send[p] * elem, ncclUint8, p, k, st), "ncclSend");
     if (recv[p] > 0) check(R, R.recv(rb + orr * elem, (size_t)recv[p] * elem, ncclUint8, p, k, st), "ncclRecv");
+    n_ops += (send[p] > 0) + (recv[p] > 0);
     os += (size_t)send[p];
     orr += (size_t)recv[p];
   }
+  c.ops.fetch_add(n_ops, std::memory_order_relaxed);
 }
 
 void comm_exchange(Engine& e, bool back, hipStream_t st, const void* sendbuf, const int64_t* send, void* recvbuf,

@@ -468,6 +468,8 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
     *value = (int64_t)v;
   } else if (k == "sharded_steps") {  // fd_sharded_step calls so far
     *value = (int64_t)e.comm.steps.load();
+  } else if (k == "rccl_ops") {  // RCCL operations issued by the engine's exchanges (send, recv, all-gather)
+    *value = (int64_t)e.comm.ops.load();
   } else if (k.rfind("sharded_host_ns_", 0) == 0) {  // host time inside fd_sharded_step by phase
     int i = 0;
     while (i < fd::ShardComm::kHostPhases && k.compare(16, std::string::npos, fd::kShardHostPhase[i]) != 0) ++i;
@@ -518,6 +520,13 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "small_streams") {  // latency batches: 2 LSTM | other forests on two side streams, 1 one, 0 none
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "small_streams must be 0, 1 or 2");
     e.small_streams = (int)value;
+  } else if (k == "count_exchange") {  // fd_sharded_step's per-peer counts: 1 one ncclAllGather per batch, 0 2G
+    // point-to-point operations in the records group, -1 (default) the all-gather from 4 ranks; set before
+    // fd_comm_init or between steps with no batch prefetched (every rank the same)
+    FD_REQUIRE(value >= -1 && value <= 1, FD_ERR_INVALID_ARG, "count_exchange must be -1, 0 or 1");
+    FD_REQUIRE(!e.comm.pending, FD_ERR_INVALID_ARG, "count_exchange: a prefetched batch's counts are in flight");
+    e.comm.count_mode = (int)value;
+    e.comm.count_gather = value == 1 || (value < 0 && e.comm.world >= 4);
   } else if (k == "comm_timeout_ms") {  // fd_sharded_step: the split-size wait gives up (FD_ERR_HIP) after this
     FD_REQUIRE(value >= 1, FD_ERR_INVALID_ARG, "comm_timeout_ms must be >= 1");
     e.comm.timeout_ms = value;

@@ -457,10 +457,17 @@ struct ShardComm {
   // opposite orders on two ranks. (Round 3 ran the next batch's forward half on a worker thread; it measured no
   // faster - 0.0932 vs 0.0943 ms per step, profiles/r03/route_overhead_stream_priority_p1.log - and had that hazard.)
   int64_t timeout_ms = 120000;  // option "comm_timeout_ms": the split-size wait gives up (FD_ERR_HIP) after this
+  // option "count_exchange": 1 a batch's per-peer counts travel as ONE ncclAllGather of every rank's send vector
+  // (cnt[s]: send [G], then the G x G matrix), issued right after the records group; 0 as 2G point-to-point
+  // operations inside it (send [G], receive [G]); -1 (default) the all-gather from 4 ranks (a separate RCCL launch
+  // costs ~2 us more host time than the world-1 group's two self operations; at 8 ranks it replaces 16)
+  int count_mode = -1;
+  bool count_gather = false;  // the form in use (count_mode, world)
   int device = 0;
   // host time inside fd_sharded_step by phase (ns, counters "sharded_host_ns_<phase>", kShardHostPhase order)
   static constexpr int kHostPhases = 8;
   std::atomic<unsigned long long> steps{0}, host_ns[kHostPhases] = {};
+  std::atomic<unsigned long long> ops{0};  // RCCL operations issued (send, recv, all-gather; counter "rccl_ops")
 };
 // "wait": the split sizes; "partition", "counts", "count_copy": a batch's route kernels, count exchange and copy to
 // the host; "records": the records exchange; "score": the owner's pipeline; "back", "scatter": results
@@ -668,6 +675,7 @@ void launch_route_count(const fd_txn_batch& t, int64_t n, int G, int64_t* totals
 struct CountPublish {
   int64_t* cnt;
   int G;
+  int gather_rank;  // >= 0: the receive counts are column gather_rank of the all-gathered matrix at cnt + G
   int64_t* h;
   unsigned long long* h_seq;
   unsigned long long seq;

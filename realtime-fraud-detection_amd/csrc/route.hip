@@ -77,7 +77,9 @@ __global__ void __launch_bounds__(1024) route_scan_kernel(int* __restrict__ blk,
   const int t = threadIdx.x;
   if (pub.cnt) {  // the sharded step's split sizes first (the host is waiting for them), then the scan
     if (t < 2 * pub.G) {
-      __hip_atomic_store(pub.h + t, pub.cnt[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const int64_t v = (t >= pub.G && pub.gather_rank >= 0) ? pub.cnt[pub.G + (t - pub.G) * pub.G + pub.gather_rank]
+                                                             : pub.cnt[t];
+      __hip_atomic_store(pub.h + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __threadfence_system();
       if (t < pub.G) pub.cnt[t] = 0;
     }

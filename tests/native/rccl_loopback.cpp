@@ -1,8 +1,10 @@
 // TEST INFRASTRUCTURE ONLY — never loaded by the product path.
 //
-// An in-process loopback of the nine RCCL entry points the engine's sharded step uses (csrc/comm.hip dlopens its
+// An in-process loopback of the ten RCCL entry points the engine's sharded step uses (csrc/comm.hip dlopens its
 // RCCL by path and calls only these): ncclGetUniqueId, ncclCommInitRank, ncclCommDestroy, ncclCommAbort,
-// ncclGroupStart, ncclGroupEnd, ncclSend, ncclRecv, ncclGetErrorString. It lets one process run several ranks — one engine and one
+// ncclGroupStart, ncclGroupEnd, ncclSend, ncclRecv, ncclAllGather, ncclGetErrorString. An all-gather is its
+// point-to-point form here (a send of the rank's buffer to every rank and a receive from every rank into its place,
+// posted as one group). It lets one process run several ranks — one engine and one
 // host thread per rank, all on the test box's one GPU — through the very fd_sharded_step the driver runs across
 // GPUs, so the N >= 2 step is executed and checked against the oracle without a multi-GPU node
 // (tests/test_gpu_sharding_loopback.py). RCCL itself refuses two ranks on one device.
@@ -303,6 +305,21 @@ ncclResult_t ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatyp
 ncclResult_t ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int peer, ncclComm_t comm,
                       hipStream_t stream) {
   return post(false, nullptr, recvbuff, count, datatype, peer, comm, stream);
+}
+
+ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcount, ncclDataType_t datatype,
+                           ncclComm_t comm, hipStream_t stream) {
+  if (!comm || type_size(datatype) == 0) return ncclInvalidArgument;
+  const size_t bytes = sendcount * type_size(datatype);
+  ncclGroupStart();
+  ncclResult_t rc = ncclSuccess;
+  for (int p = 0; p < comm->nranks && rc == ncclSuccess; ++p) {
+    rc = post(true, sendbuff, nullptr, sendcount, datatype, p, comm, stream);
+    if (rc == ncclSuccess)
+      rc = post(false, nullptr, static_cast<char*>(recvbuff) + (size_t)p * bytes, sendcount, datatype, p, comm, stream);
+  }
+  const ncclResult_t g = ncclGroupEnd();
+  return rc != ncclSuccess ? rc : g;
 }
 
 const char* ncclGetErrorString(ncclResult_t result) {

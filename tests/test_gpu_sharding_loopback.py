@@ -58,11 +58,12 @@ def _batches(streams, sizes, r):
     return out
 
 
-def _engine(pop, owned, xgb, ifm, slot_stream=-1):
+def _engine(pop, owned, xgb, ifm, slot_stream=-1, count_exchange=-1):
     from fdengine import FraudEngine
     U, M = pop["users"], pop["merchants"]
     e = FraudEngine(0)
     e.set_option("slot_stream", slot_stream)  # -1 auto: off at this table size; 2 as config 4 runs it
+    e.set_option("count_exchange", count_exchange)  # 1 one all-gather per batch's counts, 0 p2p, -1 by world
     e.state_init(4 * N_USERS + 4096, 1, 16)
     e.load_users(U["key"][owned], U["avg_amount"][owned], U["account_age_days"][owned], U["device_fp"][owned])
     e.load_merchants(M["fraud_rate"], M["risk_multiplier"])
@@ -81,7 +82,7 @@ def _prefetch_plan(s, parts):
     return parts[s + 1]
 
 
-def _run_ranks(world, slot_stream=-1):
+def _run_ranks(world, slot_stream=-1, count_exchange=-1):
     import torch
 
     from fdengine import FraudEngine
@@ -91,7 +92,8 @@ def _run_ranks(world, slot_stream=-1):
     pop, streams, sizes, xgb, ifm = _setup(world)
     path = str(LOOPBACK)
     ids = (FraudEngine.comm_unique_id(path), FraudEngine.comm_unique_id(path))
-    engines = [_engine(pop, owned_mask(pop["users"]["key"], r, world), xgb, ifm, slot_stream) for r in range(world)]
+    engines = [_engine(pop, owned_mask(pop["users"]["key"], r, world), xgb, ifm, slot_stream, count_exchange)
+               for r in range(world)]
     dev = [[{f: torch.from_numpy(np.ascontiguousarray(b[f])).cuda() for f in TXN_FIELDS}
             for b in _batches(streams, sizes, r)] for r in range(world)]
     torch.cuda.synchronize()
@@ -130,7 +132,7 @@ def _run_ranks(world, slot_stream=-1):
                 engines[r].sync()
             results[r] = (np.concatenate([np.stack([h[0].numpy(), h[1].numpy(), h[2].numpy().astype(np.float64),
                                                     h[3].numpy().astype(np.float64)]) for h in outs], axis=1),
-                          counts)
+                          counts, engines[r].counter("rccl_ops"))
             be.close_comm()
         except BaseException as ex:  # reported by the main thread
             errors[r] = ex
@@ -177,12 +179,21 @@ def _oracle(pop, streams, sizes, xgb, ifm, world):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world,slot_stream", [(2, -1), (4, -1), (8, -1), (2, 2), (4, 2), (8, 2)])
-def test_native_sharded_step_loopback_matches_oracle(world, slot_stream):
-    """slot_stream 2: the owner pipeline's slot pass on its own stream, as the config-4 card table runs it"""
+@pytest.mark.parametrize("world,slot_stream,count_exchange", [(2, -1, -1), (4, -1, -1), (8, -1, -1), (2, 2, -1),
+                                                              (4, 2, -1), (8, 2, -1), (2, -1, 1), (4, -1, 0),
+                                                              (8, 2, 0)])
+def test_native_sharded_step_loopback_matches_oracle(world, slot_stream, count_exchange):
+    """slot_stream 2: the owner pipeline's slot pass on its own stream, as the config-4 card table runs it;
+    count_exchange 1: each batch's per-peer counts as one all-gather, 0: as 2 x world sends / receives, -1 (default):
+    the all-gather from 4 ranks"""
     from fdengine.engine import shard_of
     assert LOOPBACK.exists(), "tests/native/build/librccl_loopback.so missing (fdengine/build.py build_test_libs)"
-    pop, streams, sizes, xgb, ifm, results, wrong_id = _run_ranks(world, slot_stream)
+    pop, streams, sizes, xgb, ifm, results, wrong_id = _run_ranks(world, slot_stream, count_exchange)
+    # operations issued: every batch's records and results (at most 2 x world each way) plus its counts — one
+    # all-gather, or 2 x world point-to-point operations
+    for r in range(world):
+        gather = count_exchange == 1 or (count_exchange < 0 and world >= 4)
+        assert 0 < results[r][2] <= STEPS * (4 * world + (1 if gather else 2 * world)) + 2 * world, results[r][2]
     for r in range(world):
         assert wrong_id[r] is not None and "not the prefetched batch" in wrong_id[r], wrong_id[r]
     # split sizes: every rank's send counts are its batch's owner histogram; receive = the peers' sends to it
@@ -233,7 +244,7 @@ def test_missing_peer_is_an_error_not_a_hang():
                                               [0, 1], pipelined=True), 0, 2, native=True, comm=(path, ids))
         with pytest.raises(NativeError) as ei:
             sc.step(d, len(d["card_key"]))
-        assert "ncclGroupEnd" in str(ei.value)
+        assert "ncclGroupEnd" in str(ei.value) or "ncclAllGather" in str(ei.value)
     finally:
         if old is None:
             os.environ.pop("LOOPBACK_TIMEOUT_S", None)

@@ -12,6 +12,7 @@ per operation (~2 us, DESIGN §9.3, from the world-1 RCCL self-exchange) is on t
 
 usage: python tools/loopback_host.py [worlds=1,2,4,8] [batch=16384] [steps=40]"""
 import json
+import os
 import sys
 import threading
 import time
@@ -42,6 +43,7 @@ def run(world, B, steps, cards=2_000_000):
     for r in range(world):
         own = owned_mask(U["key"], r, world)
         e = FraudEngine(0)
+        e.set_option("count_exchange", int(os.environ.get("COUNT_EXCHANGE", "1")))
         cap = 1
         while cap < int(own.sum() * 1.6) + 65536:
             cap *= 2

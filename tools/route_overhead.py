@@ -44,6 +44,8 @@ for name in VARIANTS:
     eng.load_merchants(merch["fraud_rate"], merch["risk_multiplier"])
     if os.environ.get("STREAM_PRIORITY"):
         eng.set_option("stream_priority", int(os.environ["STREAM_PRIORITY"]))
+    if os.environ.get("COUNT_EXCHANGE"):  # the native step's count exchange: 1 all-gather, 0 point-to-point
+        eng.set_option("count_exchange", int(os.environ["COUNT_EXCHANGE"]))
     sc = ShardedScorer(EngineShardBackend(eng, params, [0, 1], pipelined=True), 0, 1, force_route=routed,
                        streaming=name != "serial", native=name == "native")
     w = synth_gpu.warm_workload(eng, dev, CARDS, 0, 1, STEPS + 20, B, hours=12.0, keep_batches=0)
