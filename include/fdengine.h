@@ -674,8 +674,8 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      forests after the first on one side stream (0.095), 2 on two side streams (0.095)
      "pipeline_lean": fd_score_batch_pipelined's bucket pass, 1 (default) the lean kernel that fits beside the
      fused ensemble kernel, 0 the full bucket kernel
-     "ensemble_int_lut": the fused kernel's compact rows, 1 (default) the eight small-integer slots binned by one
-     lookup in a per-plan table of the bins of 0..31, 0 searched like the others (outputs identical)
+     (The compact rows' eight small-integer slots are always binned by one lookup in a per-plan table of the bins of
+     0..31; round 5's option to search them instead was removed after its A/B)
      "ensemble_bin_global": the fused kernel's compact rows, 1 every varying slot binned by a search of its merged
      threshold table in global memory (L2-resident; no staging pass, chunk 0's DMA issued at the kernel's start),
      0 (default) the tables staged in LDS first (outputs identical)

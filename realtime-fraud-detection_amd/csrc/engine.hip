@@ -546,10 +546,6 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(value == 0 || (value >= 8 && value <= 512 && (value & (value - 1)) == 0), FD_ERR_INVALID_ARG,
                "bucket_keys must be 0 or a power of two in 8..512");
     e.state.bucket_keys = (int)value;
-  } else if (k == "ensemble_int_lut") {  // the fused kernel's compact rows: 1 (default) the eight small-integer slots
-    // (hour, day of week, weekend, counts, account age, new device) binned by a per-plan table lookup, 0 searched
-    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_int_lut must be 0 or 1");
-    e.ens_int_lut = value != 0;
   } else if (k == "ensemble_bin_global") {  // the fused kernel's compact rows: 1 binned by searches of the merged
     // tables where they lie (L2), chunk 0's DMA issued at once; 0 the tables staged in LDS first
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_bin_global must be 0 or 1");

@@ -743,12 +743,8 @@ const void* pick_ensemble(int D) {
   }
 }
 
-const void* pick_ensemble(int out, bool wide, int D, bool lut) {
-  // engine option ensemble_int_lut 0 (A/B): the pipeline's instantiations without the small-integer table
-  if (!lut && D == 8 && out == 0)
-    return wide ? (const void*)ensemble_kernel<8, 0, true, false> : (const void*)ensemble_kernel<8, 0, false, false>;
-  if (!lut && D == 8 && out == 1)
-    return wide ? (const void*)ensemble_kernel<8, 1, true, false> : (const void*)ensemble_kernel<8, 1, false, false>;
+// (the instantiations without the small-integer table, round 5's A/B, were removed with the option: DESIGN §3)
+const void* pick_ensemble(int out, bool wide, int D) {
   if (wide) return out == 1 ? pick_ensemble<1, true>(D) : out == 2 ? pick_ensemble<2, true>(D) : pick_ensemble<0, true>(D);
   return out == 1 ? pick_ensemble<1, false>(D) : out == 2 ? pick_ensemble<2, false>(D) : pick_ensemble<0, false>(D);
 }
@@ -1021,7 +1017,7 @@ void plan_args(const EnsemblePlan& P, const float* dX, int64_t n, int32_t ld, bo
 
 // out: 0 blended columns, 1 route result records, 2 the single forest's probability column (a.fp)
 bool run_plan(Engine& e, const EnsemblePlan& P, EnsArgs& a, int out, int timing_kind) {
-  const void* fn = pick_ensemble(out, P.wide, P.D, e.ens_int_lut);
+  const void* fn = pick_ensemble(out, P.wide, P.D);
   if (!fn) return false;
   const size_t lds = ens_lds(P.nf, P.wide);
   FD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

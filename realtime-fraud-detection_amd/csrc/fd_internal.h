@@ -545,7 +545,6 @@ struct Engine {
   bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
   bool ens_prio = false;  // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels)
   bool ens_bin_global = false;  // "ensemble_bin_global": compact rows binned by searches in global memory (no staging)
-  bool ens_int_lut = true;  // "ensemble_int_lut": compact rows' small-integer slots binned by table lookup
   bool compact_vectors = true;  // "compact_vectors": the pipelined stream's compact scoring vectors (engine.hip)
   int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)
   // host-API staging

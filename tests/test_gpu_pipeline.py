@@ -120,10 +120,9 @@ def test_pipelined_stream_matches_serial(world, lean, slot_stream):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("opts", [(("ensemble_bin_global", 1),), (("ensemble_int_lut", 0),),
-                                  (("ensemble_int_lut", 0), ("ensemble_bin_global", 1)), (("lean_group", 0),),
-                                  (("lean_group", 1),)], ids=["bin_global", "no_int_lut", "no_lut_bin_global",
-                                                              "lean_group0", "lean_group1"])
+@pytest.mark.parametrize("opts", [(("ensemble_bin_global", 1),), (("lean_group", 0),), (("lean_group", 1),),
+                                  (("ensemble_bin_global", 1), ("ensemble_chunks", 2))],
+                         ids=["bin_global", "lean_group0", "lean_group1", "bin_global_compact_chunks"])
 def test_pipelined_engine_options(world, opts):
     """the compact path's A/B options (binning of the fused kernel's rows, the lean kernel's card grouping): the
     pipelined stream's outputs and end state equal the serial full-vector path's under every one"""

@@ -14,5 +14,5 @@ import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']
 print(sys.argv[1], round(d['value']/1e6,1), d['ms_per_step'], d['host_submit_ms_per_step'], r['kernel_avg_us'], r['frac'], r['alone'], r['attainable']['frac'], d['parity_vs_oracle']['timed_path']['max_abs_prob_diff'], d['p99_batch_latency_ms'])
 for k,v in (d.get('secondary_workloads') or {}).items(): print('  ', k, v.get('value'), v.get('ms_per_step'), v.get('p99_batch_latency_ms'), (v.get('roofline') or {}).get('frac'))
 " gpurun_out/$T.$f.json; done
-FD_BENCH_SECONDARY=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T.prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/$T.prof.log 2>&1 || { tail -20 gpurun_out/$T.prof.log; exit 1; }
-find gpurun_out/$T.prof -name "*kernel_stats.csv" | head -3
+FD_BENCH_SECONDARY=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/$T.prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/$T.prof.log 2>&1 || { tail -20 gpurun_out/$T.prof.log; exit 1; }
+cp "$(find /tmp/$T.prof -name "*kernel_stats.csv" | head -1)" gpurun_out/$T.prof_kernel_stats.csv && echo "kernel stats -> gpurun_out/$T.prof_kernel_stats.csv"
