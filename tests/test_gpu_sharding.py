@@ -155,8 +155,8 @@ def test_emulated_shards_match_unsharded(G):
 def test_streaming_routed_step_single_rank_matches_direct():
     """The sharded step's own GPU work on one GPU (ShardedScorer(force_route=True) over a 1-rank RCCL process group),
     in both streaming forms — native: one fd_sharded_step per batch over the engine's own RCCL communicators
-    (grouped ncclSend/ncclRecv of counts, records and results; the next batch's counts one step ahead, named by id;
-    a prefetch of the wrong batch is dropped);
+    (grouped ncclSend/ncclRecv of counts, records and results, or the counts as one ncclAllGather; the next batch's
+    counts one step ahead, named by id; a prefetch of the wrong batch is dropped);
     python: fd_route_partition_stream + torch.distributed all-to-alls on two groups + fd_score_records_pipelined —
     each step's device outputs dropped at once, bit-identical to the direct pipelined step (fd_score_batch_pipelined)
     on a twin engine."""
@@ -188,10 +188,12 @@ def test_streaming_routed_step_single_rank_matches_direct():
         parts = [{f: t[i * B:(i + 1) * B] for f, t in dev.items()} for i in range(steps)]
         torch.cuda.synchronize()
         res = []
-        for variant in ("direct", "native", "native_hostout", "python"):
+        for variant in ("direct", "native", "native_gather", "native_hostout", "python"):
             routed = variant != "direct"
             e = FraudEngine(0)
             engines.append(e)
+            if variant == "native_gather":  # the counts as one ncclAllGather (the default from 4 ranks) on real RCCL
+                e.set_option("count_exchange", 1)
             e.state_init(1 << 17, 1, 16)
             e.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
             e.load_merchants(M["fraud_rate"], M["risk_multiplier"])
