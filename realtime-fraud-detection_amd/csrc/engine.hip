@@ -565,6 +565,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(!e.pipe_slot_stream || (int)value == e.pipe_slot_mode, FD_ERR_INVALID_ARG,
                "slot_stream: set before the first pipelined call");
     e.pipe_slot_mode = (int)value;
+  } else if (k == "slot_prio") {  // pipelined stream: 1 the slot kernel's waves issue at priority 2, 0 (default) not
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "slot_prio must be 0 or 1");
+    e.state.slot_prio = value != 0;
   } else if (k == "feature_prio") {  // pipelined stream: 1 (default since round 5) the lean bucket kernel's waves issue
     // at priority 2 (0.0857 -> 0.0843 ms per config-4 step at 200 steps), 0 at the default priority
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "feature_prio must be 0 or 1");

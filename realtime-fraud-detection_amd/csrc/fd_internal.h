@@ -361,6 +361,7 @@ struct CardStore {
   // option "lean_group": how the lean bucket kernel groups a bucket's keys by card — 0 rank sort, 1 rank sort split
   // over every thread (rank_sort_split), 2 (default) LDS hash table (no sort)
   int lean_group = 2;
+  bool slot_prio = false;  // option "slot_prio": the pipelined stream's slot kernel issues at priority 2
   bool feat_prio = true;  // option "feature_prio": the pipelined stream's lean bucket kernel issues at priority 2 (default since round 5)
   int64_t n_merchants = 0;
   DeviceBuffer pages, keys, merchants, err, seq;  // pages: CardPages (header + ring per slot); keys: the compact

@@ -256,8 +256,9 @@ __global__ void __launch_bounds__(kST) feat_slot_kernel(CardPages P, unsigned lo
                                                         unsigned long long* __restrict__ pairs,
                                                         unsigned* __restrict__ ovf_cnt,
                                                         unsigned long long* __restrict__ ovf_key,
-                                                        unsigned* __restrict__ ovf_b, unsigned* err) {
+                                                        unsigned* __restrict__ ovf_b, unsigned* err, int prio) {
   extern __shared__ unsigned hist[];  // [nbm + 1] block counts | [nbm + 1] reserved run starts
+  if (prio) __builtin_amdgcn_s_setprio(2);  // engine option slot_prio (pipelined stream)
   unsigned* run = hist + nbm + 1;
   FD_TL(g_tl_feat, 0, 0);
   for (unsigned b = threadIdx.x; b <= nbm; b += kST) hist[b] = 0u;
@@ -1969,7 +1970,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
                      st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, C, g.slot.as<unsigned>(),
                      g.prep.as<Prep>(), g.bucket_fill.as<unsigned>(), g.pairs.as<unsigned long long>(),
                      g.ovf_cnt.as<unsigned>() + par, g.ovf_key.as<unsigned long long>(), g.ovf_b.as<unsigned>(),
-                     st.err.as<unsigned>());
+                     st.err.as<unsigned>(), lean && st.slot_prio ? 1 : 0);
   FD_HIP(hipGetLastError());
   if (ss != s) {
     FD_HIP(hipEventRecord(e.slot_pass_ev, ss));
