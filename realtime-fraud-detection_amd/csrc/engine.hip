@@ -449,8 +449,8 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
   const std::string k(key);
   if (k == "pipelined_batches") {  // fd_score_batch_pipelined / fd_score_records_pipelined batches so far
     *value = (int64_t)e.pipe_iter_total;
-  } else if (k == "pipelined_compact_batches") {  // of those: scored by the fused kernel from the compact 24-float
-    // vectors (no vectors requested), the variant the config-3/4 bench times
+  } else if (k == "pipelined_compact_batches") {  // of those: scored by the fused kernel from the compact 64-B
+    // rows (no vectors requested), the variant the config-3/4 bench times
     *value = (int64_t)e.pipe_compact_total;
   } else if (k == "pipelined_host_ns") {  // host nanoseconds inside fd_score_batch_pipelined (HIP launches, event
     // records and waits of the pipelined step)
@@ -507,7 +507,7 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "ensemble_chunks must be 0, 1 or 2");
     e.ens_chunks = (int)value;
   } else if (k == "compact_vectors") {  // pipelined stream: 1 (default) the fused kernel's batches carry the
-    // compact 24-float vector when nobody asked for the vectors; 0 always the 64-wide one (outputs identical)
+    // compact 64-B row when nobody asked for the vectors; 0 always the 64-wide one (outputs identical)
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "compact_vectors must be 0 or 1");
     e.compact_vectors = value != 0;
   } else if (k == "latency_fused") {  // latency batches: 1 (default) both forests' walks in one launch and their

@@ -90,7 +90,7 @@ struct EnsArgs {
   const float* thr;
   int thr_off[kMaxFeatures + 1];  // per-feature table offsets into thr (kernel arguments: scalar loads)
   int vec4;                       // rows 16-B aligned (ld % 4 == 0, aligned X): float4 row loads
-  int compact;                    // X rows are the compact vector (kCompactWidth floats), binned here
+  int compact;                    // X rows are the compact 64-B rows (fd_internal.h), binned here
   uint16_t cbin[kMaxFeatures];    // compact mode: the bins of the constant slots (0 or 0.5), per plan
   alignas(4) uint16_t lut[8 * 32];  // compact mode: [kIntSlots][kLutN] bins of the small-integer slots' values 0..31
 

@@ -644,7 +644,7 @@ void state_clear(Engine& e);
 int64_t state_count(Engine& e);
 void load_users(Engine& e, const fd_users& u);
 void load_merchants(Engine& e, const fd_merchants& m);
-// compact: d_vec rows are the fused pipeline's compact form (kCompactWidth floats), not the 64-wide vector
+// compact: d_vec rows are the fused pipeline's compact form (64-B rows: kCompactWidth words, fd_internal.h), not the 64-wide vector
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw,
                      float* d_seq = nullptr, double* d_vel5 = nullptr, hipStream_t stream = nullptr,
                      bool lean = false, int set = 0, hipEvent_t before_buckets = nullptr, bool compact = false,
@@ -727,7 +727,7 @@ bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots,
 // one forest's probabilities through the fused kernel (large batches, no raw / leaf outputs); false: not applicable
 bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int32_t ld, double* dprob,
                             hipStream_t stream);
-// compact: dX rows are the compact vector (kCompactWidth floats, ld ignored; the plan's features <= 64)
+// compact: dX rows are the compact vector (64-B rows of kCompactWidth words, ld ignored; the plan's features <= 64)
 bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
                      const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
                      uint8_t* drisk, const RouteRecord* records, ResultRecord* results, bool compact = false);

@@ -438,7 +438,7 @@ struct Outputs {
   // be truncated there: the reference's counters are unbounded, RedisTransactionSink.java:93-105); null otherwise
   unsigned long long* sat;
   int K;
-  bool compact;  // vec rows are the compact form (kCompactWidth floats: the fused pipeline's ensemble reads them)
+  bool compact;  // vec rows are the compact form (64-B rows, fd_internal.h kCompactWidth: the fused pipeline's ensemble reads them)
 };
 
 __device__ __forceinline__ void emit(const Outputs& o, int64_t i, const double* r, long long s5, float o1, float dv0) {
