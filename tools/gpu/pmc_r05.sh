@@ -2,6 +2,7 @@
 # (round 5) PMC of the current hot kernels: config 4 (ensemble, slot, lean bucket) and config 5 (lstm_kernel4, split path);
 # one rocprofv3 --pmc pass per counter group, each with its own hard limit; summaries -> gpurun_out/T.pmc_*.json
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+export FD_BENCH_SECONDARY=0  # no child workloads under the profiler
 T=${1:-pmc}
 P4=(--steps 8 --warmup 2 --no-cpu-baseline --latency-iters 2 --loaded-iters 0 --alone-iters 2 --parity-batches 1 --timing-steps 0)
 P2=(--workload config2 --steps 8 --warmup 2 --no-cpu-baseline --latency-iters 2 --loaded-iters 0 --alone-iters 2 --parity-batches 1 --timing-steps 0)
