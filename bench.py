@@ -168,7 +168,8 @@ LSTM4_SYMBOL = "fd::anon::lstm_kernel4"
 INGEST_SYMBOL = "fd::anon::ingest_json_kernel"
 
 
-def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=None, out=0, wide=True, vec_bytes=256):
+def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=None, out=0, wide=True, vec_bytes=256,
+                    fused_single=False):
     """Roofline of a forest launch against its real bound: LDS issue of the dependent walk. With the fused
     ensemble kernel (FD_TIMING_ENSEMBLE) timed, that launch is the one reported (both forests' node steps)."""
     from fdengine import _native as N
@@ -182,8 +183,11 @@ def forest_roofline(timing, kind, forest, depth, B, workload, label, forests=Non
         # the instantiation that ran: output form (0 columns, 1 route result records) and chunk layout (wide
         # unless the engine has RCCL communicators: engine option ensemble_chunks)
         symbol = ensemble_symbol(out, wide)
-    elif timing.get(N.FD_TIMING_ENSEMBLE, (0.0, 0))[1]:  # one forest through the fused kernel (config 2)
-        ms, launches = timing[N.FD_TIMING_ENSEMBLE]
+    elif fused_single or timing.get(N.FD_TIMING_ENSEMBLE, (0.0, 0))[1]:  # one forest through the fused kernel
+        # (config 2: fd_forest_predict on >= 128 tiles without raw / leaf outputs runs ensemble_kernel<D, 2>, timed
+        # under the forest's own kind)
+        if not fused_single:
+            ms, launches = timing[N.FD_TIMING_ENSEMBLE]
         steps = B * forest.n_trees * depth
         forest_bytes = forest_blob_bytes(forest)
         label = "ensemble_kernel<D=8> over one forest (probabilities only)"
@@ -462,6 +466,7 @@ class Config2:
         import fdengine
         from fdengine import synth
         self.np, self.torch = np, torch
+        self.args = args
         self.B, self.F, self.T, self.D = args.batch, args.features, args.trees, args.depth
         X_ref = synth.feature_matrix(2048, self.F, seed=7)
         doc = synth.xgboost_doc(self.T, self.D, self.F, X_ref, seed=8)
@@ -501,8 +506,13 @@ class Config2:
 
     def roofline(self, timing):
         from fdengine import _native as N
+        # the engine's default for a 64 k batch without raw / leaf outputs: the fused kernel over the one forest
+        # (unless --engine-option ensemble=0 or forest_kernel=N forces a per-model kernel)
+        forced = any(kv.replace(" ", "").startswith(("ensemble=0", "forest_kernel=")) and not
+                     kv.replace(" ", "").endswith("forest_kernel=0") for kv in self.args.engine_option)
+        fused = not forced and (self.B + 255) // 256 >= 128 and self.info["depth"] <= 8
         return forest_roofline(timing, N.FD_TIMING_XGB, self.forest, self.info["depth"], self.B, self.name,
-                               FOREST_KERNEL.format(d=self.info['depth'], t="f32", k="XGB"))
+                               FOREST_KERNEL.format(d=self.info['depth'], t="f32", k="XGB"), fused_single=fused)
 
     def kernels(self, timing):
         from fdengine import _native as N
