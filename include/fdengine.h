@@ -674,6 +674,9 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      forests after the first on one side stream (0.095), 2 on two side streams (0.095)
      "pipeline_lean": fd_score_batch_pipelined's bucket pass, 1 (default) the lean kernel that fits beside the
      fused ensemble kernel, 0 the full bucket kernel
+     "pipeline_gather": fd_score_batch_pipelined's batches of <= 4096 transactions (option slot_gather on, no slot
+     stream), 1 (default) the gather bucket kernel (card slots found inside it: one feature launch), 0 the slot +
+     lean bucket pair of the large batches
      (The compact rows' eight small-integer slots are always binned by one lookup in a per-plan table of the bins of
      0..31; round 5's option to search them instead was removed after its A/B)
      "ensemble_bin_global": the fused kernel's compact rows, 1 every varying slot binned by a search of its merged

@@ -517,6 +517,11 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "pipeline_lean") {  // fd_score_batch_pipelined's bucket pass: 1 (default) lean + deferred
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "pipeline_lean must be 0 or 1");
     e.pipe_lean = value != 0;
+  } else if (k == "pipeline_gather") {  // fd_score_batch_pipelined, batches of <= 4096 transactions (slot_gather on,
+    // no slot stream): 1 (default) the gather bucket kernel (card slots found inside it, one feature launch), 0 the
+    // slot + lean bucket pair of the large batches
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "pipeline_gather must be 0 or 1");
+    e.pipe_gather = value != 0;
   } else if (k == "small_streams") {  // latency batches: 2 LSTM | other forests on two side streams, 1 one, 0 none
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "small_streams must be 0, 1 or 2");
     e.small_streams = (int)value;
@@ -1113,6 +1118,10 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
     e.pipe_seq[s].ensure((size_t)n * e.state.S * fd::kSeqInput * sizeof(float));
     seq = e.pipe_seq[s].as<float>();
   }
+  // latency-sized batches: the gather kernel (slot pass inside the bucket launch) instead of the slot + lean pair,
+  // whose two launches cost 39 us per 1 k batch against its 18; it waits for batch i-1's card updates
+  // (before_buckets) like the lean pass
+  const bool lean = e.pipe_lean && !(e.pipe_gather && e.state.slot_gather && n <= fd::kGatherBatchMax && !Ss);
   {
     struct SlotPass {  // launch_grouped reads these for this call only
       Engine& e;
@@ -1121,9 +1130,9 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
     e.slot_pass_stream = Ss;
     e.slot_pass_ev = Ss ? e.pipe_slot_ev[s] : nullptr;
     if (records)
-      fd::launch_features_records(e, records, n, vec, seq, Sf, e.pipe_lean, s, before_buckets, compact);
+      fd::launch_features_records(e, records, n, vec, seq, Sf, lean, s, before_buckets, compact);
     else
-      fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, e.pipe_lean, s, before_buckets, compact);
+      fd::launch_features(e, *txns, n, vec, nullptr, seq, nullptr, Sf, lean, s, before_buckets, compact);
   }
   FD_HIP(hipEventRecord(e.pipe_feat_ev[s], Sf));
   e.pipe_feat_live[s] = true;

@@ -21,6 +21,7 @@ namespace fd {
 
 constexpr int kMaxSlots = 8;      // forest slots per engine
 constexpr int kTile = 256;        // transactions per workgroup in the forest kernel (one per thread)
+constexpr int kGatherBatchMax = 4096;  // largest batch the gather bucket kernel takes (features.hip kChunkCap)
 constexpr int kMaxFeatures = 64;  // model columns held in LDS ([feature][kTile] f32 = 64 KiB max)
 // The compact scoring vector of the fused pipeline (features.hip write_vector -> ensemble.hip prologue): of the 64
 // slots of the engine's vector (FeatureProcessor's 41 definitions + derived features + pad, _prepare_features) only
@@ -228,6 +229,7 @@ struct LstmModel {
   bool loaded = false;
   int input_size = 0, n_out = 0;
   DeviceBuffer wpk, wpk4, bias, wout, bout;  // wpk: 16-row kernel's B operands; wpk4: the 4-row kernel's
+  bool hh_finite = false;  // every W_hh weight finite: W_hh h_{-1} = W_hh 0 adds only zeros (lstm_kernel4 skips it)
 };
 
 // One card's keyed state header (features.hip): 128 B = one L2 line, so a transaction's state read touches one
@@ -533,6 +535,7 @@ struct Engine {
   unsigned long long pipe_host_ns = 0;  // counter "pipelined_host_ns": host time inside fd_score_batch_pipelined
   unsigned long long pipe_slot_stream_total = 0;  // counter "pipelined_slot_stream_batches": slot pass on its own stream
   bool pipe_lean = true;   // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
+  bool pipe_gather = true;  // "pipeline_gather" option: batches of <= kGatherBatchMax take the gather bucket kernel
   DeviceBuffer pipe_vec[kPipeSlots], pipe_seq[kPipeSlots];
   // the scoring streams write a batch's outputs into pipe_out[slot]; one copy kernel on `stream` moves them to the
   // caller's buffers, so the caller's memory is written only in the engine stream's order (torch's caching

@@ -43,6 +43,7 @@ constexpr int kBT = 256;          // threads of the bucket kernel (and its scans
 constexpr int kST = 256;          // threads of the slot kernel (latency-bound probes: spread over every CU)
 constexpr int kSegLong = 16;      // segments longer than this take the cooperative path
 constexpr int kChunkCap = 4096;   // (slot, txn) keys sorted per pass in LDS
+static_assert(kChunkCap == kGatherBatchMax, "the pipelined step picks the gather kernel by kGatherBatchMax");
 constexpr int kMaxBuckets = 4096;
 constexpr int kMaxBins = 4096;    // arrival-range bins of an oversized bucket
 constexpr int kMaxK = 64;

@@ -30,6 +30,12 @@
 // rows (two v_permlane32_swap + two v_permlane16_swap) then gives lane (q, unit) the i, f, g, o gates
 // of transaction q, so each lane updates ONE cell (5 transcendentals instead of 20). The workgroup
 // loops over tiles (persistent grid) with the weights resident in VGPRs.
+// Software-pipelined steps (round 5): of step t+1's 144 k-steps, the 16 of x_{t+1} and the 16 of the wave's OWN
+// hidden units (h_t of its lanes, moved into the A-operand order by one ds_bpermute, no LDS round trip) need nothing
+// from the other waves, so they are issued before step t's barrier, while the matrix pipe would otherwise idle
+// through the cell update, the h_t stores and the barrier; after the barrier only the other 7 units' blocks remain.
+// Wave w's W_hh blocks are packed in the order w, w+1, ..., w+7 (mod 8) for this. Step 0's W_hh h_{-1} (h = 0) is
+// skipped when every W_hh weight is finite (0 * w = 0 adds nothing; a non-finite weight keeps the products).
 #include <algorithm>
 #include <cmath>
 #include <utility>
@@ -170,7 +176,7 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
                                                     const float* __restrict__ wout, const float* __restrict__ bout,
                                                     int n_out, double* __restrict__ prob,
                                                     const unsigned long long* __restrict__ desc,
-                                                    const float* __restrict__ ring) {
+                                                    const float* __restrict__ ring, int h0_skip) {
 #pragma clang fp contract(off)
   // h_t and x_t in the A-operand order: (txn i, k) at lane i + 4 (k & 15), register k >> 4. h_t is stored
   // register-major, [register][lane]: a lane's reads (one word per register) and the cell writes (a wave's 64
@@ -195,11 +201,15 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
       if (idx < 4 * per && (int64_t)blockIdx.x * 4 + r < n) dsc[j] = desc[(int64_t)blockIdx.x * 4 + r];
     }
   }
-  // B operands: lane l holds W[(l >> 4) * 128 + 16 w + (l & 15)][k] for k = 0..143 (W_ih, then W_hh)
+  // B operands: lane l holds W[(l >> 4) * 128 + 16 w + (l & 15)][k] for k = 0..143 (W_ih, then W_hh's unit blocks
+  // in the order w, w+1, ..., w+7 mod 8: load_lstm)
   float bw[kKT];
 #pragma unroll
   for (int k = 0; k < kKT; ++k) bw[k] = wpk4[((size_t)w * kKT + k) * 64 + l];
   const int q = l >> 4, unit = 16 * w + (l & 15);
+  const int wq = __builtin_amdgcn_readfirstlane(w);
+  // own units into the A-operand order: lane j takes h of transaction j & 3, unit 16 w + (j >> 2)
+  const int own_src = (16 * (l & 3) + (l >> 2)) * 4;
   const float bcol = bias[q * kH + unit];
   // dense head: wave w computes output ho of transaction hr, lane l the products of units l and l + 64
   const int hr = w & 3, ho = w >> 2;
@@ -232,21 +242,26 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
     float c = 0.f, h = 0.f;
     __syncthreads();
     if (tile == blockIdx.x) FD_TL(g_tl_lstm, 2, 1);
+    f32x4 acc[4] = {f32x4{bcol, bcol, bcol, bcol}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                    f32x4{0.f, 0.f, 0.f, 0.f}};
+    mfma_abid16(xs[0][l], &bw[0], acc, std::make_integer_sequence<int, 16>{});
     for (int t = 0; t < T; ++t) {
-      f32x4 acc[4] = {f32x4{bcol, bcol, bcol, bcol}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
-                      f32x4{0.f, 0.f, 0.f, 0.f}};
-      float hv[kH / 16];
+      const float xn = xs[t + 1 < T ? t + 1 : t][l];  // x_{t+1}, read early (its LDS latency off the barrier window)
+      if (t > 0) {  // h_{t-1} of the other seven waves' units (blocks w+1 .. w+7), published by the last barrier
+        float hv[kH / 16 - 1];
 #pragma unroll
-      for (int kk = 0; kk < kH / 16; ++kk) hv[kk] = hbuf[t & 1][kk][l];
-      mfma_abid16(xs[t][l], &bw[0], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(hv[0], &bw[kI + 0], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(hv[1], &bw[kI + 16], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(hv[2], &bw[kI + 32], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(hv[3], &bw[kI + 48], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(hv[4], &bw[kI + 64], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(hv[5], &bw[kI + 80], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(hv[6], &bw[kI + 96], acc, std::make_integer_sequence<int, 16>{});
-      mfma_abid16(hv[7], &bw[kI + 112], acc, std::make_integer_sequence<int, 16>{});
+        for (int j = 1; j < kH / 16; ++j) hv[j - 1] = hbuf[t & 1][(wq + j) & (kH / 16 - 1)][l];
+        mfma_abid16(hv[0], &bw[kI + 16], acc, std::make_integer_sequence<int, 16>{});
+        mfma_abid16(hv[1], &bw[kI + 32], acc, std::make_integer_sequence<int, 16>{});
+        mfma_abid16(hv[2], &bw[kI + 48], acc, std::make_integer_sequence<int, 16>{});
+        mfma_abid16(hv[3], &bw[kI + 64], acc, std::make_integer_sequence<int, 16>{});
+        mfma_abid16(hv[4], &bw[kI + 80], acc, std::make_integer_sequence<int, 16>{});
+        mfma_abid16(hv[5], &bw[kI + 96], acc, std::make_integer_sequence<int, 16>{});
+        mfma_abid16(hv[6], &bw[kI + 112], acc, std::make_integer_sequence<int, 16>{});
+      } else if (!h0_skip) {  // W_hh h_{-1} with h_{-1} = 0, products kept (a non-finite weight makes them NaN)
+#pragma unroll
+        for (int j = 0; j < kH / 16; ++j) mfma_abid16(0.f, &bw[kI + 16 * j], acc, std::make_integer_sequence<int, 16>{});
+      }
       // register r = transaction r of this lane's gate column; after the transpose register j = gate j of
       // transaction q
       float g0 = (acc[0][0] + acc[1][0]) + (acc[2][0] + acc[3][0]);
@@ -258,6 +273,13 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
       c = fg * c + ig * gg;
       h = og * tanh_g(c);
       hbuf[(t + 1) & 1][unit >> 4][q + 4 * (unit & 15)] = h;
+      if (t + 1 < T) {  // step t+1's own k-steps before the barrier: x_{t+1}, then this wave's own units of h_t
+        acc[0] = f32x4{bcol, bcol, bcol, bcol};
+        acc[1] = acc[2] = acc[3] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mfma_abid16(xn, &bw[0], acc, std::make_integer_sequence<int, 16>{});
+        const float ho = __int_as_float(__builtin_amdgcn_ds_bpermute(own_src, __float_as_int(h)));
+        mfma_abid16(ho, &bw[kI], acc, std::make_integer_sequence<int, 16>{});
+      }
       __syncthreads();
     }
     if (tile == blockIdx.x) FD_TL(g_tl_lstm, 2, 2);
@@ -312,15 +334,25 @@ void load_lstm(Engine& e, const fd_lstm_params& p) {
           }
           pk[(((size_t)w * 4 + g) * kKS + s) * 64 + l] = v;
         }
-  // 4-row kernel: [wave][k][lane] = W[(lane >> 4) * 128 + 16 wave + (lane & 15)][k], k < 16 from W_ih
+  // 4-row kernel: [wave][k][lane] = W[(lane >> 4) * 128 + 16 wave + (lane & 15)][k'], k < 16 from W_ih (k' = k),
+  // then W_hh's 16-unit blocks rotated so that the wave's own block comes first: k = 16 + 16 j + r holds
+  // k' = 16 ((wave + j) mod 8) + r (lstm_kernel4's pipelined steps)
   std::vector<float> pk4((size_t)8 * kKT * 64);
   for (int w = 0; w < 8; ++w)
     for (int k = 0; k < kKT; ++k)
       for (int l = 0; l < 64; ++l) {
         const int row = (l >> 4) * kH + 16 * w + (l & 15);
-        const float v = k < kI ? (k < I ? p.w_ih[(size_t)row * I + k] : 0.f) : p.w_hh[(size_t)row * kH + (k - kI)];
+        float v;
+        if (k < kI) {
+          v = k < I ? p.w_ih[(size_t)row * I + k] : 0.f;
+        } else {
+          const int j = (k - kI) >> 4, r = (k - kI) & 15;
+          v = p.w_hh[(size_t)row * kH + 16 * ((w + j) & 7) + r];
+        }
         pk4[((size_t)w * kKT + k) * 64 + l] = v;
       }
+  bool hh_finite = true;
+  for (size_t i = 0; i < (size_t)4 * kH * kH; ++i) hh_finite = hh_finite && std::isfinite(p.w_hh[i]);
   std::vector<float> b(4 * kH);
   for (int i = 0; i < 4 * kH; ++i) b[i] = (p.b_ih ? p.b_ih[i] : 0.f) + (p.b_hh ? p.b_hh[i] : 0.f);
   std::vector<float> wo((size_t)p.n_out * kH), bo(p.n_out);
@@ -339,6 +371,7 @@ void load_lstm(Engine& e, const fd_lstm_params& p) {
   FD_HIP(hipMemcpy(m.bout.ptr, bo.data(), bo.size() * 4, hipMemcpyHostToDevice));
   m.input_size = I;
   m.n_out = p.n_out;
+  m.hh_finite = hh_finite;
   m.loaded = true;
 }
 
@@ -360,7 +393,7 @@ void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, i
     hipLaunchKernelGGL(lstm_kernel4, dim3((unsigned)std::min<int64_t>(tiles, 256)), dim3(512), 0, stream, d_seq, n,
                        T, m.wpk4.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),
                        m.bout.as<const float>(), m.n_out, d_prob, d_desc,
-                       d_desc ? e.state.seq.as<const float>() : nullptr);
+                       d_desc ? e.state.seq.as<const float>() : nullptr, m.hh_finite ? 1 : 0);
   } else {
     hipLaunchKernelGGL(lstm_kernel, dim3((unsigned)((n + kRows - 1) / kRows)), dim3(512), 0, stream, d_seq, n, T,
                        m.wpk.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),

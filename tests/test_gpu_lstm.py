@@ -53,6 +53,24 @@ def test_lstm_narrow_input_and_saturation(engine):
     assert np.abs(p - R.lstm_forward(w, seq)).max() <= TOL
 
 
+@pytest.mark.parametrize("rows", [4, 16])
+def test_lstm_non_finite_recurrent_weight(engine, rows):
+    """one W_hh weight +inf: PyTorch's step 0 multiplies it by h_{-1} = 0 (NaN), so every probability is NaN; the
+    4-row kernel skips step 0's W_hh h_{-1} only when every W_hh weight is finite, so it keeps that NaN too"""
+    w = L.random_weights(16, 128, 1, seed=21)
+    w.w_hh[5, 3] = np.inf
+    engine.load_lstm(w)
+    seq = np.random.default_rng(4).normal(0, 1.5, (37, 10, 16)).astype(np.float32)
+    engine.set_option("lstm_rows", rows)
+    try:
+        p = engine.lstm_predict(seq)
+    finally:
+        engine.set_option("lstm_rows", 0)
+    ref = R.lstm_forward(w, seq)
+    assert np.isnan(ref).all()
+    np.testing.assert_array_equal(np.isnan(p), np.isnan(ref))
+
+
 def test_lstm_not_loaded_raises(engine):
     engine.unload_lstm()
     with pytest.raises(ValueError):

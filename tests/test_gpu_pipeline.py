@@ -154,10 +154,12 @@ def test_pipelined_input_ready_event(world):
 
 
 @pytest.mark.timeout(300)
-def test_pipelined_lstm_and_latency_batches(world):
+@pytest.mark.parametrize("gather", [1, 0])
+def test_pipelined_lstm_and_latency_batches(world, gather):
     """models [XGBoost, IsolationForest, LSTM] (the per-model scoring path with the LSTM on its second stream and
     the card histories double-buffered) and latency-size batches (tree-split path): pipelined == serial, model
-    columns included"""
+    columns included. gather 1 (default): batches of <= 4096 transactions take the gather bucket kernel in the
+    pipelined step (option pipeline_gather) — a run of them back to back, 4096 and 4097 at the edge"""
     import torch
 
     from fdengine import lstm as L
@@ -181,7 +183,8 @@ def test_pipelined_lstm_and_latency_batches(world):
         e.set_stream(torch.cuda.current_stream().cuda_stream)
         engines.append(e)
     ref, pip = engines
-    cuts = [0, 1000, 1700, 9000, 9100, 15000]
+    pip.set_option("pipeline_gather", gather)
+    cuts = [0, 1000, 1700, 2724, 3748, 7844, 11941, 12041, 15000]
     dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f][:cuts[-1]])).cuda() for f in TXN_FIELDS}
     torch.cuda.synchronize()
     try:
