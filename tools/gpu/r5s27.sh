@@ -1,5 +1,5 @@
 #!/bin/bash
-# lstm_kernel4 with software-pipelined steps (x_{t+1} and the wave's own units of h_t before the barrier, step 0's
+# lstm_kernel4 A/B (previous library in ab_prev against the new): LSTM / latency / pipeline tests on the new one,
 # W_hh 0 skipped): LSTM / latency / pipeline tests, then config 5 alternating the previous library (ab_prev) and the new
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${1:-s27}
