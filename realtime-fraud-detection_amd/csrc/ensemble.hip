@@ -118,6 +118,7 @@ struct EnsArgs {
   ResultRecord* res;
 #ifdef FD_FOREST_PROFILE
   int prof_slot;  // which of the kEprofSlots profile buffers this launch writes (launch count mod kEprofSlots)
+  int clk_slot;   // this launch's record in g_eclk (launch count mod kEclkSlots)
 #endif
 };
 
@@ -244,6 +245,11 @@ __host__ __device__ __forceinline__ int thr_pad(int g) { return g + (g >> 5); }
 constexpr int kEprofSlots = 4;  // the last 4 launches (the pipelined stream: launches beside the next features)
 __device__ unsigned long long g_eprof[kEprofSlots * 256 * 16 * 16];
 static int g_eprof_next = 0;
+// per launch, the clocks of wave 0 of workgroups 0, 64, 128, 192: {s_memtime start, end, s_memrealtime start, end}
+// (shader clock = memtime cycles / realtime ticks x 100 MHz; tools/clock_ramp.py)
+constexpr int kEclkSlots = 1024;
+__device__ unsigned long long g_eclk[kEclkSlots * 4 * 4];
+static int g_eclk_next = 0;
 #define FD_ESTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #else
 #define FD_ESTAMP(var)
@@ -678,6 +684,13 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     o[5] = __builtin_amdgcn_s_memtime();
     o[14] = pr_rt0;
     o[15] = __builtin_amdgcn_s_memrealtime();
+    if (wave == 0 && (blockIdx.x & 63) == 0) {
+      unsigned long long* c = g_eclk + ((size_t)a.clk_slot * 4 + (blockIdx.x >> 6)) * 4;
+      c[0] = pr_t0;
+      c[1] = o[5];
+      c[2] = pr_rt0;
+      c[3] = o[15];
+    }
   }
 #endif
   if (gg != 0 || !valid) return;
@@ -945,6 +958,10 @@ extern "C" __attribute__((visibility("default"))) int fd_debug_ens_profile(unsig
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eprof), sizeof(unsigned long long) * (size_t)n);
 }
 extern "C" __attribute__((visibility("default"))) int fd_debug_ens_profile_next(void) { return g_eprof_next; }
+extern "C" __attribute__((visibility("default"))) int fd_debug_ens_clock(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eclk), sizeof(unsigned long long) * (size_t)n);
+}
+extern "C" __attribute__((visibility("default"))) int fd_debug_ens_clock_next(void) { return g_eclk_next; }
 #endif
 
 namespace {
@@ -1027,6 +1044,8 @@ bool run_plan(Engine& e, const EnsemblePlan& P, EnsArgs& a, int out, int timing_
 #ifdef FD_FOREST_PROFILE
   a.prof_slot = g_eprof_next;
   g_eprof_next = (g_eprof_next + 1) % kEprofSlots;
+  a.clk_slot = g_eclk_next;
+  g_eclk_next = (g_eclk_next + 1) % kEclkSlots;
 #endif
   void* args[] = {&a};
   FD_HIP(hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(kEnsWG), args, lds, e.stream));
