@@ -1265,7 +1265,7 @@ class Config3J(Config3):
         # pipelined (default): the codec runs on an engine of its own with its own stream, so batch i+1's parse
         # overlaps batch i's scoring on the pipelined stream; two column sets, handed over by events (the scoring
         # waits for its parse; a set's next parse waits for the scoring that read it)
-        self.pipe, self.parity_done, self.cur = not args.no_pipeline, True, 0
+        self.pipe, self.cur = not args.no_pipeline, 0
         self.extra_engines = []
         codec_eng = eng
         if self.pipe:
@@ -1319,12 +1319,8 @@ class Config3J(Config3):
 
     def step(self, i):
         s = i % self.pool
-        if not self.pipe:  # one stream, vectors kept
-            if self.pipe:
-                self.cstream.wait_stream(self.dev_stream)
+        if not self.pipe:  # one stream (the codec on the engine's), vectors kept
             self.codec.parse_device(self.bufs[s].data_ptr(), self.offs[s].data_ptr(), self.B, self.cptrs)
-            if self.pipe:
-                self.dev_stream.wait_stream(self.cstream)
             txn = {f: self.cptrs[f] for f in self.N.TXN_FIELDS}
             self.cur = 0
             self.eng.score_batch_device(self.params, self.slots, txn, self.B, self.fp.data_ptr(),
@@ -1357,7 +1353,6 @@ class Config3J(Config3):
         o = OracleFeatureState(self.cap, self.mode, self.K)
         o.load_users(self.ukeys, self.uavg, self.uage, self.ufp)
         o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
-        self.parity_done = True  # the pipelined stream from the first batch on (the timed path)
         c0 = self.eng.counter("pipelined_compact_batches")
         self.step(0)
         self.torch.cuda.synchronize()
@@ -1518,7 +1513,7 @@ def make_parser():
     ap.add_argument("--secondary", default=None,
                     help="config 4 at N = 1: other BASELINE configurations run after the line's own measurements, each "
                          "as a child process (its own engine, 200 steps), their results embedded as "
-                         "secondary_workloads (comma list; default config5,config2,config3; 'none' or "
+                         "secondary_workloads (comma list; default config5,config2,config3,config3j; 'none' or "
                          "FD_BENCH_SECONDARY=0 to skip)")
     ap.add_argument("--pipeline", action="store_true",
                     help="config5: the pipelined stream (batch i+1's features beside batch i's scoring) instead of "
@@ -1870,7 +1865,8 @@ def main():
         dist.destroy_process_group()
 
 
-SECONDARY_DEFAULT = ("config5", "config2", "config3")  # BASELINE configs[4], [1], [2]
+# BASELINE configs[4], [1], [2], and config 2's raw-JSON form (the Kafka codec ahead of the pipeline)
+SECONDARY_DEFAULT = ("config5", "config2", "config3", "config3j")
 
 
 def _secondary_list(args, world, name):

@@ -166,10 +166,12 @@ bool comm_sync_stream(Engine& e, hipStream_t st) {
 
 void comm_destroy(Engine& e) {
   ShardComm& c = e.comm;
-  // after an abort the forward stream is waited for at most comm_timeout_ms; one that never drains is leaked
-  // (its buffers too) rather than destroyed under a live operation
-  const bool drained = comm_sync_stream(e, c.x_fwd);
-  (void)comm_sync_stream(e, e.stream);
+  // after an abort the forward and engine streams are waited for at most comm_timeout_ms each; when either never
+  // drains, every buffer an operation on them may still touch is leaked (route blocks of the count / place kernels
+  // on x_fwd, the back exchange's results on the engine stream) rather than freed under a live operation
+  const bool fwd_drained = comm_sync_stream(e, c.x_fwd);
+  const bool eng_drained = comm_sync_stream(e, e.stream);
+  const bool drained = fwd_drained && eng_drained;
   if (c.ready && !c.aborted) {
     const RcclApi& R = api(c);
     if (c.fwd) (void)R.comm_destroy(static_cast<ncclComm_t>(c.fwd));
@@ -177,9 +179,11 @@ void comm_destroy(Engine& e) {
   }
   c.fwd = c.back = nullptr;
   if (!drained) {
-    c.x_fwd = nullptr;
+    if (!fwd_drained) c.x_fwd = nullptr;  // a stream still running work is not destroyed either
     for (int s = 0; s < 2; ++s) c.rec[s].ptr = c.cnt[s].ptr = c.res[s].ptr = nullptr, c.h_cnt[s] = nullptr;
     for (int q = 0; q < ShardComm::kInbox; ++q) c.inbox[q].ptr = nullptr;
+    c.back_buf.ptr = nullptr;
+    c.route_blk.ptr = nullptr;
   }
   for (int s = 0; s < 2; ++s) {
     for (auto* b : {&c.rec[s], &c.cnt[s], &c.res[s]}) b->release();

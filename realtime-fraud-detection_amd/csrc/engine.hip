@@ -419,6 +419,8 @@ int fd_engine_sync(fd_engine* eng) {
     bool ok = fd::comm_sync_stream(e, e.comm.x_fwd);
     ok = fd::comm_sync_stream(e, e.stream) && ok;
     for (hipStream_t st : e.pipe_stream) ok = fd::comm_sync_stream(e, st) && ok;
+    // the slot pass and the aux streams can be queued behind an aborted inbox event too (as fd_engine_destroy)
+    for (hipStream_t st : {e.pipe_slot_stream, e.aux_stream, e.aux2_stream}) ok = fd::comm_sync_stream(e, st) && ok;
     FD_REQUIRE(ok, FD_ERR_HIP, "streams still busy " + std::to_string(e.comm.timeout_ms) +
                                    " ms after the communicators were aborted (" + e.comm.abort_reason + ")");
   }
@@ -449,6 +451,9 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
   const std::string k(key);
   if (k == "pipelined_batches") {  // fd_score_batch_pipelined / fd_score_records_pipelined batches so far
     *value = (int64_t)e.pipe_iter_total;
+  } else if (k == "ensemble_single_launches") {  // fd_forest_predict batches scored by the fused kernel over one
+    // forest (probabilities, optionally raw scores; no leaf ids): config 2's timed kernel, ensemble_kernel<8,2>
+    *value = (int64_t)e.ens_single_total;
   } else if (k == "pipelined_compact_batches") {  // of those: scored by the fused kernel from the compact 64-B
     // rows (no vectors requested), the variant the config-3/4 bench times
     *value = (int64_t)e.pipe_compact_total;

@@ -710,8 +710,9 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     const double decision = -score - a.if_offset;
     pb = 1.0 / (1.0 + exp(decision));
   }
-  if (OUT == 2) {  // one forest: its probability (forest_predict semantics)
+  if (OUT == 2) {  // one forest: its probability (forest_predict semantics) and, when asked, its raw score
     a.fp[row] = nA > 0 ? pa : pb;
+    if (a.mp) a.mp[row] = nA > 0 ? (double)lds_load<float>(accA + txn * 4) : lds_load<double>(accB + txn * 8);
     return;
   }
   double raw[FD_MAX_MODELS];  // the two present models at their blend positions (selects: no scratch)
@@ -1093,7 +1094,7 @@ bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, 
 }
 
 bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int32_t ld, double* dprob,
-                            hipStream_t stream) {
+                            double* draw, hipStream_t stream) {
   if (!e.ensemble_on || e.forest_variant != 0 || n <= 0) return false;
   if ((n + kTile - 1) / kTile < kSplitTiles) return false;
   if (slot < 0 || slot >= kMaxSlots || !e.forests[slot].loaded) return false;
@@ -1106,6 +1107,7 @@ bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int
   plan_args(P, dX, n, ld, e.ens_owner_fixed, a);
   a.prio = e.ens_prio ? 1 : 0;
   a.fp = dprob;
+  a.mp = draw;  // one forest: its raw score (XGBoost f32 margin, IsolationForest f64 path-length sum) or null
   const hipStream_t saved = e.stream;
   if (stream) e.stream = stream;
   bool ok = false;
@@ -1116,6 +1118,7 @@ bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int
     throw;
   }
   e.stream = saved;
+  if (ok) ++e.ens_single_total;
   return ok;
 }
 

@@ -531,6 +531,8 @@ struct Engine {
   hipEvent_t slot_pass_ev = nullptr;
   unsigned long long pipe_iter = 0;
   unsigned long long pipe_iter_total = 0;  // counter "pipelined_batches"
+  unsigned long long ens_single_total = 0;    // counter "ensemble_single_launches": fd_forest_predict batches run by
+                                              // the fused kernel over one forest (config 2's timed kernel)
   unsigned long long pipe_compact_total = 0;  // counter "pipelined_compact_batches": batches scored from compact vectors
   unsigned long long pipe_host_ns = 0;  // counter "pipelined_host_ns": host time inside fd_score_batch_pipelined
   unsigned long long pipe_slot_stream_total = 0;  // counter "pipelined_slot_stream_batches": slot pass on its own stream
@@ -729,7 +731,7 @@ void read_xgboost_json(const char* path, XgbModel& out);
 bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present, int64_t n);
 // one forest's probabilities through the fused kernel (large batches, no raw / leaf outputs); false: not applicable
 bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int32_t ld, double* dprob,
-                            hipStream_t stream);
+                            double* draw, hipStream_t stream);
 // compact: dX rows are the compact vector (64-B rows of kCompactWidth words, ld ignored; the plan's features <= 64)
 bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
                      const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,

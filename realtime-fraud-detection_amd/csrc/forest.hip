@@ -1650,11 +1650,11 @@ void launch_forest(Engine& e, const PackedForest& pf, const float* d_X, int64_t 
     return;
   }
 
-  // large batches, probabilities only: the fused ensemble kernel over this one forest (its u16 merged-bin tile,
+  // large batches without leaf ids: the fused ensemble kernel over this one forest (its u16 merged-bin tile,
   // link-encoded nodes and LDS-staged leaves; the same f32 margin / f64 path-length sums in tree order)
-  if (v == 0 && !d_raw && !d_leaf) {
+  if (v == 0 && !d_leaf) {
     const int slot = (int)(&pf - e.forests);
-    if (slot >= 0 && slot < kMaxSlots && launch_ensemble_single(e, slot, d_X, n, ld, d_prob, stream)) return;
+    if (slot >= 0 && slot < kMaxSlots && launch_ensemble_single(e, slot, d_X, n, ld, d_prob, d_raw, stream)) return;
   }
 
   // + 64 B: kernel 6's two item counters after the tile_any flags

@@ -228,6 +228,46 @@ void read_all(FILE* f, void* p, size_t bytes, Fnv* h) {
 
 // Checksum pass over the whole image before anything is restored: a truncated or corrupt file (a partial copy
 // during a re-shard) fails here with the engine's state untouched. Leaves the file at the first section.
+// A v2 image's 128-B card header (before the round-5 relayout) rewritten in place as the v3 CardHeader. v2 byte
+// offsets: key 0, last_ts 8, avg 16, age 24, flags 28, ring_n / ring_head / unsorted 32-34, wc[3] 36-38, fp[3] 40,
+// ws[3] 64, wo[3] 88 (absolute oldest in-window times), rc_sum 112, rc_cnt 120. v3 keeps the oldest times as offsets
+// below last_ts and the redis_compat session amount in ws[0].
+void header_v2_to_v3(unsigned char* rec, int mode) {
+  struct V2 {
+    unsigned long long key;
+    long long last_ts;
+    double avg;
+    int age;
+    unsigned flags;
+    unsigned char ring_n, ring_head, unsorted, pad0, wc[3], pad1;
+    unsigned long long fp[3];
+    long long ws[3], wo[3], rc_sum;
+    int rc_cnt, pad2;
+  };
+  static_assert(sizeof(V2) == 128 && offsetof(V2, ws) == 64 && offsetof(V2, rc_cnt) == 120, "v2 card header");
+  V2 o;
+  std::memcpy(&o, rec, sizeof o);
+  CardHeader h;
+  std::memset(&h, 0, sizeof h);
+  h.last_ts = o.last_ts;
+  h.ring_n = o.ring_n;
+  h.ring_head = o.ring_head;
+  h.unsorted = o.unsorted;
+  for (int k = 0; k < 3; ++k) {
+    h.wc[k] = o.wc[k];
+    h.ws[k] = o.ws[k];
+    h.wod[k] = o.wc[k] > 0 ? (unsigned)(o.last_ts - o.wo[k]) : 0u;  // an in-window event is < 2^32 ms old
+    h.fp[k] = o.fp[k];
+  }
+  if (mode == FD_WINDOW_REDIS_COMPAT) h.ws[0] = o.rc_sum;
+  h.flags = o.flags;
+  h.rc_cnt = o.rc_cnt;
+  h.key = o.key;
+  h.avg = o.avg;
+  h.age = o.age;
+  std::memcpy(rec, &h, sizeof h);
+}
+
 void verify_image(FILE* f, const SnapHeader& hd, size_t rec_bytes) {
   const long start = std::ftell(f);
   std::vector<char> buf(1 << 20);
@@ -427,8 +467,8 @@ void state_restore(Engine& e, const char* path, int shard, int n_shards, int fla
   SnapHeader hd{};
   read_all(in.f, &hd, sizeof hd, nullptr);
   FD_REQUIRE(std::memcmp(hd.magic, kMagic, 8) == 0, FD_ERR_IO, "restore: not an fdengine state snapshot");
-  FD_REQUIRE(hd.version == kVersion && hd.header_bytes == sizeof(SnapHeader), FD_ERR_UNSUPPORTED,
-             "restore: unsupported snapshot version");
+  FD_REQUIRE((hd.version == kVersion || hd.version == 2) && hd.header_bytes == sizeof(SnapHeader),
+             FD_ERR_UNSUPPORTED, "restore: unsupported snapshot version (this build reads v2 and v3 images)");
   FD_REQUIRE(hd.window_mode == st.mode && hd.ring_k == st.K && hd.seq_len == st.S, FD_ERR_INVALID_ARG,
              "restore: snapshot window_mode / ring_k / seq_len differ from fd_state_init's");
   const RecMap m = rec_map(st.K, st.S, hd.has_uext != 0);
@@ -466,7 +506,9 @@ void state_restore(Engine& e, const char* path, int shard, int n_shards, int fla
   Fnv h_cards;
   for (int64_t lo = 0; lo < hd.n_cards; lo += chunk) {
     const int64_t n = std::min<int64_t>(chunk, hd.n_cards - lo);
-    read_all(in.f, pin.p, (size_t)n * rec_bytes, &h_cards);
+    read_all(in.f, pin.p, (size_t)n * rec_bytes, &h_cards);  // the checksum covers the bytes as stored
+    if (hd.version == 2)
+      for (int64_t r = 0; r < n; ++r) header_v2_to_v3(static_cast<unsigned char*>(pin.p) + (size_t)r * rec_bytes, st.mode);
     FD_HIP(hipMemcpyAsync(recs.ptr, pin.p, (size_t)n * rec_bytes, hipMemcpyHostToDevice, e.stream));
     hipLaunchKernelGGL(restore_slot_kernel, dim3(blocks(n)), dim3(256), 0, e.stream,
                        st.keys.as<unsigned long long>(), st.view(), (long long)(st.cap - 1),

@@ -152,10 +152,13 @@ def test_config4_full_size_warm_pipelined():
     simulator.py:229,302) run through the feature path so the 5 min / 1 h / 24 h windows hold events
     (RedisService.java:178-207), then three 64 k micro-batches submitted back to back through ShardedScorer at
     world 1 over EngineShardBackend(pipelined=True) -> fd_score_batch_pipelined (batch i+1's features overlap
-    batch i's forests). The first two batches request no vectors — the exact variant the bench times: compact 24-float
-    vectors into the fused ensemble kernel, slot pass on its own stream (engine counters prove both) — and their
+    batch i's forests). The first two batches request no vectors — the exact variant the bench times: compact 64-B
+    rows (14 f32 words + the 8 small-integer slots as bytes) into the fused ensemble kernel, slot pass on its own
+    stream (engine counters prove both) — and their
     fraud probability, confidence, decision and risk are checked against the oracle chain on the oracle's own vectors;
-    the third requests vectors and model probabilities (64-wide variant), checked element by element. The oracle
+    the third requests vectors and model probabilities (64-wide variant), checked element by element. (Bit-identity of
+    the compact rows with the 64-wide path at K = 64 is pinned by test_gpu_pipeline's twin-engine test: a twin does not
+    fit beside this one's 155 GB of card pages.) The oracle
     replays the history rows of exactly the cards those batches touch. K = 64 ring events per card (the bench's
     headline) in 2^27 slots (load factor ~0.78 after the history's unknown-user cards): the engine's
     window_saturated counter over the three batches equals the oracle's count of transactions whose 24 h window

@@ -69,6 +69,28 @@ def test_xgb_config2_full_batch(engine):
     assert np.abs(prob - rp).max() <= PROB_TOL
 
 
+def test_xgb_config2_timed_kernel(engine):
+    """the kernel config 2's bench line times — fd_forest_predict with no leaf ids at 500 trees x
+    depth 8, 50 features, 64 k rows selects the fused single-forest ensemble_kernel<8,2> (engine counter
+    ensemble_single_launches proves it ran, twice) — against oracle.xgb_predict: probabilities within 1e-5 on the
+    probability-only launch (the bench's exact call), and the same kernel's f32 margins bit-identical when its raw
+    output is requested (model_manager.py:309-311)."""
+    X = synth.feature_matrix(65536, 50, seed=71, nan_frac=0.01)
+    doc = synth.xgboost_doc(500, 8, 50, synth.feature_matrix(512, 50, seed=72), seed=73, p_leaf=0.05)
+    fa = xgboost_from_json_doc(doc)
+    engine.load_forest(6, fa)
+    c0 = engine.counter("ensemble_single_launches")
+    prob = engine.predict(6, X)  # probabilities only: the bench's timed call
+    assert engine.counter("ensemble_single_launches") - c0 == 1
+    prob2, raw = engine.predict(6, X, want_raw=True)  # the same kernel with its raw-score output
+    assert engine.counter("ensemble_single_launches") - c0 == 2
+    rp, rm, _ = oracle.xgb_predict(fa, X)
+    assert np.abs(prob - rp).max() <= PROB_TOL
+    np.testing.assert_array_equal(prob2, prob)
+    np.testing.assert_array_equal(raw.astype(np.float32), rm)  # the reference's f32 sum sequence, bit for bit
+    np.testing.assert_array_equal(raw, raw.astype(np.float32).astype(np.float64))
+
+
 def test_iforest_parity_vs_sklearn(engine):
     Xtr = synth.feature_matrix(4000, 64, seed=61).astype(np.float64)
     m = synth.isolation_forest(Xtr)

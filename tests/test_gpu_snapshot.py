@@ -120,6 +120,79 @@ def test_resume_equals_uninterrupted(engine, tmp_path, mode):
     assert sum(len(r[3]) for r in ref[:-1]) > 100  # user windows did fire after the cut
 
 
+def _fnv_words(b: bytes) -> int:
+    """snapshot.hip Fnv over a section whose length is a multiple of 8"""
+    h, mask = 0xCBF29CE484222325, (1 << 64) - 1
+    for w in np.frombuffer(b, dtype="<u8").tolist():
+        h = ((h ^ w) * 0x100000001B3) & mask
+    return h
+
+
+def _downgrade_to_v2(blob: bytes, mode: int) -> bytes:
+    """A v3 image rewritten as the v2 format (the card header before the round-5 relayout: key first, absolute oldest
+    in-window times, the redis_compat session amount in its own word), checksum recomputed — what a pre-relayout
+    engine wrote for the same state."""
+    import struct
+    hd = bytearray(blob[:256])
+    n_cards, rec_bytes = struct.unpack_from("<qq", hd, 48)
+    cards = bytearray(blob[256:256 + n_cards * rec_bytes])
+    for r in range(n_cards):
+        o = r * rec_bytes
+        v3 = bytes(cards[o:o + 128])
+        last_ts, rn, rh, us, _, wc0, wc1, wc2, _, flags, rc_cnt = struct.unpack_from("<q8BIi", v3, 0)
+        ws = list(struct.unpack_from("<3q", v3, 24))
+        wod = struct.unpack_from("<3I", v3, 48)
+        key, avg, age = struct.unpack_from("<Qdi", v3, 64)
+        fp = struct.unpack_from("<3Q", v3, 88)
+        wc = (wc0, wc1, wc2)
+        wo = [last_ts - wod[k] if wc[k] > 0 else 0 for k in range(3)]
+        rc_sum = 0
+        if mode == 0:  # redis_compat: the session amount had its own field
+            rc_sum, ws[0] = ws[0], 0
+        v2 = struct.pack("<QqdiI8B3Q3q3qqii", key, last_ts, avg, age, flags, rn, rh, us, 0, wc0, wc1, wc2, 0,
+                         *fp, *ws, *wo, rc_sum, rc_cnt, 0)
+        assert len(v2) == 128
+        cards[o:o + 128] = v2
+    struct.pack_into("<I", hd, 8, 2)
+    struct.pack_into("<Q", hd, 136, _fnv_words(bytes(cards)))
+    return bytes(hd) + bytes(cards) + blob[256 + n_cards * rec_bytes:]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_v2_image_restores_as_v3(engine, tmp_path, mode):
+    """images written before the round-5 header relayout (format v2) restore through a host-side
+    header conversion and continue the stream exactly as the v3 image of the same state does; other versions are
+    refused with FD_ERR_UNSUPPORTED."""
+    import struct
+    from fdengine._native import FD_ERR_UNSUPPORTED
+    pop, tx, ctx = _stream(n_users=600, n=6000, seed=41 + mode)
+    cuts = _cuts(len(tx["card_key"]), 4)
+    _setup(engine, pop, 4096, mode)
+    _run(engine, tx, ctx, cuts[:2], flush=False)
+    v3 = tmp_path / "v3.fdsnap"
+    engine.state_snapshot(v3)
+    v2 = tmp_path / "v2.fdsnap"
+    v2.write_bytes(_downgrade_to_v2(v3.read_bytes(), mode))
+    v1 = bytearray(v3.read_bytes())
+    struct.pack_into("<I", v1, 8, 1)
+    (tmp_path / "v1.fdsnap").write_bytes(bytes(v1))
+    outs = []
+    for path in (v3, v2):
+        fresh = FraudEngine(0)
+        try:
+            fresh.state_init(4096, mode, 8)
+            fresh.windows_init(1 << 16)
+            assert fresh.state_restore(path) == engine.state_info()["cards"]
+            outs.append(_run(fresh, tx, ctx, cuts[2:]))
+            if path == v2:
+                with pytest.raises(NativeError, match="unsupported snapshot version") as ei:
+                    fresh.state_restore(tmp_path / "v1.fdsnap")
+                assert ei.value.code == FD_ERR_UNSUPPORTED
+        finally:
+            fresh.close()
+    _same(outs[1], outs[0])
+
+
 def test_resume_lstm_history(engine, tmp_path):
     import torch
     pop, tx, _ = _stream(n_users=800, n=9000, seed=11)
