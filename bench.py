@@ -665,6 +665,7 @@ class Config3:
             hist = lstm_ref.SequenceState(self.seq_len)
         P = self.parity_batches
         c0 = self.eng.counter("pipelined_compact_batches") if self.pipe else None
+        q0 = self.eng.counter("pipelined_split_batches") if self.pipe else None
         out = _parity_record(P, "pipelined stream, fused kernel from compact vectors" if self.pipe else
                              "fd_score_batch_device (latency path)", self.B)
         for b in range(P + 1):
@@ -690,6 +691,7 @@ class Config3:
                                                                  float(np.abs(Mp[m] - col).max()))
         if c0 is not None:
             out["timed_path"]["compact_batches"] = self.eng.counter("pipelined_compact_batches") - c0
+            out["timed_path"]["split_row_batches"] = self.eng.counter("pipelined_split_batches") - q0
         del o
         return out
 
@@ -874,7 +876,9 @@ class Config4(Config3):
         self.scorer = ShardedScorer(EngineShardBackend(eng, self.params, [0, 1],
                                                        pipelined=not args.no_pipeline), rank, self.world)
         self.out = None
-        self.host_out = None
+        # the latency loops' host-mapped output ring, allocated here: allocated at the first step_to_host it cost that
+        # step 1.77 ms of host time (hipHostMalloc x 8: the loaded loop's sample 0 at 1.92 ms)
+        self.host_out = HostOutRing(B, 8) if (self.world == 1 or self.scorer.native) else None
         # the resident micro-batches as column views, made once (a serving loop hands the scorer batches it already
         # holds; slicing nine columns per step is harness cost, ~10-20 us of Python)
         self.parts = [{f: t[b * B:(b + 1) * B] for f, t in self.dev.items()} for b in range(self.n_batches)]
@@ -1001,6 +1005,7 @@ class Config4(Config3):
         raws = []
         sat0 = _saturated(self.eng, self)
         c0 = self.eng.counter("pipelined_compact_batches")
+        q0 = self.eng.counter("pipelined_split_batches")
         s0 = self.eng.counter("pipelined_slot_stream_batches")
         for b in range(P + 1):
             twin = b == P
@@ -1022,6 +1027,7 @@ class Config4(Config3):
                 M = mp.cpu().numpy()
                 leg["max_abs_model_prob_diff"] = max(float(np.abs(M[0] - px).max()), float(np.abs(M[1] - pi).max()))
         out["timed_path"]["compact_batches"] = self.eng.counter("pipelined_compact_batches") - c0
+        out["timed_path"]["split_row_batches"] = self.eng.counter("pipelined_split_batches") - q0
         out["timed_path"]["slot_stream_batches"] = self.eng.counter("pipelined_slot_stream_batches") - s0
         from fdengine.synth_gpu import occupancy
         allraw = np.concatenate(raws)
@@ -1354,6 +1360,7 @@ class Config3J(Config3):
         o.load_users(self.ukeys, self.uavg, self.uage, self.ufp)
         o.load_merchants(self.merchants["fraud_rate"], self.merchants["risk_multiplier"])
         c0 = self.eng.counter("pipelined_compact_batches")
+        q0 = self.eng.counter("pipelined_split_batches")
         self.step(0)
         self.torch.cuda.synchronize()
         cols = R.parse_batch(self.msgs[0][:k], {m: i for i, m in enumerate(self.merchant_ids)},
@@ -1370,6 +1377,7 @@ class Config3J(Config3):
                              else "codec -> fd_score_batch_device", k)
         _parity_compare(out["timed_path"], got, ref)
         out["timed_path"]["compact_batches"] = self.eng.counter("pipelined_compact_batches") - c0
+        out["timed_path"]["split_row_batches"] = self.eng.counter("pipelined_split_batches") - q0
         if not self.pipe:
             _parity_vectors(out["timed_path"], self.vec[:k].cpu().numpy(), rvec)
         del out["twin"]
@@ -1470,6 +1478,9 @@ def _free_port() -> int:
 # control flow on fewer GPUs (ranks share devices, exchanges staged through host memory): its numbers are not
 # the metric, the line says so in config.dist_backend.
 DIST_BACKEND = os.environ.get("FD_BENCH_DIST_BACKEND", "nccl")
+
+
+LAT_SPLIT = ("total", "submit", "native", "wait", "gpu")  # latency_split's per-sample columns (ms)
 
 
 def launch_ranks(n: int) -> int:
@@ -1611,18 +1622,58 @@ def main():
     gc.freeze()
     # p50 / p99: one micro-batch at a time, then the same from pinned host memory (run after the throughput region:
     # run before it they left the pipelined steps ~7 % slower for hundreds of steps, profiles/r05/warm_blocks)
+    # the latency loops' wait for a batch's results: a spin on an event query (what a latency-bound consumer does);
+    # hipStreamSynchronize blocks on an interrupt after a short active wait, and its wake-up is at the mercy of the
+    # host scheduler (FD_LAT_WAIT=sync for it)
+    spin = os.environ.get("FD_LAT_WAIT", "spin") != "sync"
+    lat_ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for ev in lat_ev:  # created at their first record, before the loops
+        ev.record(stream)
+    torch.cuda.synchronize()
+
+    def wait_done():
+        if spin:
+            lat_ev[2].record(stream)
+            while not lat_ev[2].query():
+                pass
+        else:
+            stream.synchronize()
+
     def latency_loops():
-        lat = []
+        lat, split = [], []
+        native = hasattr(eng, "counter")
         for i in range(args.latency_iters):
+            n0 = eng.counter("pipelined_host_ns") if native else 0
+            lat_ev[0].record(stream)
             a = time.perf_counter()
             if hasattr(wl, "step_to_host"):
                 wl.step_to_host(i, i)
             else:
                 wl.step(i)
                 wl.fetch(i)
-            stream.synchronize()
-            lat.append(time.perf_counter() - a)
+            b = time.perf_counter()
+            lat_ev[1].record(stream)
+            wait_done()
+            c = time.perf_counter()
+            lat.append(c - a)
+            n1 = eng.counter("pipelined_host_ns") if native else 0
+            # per sample: total, host submit, of which inside the engine's native call, the wait, the GPU span
+            # (stream events around the submission: from the stream reaching the step to its results copied)
+            split.append((c - a, b - a, (n1 - n0) * 1e-9, c - b, lat_ev[0].elapsed_time(lat_ev[1]) * 1e-3))
         lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
+        latency_split.clear()
+        if split:
+            S = np.array(split) * 1e3
+            worst = np.argsort(S[:, 0])[::-1][:5]
+            latency_split.update({
+                "wait": "spin on hipEventQuery" if spin else "hipStreamSynchronize",
+                "p50_ms": {k: round(float(np.percentile(S[:, j], 50)), 4) for j, k in enumerate(LAT_SPLIT)},
+                "p99_ms": {k: round(float(np.percentile(S[:, j], 99)), 4) for j, k in enumerate(LAT_SPLIT)},
+                "max_ms": {k: round(float(S[:, j].max()), 4) for j, k in enumerate(LAT_SPLIT)},
+                "worst": [[int(q)] + [round(float(x), 4) for x in S[q]] for q in worst],
+                "columns": ["sample"] + list(LAT_SPLIT),
+                "basis": "isolated loop, per sample: total = host submit + wait; native = host ns inside the engine's "
+                         "pipelined call (counter pipelined_host_ns); gpu = stream events around the submission"})
         p99 = float(np.percentile(lat_ms, 99))
         # the same with the input columns crossing PCIe from pinned host memory first (workloads that support it)
         lat_h2d = []
@@ -1630,7 +1681,7 @@ def main():
             for i in range(min(args.latency_iters, len(getattr(wl, "h2d_pool", [])) or args.latency_iters)):
                 a = time.perf_counter()
                 wl.step_h2d(i)  # H2D, the step, results in host memory
-                stream.synchronize()
+                wait_done()
                 lat_h2d.append(time.perf_counter() - a)
         p99_h2d = float(np.percentile(np.array(lat_h2d) * 1e3, 99)) if lat_h2d else -1.0
         if dist:  # the node's p99: the worst rank's
@@ -1726,8 +1777,12 @@ def main():
         if stall_trace:
             import faulthandler
         for i in range(args.loaded_iters):
-            if i >= D:
-                evs[i - D].synchronize()
+            if i >= D:  # backpressure: batch i-D's results are back (a spin, as the isolated loop's wait)
+                if spin:
+                    while not evs[i - D].query():
+                        pass
+                else:
+                    evs[i - D].synchronize()
             sub.append(time.perf_counter() - h0)
             if stall_trace:
                 faulthandler.dump_traceback_later(float(stall_trace) / 1e3, exit=False)
@@ -1759,6 +1814,7 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             loaded["p99_ms"] = float(t.item())
 
+    latency_split = {}
     lat, lat_ms, p99, lat_h2d, p99_h2d = latency_loops()
 
     # the same kernels one micro-batch at a time, nothing beside them (in the pipelined stream the next batch's
@@ -1826,6 +1882,7 @@ def main():
             "latency_samples": len(lat),
             "latency_basis": "p50/p99/max: one micro-batch at a time (submit -> scores in host memory, then the next); "
                              "loaded_latency: at the throughput operating point",
+            "latency_split": latency_split or None,
             "loaded_latency": loaded,
             "roofline": roof,
             "kernel_avg_us": wl.kernels(timing),

@@ -372,9 +372,18 @@ void exchange_ops(Engine& e, bool back, hipStream_t st, const void* sendbuf, con
   size_t os = 0, orr = 0;
   unsigned long long n_ops = 0;
   for (int p = 0; p < c.world; ++p) {
-    if (send[p] > 0) check(R, R.send(sb + os * elem, (size_t)send[p] * elem, ncclUint8, p, k, st), "ncclSend");
-    if (recv[p] > 0) check(R, R.recv(rb + orr * elem, (size_t)recv[p] * elem, ncclUint8, p, k, st), "ncclRecv");
-    n_ops += (send[p] > 0) + (recv[p] > 0);
+    if (p == c.rank) {  // this rank's own share: a device copy on the same stream, not an RCCL send / receive pair
+      // (2 x world -> 2 x (world - 1) operations per exchange). Enqueued inside the caller's group, so it runs
+      // before the group's RCCL kernel on `st`: its source and destination are ready then (the scatter / scoring
+      // that wrote sendbuf and the inbox wait precede the group on `st`). send[rank] == recv[rank] by construction.
+      FD_REQUIRE(send[p] == recv[p], FD_ERR_HIP, "corrupt split sizes (own share)");
+      if (send[p] > 0)
+        FD_HIP(hipMemcpyAsync(rb + orr * elem, sb + os * elem, (size_t)send[p] * elem, hipMemcpyDeviceToDevice, st));
+    } else {
+      if (send[p] > 0) check(R, R.send(sb + os * elem, (size_t)send[p] * elem, ncclUint8, p, k, st), "ncclSend");
+      if (recv[p] > 0) check(R, R.recv(rb + orr * elem, (size_t)recv[p] * elem, ncclUint8, p, k, st), "ncclRecv");
+      n_ops += (send[p] > 0) + (recv[p] > 0);
+    }
     os += (size_t)send[p];
     orr += (size_t)recv[p];
   }

@@ -102,7 +102,7 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
                          const uint8_t* present, const float* dX, int64_t n, int32_t ld, double* dMP,
                          double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk, const float* d_seq = nullptr,
                          int T = 0, const fd::RouteRecord* records = nullptr, fd::ResultRecord* results = nullptr,
-                         bool compact = false, const unsigned long long* d_seq_desc = nullptr) {
+                         int compact = 0, const unsigned long long* d_seq_desc = nullptr) {
   FD_REQUIRE(p.n_models > 0 && p.n_models <= FD_MAX_MODELS, FD_ERR_INVALID_ARG, "n_models out of range");
   FD_REQUIRE(slots != nullptr && (dfp != nullptr || results != nullptr), FD_ERR_INVALID_ARG, "null slots/output");
   if (n == 0) return false;
@@ -454,6 +454,8 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
   } else if (k == "ensemble_single_launches") {  // fd_forest_predict batches scored by the fused kernel over one
     // forest (probabilities, optionally raw scores; no leaf ids): config 2's timed kernel, ensemble_kernel<8,2>
     *value = (int64_t)e.ens_single_total;
+  } else if (k == "pipelined_split_batches") {  // of the compact ones: split rows (compact_vectors 2)
+    *value = (int64_t)e.pipe_split_total;
   } else if (k == "pipelined_compact_batches") {  // of those: scored by the fused kernel from the compact 64-B
     // rows (no vectors requested), the variant the config-3/4 bench times
     *value = (int64_t)e.pipe_compact_total;
@@ -511,10 +513,12 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     // communicators, else wide), 1 wide (24 / 16 trees), 2 compact (20 / 12: LDS room for an RCCL kernel beside)
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "ensemble_chunks must be 0, 1 or 2");
     e.ens_chunks = (int)value;
-  } else if (k == "compact_vectors") {  // pipelined stream: 1 (default) the fused kernel's batches carry the
-    // compact 64-B row when nobody asked for the vectors; 0 always the 64-wide one (outputs identical)
-    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "compact_vectors must be 0 or 1");
-    e.compact_vectors = value != 0;
+  } else if (k == "compact_vectors") {  // pipelined stream, the fused kernel's batches when nobody asked for the
+    // vectors: 2 (default) split rows — the card-independent half finished by the slot pass, the bucket pass reads
+    // 32-B prep records and writes the card half (features.hip Prep32 / RowA / RowB); 1 the compact 64-B row; 0 the
+    // 64-wide vector (outputs identical in every mode)
+    FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "compact_vectors must be 0, 1 or 2");
+    e.compact_vectors = (int)value;
   } else if (k == "latency_fused") {  // latency batches: 1 (default) both forests' walks in one launch and their
     // sums + the blend in another (fd::launch_forest_pair_blend); 0 the per-forest walk + sum launches + blend
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "latency_fused must be 0 or 1");
@@ -1109,8 +1113,11 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   // batch i-1's card updates
   hipEvent_t before_buckets = e.pipe_feat_live[prev] ? e.pipe_feat_ev[prev] : nullptr;
   // the fused kernel alone reads the vectors and nobody asked for them: the compact form (64 instead of 256 B per
-  // transaction written here and read by the ensemble kernel, fd_internal.h kCompactSlot)
-  const bool compact = e.compact_vectors && d_vectors == nullptr && fd::ensemble_applies(e, *params, slots, present, n);
+  // transaction written here and read by the ensemble kernel, fd_internal.h kCompactSlot), or split rows
+  // (compact 2: the slot pass writes the card-independent half, the bucket pass reads 32-B instead of 64-B prep
+  // records; the lean bucket pass only, and not with LSTM history in the card state)
+  int compact = (e.compact_vectors && d_vectors == nullptr && fd::ensemble_applies(e, *params, slots, present, n))
+                    ? e.compact_vectors : 0;
   e.pipe_vec[s].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
   float* vec = e.pipe_vec[s].as<float>();
   float* seq = nullptr;
@@ -1127,6 +1134,7 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   // whose two launches cost 39 us per 1 k batch against its 18; it waits for batch i-1's card updates
   // (before_buckets) like the lean pass
   const bool lean = e.pipe_lean && !(e.pipe_gather && e.state.slot_gather && n <= fd::kGatherBatchMax && !Ss);
+  if (compact == 2 && (!lean || want_seq || e.state.S > 0)) compact = 1;
   {
     struct SlotPass {  // launch_grouped reads these for this call only
       Engine& e;
@@ -1161,7 +1169,8 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   if (e.pipe_copy_live[s]) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_copy_ev[s], 0));
   ++e.pipe_iter;
   ++e.pipe_iter_total;
-  e.pipe_compact_total += compact;
+  e.pipe_compact_total += compact != 0;
+  e.pipe_split_total += compact == 2;
   e.pipe_slot_stream_total += Ss != nullptr;
   {  // the scoring launches go on Sc: score_matrix launches on e.stream
     struct Swap {

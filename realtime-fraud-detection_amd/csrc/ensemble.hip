@@ -90,7 +90,8 @@ struct EnsArgs {
   const float* thr;
   int thr_off[kMaxFeatures + 1];  // per-feature table offsets into thr (kernel arguments: scalar loads)
   int vec4;                       // rows 16-B aligned (ld % 4 == 0, aligned X): float4 row loads
-  int compact;                    // X rows are the compact 64-B rows (fd_internal.h), binned here
+  int compact;                    // 1: X rows are the compact 64-B rows (fd_internal.h), binned here; 2: split rows
+                                  // (RowA [n] at X, RowB [n] after it, 32 B each: features.hip, load_split)
   uint16_t cbin[kMaxFeatures];    // compact mode: the bins of the constant slots (0 or 0.5), per plan
   alignas(4) uint16_t lut[8 * 32];  // compact mode: [kIntSlots][kLutN] bins of the small-integer slots' values 0..31
 
@@ -361,6 +362,58 @@ __device__ __forceinline__ void load_compact(const float* __restrict__ xr, float
   }
 }
 
+// Split rows (features.hip Prep32 / RowA / RowB): thread Q's compact slots Q, Q + 4, ... from the slot pass's RowA
+// (card-independent) and the bucket pass's RowB (card-dependent). The derived features' positions 41..46 follow
+// FeatureProcessor's conditional order (feature_processor.py:330-363, write_vector): [amount_sqrt if amount > 0,
+// amount / user average if that average > 0, hourly velocity ratio if the 24 h count > 0, combined device-IP risk,
+// business hours, late night], the k-th present one at 41 + k, zero after. The values are RowA / RowB's f32 as stored.
+template <int Q>
+__device__ __forceinline__ void load_split(const uint4* __restrict__ ra, const uint4* __restrict__ rb,
+                                           float (&v)[16]) {
+  const uint4 a0 = ra[0], a1 = ra[1], b0 = rb[0], b1 = rb[1];
+  const unsigned fa = a1.w >> 24;                   // RowA flags
+  const int na = (fa & 1u) ? 1 : 0;                 // amount > 0
+  const int nu = ((b1.z >> 8) & 1u) ? 1 : 0;        // user average > 0
+  const int nc = ((b1.y >> 8) & 0xFFu) ? 1 : 0;     // 24 h count > 0 (its byte: clip10 of an integer)
+  const int n2 = na + nu + nc;
+  auto byte = [](unsigned w, int k) { return (float)((w >> (8 * k)) & 0xFFu); };
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int ci = Q + 4 * i;
+    float x = 0.f;
+    switch (ci) {  // compile-time per unrolled i (fd_internal.h kCompactSlot order)
+      case 0: x = __uint_as_float(a0.x); break;   // 0 amount
+      case 1: x = __uint_as_float(a0.y); break;   // 1 amount_log
+      case 2: x = byte(a1.w, 0); break;           // 5 hour
+      case 3: x = byte(a1.w, 1); break;           // 6 day of week
+      case 4: x = byte(a1.w, 2); break;           // 7 weekend
+      case 5: x = byte(b1.y, 0); break;           // 14 1 h count
+      case 6: x = byte(b1.y, 1); break;           // 15 24 h count
+      case 7: x = __uint_as_float(b0.x); break;   // 16 24 h amount
+      case 8: x = __uint_as_float(b0.y); break;   // 17 user average
+      case 9: x = byte(b1.y, 2); break;           // 19 account age
+      case 10: x = __uint_as_float(a0.w); break;  // 21 merchant fraud rate
+      case 11: x = __uint_as_float(a1.x); break;  // 23 merchant risk
+      case 12: x = byte(b1.y, 3); break;          // 26 new device
+      case 13: x = __uint_as_float(a1.y); break;  // 27 IP risk
+      case 14: x = __uint_as_float(b0.z); break;  // 31 1 h amount
+      case 15: x = byte(b1.z, 0); break;          // 32 5 min count
+      default:
+        if (ci < kCompactSlots) {  // 41 + k: the k-th present derived feature
+          const int k = ci - 16;
+          const float first = (na && k == 0) ? __uint_as_float(a0.z)
+                                             : ((nu && k == na) ? __uint_as_float(b0.w) : __uint_as_float(b1.x));
+          const int t = k - n2;  // past the conditional three: combined risk, business, late night
+          x = k < n2 ? first
+                     : (t == 0 ? __uint_as_float(a1.z)
+                               : (t == 1 ? ((fa & 2u) ? 1.f : 0.f) : (t == 2 ? ((fa & 4u) ? 1.f : 0.f) : 0.f)));
+        }
+        break;
+    }
+    v[i] = x;
+  }
+}
+
 template <int Q, int L, bool LUT>
 __device__ __forceinline__ void bin_compact_pass(const EnsArgs& a, const float (&v)[16], uint16_t* Xs,
                                                  int txn, int f0, int f1, bool glob, uint32_t tl, int o0,
@@ -468,7 +521,16 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
     // VGPRs, the bucket kernel's wave fits beside the ensemble's four per SIMD); the constant slots' bins straight
     // away
     float v[16];
-    if (valid && a.compact) {
+    if (valid && a.compact == 2) {  // split rows: RowA [n], then RowB [n]
+      const uint4* ra = reinterpret_cast<const uint4*>(a.X) + 2 * row;
+      const uint4* rb = reinterpret_cast<const uint4*>(a.X) + 2 * (a.n + row);
+      switch (q) {  // wave-uniform
+        case 0: load_split<0>(ra, rb, v); bin_compact_constants<0>(a, Xs, txn); break;
+        case 1: load_split<1>(ra, rb, v); bin_compact_constants<1>(a, Xs, txn); break;
+        case 2: load_split<2>(ra, rb, v); bin_compact_constants<2>(a, Xs, txn); break;
+        default: load_split<3>(ra, rb, v); bin_compact_constants<3>(a, Xs, txn); break;
+      }
+    } else if (valid && a.compact) {
       const float* xr = a.X + row * (int64_t)kCompactWidth;
       switch (q) {  // wave-uniform
         case 0: load_compact<0>(xr, v); bin_compact_constants<0>(a, Xs, txn); break;
@@ -1062,13 +1124,13 @@ bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots,
 
 bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
                      const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
-                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results, bool compact) {
+                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results, int compact) {
   Pair q;
   if (!select_pair(e, p, slots, present, n, q)) return false;
   const int pa = q.pa, pb = q.pb, ma = q.ma, mb = q.mb;
   EnsArgs a{};
   plan_args(e.ens, dX, n, compact ? kCompactWidth : ld, e.ens_owner_fixed, a);
-  a.compact = compact ? 1 : 0;
+  a.compact = compact;
   if (compact && e.ens_bin_global) {  // one pass, every table searched where it lies (L2), nothing staged
     a.n_pass = 1;
     a.pass_f[0] = 0;

@@ -533,6 +533,7 @@ struct Engine {
   unsigned long long pipe_iter_total = 0;  // counter "pipelined_batches"
   unsigned long long ens_single_total = 0;    // counter "ensemble_single_launches": fd_forest_predict batches run by
                                               // the fused kernel over one forest (config 2's timed kernel)
+  unsigned long long pipe_split_total = 0;    // counter "pipelined_split_batches": of those, split rows
   unsigned long long pipe_compact_total = 0;  // counter "pipelined_compact_batches": batches scored from compact vectors
   unsigned long long pipe_host_ns = 0;  // counter "pipelined_host_ns": host time inside fd_score_batch_pipelined
   unsigned long long pipe_slot_stream_total = 0;  // counter "pipelined_slot_stream_batches": slot pass on its own stream
@@ -551,7 +552,9 @@ struct Engine {
   bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
   bool ens_prio = false;  // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels)
   bool ens_bin_global = false;  // "ensemble_bin_global": compact rows binned by searches in global memory (no staging)
-  bool compact_vectors = true;  // "compact_vectors": the pipelined stream's compact scoring vectors (engine.hip)
+  int compact_vectors = 2;      // "compact_vectors": the pipelined stream's scoring rows for the fused kernel when
+                                // nobody asked for vectors: 0 the 64-wide vector, 1 compact 64-B rows, 2 split rows
+                                // (card-independent half from the slot pass; engine.hip, features.hip Prep32)
   int stream_prio = 3;    // option "stream_priority": the pipeline / forward streams' HIP priorities (engine.hip)
   // host-API staging
   DeviceBuffer stage_in, stage_out0, stage_out1, stage_out2, stage_out3;
@@ -649,15 +652,16 @@ void state_clear(Engine& e);
 int64_t state_count(Engine& e);
 void load_users(Engine& e, const fd_users& u);
 void load_merchants(Engine& e, const fd_merchants& m);
-// compact: d_vec rows are the fused pipeline's compact form (64-B rows: kCompactWidth words, fd_internal.h), not the 64-wide vector
+// compact: 0 the 64-wide vector; 1 the fused pipeline's compact form (64-B rows: kCompactWidth words, fd_internal.h);
+// 2 split rows (features.hip Prep32 / RowA / RowB: RowA [n] then RowB [n], 32 B each; lean bucket pass only)
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw,
                      float* d_seq = nullptr, double* d_vel5 = nullptr, hipStream_t stream = nullptr,
-                     bool lean = false, int set = 0, hipEvent_t before_buckets = nullptr, bool compact = false,
+                     bool lean = false, int set = 0, hipEvent_t before_buckets = nullptr, int compact = 0,
                      unsigned long long* d_seq_desc = nullptr);
 // the same over received 48-B route records (route.hip), no unpack pass; also returns nothing else
 void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq,
                              hipStream_t stream = nullptr, bool lean = false, int set = 0,
-                             hipEvent_t before_buckets = nullptr, bool compact = false);
+                             hipEvent_t before_buckets = nullptr, int compact = 0);
 void load_users_ext(Engine& e, const fd_users_ext& u);
 void load_merchants_ext(Engine& e, const fd_merchants_ext& m);
 void load_vocab(Engine& e, const uint8_t* pay_high_risk, const uint8_t* type_refund);
@@ -732,10 +736,11 @@ bool ensemble_applies(Engine& e, const fd_blend_params& p, const int32_t* slots,
 // one forest's probabilities through the fused kernel (large batches, no raw / leaf outputs); false: not applicable
 bool launch_ensemble_single(Engine& e, int slot, const float* dX, int64_t n, int32_t ld, double* dprob,
                             double* draw, hipStream_t stream);
-// compact: dX rows are the compact vector (64-B rows of kCompactWidth words, ld ignored; the plan's features <= 64)
+// compact: 1 dX rows are the compact vector (64-B rows of kCompactWidth words, ld ignored; the plan's features <= 64);
+// 2 split rows (RowA [n] then RowB [n] at dX, features.hip)
 bool launch_ensemble(Engine& e, const fd_blend_params& p, const int32_t* slots, const uint8_t* present,
                      const float* dX, int64_t n, int32_t ld, double* dMP, double* dfp, double* dconf, uint8_t* ddec,
-                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results, bool compact = false);
+                     uint8_t* drisk, const RouteRecord* records, ResultRecord* results, int compact = 0);
 void forest_loaded(PackedForest& pf, const fd_forest_params& p, const fd_tree_arrays& t);
 // blend.hip
 void launch_blend(Engine& e, const fd_blend_params& p, int64_t n, const double* const* d_probs,

@@ -243,6 +243,94 @@ __device__ __forceinline__ Prep load_prep(const Prep* __restrict__ src) {
   return p;
 }
 
+// Split rows (engine option compact_vectors 2, the pipelined stream's fused-kernel batches without LSTM history):
+// the card-independent half of the scoring row is finished by the slot kernel, which has the transaction's columns
+// in hand, and the bucket kernel reads back only what the card work needs. Per transaction (arrival order):
+//   Prep32 (32 B, slot -> bucket kernel): ts, cents, device fingerprint — the bucket kernel's random read of
+//           transaction i is one 32-B piece instead of the 64-B Prep;
+//   RowA   (32 B, slot kernel -> fused kernel): the card-independent compact slots, final (features.hip
+//           write_vector's arithmetic): amount, amount_log, amount_sqrt (derived), merchant fraud rate / risk
+//           score, IP risk, the derived combined_device_ip_risk, and as bytes hour, day of week, weekend and the
+//           flags {amount > 0, business hours, late night};
+//   RowB   (32 B, bucket kernel -> fused kernel): the card-dependent slots: 24 h / 1 h amounts, user average,
+//           amount / user average, hourly velocity ratio, and as bytes the 1 h / 24 h / 5 min counts, account age,
+//           new device, {user average > 0}.
+// The fused kernel (ensemble.hip load_split) assembles the 22 compact slots from the two rows, including the derived
+// features' data-dependent positions; every value is the f32 write_vector stores, so the bins and outputs are the
+// 64-wide path's bit for bit.
+struct __attribute__((aligned(16))) Prep32 {
+  long long ts, cents;
+  unsigned long long dfp;
+  unsigned long long pad;
+};
+static_assert(sizeof(Prep32) == 32, "Prep32 must be 32 B");
+constexpr unsigned kRowAPos = 1u, kRowABus = 2u, kRowALate = 4u;  // RowA flags (byte 31)
+constexpr unsigned kRowBUavg = 1u;                                 // RowB flags (byte 25)
+
+__device__ __forceinline__ void store_prep32(Prep32* dst, const Txn& t) {
+  uint4* q = reinterpret_cast<uint4*>(dst);
+  const unsigned long long a = (unsigned long long)t.ts, b = (unsigned long long)t.cents;
+  q[0] = make_uint4((unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32));
+  q[1] = make_uint4((unsigned)t.dfp, (unsigned)(t.dfp >> 32), 0u, 0u);
+}
+
+// the fields the card work reads (base_raw / velocity_step in split mode: cents, ts, device fingerprint)
+__device__ __forceinline__ Prep load_prep32(const Prep32* __restrict__ src) {
+  const uint4* q = reinterpret_cast<const uint4*>(src);
+  const uint4 w0 = q[0], w1 = q[1];
+  Prep p{};
+  p.ts = (long long)(((unsigned long long)w0.y << 32) | w0.x);
+  p.cents = (long long)(((unsigned long long)w0.w << 32) | w0.z);
+  p.dfp = ((unsigned long long)w1.y << 32) | w1.x;
+  return p;
+}
+
+// RowA from the slot kernel's prep (the same operations as write_vector / base_raw on these fields)
+__device__ __forceinline__ void store_row_a(uint4* dst, const Prep& p) {
+#pragma clang fp contract(off)
+  const double r0 = (double)p.cents / 100.0;
+  const double amount = pmax(r0, 0.0);
+  const double hour = pmin(pmax((double)p.hour, 0.0), 23.0);
+  const double dow = pmin(pmax((double)p.dow, 0.0), 6.0);
+  double mfr = pmin(pmax(p.mfr, 0.0), 1.0);
+  if (isnan(mfr)) mfr = 0.0;
+  const double r7 = p.ipc == 0 ? NAN : (p.ipc == 1 ? 0.1 : 0.3);
+  const double ip = isnan(r7) ? 0.5 : pmin(pmax(r7, 0.0), 1.0);
+  double mrisk = pmin(pmax(p.mult, 0.0), 1.0);
+  if (isnan(mrisk)) mrisk = 0.5;
+  unsigned b = 0u;
+  b = __builtin_amdgcn_cvt_pk_u8_f32(clip10(hour), 0, b);
+  b = __builtin_amdgcn_cvt_pk_u8_f32(clip10(dow), 1, b);
+  b = __builtin_amdgcn_cvt_pk_u8_f32(p.weekend ? 1.f : 0.f, 2, b);
+  const unsigned fl = (amount > 0 ? kRowAPos : 0u) | ((9 <= hour && hour <= 17) ? kRowABus : 0u) |
+                      ((hour < 6 || hour > 22) ? kRowALate : 0u);
+  b |= fl << 24;
+  dst[0] = make_uint4(__float_as_uint(clip10(amount)), __float_as_uint(p.o1), __float_as_uint(p.dv0),
+                      __float_as_uint(clip10(mfr)));
+  dst[1] = make_uint4(__float_as_uint(clip10(mrisk)), __float_as_uint(clip10(ip)),
+                      __float_as_uint(clip10((0.5 + ip) / 2)), b);
+}
+
+// RowB from the card work's raw features (write_vector's arithmetic for the card-dependent slots)
+__device__ __forceinline__ void store_row_b(uint4* dst, const double* r) {
+#pragma clang fp contract(off)
+  const double amount = pmax(r[0], 0.0);
+  const double uavg = isnan(r[8]) ? 0.0 : pmax(r[8], 0.0);
+  const double c5 = pmax(r[9], 0.0), c1 = pmax(r[10], 0.0), c24 = pmax(r[11], 0.0);
+  const double s1 = pmax(r[12], 0.0), s24 = pmax(r[13], 0.0);
+  const double age = pmax(r[15], 0.0);
+  unsigned b = 0u, b2 = 0u;
+  b = __builtin_amdgcn_cvt_pk_u8_f32(clip10(c1), 0, b);
+  b = __builtin_amdgcn_cvt_pk_u8_f32(clip10(c24), 1, b);
+  b = __builtin_amdgcn_cvt_pk_u8_f32(clip10(age), 2, b);
+  b = __builtin_amdgcn_cvt_pk_u8_f32(r[6] > 0.5 ? 1.f : 0.f, 3, b);
+  b2 = __builtin_amdgcn_cvt_pk_u8_f32(clip10(c5), 0, b2);
+  b2 |= (uavg > 0 ? kRowBUavg : 0u) << 8;
+  dst[0] = make_uint4(__float_as_uint(clip10(s24)), __float_as_uint(clip10(uavg)), __float_as_uint(clip10(s1)),
+                      __float_as_uint(clip10(amount / uavg)));
+  dst[1] = make_uint4(__float_as_uint(clip10(c1 / (c24 / 24))), b, b2, 0u);
+}
+
 // ------------------------------------------------------------------------------------------------
 // per-batch card grouping
 // Per transaction: card slot (find-or-insert), prep record, and its (slot, arrival index) key appended to its
@@ -257,7 +345,8 @@ __global__ void __launch_bounds__(kST) feat_slot_kernel(CardPages P, unsigned lo
                                                         unsigned long long* __restrict__ pairs,
                                                         unsigned* __restrict__ ovf_cnt,
                                                         unsigned long long* __restrict__ ovf_key,
-                                                        unsigned* __restrict__ ovf_b, unsigned* err, int prio) {
+                                                        unsigned* __restrict__ ovf_b, unsigned* err, int prio,
+                                                        uint4* __restrict__ row_a) {
   extern __shared__ unsigned hist[];  // [nbm + 1] block counts | [nbm + 1] reserved run starts
   if (prio) __builtin_amdgcn_s_setprio(2);  // engine option slot_prio (pipelined stream)
   unsigned* run = hist + nbm + 1;
@@ -271,7 +360,12 @@ __global__ void __launch_bounds__(kST) feat_slot_kernel(CardPages P, unsigned lo
   if (i < n) {
     const Txn t = src.get(i);  // in flight with the probe
     const long long s = card_slot(K, P, mask, src.get_key(i));
-    store_prep(prep + i, make_prep(t, merchants, nm));
+    if (row_a) {  // split rows: the 32-B prep the card work reads, the card-independent row finished here
+      store_prep32(reinterpret_cast<Prep32*>(prep) + i, t);
+      store_row_a(row_a + 2 * i, make_prep(t, merchants, nm));
+    } else {
+      store_prep(prep + i, make_prep(t, merchants, nm));
+    }
     if (s < 0) {
       atomicOr(err, 1u);
       slot[i] = 0xffffffffu;
@@ -442,6 +536,7 @@ struct Outputs {
   bool compact;  // vec rows are the compact form (64-B rows, fd_internal.h kCompactWidth: the fused pipeline's ensemble reads them)
 };
 
+template <bool SPLIT = false>
 __device__ __forceinline__ void emit(const Outputs& o, int64_t i, const double* r, long long s5, float o1, float dv0) {
   if (o.sat && r[11] >= (double)o.K) atomicAdd(o.sat, 1ull);  // rare: the card's last K events all within 24 h
   if (o.raw) {
@@ -449,7 +544,10 @@ __device__ __forceinline__ void emit(const Outputs& o, int64_t i, const double* 
 #pragma unroll
     for (int c = 0; c < FD_RAW_FEATURES / 2; ++c) ro[c] = make_double2(r[2 * c], r[2 * c + 1]);
   }
-  write_vector(r, o1, dv0, o.vec + (size_t)i * (o.compact ? kCompactWidth : FD_VECTOR_WIDTH), o.compact);
+  if (SPLIT)
+    store_row_b(reinterpret_cast<uint4*>(o.vec) + 2 * i, r);
+  else
+    write_vector(r, o1, dv0, o.vec + (size_t)i * (o.compact ? kCompactWidth : FD_VECTOR_WIDTH), o.compact);
   if (o.vel5) o.vel5[i] = (double)s5 / 100.0;
 }
 
@@ -676,7 +774,7 @@ struct BucketArgs {
   CardPages P;  // header + ring per card slot
   int K;
   int64_t n;
-  const Prep* prep;  // [n] in arrival order (feat_slot_kernel)
+  const Prep* prep;  // [n] in arrival order (feat_slot_kernel); split rows: Prep32 records
   Outputs out;
   unsigned* fill;                     // keys per bucket (this batch); reset here for the next batch
   const unsigned long long* pairs;    // [NB][C] bucket regions
@@ -707,6 +805,12 @@ struct GatherArgs {
   unsigned* err;
 };
 
+// transaction i's prep record as the card work reads it (split rows: the 32-B form)
+template <bool SPLIT>
+__device__ __forceinline__ Prep fetch_prep(const BucketArgs& a, int64_t i) {
+  return SPLIT ? load_prep32(reinterpret_cast<const Prep32*>(a.prep) + i) : load_prep(a.prep + i);
+}
+
 // a card's bucket in gather mode: every transaction of a card in one bucket, buckets filled evenly
 __device__ __forceinline__ unsigned gather_bucket(unsigned long long key, unsigned nbm) {
   return (unsigned)(mix64(key ^ 0x9E3779B97F4A7C15ull) >> 32) & nbm;
@@ -721,17 +825,17 @@ __device__ __forceinline__ int first_pos(bool spread) {
   return spread ? (((t & 63) << 2) | (t >> 6)) : t;
 }
 
-template <int MODE, typename KeyT = unsigned long long>
+template <int MODE, bool SPLIT, typename KeyT = unsigned long long>
 __device__ void process_short(const BucketArgs& a, unsigned s, const KeyT* keys, int len) {
   CardHeader* h = a.P.hdr(s);
   CardRegs c;
   Profile p;
-  Prep t = load_prep(a.prep + (unsigned)keys[0]);  // in flight with the header
+  Prep t = fetch_prep<SPLIT>(a, (unsigned)keys[0]);  // in flight with the header
   load_card(h, c, p);
   RingEvent* rg = a.P.ring(s);
   for (int q = 0; q < len; ++q) {
     const int64_t i = (int64_t)(unsigned)keys[q];
-    if (q > 0) t = load_prep(a.prep + i);
+    if (q > 0) t = fetch_prep<SPLIT>(a, i);
     double r[FD_RAW_FEATURES];
     base_raw(t, p, r);
     if (q == 0) FD_CSTAMP(0);
@@ -739,7 +843,7 @@ __device__ void process_short(const BucketArgs& a, unsigned s, const KeyT* keys,
     velocity_step<MODE>(c, rg, a.K, t.ts, t.cents, cw, sw);
     if (q == 0) FD_CSTAMP(1);
     velocity_raw(cw, sw, r);
-    emit(a.out, i, r, sw[0], t.o1, t.dv0);
+    emit<SPLIT>(a.out, i, r, sw[0], t.o1, t.dv0);
     if (a.out.S) seq_step(a.out, s, c.flags, i, r, q == len - 1);
     if (q == 0) FD_CSTAMP(2);
   }
@@ -778,7 +882,7 @@ __device__ void block_scan_max(int* v) {  // inclusive, kBT entries
   }
 }
 
-template <int MODE>
+template <int MODE, bool SPLIT>
 __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned long long* keys, int L, LongLds& sm) {
   const int tid = threadIdx.x, K = a.K, S = a.out.S;
   CardHeader* h = a.P.hdr(s);
@@ -822,7 +926,7 @@ __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned lon
     const int64_t i = act ? (int64_t)(unsigned)keys[t0 + j] : 0;
     Prep t{};
     if (act) {
-      t = load_prep(a.prep + i);
+      t = fetch_prep<SPLIT>(a, i);
       sm.ev_ts[K + j] = t.ts;
       sm.ev_c[K + j] = t.cents;
     }
@@ -875,7 +979,7 @@ __device__ void process_long(const BucketArgs& a, unsigned s, const unsigned lon
     if (act) {
       base_raw(t, p, r);
       velocity_raw(cw, sw, r);
-      emit(a.out, i, r, sw[0], t.o1, t.dv0);
+      emit<SPLIT>(a.out, i, r, sw[0], t.o1, t.dv0);
       if (S)
         for (int c = 0; c < kSeqInput; ++c) sm.seqb[(S + j) * kSeqInput + c] = seq_input(r[c]);
     }
@@ -1086,7 +1190,7 @@ __device__ void rank_sort_split(unsigned long long* k, int m, int* rk) {
 }
 
 // m keys (slot << 32 | arrival index) already in LDS skeys[0, m): sort, then process every segment
-template <int MODE>
+template <int MODE, bool SPLIT>
 __device__ void process_sorted(const BucketArgs& a, unsigned long long* skeys, int m, LongLds& sm, int* long_list,
                                int* n_long) {
   if (threadIdx.x == 0) *n_long = 0;
@@ -1111,7 +1215,7 @@ __device__ void process_sorted(const BucketArgs& a, unsigned long long* skeys, i
       long_list[atomicAdd(n_long, 1)] = pos;
       continue;
     }
-    process_short<MODE>(a, s, skeys + pos, len);
+    process_short<MODE, SPLIT>(a, s, skeys + pos, len);
   }
 #ifdef FD_FOREST_PROFILE
   if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)
@@ -1125,11 +1229,11 @@ __device__ void process_sorted(const BucketArgs& a, unsigned long long* skeys, i
     const unsigned s = (unsigned)(skeys[pos] >> 32);
     int len = 1;  // every thread finds the same length
     while (pos + len < m && (unsigned)(skeys[pos + len] >> 32) == s) ++len;
-    process_long<MODE>(a, s, skeys + pos, len, sm);
+    process_long<MODE, SPLIT>(a, s, skeys + pos, len, sm);
   }
 }
 
-template <int MODE, bool GATHER = false>
+template <int MODE, bool GATHER = false, bool SPLIT = false>
 __device__ void bucket_body(const BucketArgs& a, const int b, unsigned long long* skeys, LongLds& sm, int* long_list,
                             int& n_long, int& chunk_m, const GatherArgs* ga = nullptr) {
   unsigned* bins = reinterpret_cast<unsigned*>(skeys + kChunkCap);
@@ -1185,7 +1289,7 @@ __device__ void bucket_body(const BucketArgs& a, const int b, unsigned long long
       }
       __syncthreads();
     }
-    process_sorted<MODE>(a, skeys, chunk_m, sm, long_list, &n_long);
+    process_sorted<MODE, SPLIT>(a, skeys, chunk_m, sm, long_list, &n_long);
     __syncthreads();
     if (threadIdx.x == 0 && b == 0) a.ovf_cnt[a.par ^ 1] = 0u;  // as below: the next batch's overflow list
     return;
@@ -1207,7 +1311,7 @@ __device__ void bucket_body(const BucketArgs& a, const int b, unsigned long long
         if (a.ovf_b[q] == (unsigned)b) skeys[atomicAdd(&chunk_m, 1)] = a.ovf_key[q];
     }
     __syncthreads();
-    process_sorted<MODE>(a, skeys, (int)m, sm, long_list, &n_long);
+    process_sorted<MODE, SPLIT>(a, skeys, (int)m, sm, long_list, &n_long);
   } else {
     // Oversized bucket (a hot card): pass by arrival range so each pass's keys fit the LDS sort and every
     // card's transactions of pass c precede its transactions of pass c + 1 (state carried in HBM; the
@@ -1267,7 +1371,7 @@ __device__ void bucket_body(const BucketArgs& a, const int b, unsigned long long
         if (i >= i_lo && i < i_hi) skeys[atomicAdd(&chunk_m, 1)] = k;
       }
       __syncthreads();
-      process_sorted<MODE>(a, skeys, chunk_m, sm, long_list, &n_long);
+      process_sorted<MODE, SPLIT>(a, skeys, chunk_m, sm, long_list, &n_long);
       __syncthreads();
       lo = hi;
     }
@@ -1329,7 +1433,7 @@ constexpr unsigned kHashEmpty = 0xffffffffu;
 constexpr int kLeadBit = 1 << 30;  // rk[pos]: the table entry of the key at pos, | kLeadBit where it inserted the card
 static_assert(kHashCap == kBT, "one table entry per thread at initialisation");
 
-template <int MODE>
+template <int MODE, bool SPLIT>
 __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, BucketScratch* scratch) {
   // 6 KiB: beside a running ensemble_kernel workgroup (148 of the CU's 160 KiB) with room to spare
   __shared__ __attribute__((aligned(16))) unsigned long long skeys[kLeanCap];
@@ -1385,7 +1489,7 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
   }
   if (slow) {
     BucketScratch& w = scratch[b];
-    bucket_body<MODE>(a, b, w.keys, w.sm, w.long_list, w.n_long, w.chunk_m);
+    bucket_body<MODE, false, SPLIT>(a, b, w.keys, w.sm, w.long_list, w.n_long, w.chunk_m);
     return;
   }
   if (hashed) {
@@ -1395,7 +1499,7 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
       const int e = rk[pos];
       const unsigned c = hcnt[e & (kHashCap - 1)];
       if (c == 1u) {
-        process_short<MODE>(a, s, skeys + pos, 1);
+        process_short<MODE, SPLIT>(a, s, skeys + pos, 1);
         continue;
       }
       if (!(e & kLeadBit)) continue;  // the thread whose key inserted the card processes all of its transactions
@@ -1414,7 +1518,7 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
         }
         pool[base + y + 1] = v;
       }
-      process_short<MODE>(a, s, pool + base, w);
+      process_short<MODE, SPLIT>(a, s, pool + base, w);
     }
   } else {
     for (int pos = first_pos(a.spread); pos < (int)m; pos += kBT) {
@@ -1422,7 +1526,7 @@ __global__ void __launch_bounds__(kBT) feat_bucket_lean_kernel(BucketArgs a, Buc
       if (pos > 0 && (unsigned)(skeys[pos - 1] >> 32) == s) continue;
       int len = 1;
       while (pos + len < (int)m && (unsigned)(skeys[pos + len] >> 32) == s) ++len;
-      process_short<MODE>(a, s, skeys + pos, len);
+      process_short<MODE, SPLIT>(a, s, skeys + pos, len);
     }
   }
 #ifdef FD_FOREST_PROFILE
@@ -1942,11 +2046,18 @@ namespace {
 // card updates, pipelined stream) while the slot pass runs ahead
 void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, double* d_raw, float* d_seq,
                     double* d_vel5, hipStream_t stream = nullptr, bool lean = false, int set = 0,
-                    hipEvent_t before_buckets = nullptr, bool compact = false,
+                    hipEvent_t before_buckets = nullptr, int compact = 0,
                     unsigned long long* d_seq_desc = nullptr) {
   CardStore& st = e.state;
   CardStore::GroupScratch& g = st.gs[set];
   const hipStream_t s = stream ? stream : e.stream;
+  // split rows (compact 2): RowA at d_vec, RowB after the batch's n RowAs (32 B each); the pipelined stream's lean
+  // bucket pass only, and no LSTM history (seq_step reads the raw features the split card work does not form)
+  const bool split = compact == 2;
+  FD_REQUIRE(!split || (lean && st.S == 0 && !d_raw && !d_seq && !d_vel5), FD_ERR_INVALID_ARG,
+             "internal: split rows need the lean bucket pass and no raw / sequence outputs");
+  uint4* row_a = split ? reinterpret_cast<uint4*>(d_vec) : nullptr;
+  float* vec_out = split ? d_vec + (size_t)n * 8 : d_vec;
   FD_REQUIRE(n <= (int64_t)kMaxBins * kChunkCap, FD_ERR_INVALID_ARG, "micro-batch larger than 16M transactions");
   g.slot.ensure((size_t)n * 4);
   g.prep.ensure((size_t)n * sizeof(Prep));
@@ -1963,7 +2074,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   // the slot pass on the engine's slot stream when the pipelined step set one (option slot_stream), else on s
   const hipStream_t ss = e.slot_pass_stream ? e.slot_pass_stream : s;
   // latency batches: the slot pass inside the bucket kernel (no slot launch; its probes in the card loop's launch)
-  const bool gather = st.slot_gather && !lean && n <= (int64_t)kChunkCap && ss == s;
+  const bool gather = st.slot_gather && !lean && n <= (int64_t)kChunkCap && ss == s;  // (never with split: lean)
   Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_FEATURES) : nullptr;
   if (ev) FD_HIP(hipEventRecord(ev->a, ss));
   if (!gather) hipLaunchKernelGGL(feat_slot_kernel, dim3((unsigned)((n + kST - 1) / kST)), dim3(kST), 2 * nb * sizeof(unsigned),
@@ -1971,7 +2082,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
                      st.merchants.as<const Merchant>(), (int)st.n_merchants, nb - 1, C, g.slot.as<unsigned>(),
                      g.prep.as<Prep>(), g.bucket_fill.as<unsigned>(), g.pairs.as<unsigned long long>(),
                      g.ovf_cnt.as<unsigned>() + par, g.ovf_key.as<unsigned long long>(), g.ovf_b.as<unsigned>(),
-                     st.err.as<unsigned>(), lean && st.slot_prio ? 1 : 0);
+                     st.err.as<unsigned>(), lean && st.slot_prio ? 1 : 0, row_a);
   FD_HIP(hipGetLastError());
   if (ss != s) {
     FD_HIP(hipEventRecord(e.slot_pass_ev, ss));
@@ -2004,8 +2115,8 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   a.K = st.K;
   a.n = n;
   a.prep = g.prep.as<const Prep>();
-  a.out = Outputs{d_vec, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S, d_seq_desc,
-                  st.mode == FD_WINDOW_SLIDING ? st.sat.as<unsigned long long>() : nullptr, st.K, compact};
+  a.out = Outputs{vec_out, d_raw, d_vel5, d_seq, st.S ? st.seq.as<float>() : nullptr, st.S, d_seq_desc,
+                  st.mode == FD_WINDOW_SLIDING ? st.sat.as<unsigned long long>() : nullptr, st.K, compact != 0};
   a.fill = g.bucket_fill.as<unsigned>();
   a.pairs = g.pairs.as<const unsigned long long>();
   a.C = C;
@@ -2036,10 +2147,16 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
   if (lean) {
     st.bucket_scr.ensure((size_t)nb * sizeof(BucketScratch));
     BucketScratch* scr = st.bucket_scr.as<BucketScratch>();
-    if (st.mode == FD_WINDOW_SLIDING)
-      hipLaunchKernelGGL(feat_bucket_lean_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), 0, s, a, scr);
-    else
-      hipLaunchKernelGGL(feat_bucket_lean_kernel<FD_WINDOW_REDIS_COMPAT>, dim3(nb), dim3(kBT), 0, s, a, scr);
+    if (split) {
+      if (st.mode == FD_WINDOW_SLIDING)
+        hipLaunchKernelGGL((feat_bucket_lean_kernel<FD_WINDOW_SLIDING, true>), dim3(nb), dim3(kBT), 0, s, a, scr);
+      else
+        hipLaunchKernelGGL((feat_bucket_lean_kernel<FD_WINDOW_REDIS_COMPAT, true>), dim3(nb), dim3(kBT), 0, s, a, scr);
+    } else if (st.mode == FD_WINDOW_SLIDING) {
+      hipLaunchKernelGGL((feat_bucket_lean_kernel<FD_WINDOW_SLIDING, false>), dim3(nb), dim3(kBT), 0, s, a, scr);
+    } else {
+      hipLaunchKernelGGL((feat_bucket_lean_kernel<FD_WINDOW_REDIS_COMPAT, false>), dim3(nb), dim3(kBT), 0, s, a, scr);
+    }
   } else if (gather) {
     if (st.mode == FD_WINDOW_SLIDING)
       hipLaunchKernelGGL(feat_bucket_gather_kernel<FD_WINDOW_SLIDING>, dim3(nb), dim3(kBT), lds, s, a, ga);
@@ -2057,7 +2174,7 @@ void launch_grouped(Engine& e, const TxnSrc& src, int64_t n, float* d_vec, doubl
 }  // namespace
 
 void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, double* d_raw, float* d_seq,
-                     double* d_vel5, hipStream_t stream, bool lean, int set, hipEvent_t before_buckets, bool compact,
+                     double* d_vel5, hipStream_t stream, bool lean, int set, hipEvent_t before_buckets, int compact,
                      unsigned long long* d_seq_desc) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
@@ -2076,7 +2193,7 @@ void launch_features(Engine& e, const fd_txn_batch& t, int64_t n, float* d_vec, 
 }
 
 void launch_features_records(Engine& e, const void* d_records, int64_t n, float* d_vec, float* d_seq,
-                             hipStream_t stream, bool lean, int set, hipEvent_t before_buckets, bool compact) {
+                             hipStream_t stream, bool lean, int set, hipEvent_t before_buckets, int compact) {
   CardStore& st = e.state;
   FD_REQUIRE(st.ready, FD_ERR_NOT_LOADED, "card state not initialised (fd_state_init)");
   FD_REQUIRE(d_vec != nullptr && (n == 0 || d_records != nullptr), FD_ERR_INVALID_ARG, "null records / output");

@@ -191,6 +191,7 @@ def test_config4_full_size_warm_pipelined():
         got = []
         sat0 = eng.counter("window_saturated")
         c0 = eng.counter("pipelined_compact_batches")
+        q0 = eng.counter("pipelined_split_batches")
         s0 = eng.counter("pipelined_slot_stream_batches")
         for b in range(P):  # back to back: no sync between the pipelined steps
             if b < P - 1:  # the variant the bench times: no vectors requested -> compact vectors, fused kernel
@@ -203,6 +204,7 @@ def test_config4_full_size_warm_pipelined():
             got.append((vec, mp, out))
         torch.cuda.synchronize()
         assert eng.counter("pipelined_compact_batches") - c0 == P - 1
+        assert eng.counter("pipelined_split_batches") - q0 == P - 1  # split rows (the engine's default form)
         assert eng.counter("pipelined_slot_stream_batches") - s0 == P  # 2^27 slots: the slot pass on its own stream
         o = OracleFeatureState(1 << 22, 1, K)
         pr = wk["profiles"]

@@ -130,8 +130,10 @@ def test_pipelined_compact_rows_bit_identical_k64(world):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("opts", [(("ensemble_bin_global", 1),), (("lean_group", 0),), (("lean_group", 1),),
-                                  (("ensemble_bin_global", 1), ("ensemble_chunks", 2))],
-                         ids=["bin_global", "lean_group0", "lean_group1", "bin_global_compact_chunks"])
+                                  (("ensemble_bin_global", 1), ("ensemble_chunks", 2)), (("compact_vectors", 1),),
+                                  (("compact_vectors", 1), ("lean_group", 0)), (("compact_vectors", 0),)],
+                         ids=["bin_global", "lean_group0", "lean_group1", "bin_global_compact_chunks", "compact64",
+                              "compact64_lean_group0", "full_rows"])
 def test_pipelined_engine_options(world, opts):
     """the compact path's A/B options (binning of the fused kernel's rows, the lean kernel's card grouping): the
     pipelined stream's outputs and end state equal the serial full-vector path's under every one"""

@@ -303,3 +303,144 @@ def test_count_timeout_aborts_the_communicators():
                 os.environ[k] = v
         if not closed:
             e.close()
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# the headline's shapes: BASELINE configs[3]'s models and ring at world 8
+
+HL_USERS, HL_STEPS, HL_B, HL_K = 200_000, 4, 40960, 64
+
+
+@pytest.mark.timeout(900)
+def test_world8_headline_shapes_warm_matches_oracle():
+    """World 8 over the loopback at the headline's shapes: XGBoost 500 x depth 8 + IsolationForest 100 over the
+    engine's 64-wide scoring layout, K = 64 ring events per card, 40,960 transactions per rank per step (so each owner
+    receives ~40 k, above the fused ensemble kernel's 128 tiles: below them an owner takes the tree-split latency
+    path), every step prefetching the next (as bench.py's config-4 ranks run it). 200 k cards see ~6.5 transactions
+    each over the stream's ~24 h, so from the second step on the 5 min / 1 h / 24 h windows hold events (warm). The timed variant's legs:
+    every step's fraud probability / confidence / decision / risk against the oracle chain over the global arrival
+    order (compact split rows into the fused kernel on each owner), then each owner's card state after the stream
+    through a vector probe (engine.features on the cards it owns, bit-exact against the oracle's vectors). Each
+    step issues at most 2 x 7 + 2 x 7 + 1 RCCL operations per rank: its own share of the records and results is a
+    device copy, its counts one all-gather (WindowProcessor.java:44,63 keyBy)."""
+    import threading
+
+    import torch
+
+    import oracle
+    from fdengine import FraudEngine, iforest_from_sklearn, synth, xgboost_from_json_doc
+    from fdengine._native import TXN_FIELDS
+    from fdengine.engine import shard_of
+    from fdengine.sharding import EngineShardBackend, ShardedScorer, owned_mask
+    from oracle.features_c import OracleFeatureState
+    assert LOOPBACK.exists(), "tests/native/build/librccl_loopback.so missing (fdengine/build.py build_test_libs)"
+    world = 8
+    pop = synth.population(HL_USERS, 5000, seed=301)
+    total = world * HL_B * HL_STEPS
+    rate = total / 86400.0  # the whole stream spans ~24 h of event time
+    glob = synth.txn_stream(pop, total + 4096, seed=302, rate_per_s=rate)
+    # rank r's step s is the slice of the global arrival order [(s * world + r) * B, ... + B): the order every card
+    # sees is step-major, then rank, then index — the oracle replays exactly that
+    def part(s, r):
+        a = (s * world + r) * HL_B
+        return {k: v[a:a + HL_B] for k, v in glob.items()}
+    probe = {k: v[total:] for k, v in glob.items()}
+    warm = OracleFeatureState(1 << 19, 1, HL_K)
+    U, M = pop["users"], pop["merchants"]
+    warm.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+    warm.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+    _, X = warm.run({k: v[:16384] for k, v in glob.items()})
+    del warm
+    xgb = xgboost_from_json_doc(synth.xgboost_doc(500, 8, 64, X[-8192:], seed=303))
+    ifm = iforest_from_sklearn(synth.isolation_forest(X[-8192:].astype(np.float64), n_estimators=100))
+    path = str(LOOPBACK)
+    ids = (FraudEngine.comm_unique_id(path), FraudEngine.comm_unique_id(path))
+    engines = []
+    for r in range(world):
+        e = FraudEngine(0)
+        own = owned_mask(U["key"], r, world)
+        e.state_init(1 << 16, 1, HL_K)
+        e.load_users(U["key"][own], U["avg_amount"][own], U["account_age_days"][own], U["device_fp"][own])
+        e.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+        e.load_forest(0, xgb)
+        e.load_forest(1, ifm)
+        engines.append(e)
+    dev = [[{f: torch.from_numpy(np.ascontiguousarray(part(s, r)[f])).cuda() for f in TXN_FIELDS}
+            for s in range(HL_STEPS)] for r in range(world)]
+    torch.cuda.synchronize()
+    params = FraudEngine.blend_params([0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
+    results, errors, probes = [None] * world, [None] * world, [None] * world
+    bar = threading.Barrier(world)
+
+    def rank_main(r):
+        try:
+            torch.cuda.set_device(0)
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                be = EngineShardBackend(engines[r], params, [0, 1], pipelined=True)
+                sc = ShardedScorer(be, r, world, native=True, comm=(path, ids))
+                ops0, spl0 = engines[r].counter("rccl_ops"), engines[r].counter("pipelined_split_batches")
+                outs = []
+                for s in range(HL_STEPS):
+                    pre = (dev[r][s + 1], HL_B) if s + 1 < HL_STEPS else None
+                    out = sc.step(dev[r][s], HL_B, prefetch=pre)
+                    host = [torch.empty(o.shape, dtype=o.dtype, pin_memory=True) for o in out]
+                    for h, o in zip(host, out):
+                        h.copy_(o, non_blocking=True)
+                    outs.append(host)
+                st.synchronize()
+                engines[r].sync()
+                ops = engines[r].counter("rccl_ops") - ops0
+                split = engines[r].counter("pipelined_split_batches") - spl0
+                be.close_comm()
+            bar.wait(timeout=120)  # every rank's exchanges are done before any probe mutates its card state
+            mine = shard_of(probe["card_key"], world) == r
+            probes[r] = (mine, engines[r].features({k: v[mine] for k, v in probe.items()}))
+            results[r] = (np.concatenate([np.stack([h[0].numpy(), h[1].numpy(), h[2].numpy().astype(np.float64),
+                                                    h[3].numpy().astype(np.float64)]) for h in outs], axis=1),
+                          ops, split)
+        except BaseException as ex:  # reported by the main thread
+            errors[r] = ex
+
+    try:
+        threads = [threading.Thread(target=rank_main, args=(r,), daemon=True) for r in range(world)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=600)
+        if any(t.is_alive() for t in threads):
+            engines = []
+            raise AssertionError("a rank thread hung")
+        for r, ex in enumerate(errors):
+            if ex is not None:
+                raise AssertionError(f"rank {r} failed: {ex!r}") from ex
+    finally:
+        for e in engines:
+            e.close()
+    for r in range(world):
+        assert results[r][1] <= HL_STEPS * (2 * (world - 1) + 2 * (world - 1) + 1), results[r][1]
+        assert results[r][2] == HL_STEPS, results[r][2]  # every owner batch scored from split rows
+    st = OracleFeatureState(1 << 19, 1, HL_K)
+    st.load_users(U["key"], U["avg_amount"], U["account_age_days"], U["device_fp"])
+    st.load_merchants(M["fraud_rate"], M["risk_multiplier"])
+    raws = []
+    for s in range(HL_STEPS):
+        for r in range(world):
+            raw, V = st.run(part(s, r), want_raw=True)
+            raws.append(raw)
+            px, _, _ = oracle.xgb_predict(xgb, V)
+            pi, _, _ = oracle.iforest_predict(ifm, V)
+            fp, conf, dec, risk = oracle.blend_weighted(np.stack([px.astype(np.float64), pi]),
+                                                        [0.4 / 0.45, 0.05 / 0.45], [1.0, 0.5])
+            g = results[r][0][:, s * HL_B:(s + 1) * HL_B]
+            assert np.abs(g[0] - fp).max() <= 1e-5 and np.abs(g[1] - conf).max() <= 1e-5, (s, r)
+            near = np.abs(conf - 0.7) < 1e-6
+            for thr in (0.3, 0.6, 0.8, 0.95):
+                near |= np.abs(fp - thr) < 1e-6
+            assert ((g[2] == dec) | near).all() and ((g[3] == risk) | near).all(), (s, r)
+    allraw = np.concatenate(raws[world:])  # from the second step on
+    assert (allraw[:, 11] > 0).mean() > 0.5 and (allraw[:, 10] > 0).mean() > 0.02  # warm 24 h / 1 h windows
+    _, Vp = st.run(probe, want_raw=False)
+    for r in range(world):
+        mine, got = probes[r]
+        np.testing.assert_array_equal(got, Vp[mine])
