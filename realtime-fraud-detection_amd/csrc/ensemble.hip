@@ -84,32 +84,30 @@ size_t ens_lds(int nf, bool wide) {
 }
 
 struct EnsArgs {
+  // Field order: what a wave reads before its first LDS-DMA goes out (rows, pass 0's table image, chunk 0) and the
+  // other scalars first, packed into the first few 64-B scalar-cache lines; the per-feature / per-pass tables after
+  // them (round 6: the prologue's kernel-argument round trips)
   const float* X;
   int64_t n;
   int ld, nf;
   const float* thr;
-  int thr_off[kMaxFeatures + 1];  // per-feature table offsets into thr (kernel arguments: scalar loads)
   int vec4;                       // rows 16-B aligned (ld % 4 == 0, aligned X): float4 row loads
   int compact;                    // 1: X rows are the compact 64-B rows (fd_internal.h), binned here; 2: split rows
                                   // (RowA [n] at X, RowB [n] after it, 32 B each: features.hip, load_split)
-  uint16_t cbin[kMaxFeatures];    // compact mode: the bins of the constant slots (0 or 0.5), per plan
-  alignas(4) uint16_t lut[8 * 32];  // compact mode: [kIntSlots][kLutN] bins of the small-integer slots' values 0..31
-
   int owner_fixed;                // chunk owner: tree group 0 (the oldest waves: highest issue priority), else rotating
   int prio;                       // issue priority 2 above the co-running feature kernels (engine option ensemble_prio)
   int n_pass;
-  int pass_f[kMaxPass + 1];
+  int pad0;
   unsigned long long pass_global;  // bit p: pass p bins from global memory (its table does not fit LDS)
   const char* img;                 // the passes' padded table images (thr_pad layout), 1 KiB pieces
-  int img_off[kMaxPass + 1];       // pass p's image: bytes [img_off[p], img_off[p + 1]) of img
   const char* nodes[2];
   int n_chunks[2];
   int stride[2];
   float base_margin;
+  int pad1;
   double if_offset, if_denom;
   int pos[2];   // blend position (present-model order) of forest A / B
   int mcol[2];  // model-probability column (caller's model index) of forest A / B
-  BlendConsts blend;
   double* mp;
   double* fp;
   double* conf;
@@ -117,6 +115,12 @@ struct EnsArgs {
   uint8_t* risk;
   const RouteRecord* rec;
   ResultRecord* res;
+  int pass_f[kMaxPass + 1];
+  int img_off[kMaxPass + 1];       // pass p's image: bytes [img_off[p], img_off[p + 1]) of img
+  int thr_off[kMaxFeatures + 1];  // per-feature table offsets into thr (kernel arguments: scalar loads)
+  uint16_t cbin[kMaxFeatures];    // compact mode: the bins of the constant slots (0 or 0.5), per plan
+  alignas(4) uint16_t lut[8 * 32];  // compact mode: [kIntSlots][kLutN] bins of the small-integer slots' values 0..31
+  BlendConsts blend;
 #ifdef FD_FOREST_PROFILE
   int prof_slot;  // which of the kEprofSlots profile buffers this launch writes (launch count mod kEprofSlots)
   int clk_slot;   // this launch's record in g_eclk (launch count mod kEclkSlots)
