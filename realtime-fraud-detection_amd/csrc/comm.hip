@@ -180,18 +180,19 @@ void comm_destroy(Engine& e) {
   c.fwd = c.back = nullptr;
   if (!drained) {
     if (!fwd_drained) c.x_fwd = nullptr;  // a stream still running work is not destroyed either
-    for (int s = 0; s < 2; ++s) c.rec[s].ptr = c.cnt[s].ptr = c.res[s].ptr = nullptr, c.h_cnt[s] = nullptr;
-    for (int q = 0; q < ShardComm::kInbox; ++q) c.inbox[q].ptr = nullptr;
+    for (int s = 0; s < 2; ++s) c.rec[s].ptr = c.cnt[s].ptr = nullptr, c.h_cnt[s] = nullptr;
+    for (int q = 0; q < ShardComm::kInbox; ++q) c.inbox[q].ptr = c.res[q].ptr = nullptr;
     c.back_buf.ptr = nullptr;
     c.route_blk.ptr = nullptr;
   }
   for (int s = 0; s < 2; ++s) {
-    for (auto* b : {&c.rec[s], &c.cnt[s], &c.res[s]}) b->release();
+    for (auto* b : {&c.rec[s], &c.cnt[s]}) b->release();
     if (c.h_cnt[s]) (void)hipHostFree(c.h_cnt[s]);
     c.h_cnt[s] = c.d_hcnt[s] = nullptr;
   }
   for (int q = 0; q < ShardComm::kInbox; ++q) {
     c.inbox[q].release();
+    c.res[q].release();
     if (c.in_ev[q]) (void)hipEventDestroy(c.in_ev[q]);
     if (c.inbox_ev[q]) (void)hipEventDestroy(c.inbox_ev[q]);
     c.in_ev[q] = c.inbox_ev[q] = nullptr;
@@ -348,7 +349,7 @@ void comm_forward_group(Engine& e, int s, const fd_txn_batch* next, int64_t next
   c.inbox_of[s] = q;
   if (c.inbox_live[q]) FD_HIP(hipStreamWaitEvent(c.x_fwd, c.inbox_ev[q], 0));
   c.inbox[q].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(RouteRecord));
-  c.res[s].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(ResultRecord));
+  c.res[q].ensure_headroom((size_t)std::max<int64_t>(m, 1) * sizeof(ResultRecord));
   check(R, R.group_start(), "ncclGroupStart");
   exchange_ops(e, false, c.x_fwd, c.rec[s].ptr, send, c.inbox[q].ptr, recv, sizeof(RouteRecord));
   if (next && !c.count_gather) counts_ops(e, ns);

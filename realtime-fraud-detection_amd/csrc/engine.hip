@@ -1066,7 +1066,8 @@ pipe_out_copy_kernel(const double* __restrict__ fp, const double* __restrict__ c
 static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* slots, const double* const* ext_probs,
                       const uint8_t* present, const fd_txn_batch* txns, const void* records, int64_t n,
                       float* d_vectors, double* d_model_probs, double* d_fraud_prob, double* d_confidence,
-                      uint8_t* d_decision, uint8_t* d_risk, void* d_results, void* input_ready) {
+                      uint8_t* d_decision, uint8_t* d_risk, void* d_results, void* input_ready,
+                      bool results_in_place = false) {
   for (int k = 0; k < 2; ++k)
     if (!e.pipe_stream[k]) e.pipe_stream[k] = fd::make_stream(e.stream_prio >= 1 ? 1 : 0);
   if (e.pipe_slot_mode < 0)  // auto: where the feature chain outlasts the fused kernel (random card traffic over a
@@ -1157,7 +1158,11 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   // always stage the four columns (the result records are packed from them when the fused kernel does not apply).
   const int n_mp = d_model_probs ? params->n_models : 0;
   const size_t n8 = (size_t)n * 8, a8 = ((size_t)n + 7) & ~(size_t)7;
-  const size_t rbytes = records ? (size_t)n * sizeof(fd::ResultRecord) : 0;
+  // results_in_place (fd_sharded_step: d_results is the engine's own res[q], free by the step's event order, see
+  // ShardComm::res): the scoring writes the result records there, no staging copy; otherwise they are staged and
+  // copied on the engine stream like the columns (a caller's buffer is written only in the engine stream's order)
+  const bool in_place = records && results_in_place;
+  const size_t rbytes = records && !in_place ? (size_t)n * sizeof(fd::ResultRecord) : 0;
   e.pipe_out[s].ensure((2 + (size_t)n_mp) * n8 + 2 * a8 + rbytes);
   char* so = e.pipe_out[s].as<char>();
   double* s_fp = reinterpret_cast<double*>(so);
@@ -1165,7 +1170,9 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   double* s_mp = n_mp ? reinterpret_cast<double*>(so + 2 * n8) : nullptr;
   uint8_t* s_dec = (d_decision || records) ? reinterpret_cast<uint8_t*>(so + (2 + (size_t)n_mp) * n8) : nullptr;
   uint8_t* s_risk = (d_risk || records) ? reinterpret_cast<uint8_t*>(so + (2 + (size_t)n_mp) * n8 + a8) : nullptr;
-  auto* s_res = records ? reinterpret_cast<fd::ResultRecord*>(so + (2 + (size_t)n_mp) * n8 + 2 * a8) : nullptr;
+  auto* s_res = !records ? nullptr
+                         : in_place ? static_cast<fd::ResultRecord*>(d_results)
+                                    : reinterpret_cast<fd::ResultRecord*>(so + (2 + (size_t)n_mp) * n8 + 2 * a8);
   if (e.pipe_copy_live[s]) FD_HIP(hipStreamWaitEvent(Sc, e.pipe_copy_ev[s], 0));
   ++e.pipe_iter;
   ++e.pipe_iter_total;
@@ -1188,6 +1195,10 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   FD_HIP(hipEventRecord(e.pipe_done_ev[s], Sc));
   e.pipe_done_live[s] = true;
   FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[s], 0));
+  if (in_place) {  // nothing to copy: the next use of staging slot s (batch i + 2) is on this batch's stream Sc
+    e.pipe_copy_live[s] = false;
+    return;
+  }
   hipLaunchKernelGGL(pipe_out_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e.stream, s_fp, s_conf,
                      s_dec, s_risk, s_mp, n_mp, n, records ? nullptr : d_fraud_prob, d_confidence, d_decision, d_risk,
                      d_model_probs, reinterpret_cast<const float4*>(vec), reinterpret_cast<float4*>(d_vectors),
@@ -1338,13 +1349,13 @@ int fd_sharded_step(fd_engine* eng, const fd_blend_params* params, const int32_t
   const int q = c.inbox_of[s];
   if (m)
     pipe_step(e, params, slots, nullptr, present, nullptr, c.inbox[q].ptr, m, nullptr, nullptr, nullptr, nullptr,
-              nullptr, nullptr, c.res[s].ptr, c.in_ev[q]);
-  FD_HIP(hipEventRecord(c.inbox_ev[q], e.stream));  // the engine stream has passed this batch's scoring
-  c.inbox_live[q] = true;
+              nullptr, nullptr, c.res[q].ptr, c.in_ev[q], /*results_in_place=*/true);
   L(5);
   // 4. results back (reversed splits) and into arrival order, on the engine stream
   c.back_buf.ensure_headroom((size_t)std::max<int64_t>(n, 1) * sizeof(fd::ResultRecord));
-  fd::comm_exchange(e, true, e.stream, c.res[s].ptr, recv, c.back_buf.ptr, send, sizeof(fd::ResultRecord));
+  fd::comm_exchange(e, true, e.stream, c.res[q].ptr, recv, c.back_buf.ptr, send, sizeof(fd::ResultRecord));
+  FD_HIP(hipEventRecord(c.inbox_ev[q], e.stream));  // the engine stream has passed this batch's results: inbox q
+  c.inbox_live[q] = true;                           // and res[q] are free for batch i + 3
   L(6);
   if (n) fd::launch_result_scatter(e, c.back_buf.ptr, n, d_fraud_prob, d_confidence, d_decision, d_risk);
   L(7);

@@ -430,14 +430,18 @@ struct ShardComm {
   void* fwd = nullptr;   // ncclComm_t: counts + records, on x_fwd
   void* back = nullptr;  // ncclComm_t: results, on the engine stream
   hipStream_t x_fwd = nullptr;
-  DeviceBuffer rec[2], cnt[2], res[2], back_buf;
+  DeviceBuffer rec[2], cnt[2], back_buf;
   // received records: a ring of three inboxes, so a batch's records exchange waits for the scoring three batches
   // back (long done) instead of two (still running beside the pipeline) — x_fwd is then never parked on an inbox,
   // and the next batch's counts queued behind the records are not held up either (the process has 4 hardware
   // queues for 4+ streams: a parked stream stalls whatever shares its queue)
   static constexpr int kInbox = 3;
   DeviceBuffer inbox[kInbox];
-  hipEvent_t in_ev[kInbox] = {}, inbox_ev[kInbox] = {};  // records arrived / the engine stream passed their scoring
+  // the owner's result records, by inbox: the fused kernel writes them in place (round 6: no staging copy). Batch i's
+  // scoring follows its records' arrival (in_ev), which followed x_fwd's wait for inbox_ev of batch i - 3 — recorded
+  // after that batch's results exchange — so res[q] is free when batch i writes it, with no event of its own
+  DeviceBuffer res[kInbox];
+  hipEvent_t in_ev[kInbox] = {}, inbox_ev[kInbox] = {};  // records arrived / the engine stream passed their results
   bool inbox_live[kInbox] = {};
   int inbox_next = 0;                                     // the next batch's inbox
   int inbox_of[2] = {0, 0};                               // slot s's batch's inbox

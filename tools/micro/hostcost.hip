@@ -83,6 +83,18 @@ int main() {
                 (void)hipEventRecord(ev_nofence, st);
                 (void)hipStreamWaitEvent(st2, ev_nofence, 0);
               }, st));
+  {
+    uint64_t* flag = nullptr;
+    CK(hipMalloc(&flag, 64));
+    CK(hipMemset(flag, 0, 64));
+    uint64_t v = 0;
+    std::printf("hipStreamWriteValue64               %.2f us\n",
+                per_call_us(N, [&] { (void)hipStreamWriteValue64(st, flag, ++v, 0); }, st));
+    std::printf("hipStreamWaitValue64 (satisfied)    %.2f us\n",
+                per_call_us(N, [&] { (void)hipStreamWaitValue64(st2, flag, 1, hipStreamWaitValueGte, ~0ull); }, st2));
+    CK(hipStreamSynchronize(st2));
+    CK(hipFree(flag));
+  }
   std::printf("hipMemcpyAsync D2D 256 KB           %.2f us\n",
               per_call_us(N, [&] { (void)hipMemcpyAsync(d + (1 << 17), d, 1 << 18, hipMemcpyDeviceToDevice, st); }, st));
   std::printf("hipFuncSetAttribute (max dyn LDS)   %.2f us\n", per_call_us(N, [&] {
