@@ -509,6 +509,18 @@ __global__ void __launch_bounds__(kEnsWG) ensemble_kernel(EnsArgs a) {
 #ifdef FD_FOREST_PROFILE
   const unsigned long long pr_rt0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz, one clock for the whole GPU
 #endif
+  // every kernel argument the prologue branches on or addresses with, in ONE round of scalar loads: left to itself
+  // the compiler issues them lazily, one dependent kernel-argument round trip per branch (five before the row loads
+  // went out). The empty asm needs them all in SGPRs at this point; later reads of the same fields reuse them.
+  {
+    const int k_prio = a.prio, k_compact = a.compact, k_npass = a.n_pass, k_vec4 = a.vec4, k_ld = a.ld;
+    const unsigned long long k_pg = a.pass_global;
+    const float* k_x = a.X;
+    const char* k_img = a.img;
+    const int k_i0 = a.img_off[0], k_i1 = a.img_off[1], k_f1 = a.pass_f[1];
+    asm volatile("" ::"s"(k_prio), "s"(k_compact), "s"(k_npass), "s"(k_vec4), "s"(k_ld), "s"(k_pg), "s"(k_x),
+                 "s"(k_img), "s"(k_i0), "s"(k_i1), "s"(k_f1), "s"(nA), "s"(G), "s"(a.n));
+  }
   // above the feature kernels of the next micro-batch that share the CU in the pipelined stream (priority 0):
   // this kernel is the stream's critical path, theirs is latency-bound with slack
   if (a.prio) __builtin_amdgcn_s_setprio(2);
