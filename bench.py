@@ -1480,7 +1480,7 @@ def _free_port() -> int:
 DIST_BACKEND = os.environ.get("FD_BENCH_DIST_BACKEND", "nccl")
 
 
-LAT_SPLIT = ("total", "submit", "native", "wait", "gpu")  # latency_split's per-sample columns (ms)
+LAT_SPLIT = ("total", "submit", "native", "wait", "gpu", "query_max", "gap_max")  # latency_split's columns (ms)
 
 
 def launch_ranks(n: int) -> int:
@@ -1631,11 +1631,22 @@ def main():
         ev.record(stream)
     torch.cuda.synchronize()
 
+    spin_stat = [0.0, 0.0]  # the last wait's longest hipEventQuery call, and its longest gap between two calls (s)
+
     def wait_done():
         if spin:
             lat_ev[2].record(stream)
-            while not lat_ev[2].query():
-                pass
+            q_max = g_max = 0.0
+            t_prev = time.perf_counter()
+            while True:
+                t_a = time.perf_counter()
+                done = lat_ev[2].query()
+                t_b = time.perf_counter()
+                q_max, g_max = max(q_max, t_b - t_a), max(g_max, t_a - t_prev)
+                t_prev = t_b
+                if done:
+                    break
+            spin_stat[0], spin_stat[1] = q_max, g_max
         else:
             stream.synchronize()
 
@@ -1659,7 +1670,8 @@ def main():
             n1 = eng.counter("pipelined_host_ns") if native else 0
             # per sample: total, host submit, of which inside the engine's native call, the wait, the GPU span
             # (stream events around the submission: from the stream reaching the step to its results copied)
-            split.append((c - a, b - a, (n1 - n0) * 1e-9, c - b, lat_ev[0].elapsed_time(lat_ev[1]) * 1e-3))
+            split.append((c - a, b - a, (n1 - n0) * 1e-9, c - b, lat_ev[0].elapsed_time(lat_ev[1]) * 1e-3,
+                          spin_stat[0], spin_stat[1]))
         lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
         latency_split.clear()
         if split:
@@ -1673,7 +1685,9 @@ def main():
                 "worst": [[int(q)] + [round(float(x), 4) for x in S[q]] for q in worst],
                 "columns": ["sample"] + list(LAT_SPLIT),
                 "basis": "isolated loop, per sample: total = host submit + wait; native = host ns inside the engine's "
-                         "pipelined call (counter pipelined_host_ns); gpu = stream events around the submission"})
+                         "pipelined call (counter pipelined_host_ns); gpu = stream events around the submission; "
+                         "query_max / gap_max = the wait's longest single hipEventQuery call and its longest time "
+                         "between two calls (the polling thread not running: host scheduling)"})
         p99 = float(np.percentile(lat_ms, 99))
         # the same with the input columns crossing PCIe from pinned host memory first (workloads that support it)
         lat_h2d = []
