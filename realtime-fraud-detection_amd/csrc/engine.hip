@@ -505,8 +505,11 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "ensemble_owner") {  // fused kernel: 0 owner tree group rotates per chunk; 1 always group 0
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_owner must be 0 or 1");
     e.ens_owner_fixed = value != 0;
-  } else if (k == "ensemble_prio") {  // fused kernel: 1 its waves issue above the co-running feature kernels'
-    // (s_setprio 2); 0 (default) the same priority (config 4: 0.0929 vs 0.0908-0.0918 ms, profiles/r04/prio)
+  } else if (k == "ensemble_prio") {  // fused kernel: 1 (default since round 6) its waves issue above the co-running
+    // feature kernels' (s_setprio 2); 0 the same priority. Round 4 measured 1 slower (0.0929 vs 0.0908-0.0918 ms,
+    // profiles/r04/prio); with round 6's split rows the feature chain is 20 us shorter than the fused kernel beside it
+    // and the critical path is the fused kernel: with feature_prio 0, the driver's command 0.0944 -> 0.0897 ms and 200
+    // steps 0.0826 -> 0.0812 (profiles/r06/prio)
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "ensemble_prio must be 0 or 1");
     e.ens_prio = value != 0;
   } else if (k == "ensemble_chunks") {  // fused kernel's chunk layout: 0 auto (compact once the engine has RCCL
@@ -582,8 +585,9 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
   } else if (k == "slot_prio") {  // pipelined stream: 1 the slot kernel's waves issue at priority 2, 0 (default) not
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "slot_prio must be 0 or 1");
     e.state.slot_prio = value != 0;
-  } else if (k == "feature_prio") {  // pipelined stream: 1 (default since round 5) the lean bucket kernel's waves issue
-    // at priority 2 (0.0857 -> 0.0843 ms per config-4 step at 200 steps), 0 at the default priority
+  } else if (k == "feature_prio") {  // pipelined stream: 1 the lean bucket kernel's waves issue at priority 2 (round 5's
+    // default: DESIGN §3, 0.0857 -> 0.0843 ms per config-4 step at 200 steps), 0 (default since round 6) at the
+    // default priority, below the fused kernel (ensemble_prio)
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "feature_prio must be 0 or 1");
     e.state.feat_prio = value != 0;
   } else if (k == "bucket_spread") {  // feature bucket pass, >= 8 k transactions: 1 (default) card segments

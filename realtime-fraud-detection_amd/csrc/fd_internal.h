@@ -364,7 +364,8 @@ struct CardStore {
   // over every thread (rank_sort_split), 2 (default) LDS hash table (no sort)
   int lean_group = 2;
   bool slot_prio = false;  // option "slot_prio": the pipelined stream's slot kernel issues at priority 2
-  bool feat_prio = true;  // option "feature_prio": the pipelined stream's lean bucket kernel issues at priority 2 (default since round 5)
+  bool feat_prio = false;  // option "feature_prio": the pipelined stream's lean bucket kernel issues at priority 2 (the
+                           // default in round 5; off since round 6's split rows, engine.hip)
   int64_t n_merchants = 0;
   DeviceBuffer pages, keys, merchants, err, seq;  // pages: CardPages (header + ring per slot); keys: the compact
                                                   // key array card_slot probes
@@ -554,7 +555,8 @@ struct Engine {
   int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
   bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
-  bool ens_prio = false;  // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels)
+  bool ens_prio = true;   // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels;
+                          // the default since round 6's split rows, engine.hip)
   bool ens_bin_global = false;  // "ensemble_bin_global": compact rows binned by searches in global memory (no staging)
   int compact_vectors = 2;      // "compact_vectors": the pipelined stream's scoring rows for the fused kernel when
                                 // nobody asked for vectors: 0 the 64-wide vector, 1 compact 64-B rows, 2 split rows
