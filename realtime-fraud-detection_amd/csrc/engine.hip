@@ -358,6 +358,10 @@ int fd_engine_destroy(fd_engine* eng) {
     e.pipe_out[k].release();
     e.pipe_seq[k].release();
   }
+  for (int k = 0; k < Engine::kSplitRing; ++k) {
+    if (e.pipe_split_ev[k]) (void)hipEventDestroy(e.pipe_split_ev[k]);
+    e.pipe_split[k].release();
+  }
   for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
   for (auto& P1 : e.ens1)
     for (auto* b : {&P1.nodes[0], &P1.nodes[1], &P1.thr}) b->release();
@@ -1125,6 +1129,7 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
                     ? e.compact_vectors : 0;
   e.pipe_vec[s].ensure((size_t)n * FD_VECTOR_WIDTH * 4);
   float* vec = e.pipe_vec[s].as<float>();
+  const int sr = (int)(e.pipe_iter % (unsigned long long)Engine::kSplitRing);  // split rows: this batch's ring buffer
   float* seq = nullptr;
   bool want_seq = false;
   for (int m = 0; m < params->n_models && m < FD_MAX_MODELS; ++m)
@@ -1140,6 +1145,13 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   // (before_buckets) like the lean pass
   const bool lean = e.pipe_lean && !(e.pipe_gather && e.state.slot_gather && n <= fd::kGatherBatchMax && !Ss);
   if (compact == 2 && (!lean || want_seq || e.state.S > 0)) compact = 1;
+  if (compact == 2) {  // RowA | RowB in the ring; the slot pass (which writes RowA) after the last fused kernel that
+    // read this buffer — on the slot stream that is an explicit wait, on the batch's own stream the stream order
+    e.pipe_split[sr].ensure((size_t)n * 64);
+    vec = e.pipe_split[sr].as<float>();
+    if (!e.pipe_split_ev[sr]) FD_HIP(hipEventCreateWithFlags(&e.pipe_split_ev[sr], kStreamEventFlags));
+    if (Ss && e.pipe_split_live[sr]) FD_HIP(hipStreamWaitEvent(Ss, e.pipe_split_ev[sr], 0));
+  }
   {
     struct SlotPass {  // launch_grouped reads these for this call only
       Engine& e;
@@ -1195,6 +1207,10 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
                       s_risk, seq, e.state.S, rec, s_res, compact) &&
         records)
       fd::launch_result_pack(e, s_fp, s_conf, s_dec, s_risk, rec, n, s_res);
+  }
+  if (compact == 2 && Ss) {  // this batch's split rows are read: their buffer's next writer (batch i + 4) may go
+    FD_HIP(hipEventRecord(e.pipe_split_ev[sr], Sc));
+    e.pipe_split_live[sr] = true;
   }
   FD_HIP(hipEventRecord(e.pipe_done_ev[s], Sc));
   e.pipe_done_live[s] = true;

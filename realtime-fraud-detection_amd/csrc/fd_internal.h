@@ -545,6 +545,14 @@ struct Engine {
   bool pipe_lean = true;   // "pipeline_lean" option: lean bucket kernel (fits beside the ensemble kernel)
   bool pipe_gather = true;  // "pipeline_gather" option: batches of <= kGatherBatchMax take the gather bucket kernel
   DeviceBuffer pipe_vec[kPipeSlots], pipe_seq[kPipeSlots];
+  // split rows (compact_vectors 2): RowA | RowB of batch i in ring buffer i mod kSplitRing. With the slot pass on its
+  // own stream, batch i's slot kernel writes RowA while batch i - 2's fused kernel (the same pipe_vec parity) may
+  // still read its rows — the slot stream waits only for batch i - 2's bucket pass — so the split rows get a deeper
+  // ring, and the slot pass waits for the fused kernel that last read its buffer (batch i - 4: long done)
+  static constexpr int kSplitRing = 4;
+  DeviceBuffer pipe_split[kSplitRing];
+  hipEvent_t pipe_split_ev[kSplitRing] = {};
+  bool pipe_split_live[kSplitRing] = {};
   // the scoring streams write a batch's outputs into pipe_out[slot]; one copy kernel on `stream` moves them to the
   // caller's buffers, so the caller's memory is written only in the engine stream's order (torch's caching
   // allocator may hand batch i's freed outputs to batch i+1); batch i+nbuf's scoring waits for pipe_copy_ev[slot]
