@@ -1208,13 +1208,15 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
         records)
       fd::launch_result_pack(e, s_fp, s_conf, s_dec, s_risk, rec, n, s_res);
   }
-  if (compact == 2 && Ss) {  // this batch's split rows are read: their buffer's next writer (batch i + 4) may go
-    FD_HIP(hipEventRecord(e.pipe_split_ev[sr], Sc));
-    e.pipe_split_live[sr] = true;
-  }
   FD_HIP(hipEventRecord(e.pipe_done_ev[s], Sc));
   e.pipe_done_live[s] = true;
   FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[s], 0));
+  if (compact == 2 && Ss) {  // this batch's split rows are read: their buffer's next writer (batch i + 4) may go. The
+    // event goes on the engine stream, past the scoring: on Sc it would sit between this batch's fused kernel and
+    // batch i + 2's bucket pass, the feature chain's critical path (+4 us per step measured)
+    FD_HIP(hipEventRecord(e.pipe_split_ev[sr], e.stream));
+    e.pipe_split_live[sr] = true;
+  }
   if (in_place) {  // nothing to copy: the next use of staging slot s (batch i + 2) is on this batch's stream Sc
     e.pipe_copy_live[s] = false;
     return;

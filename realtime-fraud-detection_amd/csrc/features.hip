@@ -664,36 +664,15 @@ __device__ __forceinline__ void velocity_step(CardRegs& c, RingEvent* __restrict
   const bool descent = c.rn > 0 && ts < c.last_ts;
   const bool inc = c.us == 0 && !descent;
   if (inc) {  // time-sorted ring: evict each window's too-old events from its oldest end
-    // the three windows' evictions interleaved: per round, every window that still has an event to evict issues its
-    // ring reads together (its oldest in-window event's cents, the next one's time), so a transaction pays
-    // max(evictions per window) dependent ring trips instead of their sum (round 6). Each window's own sequence of
-    // evictions and sums is the sequential one's.
-    for (;;) {
-      long long ec[3], et[3];
-      bool ev[3], any = false;
-#pragma unroll
-      for (int w = 0; w < 3; ++w) {
-        ev[w] = c.wc[w] > 0 && c.wo[w] <= ts - kWin[w];
-        any = any || ev[w];
-        ec[w] = et[w] = 0;
-        if (ev[w]) {
-          int idx = c.rh - c.wc[w];
-          if (idx < 0) idx += K;
-          ec[w] = rg[idx].cents;
-          if (c.wc[w] > 1) et[w] = rg[idx + 1 == K ? 0 : idx + 1].ts;
-        }
-      }
-      if (!any) break;
-#pragma unroll
-      for (int w = 0; w < 3; ++w)
-        if (ev[w]) {
-          c.ws[w] -= ec[w];
-          c.wc[w] -= 1;
-          if (c.wc[w] > 0) c.wo[w] = et[w];
-        }
-    }
 #pragma unroll
     for (int w = 0; w < 3; ++w) {
+      while (c.wc[w] > 0 && c.wo[w] <= ts - kWin[w]) {
+        int idx = c.rh - c.wc[w];
+        if (idx < 0) idx += K;
+        c.ws[w] -= rg[idx].cents;
+        c.wc[w] -= 1;
+        if (c.wc[w] > 0) c.wo[w] = rg[idx + 1 == K ? 0 : idx + 1].ts;
+      }
       cw[w] = c.wc[w];
       sw[w] = c.ws[w];
     }
