@@ -139,6 +139,29 @@ static bool score_matrix(Engine& e, const fd_blend_params& p, const int32_t* slo
     FD_HIP(hipStreamWaitEvent(e.aux_stream, e.fork_ev, 0));
     aux_forked = true;
   };
+  // option latency_prebin: when this call runs the pair path below on e.stream (two forests, every other present
+  // model the LSTM head), the LSTM launch bins the vectors for the pair's walks in workgroups ahead of its own, and
+  // the pair skips its binning launch (fd::PreBin; the bins are for this call only)
+  struct PreBinReset {
+    Engine& e;
+    ~PreBinReset() { e.prebin.want = e.prebin.done = false; }
+  } prebin_reset{e};
+  e.prebin.want = e.prebin.done = false;
+  if (e.latency_prebin && e.latency_fused && small && n_forests == 2 && ss == 0) {
+    int fm[2], k = 0;
+    bool lstm = false, others = false;
+    for (int m = 0; m < M; ++m) {
+      if (present && !present[m]) continue;
+      if (slots[m] == FD_SLOT_LSTM) lstm = true;
+      else if (slots[m] >= 0 && slots[m] < fd::kMaxSlots && k < 2) fm[k++] = m;
+      else others = true;
+    }
+    if (lstm && !others && k == 2) {
+      const fd::PackedForest& pa = e.forests[slots[fm[0]]];
+      const fd::PackedForest& pb = e.forests[slots[fm[1]]];
+      if (pa.loaded && pb.loaded) fd::forest_pair_prebin(e, pa, pb, dX, n, ld);
+    }
+  }
   for (int m = 0; m < M; ++m) {  // the LSTM first, so it overlaps the forests
     if ((present && !present[m]) || slots[m] != FD_SLOT_LSTM) continue;
     FD_REQUIRE(d_seq != nullptr, FD_ERR_INVALID_ARG,
@@ -458,6 +481,8 @@ int fd_engine_get_counter(fd_engine* eng, const char* key, int64_t* value) {
   } else if (k == "ensemble_single_launches") {  // fd_forest_predict batches scored by the fused kernel over one
     // forest (probabilities, optionally raw scores; no leaf ids): config 2's timed kernel, ensemble_kernel<8,2>
     *value = (int64_t)e.ens_single_total;
+  } else if (k == "latency_prebinned_batches") {  // latency pair launches that used the feature kernel's bins
+    *value = (int64_t)e.prebin_total;
   } else if (k == "pipelined_split_batches") {  // of the compact ones: split rows (compact_vectors 2)
     *value = (int64_t)e.pipe_split_total;
   } else if (k == "pipelined_compact_batches") {  // of those: scored by the fused kernel from the compact 64-B
@@ -538,6 +563,10 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     // slot + lean bucket pair of the large batches
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "pipeline_gather must be 0 or 1");
     e.pipe_gather = value != 0;
+  } else if (k == "latency_prebin") {  // latency batches: 1 (default) the XGBoost + IsolationForest pair's tree-split
+    // binning done by the gather feature kernel (no binning launch), 0 the binning launch
+    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "latency_prebin must be 0 or 1");
+    e.latency_prebin = value != 0;
   } else if (k == "small_streams") {  // latency batches: 2 LSTM | other forests on two side streams, 1 one, 0 none
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "small_streams must be 0, 1 or 2");
     e.small_streams = (int)value;

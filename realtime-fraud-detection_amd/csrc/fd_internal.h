@@ -131,6 +131,24 @@ struct SplitScratch {
   DeviceBuffer bins, nan, leaves;  // nan: per-tile "holds a NaN" flags, cleared by the step's sum kernel
 };
 
+// Latency batches, option "latency_prebin": the tree-split binning of the XGBoost / IsolationForest pair done by
+// workgroups of the LSTM head's launch, ahead of its own (lstm.hip lstm_kernel4), so the pair's binning launch and its
+// queue gap go (forest.hip launch_forest_pair_blend). Filled by forest_pair_prebin before the LSTM launch (score_matrix);
+// `done` set by the LSTM launch that binned (these vectors), consumed by the pair launch.
+struct PreBin {
+  const float* thr[2] = {};        // [0] XGBoost, [1] IsolationForest: distinct thresholds, feature-major
+  const int32_t* thr_off[2] = {};
+  uint32_t* bins[2] = {};          // [feature][n_pad]
+  uint32_t* nan[2] = {};           // per-tile NaN flags
+  int nf[2] = {};
+  int64_t n = 0, n_pad = 0;
+  int ld = 0;
+  const void* fx = nullptr;        // the forests and the vectors the bins are for
+  const void* ff = nullptr;
+  const float* X = nullptr;
+  bool want = false, done = false;
+};
+
 // A forest repacked into perfect depth-D trees stored as 1-based heaps (see forest.hip header and
 // DESIGN.md "Forest layout"): per tree 2^D node records {f32 thr, u32 meta} (slot 0 unused; children
 // of slot s are 2s / 2s+1) then 2^D leaf values (f32 XGBoost, f64 Isolation Forest); chunks of
@@ -563,6 +581,9 @@ struct Engine {
   int small_streams = 0;  // score_matrix, latency batches: side streams for the LSTM / other forests (engine.hip)
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
   bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
+  bool latency_prebin = true;  // "latency_prebin": the latency pair's binning in the LSTM head's launch (PreBin)
+  PreBin prebin;
+  unsigned long long prebin_total = 0;  // counter "latency_prebinned_batches"
   bool ens_prio = true;   // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels;
                           // the default since round 6's split rows, engine.hip)
   bool ens_bin_global = false;  // "ensemble_bin_global": compact rows binned by searches in global memory (no staging)
@@ -639,6 +660,10 @@ bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedFor
                               int32_t ld, const BlendConsts& bc, const double* const* cols, int pos1, int pos2,
                               double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk,
                               hipEvent_t before_blend = nullptr);
+// e.prebin for the pair launch_forest_pair_blend will run over d_X (n rows): false (e.prebin.want cleared) when it
+// does not apply
+bool forest_pair_prebin(Engine& e, const PackedForest& p1, const PackedForest& p2, const float* d_X, int64_t n,
+                        int32_t ld);
 // windows.hip
 void windows_init(Engine& e, const fd_window_params& p);
 void windows_step(Engine& e, const fd_txn_batch& t, const fd_window_inputs& in, int64_t n, bool flush,

@@ -897,54 +897,20 @@ forest_kernel6(const float* __restrict__ X, int64_t n, int ld, int nf, const cha
 //                        goes to a [tree][n] scratch in HBM (and the leaf id when asked);
 //   split_sum_kernel   : per transaction, base margin + the leaf values in tree order (the
 //                        reference's sequential f32 / f64 sum, bit for bit), then the outputs.
-constexpr int kSplitBin = 256;
-
-// one thread per (feature, transaction): the binary search's dependent loads are the only latency
-__device__ __forceinline__ void split_bin_body(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, int f,
-                                               const float* __restrict__ thr, const int32_t* __restrict__ thr_off,
-                                               uint32_t* __restrict__ bins, uint32_t* __restrict__ tile_nan) {
-  const int64_t r = (int64_t)blockIdx.x * kSplitBin + threadIdx.x;  // row within [0, n_pad)
-  const bool ok = r < n;
-  float v = 0.f;
-  if (ok) v = f < ld ? X[r * (int64_t)ld + f] : __builtin_nanf("");  // DMatrix: missing column = NaN
-  const int o = thr_off[f], cnt = thr_off[f + 1] - o;
-  int pos = 0;
-  for (int st = lift_steps(cnt); st > 0; st >>= 1) {
-    const int np = pos + st;
-    if (np <= cnt && thr[o + np - 1] <= v) pos = np;
-  }
-  const bool isnan_v = ok && v != v;
-  bins[(size_t)f * n_pad + r] = !ok ? 0u : (isnan_v ? 0xFFFF0000u : (uint32_t)pos << 16);
-  // tile flag: nonzero when the tile holds a NaN; split_sum_kernel, the step's last launch over this scratch,
-  // clears it again, so a replayed hipGraph of the step starts from clear flags (no host-side epoch)
-  if (__ballot(isnan_v) != 0ull && (threadIdx.x & 63) == 0) tile_nan[r / kTile] = 1u;
-}
 
 __global__ void __launch_bounds__(kSplitBin)
 split_bin_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, int nf, const float* __restrict__ thr,
                  const int32_t* __restrict__ thr_off, int bin_steps, uint32_t* __restrict__ bins,
                  uint32_t* __restrict__ tile_nan) {
-  split_bin_body(X, n, n_pad, ld, (int)blockIdx.y, thr, thr_off, bins, tile_nan);
+  split_bin_body(X, n, n_pad, ld, (int)blockIdx.y, (int64_t)blockIdx.x * kSplitBin + threadIdx.x, thr, thr_off, bins,
+                 tile_nan);
 }
-
-// one forest's binning inputs / outputs (split_bin_pair_kernel)
-struct SplitBinArgs {
-  const float* thr;
-  const int32_t* thr_off;
-  uint32_t* bins;
-  uint32_t* tile_nan;
-  int nf;
-};
 
 // both forests of a latency batch binned in one launch: grid.y = nf_a + nf_b
 __global__ void __launch_bounds__(kSplitBin)
 split_bin_pair_kernel(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, SplitBinArgs a, SplitBinArgs b) {
   FD_TL(g_tl_forest, 3, 0);
-  const int y = (int)blockIdx.y;
-  if (y < a.nf)
-    split_bin_body(X, n, n_pad, ld, y, a.thr, a.thr_off, a.bins, a.tile_nan);
-  else
-    split_bin_body(X, n, n_pad, ld, y - a.nf, b.thr, b.thr_off, b.bins, b.tile_nan);
+  split_bin_pair_cell(X, n, n_pad, ld, a, b, (int)blockIdx.y, (int64_t)blockIdx.x * kSplitBin + threadIdx.x);
   FD_TL(g_tl_forest, 3, 3);
 }
 
@@ -1553,32 +1519,81 @@ void walk_groups(const PackedForest& pf, int64_t tiles, int& cpg, int& groups) {
   cpg = std::max(1, (pf.b_n_chunks + want - 1) / want);
   groups = (pf.b_n_chunks + cpg - 1) / cpg;
 }
-}  // namespace
 
-bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedForest& p2, const float* d_X, int64_t n,
-                              int32_t ld, const BlendConsts& bc, const double* const* cols, int pos1, int pos2,
-                              double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk, hipEvent_t before_blend) {
+// The pair path's forests (XGBoost first) and its walk kernel, or false when it does not apply
+bool pair_blend_plan(const Engine& e, const PackedForest& p1, const PackedForest& p2, int64_t n,
+                     const PackedForest*& xf, const PackedForest*& ff, const void*& walk, size_t& lds) {
   if (n == 0 || &p1 == &p2 || !split_path(e, p1, n) || !split_path(e, p2, n)) return false;
   const bool x1 = p1.kind == FD_FOREST_XGB_BINARY_LOGISTIC, x2 = p2.kind == FD_FOREST_XGB_BINARY_LOGISTIC;
   if (x1 == x2) return false;  // one XGBoost and one IsolationForest
   const PackedForest& X = x1 ? p1 : p2;
   const PackedForest& F = x1 ? p2 : p1;
   if (X.depth != 8 || F.depth != 8 || X.num_feature != F.num_feature) return false;
-  const void* walk = pick_walk_pair(X.b_chunk, F.b_chunk);
+  walk = pick_walk_pair(X.b_chunk, F.b_chunk);
   if (!walk) return false;
-  const int nf = X.num_feature;
-  const size_t lds = (size_t)nf * 1024 + 2 * std::max(X.b_chunk_stride, F.b_chunk_stride) + 1024;
+  lds = (size_t)X.num_feature * 1024 + 2 * std::max(X.b_chunk_stride, F.b_chunk_stride) + 1024;
   if (lds > kLdsBudget) return false;
+  xf = &X;
+  ff = &F;
+  return true;
+}
+}  // namespace
+
+bool forest_pair_prebin(Engine& e, const PackedForest& p1, const PackedForest& p2, const float* d_X, int64_t n,
+                        int32_t ld) {
+  PreBin& pb = e.prebin;
+  pb.want = pb.done = false;
+  const PackedForest *xf = nullptr, *ff = nullptr;
+  const void* walk = nullptr;
+  size_t lds = 0;
+  if (!e.latency_prebin || !pair_blend_plan(e, p1, p2, n, xf, ff, walk, lds)) return false;
+  const int64_t tiles = (n + kTile - 1) / kTile;
+  const SplitBinArgs a = split_prepare<float>(*xf, n, tiles, e.stream);
+  const SplitBinArgs b = split_prepare<double>(*ff, n, tiles, e.stream);
+  pb.thr[0] = a.thr, pb.thr[1] = b.thr;
+  pb.thr_off[0] = a.thr_off, pb.thr_off[1] = b.thr_off;
+  pb.bins[0] = a.bins, pb.bins[1] = b.bins;
+  pb.nan[0] = a.tile_nan, pb.nan[1] = b.tile_nan;
+  pb.nf[0] = a.nf, pb.nf[1] = b.nf;
+  pb.n = n;
+  pb.n_pad = tiles * kTile;
+  pb.ld = ld;
+  pb.fx = xf;
+  pb.ff = ff;
+  pb.X = d_X;
+  pb.want = true;
+  return true;
+}
+
+bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedForest& p2, const float* d_X, int64_t n,
+                              int32_t ld, const BlendConsts& bc, const double* const* cols, int pos1, int pos2,
+                              double* dfp, double* dconf, uint8_t* ddec, uint8_t* drisk, hipEvent_t before_blend) {
+  const PackedForest *xf = nullptr, *ff = nullptr;
+  const void* walk = nullptr;
+  size_t lds = 0;
+  // the bins of an LSTM launch that binned these vectors for this pair (PreBin), consumed here
+  const bool prebinned = e.prebin.done && e.prebin.X == d_X && e.prebin.n == n && e.prebin.ld == ld;
+  const void* pre_fx = e.prebin.fx;
+  const void* pre_ff = e.prebin.ff;
+  e.prebin.want = e.prebin.done = false;
+  if (!pair_blend_plan(e, p1, p2, n, xf, ff, walk, lds)) return false;
+  const PackedForest& X = *xf;
+  const PackedForest& F = *ff;
+  const int nf = X.num_feature;
   FD_REQUIRE(d_X && dfp && cols && ld > 0, FD_ERR_INVALID_ARG, "null buffer or bad ld");
   const int64_t tiles = (n + kTile - 1) / kTile, n_pad = tiles * kTile;
   const hipStream_t st = e.stream;
-  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_XGB) : nullptr;  // the pair's three launches
+  Engine::Timed* ev = e.timing ? e.next_event_pair(FD_TIMING_XGB) : nullptr;  // the pair's launches
   if (ev) FD_HIP(hipEventRecord(ev->a, st));
   const SplitBinArgs a = split_prepare<float>(X, n, tiles, st);
   const SplitBinArgs b = split_prepare<double>(F, n, tiles, st);
-  hipLaunchKernelGGL(split_bin_pair_kernel, dim3((unsigned)(tiles * kTile / kSplitBin), (unsigned)(a.nf + b.nf)),
-                     dim3(kSplitBin), 0, st, d_X, n, n_pad, (int)ld, a, b);
-  FD_HIP(hipGetLastError());
+  if (prebinned && pre_fx == &X && pre_ff == &F) {
+    ++e.prebin_total;
+  } else {
+    hipLaunchKernelGGL(split_bin_pair_kernel, dim3((unsigned)(tiles * kTile / kSplitBin), (unsigned)(a.nf + b.nf)),
+                       dim3(kSplitBin), 0, st, d_X, n, n_pad, (int)ld, a, b);
+    FD_HIP(hipGetLastError());
+  }
   SplitWalkArgs wx{}, wf{};
   wx.bins = a.bins;
   wx.tile_nan = a.tile_nan;
@@ -1604,6 +1619,7 @@ bool launch_forest_pair_blend(Engine& e, const PackedForest& p1, const PackedFor
   PairBlendArgs pa{};
   pa.blend = bc;
   for (int m = 0; m < bc.n_models; ++m) pa.cols.p[m] = cols[m];
+  const bool x1 = &X == &p1;
   pa.pos_x = x1 ? pos1 : pos2;
   pa.pos_f = x1 ? pos2 : pos1;
   pa.base_margin = X.base_margin;

@@ -41,6 +41,7 @@
 #include <utility>
 
 #include "fd_internal.h"
+#include "walk_common.h"
 
 namespace fd {
 #ifdef FD_FOREST_PROFILE
@@ -171,13 +172,32 @@ __device__ __forceinline__ void mfma_abid16(float a, const float* b, f32x4* acc,
   ((acc[J & 3] = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b[J], acc[J & 3], 4, J, 0)), ...);
 }
 
+// option latency_prebin (fd_internal.h PreBin): the XGBoost + IsolationForest pair's tree-split binning
+// (split_bin_pair_kernel's cells, two per workgroup) in the first `blocks` workgroups of the LSTM launch, which the
+// dispatcher places ahead of the LSTM's own: the pair's binning launch and its queue gap go
+struct LstmBinArgs {
+  const float* X;
+  int64_t n, n_pad;
+  int ld;
+  SplitBinArgs a, b;
+  int blocks, row_blocks;
+};
+
 __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ seq, int64_t n, int T,
                                                     const float* __restrict__ wpk4, const float* __restrict__ bias,
                                                     const float* __restrict__ wout, const float* __restrict__ bout,
                                                     int n_out, double* __restrict__ prob,
                                                     const unsigned long long* __restrict__ desc,
-                                                    const float* __restrict__ ring, int h0_skip) {
+                                                    const float* __restrict__ ring, int h0_skip, LstmBinArgs pb) {
 #pragma clang fp contract(off)
+  if ((int)blockIdx.x < pb.blocks) {  // a binning workgroup: cells 2b and 2b + 1, a half-workgroup (4 waves) each
+    const int cell = (int)blockIdx.x * 2 + (int)(threadIdx.x >> 8);
+    const int y = cell / pb.row_blocks, rb = cell - y * pb.row_blocks;
+    if (y < pb.a.nf + pb.b.nf)
+      split_bin_pair_cell(pb.X, pb.n, pb.n_pad, pb.ld, pb.a, pb.b, y, (int64_t)rb * kSplitBin + (threadIdx.x & 255));
+    return;
+  }
+  const unsigned bx = blockIdx.x - (unsigned)pb.blocks, gx = gridDim.x - (unsigned)pb.blocks;
   // h_t and x_t in the A-operand order: (txn i, k) at lane i + 4 (k & 15), register k >> 4. h_t is stored
   // register-major, [register][lane]: a lane's reads (one word per register) and the cell writes (a wave's 64
   // lanes cover 64 consecutive words of one register row) are both bank-conflict free. (Lane-major [lane][8],
@@ -194,11 +214,11 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
   // latency path: the first tile's sequence descriptors are loaded before the weights (vector loads retire in
   // order, so the ring gather below waits for these alone, and its own loads overlap the weights')
   unsigned long long dsc[2] = {0ull, 0ull};
-  if (desc != nullptr && blockIdx.x < ntiles) {
+  if (desc != nullptr && bx < ntiles) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int idx = tid + 512 * j, r = idx / per;
-      if (idx < 4 * per && (int64_t)blockIdx.x * 4 + r < n) dsc[j] = desc[(int64_t)blockIdx.x * 4 + r];
+      if (idx < 4 * per && (int64_t)bx * 4 + r < n) dsc[j] = desc[(int64_t)bx * 4 + r];
     }
   }
   // B operands: lane l holds W[(l >> 4) * 128 + 16 w + (l & 15)][k] for k = 0..143 (W_ih, then W_hh's unit blocks
@@ -215,7 +235,7 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
   const int hr = w & 3, ho = w >> 2;
   const float wo0 = ho < n_out ? wout[ho * kH + l] : 0.f, wo1 = ho < n_out ? wout[ho * kH + 64 + l] : 0.f;
   const float bo = ho < n_out ? bout[ho] : 0.f;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int64_t tile = bx; tile < ntiles; tile += gx) {
     const int64_t row0 = tile * 4;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -224,7 +244,7 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
       const int r = idx / per, rem = idx - r * per, t = rem / kI, k = rem - t * kI;
       float v = 0.f;
       if (row0 + r < n) {
-        const unsigned long long d = desc == nullptr ? kSeqMaterialized : (tile == blockIdx.x ? dsc[j] : desc[row0 + r]);
+        const unsigned long long d = desc == nullptr ? kSeqMaterialized : (tile == bx ? dsc[j] : desc[row0 + r]);
         if (d & kSeqMaterialized) {
           v = seq[(size_t)(row0 + r) * per + rem];
         } else {  // the card's ring: oldest -> newest, left-padded with zero events (features.hip seq_step)
@@ -241,7 +261,7 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
     (&hbuf[0][0][0])[tid] = 0.f;  // 512 threads = 4 x 128
     float c = 0.f, h = 0.f;
     __syncthreads();
-    if (tile == blockIdx.x) FD_TL(g_tl_lstm, 2, 1);
+    if (tile == bx) FD_TL(g_tl_lstm, 2, 1);
     f32x4 acc[4] = {f32x4{bcol, bcol, bcol, bcol}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
                     f32x4{0.f, 0.f, 0.f, 0.f}};
     mfma_abid16(xs[0][l], &bw[0], acc, std::make_integer_sequence<int, 16>{});
@@ -282,7 +302,7 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
       }
       __syncthreads();
     }
-    if (tile == blockIdx.x) FD_TL(g_tl_lstm, 2, 2);
+    if (tile == bx) FD_TL(g_tl_lstm, 2, 2);
     hT[q][unit] = h;
     __syncthreads();
     if (ho < n_out) {  // dense head over h_T: a wave's 64 two-product partials, then a butterfly sum
@@ -390,10 +410,23 @@ void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, i
              "internal: sequence descriptors need the 4-row LSTM kernel and the engine's history ring");
   if (rows == 4) {  // one 512-thread workgroup per CU (bw[] holds 144 VGPRs), looping over 4-row tiles
     const int64_t tiles = (n + 3) / 4;
-    hipLaunchKernelGGL(lstm_kernel4, dim3((unsigned)std::min<int64_t>(tiles, 256)), dim3(512), 0, stream, d_seq, n,
-                       T, m.wpk4.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),
+    LstmBinArgs pb{};
+    PreBin& q = e.prebin;
+    if (q.want && stream == e.stream) {  // the forest pair's binning ahead of the LSTM's workgroups (PreBin)
+      pb.X = q.X;
+      pb.n = q.n;
+      pb.n_pad = q.n_pad;
+      pb.ld = q.ld;
+      pb.a = SplitBinArgs{q.thr[0], q.thr_off[0], q.bins[0], q.nan[0], q.nf[0]};
+      pb.b = SplitBinArgs{q.thr[1], q.thr_off[1], q.bins[1], q.nan[1], q.nf[1]};
+      pb.row_blocks = (int)(q.n_pad / kSplitBin);
+      pb.blocks = (pb.row_blocks * (q.nf[0] + q.nf[1]) + 1) / 2;
+      q.done = true;
+    }
+    hipLaunchKernelGGL(lstm_kernel4, dim3((unsigned)(std::min<int64_t>(tiles, 256) + pb.blocks)), dim3(512), 0, stream,
+                       d_seq, n, T, m.wpk4.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),
                        m.bout.as<const float>(), m.n_out, d_prob, d_desc,
-                       d_desc ? e.state.seq.as<const float>() : nullptr, m.hh_finite ? 1 : 0);
+                       d_desc ? e.state.seq.as<const float>() : nullptr, m.hh_finite ? 1 : 0, pb);
   } else {
     hipLaunchKernelGGL(lstm_kernel, dim3((unsigned)((n + kRows - 1) / kRows)), dim3(512), 0, stream, d_seq, n, T,
                        m.wpk.as<const float>(), m.bias.as<const float>(), m.wout.as<const float>(),

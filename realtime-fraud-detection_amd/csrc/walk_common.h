@@ -157,6 +157,50 @@ __device__ __forceinline__ void walk4(uint32_t buf, int gg, uint32_t lane4, uint
 // steps (a feature no split uses — the 64-wide vector's pad slots — costs none)
 __device__ __forceinline__ int lift_steps(int cnt) { return cnt > 0 ? (int)(1u << (31 - __clz(cnt))) : 0; }
 
+// ---- tree-split binning (forest.hip split_bin_kernel / split_bin_pair_kernel; lstm.hip lstm_kernel4's bin blocks)
+constexpr int kSplitBin = 256;  // rows per binning workgroup (one thread each)
+
+// one thread per (feature f, row r): the binary search's dependent loads are the only latency
+__device__ __forceinline__ void split_bin_body(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld, int f,
+                                               int64_t r, const float* __restrict__ thr,
+                                               const int32_t* __restrict__ thr_off, uint32_t* __restrict__ bins,
+                                               uint32_t* __restrict__ tile_nan) {
+  const bool ok = r < n;  // r within [0, n_pad)
+  float v = 0.f;
+  if (ok) v = f < ld ? X[r * (int64_t)ld + f] : __builtin_nanf("");  // DMatrix: missing column = NaN
+  const int o = thr_off[f], cnt = thr_off[f + 1] - o;
+  int pos = 0;
+  for (int st = lift_steps(cnt); st > 0; st >>= 1) {
+    const int np = pos + st;
+    if (np <= cnt && thr[o + np - 1] <= v) pos = np;
+  }
+  const bool isnan_v = ok && v != v;
+  bins[(size_t)f * n_pad + r] = !ok ? 0u : (isnan_v ? 0xFFFF0000u : (uint32_t)pos << 16);
+  // tile flag: nonzero when the tile holds a NaN; the step's sum kernel, its last launch over this scratch, clears it
+  // again, so a replayed hipGraph of the step starts from clear flags (no host-side epoch). (kTile rows per tile, a
+  // multiple of the 64 rows of a wave)
+  if (__ballot(isnan_v) != 0ull && (threadIdx.x & 63) == 0) tile_nan[r / kTile] = 1u;
+}
+
+// one forest's binning inputs / outputs
+struct SplitBinArgs {
+  const float* thr;
+  const int32_t* thr_off;
+  uint32_t* bins;
+  uint32_t* tile_nan;
+  int nf;
+};
+
+// cell y of a forest pair's binning: features 0..a.nf-1 of the first forest, then the second's
+__device__ __forceinline__ void split_bin_pair_cell(const float* __restrict__ X, int64_t n, int64_t n_pad, int ld,
+                                                    const SplitBinArgs& a, const SplitBinArgs& b, int y, int64_t r) {
+  if (y < a.nf)
+    split_bin_body(X, n, n_pad, ld, y, r, a.thr, a.thr_off, a.bins, a.tile_nan);
+  else
+    split_bin_body(X, n, n_pad, ld, y - a.nf, r, b.thr, b.thr_off, b.bins, b.tile_nan);
+}
+
+
 // bin(v) = #{t in tbl[0, cnt) : t <= v}, tbl ascending; steps = largest power of two <= cnt.
 template <bool IN_LDS>
 __device__ __forceinline__ uint32_t bin_of(float v, const float* __restrict__ gt, uint32_t lt, int cnt, int steps) {

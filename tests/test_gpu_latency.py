@@ -226,3 +226,50 @@ def test_slot_gather_identical(world, users):
     finally:
         for e in engs:
             e.close()
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("lstm", [True, False])
+def test_prebin_in_lstm_launch_identical(world, lstm):
+    """Latency batches bin the XGBoost + IsolationForest pair's vectors for the tree-split walks in workgroups of the
+    LSTM head's launch, ahead of its own (engine option latency_prebin 1, no binning launch), instead of
+    split_bin_pair_kernel (0): the same outputs bit for bit, batch after batch — vectors also written to the caller's
+    buffer, ragged sizes (a tile's padding rows), a batch of 1, and the sizes where the 16-row LSTM kernel runs
+    (4096, 4097: the binning launch). The engine counter latency_prebinned_batches counts the pair launches that used
+    the LSTM launch's bins; without the LSTM head there are none (the binning launch stays)."""
+    import torch
+    _, _, xgb, ifm = world
+    pop = synth.population(3000, 500, seed=95)
+    tx = synth.txn_stream(pop, 16000, seed=96, rate_per_s=50.0)
+    lw = L.random_weights(seed=8) if lstm else None
+    params = _params(lstm)
+    slots = [0, 1, FD_SLOT_LSTM] if lstm else [0, 1]
+    dev = {f: torch.from_numpy(np.ascontiguousarray(tx[f])).cuda() for f in TXN_FIELDS}
+    engs = [_setup(pop, xgb, ifm, lw) for _ in range(2)]
+    sizes = [1, 1000, 997, 4096, 4097, 1024, 300]
+    try:
+        res = []
+        for v, e in enumerate(engs):
+            e.set_option("latency_prebin", v)
+            e.set_stream(torch.cuda.current_stream().cuda_stream)
+            out, a = [], 0
+            for k, B in enumerate(sizes):
+                fp, conf = (torch.empty(B, dtype=torch.float64, device="cuda") for _ in range(2))
+                dec, risk = (torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(2))
+                mp = torch.empty((len(slots), B), dtype=torch.float64, device="cuda")
+                vec = torch.empty((B, 64), dtype=torch.float32, device="cuda") if k % 2 else None
+                e.score_batch_device(params, slots, {f: t[a:a + B].data_ptr() for f, t in dev.items()}, B,
+                                     fp.data_ptr(), conf.data_ptr(), dec.data_ptr(), risk.data_ptr(),
+                                     model_probs_ptr=mp.data_ptr(), vec_ptr=vec.data_ptr() if vec is not None else 0)
+                out.append([fp, conf, dec, risk, mp] + ([vec] if vec is not None else []))
+                a += B
+            res.append(out)
+        torch.cuda.synchronize()
+        for b, (x, y) in enumerate(zip(res[1], res[0])):
+            for s, t in zip(x, y):
+                assert np.array_equal(s.cpu().numpy(), t.cpu().numpy()), f"batch {b}"
+        assert engs[0].counter("latency_prebinned_batches") == 0
+        assert engs[1].counter("latency_prebinned_batches") == (sum(B < 4096 for B in sizes) if lstm else 0)
+    finally:
+        for e in engs:
+            e.close()
