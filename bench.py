@@ -720,7 +720,15 @@ class Config3:
         lean = getattr(self, "pipe", None)
         if lean is None:
             lean = bool(getattr(getattr(getattr(self, "scorer", None), "be", None), "pipelined", True))
-        bucket = "fd::anon::feat_bucket_lean_kernel<1>" if lean else "fd::anon::feat_bucket_kernel<1>"
+        # the lean kernel's template form: split scoring rows (<1, true>, the default when nothing asks for the
+        # vectors) or the compact / full rows (<1, false>), as this run's engine counted them
+        split = False
+        try:
+            split = self.eng.counter("pipelined_split_batches") > 0
+        except Exception:
+            pass
+        bucket = (f"fd::anon::feat_bucket_lean_kernel<1, {'true' if split else 'false'}>" if lean
+                  else "fd::anon::feat_bucket_kernel<1>")
         g = {"features": (["fd::anon::feat_slot_kernel", bucket], "features")}
         sym = (roof or {}).get("kernel_symbol")
         if sym:
@@ -762,7 +770,8 @@ class Config5(Config3):
                 "traffic": pmc_traffic(self.name, self.B, LSTM4_SYMBOL), "kernel_samples": launches,
                 "kernel": "lstm_kernel4 (v_mfma_f32_4x4x1_16b_f32, 4 transactions per workgroup)",
                 "kernel_avg_us": round(avg * 1e6, 3), "flops_per_launch": flops, "flops_per_txn": flops // self.B,
-                "note": "latency-bound 1k batch; f32 MFMA = reference fp32 precision"}
+                "note": "latency-bound 1k batch; f32 MFMA = reference fp32 precision; the launch also carries the forest "
+                        "pair's tree-split binning workgroups (engine option latency_prebin, DESIGN §3), timed with it"}
 
     def counter_groups(self, roof):
         # batches of <= 4096 transactions: the slot pass runs inside the bucket launch (engine option slot_gather)

@@ -563,10 +563,12 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     // slot + lean bucket pair of the large batches
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "pipeline_gather must be 0 or 1");
     e.pipe_gather = value != 0;
-  } else if (k == "latency_prebin") {  // latency batches: 1 (default) the XGBoost + IsolationForest pair's tree-split
-    // binning done by the gather feature kernel (no binning launch), 0 the binning launch
-    FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "latency_prebin must be 0 or 1");
+  } else if (k == "latency_prebin") {  // latency batches with the LSTM head: the XGBoost + IsolationForest pair's
+    // tree-split binning in workgroups of the LSTM launch, 2 (default) after the LSTM's own (they fill the CUs the
+    // LSTM's workgroups leave as they finish), 1 ahead of them; 0 the pair's own binning launch
+    FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "latency_prebin must be 0, 1 or 2");
     e.latency_prebin = value != 0;
+    if (value) e.latency_prebin_mode = (int)value;
   } else if (k == "small_streams") {  // latency batches: 2 LSTM | other forests on two side streams, 1 one, 0 none
     FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "small_streams must be 0, 1 or 2");
     e.small_streams = (int)value;

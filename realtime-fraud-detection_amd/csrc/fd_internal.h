@@ -582,6 +582,7 @@ struct Engine {
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
   bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
   bool latency_prebin = true;  // "latency_prebin": the latency pair's binning in the LSTM head's launch (PreBin)
+  int latency_prebin_mode = 2;  // its value: 1 the binning workgroups ahead of the LSTM's, 2 (default) after them
   PreBin prebin;
   unsigned long long prebin_total = 0;  // counter "latency_prebinned_batches"
   bool ens_prio = true;   // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels;

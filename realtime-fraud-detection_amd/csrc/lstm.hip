@@ -181,6 +181,7 @@ struct LstmBinArgs {
   int ld;
   SplitBinArgs a, b;
   int blocks, row_blocks;
+  int last;  // the binning workgroups after the LSTM's (option latency_prebin 2) instead of ahead of them
 };
 
 __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ seq, int64_t n, int T,
@@ -190,14 +191,16 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
                                                     const unsigned long long* __restrict__ desc,
                                                     const float* __restrict__ ring, int h0_skip, LstmBinArgs pb) {
 #pragma clang fp contract(off)
-  if ((int)blockIdx.x < pb.blocks) {  // a binning workgroup: cells 2b and 2b + 1, a half-workgroup (4 waves) each
-    const int cell = (int)blockIdx.x * 2 + (int)(threadIdx.x >> 8);
+  const unsigned gx = gridDim.x - (unsigned)pb.blocks;  // the LSTM's workgroups
+  const int bin_wg = pb.last ? (int)blockIdx.x - (int)gx : (int)blockIdx.x;
+  if (bin_wg >= 0 && bin_wg < pb.blocks) {  // a binning workgroup: cells 2b and 2b + 1, a half-workgroup (4 waves) each
+    const int cell = bin_wg * 2 + (int)(threadIdx.x >> 8);
     const int y = cell / pb.row_blocks, rb = cell - y * pb.row_blocks;
     if (y < pb.a.nf + pb.b.nf)
       split_bin_pair_cell(pb.X, pb.n, pb.n_pad, pb.ld, pb.a, pb.b, y, (int64_t)rb * kSplitBin + (threadIdx.x & 255));
     return;
   }
-  const unsigned bx = blockIdx.x - (unsigned)pb.blocks, gx = gridDim.x - (unsigned)pb.blocks;
+  const unsigned bx = pb.last ? blockIdx.x : blockIdx.x - (unsigned)pb.blocks;
   // h_t and x_t in the A-operand order: (txn i, k) at lane i + 4 (k & 15), register k >> 4. h_t is stored
   // register-major, [register][lane]: a lane's reads (one word per register) and the cell writes (a wave's 64
   // lanes cover 64 consecutive words of one register row) are both bank-conflict free. (Lane-major [lane][8],
@@ -421,6 +424,7 @@ void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, i
       pb.b = SplitBinArgs{q.thr[1], q.thr_off[1], q.bins[1], q.nan[1], q.nf[1]};
       pb.row_blocks = (int)(q.n_pad / kSplitBin);
       pb.blocks = (pb.row_blocks * (q.nf[0] + q.nf[1]) + 1) / 2;
+      pb.last = e.latency_prebin_mode == 2 ? 1 : 0;
       q.done = true;
     }
     hipLaunchKernelGGL(lstm_kernel4, dim3((unsigned)(std::min<int64_t>(tiles, 256) + pb.blocks)), dim3(512), 0, stream,

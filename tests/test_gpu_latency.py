@@ -229,10 +229,10 @@ def test_slot_gather_identical(world, users):
 
 
 @pytest.mark.timeout(200)
-@pytest.mark.parametrize("lstm", [True, False])
-def test_prebin_in_lstm_launch_identical(world, lstm):
+@pytest.mark.parametrize("lstm,mode", [(True, 1), (True, 2), (False, 1)])
+def test_prebin_in_lstm_launch_identical(world, lstm, mode):
     """Latency batches bin the XGBoost + IsolationForest pair's vectors for the tree-split walks in workgroups of the
-    LSTM head's launch, ahead of its own (engine option latency_prebin 1, no binning launch), instead of
+    LSTM head's launch, ahead of its own (engine option latency_prebin 1) or after them (2) — no binning launch —, instead of
     split_bin_pair_kernel (0): the same outputs bit for bit, batch after batch — vectors also written to the caller's
     buffer, ragged sizes (a tile's padding rows), a batch of 1, and the sizes where the 16-row LSTM kernel runs
     (4096, 4097: the binning launch). The engine counter latency_prebinned_batches counts the pair launches that used
@@ -250,7 +250,7 @@ def test_prebin_in_lstm_launch_identical(world, lstm):
     try:
         res = []
         for v, e in enumerate(engs):
-            e.set_option("latency_prebin", v)
+            e.set_option("latency_prebin", mode if v else 0)
             e.set_stream(torch.cuda.current_stream().cuda_stream)
             out, a = [], 0
             for k, B in enumerate(sizes):
