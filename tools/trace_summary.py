@@ -1,3 +1,9 @@
+"""Steady-state summary of a pipelined config-3/4 kernel trace (the compact CSV `tools/trace_steps.py ... dump` writes):
+over the longest cluster of fused-kernel launches, the medians / min / max of the fused, lean and slot durations, the
+time from each batch's lean pass ending to its fused kernel starting (the feature chain's slack) and from the previous
+fused launch ending (negative: the launches overlap).
+
+usage: python tools/trace_summary.py steps.csv"""
 import csv, sys
 rows=[(int(r['Start_Timestamp']),int(r['End_Timestamp']),r['Kernel_Name']) for r in csv.DictReader(open(sys.argv[1]))]
 rows.sort()
