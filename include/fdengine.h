@@ -686,8 +686,9 @@ int fd_engine_set_timing(fd_engine* eng, int enable);
      LDS hash table of card slots (no sort), 1 a rank sort split over all threads, 0 the first m threads each rank
      one key over the whole list
      "latency_prebin": latency batches scored by the XGBoost + IsolationForest pair path with the LSTM head: the
-     pair's tree-split binning in workgroups of the LSTM launch (no binning launch; counter
-     "latency_prebinned_batches"), 2 (default) after the LSTM's own workgroups, 1 ahead of them; 0 its own binning
+     pair's tree-split binning in the LSTM launch (no binning launch; counter "latency_prebinned_batches"), 3
+     (default) inside the LSTM's own workgroups, a binary-search level per recurrence step (2 where a thread would
+     take more than two searches), 2 in extra workgroups after the LSTM's own, 1 ahead of them; 0 its own binning
      launch (outputs identical)
      (further options — "slot_stream", "slot_gather", "bucket_spread", "feature_prio", "ensemble_prio",
      "compact_vectors", "latency_fused", "seq_ring_lstm", "bucket_keys" — are listed with their measurements in

@@ -564,9 +564,11 @@ int fd_engine_set_option(fd_engine* eng, const char* key, int64_t value) {
     FD_REQUIRE(value == 0 || value == 1, FD_ERR_INVALID_ARG, "pipeline_gather must be 0 or 1");
     e.pipe_gather = value != 0;
   } else if (k == "latency_prebin") {  // latency batches with the LSTM head: the XGBoost + IsolationForest pair's
-    // tree-split binning in workgroups of the LSTM launch, 2 (default) after the LSTM's own (they fill the CUs the
-    // LSTM's workgroups leave as they finish), 1 ahead of them; 0 the pair's own binning launch
-    FD_REQUIRE(value >= 0 && value <= 2, FD_ERR_INVALID_ARG, "latency_prebin must be 0, 1 or 2");
+    // tree-split binning in the LSTM launch: 3 (default) inside the LSTM's own workgroups (a lifting level per
+    // recurrence step; 2 where a thread would have more than two searches), 2 in extra workgroups after the LSTM's
+    // own (they fill the CUs the LSTM's workgroups leave as they finish), 1 ahead of them; 0 the pair's own binning
+    // launch
+    FD_REQUIRE(value >= 0 && value <= 3, FD_ERR_INVALID_ARG, "latency_prebin must be 0, 1, 2 or 3");
     e.latency_prebin = value != 0;
     if (value) e.latency_prebin_mode = (int)value;
   } else if (k == "small_streams") {  // latency batches: 2 LSTM | other forests on two side streams, 1 one, 0 none

@@ -143,6 +143,7 @@ struct PreBin {
   int nf[2] = {};
   int64_t n = 0, n_pad = 0;
   int ld = 0;
+  int steps[2] = {};               // each forest's largest lifting step (PackedForest::bin_steps)
   const void* fx = nullptr;        // the forests and the vectors the bins are for
   const void* ff = nullptr;
   const float* X = nullptr;
@@ -582,7 +583,9 @@ struct Engine {
   bool latency_fused = true;  // "latency_fused": latency pair walk + sums + blend in 2 launches (forest.hip)
   bool seq_ring_lstm = true;  // "seq_ring_lstm": latency batches' LSTM reads card histories from the ring
   bool latency_prebin = true;  // "latency_prebin": the latency pair's binning in the LSTM head's launch (PreBin)
-  int latency_prebin_mode = 2;  // its value: 1 the binning workgroups ahead of the LSTM's, 2 (default) after them
+  int latency_prebin_mode = 3;  // its value: 1 the binning workgroups ahead of the LSTM's, 2 after them, 3 (default)
+                                // the searches inside the LSTM's own workgroups (lstm.hip InlineSearch; 2 where a
+                                // thread would take more than two)
   PreBin prebin;
   unsigned long long prebin_total = 0;  // counter "latency_prebinned_batches"
   bool ens_prio = true;   // "ensemble_prio": the fused kernel's waves issue at priority 2 (above the feature kernels;

@@ -1555,6 +1555,7 @@ bool forest_pair_prebin(Engine& e, const PackedForest& p1, const PackedForest& p
   pb.bins[0] = a.bins, pb.bins[1] = b.bins;
   pb.nan[0] = a.tile_nan, pb.nan[1] = b.tile_nan;
   pb.nf[0] = a.nf, pb.nf[1] = b.nf;
+  pb.steps[0] = xf->bin_steps, pb.steps[1] = ff->bin_steps;
   pb.n = n;
   pb.n_pad = tiles * kTile;
   pb.ld = ld;

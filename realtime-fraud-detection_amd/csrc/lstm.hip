@@ -182,7 +182,58 @@ struct LstmBinArgs {
   SplitBinArgs a, b;
   int blocks, row_blocks;
   int last;  // the binning workgroups after the LSTM's (option latency_prebin 2) instead of ahead of them
+  // option latency_prebin 3 (blocks 0): the searches inside the LSTM's own workgroups instead — thread g of the
+  // launch takes searches g and g + 512 gridDim.x of the n_pad x (a.nf + b.nf) (feature-major), one binary-lifting
+  // level per recurrence step of its first tile (the load in flight behind the step's MFMAs), the rest after (two
+  // levels per step, the second load behind the gate tail, measured slower: the LSTM launch 22.0 -> 22.3 us)
+  int inline_searches;
+  int steps;  // the lifting's first step: a power of two >= every feature's largest one (higher ones are skipped)
 };
+
+// one (row, feature) search of the inline form: split_bin_body's count of the feature's ascending thresholds <= v,
+// advanced one level at a time
+struct InlineSearch {
+  const float* thr;
+  float v;
+  int o, cnt, pos;
+  bool act;
+};
+
+__device__ __forceinline__ void inline_search_init(const LstmBinArgs& pb, int64_t s, InlineSearch& q) {
+  const int64_t total = pb.n_pad * (int64_t)(pb.a.nf + pb.b.nf);
+  q.act = s < total;
+  const int y = q.act ? (int)(s / pb.n_pad) : 0;
+  const int64_t r = q.act ? s - (int64_t)y * pb.n_pad : 0;
+  const bool fb = y >= pb.a.nf;
+  const int f = fb ? y - pb.a.nf : y;
+  const int32_t* to = fb ? pb.b.thr_off : pb.a.thr_off;
+  q.thr = fb ? pb.b.thr : pb.a.thr;
+  q.o = to[f];
+  q.cnt = (q.act && r < pb.n) ? to[f + 1] - q.o : 0;
+  q.v = (q.act && r < pb.n) ? (f < pb.ld ? pb.X[r * (int64_t)pb.ld + f] : __builtin_nanf("")) : 0.f;
+  q.pos = 0;
+}
+
+__device__ __forceinline__ float inline_search_load(const InlineSearch& q, int st) {
+  return q.thr[max(q.o + min(q.pos + st, q.cnt) - 1, 0)];
+}
+
+__device__ __forceinline__ void inline_search_step(InlineSearch& q, int st, float t) {
+  const int np = q.pos + st;
+  if (np <= q.cnt && t <= q.v) q.pos = np;
+}
+
+__device__ __forceinline__ void inline_search_store(const LstmBinArgs& pb, int64_t s, const InlineSearch& q) {
+  if (!q.act) return;
+  const int y = (int)(s / pb.n_pad);
+  const int64_t r = s - (int64_t)y * pb.n_pad;
+  const bool fb = y >= pb.a.nf;
+  const int f = fb ? y - pb.a.nf : y;
+  const SplitBinArgs& A = fb ? pb.b : pb.a;
+  const bool ok = r < pb.n, isnan_v = ok && q.v != q.v;
+  A.bins[(size_t)f * pb.n_pad + r] = !ok ? 0u : (isnan_v ? 0xFFFF0000u : (uint32_t)q.pos << 16);
+  if (isnan_v) A.tile_nan[r / kTile] = 1u;
+}
 
 __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ seq, int64_t n, int T,
                                                     const float* __restrict__ wpk4, const float* __restrict__ bias,
@@ -223,6 +274,16 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
       const int idx = tid + 512 * j, r = idx / per;
       if (idx < 4 * per && (int64_t)bx * 4 + r < n) dsc[j] = desc[(int64_t)bx * 4 + r];
     }
+  }
+  // latency_prebin 3: this thread's two searches, their values and table bounds loaded before the weights (so the
+  // first level's wait does not wait for those)
+  const bool inl = pb.inline_searches != 0;
+  const int64_t s0 = (int64_t)bx * 512 + tid, s1 = s0 + (int64_t)gx * 512;
+  InlineSearch is0{}, is1{};
+  int ist = pb.steps;
+  if (inl) {
+    inline_search_init(pb, s0, is0);
+    inline_search_init(pb, s1, is1);
   }
   // B operands: lane l holds W[(l >> 4) * 128 + 16 w + (l & 15)][k] for k = 0..143 (W_ih, then W_hh's unit blocks
   // in the order w, w+1, ..., w+7 mod 8: load_lstm)
@@ -270,6 +331,13 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
     mfma_abid16(xs[0][l], &bw[0], acc, std::make_integer_sequence<int, 16>{});
     for (int t = 0; t < T; ++t) {
       const float xn = xs[t + 1 < T ? t + 1 : t][l];  // x_{t+1}, read early (its LDS latency off the barrier window)
+      // latency_prebin 3: one lifting level of this thread's searches, its loads in flight behind the step
+      const bool lvl = inl && tile == bx && ist > 0;
+      float it0 = 0.f, it1 = 0.f;
+      if (lvl) {
+        it0 = inline_search_load(is0, ist);
+        it1 = inline_search_load(is1, ist);
+      }
       if (t > 0) {  // h_{t-1} of the other seven waves' units (blocks w+1 .. w+7), published by the last barrier
         float hv[kH / 16 - 1];
 #pragma unroll
@@ -303,6 +371,11 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
         const float ho = __int_as_float(__builtin_amdgcn_ds_bpermute(own_src, __float_as_int(h)));
         mfma_abid16(ho, &bw[kI], acc, std::make_integer_sequence<int, 16>{});
       }
+      if (lvl) {
+        inline_search_step(is0, ist, it0);
+        inline_search_step(is1, ist, it1);
+        ist >>= 1;
+      }
       __syncthreads();
     }
     if (tile == bx) FD_TL(g_tl_lstm, 2, 2);
@@ -327,6 +400,15 @@ __global__ void __launch_bounds__(512) lstm_kernel4(const float* __restrict__ se
       prob[row0 + tid] = (double)p;
     }
     __syncthreads();  // xs / hbuf / hT / zs are rewritten by the next tile
+  }
+  if (inl) {  // the levels the recurrence did not cover, then the bins
+    for (; ist > 0; ist >>= 1) {
+      const float t0 = inline_search_load(is0, ist), t1 = inline_search_load(is1, ist);
+      inline_search_step(is0, ist, t0);
+      inline_search_step(is1, ist, t1);
+    }
+    inline_search_store(pb, s0, is0);
+    inline_search_store(pb, s1, is1);
   }
   FD_TL(g_tl_lstm, 2, 3);
 }
@@ -425,6 +507,12 @@ void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, i
       pb.row_blocks = (int)(q.n_pad / kSplitBin);
       pb.blocks = (pb.row_blocks * (q.nf[0] + q.nf[1]) + 1) / 2;
       pb.last = e.latency_prebin_mode == 2 ? 1 : 0;
+      const int64_t searches = q.n_pad * (int64_t)(q.nf[0] + q.nf[1]);
+      if (e.latency_prebin_mode == 3 && searches <= 2 * 512 * std::min<int64_t>(tiles, 256)) {
+        pb.inline_searches = 1;  // two searches per LSTM thread at most; else the extra workgroups (2)
+        pb.blocks = 0;
+        pb.steps = std::max(q.steps[0], q.steps[1]);
+      }
       q.done = true;
     }
     hipLaunchKernelGGL(lstm_kernel4, dim3((unsigned)(std::min<int64_t>(tiles, 256) + pb.blocks)), dim3(512), 0, stream,

@@ -229,10 +229,11 @@ def test_slot_gather_identical(world, users):
 
 
 @pytest.mark.timeout(200)
-@pytest.mark.parametrize("lstm,mode", [(True, 1), (True, 2), (False, 1)])
+@pytest.mark.parametrize("lstm,mode", [(True, 1), (True, 2), (True, 3), (False, 1)])
 def test_prebin_in_lstm_launch_identical(world, lstm, mode):
     """Latency batches bin the XGBoost + IsolationForest pair's vectors for the tree-split walks in workgroups of the
-    LSTM head's launch, ahead of its own (engine option latency_prebin 1) or after them (2) — no binning launch —, instead of
+    LSTM head's launch, ahead of its own (engine option latency_prebin 1) or after them (2), or inside the LSTM's own
+    workgroups a lifting level per recurrence step (3; a batch of 1 falls back to 2) — no binning launch —, instead of
     split_bin_pair_kernel (0): the same outputs bit for bit, batch after batch — vectors also written to the caller's
     buffer, ragged sizes (a tile's padding rows), a batch of 1, and the sizes where the 16-row LSTM kernel runs
     (4096, 4097: the binning launch). The engine counter latency_prebinned_batches counts the pair launches that used
