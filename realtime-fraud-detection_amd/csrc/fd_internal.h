@@ -144,6 +144,7 @@ struct PreBin {
   int64_t n = 0, n_pad = 0;
   int ld = 0;
   int steps[2] = {};               // each forest's largest lifting step (PackedForest::bin_steps)
+  bool thr_nonempty = false;       // both tables hold a threshold (the inline searches read clamped positions)
   const void* fx = nullptr;        // the forests and the vectors the bins are for
   const void* ff = nullptr;
   const float* X = nullptr;

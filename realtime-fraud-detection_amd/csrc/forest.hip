@@ -1556,6 +1556,8 @@ bool forest_pair_prebin(Engine& e, const PackedForest& p1, const PackedForest& p
   pb.nan[0] = a.tile_nan, pb.nan[1] = b.tile_nan;
   pb.nf[0] = a.nf, pb.nf[1] = b.nf;
   pb.steps[0] = xf->bin_steps, pb.steps[1] = ff->bin_steps;
+  pb.thr_nonempty = xf->b_thr.bytes >= sizeof(float) && ff->b_thr.bytes >= sizeof(float) && xf->bin_steps > 0 &&
+                    ff->bin_steps > 0;
   pb.n = n;
   pb.n_pad = tiles * kTile;
   pb.ld = ld;

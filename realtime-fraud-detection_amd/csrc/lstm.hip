@@ -508,7 +508,7 @@ void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, i
       pb.blocks = (pb.row_blocks * (q.nf[0] + q.nf[1]) + 1) / 2;
       pb.last = e.latency_prebin_mode == 2 ? 1 : 0;
       const int64_t searches = q.n_pad * (int64_t)(q.nf[0] + q.nf[1]);
-      if (e.latency_prebin_mode == 3 && searches <= 2 * 512 * std::min<int64_t>(tiles, 256)) {
+      if (e.latency_prebin_mode == 3 && q.thr_nonempty && searches <= 2 * 512 * std::min<int64_t>(tiles, 256)) {
         pb.inline_searches = 1;  // two searches per LSTM thread at most; else the extra workgroups (2)
         pb.blocks = 0;
         pb.steps = std::max(q.steps[0], q.steps[1]);
