@@ -506,7 +506,7 @@ void launch_lstm(Engine& e, hipStream_t stream, const float* d_seq, int64_t n, i
       pb.b = SplitBinArgs{q.thr[1], q.thr_off[1], q.bins[1], q.nan[1], q.nf[1]};
       pb.row_blocks = (int)(q.n_pad / kSplitBin);
       pb.blocks = (pb.row_blocks * (q.nf[0] + q.nf[1]) + 1) / 2;
-      pb.last = e.latency_prebin_mode == 2 ? 1 : 0;
+      pb.last = e.latency_prebin_mode >= 2 ? 1 : 0;  // (3 falls back to 2 below)
       const int64_t searches = q.n_pad * (int64_t)(q.nf[0] + q.nf[1]);
       if (e.latency_prebin_mode == 3 && q.thr_nonempty && searches <= 2 * 512 * std::min<int64_t>(tiles, 256)) {
         pb.inline_searches = 1;  // two searches per LSTM thread at most; else the extra workgroups (2)
