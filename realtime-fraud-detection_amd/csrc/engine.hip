@@ -375,14 +375,13 @@ int fd_engine_destroy(fd_engine* eng) {
   for (int k = 0; k < Engine::kPipeSlots; ++k) {
     if (e.pipe_slot_ev[k]) (void)hipEventDestroy(e.pipe_slot_ev[k]);
     if (e.pipe_feat_ev[k]) (void)hipEventDestroy(e.pipe_feat_ev[k]);
-    if (e.pipe_done_ev[k]) (void)hipEventDestroy(e.pipe_done_ev[k]);
     if (e.pipe_copy_ev[k]) (void)hipEventDestroy(e.pipe_copy_ev[k]);
     e.pipe_vec[k].release();
     e.pipe_out[k].release();
     e.pipe_seq[k].release();
   }
   for (int k = 0; k < Engine::kSplitRing; ++k) {
-    if (e.pipe_split_ev[k]) (void)hipEventDestroy(e.pipe_split_ev[k]);
+    if (e.pipe_done_ev[k]) (void)hipEventDestroy(e.pipe_done_ev[k]);
     e.pipe_split[k].release();
   }
   for (auto* b : {&e.state.uext, &e.state.mext, &e.state.vocab, &e.feat_ext}) b->release();
@@ -417,7 +416,7 @@ int fd_engine_destroy(fd_engine* eng) {
 // the new engine stream inherits the order of the old one over pipelined batches: their scoring is complete
 // before anything queued on it (fd_score_batch_pipelined's outputs stay ordered on the engine stream)
 static void rebind_stream(Engine& e, hipStream_t s) {
-  for (int k = 0; k < Engine::kPipeSlots; ++k)
+  for (int k = 0; k < Engine::kDoneRing; ++k)
     if (e.pipe_done_live[k] && s != e.stream) FD_HIP(hipStreamWaitEvent(s, e.pipe_done_ev[k], 0));
   e.stream = s;
 }
@@ -1122,9 +1121,9 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
     FD_HIP(hipEventCreateWithFlags(&e.pipe_entry_ev, kStreamEventFlags));
     for (int k = 0; k < Engine::kPipeSlots; ++k) {
       FD_HIP(hipEventCreateWithFlags(&e.pipe_feat_ev[k], kStreamEventFlags));
-      FD_HIP(hipEventCreateWithFlags(&e.pipe_done_ev[k], kStreamEventFlags));
       FD_HIP(hipEventCreateWithFlags(&e.pipe_copy_ev[k], kStreamEventFlags));
     }
+    for (int k = 0; k < Engine::kDoneRing; ++k) FD_HIP(hipEventCreateWithFlags(&e.pipe_done_ev[k], kStreamEventFlags));
   }
   // Batch i: buffer slot s = i mod 2, its features and its scoring on Sc = pipe_stream[i & 1] (Sf: the same
   // stream). Card-state order: batch i's bucket pass after batch i-1's (an event). Buffer s is free once batch
@@ -1182,8 +1181,7 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
     // read this buffer — on the slot stream that is an explicit wait, on the batch's own stream the stream order
     e.pipe_split[sr].ensure((size_t)n * 64);
     vec = e.pipe_split[sr].as<float>();
-    if (!e.pipe_split_ev[sr]) FD_HIP(hipEventCreateWithFlags(&e.pipe_split_ev[sr], kStreamEventFlags));
-    if (Ss && e.pipe_split_live[sr]) FD_HIP(hipStreamWaitEvent(Ss, e.pipe_split_ev[sr], 0));
+    if (Ss && e.pipe_done_live[sr]) FD_HIP(hipStreamWaitEvent(Ss, e.pipe_done_ev[sr], 0));  // batch i - 4's
   }
   {
     struct SlotPass {  // launch_grouped reads these for this call only
@@ -1201,8 +1199,9 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
   e.pipe_feat_live[s] = true;
   // scoring paths other than the fused kernel share engine scratch (per-model columns, tree-split and LSTM
   // buffers): those batches also wait for the previous batch's scoring
-  if (e.pipe_done_live[prev] && !compact && !fd::ensemble_applies(e, *params, slots, present, n))
-    FD_HIP(hipStreamWaitEvent(Sc, e.pipe_done_ev[prev], 0));
+  const int pr = (sr + Engine::kDoneRing - 1) % Engine::kDoneRing;  // batch i - 1's done event
+  if (e.pipe_done_live[pr] && !compact && !fd::ensemble_applies(e, *params, slots, present, n))
+    FD_HIP(hipStreamWaitEvent(Sc, e.pipe_done_ev[pr], 0));
   // this slot's output staging: free once batch i-nbuf's copy to its caller (on e.stream) is done. Routed batches
   // always stage the four columns (the result records are packed from them when the fused kernel does not apply).
   const int n_mp = d_model_probs ? params->n_models : 0;
@@ -1241,15 +1240,11 @@ static void pipe_step(Engine& e, const fd_blend_params* params, const int32_t* s
         records)
       fd::launch_result_pack(e, s_fp, s_conf, s_dec, s_risk, rec, n, s_res);
   }
-  FD_HIP(hipEventRecord(e.pipe_done_ev[s], Sc));
-  e.pipe_done_live[s] = true;
-  FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[s], 0));
-  if (compact == 2 && Ss) {  // this batch's split rows are read: their buffer's next writer (batch i + 4) may go. The
-    // event goes on the engine stream, past the scoring: on Sc it would sit between this batch's fused kernel and
-    // batch i + 2's bucket pass, the feature chain's critical path (+4 us per step measured)
-    FD_HIP(hipEventRecord(e.pipe_split_ev[sr], e.stream));
-    e.pipe_split_live[sr] = true;
-  }
+  // (split rows: this event also releases ring buffer sr to batch i + 4's slot pass — no event of its own, which
+  // cost a record per step on the engine stream; recorded on Sc beside the fused kernel it cost 4 % in round 6)
+  FD_HIP(hipEventRecord(e.pipe_done_ev[sr], Sc));
+  e.pipe_done_live[sr] = true;
+  FD_HIP(hipStreamWaitEvent(e.stream, e.pipe_done_ev[sr], 0));
   if (in_place) {  // nothing to copy: the next use of staging slot s (batch i + 2) is on this batch's stream Sc
     e.pipe_copy_live[s] = false;
     return;

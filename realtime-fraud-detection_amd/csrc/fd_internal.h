@@ -541,8 +541,12 @@ struct Engine {
   // sequences double-buffered by batch parity
   static constexpr int kPipeSlots = 2;
   hipStream_t pipe_stream[2] = {nullptr, nullptr};
-  hipEvent_t pipe_entry_ev = nullptr, pipe_feat_ev[kPipeSlots] = {}, pipe_done_ev[kPipeSlots] = {};
-  bool pipe_feat_live[kPipeSlots] = {}, pipe_done_live[kPipeSlots] = {};
+  // batch i's scoring-done event is pipe_done_ev[i mod kDoneRing]: the engine stream, the next batch of a per-model
+  // scoring path and — split rows — batch i + 4's slot pass (which rewrites the ring buffer batch i's fused kernel
+  // read) wait on it
+  static constexpr int kDoneRing = 4;
+  hipEvent_t pipe_entry_ev = nullptr, pipe_feat_ev[kPipeSlots] = {}, pipe_done_ev[kDoneRing] = {};
+  bool pipe_feat_live[kPipeSlots] = {}, pipe_done_live[kDoneRing] = {};
   bool pipe_dirty = true;  // another engine call since the last pipelined one: order after `stream` first
   // option "slot_stream" (0 off, 1 high-priority stream, 2 low): batch i's slot pass on a stream of its own, so it
   // does not queue behind batch i-2's fused kernel on pipe_stream[i & 1]; its bucket pass waits for it by event.
@@ -568,11 +572,11 @@ struct Engine {
   // split rows (compact_vectors 2): RowA | RowB of batch i in ring buffer i mod kSplitRing. With the slot pass on its
   // own stream, batch i's slot kernel writes RowA while batch i - 2's fused kernel (the same pipe_vec parity) may
   // still read its rows — the slot stream waits only for batch i - 2's bucket pass — so the split rows get a deeper
-  // ring, and the slot pass waits for the fused kernel that last read its buffer (batch i - 4: long done)
+  // ring, and the slot pass waits for the fused kernel that last read its buffer (batch i - 4's pipe_done_ev: long
+  // done)
   static constexpr int kSplitRing = 4;
+  static_assert(kSplitRing == kDoneRing, "the split-row ring's buffers are released by the done events");
   DeviceBuffer pipe_split[kSplitRing];
-  hipEvent_t pipe_split_ev[kSplitRing] = {};
-  bool pipe_split_live[kSplitRing] = {};
   // the scoring streams write a batch's outputs into pipe_out[slot]; one copy kernel on `stream` moves them to the
   // caller's buffers, so the caller's memory is written only in the engine stream's order (torch's caching
   // allocator may hand batch i's freed outputs to batch i+1); batch i+nbuf's scoring waits for pipe_copy_ev[slot]
